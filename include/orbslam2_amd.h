@@ -1,0 +1,120 @@
+/*
+ * orbslam2_amd — C-ABI of the MI355X-native ORB-SLAM2 per-frame hot path.
+ *
+ * Plain pointers, sizes and POD structs only (no OpenCV / Eigen / torch types). Every
+ * entry point returns int status: 0 = OK, < 0 = error (never throws across the ABI).
+ * Each declaration names the reference interface it replaces (paths relative to the
+ * QiuYue-bit/ORB-SLAM2-noted tree). INTEGRATION.md shows the C++ adapters that keep the
+ * reference class signatures (ORBextractor / ORBmatcher / Frame / Optimizer) on top.
+ */
+#ifndef ORBSLAM2_AMD_H
+#define ORBSLAM2_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBX_OK 0
+#define ORBX_EINVAL (-1)     /* bad argument / shape */
+#define ORBX_EDEVICE (-2)    /* HIP runtime error or no device */
+#define ORBX_ECAP (-3)       /* caller buffer too small; *n holds the required count */
+#define ORBX_ESTATE (-4)     /* call order (e.g. results before extract) */
+
+/* cv::KeyPoint memory layout (28 bytes): pt.x, pt.y, size, angle, response, octave,
+ * class_id. Keypoints cross the ABI in exactly this layout. */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbx_kp;
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+ * -- include/ORBextractor.h:89 (ORBextractor.cc:471-579). resize_mode selects the pinned
+ * cv::resize INTER_LINEAR vertical-pass variant: 0 scalar FixedPtCast
+ * (default), 1 SSE2 VResizeLinearVec_32s8u layout. */
+typedef struct {
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+    int32_t resize_mode;
+} orbx_params;
+
+typedef struct orbx_engine orbx_engine;
+
+/* -------- extractor (replaces ORBextractor, include/ORBextractor.h:80-216) -------- */
+
+/* constructor: ORBextractor::ORBextractor (ORBextractor.h:89). Binds the current HIP
+ * device; creates a private stream (one instance per thread, as Frame.cc:144-153 runs the
+ * left and right extractors on two threads). */
+int orbx_create(const orbx_params *p, orbx_engine **out);
+void orbx_destroy(orbx_engine *e);
+
+/* GetLevels / GetScaleFactor(s) / GetInverseScaleFactors / GetScaleSigmaSquares /
+ * GetInverseScaleSigmaSquares (ORBextractor.h:115-155). Any pointer may be NULL; arrays
+ * hold nlevels entries. features_per_level = mnFeaturesPerLevel (ORBextractor.cc:514-531). */
+int orbx_levels(const orbx_engine *e, int *nlevels, float *scale, float *inv_scale,
+                float *sigma2, float *inv_sigma2, int *features_per_level);
+
+/* ORBextractor::operator()(image, mask, keypoints, descriptors) (ORBextractor.h:107,
+ * ORBextractor.cc:1543-1658) on a host u8 image (row pitch `stride` bytes). Writes up to
+ * `cap` keypoints (level-major, quadtree list order) and N x 32 descriptor bytes; *n gets
+ * the count. Empty image (w or h == 0) -> *n = 0 (reference returns untouched). The mask is
+ * ignored, as in the reference. The pyramid stays resident on the device for
+ * orbm_stereo_match (Frame::ComputeStereoMatches reads mvImagePyramid). */
+int orbx_extract(orbx_engine *e, const uint8_t *img, int w, int h, int stride, orbx_kp *kps,
+                 uint8_t *desc, int cap, int *n);
+
+/* mvImagePyramid[level] (ORBextractor.h:158) copied to host (dst may be NULL to query w/h). */
+int orbx_pyramid_level(orbx_engine *e, int image, int level, uint8_t *dst, int *w, int *h);
+
+/* -------- batched device-resident path (many frames per launch) -------- */
+
+/* Size device buffers for up to max_images images of w x h. */
+int orbx_reserve(orbx_engine *e, int w, int h, int max_images);
+/* Extract n_images frames already resident in device memory (u8, image i at
+ * d_imgs + i * image_stride, rows `pitch` bytes apart). Asynchronous on `stream`
+ * (hipStream_t; NULL = the engine's stream). Results stay on the device. */
+int orbx_extract_batch_device(orbx_engine *e, const uint8_t *d_imgs, int n_images, int w,
+                              int h, int pitch, size_t image_stride, void *stream);
+/* Device pointers of the last batch: counts[n_images], kps[n_images][cap],
+ * desc[n_images][cap][32]. */
+int orbx_batch_results(orbx_engine *e, const int **d_counts, const orbx_kp **d_kps,
+                       const uint8_t **d_desc, int *cap);
+/* Copy one image's results of the last batch to host. */
+int orbx_batch_fetch(orbx_engine *e, int image, orbx_kp *kps, uint8_t *desc, int cap, int *n);
+/* The engine's HIP stream (hipStream_t). */
+void *orbx_stream(orbx_engine *e);
+
+/* -------- stereo / matching (replaces Frame::ComputeStereoMatches and the ORBmatcher
+ * Hamming core) -------- */
+
+/* Frame::ComputeStereoMatches (include/Frame.h:249, Frame.cc:831-1128) for the frame whose
+ * left image was last extracted by `left` and right image by `right` (orbx_extract).
+ * mbf = Camera.bf, mb = mbf / fx. Writes mvuRight[n] and mvDepth[n] (-1 = no match). */
+int orbm_stereo_match(orbx_engine *left, orbx_engine *right, float mbf, float mb,
+                      float *u_right, float *depth, int n);
+
+/* Batched stereo over the engine's last device batch: image 2p = left, 2p+1 = right of
+ * pair p. Results stay on device: u_right / depth [n_pairs][cap]. */
+int orbm_stereo_match_batch_device(orbx_engine *e, int n_pairs, float mbf, float mb, void *stream);
+int orbm_stereo_results(orbx_engine *e, const float **d_u_right, const float **d_depth);
+int orbm_stereo_fetch(orbx_engine *e, int pair, float *u_right, float *depth, int cap);
+
+/* ORBmatcher::DescriptorDistance (ORBmatcher.h:65, ORBmatcher.cc:2123-2143) batched as a
+ * brute-force scan: for each query row the first minimum Hamming distance over db, its
+ * index and the second-best distance (best/second-best update order of ORBmatcher's
+ * matchers). Host pointers. */
+int orbm_hamming_best2(const uint8_t *q, int nq, const uint8_t *db, int ndb, int *best_idx,
+                       int *best_d, int *second_d);
+
+/* -------- library -------- */
+const char *orbslam2_amd_version(void);
+int orbslam2_amd_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,236 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of the CPU restatement in oracle/_build/liborb_oracle.so (built by
+oracle/Makefile). Imported only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg — never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "liborb_oracle.so"
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+MAXL = 16
+
+
+class OrcExtractor(C.Structure):
+    _fields_ = [
+        ("nfeatures", C.c_int), ("scaleFactor", C.c_double), ("nlevels", C.c_int),
+        ("iniThFAST", C.c_int), ("minThFAST", C.c_int), ("resize_mode", C.c_int),
+        ("mvScaleFactor", C.c_float * MAXL), ("mvInvScaleFactor", C.c_float * MAXL),
+        ("mvLevelSigma2", C.c_float * MAXL), ("mvInvLevelSigma2", C.c_float * MAXL),
+        ("mnFeaturesPerLevel", C.c_int * MAXL), ("umax", C.c_int * 16), ("pattern", C.c_int * 1024),
+        ("lw", C.c_int * MAXL), ("lh", C.c_int * MAXL),
+        ("level", C.POINTER(C.c_uint8) * MAXL), ("blurred", C.POINTER(C.c_uint8) * MAXL),
+    ]
+
+
+class OrcGrid(C.Structure):
+    _fields_ = [("N", C.c_int), ("keysUn", C.c_void_p), ("desc", C.c_void_p),
+                ("minX", C.c_float), ("maxX", C.c_float), ("minY", C.c_float), ("maxY", C.c_float),
+                ("gridInvW", C.c_float), ("gridInvH", C.c_float),
+                ("cell_start", C.c_void_p), ("cell_items", C.c_void_p)]
+
+
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(LIB_PATH))
+        P = C.c_void_p
+        L.orc_extractor_init.argtypes = [C.POINTER(OrcExtractor), C.c_int, C.c_float, C.c_int, C.c_int, C.c_int]
+        L.orc_extractor_free.argtypes = [C.POINTER(OrcExtractor)]
+        L.orc_extract.argtypes = [C.POINTER(OrcExtractor), P, C.c_int, C.c_int, C.c_int, P, P, C.c_int]
+        L.orc_resize_linear.argtypes = [P, C.c_int, C.c_int, C.c_int, P, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_fast_roi.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int]
+        L.orc_gaussian_blur9.argtypes = [P, C.c_int, C.c_int, P]
+        L.orc_fast_atan2.argtypes = [C.c_float, C.c_float]
+        L.orc_fast_atan2.restype = C.c_float
+        L.orc_cosf.argtypes = [C.c_float]
+        L.orc_cosf.restype = C.c_float
+        L.orc_sinf.argtypes = [C.c_float]
+        L.orc_sinf.restype = C.c_float
+        L.orc_ic_angle.argtypes = [P, C.c_int, C.c_float, C.c_float, P]
+        L.orc_ic_angle.restype = C.c_float
+        L.orc_orb_descriptor.argtypes = [P, C.c_int, C.c_float, C.c_float, C.c_float, P, P]
+        L.orc_descriptor_distance.argtypes = [P, P]
+        L.orc_level_candidates.argtypes = [C.POINTER(OrcExtractor), C.c_int, P, C.c_int]
+        L.orc_distribute_octtree.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]
+        L.orc_stereo_matches.argtypes = [C.POINTER(OrcExtractor), C.POINTER(OrcExtractor), P, P, C.c_int,
+                                         P, P, C.c_int, C.c_float, C.c_float, P, P]
+        L.orc_image_bounds.argtypes = [C.c_int, C.c_int, P, P, P, P, P, P]
+        L.orc_grid_build.argtypes = [C.POINTER(OrcGrid), P, P, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float]
+        L.orc_grid_free.argtypes = [C.POINTER(OrcGrid)]
+        L.orc_features_in_area.argtypes = [C.POINTER(OrcGrid), C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, P, C.c_int]
+        L.orc_search_for_initialization.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcGrid), P, P, C.c_int, C.c_float, C.c_int]
+        L.orc_undistort_points.argtypes = [P, P, C.c_int, P, P]
+        L.orc_stereo_from_rgbd.argtypes = [P, P, C.c_int, P, C.c_int, C.c_float, P, P]
+        L.orc_hamming_best2.argtypes = [P, C.c_int, P, C.c_int, P, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data)
+
+
+class Extractor:
+    """Python face of the oracle ORBextractor (ORBextractor.h:89-158)."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, resize_mode=0):
+        self.s = OrcExtractor()
+        rc = lib().orc_extractor_init(C.byref(self.s), nfeatures, scale_factor, nlevels, ini_th, min_th)
+        if rc != 0:
+            raise ValueError("bad extractor params")
+        self.s.resize_mode = resize_mode
+        self.nfeatures = nfeatures
+        self.nlevels = nlevels
+
+    def __del__(self):
+        try:
+            lib().orc_extractor_free(C.byref(self.s))
+        except Exception:
+            pass
+
+    @property
+    def scale_factors(self):
+        return np.array(self.s.mvScaleFactor[: self.nlevels], np.float32)
+
+    @property
+    def inv_scale_factors(self):
+        return np.array(self.s.mvInvScaleFactor[: self.nlevels], np.float32)
+
+    @property
+    def features_per_level(self):
+        return list(self.s.mnFeaturesPerLevel[: self.nlevels])
+
+    @property
+    def umax(self):
+        return np.array(self.s.umax[:], np.int32)
+
+    @property
+    def pattern(self):
+        return np.array(self.s.pattern[:], np.int32)
+
+    def extract(self, img: np.ndarray):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        cap = self.nfeatures * 2 + 256
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = lib().orc_extract(C.byref(self.s), _p(img), w, h, w, _p(kps), _p(desc), cap)
+        if n < 0:
+            raise RuntimeError("oracle capacity exceeded")
+        return kps[:n].copy(), desc[:n].copy()
+
+    def level(self, l: int) -> np.ndarray:
+        w, h = self.s.lw[l], self.s.lh[l]
+        buf = C.cast(self.s.level[l], C.POINTER(C.c_uint8 * (w * h))).contents
+        return np.frombuffer(buf, np.uint8).reshape(h, w).copy()
+
+    def level_candidates(self, l: int):
+        cap = self.s.lw[l] * self.s.lh[l] // 2 + 16
+        out = np.zeros(cap, KP_DTYPE)
+        n = lib().orc_level_candidates(C.byref(self.s), l, _p(out), cap)
+        return out[:n].copy()
+
+
+def stereo_matches(exL: Extractor, exR: Extractor, kL, dL, kR, dR, mbf, mb):
+    nL = len(kL)
+    uR = np.zeros(max(nL, 1), np.float32)
+    dep = np.zeros(max(nL, 1), np.float32)
+    kL = np.ascontiguousarray(kL)
+    kR = np.ascontiguousarray(kR)
+    dL = np.ascontiguousarray(dL)
+    dR = np.ascontiguousarray(dR)
+    lib().orc_stereo_matches(C.byref(exL.s), C.byref(exR.s), _p(kL), _p(dL), nL, _p(kR), _p(dR), len(kR),
+                             mbf, mb, _p(uR), _p(dep))
+    return uR[:nL], dep[:nL]
+
+
+def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().orc_descriptor_distance(_p(a), _p(b))
+
+
+def hamming_best2(q: np.ndarray, db: np.ndarray):
+    q = np.ascontiguousarray(q, np.uint8)
+    db = np.ascontiguousarray(db, np.uint8)
+    n = len(q)
+    bi = np.zeros(max(n, 1), np.int32)
+    bd = np.zeros(max(n, 1), np.int32)
+    sd = np.zeros(max(n, 1), np.int32)
+    lib().orc_hamming_best2(_p(q), n, _p(db), len(db), _p(bi), _p(bd), _p(sd))
+    return bi[:n], bd[:n], sd[:n]
+
+
+def undistort_points(xy: np.ndarray, K, dist):
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    out = np.zeros_like(xy)
+    Ka = np.asarray(K, np.float32)
+    Da = np.asarray(dist, np.float32)
+    lib().orc_undistort_points(_p(xy), _p(out), len(xy), _p(Ka), _p(Da))
+    return out
+
+
+def image_bounds(cols, rows, K, dist):
+    Ka = np.asarray(K, np.float32)
+    Da = np.asarray(dist, np.float32)
+    vals = [C.c_float() for _ in range(4)]
+    lib().orc_image_bounds(cols, rows, _p(Ka), _p(Da), *[C.byref(v) for v in vals])
+    return tuple(v.value for v in vals)
+
+
+def stereo_from_rgbd(keys, keys_un, depth: np.ndarray, mbf):
+    n = len(keys)
+    uR = np.zeros(max(n, 1), np.float32)
+    dep = np.zeros(max(n, 1), np.float32)
+    depth = np.ascontiguousarray(depth, np.float32)
+    lib().orc_stereo_from_rgbd(_p(np.ascontiguousarray(keys)), _p(np.ascontiguousarray(keys_un)), n, _p(depth),
+                               depth.shape[1], mbf, _p(uR), _p(dep))
+    return uR[:n], dep[:n]
+
+
+class Grid:
+    def __init__(self, keys_un, desc, bounds):
+        self.keys_un = np.ascontiguousarray(keys_un)
+        self.desc = np.ascontiguousarray(desc, np.uint8)
+        self.g = OrcGrid()
+        lib().orc_grid_build(C.byref(self.g), _p(self.keys_un), _p(self.desc), len(self.keys_un), *bounds)
+
+    def __del__(self):
+        try:
+            lib().orc_grid_free(C.byref(self.g))
+        except Exception:
+            pass
+
+    def features_in_area(self, x, y, r, min_level=-1, max_level=-1):
+        out = np.zeros(len(self.keys_un) + 1, np.int32)
+        n = lib().orc_features_in_area(C.byref(self.g), x, y, r, min_level, max_level, _p(out), len(out))
+        return out[:n].copy()
+
+
+def search_for_initialization(F1: Grid, F2: Grid, prev_xy: np.ndarray, window=100, nnratio=0.9, check_ori=True):
+    prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.zeros(max(len(F1.keys_un), 1), np.int32)
+    n = lib().orc_search_for_initialization(C.byref(F1.g), C.byref(F2.g), _p(prev), _p(m12), window, nnratio,
+                                            1 if check_ori else 0)
+    return n, m12[: len(F1.keys_un)], prev

@@ -1,0 +1,102 @@
+// Device-side numerics shared by the orbslam2_amd HIP kernels (gfx950).
+//
+// Every helper reproduces a host-side primitive of the reference bit-for-bit:
+//   * cv_round_f        cvRound(float)  = SSE2 cvtss2si, round-half-even
+//   * fast_atan2_deg    cv::fastAtan2   (SURVEY.md A.4), float, no contraction
+//   * glibc_cosf/sinf   glibc >= 2.28 cosf/sinf as called by computeOrbDescriptor
+//                       (ORBextractor.cc:157-158); double evaluation identical to
+//                       sysdeps/ieee754/flt-32/{s_cosf,s_sinf}.c
+// The whole library is compiled with -ffp-contract=off so a*b+c stays two roundings,
+// like the reference's x86-64 SSE2 build (CMakeLists.txt:19-23, no -march=native).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace orbamd {
+
+__device__ __forceinline__ int cv_round_f(float v) { return (int)__builtin_rintf(v); }
+
+__device__ __forceinline__ float fast_atan2_deg(float y, float x) {
+    const float kR2D = (float)(180.0 / 3.1415926535897932384626433832795);
+    const float p1 = 0.9997878412794807f * kR2D;
+    const float p3 = -0.3258083974640975f * kR2D;
+    const float p5 = 0.1555786518463281f * kR2D;
+    const float p7 = -0.04432655554792128f * kR2D;
+    const float eps = (float)2.2204460492503131e-16;
+    float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+struct SinCosTab {
+    double sign[4];
+    double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
+};
+
+static __constant__ SinCosTab kSinCosTab[2] = {
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0,
+     -0x1ffffffd0c621cp-54, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10,
+     0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7,
+     -0x1.994eb3774cf24p-13},
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0,
+     0x1ffffffd0c621cp-54, -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10,
+     -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7,
+     -0x1.994eb3774cf24p-13}};
+
+__device__ __forceinline__ const SinCosTab &sincos_tab(int i) { return kSinCosTab[i]; }
+
+__device__ __forceinline__ uint32_t abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
+
+__device__ __forceinline__ float sc_poly(double x, double x2, const SinCosTab &p, int n) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2, s1 = p.s2 + x2 * p.s3, x7 = x3 * x2, s = x + x3 * p.s1;
+        return (float)(s + x7 * s1);
+    }
+    double x4 = x2 * x2, c2 = p.c3 + x2 * p.c4, c1 = p.c0 + x2 * p.c1, x6 = x4 * x2;
+    double c = c1 + x4 * p.c2;
+    return (float)(c + x6 * c2);
+}
+
+// cos and sin of a float angle in [0, 2*pi] exactly as glibc's cosf / sinf.
+__device__ __forceinline__ void glibc_sincosf(float y, float *s_out, float *c_out) {
+    double x = y;
+    const float pio4 = 0x1.921FB6p-1f;
+    if (abstop12(y) < abstop12(pio4)) {
+        if (abstop12(y) < abstop12(0x1p-12f)) { *c_out = 1.0f; *s_out = y; return; }
+        const SinCosTab &p = sincos_tab(0);
+        *c_out = sc_poly(x, x * x, p, 1);
+        *s_out = sc_poly(x, x * x, p, 0);
+        return;
+    }
+    const SinCosTab &p0 = sincos_tab(0);
+    double r = x * p0.hpi_inv;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    x = x - n * p0.hpi;
+    double s = p0.sign[n & 3];
+    const SinCosTab &p = sincos_tab((n & 2) ? 1 : 0);
+    *c_out = sc_poly(x * s, x * x, p, n ^ 1);
+    *s_out = sc_poly(x * s, x * x, p, n);
+}
+
+// Packed candidate key: score (8b) | x (12b) << 8 | y (12b) << 20, x/y relative to
+// (minBorderX, minBorderY) as in ComputeKeyPointsOctTree (ORBextractor.cc:1141-1146).
+__device__ __forceinline__ uint32_t pack_key(int x, int y, int score) {
+    return (uint32_t)score | ((uint32_t)x << 8) | ((uint32_t)y << 20);
+}
+__device__ __forceinline__ int key_score(uint32_t k) { return (int)(k & 0xFF); }
+__device__ __forceinline__ int key_x(uint32_t k) { return (int)((k >> 8) & 0xFFF); }
+__device__ __forceinline__ int key_y(uint32_t k) { return (int)(k >> 20); }
+
+__device__ __forceinline__ int wave_lane() { return (int)__lane_id(); }
+
+}  // namespace orbamd

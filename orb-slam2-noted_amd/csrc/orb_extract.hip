@@ -1,0 +1,1134 @@
+// MI355X-native ORBextractor: pyramid, per-cell FAST, quadtree distribution, IC_Angle,
+// Gaussian blur and steered BRIEF as hand-written HIP kernels for gfx950, batched over
+// many images per launch. Behaviour follows ORBextractor::operator() of ORB-SLAM2-noted
+// (ORBextractor.cc:1543-1658) bit-for-bit; the OpenCV primitives follow SURVEY.md
+// Appendix A. See DESIGN.md for layout and rooflines.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "orb_device.h"
+#include "orb_engine.h"
+#include "orb_pattern_31.inc"
+
+using namespace orbamd;
+
+namespace orbamd {
+
+static __constant__ int8_t c_pattern[1024];  // bit_pattern_31_ (ORBextractor.cc:209-467) as data
+static __constant__ int c_umax[16];
+
+#define HIPCHK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "orbslam2_amd: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return ORBX_EDEVICE;                                                    \
+        }                                                                           \
+    } while (0)
+
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+int DevBuf::ensure(size_t n) {
+    if (n <= bytes && p) return 0;
+    release();
+    if (n == 0) n = 16;
+    if (hipMalloc(&p, n) != hipSuccess) { p = nullptr; return ORBX_EDEVICE; }
+    bytes = n;
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// Level image addressing. Level 0 is the caller's input buffer (no copy); levels >= 1 live
+// in the engine's pyramid block. Unpadded: the 19-px border of ComputePyramid
+// (ORBextractor.cc:1704-1727) is never read downstream.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ const uint8_t *level_ptr(const ExtractGeom &g, const uint8_t *in,
+                                                    const uint8_t *pyr, int b, int l, int *pitch) {
+    if (l == 0) { *pitch = g.in_pitch; return in + (long long)b * g.in_stride; }
+    *pitch = g.lw[l];
+    return pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
+}
+
+// ------------------------------------------------------------------------------------
+// K1: cv::resize(INTER_LINEAR) of level l-1 into level l (ComputePyramid :1686-1691,
+// SURVEY.md A.2). Column/row coefficient tables are precomputed on the host with the
+// reference's float/double arithmetic; the kernel does the exact integer math.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, const int4 *rz,
+                                                           const uint8_t *in, uint8_t *pyr) {
+    const int dw = g.lw[l], dh = g.lh[l];
+    const int b = blockIdx.z, dy = blockIdx.y;
+    const int dx = blockIdx.x * 256 + threadIdx.x;
+    if (dx >= dw || dy >= dh) return;
+    int sp;
+    const uint8_t *src = level_ptr(g, in, pyr, b, l - 1, &sp);
+    uint8_t *dst = pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
+    const int4 cx = rz[g.rz_col_off[l] + dx];   // sx, sx1, a0, a1
+    const int4 ry = rz[g.rz_row_off[l] + dy];   // r0, r1, b0, b1
+    const uint8_t *p0 = src + (long long)ry.x * sp, *p1 = src + (long long)ry.y * sp;
+    const int S0 = p0[cx.x] * cx.z + p0[cx.y] * cx.w;
+    const int S1 = p1[cx.x] * cx.z + p1[cx.y] * cx.w;
+    int v;
+    if (dx < g.rz_simd_end[l]) {  // SSE2 VResizeLinearVec_32s8u lane arithmetic
+        int x0 = S0 >> 4, y0 = S1 >> 4;
+        x0 = min(max(x0, -32768), 32767);
+        y0 = min(max(y0, -32768), 32767);
+        int t = ((x0 * (int)(int16_t)ry.z) >> 16) + ((y0 * (int)(int16_t)ry.w) >> 16);
+        t = min(max(t, -32768), 32767);
+        t = min(max(t + 2, -32768), 32767) >> 2;
+        v = t;
+    } else {                      // FixedPtCast<int, uchar, 22>
+        v = (S0 * ry.z + S1 * ry.w + (1 << 21)) >> 22;
+    }
+    dst[(long long)dy * dw + dx] = (uint8_t)min(max(v, 0), 255);
+}
+
+// ------------------------------------------------------------------------------------
+// K2: per-cell FAST-9/16 with 3x3 NMS inside the cell ROI and the dual-threshold retry
+// (ORBextractor.cc:1084-1153 + cv::FAST). One wavefront per cell, ROI
+// staged in LDS. Keypoints are emitted row-major (the order cv::FAST pushes them).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ bool has9(uint32_t m) {
+    uint32_t m32 = m | (m << 16);
+    uint32_t t = m32 & (m32 >> 1);
+    t &= t >> 2;
+    t &= t >> 4;
+    t &= m32 >> 8;
+    return (t & 0xFFFFu) != 0;
+}
+
+// cornerScore<16> (OpenCV fast_score.cpp), d[k] = v - ring[k].
+__device__ __forceinline__ int corner_score16(const int *d, int threshold) {
+    int a0 = threshold;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(d[k + 1], d[k + 2]);
+        a = min(a, d[k + 3]);
+        if (a <= a0) continue;
+        a = min(a, d[k + 4]);
+        a = min(a, d[k + 5]);
+        a = min(a, d[k + 6]);
+        a = min(a, d[k + 7]);
+        a = min(a, d[k + 8]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[k + 9]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int b = max(d[k + 1], d[k + 2]);
+        b = max(b, d[k + 3]);
+        b = max(b, d[k + 4]);
+        b = max(b, d[k + 5]);
+        if (b >= b0) continue;
+        b = max(b, d[k + 6]);
+        b = max(b, d[k + 7]);
+        b = max(b, d[k + 8]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+__device__ __forceinline__ int fast_pixel_score(const uint8_t *t, int i, int j, int th) {
+    // ring offsets (dx, dy) of OpenCV's offsets16, extended to 25 by wrapping
+    const int8_t RX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    const int8_t RY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    const int v = t[i * ORBX_TMAX + j];
+    int d[25];
+    uint32_t dk = 0, br = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        int p = t[(i + RY[k]) * ORBX_TMAX + j + RX[k]];
+        d[k] = v - p;
+        dk |= (uint32_t)(p < v - th) << k;
+        br |= (uint32_t)(p > v + th) << k;
+    }
+    if (!has9(dk) && !has9(br)) return 0;
+#pragma unroll
+    for (int k = 16; k < 25; k++) d[k] = d[k - 16];
+    return corner_score16(d, th) & 0xFF;  // stored as uchar (fast.cpp curr[j])
+}
+
+__global__ __launch_bounds__(64) void fast_cells_kernel(ExtractGeom g, const CellDesc *cells,
+                                                        const uint8_t *in, const uint8_t *pyr,
+                                                        int *cell_cnt, uint32_t *cell_keys) {
+    __shared__ uint8_t tile[ORBX_TMAX * ORBX_TMAX];
+    __shared__ uint8_t score[ORBX_TMAX * ORBX_TMAX];
+    const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+    const CellDesc cd = cells[c];
+    int pitch;
+    const uint8_t *img = level_ptr(g, in, pyr, b, cd.level, &pitch);
+    const int rh = cd.rh, rw = cd.rw;
+    const uint8_t *src = img + (long long)cd.r0 * pitch + cd.c0;
+    for (int i = lane; i < rh * rw; i += 64) {
+        const int r = i / rw, cc = i - r * rw;
+        tile[r * ORBX_TMAX + cc] = src[(long long)r * pitch + cc];
+    }
+    const int dh = rh - 6, dwid = rw - 6;
+    const int ndet = (dh > 0 && dwid > 0) ? dh * dwid : 0;
+    int th = g.ini_th;
+    int total = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        th = min(max(th, 0), 255);
+        for (int i = lane; i < ORBX_TMAX * ORBX_TMAX; i += 64) score[i] = 0;
+        __syncthreads();
+        for (int idx = lane; idx < ndet; idx += 64) {
+            const int i = 3 + idx / dwid, j = 3 + idx % dwid;
+            score[i * ORBX_TMAX + j] = (uint8_t)fast_pixel_score(tile, i, j, th);
+        }
+        __syncthreads();
+        total = 0;
+        for (int base = 0; base < ndet; base += 64) {
+            const int idx = base + lane;
+            bool keep = false;
+            if (idx < ndet) {
+                const int i = 3 + idx / dwid, j = 3 + idx % dwid;
+                const uint8_t *s = score + i * ORBX_TMAX + j;
+                const int v = s[0];
+                keep = v > s[1] && v > s[-1] && v > s[-ORBX_TMAX - 1] && v > s[-ORBX_TMAX] &&
+                       v > s[-ORBX_TMAX + 1] && v > s[ORBX_TMAX - 1] && v > s[ORBX_TMAX] &&
+                       v > s[ORBX_TMAX + 1];
+            }
+            total += __popcll(__ballot(keep));
+        }
+        if (total > 0) break;
+        th = g.min_th;
+    }
+    uint32_t *out = cell_keys + ((long long)b * g.ncell_total + c) * g.cell_cap;
+    int written = 0;
+    if (total > 0) {
+        for (int base = 0; base < ndet; base += 64) {
+            const int idx = base + lane;
+            bool keep = false;
+            int i = 0, j = 0, v = 0;
+            if (idx < ndet) {
+                i = 3 + idx / dwid;
+                j = 3 + idx % dwid;
+                const uint8_t *s = score + i * ORBX_TMAX + j;
+                v = s[0];
+                keep = v > s[1] && v > s[-1] && v > s[-ORBX_TMAX - 1] && v > s[-ORBX_TMAX] &&
+                       v > s[-ORBX_TMAX + 1] && v > s[ORBX_TMAX - 1] && v > s[ORBX_TMAX] &&
+                       v > s[ORBX_TMAX + 1];
+            }
+            const unsigned long long m = __ballot(keep);
+            const int rank = __popcll(m & ((1ull << lane) - 1ull));
+            if (keep && written + rank < g.cell_cap)
+                out[written + rank] = pack_key(j + cd.offx, i + cd.offy, v);
+            written += __popcll(m);
+        }
+    }
+    if (lane == 0) cell_cnt[(long long)b * g.ncell_total + c] = min(written, g.cell_cap);
+}
+
+// ------------------------------------------------------------------------------------
+// K3: cv::GaussianBlur(9x9, sigma 2, REFLECT_101) on each level (ORBextractor.cc:1617-1625;
+// bit-exact fixed-point path). 64x16 output tiles, (16+8)x(64+8) LDS halo,
+// exact integer row sums then Q16 column sums.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int refl101(int i, int n) {
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+__global__ __launch_bounds__(256) void blur_kernel(ExtractGeom g, const uint8_t *in,
+                                                   const uint8_t *pyr, uint8_t *blur) {
+    __shared__ uint8_t tin[24][72];
+    __shared__ int trow[24][64];
+    const int b = blockIdx.y;
+    int t = blockIdx.x, l = 0;
+    while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
+    t -= g.blur_tile_base[l];
+    const int tx = t % g.blur_tiles_x[l], ty = t / g.blur_tiles_x[l];
+    const int w = g.lw[l], h = g.lh[l];
+    const int x0 = tx * 64, y0 = ty * 16;
+    int pitch;
+    const uint8_t *src = level_ptr(g, in, pyr, b, l, &pitch);
+    for (int i = threadIdx.x; i < 24 * 72; i += 256) {
+        const int r = i / 72, cc = i % 72;
+        const int sy = refl101(y0 + r - 4, h), sx = refl101(x0 + cc - 4, w);
+        tin[r][cc] = src[(long long)sy * pitch + sx];
+    }
+    __syncthreads();
+    const int K[9] = {7, 17, 32, 46, 52, 46, 32, 17, 7};
+    for (int i = threadIdx.x; i < 24 * 64; i += 256) {
+        const int r = i / 64, cc = i % 64;
+        int acc = 0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) acc += K[k] * tin[r][cc + k];
+        trow[r][cc] = acc;
+    }
+    __syncthreads();
+    uint8_t *dst = blur + (long long)b * g.blur_stride + g.blur_off[l];
+    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
+        const int r = i / 64, cc = i % 64;
+        const int y = y0 + r, x = x0 + cc;
+        if (y >= h || x >= w) continue;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) acc += (uint32_t)K[k] * (uint32_t)trow[r + k][cc];
+        dst[(long long)y * w + x] = (uint8_t)min((int)((acc + 32768u) >> 16), 255);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// K4: DistributeOctTree (ORBextractor.cc:696-1042), one 256-thread workgroup per
+// (level, image). Exact reformulation of the list algorithm:
+//  * the final std::list order equals DESCENDING node creation sequence (every node is
+//    push_front'ed, :831-886/:946-986), with the push_back'ed roots last in ascending
+//    order -> every node carries a sort key (creation id; roots -1-i);
+//  * a phase-1 round splits every non-leaf node in list order (= reverse creation order
+//    of the previous round's multi-key children); children get consecutive ids in
+//    n1,n2,n3,n4 order;
+//  * the final phase orders the last round's multi-key nodes by (size, id) descending
+//    (the sort at :935 iterated back to front, pointer tie pinned to creation order) and
+//    stops at the first node that brings the size to >= N (:991).
+// Node keys live in a ping-pong key array (LDS when they fit); stable partitions keep each
+// node's keys in candidate order, so "first max response" (:1028) is first in array order.
+// ------------------------------------------------------------------------------------
+struct QNode {
+    int16_t x0, y0, x1, y1;
+    int s;      // segment start | buffer bit << 30
+    int n;      // key count
+    int id;     // creation id
+};
+
+__device__ __forceinline__ int qnode_start(const QNode &q) { return q.s & 0x3FFFFFFF; }
+__device__ __forceinline__ int qnode_buf(const QNode &q) { return (q.s >> 30) & 1; }
+
+__device__ __forceinline__ int quadrant(uint32_t k, int midx, int midy) {
+    return (key_x(k) >= midx ? 1 : 0) + (key_y(k) >= midy ? 2 : 0);
+}
+
+struct QShared {
+    int live, next_id, n_out, n_next, n_act, prev_size, cross;
+    int tot[4];
+    int root_cnt[64], root_start[64], root_fill[64];
+    int wcnt[4][64];
+    int scan[ORBX_QT_THREADS];
+};
+
+// block-wide exclusive scan of one int per thread; returns exclusive prefix, *total = sum
+__device__ __forceinline__ int block_excl_scan(QShared &S, int v, int *total) {
+    const int tid = threadIdx.x;
+    S.scan[tid] = v;
+    __syncthreads();
+    for (int off = 1; off < ORBX_QT_THREADS; off <<= 1) {
+        int add = tid >= off ? S.scan[tid - off] : 0;
+        __syncthreads();
+        S.scan[tid] += add;
+        __syncthreads();
+    }
+    const int incl = S.scan[tid];
+    *total = S.scan[ORBX_QT_THREADS - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+// counts of the four children of node q (no writes)
+__device__ __forceinline__ void qnode_counts(const QNode &q, uint32_t *const K[2], int c[4]) {
+    const int hx = (int)ceilf((float)(q.x1 - q.x0) / 2);
+    const int hy = (int)ceilf((float)(q.y1 - q.y0) / 2);
+    const int midx = q.x0 + hx, midy = q.y0 + hy;
+    const uint32_t *src = K[qnode_buf(q)] + qnode_start(q);
+    c[0] = c[1] = c[2] = c[3] = 0;
+    for (int i = 0; i < q.n; i++) c[quadrant(src[i], midx, midy)]++;
+}
+
+// DivideNode (:610-682): stable 4-way partition into the other buffer, children boxes
+__device__ __forceinline__ void qnode_divide(const QNode &q, uint32_t *const K[2], int c[4],
+                                             QNode ch[4]) {
+    const int hx = (int)ceilf((float)(q.x1 - q.x0) / 2);
+    const int hy = (int)ceilf((float)(q.y1 - q.y0) / 2);
+    const int midx = q.x0 + hx, midy = q.y0 + hy;
+    const int s = qnode_start(q), bsrc = qnode_buf(q), bdst = bsrc ^ 1;
+    const uint32_t *src = K[bsrc] + s;
+    uint32_t *dst = K[bdst] + s;
+    c[0] = c[1] = c[2] = c[3] = 0;
+    for (int i = 0; i < q.n; i++) c[quadrant(src[i], midx, midy)]++;
+    int pos[4] = {0, c[0], c[0] + c[1], c[0] + c[1] + c[2]};
+    for (int k = 0; k < 4; k++) {
+        ch[k].s = (s + pos[k]) | (bdst << 30);
+        ch[k].n = c[k];
+    }
+    for (int i = 0; i < q.n; i++) {
+        const uint32_t k = src[i];
+        dst[pos[quadrant(k, midx, midy)]++] = k;
+    }
+    ch[0].x0 = q.x0; ch[0].y0 = q.y0; ch[0].x1 = (int16_t)midx; ch[0].y1 = (int16_t)midy;
+    ch[1].x0 = (int16_t)midx; ch[1].y0 = q.y0; ch[1].x1 = q.x1; ch[1].y1 = (int16_t)midy;
+    ch[2].x0 = q.x0; ch[2].y0 = (int16_t)midy; ch[2].x1 = (int16_t)midx; ch[2].y1 = q.y1;
+    ch[3].x0 = (int16_t)midx; ch[3].y0 = (int16_t)midy; ch[3].x1 = q.x1; ch[3].y1 = q.y1;
+}
+
+// first key with maximal response (strict >, :1028-1036)
+__device__ __forceinline__ uint32_t qnode_best(const QNode &q, uint32_t *const K[2]) {
+    const uint32_t *src = K[qnode_buf(q)] + qnode_start(q);
+    uint32_t best = src[0];
+    for (int i = 1; i < q.n; i++)
+        if (key_score(src[i]) > key_score(best)) best = src[i];
+    return best;
+}
+
+// bitonic sort of n (pow2) u64 values, descending
+__device__ void block_sort_desc(unsigned long long *a, int n) {
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += ORBX_QT_THREADS) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long x = a[i], y = a[ixj];
+                    const bool desc = (i & k) == 0;
+                    if (desc ? (x < y) : (x > y)) { a[i] = y; a[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// One split round over `na` nodes taken from cur[] in the given order (perm: optional
+// index list; reverse: process cur[na-1-t]). limit = number of leading nodes (in processing
+// order) that are actually divided; the rest are left as leftovers. Children with one key
+// go to outrec (leaf), multi-key children to nxt[] in creation order.
+__device__ void qt_split(QShared &S, const QNode *cur, int na, bool reverse,
+                         const unsigned long long *order, int limit, QNode *nxt,
+                         unsigned long long *outrec, uint32_t *const K[2], int rec_cap,
+                         int nxt_cap) {
+    for (int cb = 0; cb < na; cb += ORBX_QT_THREADS) {
+        const int t = cb + (int)threadIdx.x;
+        const bool valid = t < na;
+        const bool divide = valid && t < limit;
+        QNode q{};
+        if (valid) {
+            const int idx = order ? (int)(order[t] & 0xFFFF) : (reverse ? na - 1 - t : t);
+            q = cur[idx];
+        }
+        int c[4] = {0, 0, 0, 0};
+        QNode ch[4];
+        if (divide) qnode_divide(q, K, c, ch);
+        int ne = 0, mu = 0, si = 0;
+        for (int k = 0; k < 4; k++) { ne += c[k] > 0; mu += c[k] > 1; si += c[k] == 1; }
+        const bool left = valid && !divide;  // leftover (final phase)
+        int tot_ne, tot_mu, tot_si, tot_left;
+        const int pre_ne = block_excl_scan(S, ne, &tot_ne);
+        const int pre_mu = block_excl_scan(S, mu, &tot_mu);
+        const int pre_si = block_excl_scan(S, si + (left ? 1 : 0), &tot_si);
+        const int ndiv = block_excl_scan(S, divide ? 1 : 0, &tot_left);
+        (void)ndiv;
+        if (divide) {
+            int id = S.next_id + pre_ne, m = S.n_next + pre_mu, o = S.n_out + pre_si;
+            for (int k = 0; k < 4; k++) {
+                if (c[k] == 0) continue;
+                ch[k].id = id++;
+                if (c[k] == 1) {
+                    const uint32_t key = K[qnode_buf(ch[k])][qnode_start(ch[k])];
+                    if (o < rec_cap) outrec[o] = ((unsigned long long)(uint32_t)(ch[k].id + 0x40000000) << 32) | key;
+                    o++;
+                } else {
+                    if (m < nxt_cap) nxt[m] = ch[k];
+                    m++;
+                }
+            }
+        } else if (left) {
+            const int o = S.n_out + pre_si;
+            if (o < rec_cap)
+                outrec[o] = ((unsigned long long)(uint32_t)(q.id + 0x40000000) << 32) | qnode_best(q, K);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            S.next_id += tot_ne;
+            S.n_next += tot_mu;
+            S.n_out += tot_si;
+            S.live += tot_ne - tot_left;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
+    ExtractGeom g, const int *cell_cnt, const uint32_t *cell_keys, uint32_t *qt_keys,
+    unsigned char *qt_nodes, uint32_t *sel, int *sel_cnt) {
+    extern __shared__ __align__(16) unsigned char qt_lds[];
+    __shared__ QShared S;
+    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int cb0 = g.cell_base[l], ncell = g.cell_base[l + 1] - cb0;
+    const int N = g.N[l], nIni = g.nIni[l];
+    const int NC = g.node_cap, NP = g.node_pow2;
+    // ---- LDS / global carving
+    unsigned char *lds = qt_lds;
+    QNode *nodes0, *nodes1;
+    unsigned long long *outrec, *sortbuf;
+    if (g.qt_nodes_in_lds) {
+        nodes0 = (QNode *)lds; lds += sizeof(QNode) * NC;
+        nodes1 = (QNode *)lds; lds += sizeof(QNode) * NC;
+        outrec = (unsigned long long *)lds; lds += 8 * NP;
+        sortbuf = (unsigned long long *)lds; lds += 8 * NP;
+    } else {
+        unsigned char *gn = qt_nodes + ((long long)b * g.nlevels + l) * g.qt_node_stride * 4;
+        nodes0 = (QNode *)gn; gn += sizeof(QNode) * NC;
+        nodes1 = (QNode *)gn; gn += sizeof(QNode) * NC;
+        outrec = (unsigned long long *)gn; gn += 8 * NP;
+        sortbuf = (unsigned long long *)gn;
+    }
+    uint32_t *ldskeys = (uint32_t *)lds;
+    // ---- 1. gather candidates in cell (row-major) order -> M
+    const int *cnt = cell_cnt + (long long)b * g.ncell_total + cb0;
+    int M = 0;
+    for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS) {
+        const int c = c0 + tid;
+        const int v = c < ncell ? cnt[c] : 0;
+        int tot;
+        block_excl_scan(S, v, &tot);
+        M += tot;
+    }
+    uint32_t *K0, *K1;
+    if (M <= ORBX_QT_KL) { K0 = ldskeys; K1 = ldskeys + ORBX_QT_KL; }
+    else {
+        uint32_t *gk = qt_keys + (long long)b * g.qt_off[g.nlevels] + g.qt_off[l];
+        K0 = gk; K1 = gk + (g.qt_off[l + 1] - g.qt_off[l]) / 2;
+    }
+    uint32_t *const K[2] = {K0, K1};
+    {
+        int base = 0;
+        for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS) {
+            const int c = c0 + tid;
+            const int v = c < ncell ? cnt[c] : 0;
+            int tot;
+            const int pre = block_excl_scan(S, v, &tot);
+            if (c < ncell) {
+                const uint32_t *src = cell_keys + ((long long)b * g.ncell_total + cb0 + c) * g.cell_cap;
+                for (int i = 0; i < v; i++) K0[base + pre + i] = src[i];
+            }
+            base += tot;
+        }
+    }
+    // ---- 2. roots (:700-745): stable counting partition into K1
+    const float hX = g.hX[l];
+    if (tid < 64) { S.root_cnt[tid] = 0; S.root_fill[tid] = 0; }
+    if (tid == 0) { S.live = 0; S.next_id = nIni; S.n_out = 0; S.n_next = 0; }
+    __syncthreads();
+    for (int i = tid; i < M; i += ORBX_QT_THREADS) {
+        int r = (int)((float)key_x(K0[i]) / hX);
+        r = min(r, nIni - 1);
+        atomicAdd(&S.root_cnt[r], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int a = 0;
+        for (int r = 0; r < nIni; r++) { S.root_start[r] = a; a += S.root_cnt[r]; }
+    }
+    __syncthreads();
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int cs = 0; cs < M; cs += ORBX_QT_THREADS) {
+        const int i = cs + tid;
+        int r = -1;
+        uint32_t key = 0;
+        if (i < M) { key = K0[i]; r = min((int)((float)key_x(key) / hX), nIni - 1); }
+        int my_rank = 0;
+        for (int rr = 0; rr < nIni; rr++) {
+            const unsigned long long m = __ballot(r == rr);
+            if (r == rr) my_rank = __popcll(m & ((1ull << lane) - 1ull));
+            if (lane == 0) S.wcnt[wv][rr] = __popcll(m);
+        }
+        __syncthreads();
+        if (r >= 0) {
+            int pos = S.root_start[r] + S.root_fill[r] + my_rank;
+            for (int w = 0; w < wv; w++) pos += S.wcnt[w][r];
+            K1[pos] = key;
+        }
+        __syncthreads();
+        if (tid < nIni) {
+            int add = 0;
+            for (int w = 0; w < ORBX_QT_THREADS / 64; w++) add += S.wcnt[w][tid];
+            S.root_fill[tid] += add;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const int H = g.maxBY[l] - 16;
+        int na = 0, live = 0, no = 0;
+        for (int r = 0; r < nIni; r++) {
+            const int n = S.root_cnt[r];
+            if (n == 0) continue;
+            live++;
+            if (n == 1) {
+                outrec[no++] = ((unsigned long long)(uint32_t)(-1 - r + 0x40000000) << 32) | K1[S.root_start[r]];
+            } else {
+                QNode q;
+                q.x0 = (int16_t)(int)(hX * (float)r);
+                q.x1 = (int16_t)(int)(hX * (float)(r + 1));
+                q.y0 = 0;
+                q.y1 = (int16_t)H;
+                q.s = S.root_start[r] | (1 << 30);
+                q.n = n;
+                q.id = -1 - r;
+                nodes0[na++] = q;
+            }
+        }
+        S.live = live; S.n_out = no; S.n_act = na;
+    }
+    __syncthreads();
+    // ---- 3. phase-1 rounds (:772-913)
+    QNode *cur = nodes0, *nxt = nodes1;
+    bool reverse = false;  // roots are processed in ascending order (push_back'ed)
+    bool finished = false;
+    bool final_phase = false;
+    while (!finished) {
+        const int prev = S.live;
+        const int na = S.n_act;
+        if (tid == 0) S.n_next = 0;
+        __syncthreads();
+        qt_split(S, cur, na, reverse, nullptr, na, nxt, outrec, K, NP, NC);
+        QNode *tmp = cur; cur = nxt; nxt = tmp;
+        reverse = true;
+        if (tid == 0) S.n_act = S.n_next;
+        __syncthreads();
+        const int live = S.live, nToExpand = S.n_act;
+        if (live >= N || live == prev) finished = true;
+        else if (live + nToExpand * 3 > N) { final_phase = true; finished = true; }
+    }
+    // ---- 4. final phase (:914-997)
+    if (final_phase) {
+        bool done = false;
+        while (!done) {
+            const int prev = S.live;
+            const int na = S.n_act;
+            for (int i = tid; i < NP; i += ORBX_QT_THREADS) {
+                unsigned long long v = 0;
+                if (i < na) {
+                    const QNode &q = cur[i];
+                    v = ((unsigned long long)(uint32_t)q.n << 40) | ((unsigned long long)(uint32_t)(q.id & 0xFFFFFF) << 16) | (unsigned)i;
+                }
+                sortbuf[i] = v;
+            }
+            __syncthreads();
+            int np2 = 1;
+            while (np2 < na) np2 <<= 1;
+            block_sort_desc(sortbuf, np2);
+            // first sorted position whose split brings the size to >= N
+            if (tid == 0) S.cross = na;
+            __syncthreads();
+            int run = S.live;
+            for (int cb = 0; cb < na; cb += ORBX_QT_THREADS) {
+                const int t = cb + tid;
+                int delta = 0;
+                if (t < na) {
+                    int c[4];
+                    qnode_counts(cur[sortbuf[t] & 0xFFFF], K, c);
+                    delta = (c[0] > 0) + (c[1] > 0) + (c[2] > 0) + (c[3] > 0) - 1;
+                }
+                int tot;
+                const int pre = block_excl_scan(S, delta, &tot);
+                if (t < na && run + pre + delta >= N) atomicMin(&S.cross, t);
+                run += tot;
+                __syncthreads();
+            }
+            const int limit = min(S.cross + 1, na);
+            if (tid == 0) S.n_next = 0;
+            __syncthreads();
+            qt_split(S, cur, na, false, sortbuf, limit, nxt, outrec, K, NP, NC);
+            QNode *tmp = cur; cur = nxt; nxt = tmp;
+            if (tid == 0) S.n_act = S.n_next;
+            __syncthreads();
+            if (S.live >= N || S.live == prev) done = true;
+        }
+    }
+    // ---- 5. leftover multi-key nodes -> first max response; output in list order
+    {
+        const int na = S.n_act;
+        for (int cb = 0; cb < na; cb += ORBX_QT_THREADS) {
+            const int t = cb + tid;
+            int tot;
+            const int pre = block_excl_scan(S, t < na ? 1 : 0, &tot);
+            if (t < na && S.n_out + pre < NP) {
+                const QNode &q = cur[t];
+                outrec[S.n_out + pre] = ((unsigned long long)(uint32_t)(q.id + 0x40000000) << 32) | qnode_best(q, K);
+            }
+            __syncthreads();
+            if (tid == 0) S.n_out += tot;
+            __syncthreads();
+        }
+    }
+    const int nout = min(S.n_out, NP);
+    for (int i = nout + tid; i < NP; i += ORBX_QT_THREADS) outrec[i] = 0;
+    __syncthreads();
+    block_sort_desc(outrec, NP);
+    const int ncap = min(nout, g.out_cap[l]);
+    uint32_t *dst = sel + (long long)b * g.out_base[g.nlevels] + g.out_base[l];
+    for (int i = tid; i < ncap; i += ORBX_QT_THREADS) dst[i] = (uint32_t)(outrec[i] & 0xFFFFFFFFull);
+    if (tid == 0) sel_cnt[b * g.nlevels + l] = ncap;
+}
+
+// ------------------------------------------------------------------------------------
+// K5: IC_Angle (:94-141) + computeOrbDescriptor (:153-204) + keypoint assembly
+// (:1603-1657). One wavefront per selected keypoint; the moments are exact integer
+// wave reductions, the 256 tests are packed with one ballot per 64 bits.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint8_t *in,
+                                                       const uint8_t *pyr, const uint8_t *blur,
+                                                       const uint32_t *sel, const int *sel_cnt,
+                                                       orbx_kp *kps, uint8_t *desc, int *cnt) {
+    const int lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    const int L = g.nlevels, cap = g.out_base[L];
+    if (slot >= cap) return;
+    int l = 0;
+    while (l + 1 < L && slot >= g.out_base[l + 1]) l++;
+    const int idx = slot - g.out_base[l];
+    const int *sc = sel_cnt + b * L;
+    if (slot == 0 && lane == 0) {
+        int tot = 0;
+        for (int k = 0; k < L; k++) tot += sc[k];
+        cnt[b] = tot;
+    }
+    if (idx >= sc[l]) return;
+    int off = idx;
+    for (int k = 0; k < l; k++) off += sc[k];
+    const uint32_t key = sel[(long long)b * cap + slot];
+    const int x = key_x(key) + 16, y = key_y(key) + 16;  // + minBorderX/Y (:1177-1186)
+    int pitch;
+    const uint8_t *img = level_ptr(g, in, pyr, b, l, &pitch);
+    // IC_Angle over the circular patch (|u| <= umax[|v|])
+    const uint8_t *center = img + (long long)y * pitch + x;
+    int m01 = 0, m10 = 0;
+    for (int t = lane; t < 31 * 31; t += 64) {
+        const int v = t / 31 - 15, u = t % 31 - 15;
+        const int av = v < 0 ? -v : v;
+        if ((u < 0 ? -u : u) <= c_umax[av]) {
+            const int p = center[(long long)v * pitch + u];
+            m10 += u * p;
+            m01 += v * p;
+        }
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    // steered BRIEF on the blurred level
+    const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+    float sa, ca;
+    glibc_sincosf(angle * factorPI, &sa, &ca);
+    const float a = ca, bs = sa;
+    const int bw = g.lw[l];
+    const uint8_t *bc = blur + (long long)b * g.blur_stride + g.blur_off[l] + (long long)y * bw + x;
+    unsigned long long words[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int p = w * 64 + lane;
+        const float px0 = (float)c_pattern[4 * p], py0 = (float)c_pattern[4 * p + 1];
+        const float px1 = (float)c_pattern[4 * p + 2], py1 = (float)c_pattern[4 * p + 3];
+        const int t0 = bc[(long long)cv_round_f(px0 * bs + py0 * a) * bw + cv_round_f(px0 * a - py0 * bs)];
+        const int t1 = bc[(long long)cv_round_f(px1 * bs + py1 * a) * bw + cv_round_f(px1 * a - py1 * bs)];
+        words[w] = __ballot(t0 < t1);
+    }
+    const long long o = (long long)b * cap + off;
+    if (lane == 0) {
+        unsigned long long *d = (unsigned long long *)(desc + o * 32);
+        d[0] = words[0]; d[1] = words[1]; d[2] = words[2]; d[3] = words[3];
+        orbx_kp kp;
+        const float s = g.scale[l];
+        kp.x = (float)x;
+        kp.y = (float)y;
+        if (l != 0) { kp.x *= s; kp.y *= s; }  // :1642-1651
+        kp.size = (float)g.scaled_patch[l];
+        kp.angle = angle;
+        kp.response = (float)key_score(key);
+        kp.octave = l;
+        kp.class_id = -1;
+        kps[o] = kp;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Host: tables and geometry
+// ------------------------------------------------------------------------------------
+static inline int host_round(float v) { return (int)std::lrintf(v); }
+
+static void compute_tables(orbx_engine *e) {
+    const orbx_params &p = e->p;
+    const double sf = (double)p.scale_factor;  // ORBextractor.h:203 double member
+    e->scale[0] = 1.0f;
+    e->sigma2[0] = 1.0f;
+    for (int i = 1; i < p.nlevels; i++) {
+        e->scale[i] = (float)((double)e->scale[i - 1] * sf);
+        e->sigma2[i] = e->scale[i] * e->scale[i];
+    }
+    for (int i = 0; i < p.nlevels; i++) {
+        e->inv_scale[i] = 1.0f / e->scale[i];
+        e->inv_sigma2[i] = 1.0f / e->sigma2[i];
+    }
+    const float factor = (float)(1.0f / sf);
+    float nDesired = p.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)p.nlevels));
+    int sum = 0;
+    for (int l = 0; l < p.nlevels - 1; l++) {
+        e->nfeat[l] = host_round(nDesired);
+        sum += e->nfeat[l];
+        nDesired *= factor;
+    }
+    e->nfeat[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+    const char *hex = ORB_PATTERN_31_HEX;
+    for (int i = 0; i < 1024; i++) {
+        auto nib = [](char ch) { return ch <= '9' ? ch - '0' : (ch | 0x20) - 'a' + 10; };
+        e->pattern[i] = (int8_t)(uint8_t)(nib(hex[2 * i]) * 16 + nib(hex[2 * i + 1]));
+    }
+    int v, v0, vmax = (int)std::floor(15 * std::sqrt(2.f) / 2 + 1);
+    int vmin = (int)std::ceil(15 * std::sqrt(2.f) / 2);
+    const double hp2 = 15 * 15;
+    for (v = 0; v <= vmax; ++v) e->umax[v] = (int)std::lrint(std::sqrt(hp2 - v * v));
+    for (v = 15, v0 = 0; v >= vmin; --v) {
+        while (e->umax[v0] == e->umax[v0 + 1]) ++v0;
+        e->umax[v] = v0;
+        ++v0;
+    }
+}
+
+static int simd_end_for(int width) {
+    int x = 0;
+    for (; x <= width - 16; x += 16) {}
+    for (; x < width - 4; x += 4) {}
+    return x;
+}
+
+int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
+    if (W <= 0 || H <= 0 || max_images <= 0) return ORBX_EINVAL;
+    if (W > 4000 || H > 4000) return ORBX_EINVAL;  // packed keys use 12-bit coordinates
+    HIPCHK(hipSetDevice(e->device));
+    const bool same = (W == e->W && H == e->H);
+    if (same && max_images <= e->max_images) return ORBX_OK;
+    ExtractGeom &g = e->g;
+    if (!same) {
+        g = ExtractGeom{};
+        const int L = e->p.nlevels;
+        g.nlevels = L; g.W = W; g.H = H;
+        long long pyr = 0, blur = 0;
+        for (int l = 0; l < L; l++) {
+            g.lw[l] = host_round((float)W * e->inv_scale[l]);
+            g.lh[l] = host_round((float)H * e->inv_scale[l]);
+            if (g.lw[l] < 40 || g.lh[l] < 40) return ORBX_EINVAL;
+            g.pyr_off[l] = l == 0 ? 0 : pyr;
+            if (l > 0) pyr += ((long long)g.lw[l] * g.lh[l] + 63) & ~63LL;
+            g.blur_off[l] = blur;
+            blur += ((long long)g.lw[l] * g.lh[l] + 63) & ~63LL;
+            g.scale[l] = e->scale[l];
+            g.scaled_patch[l] = (int)(31 * e->scale[l]);
+        }
+        g.pyr_stride = std::max(pyr, 64LL);
+        g.blur_stride = blur;
+        // FAST cell grid (:1046-1153)
+        e->cells.clear();
+        int cell_cap = 0, maxM_total = 0;
+        long long qt = 0;
+        int node_cap = 0;
+        for (int l = 0; l < L; l++) {
+            const int minB = 16, maxBX = g.lw[l] - 19 + 3, maxBY = g.lh[l] - 19 + 3;
+            g.maxBX[l] = maxBX; g.maxBY[l] = maxBY;
+            const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
+            const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
+            if (nCols <= 0 || nRows <= 0) return ORBX_EINVAL;
+            const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+            if (wCell + 6 > ORBX_TMAX || hCell + 6 > ORBX_TMAX) return ORBX_EINVAL;
+            cell_cap = std::max(cell_cap, ((wCell + 1) / 2) * ((hCell + 1) / 2));
+            g.cell_base[l] = (int)e->cells.size();
+            for (int i = 0; i < nRows; i++) {
+                const float iniY = (float)(minB + i * hCell);
+                float maxY = iniY + hCell + 6;
+                if (iniY >= maxBY - 3) continue;
+                if (maxY > maxBY) maxY = (float)maxBY;
+                for (int j = 0; j < nCols; j++) {
+                    const float iniX = (float)(minB + j * wCell);
+                    float maxX = iniX + wCell + 6;
+                    if (iniX >= maxBX - 6) continue;  // this fork's bound (:1112)
+                    if (maxX > maxBX) maxX = (float)maxBX;
+                    CellDesc cd;
+                    cd.level = (int16_t)l;
+                    cd.r0 = (int16_t)(int)iniY; cd.c0 = (int16_t)(int)iniX;
+                    cd.rh = (int16_t)((int)maxY - (int)iniY); cd.rw = (int16_t)((int)maxX - (int)iniX);
+                    cd.offx = (int16_t)(j * wCell); cd.offy = (int16_t)(i * hCell);
+                    cd.pad = 0;
+                    e->cells.push_back(cd);
+                }
+            }
+            const int ncl = (int)e->cells.size() - g.cell_base[l];
+            // quadtree parameters (:700-705)
+            g.N[l] = e->nfeat[l];
+            const int nIni = (int)std::round((float)(maxBX - minB) / (maxBY - minB));
+            if (nIni <= 0 || nIni > 64) return ORBX_EINVAL;
+            g.nIni[l] = nIni;
+            g.hX[l] = (float)(maxBX - minB) / nIni;
+            g.out_cap[l] = std::max(g.N[l] + 3, 4 * nIni);
+            node_cap = std::max(node_cap, g.out_cap[l] + 4);
+            (void)ncl;
+        }
+        g.cell_base[L] = (int)e->cells.size();
+        g.ncell_total = g.cell_base[L];
+        g.cell_cap = cell_cap;
+        g.out_base[0] = 0;
+        for (int l = 0; l < L; l++) g.out_base[l + 1] = g.out_base[l] + g.out_cap[l];
+        for (int l = 0; l < L; l++) {
+            g.qt_off[l] = qt;
+            const long long mcap = (long long)(g.cell_base[l + 1] - g.cell_base[l]) * cell_cap;
+            qt += 2 * mcap;
+            maxM_total = std::max<long long>(maxM_total, mcap);
+        }
+        g.qt_off[L] = qt;
+        g.node_cap = (node_cap + 63) & ~63;
+        int np2 = 1;
+        while (np2 < g.node_cap) np2 <<= 1;
+        g.node_pow2 = np2;
+        const size_t node_bytes = 2 * sizeof(QNode) * g.node_cap + 16 * (size_t)np2;
+        g.qt_nodes_in_lds = node_bytes + 8 * ORBX_QT_KL <= 96 * 1024 ? 1 : 0;
+        g.qt_node_stride = (long long)((node_bytes + 15) / 16) * 4;
+        g.ini_th = e->p.ini_th_fast;
+        g.min_th = e->p.min_th_fast;
+        g.resize_mode = e->p.resize_mode;
+        // resize coefficient tables
+        std::vector<int4> rz;
+        for (int l = 1; l < L; l++) {
+            const int sw = g.lw[l - 1], sh = g.lh[l - 1], dw = g.lw[l], dh = g.lh[l];
+            const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+            g.rz_col_off[l] = (int)rz.size();
+            for (int dx = 0; dx < dw; dx++) {
+                float fx = (float)((dx + 0.5) * scale_x - 0.5);
+                int sx = (int)std::floor(fx);
+                fx -= sx;
+                if (sx < 0) { fx = 0; sx = 0; }
+                if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+                auto satS = [](float v) { int r = host_round(v); return std::min(std::max(r, -32768), 32767); };
+                rz.push_back(make_int4(sx, std::min(sx + 1, sw - 1), satS((1.f - fx) * 2048), satS(fx * 2048)));
+            }
+            g.rz_row_off[l] = (int)rz.size();
+            for (int dy = 0; dy < dh; dy++) {
+                float fy = (float)((dy + 0.5) * scale_y - 0.5);
+                int sy = (int)std::floor(fy);
+                fy -= sy;
+                auto satS = [](float v) { int r = host_round(v); return std::min(std::max(r, -32768), 32767); };
+                auto clip = [sh](int y) { return y >= 0 ? (y < sh ? y : sh - 1) : 0; };
+                rz.push_back(make_int4(clip(sy), clip(sy + 1), satS((1.f - fy) * 2048), satS(fy * 2048)));
+            }
+            g.rz_simd_end[l] = e->p.resize_mode ? simd_end_for(dw) : 0;
+        }
+        if (rz.empty()) rz.push_back(make_int4(0, 0, 0, 0));
+        // blur tiles
+        g.blur_tile_base[0] = 0;
+        for (int l = 0; l < L; l++) {
+            g.blur_tiles_x[l] = (g.lw[l] + 63) / 64;
+            g.blur_tiles_y[l] = (g.lh[l] + 15) / 16;
+            g.blur_tile_base[l + 1] = g.blur_tile_base[l] + g.blur_tiles_x[l] * g.blur_tiles_y[l];
+        }
+        if (e->d_cells.ensure(sizeof(CellDesc) * e->cells.size())) return ORBX_EDEVICE;
+        HIPCHK(hipMemcpy(e->d_cells.p, e->cells.data(), sizeof(CellDesc) * e->cells.size(), hipMemcpyHostToDevice));
+        if (e->d_rz.ensure(sizeof(int4) * rz.size())) return ORBX_EDEVICE;
+        HIPCHK(hipMemcpy(e->d_rz.p, rz.data(), sizeof(int4) * rz.size(), hipMemcpyHostToDevice));
+        e->W = W; e->H = H;
+        e->max_images = 0;
+    }
+    const long long B = max_images;
+    if (e->d_pyr.ensure(B * g.pyr_stride) || e->d_blur.ensure(B * g.blur_stride) ||
+        e->d_cell_cnt.ensure(sizeof(int) * B * g.ncell_total) ||
+        e->d_cell_keys.ensure(sizeof(uint32_t) * B * g.ncell_total * g.cell_cap) ||
+        e->d_qt.ensure(sizeof(uint32_t) * B * g.qt_off[g.nlevels]) ||
+        e->d_qt_nodes.ensure(g.qt_nodes_in_lds ? 16 : (size_t)4 * B * g.nlevels * g.qt_node_stride) ||
+        e->d_sel.ensure(sizeof(uint32_t) * B * g.out_base[g.nlevels]) ||
+        e->d_sel_cnt.ensure(sizeof(int) * B * g.nlevels) ||
+        e->d_kps.ensure(sizeof(orbx_kp) * B * g.out_base[g.nlevels]) ||
+        e->d_desc.ensure((size_t)32 * B * g.out_base[g.nlevels]) || e->d_cnt.ensure(sizeof(int) * B))
+        return ORBX_EDEVICE;
+    e->max_images = max_images;
+    return ORBX_OK;
+}
+
+int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitch,
+                          long long stride, hipStream_t s) {
+    ExtractGeom g = e->g;
+    g.nimg = n;
+    g.in_pitch = pitch;
+    g.in_stride = stride;
+    const int L = g.nlevels;
+    uint8_t *pyr = e->d_pyr.as<uint8_t>();
+    for (int l = 1; l < L; l++) {
+        dim3 grid((g.lw[l] + 255) / 256, g.lh[l], n);
+        resize_level_kernel<<<grid, 256, 0, s>>>(g, l, e->d_rz.as<int4>(), d_imgs, pyr);
+    }
+    fast_cells_kernel<<<dim3(g.ncell_total, n), 64, 0, s>>>(g, e->d_cells.as<CellDesc>(), d_imgs, pyr,
+                                                          e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
+    blur_kernel<<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>());
+    size_t lds = 8 * (size_t)ORBX_QT_KL;
+    if (g.qt_nodes_in_lds) lds += 2 * sizeof(QNode) * g.node_cap + 16 * (size_t)g.node_pow2;
+    quadtree_kernel<<<dim3(L, n), ORBX_QT_THREADS, lds, s>>>(
+        g, e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>(), e->d_qt.as<uint32_t>(),
+        e->d_qt_nodes.as<unsigned char>(), e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>());
+    const int cap = g.out_base[L];
+    describe_kernel<<<dim3((cap + 3) / 4, n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
+                                                          e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>(),
+                                                          e->d_kps.as<orbx_kp>(), e->d_desc.as<uint8_t>(),
+                                                          e->d_cnt.as<int>());
+    HIPCHK(hipGetLastError());
+    e->last_in = d_imgs;
+    e->last_pitch = pitch;
+    e->last_stride = stride;
+    e->last_n = n;
+    return ORBX_OK;
+}
+
+}  // namespace orbamd
+
+// ------------------------------------------------------------------------------------
+// C-ABI
+// ------------------------------------------------------------------------------------
+extern "C" {
+
+const char *orbslam2_amd_version(void) { return "orbslam2_amd 0.1 (gfx950)"; }
+
+int orbslam2_amd_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int orbx_create(const orbx_params *p, orbx_engine **out) {
+    if (!p || !out) return ORBX_EINVAL;
+    *out = nullptr;
+    if (p->nlevels < 1 || p->nlevels > ORBX_MAXL || p->nfeatures < 0 || !(p->scale_factor > 1.0f))
+        return ORBX_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ORBX_EDEVICE;
+    orbx_engine *e = new orbx_engine();
+    e->p = *p;
+    if (hipGetDevice(&e->device) != hipSuccess) { delete e; return ORBX_EDEVICE; }
+    compute_tables(e);
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return ORBX_EDEVICE; }
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), e->pattern, 1024) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_umax), e->umax, sizeof(e->umax)) != hipSuccess) {
+        (void)hipStreamDestroy(e->stream);
+        delete e;
+        return ORBX_EDEVICE;
+    }
+    *out = e;
+    return ORBX_OK;
+}
+
+void orbx_destroy(orbx_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    orbamd::DevBuf *bufs[] = {&e->d_cells, &e->d_rz, &e->d_pattern, &e->d_in, &e->d_pyr, &e->d_blur,
+                              &e->d_cell_cnt, &e->d_cell_keys, &e->d_qt, &e->d_qt_nodes, &e->d_sel,
+                              &e->d_sel_cnt, &e->d_kps, &e->d_desc, &e->d_cnt, &e->d_st_sorted,
+                              &e->d_st_res, &e->d_st_u, &e->d_st_depth, &e->d_st_dist};
+    for (auto *b : bufs) b->release();
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+int orbx_levels(const orbx_engine *e, int *nlevels, float *scale, float *inv_scale, float *sigma2,
+                float *inv_sigma2, int *features_per_level) {
+    if (!e) return ORBX_EINVAL;
+    const int L = e->p.nlevels;
+    if (nlevels) *nlevels = L;
+    for (int l = 0; l < L; l++) {
+        if (scale) scale[l] = e->scale[l];
+        if (inv_scale) inv_scale[l] = e->inv_scale[l];
+        if (sigma2) sigma2[l] = e->sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = e->inv_sigma2[l];
+        if (features_per_level) features_per_level[l] = e->nfeat[l];
+    }
+    return ORBX_OK;
+}
+
+void *orbx_stream(orbx_engine *e) { return e ? (void *)e->stream : nullptr; }
+
+int orbx_reserve(orbx_engine *e, int w, int h, int max_images) {
+    if (!e) return ORBX_EINVAL;
+    return orbamd::engine_reserve(e, w, h, max_images);
+}
+
+int orbx_extract_batch_device(orbx_engine *e, const uint8_t *d_imgs, int n_images, int w, int h,
+                              int pitch, size_t image_stride, void *stream) {
+    if (!e || !d_imgs || n_images <= 0 || pitch < w) return ORBX_EINVAL;
+    int rc = orbamd::engine_reserve(e, w, h, std::max(n_images, e->max_images));
+    if (rc) return rc;
+    return orbamd::engine_extract_device(e, d_imgs, n_images, pitch, (long long)image_stride,
+                                         stream ? (hipStream_t)stream : e->stream);
+}
+
+int orbx_batch_results(orbx_engine *e, const int **d_counts, const orbx_kp **d_kps,
+                       const uint8_t **d_desc, int *cap) {
+    if (!e || e->last_n == 0) return ORBX_ESTATE;
+    if (d_counts) *d_counts = e->d_cnt.as<int>();
+    if (d_kps) *d_kps = e->d_kps.as<orbx_kp>();
+    if (d_desc) *d_desc = e->d_desc.as<uint8_t>();
+    if (cap) *cap = e->g.out_base[e->g.nlevels];
+    return ORBX_OK;
+}
+
+int orbx_batch_fetch(orbx_engine *e, int image, orbx_kp *kps, uint8_t *desc, int cap, int *n) {
+    if (!e || !n) return ORBX_EINVAL;
+    if (e->last_n == 0 || image < 0 || image >= e->last_n) return ORBX_ESTATE;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipDeviceSynchronize());
+    int cnt = 0;
+    HIPCHK(hipMemcpy(&cnt, e->d_cnt.as<int>() + image, sizeof(int), hipMemcpyDeviceToHost));
+    *n = cnt;
+    if (cnt > cap) return ORBX_ECAP;
+    const long long kc = e->g.out_base[e->g.nlevels];
+    if (cnt > 0) {
+        if (kps) HIPCHK(hipMemcpy(kps, e->d_kps.as<orbx_kp>() + image * kc, sizeof(orbx_kp) * cnt, hipMemcpyDeviceToHost));
+        if (desc) HIPCHK(hipMemcpy(desc, e->d_desc.as<uint8_t>() + image * kc * 32, 32 * (size_t)cnt, hipMemcpyDeviceToHost));
+    }
+    return ORBX_OK;
+}
+
+int orbx_extract(orbx_engine *e, const uint8_t *img, int w, int h, int stride, orbx_kp *kps,
+                 uint8_t *desc, int cap, int *n) {
+    if (!e || !n) return ORBX_EINVAL;
+    *n = 0;
+    if (!img || w == 0 || h == 0) return ORBX_OK;  // ORBextractor.cc:1547 returns untouched
+    if (w < 0 || h < 0 || stride < w) return ORBX_EINVAL;
+    HIPCHK(hipSetDevice(e->device));
+    int rc = orbamd::engine_reserve(e, w, h, std::max(1, e->max_images));
+    if (rc) return rc;
+    if (e->d_in.ensure((size_t)w * h)) return ORBX_EDEVICE;
+    HIPCHK(hipMemcpy2DAsync(e->d_in.p, w, img, stride, w, h, hipMemcpyHostToDevice, e->stream));
+    rc = orbamd::engine_extract_device(e, e->d_in.as<uint8_t>(), 1, w, (long long)w * h, e->stream);
+    if (rc) return rc;
+    return orbx_batch_fetch(e, 0, kps, desc, cap, n);
+}
+
+int orbx_pyramid_level(orbx_engine *e, int image, int level, uint8_t *dst, int *w, int *h) {
+    if (!e || level < 0 || level >= e->p.nlevels) return ORBX_EINVAL;
+    if (e->last_n == 0 || image < 0 || image >= e->last_n) return ORBX_ESTATE;
+    const int lw = e->g.lw[level], lh = e->g.lh[level];
+    if (w) *w = lw;
+    if (h) *h = lh;
+    if (!dst) return ORBX_OK;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (level == 0) {
+        HIPCHK(hipMemcpy2D(dst, lw, e->last_in + image * e->last_stride, e->last_pitch, lw, lh, hipMemcpyDeviceToHost));
+    } else {
+        HIPCHK(hipMemcpy(dst, e->d_pyr.as<uint8_t>() + image * e->g.pyr_stride + e->g.pyr_off[level],
+                         (size_t)lw * lh, hipMemcpyDeviceToHost));
+    }
+    return ORBX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,445 @@
+// MI355X-native Frame::ComputeStereoMatches (Frame.cc:831-1128) and the ORBmatcher
+// Hamming core (ORBmatcher.cc:2123-2143).
+//
+// Three kernels per batch of stereo pairs:
+//   S1 stereo_sort_right  one workgroup per pair: right keypoints sorted by y (LDS bitonic)
+//                         -> replaces the vRowIndices row buckets (:858-888)
+//   S2 stereo_match_left  one wavefront per left keypoint: row-band candidates from the
+//                         sorted list, 64-wide popcount Hamming + (dist, index) min-reduce
+//                         (= first minimum in right-index order, :912-978), then the 11x11
+//                         SAD over incR in [-5, 5] (:981-1063), parabola fit and depth
+//   S3 stereo_median_cut  one workgroup per pair: median of the SAD distances and the
+//                         1.5*1.4*median rejection (:1112-1127)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+
+#include "orb_device.h"
+#include "orb_engine.h"
+
+using namespace orbamd;
+
+namespace orbamd {
+
+#define HIPCHK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "orbslam2_amd: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return ORBX_EDEVICE;                                                    \
+        }                                                                           \
+    } while (0)
+
+// One side (left or right) of a batch of stereo pairs: where image p's keypoints,
+// descriptors, counts and pyramid live.
+struct StereoSide {
+    const orbx_kp *kps;
+    const uint8_t *desc;
+    const int *cnt;
+    const uint8_t *in;       // level 0
+    const uint8_t *pyr;      // levels >= 1
+    long long in_stride;
+    int in_pitch;
+    int img_base, img_step;  // image index of pair p = img_base + img_step * p
+};
+
+struct StereoArgs {
+    StereoSide L, R;
+    int cap;                 // keypoint slots per image
+    int sort_cap;            // pow2 >= cap
+    float mbf, mb;
+    float rmax;              // 2 * max scale factor (row-band half-width bound)
+};
+
+__device__ __forceinline__ const uint8_t *side_level(const ExtractGeom &g, const StereoSide &s, int img,
+                                                     int l, int *pitch) {
+    if (l == 0) { *pitch = s.in_pitch; return s.in + (long long)img * s.in_stride; }
+    *pitch = g.lw[l];
+    return s.pyr + (long long)img * g.pyr_stride + g.pyr_off[l];
+}
+
+__device__ __forceinline__ int hamming32(const uint8_t *a, const uint8_t *b) {
+    const uint4 *pa = (const uint4 *)a, *pb = (const uint4 *)b;
+    const uint4 x0 = pa[0], x1 = pa[1], y0 = pb[0], y1 = pb[1];
+    return __popc(x0.x ^ y0.x) + __popc(x0.y ^ y0.y) + __popc(x0.z ^ y0.z) + __popc(x0.w ^ y0.w) +
+           __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
+}
+
+// ---- S1: sort right keypoints of each pair by y (key = float bits, positive floats)
+__global__ __launch_bounds__(256) void stereo_sort_right(StereoArgs a, unsigned long long *sorted) {
+    extern __shared__ unsigned long long sbuf[];
+    const int p = blockIdx.x;
+    const int imgR = a.R.img_base + a.R.img_step * p;
+    const int nR = min(a.R.cnt[imgR], a.cap);
+    const orbx_kp *kR = a.R.kps + (long long)imgR * a.cap;
+    const int n = a.sort_cap;
+    for (int i = threadIdx.x; i < n; i += 256)
+        sbuf[i] = i < nR ? (((unsigned long long)__float_as_uint(kR[i].y) << 32) | (unsigned)i) : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long x = sbuf[i], y = sbuf[ixj];
+                    const bool asc = (i & k) == 0;
+                    if (asc ? (x > y) : (x < y)) { sbuf[i] = y; sbuf[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < n; i += 256) sorted[(long long)p * n + i] = sbuf[i];
+}
+
+// ---- S2: per left keypoint
+__global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoArgs a,
+                                                         const unsigned long long *sorted,
+                                                         float *u_right, float *depth, int *sad) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int iL = blockIdx.x * 4 + wv, p = blockIdx.y;
+    if (iL >= a.cap) return;
+    const int imgL = a.L.img_base + a.L.img_step * p, imgR = a.R.img_base + a.R.img_step * p;
+    const int nL = min(a.L.cnt[imgL], a.cap), nR = min(a.R.cnt[imgR], a.cap);
+    const long long o = (long long)p * a.cap + iL;
+    if (iL >= nL) return;
+    float outU = -1.0f, outD = -1.0f;
+    int outS = -1;
+    const orbx_kp kpL = a.L.kps[(long long)imgL * a.cap + iL];
+    const orbx_kp *kR = a.R.kps + (long long)imgR * a.cap;
+    const int levelL = kpL.octave;
+    const float vL = kpL.y, uL = kpL.x;
+    const float minZ = a.mb, minD = 0, maxD = a.mbf / minZ;
+    const float minU = uL - maxD, maxU = uL - minD;
+    const int row = (int)vL;
+    int bestDist = 100;  // ORBmatcher::TH_HIGH
+    int bestIdxR = 0;
+    if (maxU >= 0) {
+        // candidates: right keypoints whose band [floor(y-r), ceil(y+r)] contains `row`
+        const unsigned long long *srt = sorted + (long long)p * a.sort_cap;
+        const float ylo = (float)row - a.rmax - 2.0f;
+        int lo = 0, hi = nR;  // first entry with y >= ylo
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (__uint_as_float((unsigned)(srt[mid] >> 32)) < ylo) lo = mid + 1; else hi = mid;
+        }
+        const float yhi = (float)row + a.rmax + 2.0f;
+        const uint8_t *dL = a.L.desc + ((long long)imgL * a.cap + iL) * 32;
+        const uint8_t *dR = a.R.desc + (long long)imgR * a.cap * 32;
+        unsigned best = 0xFFFFFFFFu;
+        for (int base = lo; base < nR; base += 64) {
+            const int c = base + lane;
+            bool stop = false;
+            if (c < nR) {
+                const unsigned long long e = srt[c];
+                const float ky = __uint_as_float((unsigned)(e >> 32));
+                if (ky > yhi) stop = true;
+                else {
+                    const int iR = (int)(e & 0xFFFFFFFFu);
+                    const orbx_kp kp = kR[iR];
+                    const float r = 2.0f * g.scale[kp.octave];
+                    const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
+                    if (row >= minr && row <= maxr && kp.octave >= levelL - 1 && kp.octave <= levelL + 1 &&
+                        kp.x >= minU && kp.x <= maxU) {
+                        const int dist = hamming32(dL, dR + (long long)iR * 32);
+                        const unsigned key = ((unsigned)dist << 16) | (unsigned)iR;
+                        best = min(best, key);
+                    }
+                }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) best = min(best, (unsigned)__shfl_xor((int)best, off, 64));
+            if (__any(stop)) break;
+        }
+        if (best != 0xFFFFFFFFu && (int)(best >> 16) < bestDist) {
+            bestDist = (int)(best >> 16);
+            bestIdxR = (int)(best & 0xFFFF);
+        }
+    }
+    const int thOrbDist = (100 + 50) / 2;
+    bool ok = maxU >= 0 && bestDist < thOrbDist;
+    int oct = levelL;
+    float scaleduR0 = 0, scaledvL = 0, scaleduL = 0;
+    int pitchL = 0, pitchR = 0;
+    const uint8_t *imL = nullptr, *imR = nullptr;
+    if (ok) {
+        const float uR0 = kR[bestIdxR].x;
+        const float sf = 1.0f / g.scale[oct];  // mvInvScaleFactors (ORBextractor.cc:503)
+        scaleduL = roundf(kpL.x * sf);
+        scaledvL = roundf(kpL.y * sf);
+        scaleduR0 = roundf(uR0 * sf);
+        const float iniu = scaleduR0 - 5 - 5, endu = scaleduR0 + 5 + 5 + 1;
+        if (iniu < 0 || endu >= g.lw[oct]) ok = false;
+        imL = side_level(g, a.L, imgL, oct, &pitchL);
+        imR = side_level(g, a.R, imgR, oct, &pitchR);
+    }
+    if (ok) {
+        const int r0 = (int)scaledvL - 5, cL0 = (int)scaleduL - 5, cR = (int)scaleduR0;
+        const int cl = imL[(long long)(r0 + 5) * pitchL + cL0 + 5];
+        // partial SAD of (incR, row) pairs t = (inc+5)*11 + rr: lane holds t = lane, lane+64
+        int part0 = 0, part1 = 0;
+        for (int h = 0; h < 2; h++) {
+            const int t = lane + 64 * h;
+            if (t >= 121) continue;
+            const int inc = t / 11 - 5, rr = t % 11;
+            const int cr = imR[(long long)(r0 + 5) * pitchR + cR + inc];
+            const uint8_t *pl = imL + (long long)(r0 + rr) * pitchL + cL0;
+            const uint8_t *pr = imR + (long long)(r0 + rr) * pitchR + cR + inc - 5;
+            int acc = 0;
+#pragma unroll
+            for (int xx = 0; xx < 11; xx++) {
+                const int d = (pl[xx] - cl) - (pr[xx] - cr);
+                acc += d < 0 ? -d : d;
+            }
+            if (h == 0) part0 = acc; else part1 = acc;
+        }
+        // lane k < 11 gathers the 11 rows of incR = k - 5
+        int sum = 0;
+        for (int rr = 0; rr < 11; rr++) {
+            const int src = min(lane, 10) * 11 + rr;
+            const int v0 = __shfl(part0, src & 63, 64);
+            const int v1 = __shfl(part1, src & 63, 64);
+            sum += src < 64 ? v0 : v1;
+        }
+        int sums[11];
+#pragma unroll
+        for (int k = 0; k < 11; k++) sums[k] = __shfl(sum, k, 64);
+        if (lane == 0) {
+            float vd[11];
+            int bestS = INT_MAX, bestinc = 0;
+            for (int inc = -5; inc <= 5; inc++) {
+                const float dist = (float)sums[inc + 5];
+                if (dist < (float)bestS) { bestS = (int)dist; bestinc = inc; }
+                vd[inc + 5] = dist;
+            }
+            if (bestinc != -5 && bestinc != 5) {
+                const float d1 = vd[5 + bestinc - 1], d2 = vd[5 + bestinc], d3 = vd[5 + bestinc + 1];
+                const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
+                if (!(deltaR < -1 || deltaR > 1)) {
+                    float bestuR = g.scale[oct] * ((float)scaleduR0 + (float)bestinc + deltaR);
+                    float disparity = uL - bestuR;
+                    if (disparity >= minD && disparity < maxD) {
+                        if (disparity <= 0) {
+                            disparity = (float)0.01;
+                            bestuR = (float)((double)uL - 0.01);
+                        }
+                        outD = a.mbf / disparity;
+                        outU = bestuR;
+                        outS = bestS;
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        u_right[o] = outU;
+        depth[o] = outD;
+        sad[o] = outS;
+    }
+}
+
+// ---- S3: median of SAD distances and outlier cut
+__global__ __launch_bounds__(256) void stereo_median_cut(StereoArgs a, float *u_right, float *depth,
+                                                         const int *sad) {
+    extern __shared__ int ibuf[];
+    __shared__ int nd;
+    const int p = blockIdx.x;
+    const int imgL = a.L.img_base + a.L.img_step * p;
+    const int nL = min(a.L.cnt[imgL], a.cap);
+    const int n = a.sort_cap;
+    const int *s = sad + (long long)p * a.cap;
+    if (threadIdx.x == 0) nd = 0;
+    for (int i = threadIdx.x; i < n; i += 256) ibuf[i] = INT_MAX;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nL; i += 256) {
+        const int v = s[i];
+        if (v >= 0) ibuf[atomicAdd(&nd, 1)] = v;
+    }
+    __syncthreads();
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const int x = ibuf[i], y = ibuf[ixj];
+                    const bool asc = (i & k) == 0;
+                    if (asc ? (x > y) : (x < y)) { ibuf[i] = y; ibuf[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (nd == 0) return;
+    const float median = (float)ibuf[nd / 2];
+    const float thDist = 1.5f * 1.4f * median;
+    float *u = u_right + (long long)p * a.cap;
+    float *d = depth + (long long)p * a.cap;
+    for (int i = threadIdx.x; i < nL; i += 256) {
+        const int v = s[i];
+        if (v >= 0 && !((float)v < thDist)) { u[i] = -1; d[i] = -1; }
+    }
+}
+
+static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_engine *store,
+                      hipStream_t s) {
+    int sc = 1;
+    while (sc < a.cap) sc <<= 1;
+    a.sort_cap = sc;
+    float smax = 0;
+    for (int l = 0; l < g.nlevels; l++) smax = std::max(smax, g.scale[l]);
+    a.rmax = 2.0f * smax;
+    const size_t slots = (size_t)n_pairs * a.cap;
+    if (store->d_st_sorted.ensure(8 * (size_t)n_pairs * sc) || store->d_st_u.ensure(4 * slots) ||
+        store->d_st_depth.ensure(4 * slots) || store->d_st_dist.ensure(4 * slots))
+        return ORBX_EDEVICE;
+    float *u = store->d_st_u.as<float>(), *d = store->d_st_depth.as<float>();
+    int *sad = store->d_st_dist.as<int>();
+    if (sc * 8 > 64 * 1024) return ORBX_EINVAL;
+    stereo_sort_right<<<n_pairs, 256, 8 * sc, s>>>(a, store->d_st_sorted.as<unsigned long long>());
+    stereo_match_left<<<dim3((a.cap + 3) / 4, n_pairs), 256, 0, s>>>(
+        g, a, store->d_st_sorted.as<unsigned long long>(), u, d, sad);
+    stereo_median_cut<<<n_pairs, 256, 4 * sc, s>>>(a, u, d, sad);
+    HIPCHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+static StereoSide side_of(orbx_engine *e, int base, int step) {
+    StereoSide s;
+    s.kps = e->d_kps.as<orbx_kp>();
+    s.desc = e->d_desc.as<uint8_t>();
+    s.cnt = e->d_cnt.as<int>();
+    s.in = e->last_in;
+    s.pyr = e->d_pyr.as<uint8_t>();
+    s.in_stride = e->last_stride;
+    s.in_pitch = e->last_pitch;
+    s.img_base = base;
+    s.img_step = step;
+    return s;
+}
+
+// ---- brute-force Hamming best / second best (ORBmatcher scan core)
+__global__ __launch_bounds__(256) void hamming_best2_kernel(const uint8_t *q, int nq, const uint8_t *db,
+                                                            int ndb, int *best_idx, int *best_d,
+                                                            int *second_d) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= nq) return;
+    const uint8_t *qi = q + (long long)i * 32;
+    // per-lane (best, second) over its strided subset in ascending index order, then a
+    // merge that keeps the (dist, index) lexicographic minimum as best.
+    unsigned b1 = 0xFFFFFFFFu;   // (dist << 20) | idx
+    int d2 = INT_MAX;
+    for (int j = lane; j < ndb; j += 64) {
+        const int d = hamming32(qi, db + (long long)j * 32);
+        const unsigned key = ((unsigned)d << 20) | (unsigned)j;
+        if (key < b1) {
+            if (b1 != 0xFFFFFFFFu) d2 = min(d2, (int)(b1 >> 20));
+            b1 = key;
+        } else {
+            d2 = min(d2, d);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned ob1 = (unsigned)__shfl_xor((int)b1, off, 64);
+        const int od2 = __shfl_xor(d2, off, 64);
+        const unsigned lo = min(b1, ob1), hi = max(b1, ob1);
+        int s2 = min(d2, od2);
+        if (hi != 0xFFFFFFFFu) s2 = min(s2, (int)(hi >> 20));
+        b1 = lo;
+        d2 = s2;
+    }
+    if (lane == 0) {
+        best_idx[i] = b1 == 0xFFFFFFFFu ? -1 : (int)(b1 & 0xFFFFF);
+        best_d[i] = b1 == 0xFFFFFFFFu ? INT_MAX : (int)(b1 >> 20);
+        second_d[i] = d2;
+    }
+}
+
+}  // namespace orbamd
+
+extern "C" {
+
+int orbm_stereo_match(orbx_engine *left, orbx_engine *right, float mbf, float mb, float *u_right,
+                      float *depth, int n) {
+    if (!left || !right || n < 0) return ORBX_EINVAL;
+    if (left->last_n < 1 || right->last_n < 1) return ORBX_ESTATE;
+    if (left->W != right->W || left->H != right->H || left->p.nlevels != right->p.nlevels) return ORBX_EINVAL;
+    HIPCHK(hipSetDevice(left->device));
+    HIPCHK(hipStreamSynchronize(right->stream));
+    StereoArgs a{};
+    a.L = side_of(left, 0, 1);
+    a.R = side_of(right, 0, 1);
+    a.cap = left->g.out_base[left->g.nlevels];
+    if (right->g.out_base[right->g.nlevels] != a.cap) return ORBX_EINVAL;
+    a.mbf = mbf;
+    a.mb = mb;
+    int rc = run_stereo(left->g, a, 1, left, left->stream);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(left->stream));
+    int cnt = 0;
+    HIPCHK(hipMemcpy(&cnt, left->d_cnt.as<int>(), sizeof(int), hipMemcpyDeviceToHost));
+    if (n != cnt) return ORBX_EINVAL;
+    if (n > 0) {
+        HIPCHK(hipMemcpy(u_right, left->d_st_u.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(depth, left->d_st_depth.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    }
+    return ORBX_OK;
+}
+
+int orbm_stereo_match_batch_device(orbx_engine *e, int n_pairs, float mbf, float mb, void *stream) {
+    if (!e || n_pairs <= 0) return ORBX_EINVAL;
+    if (e->last_n < 2 * n_pairs) return ORBX_ESTATE;
+    StereoArgs a{};
+    a.L = side_of(e, 0, 2);
+    a.R = side_of(e, 1, 2);
+    a.cap = e->g.out_base[e->g.nlevels];
+    a.mbf = mbf;
+    a.mb = mb;
+    return run_stereo(e->g, a, n_pairs, e, stream ? (hipStream_t)stream : e->stream);
+}
+
+int orbm_stereo_results(orbx_engine *e, const float **d_u_right, const float **d_depth) {
+    if (!e || !e->d_st_u.p) return ORBX_ESTATE;
+    if (d_u_right) *d_u_right = e->d_st_u.as<float>();
+    if (d_depth) *d_depth = e->d_st_depth.as<float>();
+    return ORBX_OK;
+}
+
+int orbm_stereo_fetch(orbx_engine *e, int pair, float *u_right, float *depth, int cap) {
+    if (!e || !e->d_st_u.p) return ORBX_ESTATE;
+    const int kc = e->g.out_base[e->g.nlevels];
+    if (cap < kc) return ORBX_ECAP;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(u_right, e->d_st_u.as<float>() + (size_t)pair * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(depth, e->d_st_depth.as<float>() + (size_t)pair * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
+    return ORBX_OK;
+}
+
+int orbm_hamming_best2(const uint8_t *q, int nq, const uint8_t *db, int ndb, int *best_idx, int *best_d,
+                       int *second_d) {
+    if (nq < 0 || ndb < 0 || ndb >= (1 << 20)) return ORBX_EINVAL;
+    if (nq == 0) return ORBX_OK;
+    if (!q || !best_idx || !best_d || !second_d || (ndb > 0 && !db)) return ORBX_EINVAL;
+    uint8_t *dq = nullptr, *ddb = nullptr;
+    int *dout = nullptr;
+    HIPCHK(hipMalloc(&dq, 32 * (size_t)nq));
+    HIPCHK(hipMalloc(&ddb, 32 * (size_t)std::max(ndb, 1)));
+    HIPCHK(hipMalloc(&dout, 12 * (size_t)nq));
+    HIPCHK(hipMemcpy(dq, q, 32 * (size_t)nq, hipMemcpyHostToDevice));
+    if (ndb > 0) HIPCHK(hipMemcpy(ddb, db, 32 * (size_t)ndb, hipMemcpyHostToDevice));
+    hamming_best2_kernel<<<(nq + 3) / 4, 256>>>(dq, nq, ddb, ndb, dout, dout + nq, dout + 2 * nq);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(best_idx, dout, 4 * (size_t)nq, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(best_d, dout + nq, 4 * (size_t)nq, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(second_d, dout + 2 * nq, 4 * (size_t)nq, hipMemcpyDeviceToHost));
+    (void)hipFree(dq);
+    (void)hipFree(ddb);
+    (void)hipFree(dout);
+    return ORBX_OK;
+}
+
+}  // extern "C"

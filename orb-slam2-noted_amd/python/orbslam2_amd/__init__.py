@@ -1,0 +1,239 @@
+"""orbslam2_amd — Python face of the MI355X-native ORB-SLAM2 hot path.
+
+Thin ctypes binding of the C-ABI in include/orbslam2_amd.h (liborbslam2_amd.so, built
+in-tree by orb-slam2-noted_amd/Makefile). The classes mirror the reference classes the
+C-ABI replaces so tests read like the reference's call sites:
+
+* ``ORBextractor``   — ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST),
+                        ``__call__(image) -> (keypoints, descriptors)`` (ORBextractor.h:89-158)
+* ``ORBmatcher``     — ``DescriptorDistance`` and the brute-force best/second-best scan
+                        (ORBmatcher.h:57-65)
+* ``compute_stereo_matches`` — Frame::ComputeStereoMatches (Frame.h:249)
+* ``BatchExtractor`` — the batched, device-resident path used by bench.py
+
+There is no CPU fallback: if the shared library or a GPU is missing, constructing any of
+these raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_ROOT = Path(__file__).resolve().parents[2]          # orb-slam2-noted_amd/
+LIB_PATH = PKG_ROOT / "liborbslam2_amd.so"
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+ORBX_OK, ORBX_EINVAL, ORBX_EDEVICE, ORBX_ECAP, ORBX_ESTATE = 0, -1, -2, -3, -4
+
+
+class OrbxParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32), ("resize_mode", C.c_int32)]
+
+
+class OrbslamError(RuntimeError):
+    pass
+
+
+_lib = None
+
+# (name, restype, argtypes) of every exported C-ABI symbol declared in include/orbslam2_amd.h
+_P = C.c_void_p
+_I = C.c_int
+_F = C.c_float
+SIGNATURES = [
+    ("orbx_create", _I, [C.POINTER(OrbxParams), C.POINTER(C.c_void_p)]),
+    ("orbx_destroy", None, [_P]),
+    ("orbx_levels", _I, [_P, _P, _P, _P, _P, _P, _P]),
+    ("orbx_extract", _I, [_P, _P, _I, _I, _I, _P, _P, _I, _P]),
+    ("orbx_pyramid_level", _I, [_P, _I, _I, _P, _P, _P]),
+    ("orbx_reserve", _I, [_P, _I, _I, _I]),
+    ("orbx_extract_batch_device", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _P]),
+    ("orbx_batch_results", _I, [_P, _P, _P, _P, _P]),
+    ("orbx_batch_fetch", _I, [_P, _I, _P, _P, _I, _P]),
+    ("orbx_stream", _P, [_P]),
+    ("orbm_stereo_match", _I, [_P, _P, _F, _F, _P, _P, _I]),
+    ("orbm_stereo_match_batch_device", _I, [_P, _I, _F, _F, _P]),
+    ("orbm_stereo_results", _I, [_P, _P, _P]),
+    ("orbm_stereo_fetch", _I, [_P, _I, _P, _P, _I]),
+    ("orbm_hamming_best2", _I, [_P, _I, _P, _I, _P, _P, _P]),
+    ("orbslam2_amd_version", C.c_char_p, []),
+    ("orbslam2_amd_device_count", _I, []),
+]
+
+
+def lib() -> C.CDLL:
+    """Load the in-tree HIP library (fails loudly: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise OrbslamError(f"{LIB_PATH} missing: build it with `make -C {PKG_ROOT}` "
+                               "(or __graft_entry__.build())")
+        L = C.CDLL(str(LIB_PATH))
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != ORBX_OK:
+        raise OrbslamError(f"{what} failed with status {rc}")
+
+
+def _p(a: np.ndarray) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data)
+
+
+def device_count() -> int:
+    return lib().orbslam2_amd_device_count()
+
+
+class ORBextractor:
+    """ORBextractor (include/ORBextractor.h:80-216) backed by the HIP kernels."""
+
+    def __init__(self, nfeatures: int, scaleFactor: float = 1.2, nlevels: int = 8,
+                 iniThFAST: int = 20, minThFAST: int = 7, resize_mode: int = 0):
+        self._h = C.c_void_p()
+        p = OrbxParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_mode)
+        _check(lib().orbx_create(C.byref(p), C.byref(self._h)), "orbx_create")
+        self.nfeatures = nfeatures
+        self.nlevels = nlevels
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().orbx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _levels(self):
+        L = self.nlevels
+        arrs = [np.zeros(L, np.float32) for _ in range(4)] + [np.zeros(L, np.int32)]
+        n = C.c_int()
+        _check(lib().orbx_levels(self._h, C.byref(n), *[_p(a) for a in arrs]), "orbx_levels")
+        return arrs
+
+    def GetLevels(self) -> int:
+        return self.nlevels
+
+    def GetScaleFactors(self):
+        return self._levels()[0]
+
+    def GetInverseScaleFactors(self):
+        return self._levels()[1]
+
+    def GetScaleSigmaSquares(self):
+        return self._levels()[2]
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._levels()[3]
+
+    def features_per_level(self):
+        return list(self._levels()[4])
+
+    def __call__(self, image: np.ndarray, mask=None):
+        """operator()(image, mask, keypoints, descriptors); returns (keypoints, descriptors)."""
+        img = np.ascontiguousarray(image, np.uint8)
+        if img.ndim != 2:
+            raise ValueError("expects a single-channel u8 image (ORBextractor.cc:1553)")
+        h, w = img.shape
+        cap = max(64, self.nfeatures * 2 + 512)
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int()
+        _check(lib().orbx_extract(self._h, _p(img), w, h, w, _p(kps), _p(desc), cap, C.byref(n)),
+               "orbx_extract")
+        return kps[: n.value].copy(), desc[: n.value].copy()
+
+    def pyramid_level(self, level: int, image: int = 0) -> np.ndarray:
+        w, h = C.c_int(), C.c_int()
+        _check(lib().orbx_pyramid_level(self._h, image, level, None, C.byref(w), C.byref(h)), "pyramid")
+        out = np.zeros((h.value, w.value), np.uint8)
+        _check(lib().orbx_pyramid_level(self._h, image, level, _p(out), None, None), "pyramid")
+        return out
+
+
+class BatchExtractor(ORBextractor):
+    """Batched device-resident extraction: many frames per launch (bench / throughput)."""
+
+    def reserve(self, w: int, h: int, max_images: int):
+        _check(lib().orbx_reserve(self._h, w, h, max_images), "orbx_reserve")
+
+    def extract_device(self, d_ptr: int, n_images: int, w: int, h: int, pitch: int,
+                       image_stride: int, stream: int | None = None):
+        _check(lib().orbx_extract_batch_device(self._h, C.c_void_p(d_ptr), n_images, w, h, pitch,
+                                               image_stride, C.c_void_p(stream or 0)),
+               "orbx_extract_batch_device")
+
+    def stream(self) -> int:
+        return lib().orbx_stream(self._h) or 0
+
+    def fetch(self, image: int):
+        cap = max(64, self.nfeatures * 2 + 512)
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int()
+        _check(lib().orbx_batch_fetch(self._h, image, _p(kps), _p(desc), cap, C.byref(n)), "orbx_batch_fetch")
+        return kps[: n.value].copy(), desc[: n.value].copy()
+
+    def results(self):
+        cnt, kps, desc, cap = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int()
+        _check(lib().orbx_batch_results(self._h, C.byref(cnt), C.byref(kps), C.byref(desc), C.byref(cap)),
+               "orbx_batch_results")
+        return cnt.value, kps.value, desc.value, cap.value
+
+    def stereo_batch(self, n_pairs: int, mbf: float, mb: float, stream: int | None = None):
+        _check(lib().orbm_stereo_match_batch_device(self._h, n_pairs, mbf, mb, C.c_void_p(stream or 0)),
+               "orbm_stereo_match_batch_device")
+
+    def stereo_fetch(self, pair: int):
+        cap = max(64, self.nfeatures * 2 + 512)
+        u = np.zeros(cap, np.float32)
+        d = np.zeros(cap, np.float32)
+        _check(lib().orbm_stereo_fetch(self._h, pair, _p(u), _p(d), cap), "orbm_stereo_fetch")
+        return u, d
+
+
+def compute_stereo_matches(left: ORBextractor, right: ORBextractor, n_left: int, mbf: float, mb: float):
+    """Frame::ComputeStereoMatches over the two extractors' last frames -> (mvuRight, mvDepth)."""
+    u = np.zeros(max(n_left, 1), np.float32)
+    d = np.zeros(max(n_left, 1), np.float32)
+    _check(lib().orbm_stereo_match(left.handle, right.handle, mbf, mb, _p(u), _p(d), n_left), "orbm_stereo_match")
+    return u[:n_left], d[:n_left]
+
+
+class ORBmatcher:
+    """ORBmatcher Hamming core (ORBmatcher.h:57-65)."""
+
+    TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True):
+        self.mfNNratio = nnratio
+        self.mbCheckOrientation = checkOri
+
+    @staticmethod
+    def hamming_best2(q: np.ndarray, db: np.ndarray):
+        q = np.ascontiguousarray(q, np.uint8)
+        db = np.ascontiguousarray(db, np.uint8)
+        n = len(q)
+        bi = np.zeros(max(n, 1), np.int32)
+        bd = np.zeros(max(n, 1), np.int32)
+        sd = np.zeros(max(n, 1), np.int32)
+        _check(lib().orbm_hamming_best2(_p(q), n, _p(db), len(db), _p(bi), _p(bd), _p(sd)), "orbm_hamming_best2")
+        return bi[:n], bd[:n], sd[:n]

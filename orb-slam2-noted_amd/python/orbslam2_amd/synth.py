@@ -1,0 +1,117 @@
+"""Seeded synthetic inputs for the benchmark configs.
+
+No datasets exist on the build or GPU boxes, so every workload is synthetic:
+
+* ``textured_image``  — value noise (4 octaves, base 64 px) + 200 rectangles (axis-aligned
+  and rotated) + 100 discs with random u8 intensities + uniform noise in [-4, 4], clamped
+  to u8 (C1/C2/C3 generator).
+* ``stereo_pair``     — the left image plus a right image warped by a piecewise-planar
+  disparity field d(x, y) in [2, 96] px built from 8 random planes, with +-2 noise (C2).
+* ``rgbd_frame``      — gray frame + float depth (metres) from a piecewise-planar Z field in
+  [0.5, 4] m with 5 % zero holes (C3; depth = u16/5000 as TUM1.yaml:35 / Tracking.cc:334).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _value_noise(rng: np.random.Generator, h: int, w: int, base: int = 64, octaves: int = 4) -> np.ndarray:
+    out = np.zeros((h, w), np.float64)
+    amp, total = 1.0, 0.0
+    for o in range(octaves):
+        step = max(2, base >> o)
+        gh, gw = h // step + 2, w // step + 2
+        grid = rng.random((gh, gw))
+        ys = np.arange(h) / step
+        xs = np.arange(w) / step
+        y0 = ys.astype(int)
+        x0 = xs.astype(int)
+        fy = (ys - y0)[:, None]
+        fx = (xs - x0)[None, :]
+        g00 = grid[y0][:, x0]
+        g01 = grid[y0][:, x0 + 1]
+        g10 = grid[y0 + 1][:, x0]
+        g11 = grid[y0 + 1][:, x0 + 1]
+        out += amp * ((1 - fy) * ((1 - fx) * g00 + fx * g01) + fy * ((1 - fx) * g10 + fx * g11))
+        total += amp
+        amp *= 0.5
+    return out / total
+
+
+def textured_image(h: int, w: int, seed: int) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    img = 40.0 + 175.0 * _value_noise(rng, h, w)
+    yy, xx = np.mgrid[0:h, 0:w]
+    for _ in range(200):
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        hw, hh = rng.uniform(4, 40), rng.uniform(4, 40)
+        val = rng.integers(0, 256)
+        if rng.random() < 0.5:
+            x0, x1 = int(max(cx - hw, 0)), int(min(cx + hw, w))
+            y0, y1 = int(max(cy - hh, 0)), int(min(cy + hh, h))
+            img[y0:y1, x0:x1] = val
+        else:
+            th = rng.uniform(0, np.pi)
+            r = int(np.ceil(np.hypot(hw, hh))) + 1
+            x0, x1 = int(max(cx - r, 0)), int(min(cx + r, w))
+            y0, y1 = int(max(cy - r, 0)), int(min(cy + r, h))
+            if x1 <= x0 or y1 <= y0:
+                continue
+            dx = xx[y0:y1, x0:x1] - cx
+            dy = yy[y0:y1, x0:x1] - cy
+            u = dx * np.cos(th) + dy * np.sin(th)
+            v = -dx * np.sin(th) + dy * np.cos(th)
+            m = (np.abs(u) <= hw) & (np.abs(v) <= hh)
+            img[y0:y1, x0:x1][m] = val
+    for _ in range(100):
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        r = rng.uniform(3, 30)
+        val = rng.integers(0, 256)
+        x0, x1 = int(max(cx - r, 0)), int(min(cx + r + 1, w))
+        y0, y1 = int(max(cy - r, 0)), int(min(cy + r + 1, h))
+        if x1 <= x0 or y1 <= y0:
+            continue
+        m = (xx[y0:y1, x0:x1] - cx) ** 2 + (yy[y0:y1, x0:x1] - cy) ** 2 <= r * r
+        img[y0:y1, x0:x1][m] = val
+    img += rng.integers(-4, 5, size=(h, w))
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def _planar_field(rng: np.random.Generator, h: int, w: int, lo: float, hi: float, nplanes: int = 8) -> np.ndarray:
+    sx, sy = rng.uniform(0, w, nplanes), rng.uniform(0, h, nplanes)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    d2 = (xx[None] - sx[:, None, None]) ** 2 + (yy[None] - sy[:, None, None]) ** 2
+    lab = np.argmin(d2, axis=0)
+    a = rng.uniform(lo, hi, nplanes)
+    bx = rng.uniform(-0.02, 0.02, nplanes) * (hi - lo) / 10
+    by = rng.uniform(-0.02, 0.02, nplanes) * (hi - lo) / 10
+    f = a[lab] + bx[lab] * (xx - sx[lab]) + by[lab] * (yy - sy[lab])
+    return np.clip(f, lo, hi)
+
+
+def stereo_pair(h: int, w: int, t: int, base_seed: int = 2) -> tuple[np.ndarray, np.ndarray]:
+    """C2 generator: left = textured_image(seed 2+t); right = left warped by disparity."""
+    left = textured_image(h, w, base_seed + t)
+    rng = np.random.default_rng(1000 + base_seed + t)
+    disp = _planar_field(rng, h, w, 2.0, 96.0)
+    xs = np.arange(w)[None, :] + disp
+    xi = np.clip(np.rint(xs).astype(int), 0, w - 1)
+    right = np.take_along_axis(left, xi, axis=1).astype(np.int32)
+    nrng = np.random.default_rng(2000 + base_seed + t)
+    right += nrng.integers(-2, 3, size=(h, w))
+    return left, np.clip(right, 0, 255).astype(np.uint8)
+
+
+def rgbd_frame(h: int, w: int, t: int, base_seed: int = 3) -> tuple[np.ndarray, np.ndarray]:
+    """C3 generator: gray frame shifted 0-3 px per frame + float depth (m), 5 % holes."""
+    base = textured_image(h + 64, w + 64, base_seed)
+    sx = (t * 3) % 32
+    sy = (t * 2) % 32
+    gray = np.ascontiguousarray(base[sy:sy + h, sx:sx + w])
+    rng = np.random.default_rng(5000 + base_seed + t)
+    z = _planar_field(rng, h, w, 0.5, 4.0)
+    depth_u16 = np.rint(z * 5000.0).astype(np.uint16)
+    holes = rng.random((h, w)) < 0.05
+    depth_u16[holes] = 0
+    depth = (depth_u16.astype(np.float32) * np.float32(1.0 / 5000.0)).astype(np.float32)
+    return gray, depth
