@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: ORB extract + stereo match throughput (BASELINE.json metric) on MI355X.
+
+Workload (BASELINE.json configs[1]): KITTI-like synthetic stereo pairs
+1241x376, ORBextractor(2000, 1.2, 8, 20, 7) on left and right + Frame::ComputeStereoMatches
+(KITTI00-02.yaml bf=386.1448, fx=718.856). One step = one batch of B stereo frames already
+resident in HBM: 2B images through pyramid / FAST / blur / quadtree / IC_Angle+BRIEF, then
+B stereo matches. `value` = stereo frames/s over all ranks.
+
+Multi-GPU (C5): one process per GPU (torchrun), each rank runs its own stream of batches
+(weak scaling); the shared read-only extractor/camera state is broadcast from rank 0 once
+over RCCL (torch.distributed nccl backend) before timing. No per-frame collective.
+
+Also reported: `roofline` for the dominant kernel (hipEvent durations on the engine's
+stream over the timed region) and `cpu_baseline` = the CPU oracle (single-threaded C
+restatement, oracle/) on a bounded sample of the same workload, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "orb-slam2-noted_amd" / "python"))
+
+KITTI_BF = 386.1448
+KITTI_FX = 718.856
+W, H = 1241, 376
+NFEAT = 2000
+BYTES_PER_STEREO_FRAME = 2 * W * H + 2 * NFEAT * (28 + 32) + NFEAT * 8   # 1,189,232 B
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_pool(n_pairs: int, seed0: int):
+    from orbslam2_amd import synth
+    return [synth.stereo_pair(H, W, seed0 + t) for t in range(n_pairs)]
+
+
+def cpu_baseline(pool, n_frames: int):
+    """Time the CPU oracle (test infrastructure) on n_frames stereo frames, one thread."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    oracle.build()
+    exL, exR = oracle.Extractor(NFEAT), oracle.Extractor(NFEAT)
+    mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        L, R = pool[i % len(pool)]
+        kL, dL = exL.extract(L)
+        kR, dR = exR.extract(R)
+        oracle.stereo_matches(exL, exR, kL, dL, kR, dR, KITTI_BF, mb)
+    dt = time.perf_counter() - t0
+    return {"value": round(n_frames / dt, 3), "unit": "stereo frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n_frames} synthetic 1241x376 stereo frames (C2 generator, {len(pool)} distinct), "
+                      f"oracle extract L+R + ComputeStereoMatches, single thread, {dt:.1f} s"}
+
+
+def load_traffic(kernel: str, batch: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        ent = d.get("kernels", {}).get(kernel)
+        if ent and int(d.get("batch", -1)) == batch:
+            return ent.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=128, help="stereo frames per step")
+    ap.add_argument("--pool", type=int, default=8, help="distinct synthetic stereo pairs")
+    ap.add_argument("--bufs", type=int, default=4, help="rotating resident input batches")
+    ap.add_argument("--cpu-frames", type=int, default=96)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    torch.cuda.set_device(local_rank)
+    torch.cuda.init()
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    import orbslam2_amd as amd
+    amd.set_device(local_rank)
+
+    B = args.batch
+    # shared read-only state: ORB params + camera, broadcast once from rank 0 over RCCL
+    shared = torch.tensor([NFEAT, 1.2, 8, 20, 7, KITTI_BF, KITTI_FX, W, H], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        dist.broadcast(shared, src=0)
+    nf, sf, nl, ith, mth, bf, fx, w, h = shared.tolist()
+    mb = float(np.float32(bf) / np.float32(fx))
+
+    pool = make_pool(args.pool, 2 + 100 * rank)
+    bufs = []
+    for k in range(args.bufs):
+        imgs = np.empty((2 * B, H, W), np.uint8)
+        for i in range(B):
+            L, R = pool[(i + 3 * k) % len(pool)]
+            if k:  # make rotating buffers differ (avoid identical cached inputs)
+                L = np.roll(L, 7 * k, axis=1)
+                R = np.roll(R, 7 * k, axis=1)
+            imgs[2 * i], imgs[2 * i + 1] = L, R
+        bufs.append(torch.from_numpy(imgs).cuda())
+    torch.cuda.synchronize()
+
+    ex = amd.BatchExtractor(int(nf), float(sf), int(nl), int(ith), int(mth))
+    ex.reserve(W, H, 2 * B)
+
+    def step(k):
+        t = bufs[k % len(bufs)]
+        ex.extract_device(t.data_ptr(), 2 * B, W, H, W, W * H)
+        ex.stereo_batch(B, float(bf), mb)
+
+    for k in range(args.warmup):
+        step(k)
+    amd.device_sync()
+    if not args.no_profile:
+        ex.profile(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    amd.device_sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    amd.device_sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = ex.profile_read() if not args.no_profile else {}
+    ex.profile(False)
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # sanity: the batch produced keypoints and stereo matches
+    k0, _ = ex.fetch(0)
+    u0, _ = ex.stereo_fetch(0)
+    n_match = int((u0[: len(k0)] >= 0).sum())
+    if len(k0) < 100 or n_match < 10:
+        raise RuntimeError(f"implausible output: {len(k0)} keypoints, {n_match} stereo matches")
+
+    frames = B * args.steps * world
+    value = frames / elapsed
+    out = {
+        "metric": "frames/sec ORB extract+match @1241x376 (1 GPU) + LocalBA keyframes/sec",
+        "value": round(value, 2),
+        "unit": "stereo frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": "C2: KITTI-like synthetic stereo 1241x376, ORBextractor(2000,1.2,8,20,7) L+R "
+                        "+ Frame::ComputeStereoMatches",
+            "stereo_frames_per_step_per_gpu": B,
+            "image": f"{W}x{H}",
+            "nfeatures": NFEAT,
+            "parallelism": f"independent sequence per GPU x{world}",
+            "keypoints_img0": int(len(k0)),
+            "stereo_matches_img0": n_match,
+        },
+        "localba_kf_per_s": None,
+    }
+    if prof:
+        name, (tot, n) = max(prof.items(), key=lambda kv: kv[1][0])
+        avg_s = tot / n / 1000.0
+        achieved = BYTES_PER_STEREO_FRAME * B / avg_s / 1e9
+        traffic = load_traffic(name, B)
+        out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 3),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                           "traffic": traffic, "avg_launch_ms": round(tot / n, 4),
+                           "algorithmic_bytes_per_launch": BYTES_PER_STEREO_FRAME * B}
+        out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pool, args.cpu_frames)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

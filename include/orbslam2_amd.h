@@ -110,9 +110,20 @@ int orbm_stereo_fetch(orbx_engine *e, int pair, float *u_right, float *depth, in
 int orbm_hamming_best2(const uint8_t *q, int nq, const uint8_t *db, int ndb, int *best_idx,
                        int *best_d, int *second_d);
 
-/* -------- library -------- */
+/* -------- library / measurement -------- */
 const char *orbslam2_amd_version(void);
 int orbslam2_amd_device_count(void);
+/* hipSetDevice for the calling thread (engines bind the current device at create). */
+int orbslam2_amd_set_device(int device);
+/* hipDeviceSynchronize on this library's HIP runtime. */
+int orbslam2_amd_device_sync(void);
+/* Per-kernel hipEvent timing on the launch stream (bench roofline). enable != 0 clears
+ * and starts recording; orbx_profile_read aggregates record idx (0..) by kernel name and
+ * returns ORBX_ESTATE past the last name. No reference counterpart (the reference only
+ * times whole frames, stereo_kitti.cc:96-102). */
+int orbx_profile(orbx_engine *e, int enable);
+int orbx_profile_read(orbx_engine *e, int idx, char *name, int name_cap, double *total_ms,
+                      int *launches);
 
 #ifdef __cplusplus
 }

@@ -83,9 +83,19 @@ struct orbx_engine {
     long long last_stride = 0;
     int last_n = 0;
     std::string err;
+    // per-kernel hipEvent profiling (bench.py roofline), recorded on the launch stream
+    bool prof = false;
+    struct ProfRec { const char *name; hipEvent_t a, b; };
+    std::vector<ProfRec> prof_recs;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
 };
 
 namespace orbamd {
+// profiling helpers: prof_begin records a start event (returns a handle), prof_end the
+// matching stop event; both are no-ops when profiling is off.
+int prof_begin(orbx_engine *e, hipStream_t s);
+void prof_end(orbx_engine *e, hipStream_t s, int h, const char *name);
 int engine_reserve(orbx_engine *e, int w, int h, int max_images);
 int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitch,
                           long long stride, hipStream_t s);

@@ -800,6 +800,27 @@ static void compute_tables(orbx_engine *e) {
     }
 }
 
+int prof_begin(orbx_engine *e, hipStream_t s) {
+    if (!e->prof) return -1;
+    if (e->ev_used + 2 > e->ev_pool.size()) {
+        for (int k = 0; k < 64; k++) {
+            hipEvent_t ev;
+            if (hipEventCreate(&ev) != hipSuccess) return -1;
+            e->ev_pool.push_back(ev);
+        }
+    }
+    const int h = (int)e->ev_used;
+    e->ev_used += 2;
+    (void)hipEventRecord(e->ev_pool[h], s);
+    return h;
+}
+
+void prof_end(orbx_engine *e, hipStream_t s, int h, const char *name) {
+    if (!e->prof || h < 0) return;
+    (void)hipEventRecord(e->ev_pool[h + 1], s);
+    e->prof_recs.push_back({name, e->ev_pool[h], e->ev_pool[h + 1]});
+}
+
 static int simd_end_for(int width) {
     int x = 0;
     for (; x <= width - 16; x += 16) {}
@@ -963,23 +984,33 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     g.in_stride = stride;
     const int L = g.nlevels;
     uint8_t *pyr = e->d_pyr.as<uint8_t>();
+    int ph = prof_begin(e, s);
     for (int l = 1; l < L; l++) {
         dim3 grid((g.lw[l] + 255) / 256, g.lh[l], n);
         resize_level_kernel<<<grid, 256, 0, s>>>(g, l, e->d_rz.as<int4>(), d_imgs, pyr);
     }
+    prof_end(e, s, ph, "resize_level_kernel");
+    ph = prof_begin(e, s);
     fast_cells_kernel<<<dim3(g.ncell_total, n), 64, 0, s>>>(g, e->d_cells.as<CellDesc>(), d_imgs, pyr,
                                                           e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
+    prof_end(e, s, ph, "fast_cells_kernel");
+    ph = prof_begin(e, s);
     blur_kernel<<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>());
+    prof_end(e, s, ph, "blur_kernel");
+    ph = prof_begin(e, s);
     size_t lds = 8 * (size_t)ORBX_QT_KL;
     if (g.qt_nodes_in_lds) lds += 2 * sizeof(QNode) * g.node_cap + 16 * (size_t)g.node_pow2;
     quadtree_kernel<<<dim3(L, n), ORBX_QT_THREADS, lds, s>>>(
         g, e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>(), e->d_qt.as<uint32_t>(),
         e->d_qt_nodes.as<unsigned char>(), e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>());
+    prof_end(e, s, ph, "quadtree_kernel");
     const int cap = g.out_base[L];
+    ph = prof_begin(e, s);
     describe_kernel<<<dim3((cap + 3) / 4, n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
                                                           e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>(),
                                                           e->d_kps.as<orbx_kp>(), e->d_desc.as<uint8_t>(),
                                                           e->d_cnt.as<int>());
+    prof_end(e, s, ph, "describe_kernel");
     HIPCHK(hipGetLastError());
     e->last_in = d_imgs;
     e->last_pitch = pitch;
@@ -1034,6 +1065,7 @@ void orbx_destroy(orbx_engine *e) {
                               &e->d_sel_cnt, &e->d_kps, &e->d_desc, &e->d_cnt, &e->d_st_sorted,
                               &e->d_st_res, &e->d_st_u, &e->d_st_depth, &e->d_st_dist};
     for (auto *b : bufs) b->release();
+    for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -1054,6 +1086,48 @@ int orbx_levels(const orbx_engine *e, int *nlevels, float *scale, float *inv_sca
 }
 
 void *orbx_stream(orbx_engine *e) { return e ? (void *)e->stream : nullptr; }
+
+int orbslam2_amd_set_device(int device) {
+    return hipSetDevice(device) == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+int orbslam2_amd_device_sync(void) {
+    return hipDeviceSynchronize() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+int orbx_profile(orbx_engine *e, int enable) {
+    if (!e) return ORBX_EINVAL;
+    if (e->prof) (void)hipDeviceSynchronize();
+    e->prof = enable != 0;
+    e->prof_recs.clear();
+    e->ev_used = 0;
+    return ORBX_OK;
+}
+
+int orbx_profile_read(orbx_engine *e, int idx, char *name, int name_cap, double *total_ms,
+                      int *launches) {
+    if (!e || idx < 0) return ORBX_EINVAL;
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<std::string> names;
+    for (auto &r : e->prof_recs)
+        if (std::find(names.begin(), names.end(), std::string(r.name)) == names.end()) names.push_back(r.name);
+    if (idx >= (int)names.size()) return ORBX_ESTATE;
+    double tot = 0;
+    int cnt = 0;
+    for (auto &r : e->prof_recs) {
+        if (names[idx] != r.name) continue;
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, r.a, r.b));
+        tot += ms;
+        cnt++;
+    }
+    if (name && name_cap > 0) {
+        std::snprintf(name, (size_t)name_cap, "%s", names[idx].c_str());
+    }
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = cnt;
+    return ORBX_OK;
+}
 
 int orbx_reserve(orbx_engine *e, int w, int h, int max_images) {
     if (!e) return ORBX_EINVAL;

@@ -297,10 +297,16 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
     float *u = store->d_st_u.as<float>(), *d = store->d_st_depth.as<float>();
     int *sad = store->d_st_dist.as<int>();
     if (sc * 8 > 64 * 1024) return ORBX_EINVAL;
+    int ph = prof_begin(store, s);
     stereo_sort_right<<<n_pairs, 256, 8 * sc, s>>>(a, store->d_st_sorted.as<unsigned long long>());
+    prof_end(store, s, ph, "stereo_sort_right");
+    ph = prof_begin(store, s);
     stereo_match_left<<<dim3((a.cap + 3) / 4, n_pairs), 256, 0, s>>>(
         g, a, store->d_st_sorted.as<unsigned long long>(), u, d, sad);
+    prof_end(store, s, ph, "stereo_match_left");
+    ph = prof_begin(store, s);
     stereo_median_cut<<<n_pairs, 256, 4 * sc, s>>>(a, u, d, sad);
+    prof_end(store, s, ph, "stereo_median_cut");
     HIPCHK(hipGetLastError());
     return ORBX_OK;
 }

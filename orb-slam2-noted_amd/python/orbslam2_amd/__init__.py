@@ -64,13 +64,37 @@ SIGNATURES = [
     ("orbm_hamming_best2", _I, [_P, _I, _P, _I, _P, _P, _P]),
     ("orbslam2_amd_version", C.c_char_p, []),
     ("orbslam2_amd_device_count", _I, []),
+    ("orbslam2_amd_device_sync", _I, []),
+    ("orbslam2_amd_set_device", _I, [_I]),
+    ("orbx_profile", _I, [_P, _I]),
+    ("orbx_profile_read", _I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 ]
+
+
+def _init_torch_runtime_first():
+    """torch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so) while this library
+    links /opt/rocm's. Both coexist in one process -- and device pointers are shared -- only
+    if torch's runtime initialises the device first (probed on MI355X by
+    tools/probe_runtime.py), so touch torch.cuda before loading our library when torch is
+    importable. Without torch nothing is needed."""
+    if os.environ.get("ORBSLAM2_AMD_NO_TORCH"):
+        return
+    try:
+        import torch
+    except Exception:
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
 
 
 def lib() -> C.CDLL:
     """Load the in-tree HIP library (fails loudly: there is no CPU fallback)."""
     global _lib
     if _lib is None:
+        _init_torch_runtime_first()
         if not LIB_PATH.exists():
             raise OrbslamError(f"{LIB_PATH} missing: build it with `make -C {PKG_ROOT}` "
                                "(or __graft_entry__.build())")
@@ -94,6 +118,14 @@ def _p(a: np.ndarray) -> C.c_void_p:
 
 def device_count() -> int:
     return lib().orbslam2_amd_device_count()
+
+
+def set_device(device: int):
+    _check(lib().orbslam2_amd_set_device(device), "set_device")
+
+
+def device_sync():
+    _check(lib().orbslam2_amd_device_sync(), "device_sync")
 
 
 class ORBextractor:
@@ -183,6 +215,24 @@ class BatchExtractor(ORBextractor):
 
     def stream(self) -> int:
         return lib().orbx_stream(self._h) or 0
+
+    def profile(self, enable: bool):
+        _check(lib().orbx_profile(self._h, 1 if enable else 0), "orbx_profile")
+
+    def profile_read(self) -> dict:
+        """{kernel name: (total ms, launches)} of the hipEvent records since profile(True)."""
+        out = {}
+        i = 0
+        buf = C.create_string_buffer(64)
+        while True:
+            ms, n = C.c_double(), C.c_int()
+            rc = lib().orbx_profile_read(self._h, i, buf, 64, C.byref(ms), C.byref(n))
+            if rc == ORBX_ESTATE:
+                break
+            _check(rc, "orbx_profile_read")
+            out[buf.value.decode()] = (ms.value, n.value)
+            i += 1
+        return out
 
     def fetch(self, image: int):
         cap = max(64, self.nfeatures * 2 + 512)
