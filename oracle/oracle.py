@@ -234,3 +234,51 @@ def search_for_initialization(F1: Grid, F2: Grid, prev_xy: np.ndarray, window=10
     n = lib().orc_search_for_initialization(C.byref(F1.g), C.byref(F2.g), _p(prev), _p(m12), window, nnratio,
                                             1 if check_ori else 0)
     return n, m12[: len(F1.keys_un)], prev
+
+
+def distribute_octtree(keys: np.ndarray, minX: int, maxX: int, minY: int, maxY: int, N: int):
+    """ExtractorNode quadtree (ORBextractor.cc:696-1042) on cell-offset candidates."""
+    keys = np.ascontiguousarray(keys, KP_DTYPE)
+    cap = max(N, 0) + 4 * 64 + len(keys) + 16
+    out = np.zeros(cap, KP_DTYPE)
+    n = lib().orc_distribute_octtree(_p(keys), len(keys), minX, maxX, minY, maxY, N, _p(out), cap)
+    if n < 0:
+        raise ValueError("nIni == 0")
+    return out[:n].copy()
+
+
+def fast_roi(roi: np.ndarray, th: int):
+    roi = np.ascontiguousarray(roi, np.uint8)
+    h, w = roi.shape
+    cap = h * w + 1
+    xs, ys, sc = (np.zeros(cap, np.int32) for _ in range(3))
+    n = lib().orc_fast_roi(_p(roi), w, h, w, th, _p(xs), _p(ys), _p(sc), cap)
+    return xs[:n].copy(), ys[:n].copy(), sc[:n].copy()
+
+
+def gaussian_blur9(img: np.ndarray) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros_like(img)
+    lib().orc_gaussian_blur9(_p(img), img.shape[1], img.shape[0], _p(out))
+    return out
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int, mode: int = 0) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros((dh, dw), np.uint8)
+    lib().orc_resize_linear(_p(src), src.shape[1], src.shape[0], src.shape[1], _p(out), dw, dh, dw, mode)
+    return out
+
+
+def ic_angle(img: np.ndarray, x: float, y: float, umax) -> float:
+    img = np.ascontiguousarray(img, np.uint8)
+    um = np.ascontiguousarray(umax, np.int32)
+    return lib().orc_ic_angle(_p(img), img.shape[1], x, y, _p(um))
+
+
+def orb_descriptor(blur: np.ndarray, x: float, y: float, angle: float, pattern) -> np.ndarray:
+    blur = np.ascontiguousarray(blur, np.uint8)
+    pat = np.ascontiguousarray(pattern, np.int32)
+    out = np.zeros(32, np.uint8)
+    lib().orc_orb_descriptor(_p(blur), blur.shape[1], x, y, angle, _p(pat), _p(out))
+    return out

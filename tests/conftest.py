@@ -14,6 +14,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "orb-slam2-noted_amd" / "python"))
 sys.path.insert(0, str(ROOT / "oracle"))
 sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
 
 
 def pytest_configure(config):

@@ -103,3 +103,20 @@ def test_batch_device_matches_single(amd, oracle_mod):
     ref = oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
     for i in range(n):
         _assert_same_kps(ex.fetch(i), ref.extract(imgs[i]), f"batch[{i}]")
+
+
+def test_golden_c1_c2_on_device(amd):
+    """HIP path == committed golden fixtures (independent of the oracle at run time)."""
+    from test_golden_cpu import load_c1, load_c2
+    img, g = load_c1()
+    k, d = amd.ORBextractor(1000)(img)
+    assert k.tobytes() == g["kps"].tobytes() and np.array_equal(d, g["desc"])
+    L, R, g2 = load_c2()
+    exL, exR = amd.ORBextractor(2000), amd.ORBextractor(2000)
+    kL, dL = exL(L)
+    kR, _ = exR(R)
+    assert kL.tobytes() == g2["kps_left"].tobytes() and np.array_equal(dL, g2["desc_left"])
+    assert kR.tobytes() == g2["kps_right"].tobytes()
+    bf, fx, mb = g2["camera"]
+    u, dep = amd.compute_stereo_matches(exL, exR, len(kL), float(bf), float(mb))
+    assert u.tobytes() == g2["u_right"].tobytes() and dep.tobytes() == g2["depth"].tobytes()
