@@ -23,9 +23,9 @@ for s in $STEPS; do
       rc=$?; echo "bench rc=$rc" | tee -a $OUT/session.log; cat $OUT/bench.json; tail -3 $OUT/bench.err; [ $rc -eq 0 ] || exit $rc ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err"
       rc=$?; cd "$GRAFT_REPO_ROOT"; echo "prof rc=$rc" | tee -a $OUT/session.log; [ $rc -eq 0 ] || exit $rc
-      find $OUT/prof -name "*stats*" | head ;;
+      find $OUT/prof -name "*stats*" ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp
       for ctr in FETCH_SIZE WRITE_SIZE; do

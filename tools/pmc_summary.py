@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs into profiles/pmc_traffic.json.
+
+HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, following
+MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE (KB) reports half the bytes of wide coalesced
+reads (double it); WRITE_SIZE reads exact for streaming stores. Narrow/gather access widths
+are uncalibrated there, so the figure is an estimate; ratios between variants are exact.
+Usage: pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <batch> <out.json>
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def short(name: str) -> str:
+    base = name.split("(")[0]
+    return base.split("::")[-1]
+
+
+def load(d: Path, counter: str):
+    acc = defaultdict(list)
+    for f in d.rglob("*counter_collection.csv"):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] == counter:
+                    acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+    return acc
+
+
+def main():
+    fdir, wdir, batch, out = Path(sys.argv[1]), Path(sys.argv[2]), int(sys.argv[3]), Path(sys.argv[4])
+    fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        fv, wv = fetch.get(k, []), write.get(k, [])
+        f_avg = sum(fv) / len(fv) if fv else 0.0
+        w_avg = sum(wv) / len(wv) if wv else 0.0
+        res[k] = {"launches": max(len(fv), len(wv)), "FETCH_SIZE_KB": round(f_avg, 3),
+                  "WRITE_SIZE_KB": round(w_avg, 3),
+                  "hbm_bytes_per_launch": int((2 * f_avg + w_avg) * 1024)}
+    doc = {"batch": batch, "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE read correction)",
+           "kernels": res}
+    out.write_text(json.dumps(doc, indent=1))
+    print(json.dumps(doc, indent=1))
+
+
+if __name__ == "__main__":
+    main()
