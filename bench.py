@@ -63,6 +63,43 @@ def cpu_baseline(pool, n_frames: int):
                       f"oracle extract L+R + ComputeStereoMatches, single thread, {dt:.1f} s"}
 
 
+def bench_localba(amd, args, dist, world, with_cpu):
+    """C4: LocalBundleAdjustment on the synthetic 20 KF x 3000 MP graph; one LocalBA call per
+    inserted keyframe (LocalMapping.cc:116-118) -> keyframes/s = calls/s, summed over ranks."""
+    from orbslam2_amd import synth
+    prob = synth.localba_problem(seed=4)
+    lba = amd.LocalBundleAdjustment()
+    for _ in range(2):
+        r = lba.solve(prob)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.lba_steps):
+        r = lba.solve(prob)
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    res = {"localba_kf_per_s": round(world * args.lba_steps / dt, 3),
+           "localba": {"ms_per_call": round(1000 * dt / args.lba_steps, 3), "edges": int(len(prob["edge_point"])),
+                       "keyframes": 20, "map_points": 3000, "lm_iterations": list(r["iterations"]),
+                       "dtype": "f64", "host_loop": "LM accept/reject on host, 1 readback per trial"}}
+    if with_cpu:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 5.0:
+            oracle.lba_solve(prob)
+            n += 1
+        cdt = time.perf_counter() - t0
+        res["localba"]["cpu_baseline"] = {"value": round(n / cdt, 3), "unit": "keyframes/s", "cores": 1,
+                                          "kind": "port", "sample": f"{n} LocalBA calls on the C4 graph, {cdt:.1f} s"}
+    return res
+
+
 def load_traffic(kernel: str, batch: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
     f = ROOT / "profiles" / "pmc_traffic.json"
@@ -89,6 +126,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=96)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--lba-steps", type=int, default=10, help="timed LocalBA calls (C4 graph)")
+    ap.add_argument("--no-lba", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -190,7 +229,6 @@ def main():
             "keypoints_img0": int(len(k0)),
             "stereo_matches_img0": n_match,
         },
-        "localba_kf_per_s": None,
     }
     if prof:
         name, (tot, n) = max(prof.items(), key=lambda kv: kv[1][0])
@@ -202,6 +240,8 @@ def main():
                            "traffic": traffic, "avg_launch_ms": round(tot / n, 4),
                            "algorithmic_bytes_per_launch": BYTES_PER_STEREO_FRAME * B}
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
+    if not args.no_lba:
+        out.update(bench_localba(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pool, args.cpu_frames)
     if rank == 0:

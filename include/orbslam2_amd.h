@@ -110,6 +110,52 @@ int orbm_stereo_fetch(orbx_engine *e, int pair, float *u_right, float *depth, in
 int orbm_hamming_best2(const uint8_t *q, int nq, const uint8_t *db, int ndb, int *best_idx,
                        int *best_d, int *second_d);
 
+/* -------- local bundle adjustment (replaces Optimizer::LocalBundleAdjustment) -------- */
+
+/* The graph Optimizer::LocalBundleAdjustment (Optimizer.cc:646-898) builds from the map,
+ * flattened by the caller's graph walk (local KFs, fixed KFs, local map points and their
+ * observations). Poses cross the boundary as cv::Mat CV_32F Tcw, points as CV_32F Xw
+ * (Converter::toSE3Quat / toVector3d, Converter.cc:63-139). Edges are in g2o insertion
+ * order: local map points in list order, each point's observations in map order
+ * (Optimizer.cc:806-898). edge_obs = (u, v, uR) of the undistorted keypoint; uR < 0 ->
+ * monocular EdgeSE3ProjectXYZ, else EdgeStereoSE3ProjectXYZ. */
+typedef struct {
+    int32_t n_poses;
+    const int32_t *pose_id;      /* vertex id (KeyFrame::mnId) */
+    const uint8_t *pose_fixed;   /* mnId == 0 or a fixed (non-local) camera */
+    const float *pose_Tcw;       /* [n_poses][16] row-major 4x4 */
+    const float *pose_cam;       /* [n_poses][5] fx, fy, cx, cy, bf (KeyFrame members) */
+    int32_t n_points;
+    const int32_t *point_id;     /* vertex id = MapPoint::mnId + maxKFid + 1 */
+    const float *point_Xw;       /* [n_points][3] */
+    int32_t n_edges;
+    const int32_t *edge_point;   /* index into points */
+    const int32_t *edge_pose;    /* index into poses */
+    const float *edge_obs;       /* [n_edges][3] */
+    const float *edge_inv_sigma2;/* mvInvLevelSigma2[octave] */
+} lba_problem;
+
+typedef struct {
+    float *pose_Tcw;             /* [n_poses][16] out: SetPose(Converter::toCvMat(...)) */
+    float *point_Xw;             /* [n_points][3] out: SetWorldPos */
+    uint8_t *edge_erase;         /* [n_edges] out: 1 = pair in vToErase (Optimizer.cc:977-1008) */
+    int32_t iterations[2];       /* LM iterations run in optimize(5) / optimize(10) */
+    double chi2[2];              /* active robust chi2 after each phase */
+    int32_t stopped;             /* 1 = *stop was set (early return / phase 2 skipped) */
+} lba_result;
+
+typedef struct lba_engine lba_engine;
+
+/* Optimizer::LocalBundleAdjustment(KeyFrame*, bool* pbStopFlag, Map*) (Optimizer.h:112,
+ * Optimizer.cc:646-1049) minus the map walk / write-back, which stay in the caller's
+ * adapter: two Levenberg-Marquardt runs (5 iterations with Huber kernels, then 10 without
+ * the outliers, optimization_algorithm_levenberg.cpp:61-164) with the Schur complement onto
+ * the poses (block_solver.hpp:354-486) on the GPU. `stop` mirrors pbStopFlag: polled
+ * before each LM iteration and trial (sparse_optimizer.cpp:376, levenberg.cpp:149). */
+int lba_create(lba_engine **out);
+void lba_destroy(lba_engine *e);
+int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile int32_t *stop);
+
 /* -------- library / measurement -------- */
 const char *orbslam2_amd_version(void);
 int orbslam2_amd_device_count(void);

@@ -1,0 +1,657 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * Double-precision CPU restatement of Optimizer::LocalBundleAdjustment's optimisation
+ * (Optimizer.cc:900-1008) over the vendored g2o subset it uses:
+ *   SparseOptimizer::optimize / initializeOptimization / computeActiveErrors /
+ *     activeRobustChi2 / update / push / pop   (sparse_optimizer.cpp:61-114,206-267,354-435)
+ *   OptimizationAlgorithmLevenberg::solve / computeLambdaInit / computeScale
+ *                                            (optimization_algorithm_levenberg.cpp:61-189)
+ *   BlockSolver<6,3>::buildSystem / setLambda / restoreDiagonal / solve (Schur)
+ *                                            (block_solver.hpp:354-604)
+ *   BaseBinaryEdge::constructQuadraticForm   (base_binary_edge.hpp:55-120)
+ *   RobustKernelHuber::robustify             (robust_kernel_impl.cpp:78-90)
+ *   EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ computeError / linearizeOplus /
+ *     isDepthPositive                        (types_six_dof_expmap.{h,cpp}:80-234)
+ *   SE3Quat exp / map / operator* / normalizeRotation (se3quat.h:60-285)
+ *   Converter::toSE3Quat / toCvMat           (Converter.cc:63-139)
+ * Eigen pieces restated: Quaternion(Matrix3) trace-branch construction, normalize,
+ * _transformVector, toRotationMatrix, the 3x3 cofactor inverse. The sparse LDLT+AMD of
+ * LinearSolverEigen is replaced by a dense Cholesky of the Schur matrix (the
+ * ordering only changes rounding; the LocalBA tolerance is 1e-4 relative).
+ * Parity unpinned: Eigen/g2o cannot be built in this image.
+ */
+#define _GNU_SOURCE
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "lba_oracle.h"
+
+typedef struct { double x, y, z, w; } quat;
+typedef struct { quat r; double t[3]; } se3;
+
+/* Eigen::Quaternion(const Matrix3&) */
+static quat quat_from_R(const double m[9]) {
+#define M(i, j) m[3 * (i) + (j)]
+    quat q;
+    double c[3];
+    double t = M(0, 0) + M(1, 1) + M(2, 2);
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (M(2, 1) - M(1, 2)) * t;
+        q.y = (M(0, 2) - M(2, 0)) * t;
+        q.z = (M(1, 0) - M(0, 1)) * t;
+    } else {
+        int i = 0;
+        if (M(1, 1) > M(0, 0)) i = 1;
+        if (M(2, 2) > M(i, i)) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(M(i, i) - M(j, j) - M(k, k) + 1.0);
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        q.w = (M(k, j) - M(j, k)) * t;
+        c[j] = (M(j, i) + M(i, j)) * t;
+        c[k] = (M(k, i) + M(i, k)) * t;
+        q.x = c[0]; q.y = c[1]; q.z = c[2];
+    }
+#undef M
+    return q;
+}
+
+/* SE3Quat::normalizeRotation (se3quat.h:280-285) */
+static void quat_normalize_g2o(quat *q) {
+    if (q->w < 0) { q->x = -q->x; q->y = -q->y; q->z = -q->z; q->w = -q->w; }
+    const double n = sqrt(q->x * q->x + q->y * q->y + q->z * q->z + q->w * q->w);
+    q->x /= n; q->y /= n; q->z /= n; q->w /= n;
+}
+
+static quat quat_mul(quat a, quat b) {
+    quat r;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+    return r;
+}
+
+/* Quaternion::_transformVector */
+static void quat_rotate(quat q, const double v[3], double out[3]) {
+    double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    const double cx = q.y * uv[2] - q.z * uv[1], cy = q.z * uv[0] - q.x * uv[2], cz = q.x * uv[1] - q.y * uv[0];
+    out[0] = v[0] + q.w * uv[0] + cx;
+    out[1] = v[1] + q.w * uv[1] + cy;
+    out[2] = v[2] + q.w * uv[2] + cz;
+}
+
+static void quat_to_R(quat q, double R[9]) {
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+    R[3] = txy + twz; R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
+}
+
+static void se3_map(const se3 *T, const double X[3], double out[3]) {
+    quat_rotate(T->r, X, out);
+    out[0] += T->t[0]; out[1] += T->t[1]; out[2] += T->t[2];
+}
+
+/* SE3Quat::exp (se3quat.h:223-257) */
+static se3 se3_exp(const double u[6]) {
+    const double w0 = u[0], w1 = u[1], w2 = u[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double O2[9], R[9], V[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += O[3 * i + k] * O[3 * k + j];
+            O2[3 * i + j] = s;
+        }
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
+        memcpy(V, R, sizeof(R));
+    } else {
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+        const double c = (theta - sin(theta)) / pow(theta, 3);
+        for (int i = 0; i < 9; i++) {
+            const double I = i % 4 == 0 ? 1.0 : 0.0;
+            R[i] = I + a * O[i] + b * O2[i];
+            V[i] = I + b * O[i] + c * O2[i];
+        }
+    }
+    se3 T;
+    T.r = quat_from_R(R);
+    for (int i = 0; i < 3; i++) T.t[i] = V[3 * i] * u[3] + V[3 * i + 1] * u[4] + V[3 * i + 2] * u[5];
+    quat_normalize_g2o(&T.r);
+    return T;
+}
+
+/* SE3Quat::operator* */
+static se3 se3_mul(const se3 *a, const se3 *b) {
+    se3 r;
+    double rt[3];
+    quat_rotate(a->r, b->t, rt);
+    r.t[0] = a->t[0] + rt[0]; r.t[1] = a->t[1] + rt[1]; r.t[2] = a->t[2] + rt[2];
+    r.r = quat_mul(a->r, b->r);
+    quat_normalize_g2o(&r.r);
+    return r;
+}
+
+/* Eigen 3x3 inverse (cofactors / determinant) */
+static void inv3(const double m[9], double o[9]) {
+    const double c00 = m[4] * m[8] - m[5] * m[7];
+    const double c10 = m[5] * m[6] - m[3] * m[8];
+    const double c20 = m[3] * m[7] - m[4] * m[6];
+    const double det = m[0] * c00 + m[1] * c10 + m[2] * c20;
+    const double id = 1.0 / det;
+    o[0] = c00 * id; o[1] = (m[2] * m[7] - m[1] * m[8]) * id; o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+    o[3] = c10 * id; o[4] = (m[0] * m[8] - m[2] * m[6]) * id; o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    o[6] = c20 * id; o[7] = (m[1] * m[6] - m[0] * m[7]) * id; o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+typedef struct {
+    int pose, point, stereo, level, robust, active;
+    double obs[3], info, delta, dsqr;
+    double fx, fy, cx, cy, bf;
+    double err[3];   /* _error: recomputed by computeActiveErrors only (stale after pop) */
+    int dim;
+} edge_t;
+
+typedef struct {
+    int np, nq, ne;
+    se3 *T;
+    double (*X)[3];
+    const uint8_t *fixed;
+    const int32_t *pose_id, *point_id;
+    edge_t *E;
+    /* active structure */
+    int P, Lm;            /* free active poses / active points */
+    int *pose_hidx, *point_hidx; /* -1 if not in index mapping */
+    int *hpose, *hpoint;  /* hessian index -> vertex */
+    const volatile int32_t *stop;
+} graph_t;
+
+static int terminate_flag(const graph_t *g) { return g->stop ? (*g->stop != 0) : 0; }
+
+/* EdgeSE3ProjectXYZ::computeError / EdgeStereoSE3ProjectXYZ::computeError */
+static void edge_error(const graph_t *g, edge_t *e) {
+    double p[3];
+    se3_map(&g->T[e->pose], g->X[e->point], p);
+    if (!e->stereo) {
+        const double u = p[0] / p[2], v = p[1] / p[2];
+        e->err[0] = e->obs[0] - (u * e->fx + e->cx);
+        e->err[1] = e->obs[1] - (v * e->fy + e->cy);
+        e->err[2] = 0;
+    } else {
+        const float invz = (float)(1.0f / p[2]);
+        const float bff = (float)e->bf;
+        const double r0 = p[0] * invz * e->fx + e->cx;
+        const double r1 = p[1] * invz * e->fy + e->cy;
+        const double r2 = r0 - (double)(bff * invz);
+        e->err[0] = e->obs[0] - r0;
+        e->err[1] = e->obs[1] - r1;
+        e->err[2] = e->obs[2] - r2;
+    }
+}
+
+static double edge_chi2(const edge_t *e) {
+    double s = e->err[0] * e->info * e->err[0] + e->err[1] * e->info * e->err[1];
+    if (e->stereo) s += e->err[2] * e->info * e->err[2];
+    return s;
+}
+
+static void huber(const edge_t *e, double chi, double rho[2]) {
+    if (chi <= e->dsqr) { rho[0] = chi; rho[1] = 1.0; }
+    else { const double s = sqrt(chi); rho[0] = 2 * s * e->delta - e->dsqr; rho[1] = e->delta / s; }
+}
+
+static double active_robust_chi2(const graph_t *g) {
+    double chi = 0;
+    for (int k = 0; k < g->ne; k++) {
+        const edge_t *e = &g->E[k];
+        if (!e->active) continue;
+        const double c = edge_chi2(e);
+        if (e->robust) { double rho[2]; huber(e, c, rho); chi += rho[0]; }
+        else chi += c;
+    }
+    return chi;
+}
+
+static void compute_active_errors(const graph_t *g) {
+    for (int k = 0; k < g->ne; k++)
+        if (g->E[k].active) edge_error(g, &g->E[k]);
+}
+
+/* linearizeOplus: Jp = d err / d point (dim x 3), Jt = d err / d pose (dim x 6) */
+static void edge_jacobians(const graph_t *g, const edge_t *e, double Jp[9], double Jt[18]) {
+    double p[3], R[9];
+    const se3 *T = &g->T[e->pose];
+    se3_map(T, g->X[e->point], p);
+    quat_to_R(T->r, R);
+    const double x = p[0], y = p[1], z = p[2], z2 = z * z, fx = e->fx, fy = e->fy, bf = e->bf;
+    if (!e->stereo) {
+        const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++) {
+                double s = 0;
+                for (int k = 0; k < 3; k++) s += (-1. / z * tmp[3 * i + k]) * R[3 * k + j];
+                Jp[3 * i + j] = s;
+            }
+    } else {
+        for (int j = 0; j < 3; j++) {
+            Jp[j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
+            Jp[3 + j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
+            Jp[6 + j] = Jp[j] - bf * R[6 + j] / z2;
+        }
+    }
+    Jt[0] = x * y / z2 * fx; Jt[1] = -(1 + (x * x / z2)) * fx; Jt[2] = y / z * fx;
+    Jt[3] = -1. / z * fx; Jt[4] = 0; Jt[5] = x / z2 * fx;
+    Jt[6] = (1 + y * y / z2) * fy; Jt[7] = -x * y / z2 * fy; Jt[8] = -x / z * fy;
+    Jt[9] = 0; Jt[10] = -1. / z * fy; Jt[11] = y / z2 * fy;
+    if (e->stereo) {
+        Jt[12] = Jt[0] - bf * y / z2; Jt[13] = Jt[1] + bf * x / z2; Jt[14] = Jt[2];
+        Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf / z2;
+    }
+}
+
+/* system storage (Hessian index space) */
+typedef struct {
+    int P, Lm, nx;
+    double *Hpp;    /* P*6 x P*6 dense (block diagonal here: no pose-pose edges) */
+    double *Hll;    /* Lm x 9 */
+    double *Hpl;    /* per active edge with free pose: 18 (6x3), indexed by edge */
+    double *b;      /* nx = 6P + 3Lm */
+    double *x;
+    double *diag_backup_p, *diag_backup_l;
+} sys_t;
+
+static void build_system(graph_t *g, sys_t *S) {
+    const int n6 = 6 * S->P;
+    memset(S->Hpp, 0, sizeof(double) * n6 * n6);
+    memset(S->Hll, 0, sizeof(double) * 9 * S->Lm);
+    memset(S->b, 0, sizeof(double) * S->nx);
+    for (int k = 0; k < g->ne; k++) {
+        edge_t *e = &g->E[k];
+        if (!e->active) continue;
+        double Jp[9], Jt[18];
+        edge_jacobians(g, e, Jp, Jt);
+        const int D = e->dim;
+        double w = e->info, r1 = 1.0;
+        if (e->robust) { double rho[2]; huber(e, edge_chi2(e), rho); r1 = rho[1]; }
+        const double wW = r1 * w;              /* weighted information (diagonal) */
+        double omr[3];
+        for (int i = 0; i < D; i++) omr[i] = -(w * e->err[i]) * r1;
+        const int li = g->point_hidx[e->point];
+        const int pi = g->pose_hidx[e->pose];
+        double *bl = S->b + n6 + 3 * li;
+        double *Hl = S->Hll + 9 * li;
+        for (int a = 0; a < 3; a++) {
+            double s = 0;
+            for (int i = 0; i < D; i++) s += Jp[3 * i + a] * omr[i];
+            bl[a] += s;
+            for (int c = 0; c < 3; c++) {
+                double h = 0;
+                for (int i = 0; i < D; i++) h += Jp[3 * i + a] * wW * Jp[3 * i + c];
+                Hl[3 * a + c] += h;
+            }
+        }
+        if (pi >= 0) {
+            double *hpl = S->Hpl + 18 * k;
+            for (int a = 0; a < 6; a++)
+                for (int c = 0; c < 3; c++) {
+                    double h = 0;
+                    for (int i = 0; i < D; i++) h += Jt[6 * i + a] * wW * Jp[3 * i + c];
+                    hpl[3 * a + c] = h;
+                }
+            double *bp = S->b + 6 * pi;
+            for (int a = 0; a < 6; a++) {
+                double s = 0;
+                for (int i = 0; i < D; i++) s += Jt[6 * i + a] * omr[i];
+                bp[a] += s;
+                for (int c = 0; c < 6; c++) {
+                    double h = 0;
+                    for (int i = 0; i < D; i++) h += Jt[6 * i + a] * wW * Jt[6 * i + c];
+                    S->Hpp[(size_t)(6 * pi + a) * n6 + 6 * pi + c] += h;
+                }
+            }
+        }
+    }
+}
+
+static double lambda_init(const sys_t *S) {
+    double m = 0;
+    const int n6 = 6 * S->P;
+    for (int i = 0; i < n6; i++) m = fmax(fabs(S->Hpp[(size_t)i * n6 + i]), m);
+    for (int l = 0; l < S->Lm; l++)
+        for (int j = 0; j < 3; j++) m = fmax(fabs(S->Hll[9 * l + 4 * j]), m);
+    return 1e-5 * m;
+}
+
+static void set_lambda(sys_t *S, double lambda) {
+    const int n6 = 6 * S->P;
+    for (int i = 0; i < n6; i++) { S->diag_backup_p[i] = S->Hpp[(size_t)i * n6 + i]; S->Hpp[(size_t)i * n6 + i] += lambda; }
+    for (int l = 0; l < S->Lm; l++)
+        for (int j = 0; j < 3; j++) { S->diag_backup_l[3 * l + j] = S->Hll[9 * l + 4 * j]; S->Hll[9 * l + 4 * j] += lambda; }
+}
+
+static void restore_diagonal(sys_t *S) {
+    const int n6 = 6 * S->P;
+    for (int i = 0; i < n6; i++) S->Hpp[(size_t)i * n6 + i] = S->diag_backup_p[i];
+    for (int l = 0; l < S->Lm; l++)
+        for (int j = 0; j < 3; j++) S->Hll[9 * l + 4 * j] = S->diag_backup_l[3 * l + j];
+}
+
+/* BlockSolver::solve with the Schur complement; dense Cholesky on Hschur */
+static int schur_solve(const graph_t *g, sys_t *S) {
+    const int n6 = 6 * S->P;
+    double *Hs = (double *)malloc(sizeof(double) * (n6 * n6 + 1));
+    double *coef = (double *)calloc(n6 + 1, sizeof(double));
+    double *Dinv = (double *)malloc(sizeof(double) * 9 * (S->Lm + 1));
+    memcpy(Hs, S->Hpp, sizeof(double) * n6 * n6);
+    /* landmark columns: edges of each active point with a free pose */
+    int *cnt = (int *)calloc(S->Lm + 1, sizeof(int));
+    for (int k = 0; k < g->ne; k++) {
+        const edge_t *e = &g->E[k];
+        if (e->active && g->pose_hidx[e->pose] >= 0) cnt[g->point_hidx[e->point] + 1]++;
+    }
+    for (int l = 0; l < S->Lm; l++) cnt[l + 1] += cnt[l];
+    int *col = (int *)malloc(sizeof(int) * (cnt[S->Lm] + 1));
+    int *fill = (int *)calloc(S->Lm + 1, sizeof(int));
+    for (int k = 0; k < g->ne; k++) {
+        const edge_t *e = &g->E[k];
+        if (e->active && g->pose_hidx[e->pose] >= 0) {
+            const int l = g->point_hidx[e->point];
+            col[cnt[l] + fill[l]++] = k;
+        }
+    }
+    for (int l = 0; l < S->Lm; l++) {
+        double *Di = Dinv + 9 * l;
+        inv3(S->Hll + 9 * l, Di);
+        const double *bl = S->b + n6 + 3 * l;
+        double db[3];
+        for (int a = 0; a < 3; a++) db[a] = Di[3 * a] * bl[0] + Di[3 * a + 1] * bl[1] + Di[3 * a + 2] * bl[2];
+        for (int u = cnt[l]; u < cnt[l + 1]; u++) {
+            const int k1 = col[u];
+            const int i1 = g->pose_hidx[g->E[k1].pose];
+            const double *B1 = S->Hpl + 18 * k1;
+            double BD[18];
+            for (int a = 0; a < 6; a++)
+                for (int c = 0; c < 3; c++)
+                    BD[3 * a + c] = B1[3 * a] * Di[c] + B1[3 * a + 1] * Di[3 + c] + B1[3 * a + 2] * Di[6 + c];
+            for (int a = 0; a < 6; a++) coef[6 * i1 + a] += B1[3 * a] * db[0] + B1[3 * a + 1] * db[1] + B1[3 * a + 2] * db[2];
+            for (int v = cnt[l]; v < cnt[l + 1]; v++) {
+                const int k2 = col[v];
+                const int i2 = g->pose_hidx[g->E[k2].pose];
+                if (i2 < i1) continue;
+                const double *B2 = S->Hpl + 18 * k2;
+                for (int a = 0; a < 6; a++)
+                    for (int c = 0; c < 6; c++) {
+                        const double h = BD[3 * a] * B2[3 * c] + BD[3 * a + 1] * B2[3 * c + 1] + BD[3 * a + 2] * B2[3 * c + 2];
+                        Hs[(size_t)(6 * i1 + a) * n6 + 6 * i2 + c] -= h;
+                        if (i2 != i1) Hs[(size_t)(6 * i2 + c) * n6 + 6 * i1 + a] -= h;
+                    }
+            }
+        }
+    }
+    double *bs = (double *)malloc(sizeof(double) * (n6 + 1));
+    for (int i = 0; i < n6; i++) bs[i] = S->b[i] - coef[i];
+    /* dense Cholesky Hs = L L^T */
+    int ok = 1;
+    for (int j = 0; j < n6 && ok; j++) {
+        double d = Hs[(size_t)j * n6 + j];
+        for (int k = 0; k < j; k++) d -= Hs[(size_t)j * n6 + k] * Hs[(size_t)j * n6 + k];
+        if (!(d > 0)) { ok = 0; break; }
+        const double ljj = sqrt(d);
+        Hs[(size_t)j * n6 + j] = ljj;
+        for (int i = j + 1; i < n6; i++) {
+            double s = Hs[(size_t)i * n6 + j];
+            for (int k = 0; k < j; k++) s -= Hs[(size_t)i * n6 + k] * Hs[(size_t)j * n6 + k];
+            Hs[(size_t)i * n6 + j] = s / ljj;
+        }
+    }
+    if (ok) {
+        double *xp = S->x;
+        for (int i = 0; i < n6; i++) {
+            double s = bs[i];
+            for (int k = 0; k < i; k++) s -= Hs[(size_t)i * n6 + k] * xp[k];
+            xp[i] = s / Hs[(size_t)i * n6 + i];
+        }
+        for (int i = n6 - 1; i >= 0; i--) {
+            double s = xp[i];
+            for (int k = i + 1; k < n6; k++) s -= Hs[(size_t)k * n6 + i] * xp[k];
+            xp[i] = s / Hs[(size_t)i * n6 + i];
+        }
+        /* landmarks: x_l = Dinv (b_l - Hpl^T x_p) */
+        for (int l = 0; l < S->Lm; l++) {
+            double c[3];
+            const double *bl = S->b + n6 + 3 * l;
+            c[0] = bl[0]; c[1] = bl[1]; c[2] = bl[2];
+            for (int u = cnt[l]; u < cnt[l + 1]; u++) {
+                const int k = col[u];
+                const int i1 = g->pose_hidx[g->E[k].pose];
+                const double *B = S->Hpl + 18 * k;
+                for (int cc = 0; cc < 3; cc++) {
+                    double s = 0;
+                    for (int a = 0; a < 6; a++) s += B[3 * a + cc] * (-xp[6 * i1 + a]);
+                    c[cc] += s;
+                }
+            }
+            const double *Di = Dinv + 9 * l;
+            double *xl = S->x + n6 + 3 * l;
+            for (int a = 0; a < 3; a++) xl[a] = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
+        }
+    }
+    free(Hs); free(coef); free(Dinv); free(cnt); free(col); free(fill); free(bs);
+    return ok;
+}
+
+static void apply_update(graph_t *g, const sys_t *S) {
+    for (int i = 0; i < S->P; i++) {
+        const int v = g->hpose[i];
+        se3 d = se3_exp(S->x + 6 * i);
+        g->T[v] = se3_mul(&d, &g->T[v]);
+    }
+    for (int l = 0; l < S->Lm; l++) {
+        const int v = g->hpoint[l];
+        const double *dx = S->x + 6 * S->P + 3 * l;
+        g->X[v][0] += dx[0]; g->X[v][1] += dx[1]; g->X[v][2] += dx[2];
+    }
+}
+
+static int cmp_int_by_key(const void *a, const void *b, void *key) {
+    const int32_t *k = (const int32_t *)key;
+    const int x = *(const int *)a, y = *(const int *)b;
+    return k[x] < k[y] ? -1 : (k[x] > k[y] ? 1 : 0);
+}
+
+/* SparseOptimizer::initializeOptimization(level) + buildIndexMapping */
+static void initialize(graph_t *g, int level) {
+    int *pa = (int *)calloc(g->np, sizeof(int)), *qa = (int *)calloc(g->nq, sizeof(int));
+    for (int k = 0; k < g->ne; k++) {
+        edge_t *e = &g->E[k];
+        e->active = (level < 0 || e->level == level);
+        if (e->active) { pa[e->pose] = 1; qa[e->point] = 1; }
+    }
+    int P = 0, Lm = 0;
+    for (int i = 0; i < g->np; i++) if (pa[i] && !g->fixed[i]) g->hpose[P++] = i;
+    for (int i = 0; i < g->nq; i++) if (qa[i]) g->hpoint[Lm++] = i;
+    qsort_r(g->hpose, P, sizeof(int), cmp_int_by_key, (void *)g->pose_id);
+    qsort_r(g->hpoint, Lm, sizeof(int), cmp_int_by_key, (void *)g->point_id);
+    for (int i = 0; i < g->np; i++) g->pose_hidx[i] = -1;
+    for (int i = 0; i < g->nq; i++) g->point_hidx[i] = -1;
+    for (int i = 0; i < P; i++) g->pose_hidx[g->hpose[i]] = i;
+    for (int i = 0; i < Lm; i++) g->point_hidx[g->hpoint[i]] = i;
+    g->P = P; g->Lm = Lm;
+    free(pa); free(qa);
+}
+
+/* SparseOptimizer::optimize(iterations) with OptimizationAlgorithmLevenberg */
+static int optimize(graph_t *g, int iterations, double *final_chi) {
+    if (g->P + g->Lm == 0) return -1;
+    sys_t S;
+    S.P = g->P; S.Lm = g->Lm; S.nx = 6 * g->P + 3 * g->Lm;
+    const int n6 = 6 * S.P;
+    S.Hpp = (double *)calloc((size_t)n6 * n6 + 1, sizeof(double));
+    S.Hll = (double *)calloc(9 * (size_t)S.Lm + 1, sizeof(double));
+    S.Hpl = (double *)calloc(18 * (size_t)g->ne + 1, sizeof(double));
+    S.b = (double *)calloc(S.nx + 1, sizeof(double));
+    S.x = (double *)calloc(S.nx + 1, sizeof(double));
+    S.diag_backup_p = (double *)calloc(n6 + 1, sizeof(double));
+    S.diag_backup_l = (double *)calloc(3 * (size_t)S.Lm + 1, sizeof(double));
+    se3 *saveT = (se3 *)malloc(sizeof(se3) * (g->np + 1));
+    double (*saveX)[3] = (double (*)[3])malloc(sizeof(double) * 3 * (g->nq + 1));
+    double lambda = 0, ni = 2;
+    int nBad = 0, it = 0;
+    for (int i = 0; i < iterations && !terminate_flag(g); i++) {
+        compute_active_errors(g);
+        double currentChi = active_robust_chi2(g), iniChi = currentChi, tempChi;
+        build_system(g, &S);
+        if (i == 0) { lambda = lambda_init(&S); ni = 2; nBad = 0; }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            memcpy(saveT, g->T, sizeof(se3) * g->np);               /* push */
+            memcpy(saveX, g->X, sizeof(double) * 3 * g->nq);
+            set_lambda(&S, lambda);
+            const int ok2 = schur_solve(g, &S);
+            apply_update(g, &S);
+            restore_diagonal(&S);
+            compute_active_errors(g);
+            tempChi = active_robust_chi2(g);
+            if (!ok2) tempChi = DBL_MAX;
+            rho = currentChi - tempChi;
+            double scale = 0;
+            for (int j = 0; j < S.nx; j++) scale += S.x[j] * (lambda * S.x[j] + S.b[j]);
+            scale += 1e-3;
+            rho /= scale;
+            if (rho > 0 && isfinite(tempChi)) {
+                double alpha = 1. - pow((2 * rho - 1), 3);
+                alpha = fmin(alpha, 2. / 3.);
+                const double sf = fmax(1. / 3., alpha);
+                lambda *= sf;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                memcpy(g->T, saveT, sizeof(se3) * g->np);            /* pop */
+                memcpy(g->X, saveX, sizeof(double) * 3 * g->nq);
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10 && !terminate_flag(g));
+        it++;
+        *final_chi = currentChi;
+        int result_ok = 1;
+        if (qmax == 10 || rho == 0) result_ok = 0;
+        else {
+            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++; else nBad = 0;
+            if (nBad >= 3) result_ok = 0;
+        }
+        if (!result_ok) break;
+    }
+    free(S.Hpp); free(S.Hll); free(S.Hpl); free(S.b); free(S.x); free(S.diag_backup_p); free(S.diag_backup_l);
+    free(saveT); free(saveX);
+    return it;
+}
+
+static int depth_positive(const graph_t *g, const edge_t *e) {
+    double p[3];
+    se3_map(&g->T[e->pose], g->X[e->point], p);
+    return p[2] > 0.0;
+}
+
+int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile int32_t *stop) {
+    graph_t g;
+    memset(&g, 0, sizeof(g));
+    g.np = pr->n_poses; g.nq = pr->n_points; g.ne = pr->n_edges;
+    g.fixed = pr->pose_fixed; g.pose_id = pr->pose_id; g.point_id = pr->point_id;
+    g.stop = stop;
+    g.T = (se3 *)malloc(sizeof(se3) * (g.np + 1));
+    g.X = (double (*)[3])malloc(sizeof(double) * 3 * (g.nq + 1));
+    g.E = (edge_t *)calloc(g.ne + 1, sizeof(edge_t));
+    g.pose_hidx = (int *)malloc(sizeof(int) * (g.np + 1));
+    g.point_hidx = (int *)malloc(sizeof(int) * (g.nq + 1));
+    g.hpose = (int *)malloc(sizeof(int) * (g.np + 1));
+    g.hpoint = (int *)malloc(sizeof(int) * (g.nq + 1));
+    for (int i = 0; i < g.np; i++) {     /* Converter::toSE3Quat */
+        const float *m = pr->pose_Tcw + 16 * i;
+        const double R[9] = {m[0], m[1], m[2], m[4], m[5], m[6], m[8], m[9], m[10]};
+        g.T[i].r = quat_from_R(R);
+        g.T[i].t[0] = m[3]; g.T[i].t[1] = m[7]; g.T[i].t[2] = m[11];
+        quat_normalize_g2o(&g.T[i].r);
+    }
+    for (int i = 0; i < g.nq; i++)
+        for (int j = 0; j < 3; j++) g.X[i][j] = pr->point_Xw[3 * i + j];
+    const float thMono = (float)sqrt(5.991), thStereo = (float)sqrt(7.815);
+    for (int k = 0; k < g.ne; k++) {
+        edge_t *e = &g.E[k];
+        e->point = pr->edge_point[k];
+        e->pose = pr->edge_pose[k];
+        const float *ob = pr->edge_obs + 3 * k;
+        e->stereo = ob[2] >= 0;
+        e->dim = e->stereo ? 3 : 2;
+        e->obs[0] = ob[0]; e->obs[1] = ob[1]; e->obs[2] = e->stereo ? ob[2] : 0;
+        e->info = pr->edge_inv_sigma2[k];
+        e->robust = 1;
+        e->delta = e->stereo ? thStereo : thMono;
+        e->dsqr = e->delta * e->delta;
+        const float *cam = pr->pose_cam + 5 * e->pose;
+        e->fx = cam[0]; e->fy = cam[1]; e->cx = cam[2]; e->cy = cam[3]; e->bf = cam[4];
+        e->level = 0;
+    }
+    res->iterations[0] = res->iterations[1] = 0;
+    res->chi2[0] = res->chi2[1] = 0;
+    res->stopped = 0;
+    int rc = 0;
+    if (stop && *stop) {                  /* Optimizer.cc:902-904: return before optimising */
+        res->stopped = 1;
+        memcpy(res->pose_Tcw, pr->pose_Tcw, sizeof(float) * 16 * g.np);
+        memcpy(res->point_Xw, pr->point_Xw, sizeof(float) * 3 * g.nq);
+        memset(res->edge_erase, 0, g.ne);
+        free(g.T); free(g.X); free(g.E); free(g.pose_hidx); free(g.point_hidx); free(g.hpose); free(g.hpoint);
+        return rc;
+    } else {
+        initialize(&g, 0);
+        res->iterations[0] = optimize(&g, 5, &res->chi2[0]);
+        int bDoMore = !(stop && *stop);
+        if (bDoMore) {
+            for (int k = 0; k < g.ne; k++) {   /* :925-962 (stale _error) */
+                edge_t *e = &g.E[k];
+                const double th = e->stereo ? 7.815 : 5.991;
+                if (edge_chi2(e) > th || !depth_positive(&g, e)) e->level = 1;
+                e->robust = 0;
+            }
+            initialize(&g, 0);
+            res->iterations[1] = optimize(&g, 10, &res->chi2[1]);
+        } else {
+            res->stopped = 1;
+        }
+    }
+    for (int k = 0; k < g.ne; k++) {           /* :977-1008 */
+        edge_t *e = &g.E[k];
+        const double th = e->stereo ? 7.815 : 5.991;
+        res->edge_erase[k] = (edge_chi2(e) > th || !depth_positive(&g, e)) ? 1 : 0;
+    }
+    for (int i = 0; i < g.np; i++) {           /* :1033-1048 Converter::toCvMat */
+        double R[9];
+        quat_to_R(g.T[i].r, R);
+        float *o = res->pose_Tcw + 16 * i;
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) o[4 * r + c] = (float)R[3 * r + c];
+            o[4 * r + 3] = (float)g.T[i].t[r];
+        }
+        o[12] = 0; o[13] = 0; o[14] = 0; o[15] = 1;
+    }
+    for (int i = 0; i < g.nq; i++)
+        for (int j = 0; j < 3; j++) res->point_Xw[3 * i + j] = (float)g.X[i][j];
+    free(g.T); free(g.X); free(g.E); free(g.pose_hidx); free(g.point_hidx); free(g.hpose); free(g.hpoint);
+    return rc;
+}

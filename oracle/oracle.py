@@ -282,3 +282,52 @@ def orb_descriptor(blur: np.ndarray, x: float, y: float, angle: float, pattern) 
     out = np.zeros(32, np.uint8)
     lib().orc_orb_descriptor(_p(blur), blur.shape[1], x, y, angle, _p(pat), _p(out))
     return out
+
+
+class LbaProblem(C.Structure):
+    _fields_ = [("n_poses", C.c_int32), ("pose_id", C.c_void_p), ("pose_fixed", C.c_void_p),
+                ("pose_Tcw", C.c_void_p), ("pose_cam", C.c_void_p), ("n_points", C.c_int32),
+                ("point_id", C.c_void_p), ("point_Xw", C.c_void_p), ("n_edges", C.c_int32),
+                ("edge_point", C.c_void_p), ("edge_pose", C.c_void_p), ("edge_obs", C.c_void_p),
+                ("edge_inv_sigma2", C.c_void_p)]
+
+
+class LbaResult(C.Structure):
+    _fields_ = [("pose_Tcw", C.c_void_p), ("point_Xw", C.c_void_p), ("edge_erase", C.c_void_p),
+                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2), ("stopped", C.c_int32)]
+
+
+def make_lba_structs(prob: dict):
+    """Build (LbaProblem, keepalive arrays) from a synth.localba_problem dict."""
+    keep = {}
+    for k in ("pose_id", "pose_fixed", "pose_Tcw", "pose_cam", "point_id", "point_Xw", "edge_point",
+              "edge_pose", "edge_obs", "edge_inv_sigma2"):
+        keep[k] = np.ascontiguousarray(prob[k])
+    P = LbaProblem(len(keep["pose_id"]), keep["pose_id"].ctypes.data, keep["pose_fixed"].ctypes.data,
+                   keep["pose_Tcw"].ctypes.data, keep["pose_cam"].ctypes.data, len(keep["point_id"]),
+                   keep["point_id"].ctypes.data, keep["point_Xw"].ctypes.data, len(keep["edge_point"]),
+                   keep["edge_point"].ctypes.data, keep["edge_pose"].ctypes.data, keep["edge_obs"].ctypes.data,
+                   keep["edge_inv_sigma2"].ctypes.data)
+    return P, keep
+
+
+def make_lba_result(prob: dict):
+    out = {"pose_Tcw": np.zeros((len(prob["pose_id"]), 16), np.float32),
+           "point_Xw": np.zeros((len(prob["point_id"]), 3), np.float32),
+           "edge_erase": np.zeros(len(prob["edge_point"]), np.uint8)}
+    R = LbaResult(out["pose_Tcw"].ctypes.data, out["point_Xw"].ctypes.data, out["edge_erase"].ctypes.data)
+    return R, out
+
+
+def lba_solve(prob: dict, stop: bool = False):
+    """Optimizer::LocalBundleAdjustment optimisation core on the CPU (double precision)."""
+    L = lib()
+    L.lba_oracle_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    P, keep = make_lba_structs(prob)
+    R, out = make_lba_result(prob)
+    flag = C.c_int32(1 if stop else 0)
+    L.lba_oracle_solve(C.byref(P), C.byref(R), C.byref(flag))
+    out["iterations"] = tuple(R.iterations)
+    out["chi2"] = tuple(R.chi2)
+    out["stopped"] = R.stopped
+    return out

@@ -1,0 +1,960 @@
+// MI355X-native Optimizer::LocalBundleAdjustment core (Optimizer.cc:900-1008) over the
+// g2o LM + Schur path it uses (BlockSolver_6_3 + OptimizationAlgorithmLevenberg), FP64.
+//
+// Device work per LM iteration (N10-N13 of SURVEY.md §2.1):
+//   lba_linearize     one thread per active edge: residual, Huber weight, analytic 2x9 /
+//                     3x9 Jacobians, per-edge quadratic-form pieces (Hpl block kept)
+//   lba_reduce_points one thread per landmark: Hll (3x3), b_l  (edges of a point are a CSR
+//                     segment -> deterministic order)
+//   lba_reduce_poses  one workgroup per free pose: Hpp (6x6), b_p tree reduction
+// per LM trial:
+//   lba_schur_points  one thread per landmark: Dinv = (Hll + lambda I)^-1 (Eigen cofactor
+//                     inverse), L = chol(Dinv), Y_l = Hpl_l L, w_l = L^T b_l
+//   lba_syrk_mfma     Hpp - Y Y^T on FP64 matrix cores (v_mfma_f64_16x16x4f64), one wave per
+//                     16x16 upper tile per K slice, partial slabs reduced in fixed order
+//   lba_schur_reduce  Hschur = Hpp + lambda I - sum(slabs), b_schur = b_p - Y w
+//   lba_chol_solve    dense Cholesky of the <=126x126 Schur matrix in LDS + two solves
+//   lba_backsub       x_l = Dinv (b_l - Hpl^T x_p)
+//   lba_update        T <- exp(x_p) T (SE3Quat::exp, left-multiplied), X <- X + x_l
+//   lba_errors        trial residuals (kept as g2o's stale _error) + robust chi2 + scale
+// The LM accept/reject/lambda logic (optimization_algorithm_levenberg.cpp:61-164) runs on
+// the host with one 3-double readback per trial.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "orb_engine.h"
+#include "orbslam2_amd.h"
+
+#define LBA_CHK(x)                                                                  \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "orbslam2_amd lba: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return ORBX_EDEVICE;                                                    \
+        }                                                                           \
+    } while (0)
+
+namespace lbaamd {
+
+constexpr int kMaxPoses = 21;        // 6 * 21 = 126 <= 128 (one Schur matrix in LDS)
+constexpr int kNP = 128;             // padded Schur dimension
+constexpr int kRedBlocks = 16384;    // partial-sum region stride (blocks) for scalar reductions
+
+struct Quat { double x, y, z, w; };
+struct Pose { double q[4]; double t[3]; double pad; };   // q = (x, y, z, w)
+
+__host__ __device__ inline void quat_rotate(const double q[4], const double v[3], double o[3]) {
+    double uv[3] = {q[1] * v[2] - q[2] * v[1], q[2] * v[0] - q[0] * v[2], q[0] * v[1] - q[1] * v[0]};
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    const double cx = q[1] * uv[2] - q[2] * uv[1], cy = q[2] * uv[0] - q[0] * uv[2], cz = q[0] * uv[1] - q[1] * uv[0];
+    o[0] = v[0] + q[3] * uv[0] + cx;
+    o[1] = v[1] + q[3] * uv[1] + cy;
+    o[2] = v[2] + q[3] * uv[2] + cz;
+}
+
+__host__ __device__ inline void quat_to_R(const double q[4], double R[9]) {
+    const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+    const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    const double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    const double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+    R[3] = txy + twz; R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
+}
+
+// Eigen::Quaternion(const Matrix3&) + SE3Quat::normalizeRotation
+__host__ __device__ inline void quat_from_R_norm(const double m[9], double q[4]) {
+    double t = m[0] + m[4] + m[8];
+    double c[3], w;
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        w = 0.5 * t;
+        t = 0.5 / t;
+        c[0] = (m[7] - m[5]) * t;
+        c[1] = (m[2] - m[6]) * t;
+        c[2] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[4 * i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(m[4 * i] - m[4 * j] - m[4 * k] + 1.0);
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        w = (m[3 * k + j] - m[3 * j + k]) * t;
+        c[j] = (m[3 * j + i] + m[3 * i + j]) * t;
+        c[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+    }
+    if (w < 0) { c[0] = -c[0]; c[1] = -c[1]; c[2] = -c[2]; w = -w; }
+    const double n = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2] + w * w);
+    q[0] = c[0] / n; q[1] = c[1] / n; q[2] = c[2] / n; q[3] = w / n;
+}
+
+__device__ inline void pose_map(const Pose &T, const double X[3], double o[3]) {
+    quat_rotate(T.q, X, o);
+    o[0] += T.t[0]; o[1] += T.t[1]; o[2] += T.t[2];
+}
+
+// exp(u) * T  (VertexSE3Expmap::oplusImpl, se3quat.h:223-257 + operator*)
+__device__ inline Pose pose_oplus(const Pose &T, const double u[6]) {
+    const double w0 = u[0], w1 = u[1], w2 = u[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double O2[9], R[9], V[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) { R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i]; V[i] = R[i]; }
+    } else {
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+        const double c = (theta - sin(theta)) / (theta * theta * theta);
+        for (int i = 0; i < 9; i++) {
+            const double I = i % 4 == 0 ? 1.0 : 0.0;
+            R[i] = I + a * O[i] + b * O2[i];
+            V[i] = I + b * O[i] + c * O2[i];
+        }
+    }
+    double dq[4], dt[3];
+    quat_from_R_norm(R, dq);
+    for (int i = 0; i < 3; i++) dt[i] = V[3 * i] * u[3] + V[3 * i + 1] * u[4] + V[3 * i + 2] * u[5];
+    Pose r;
+    double rt[3];
+    quat_rotate(dq, T.t, rt);
+    r.t[0] = dt[0] + rt[0]; r.t[1] = dt[1] + rt[1]; r.t[2] = dt[2] + rt[2];
+    const double *a = dq, *b = T.q;  // (x, y, z, w)
+    double q[4];
+    q[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    q[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    q[1] = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+    q[2] = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+    if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    r.q[0] = q[0] / n; r.q[1] = q[1] / n; r.q[2] = q[2] / n; r.q[3] = q[3] / n;
+    r.pad = 0;
+    return r;
+}
+
+struct EdgeDev {
+    int point, pose;
+    double obs[3];
+    double info, delta, dsqr;
+    double fx, fy, cx, cy, bf;
+    int stereo, robust;
+};
+
+struct Graph {
+    // vertices
+    Pose *T, *T2;
+    double *X, *X2;
+    // edges
+    const EdgeDev *E;
+    double *err;           // [ne][3] g2o _error
+    const int *act;        // active edge indices (edge order)
+    int nact;
+    const int *pose_hidx;  // per pose vertex, -1 = fixed / inactive
+    const int *point_hidx;
+    const int *hpose, *hpoint;  // hessian index -> vertex
+    int P, Lm;
+    const int *pt_start, *pt_items;  // per active point: active slots (all edges of the point)
+    const int *ps_start, *ps_items;  // per free pose: active slots
+    // system
+    double *con;           // [nact][36] per-slot Hll(6) bl(3) Hpp(21) bp(6)
+    double *hpl;           // [nact][18]
+    double *Hll, *bl;      // [Lm][9], [Lm][3]
+    double *Hpp, *bp;      // [P][36], [P][6]
+    double *Dinv;          // [Lm][9]
+    double *Y;             // [kNP][Kpad] row-major
+    double *w;             // [Kpad]
+    double *slab;          // [S][kNP][kNP]
+    double *Hs, *bs;       // [kNP][kNP], [kNP]
+    double *x;             // [6P + 3Lm]
+    double *partial;       // [4][kRedBlocks]
+    double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok
+    int Kpad, S;
+};
+
+__device__ inline void edge_error(const Graph &g, const EdgeDev &e, const Pose *T, const double *X, double err[3]) {
+    double p[3];
+    pose_map(T[e.pose], X + 3 * e.point, p);
+    if (!e.stereo) {
+        const double u = p[0] / p[2], v = p[1] / p[2];
+        err[0] = e.obs[0] - (u * e.fx + e.cx);
+        err[1] = e.obs[1] - (v * e.fy + e.cy);
+        err[2] = 0;
+    } else {
+        const float invz = (float)(1.0f / p[2]);          // types_six_dof_expmap.cpp:151
+        const float bff = (float)e.bf;
+        const double r0 = p[0] * invz * e.fx + e.cx;
+        const double r1 = p[1] * invz * e.fy + e.cy;
+        const double r2 = r0 - (double)(bff * invz);
+        err[0] = e.obs[0] - r0;
+        err[1] = e.obs[1] - r1;
+        err[2] = e.obs[2] - r2;
+    }
+}
+
+__device__ inline double edge_chi2(const EdgeDev &e, const double err[3]) {
+    double s = err[0] * e.info * err[0] + err[1] * e.info * err[1];
+    if (e.stereo) s += err[2] * e.info * err[2];
+    return s;
+}
+
+__device__ inline void huber(const EdgeDev &e, double chi, double &rho0, double &rho1) {
+    if (chi <= e.dsqr) { rho0 = chi; rho1 = 1.0; }
+    else { const double s = sqrt(chi); rho0 = 2 * s * e.delta - e.dsqr; rho1 = e.delta / s; }
+}
+
+// block sum of one double per thread into partial[blockIdx.x]
+__device__ inline void block_sum_to(double v, double *dst) {
+    __shared__ double sh[256];
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *dst = sh[0];
+}
+
+// ---- linearize: errors + robust chi2 + per-edge quadratic-form pieces
+__global__ __launch_bounds__(256) void lba_linearize(Graph g) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    double rchi = 0;
+    if (s < g.nact) {
+        const int k = g.act[s];
+        const EdgeDev e = g.E[k];
+        double err[3];
+        edge_error(g, e, g.T, g.X, err);
+        g.err[3 * k] = err[0]; g.err[3 * k + 1] = err[1]; g.err[3 * k + 2] = err[2];
+        const double chi = edge_chi2(e, err);
+        double r0 = chi, r1 = 1.0;
+        if (e.robust) huber(e, chi, r0, r1);
+        rchi = r0;
+        // Jacobians (types_six_dof_expmap.cpp:103-139, 188-234)
+        const Pose T = g.T[e.pose];
+        double p[3], R[9];
+        pose_map(T, g.X + 3 * e.point, p);
+        quat_to_R(T.q, R);
+        const double x = p[0], y = p[1], z = p[2], z2 = z * z, fx = e.fx, fy = e.fy, bf = e.bf;
+        double Jp[9], Jt[18];
+        if (!e.stereo) {
+            const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
+            for (int i = 0; i < 2; i++)
+                for (int j = 0; j < 3; j++)
+                    Jp[3 * i + j] = (-1. / z * tmp[3 * i]) * R[j] + (-1. / z * tmp[3 * i + 1]) * R[3 + j] +
+                                    (-1. / z * tmp[3 * i + 2]) * R[6 + j];
+        } else {
+            for (int j = 0; j < 3; j++) {
+                Jp[j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
+                Jp[3 + j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
+                Jp[6 + j] = Jp[j] - bf * R[6 + j] / z2;
+            }
+        }
+        Jt[0] = x * y / z2 * fx; Jt[1] = -(1 + (x * x / z2)) * fx; Jt[2] = y / z * fx;
+        Jt[3] = -1. / z * fx; Jt[4] = 0; Jt[5] = x / z2 * fx;
+        Jt[6] = (1 + y * y / z2) * fy; Jt[7] = -x * y / z2 * fy; Jt[8] = -x / z * fy;
+        Jt[9] = 0; Jt[10] = -1. / z * fy; Jt[11] = y / z2 * fy;
+        if (e.stereo) {
+            Jt[12] = Jt[0] - bf * y / z2; Jt[13] = Jt[1] + bf * x / z2; Jt[14] = Jt[2];
+            Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf / z2;
+        }
+        const int D = e.stereo ? 3 : 2;
+        const double wW = r1 * e.info;
+        double omr[3];
+        for (int i = 0; i < D; i++) omr[i] = -(e.info * err[i]) * r1;
+        double *c = g.con + (long long)s * 36;
+        int u = 0;
+        for (int a = 0; a < 3; a++)
+            for (int b = a; b < 3; b++) {
+                double h = 0;
+                for (int i = 0; i < D; i++) h += Jp[3 * i + a] * wW * Jp[3 * i + b];
+                c[u++] = h;
+            }
+        for (int a = 0; a < 3; a++) {
+            double v = 0;
+            for (int i = 0; i < D; i++) v += Jp[3 * i + a] * omr[i];
+            c[6 + a] = v;
+        }
+        if (g.pose_hidx[e.pose] >= 0) {
+            u = 9;
+            for (int a = 0; a < 6; a++)
+                for (int b = a; b < 6; b++) {
+                    double h = 0;
+                    for (int i = 0; i < D; i++) h += Jt[6 * i + a] * wW * Jt[6 * i + b];
+                    c[u++] = h;
+                }
+            for (int a = 0; a < 6; a++) {
+                double v = 0;
+                for (int i = 0; i < D; i++) v += Jt[6 * i + a] * omr[i];
+                c[30 + a] = v;
+            }
+            double *hp = g.hpl + (long long)s * 18;
+            for (int a = 0; a < 6; a++)
+                for (int b = 0; b < 3; b++) {
+                    double h = 0;
+                    for (int i = 0; i < D; i++) h += Jt[6 * i + a] * wW * Jp[3 * i + b];
+                    hp[3 * a + b] = h;
+                }
+        }
+    }
+    block_sum_to(rchi, g.partial + blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    double dmax = 0;
+    if (l < g.Lm) {
+        double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+        for (int i = g.pt_start[l]; i < g.pt_start[l + 1]; i++) {
+            const double *c = g.con + (long long)g.pt_items[i] * 36;
+            for (int k = 0; k < 6; k++) h[k] += c[k];
+            for (int k = 0; k < 3; k++) b[k] += c[6 + k];
+        }
+        double *H = g.Hll + 9 * l;
+        H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
+        H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
+        H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
+        g.bl[3 * l] = b[0]; g.bl[3 * l + 1] = b[1]; g.bl[3 * l + 2] = b[2];
+        dmax = fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5])));
+    }
+    __shared__ double sh[256];
+    sh[threadIdx.x] = dmax;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) g.partial[kRedBlocks + blockIdx.x] = sh[0];
+}
+
+__global__ __launch_bounds__(256) void lba_reduce_poses(Graph g) {
+    const int i = blockIdx.x;
+    double acc[27];
+    for (int k = 0; k < 27; k++) acc[k] = 0;
+    for (int t = g.ps_start[i] + (int)threadIdx.x; t < g.ps_start[i + 1]; t += 256) {
+        const double *c = g.con + (long long)g.ps_items[t] * 36 + 9;
+        for (int k = 0; k < 27; k++) acc[k] += c[k];
+    }
+    __shared__ double sh[27][256];
+    for (int k = 0; k < 27; k++) sh[k][threadIdx.x] = acc[k];
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s)
+            for (int k = 0; k < 27; k++) sh[k][threadIdx.x] += sh[k][threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x < 36) {
+        const int a = threadIdx.x / 6, b = threadIdx.x % 6;
+        const int lo = min(a, b), hi = max(a, b);
+        const int u = lo * 6 - lo * (lo - 1) / 2 + (hi - lo);   // packed upper index
+        g.Hpp[36 * i + threadIdx.x] = sh[u][0];
+    }
+    if (threadIdx.x < 6) g.bp[6 * i + threadIdx.x] = sh[21 + threadIdx.x][0];
+    if (threadIdx.x == 0) {
+        double m = 0;
+        for (int a = 0; a < 6; a++) {
+            const int u = a * 6 - a * (a - 1) / 2;
+            m = fmax(m, fabs(sh[u][0]));
+        }
+        g.partial[2 * kRedBlocks + i] = m;
+    }
+}
+
+// final scalar reductions: mode 0 -> chi2 (sum) + maxdiag (max); mode 1 -> tempChi + scale
+__global__ __launch_bounds__(256) void lba_finish(Graph g, int mode, int n0, int n1, int n2) {
+    __shared__ double sa[256], sb[256];
+    double a = 0, b = 0;
+    for (int i = threadIdx.x; i < n0; i += 256) a += g.partial[i];
+    if (mode == 0) {
+        for (int i = threadIdx.x; i < n1; i += 256) b = fmax(b, g.partial[kRedBlocks + i]);
+        for (int i = threadIdx.x; i < n2; i += 256) b = fmax(b, g.partial[2 * kRedBlocks + i]);
+    } else {
+        for (int i = threadIdx.x; i < n1; i += 256) b += g.partial[kRedBlocks + i];
+    }
+    sa[threadIdx.x] = a;
+    sb[threadIdx.x] = b;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            sa[threadIdx.x] += sa[threadIdx.x + s];
+            sb[threadIdx.x] = mode == 0 ? fmax(sb[threadIdx.x], sb[threadIdx.x + s]) : sb[threadIdx.x] + sb[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (mode == 0) { g.scalars[0] = sa[0]; g.scalars[1] = sb[0]; }
+        else { g.scalars[2] = sa[0]; g.scalars[3] = sb[0]; }
+    }
+}
+
+// ---- Schur: per landmark Dinv, L = chol(Dinv), Y block and w
+__device__ inline void inv3(const double m[9], double o[9]) {
+    const double c00 = m[4] * m[8] - m[5] * m[7];
+    const double c10 = m[5] * m[6] - m[3] * m[8];
+    const double c20 = m[3] * m[7] - m[4] * m[6];
+    const double det = m[0] * c00 + m[1] * c10 + m[2] * c20;
+    const double id = 1.0 / det;
+    o[0] = c00 * id; o[1] = (m[2] * m[7] - m[1] * m[8]) * id; o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+    o[3] = c10 * id; o[4] = (m[0] * m[8] - m[2] * m[6]) * id; o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    o[6] = c20 * id; o[7] = (m[1] * m[6] - m[0] * m[7]) * id; o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+__global__ __launch_bounds__(256) void lba_schur_points(Graph g, double lambda) {
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    if (l >= g.Lm) return;
+    double D[9];
+    for (int k = 0; k < 9; k++) D[k] = g.Hll[9 * l + k];
+    D[0] += lambda; D[4] += lambda; D[8] += lambda;
+    double Di[9];
+    inv3(D, Di);
+    for (int k = 0; k < 9; k++) g.Dinv[9 * l + k] = Di[k];
+    // Dinv = L L^T (symmetrised)
+    const double a00 = Di[0], a10 = 0.5 * (Di[3] + Di[1]), a11 = Di[4];
+    const double a20 = 0.5 * (Di[6] + Di[2]), a21 = 0.5 * (Di[7] + Di[5]), a22 = Di[8];
+    const double L00 = sqrt(a00), L10 = a10 / L00, L20 = a20 / L00;
+    const double L11 = sqrt(a11 - L10 * L10), L21 = (a21 - L20 * L10) / L11;
+    const double L22 = sqrt(a22 - L20 * L20 - L21 * L21);
+    const double *b = g.bl + 3 * l;
+    const long long K = g.Kpad, c0 = 3LL * l;
+    g.w[c0] = L00 * b[0] + L10 * b[1] + L20 * b[2];
+    g.w[c0 + 1] = L11 * b[1] + L21 * b[2];
+    g.w[c0 + 2] = L22 * b[2];
+    for (int i = g.pt_start[l]; i < g.pt_start[l + 1]; i++) {
+        const int s = g.pt_items[i];
+        const int ph = g.pose_hidx[g.E[g.act[s]].pose];
+        if (ph < 0) continue;
+        const double *B = g.hpl + (long long)s * 18;
+        for (int r = 0; r < 6; r++) {
+            const double b0 = B[3 * r], b1 = B[3 * r + 1], b2 = B[3 * r + 2];
+            double *yr = g.Y + (long long)(6 * ph + r) * K + c0;
+            yr[0] = b0 * L00 + b1 * L10 + b2 * L20;
+            yr[1] = b1 * L11 + b2 * L21;
+            yr[2] = b2 * L22;
+        }
+    }
+}
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+// Y Y^T on FP64 MFMA: one wave per (upper tile pair, K slice); slab[s] = partial tile sums
+__global__ __launch_bounds__(64) void lba_syrk_mfma(Graph g, int ntile, int kchunk) {
+    const int lane = threadIdx.x;
+    int pair = blockIdx.x, I = 0;
+    while (pair >= ntile - I) { pair -= ntile - I; I++; }
+    const int J = I + pair;
+    const int s = blockIdx.y;
+    const long long K = g.Kpad;
+    const int k0 = s * kchunk, k1 = min((int)K, k0 + kchunk);
+    const double *ya = g.Y + (long long)(16 * I + (lane & 15)) * K;
+    const double *yb = g.Y + (long long)(16 * J + (lane & 15)) * K;
+    double4_t acc = {0, 0, 0, 0};
+    for (int kk = k0; kk < k1; kk += 4) {  // (k1 - k0) % 4 == 0: every lane runs every step
+        const int k = kk + (lane >> 4);
+        const double a = ya[k], b = yb[k];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    double *out = g.slab + (long long)s * kNP * kNP;
+    // C/D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * reg
+    for (int r = 0; r < 4; r++) {
+        const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
+        out[(long long)row * kNP + col] = acc[r];
+    }
+}
+
+__global__ __launch_bounds__(256) void lba_schur_reduce(Graph g, double lambda) {
+    const int n6 = 6 * g.P;
+    const int r = blockIdx.x;  // row
+    const long long K = g.Kpad;
+    // b_schur[r] = b_p[r] - (Y w)[r]
+    __shared__ double sh[256];
+    double acc = 0;
+    const double *yr = g.Y + (long long)r * K;
+    for (long long k = threadIdx.x; k < K; k += 256) acc += yr[k] * g.w[k];
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) g.bs[r] = g.bp[r] - sh[0];
+    for (int c = threadIdx.x; c < n6; c += 256) {
+        const int lo = min(r, c), hi = max(r, c);   // slabs hold upper tiles
+        double v = 0;
+        for (int s = 0; s < g.S; s++) v += g.slab[(long long)s * kNP * kNP + (long long)lo * kNP + hi];
+        double h = 0;
+        if (r / 6 == c / 6) h = g.Hpp[36 * (r / 6) + 6 * (r % 6) + (c % 6)];
+        if (r == c) h += lambda;
+        g.Hs[(long long)r * kNP + c] = h - v;
+    }
+}
+
+// dense Cholesky of the n6 x n6 Schur matrix in LDS + forward / back substitution
+// (replaces LinearSolverEigen's SimplicialLDLT; failure -> the trial is rejected,
+// optimization_algorithm_levenberg.cpp:126-127)
+__global__ __launch_bounds__(256) void lba_chol_solve(Graph g) {
+    extern __shared__ double A[];   // n6 x (n6 + 1), column n6 = right-hand side
+    const int n = 6 * g.P, ld = n + 1, tid = threadIdx.x;
+    for (int i = tid; i < n * n; i += 256) A[(i / n) * ld + i % n] = g.Hs[(long long)(i / n) * kNP + i % n];
+    for (int i = tid; i < n; i += 256) A[i * ld + n] = g.bs[i];
+    __syncthreads();
+    for (int j = 0; j < n; j++) {
+        const double d = A[j * ld + j];
+        if (!(d > 0)) {                 // uniform: every thread read the same value
+            if (tid == 0) g.scalars[4] = 0;
+            return;
+        }
+        const double ljj = sqrt(d);
+        for (int i = j + 1 + tid; i < n; i += 256) A[i * ld + j] /= ljj;
+        __syncthreads();
+        if (tid == 0) A[j * ld + j] = ljj;
+        const int m = n - j - 1;
+        for (int t = tid; t < m * m; t += 256) {
+            const int r = j + 1 + t / m, c = j + 1 + t % m;
+            if (c <= r) A[r * ld + c] -= A[r * ld + j] * A[c * ld + j];
+        }
+        __syncthreads();
+    }
+    for (int k = 0; k < n; k++) {       // L y = b (column sweep)
+        const double yk = A[k * ld + n] / A[k * ld + k];
+        __syncthreads();
+        if (tid == 0) A[k * ld + n] = yk;
+        for (int i = k + 1 + tid; i < n; i += 256) A[i * ld + n] -= A[i * ld + k] * yk;
+        __syncthreads();
+    }
+    for (int k = n - 1; k >= 0; k--) {  // L^T x = y
+        const double xk = A[k * ld + n] / A[k * ld + k];
+        __syncthreads();
+        if (tid == 0) A[k * ld + n] = xk;
+        for (int i = tid; i < k; i += 256) A[i * ld + n] -= A[k * ld + i] * xk;
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += 256) g.x[i] = A[i * ld + n];
+    if (tid == 0) g.scalars[4] = 1;
+}
+
+__global__ void lba_set_ok(Graph g) { g.scalars[4] = 1; }
+
+__global__ __launch_bounds__(256) void lba_backsub(Graph g) {
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    if (l >= g.Lm) return;
+    double c[3] = {g.bl[3 * l], g.bl[3 * l + 1], g.bl[3 * l + 2]};
+    for (int i = g.pt_start[l]; i < g.pt_start[l + 1]; i++) {
+        const int s = g.pt_items[i];
+        const int ph = g.pose_hidx[g.E[g.act[s]].pose];
+        if (ph < 0) continue;
+        const double *B = g.hpl + (long long)s * 18;
+        const double *xp = g.x + 6 * ph;
+        for (int cc = 0; cc < 3; cc++) {
+            double v = 0;
+            for (int a = 0; a < 6; a++) v += B[3 * a + cc] * (-xp[a]);
+            c[cc] += v;
+        }
+    }
+    const double *Di = g.Dinv + 9 * l;
+    double *xl = g.x + 6 * g.P + 3 * l;
+    for (int a = 0; a < 3; a++) xl[a] = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
+}
+
+__global__ __launch_bounds__(256) void lba_update(Graph g, double lambda, const double *b_full) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    double sc = 0;
+    if (t < g.P) {
+        const int v = g.hpose[t];
+        g.T2[v] = pose_oplus(g.T[v], g.x + 6 * t);
+    } else if (t < g.P + g.Lm) {
+        const int l = t - g.P, v = g.hpoint[l];
+        const double *dx = g.x + 6 * g.P + 3 * l;
+        for (int k = 0; k < 3; k++) g.X2[3 * v + k] = g.X[3 * v + k] + dx[k];
+    }
+    // computeScale pieces: x (lambda x + b) over this thread's entries
+    const int nx = 6 * g.P + 3 * g.Lm;
+    for (int j = t; j < nx; j += gridDim.x * 256) sc += g.x[j] * (lambda * g.x[j] + b_full[j]);
+    block_sum_to(sc, g.partial + kRedBlocks + blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void lba_errors(Graph g) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    double r0 = 0;
+    if (s < g.nact) {
+        const int k = g.act[s];
+        const EdgeDev e = g.E[k];
+        double err[3];
+        edge_error(g, e, g.T2, g.X2, err);
+        g.err[3 * k] = err[0]; g.err[3 * k + 1] = err[1]; g.err[3 * k + 2] = err[2];
+        const double chi = edge_chi2(e, err);
+        double r1 = 1;
+        r0 = chi;
+        if (e.robust) huber(e, chi, r0, r1);
+    }
+    block_sum_to(r0, g.partial + blockIdx.x);
+}
+
+// outlier test of Optimizer.cc:925-962 / 977-1008: chi2 (stale _error) + depth sign
+__global__ __launch_bounds__(256) void lba_outliers(const EdgeDev *E, const double *err, const Pose *T,
+                                                    const double *X, int ne, uint8_t *flag) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= ne) return;
+    const EdgeDev e = E[k];
+    const double *er = err + 3 * k;
+    const double chi = edge_chi2(e, er);
+    double p[3];
+    pose_map(T[e.pose], X + 3 * e.point, p);
+    const double th = e.stereo ? 7.815 : 5.991;
+    flag[k] = (chi > th || !(p[2] > 0.0)) ? 1 : 0;
+}
+
+// b vector in hessian order for computeScale: [b_p (6P) | b_l (3Lm)]
+__global__ __launch_bounds__(256) void lba_gather_b(Graph g, double *b_full) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int n6 = 6 * g.P;
+    if (t < n6) b_full[t] = g.bp[t];
+    else if (t < n6 + 3 * g.Lm) b_full[t] = g.bl[t - n6];
+}
+
+}  // namespace lbaamd
+
+using namespace lbaamd;
+
+struct DBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n && p) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc(&p, std::max<size_t>(bytes, 64)) != hipSuccess) return -1;
+        n = std::max<size_t>(bytes, 64);
+        return 0;
+    }
+    template <class T> T *as() { return (T *)p; }
+    ~DBuf() { if (p) (void)hipFree(p); }
+};
+
+struct lba_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DBuf T, T2, X, X2, E, err, act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items,
+        ps_start, ps_items, con, hpl, Hll, bl, Hpp, bp, Dinv, Y, w, slab, Hs, bs, x, partial,
+        scalars, bfull, flags;
+    double *h_scalars = nullptr;  // pinned
+};
+
+namespace {
+
+struct HostGraph {
+    int np, nq, ne;
+    std::vector<int> level, robust_on;
+    const int32_t *pose_id, *point_id;
+    const uint8_t *fixed;
+    std::vector<int> edge_point, edge_pose;
+};
+
+struct ActiveSet {
+    int P = 0, Lm = 0;
+    std::vector<int> act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items, ps_start, ps_items;
+};
+
+// SparseOptimizer::initializeOptimization(level) + buildIndexMapping + block structure
+void build_active(const HostGraph &h, ActiveSet &A) {
+    A = ActiveSet();
+    std::vector<char> pa(h.np, 0), qa(h.nq, 0);
+    for (int k = 0; k < h.ne; k++)
+        if (h.level[k] == 0) { A.act.push_back(k); pa[h.edge_pose[k]] = 1; qa[h.edge_point[k]] = 1; }
+    for (int i = 0; i < h.np; i++) if (pa[i] && !h.fixed[i]) A.hpose.push_back(i);
+    for (int i = 0; i < h.nq; i++) if (qa[i]) A.hpoint.push_back(i);
+    std::stable_sort(A.hpose.begin(), A.hpose.end(), [&](int a, int b) { return h.pose_id[a] < h.pose_id[b]; });
+    std::stable_sort(A.hpoint.begin(), A.hpoint.end(), [&](int a, int b) { return h.point_id[a] < h.point_id[b]; });
+    A.P = (int)A.hpose.size();
+    A.Lm = (int)A.hpoint.size();
+    A.pose_hidx.assign(h.np, -1);
+    A.point_hidx.assign(h.nq, -1);
+    for (int i = 0; i < A.P; i++) A.pose_hidx[A.hpose[i]] = i;
+    for (int i = 0; i < A.Lm; i++) A.point_hidx[A.hpoint[i]] = i;
+    A.pt_start.assign(A.Lm + 1, 0);
+    A.ps_start.assign(A.P + 1, 0);
+    for (int s = 0; s < (int)A.act.size(); s++) {
+        const int k = A.act[s];
+        A.pt_start[A.point_hidx[h.edge_point[k]] + 1]++;
+        const int ph = A.pose_hidx[h.edge_pose[k]];
+        if (ph >= 0) A.ps_start[ph + 1]++;
+    }
+    for (int l = 0; l < A.Lm; l++) A.pt_start[l + 1] += A.pt_start[l];
+    for (int i = 0; i < A.P; i++) A.ps_start[i + 1] += A.ps_start[i];
+    A.pt_items.assign(std::max(1, A.pt_start[A.Lm]), 0);
+    A.ps_items.assign(std::max(1, A.ps_start[A.P]), 0);
+    std::vector<int> fl(A.Lm, 0), fp(A.P, 0);
+    for (int s = 0; s < (int)A.act.size(); s++) {
+        const int k = A.act[s];
+        const int l = A.point_hidx[h.edge_point[k]];
+        A.pt_items[A.pt_start[l] + fl[l]++] = s;
+        const int ph = A.pose_hidx[h.edge_pose[k]];
+        if (ph >= 0) A.ps_items[A.ps_start[ph] + fp[ph]++] = s;
+    }
+}
+
+template <class T> int upload(DBuf &b, const std::vector<T> &v, hipStream_t s) {
+    if (b.ensure(sizeof(T) * std::max<size_t>(1, v.size()))) return -1;
+    if (!v.empty() && hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+    return 0;
+}
+
+int nblk(int n) { return std::max(1, (n + 255) / 256); }
+
+}  // namespace
+
+// One SparseOptimizer::optimize(iterations) on the device; returns iterations run.
+static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterations,
+                        const volatile int32_t *stop, double *final_chi) {
+    hipStream_t s = e->stream;
+    auto term = [&]() { return stop && *stop; };
+    if (A.P + A.Lm == 0) return -1;
+    if (A.P > kMaxPoses) return -2;
+    double lambda = 0, ni = 2;
+    int nBad = 0, it = 0;
+    const int nact = (int)A.act.size();
+    const int n6 = 6 * A.P, nx = n6 + 3 * A.Lm;
+    const int ntile = std::max(1, (n6 + 15) / 16);
+    const int npair = ntile * (ntile + 1) / 2;
+    for (int i = 0; i < iterations && !term(); i++) {
+        lba_linearize<<<nblk(nact), 256, 0, s>>>(g);
+        lba_reduce_points<<<nblk(A.Lm), 256, 0, s>>>(g);
+        if (A.P > 0) lba_reduce_poses<<<A.P, 256, 0, s>>>(g);
+        lba_finish<<<1, 256, 0, s>>>(g, 0, nblk(nact), nblk(A.Lm), A.P);
+        lba_gather_b<<<nblk(nx), 256, 0, s>>>(g, e->bfull.as<double>());
+        if (hipMemcpyAsync(e->h_scalars, g.scalars, 2 * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -3;
+        double currentChi = e->h_scalars[0], iniChi = currentChi, tempChi;
+        if (i == 0) { lambda = 1e-5 * e->h_scalars[1]; ni = 2; nBad = 0; }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            // setLambda + Schur + solve + update + errors (push/pop = T/T2 double buffering)
+            lba_schur_points<<<nblk(A.Lm), 256, 0, s>>>(g, lambda);
+            if (A.P > 0) {
+                const int kchunk = (((g.Kpad + g.S - 1) / g.S + 3) / 4) * 4;  // S * kchunk >= Kpad
+                lba_syrk_mfma<<<dim3(npair, g.S), 64, 0, s>>>(g, ntile, kchunk);
+                lba_schur_reduce<<<n6, 256, 0, s>>>(g, lambda);
+                lba_chol_solve<<<1, 256, sizeof(double) * n6 * (n6 + 1), s>>>(g);
+            } else {
+                lba_set_ok<<<1, 1, 0, s>>>(g);
+            }
+            lba_backsub<<<nblk(A.Lm), 256, 0, s>>>(g);
+            lba_update<<<nblk(A.P + A.Lm), 256, 0, s>>>(g, lambda, e->bfull.as<double>());
+            lba_errors<<<nblk(nact), 256, 0, s>>>(g);
+            lba_finish<<<1, 256, 0, s>>>(g, 1, nblk(nact), nblk(A.P + A.Lm), 0);
+            if (hipMemcpyAsync(e->h_scalars + 2, g.scalars + 2, 3 * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return -3;
+            const bool ok2 = e->h_scalars[4] != 0;
+            tempChi = ok2 ? e->h_scalars[2] : DBL_MAX;
+            rho = currentChi - tempChi;
+            double scale = e->h_scalars[3] + 1e-3;
+            rho /= scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                lambda *= std::max(1. / 3., alpha);
+                ni = 2;
+                currentChi = tempChi;
+                std::swap(g.T, g.T2);     // discardTop: keep the trial estimate
+                std::swap(g.X, g.X2);
+            } else {
+                lambda *= ni;
+                ni *= 2;                  // pop: keep the current estimate
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10 && !term());
+        it++;
+        *final_chi = currentChi;
+        bool ok = true;
+        if (qmax == 10 || rho == 0) ok = false;
+        else {
+            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++; else nBad = 0;
+            if (nBad >= 3) ok = false;
+        }
+        if (!ok) break;
+    }
+    return it;
+}
+
+extern "C" {
+
+int lba_create(lba_engine **out) {
+    if (!out) return ORBX_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORBX_EDEVICE;
+    lba_engine *e = new lba_engine();
+    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&e->h_scalars, 8 * sizeof(double)) != hipSuccess) {
+        delete e;
+        return ORBX_EDEVICE;
+    }
+    *out = e;
+    return ORBX_OK;
+}
+
+void lba_destroy(lba_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
+    if (e->h_scalars) (void)hipHostFree(e->h_scalars);
+    delete e;
+}
+
+int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile int32_t *stop) {
+    if (!e || !p || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return ORBX_EINVAL;
+    LBA_CHK(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    const int np = p->n_poses, nq = p->n_points, ne = p->n_edges;
+    r->iterations[0] = r->iterations[1] = 0;
+    r->chi2[0] = r->chi2[1] = 0;
+    r->stopped = 0;
+    if (stop && *stop) {  // Optimizer.cc:902-904: return before optimising, nothing written back
+        r->stopped = 1;
+        std::memcpy(r->pose_Tcw, p->pose_Tcw, sizeof(float) * 16 * np);
+        std::memcpy(r->point_Xw, p->point_Xw, sizeof(float) * 3 * nq);
+        std::memset(r->edge_erase, 0, ne);
+        return ORBX_OK;
+    }
+    // vertices (Converter::toSE3Quat / toVector3d)
+    std::vector<Pose> T(np);
+    for (int i = 0; i < np; i++) {
+        const float *m = p->pose_Tcw + 16 * i;
+        const double R[9] = {m[0], m[1], m[2], m[4], m[5], m[6], m[8], m[9], m[10]};
+        quat_from_R_norm(R, T[i].q);
+        T[i].t[0] = m[3]; T[i].t[1] = m[7]; T[i].t[2] = m[11];
+        T[i].pad = 0;
+    }
+    std::vector<double> X(3 * (size_t)nq);
+    for (int i = 0; i < 3 * nq; i++) X[i] = p->point_Xw[i];
+    HostGraph h;
+    h.np = np; h.nq = nq; h.ne = ne;
+    h.pose_id = p->pose_id; h.point_id = p->point_id; h.fixed = p->pose_fixed;
+    h.edge_point.assign(p->edge_point, p->edge_point + ne);
+    h.edge_pose.assign(p->edge_pose, p->edge_pose + ne);
+    h.level.assign(ne, 0);
+    for (int k = 0; k < ne; k++)
+        if (h.edge_point[k] < 0 || h.edge_point[k] >= nq || h.edge_pose[k] < 0 || h.edge_pose[k] >= np) return ORBX_EINVAL;
+    const float thMono = (float)std::sqrt(5.991), thStereo = (float)std::sqrt(7.815);
+    std::vector<EdgeDev> E(ne);
+    for (int k = 0; k < ne; k++) {
+        EdgeDev &d = E[k];
+        const float *ob = p->edge_obs + 3 * k;
+        d.point = h.edge_point[k];
+        d.pose = h.edge_pose[k];
+        d.stereo = ob[2] >= 0;
+        d.obs[0] = ob[0]; d.obs[1] = ob[1]; d.obs[2] = d.stereo ? ob[2] : 0;
+        d.info = p->edge_inv_sigma2[k];
+        d.robust = 1;
+        d.delta = d.stereo ? thStereo : thMono;
+        d.dsqr = d.delta * d.delta;
+        const float *cam = p->pose_cam + 5 * d.pose;
+        d.fx = cam[0]; d.fy = cam[1]; d.cx = cam[2]; d.cy = cam[3]; d.bf = cam[4];
+    }
+    if (upload(e->T, T, s) || upload(e->T2, T, s) || upload(e->X, X, s) || upload(e->X2, X, s) ||
+        upload(e->E, E, s) || e->err.ensure(sizeof(double) * 3 * std::max(ne, 1)) ||
+        e->flags.ensure(std::max(ne, 1)) || e->scalars.ensure(8 * sizeof(double)) ||
+        e->partial.ensure(sizeof(double) * 4 * kRedBlocks))
+        return ORBX_EDEVICE;
+    LBA_CHK(hipMemsetAsync(e->err.p, 0, sizeof(double) * 3 * std::max(ne, 1), s));
+    Graph g{};
+    g.T = e->T.as<Pose>(); g.T2 = e->T2.as<Pose>();
+    g.X = e->X.as<double>(); g.X2 = e->X2.as<double>();
+    g.E = e->E.as<EdgeDev>();
+    g.err = e->err.as<double>();
+    g.scalars = e->scalars.as<double>();
+    g.partial = e->partial.as<double>();
+    auto setup = [&](ActiveSet &A) -> int {
+        if (upload(e->act, A.act, s) || upload(e->pose_hidx, A.pose_hidx, s) || upload(e->point_hidx, A.point_hidx, s) ||
+            upload(e->hpose, A.hpose, s) || upload(e->hpoint, A.hpoint, s) || upload(e->pt_start, A.pt_start, s) ||
+            upload(e->pt_items, A.pt_items, s) || upload(e->ps_start, A.ps_start, s) || upload(e->ps_items, A.ps_items, s))
+            return -1;
+        const int nact = (int)A.act.size();
+        g.act = e->act.as<int>(); g.nact = nact;
+        g.pose_hidx = e->pose_hidx.as<int>(); g.point_hidx = e->point_hidx.as<int>();
+        g.hpose = e->hpose.as<int>(); g.hpoint = e->hpoint.as<int>();
+        g.P = A.P; g.Lm = A.Lm;
+        g.pt_start = e->pt_start.as<int>(); g.pt_items = e->pt_items.as<int>();
+        g.ps_start = e->ps_start.as<int>(); g.ps_items = e->ps_items.as<int>();
+        g.Kpad = std::max(4, ((3 * A.Lm + 3) / 4) * 4);
+        g.S = std::max(1, std::min(64, g.Kpad / 256));
+        if (e->con.ensure(sizeof(double) * 36 * std::max(nact, 1)) || e->hpl.ensure(sizeof(double) * 18 * std::max(nact, 1)) ||
+            e->Hll.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) || e->bl.ensure(sizeof(double) * 3 * std::max(A.Lm, 1)) ||
+            e->Hpp.ensure(sizeof(double) * 36 * std::max(A.P, 1)) || e->bp.ensure(sizeof(double) * 6 * std::max(A.P, 1)) ||
+            e->Dinv.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) ||
+            e->Y.ensure(sizeof(double) * kNP * (size_t)g.Kpad) || e->w.ensure(sizeof(double) * g.Kpad) ||
+            e->slab.ensure(sizeof(double) * (size_t)g.S * kNP * kNP) || e->Hs.ensure(sizeof(double) * kNP * kNP) ||
+            e->bs.ensure(sizeof(double) * kNP) || e->x.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)) ||
+            e->bfull.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)))
+            return -1;
+        g.con = e->con.as<double>(); g.hpl = e->hpl.as<double>();
+        g.Hll = e->Hll.as<double>(); g.bl = e->bl.as<double>();
+        g.Hpp = e->Hpp.as<double>(); g.bp = e->bp.as<double>();
+        g.Dinv = e->Dinv.as<double>(); g.Y = e->Y.as<double>(); g.w = e->w.as<double>();
+        g.slab = e->slab.as<double>(); g.Hs = e->Hs.as<double>(); g.bs = e->bs.as<double>();
+        g.x = e->x.as<double>();
+        if (hipMemsetAsync(g.Y, 0, sizeof(double) * kNP * (size_t)g.Kpad, s) != hipSuccess ||
+            hipMemsetAsync(g.w, 0, sizeof(double) * g.Kpad, s) != hipSuccess ||
+            hipMemsetAsync(g.slab, 0, sizeof(double) * (size_t)g.S * kNP * kNP, s) != hipSuccess ||
+            hipMemsetAsync(g.x, 0, sizeof(double) * (6 * A.P + 3 * A.Lm + 8), s) != hipSuccess)
+            return -1;
+        // trial buffers start equal to the current estimate (inactive vertices never change)
+        if (hipMemcpyAsync(g.T2, g.T, sizeof(Pose) * std::max(np, 1), hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(g.X2, g.X, sizeof(double) * 3 * std::max(nq, 1), hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return -1;
+        return 0;
+    };
+    ActiveSet A;
+    build_active(h, A);
+    if (setup(A)) return ORBX_EDEVICE;
+    r->iterations[0] = lba_optimize(e, g, A, 5, stop, &r->chi2[0]);
+    if (r->iterations[0] < -1) return ORBX_EINVAL;
+    const bool bDoMore = !(stop && *stop);
+    std::vector<uint8_t> flag(std::max(ne, 1));
+    if (bDoMore) {
+        lba_outliers<<<nblk(ne), 256, 0, s>>>(g.E, g.err, g.T, g.X, ne, e->flags.as<uint8_t>());
+        LBA_CHK(hipMemcpyAsync(flag.data(), e->flags.p, ne, hipMemcpyDeviceToHost, s));
+        LBA_CHK(hipStreamSynchronize(s));
+        for (int k = 0; k < ne; k++) {
+            if (flag[k]) h.level[k] = 1;
+            E[k].robust = 0;
+        }
+        if (upload(e->E, E, s)) return ORBX_EDEVICE;
+        g.E = e->E.as<EdgeDev>();
+        build_active(h, A);
+        if (setup(A)) return ORBX_EDEVICE;
+        r->iterations[1] = lba_optimize(e, g, A, 10, stop, &r->chi2[1]);
+    } else {
+        r->stopped = 1;
+    }
+    lba_outliers<<<nblk(ne), 256, 0, s>>>(g.E, g.err, g.T, g.X, ne, e->flags.as<uint8_t>());
+    LBA_CHK(hipGetLastError());
+    LBA_CHK(hipMemcpyAsync(r->edge_erase, e->flags.p, ne, hipMemcpyDeviceToHost, s));
+    LBA_CHK(hipMemcpyAsync(T.data(), g.T, sizeof(Pose) * np, hipMemcpyDeviceToHost, s));
+    LBA_CHK(hipMemcpyAsync(X.data(), g.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, s));
+    LBA_CHK(hipStreamSynchronize(s));
+    for (int i = 0; i < np; i++) {  // Converter::toCvMat(SE3Quat)
+        double R[9];
+        quat_to_R(T[i].q, R);
+        float *o = r->pose_Tcw + 16 * i;
+        for (int a = 0; a < 3; a++) {
+            for (int c = 0; c < 3; c++) o[4 * a + c] = (float)R[3 * a + c];
+            o[4 * a + 3] = (float)T[i].t[a];
+        }
+        o[12] = 0; o[13] = 0; o[14] = 0; o[15] = 1;
+    }
+    for (int i = 0; i < 3 * nq; i++) r->point_Xw[i] = (float)X[i];
+    return ORBX_OK;
+}
+
+}  // extern "C"

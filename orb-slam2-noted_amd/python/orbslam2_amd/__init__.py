@@ -67,6 +67,9 @@ SIGNATURES = [
     ("orbslam2_amd_device_sync", _I, []),
     ("orbslam2_amd_set_device", _I, [_I]),
     ("orbx_profile", _I, [_P, _I]),
+    ("lba_create", _I, [C.POINTER(C.c_void_p)]),
+    ("lba_destroy", None, [_P]),
+    ("lba_solve", _I, [_P, _P, _P, _P]),
     ("orbx_profile_read", _I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 ]
 
@@ -287,3 +290,64 @@ class ORBmatcher:
         sd = np.zeros(max(n, 1), np.int32)
         _check(lib().orbm_hamming_best2(_p(q), n, _p(db), len(db), _p(bi), _p(bd), _p(sd)), "orbm_hamming_best2")
         return bi[:n], bd[:n], sd[:n]
+
+
+class LbaProblem(C.Structure):
+    """lba_problem (include/orbslam2_amd.h): the graph Optimizer::LocalBundleAdjustment builds."""
+    _fields_ = [("n_poses", C.c_int32), ("pose_id", C.c_void_p), ("pose_fixed", C.c_void_p),
+                ("pose_Tcw", C.c_void_p), ("pose_cam", C.c_void_p), ("n_points", C.c_int32),
+                ("point_id", C.c_void_p), ("point_Xw", C.c_void_p), ("n_edges", C.c_int32),
+                ("edge_point", C.c_void_p), ("edge_pose", C.c_void_p), ("edge_obs", C.c_void_p),
+                ("edge_inv_sigma2", C.c_void_p)]
+
+
+class LbaResult(C.Structure):
+    _fields_ = [("pose_Tcw", C.c_void_p), ("point_Xw", C.c_void_p), ("edge_erase", C.c_void_p),
+                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2), ("stopped", C.c_int32)]
+
+
+_LBA_FIELDS = ("pose_id", "pose_fixed", "pose_Tcw", "pose_cam", "point_id", "point_Xw", "edge_point",
+               "edge_pose", "edge_obs", "edge_inv_sigma2")
+_LBA_DTYPES = {"pose_id": np.int32, "pose_fixed": np.uint8, "pose_Tcw": np.float32, "pose_cam": np.float32,
+               "point_id": np.int32, "point_Xw": np.float32, "edge_point": np.int32, "edge_pose": np.int32,
+               "edge_obs": np.float32, "edge_inv_sigma2": np.float32}
+
+
+class LocalBundleAdjustment:
+    """Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap) (Optimizer.h:112) on the GPU.
+
+    ``solve(problem)`` takes the flattened graph (see synth.localba_problem) and returns the
+    optimised poses (Tcw 4x4 float), points and the per-edge erase flags (vToErase)."""
+
+    def __init__(self):
+        self._h = C.c_void_p()
+        _check(lib().lba_create(C.byref(self._h)), "lba_create")
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().lba_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, prob: dict, stop: bool = False) -> dict:
+        keep = {k: np.ascontiguousarray(prob[k], _LBA_DTYPES[k]) for k in _LBA_FIELDS}
+        P = LbaProblem(len(keep["pose_id"]), keep["pose_id"].ctypes.data, keep["pose_fixed"].ctypes.data,
+                       keep["pose_Tcw"].ctypes.data, keep["pose_cam"].ctypes.data, len(keep["point_id"]),
+                       keep["point_id"].ctypes.data, keep["point_Xw"].ctypes.data, len(keep["edge_point"]),
+                       keep["edge_point"].ctypes.data, keep["edge_pose"].ctypes.data,
+                       keep["edge_obs"].ctypes.data, keep["edge_inv_sigma2"].ctypes.data)
+        out = {"pose_Tcw": np.zeros((len(keep["pose_id"]), 16), np.float32),
+               "point_Xw": np.zeros((len(keep["point_id"]), 3), np.float32),
+               "edge_erase": np.zeros(len(keep["edge_point"]), np.uint8)}
+        R = LbaResult(out["pose_Tcw"].ctypes.data, out["point_Xw"].ctypes.data, out["edge_erase"].ctypes.data)
+        flag = C.c_int32(1 if stop else 0)
+        _check(lib().lba_solve(self._h, C.byref(P), C.byref(R), C.byref(flag)), "lba_solve")
+        out["iterations"] = tuple(R.iterations)
+        out["chi2"] = tuple(R.chi2)
+        out["stopped"] = R.stopped
+        return out

@@ -115,3 +115,113 @@ def rgbd_frame(h: int, w: int, t: int, base_seed: int = 3) -> tuple[np.ndarray, 
     depth_u16[holes] = 0
     depth = (depth_u16.astype(np.float32) * np.float32(1.0 / 5000.0)).astype(np.float32)
     return gray, depth
+
+
+# ---------------------------------------------------------------------------------------
+# C4: synthetic LocalBundleAdjustment graph, after the homework simulator
+# pattern (orbslam_homework/hw4_answer/src/utils.cpp:35-69, demo/main.cpp:28-86):
+# 20 local KFs on a forward path 1 m apart with +-2 deg yaw (mnId 1..20, free) plus two fixed
+# cameras (mnId 0 and 21); 3000 points at 4-40 m, each seen by a contiguous run of 3..8 KFs;
+# 70 % stereo observations; octave ~ features per level, pixel noise sigma = scale[octave];
+# 5 % outliers (+-20 px); initial poses perturbed 0.5 deg / 5 cm, points 10 cm.
+# ---------------------------------------------------------------------------------------
+KITTI_CAM = (718.856, 718.856, 607.1928, 185.2157, 386.1448)   # Stereo/KITTI00-02.yaml
+
+
+def _rot_y(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+
+
+def _small_rot(rng, deg):
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    ang = np.deg2rad(deg) * rng.uniform(-1, 1)
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+
+
+def localba_problem(seed: int = 4, n_kf: int = 20, n_points: int = 3000, stereo_frac: float = 0.7,
+                    outlier_frac: float = 0.05, W: int = 1241, H: int = 376):
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = KITTI_CAM
+    scales = np.float32(1.2) ** np.arange(8, dtype=np.float32)
+    inv_sigma2 = (np.float32(1) / (scales * scales)).astype(np.float32)
+    feat = np.array([434, 362, 302, 251, 209, 175, 145, 122], np.float64)
+    oct_p = feat / feat.sum()
+    ids = list(range(0, n_kf + 2))                       # 0 = fixed, 1..n_kf free, n_kf+1 fixed
+    Rwc, Cw = [], []
+    for i in ids:
+        Rwc.append(_rot_y(np.deg2rad(rng.uniform(-2, 2))))
+        Cw.append(np.array([rng.normal(0, 0.05), rng.normal(0, 0.02), float(i)]))
+    Tcw_true = []
+    for R, C in zip(Rwc, Cw):
+        Rcw = R.T
+        T = np.eye(4)
+        T[:3, :3] = Rcw
+        T[:3, 3] = -Rcw @ C
+        Tcw_true.append(T)
+    pts, obs = [], []
+    for p in range(n_points):
+        k = int(rng.integers(3, 9))
+        first = int(rng.integers(1, n_kf - k + 2))
+        run = list(range(first, first + k))
+        if first == 1 and rng.random() < 0.5:
+            run = [0] + run
+        if run[-1] == n_kf and rng.random() < 0.5:
+            run = run + [n_kf + 1]
+        last = run[-1]
+        z = rng.uniform(4, 40)
+        u = rng.uniform(0.3 * W, 0.7 * W)
+        v = rng.uniform(0.3 * H, 0.7 * H)
+        Xc = np.array([(u - cx) / fx * z, (v - cy) / fy * z, z])
+        T = Tcw_true[last]
+        Xw = T[:3, :3].T @ (Xc - T[:3, 3])
+        pts.append(Xw)
+        for kf in run:
+            T = Tcw_true[kf]
+            Xc = T[:3, :3] @ Xw + T[:3, 3]
+            if Xc[2] <= 0.5:
+                continue
+            o = int(rng.choice(8, p=oct_p))
+            sig = float(scales[o])
+            uu = fx * Xc[0] / Xc[2] + cx + rng.normal(0, sig)
+            vv = fy * Xc[1] / Xc[2] + cy + rng.normal(0, sig)
+            uR = -1.0
+            if rng.random() < stereo_frac:
+                uR = uu - bf / Xc[2] + rng.normal(0, sig)
+            if rng.random() < outlier_frac:
+                du, dv = rng.uniform(-20, 20, 2)
+                uu += du
+                vv += dv
+                if uR >= 0:
+                    uR += du
+            obs.append((p, kf, uu, vv, uR, inv_sigma2[o]))
+    # perturbed initial estimates (what LocalBA starts from)
+    Tcw0 = []
+    for i, T in enumerate(Tcw_true):
+        T0 = T.copy()
+        if 1 <= i <= n_kf:
+            Rw = T[:3, :3].T @ _small_rot(rng, 0.5)
+            Cc = -T[:3, :3].T @ T[:3, 3] + rng.uniform(-0.05, 0.05, 3)
+            T0[:3, :3] = Rw.T
+            T0[:3, 3] = -Rw.T @ Cc
+        Tcw0.append(T0)
+    X0 = np.array(pts) + rng.uniform(-0.1, 0.1, (n_points, 3))
+    maxKFid = max(ids)
+    obs.sort(key=lambda o: (o[0], o[1]))                  # point list order, then KF order
+    ob = np.array(obs, dtype=np.float64)
+    return {
+        "pose_id": np.array(ids, np.int32),
+        "pose_fixed": np.array([1 if (i == 0 or i == n_kf + 1) else 0 for i in ids], np.uint8),
+        "pose_Tcw": np.array(Tcw0, np.float32).reshape(-1, 16),
+        "pose_cam": np.tile(np.array(KITTI_CAM, np.float32), (len(ids), 1)),
+        "point_id": (np.arange(n_points) + maxKFid + 1).astype(np.int32),
+        "point_Xw": X0.astype(np.float32),
+        "edge_point": ob[:, 0].astype(np.int32),
+        "edge_pose": ob[:, 1].astype(np.int32),
+        "edge_obs": ob[:, 2:5].astype(np.float32),
+        "edge_inv_sigma2": ob[:, 5].astype(np.float32),
+        "truth_Tcw": np.array(Tcw_true, np.float64),
+        "truth_Xw": np.array(pts, np.float64),
+    }

@@ -1,0 +1,55 @@
+"""GPU LocalBA (Optimizer::LocalBundleAdjustment, Optimizer.cc:646-1049) vs the CPU oracle.
+
+Tolerance (BASELINE.json north_star): poses and points within 1e-4 relative; the outlier
+set (vToErase) identical; same LM iteration counts.
+"""
+import numpy as np
+import pytest
+
+from orbslam2_amd import synth
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-12)
+
+
+@pytest.mark.parametrize("seed,n_kf,n_pts", [(4, 20, 3000), (5, 10, 800), (6, 20, 1500)])
+def test_lba_matches_oracle(amd, oracle_mod, seed, n_kf, n_pts):
+    prob = synth.localba_problem(seed=seed, n_kf=n_kf, n_points=n_pts)
+    ref = oracle_mod.lba_solve(prob)
+    got = amd.LocalBundleAdjustment().solve(prob)
+    print("iters", got["iterations"], ref["iterations"], "chi2", got["chi2"], ref["chi2"],
+          "erase diff", int((got["edge_erase"] != ref["edge_erase"]).sum()),
+          "pose rel", _rel(got["pose_Tcw"], ref["pose_Tcw"]), "pt rel", _rel(got["point_Xw"], ref["point_Xw"]))
+    assert got["iterations"] == ref["iterations"]
+    np.testing.assert_allclose(got["chi2"], ref["chi2"], rtol=1e-5)
+    assert _rel(got["pose_Tcw"], ref["pose_Tcw"]) < RTOL
+    assert _rel(got["point_Xw"], ref["point_Xw"]) < RTOL
+    # per point relative (scale-aware) check too
+    d = np.linalg.norm(got["point_Xw"] - ref["point_Xw"], axis=1)
+    n = np.linalg.norm(ref["point_Xw"], axis=1)
+    assert (d / n).max() < RTOL
+    assert np.array_equal(got["edge_erase"], ref["edge_erase"])
+
+
+def test_lba_stop_flag(amd, oracle_mod):
+    prob = synth.localba_problem(seed=7, n_kf=8, n_points=300)
+    got = amd.LocalBundleAdjustment().solve(prob, stop=True)
+    assert got["stopped"] == 1 and got["iterations"] == (0, 0)
+    assert np.array_equal(got["pose_Tcw"], prob["pose_Tcw"].reshape(-1, 16))
+    assert got["edge_erase"].sum() == 0
+
+
+def test_lba_mono_only_and_fixed(amd, oracle_mod):
+    prob = synth.localba_problem(seed=8, n_kf=12, n_points=1000, stereo_frac=0.0)
+    ref = oracle_mod.lba_solve(prob)
+    got = amd.LocalBundleAdjustment().solve(prob)
+    assert got["iterations"] == ref["iterations"]
+    assert _rel(got["pose_Tcw"], ref["pose_Tcw"]) < RTOL
+    assert _rel(got["point_Xw"], ref["point_Xw"]) < RTOL
+    assert np.array_equal(got["edge_erase"], ref["edge_erase"])
