@@ -150,11 +150,11 @@ typedef struct lba_engine lba_engine;
  * Optimizer.cc:646-1049) minus the map walk / write-back, which stay in the caller's
  * adapter: two Levenberg-Marquardt runs (5 iterations with Huber kernels, then 10 without
  * the outliers, optimization_algorithm_levenberg.cpp:61-164) with the Schur complement onto
- * the poses (block_solver.hpp:354-486) on the GPU. `stop` mirrors pbStopFlag: polled
+ * the poses (block_solver.hpp:354-486) on the GPU. `stop` is pbStopFlag itself (a C++ bool, read as one byte): polled
  * before each LM iteration and trial (sparse_optimizer.cpp:376, levenberg.cpp:149). */
 int lba_create(lba_engine **out);
 void lba_destroy(lba_engine *e);
-int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile int32_t *stop);
+int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile uint8_t *stop);
 
 /* -------- library / measurement -------- */
 const char *orbslam2_amd_version(void);

@@ -176,7 +176,7 @@ typedef struct {
     int P, Lm;            /* free active poses / active points */
     int *pose_hidx, *point_hidx; /* -1 if not in index mapping */
     int *hpose, *hpoint;  /* hessian index -> vertex */
-    const volatile int32_t *stop;
+    const volatile uint8_t *stop;
 } graph_t;
 
 static int terminate_flag(const graph_t *g) { return g->stop ? (*g->stop != 0) : 0; }
@@ -568,7 +568,7 @@ static int depth_positive(const graph_t *g, const edge_t *e) {
     return p[2] > 0.0;
 }
 
-int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile int32_t *stop) {
+int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint8_t *stop) {
     graph_t g;
     memset(&g, 0, sizeof(g));
     g.np = pr->n_poses; g.nq = pr->n_points; g.ne = pr->n_edges;

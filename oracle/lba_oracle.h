@@ -9,7 +9,7 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
-int lba_oracle_solve(const lba_problem *p, lba_result *r, const volatile int32_t *stop);
+int lba_oracle_solve(const lba_problem *p, lba_result *r, const volatile uint8_t *stop);
 #ifdef __cplusplus
 }
 #endif

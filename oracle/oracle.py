@@ -325,7 +325,7 @@ def lba_solve(prob: dict, stop: bool = False):
     L.lba_oracle_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     P, keep = make_lba_structs(prob)
     R, out = make_lba_result(prob)
-    flag = C.c_int32(1 if stop else 0)
+    flag = C.c_uint8(1 if stop else 0)
     L.lba_oracle_solve(C.byref(P), C.byref(R), C.byref(flag))
     out["iterations"] = tuple(R.iterations)
     out["chi2"] = tuple(R.chi2)

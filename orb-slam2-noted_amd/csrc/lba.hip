@@ -713,7 +713,7 @@ int nblk(int n) { return std::max(1, (n + 255) / 256); }
 
 // One SparseOptimizer::optimize(iterations) on the device; returns iterations run.
 static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterations,
-                        const volatile int32_t *stop, double *final_chi) {
+                        const volatile uint8_t *stop, double *final_chi) {
     hipStream_t s = e->stream;
     auto term = [&]() { return stop && *stop; };
     if (A.P + A.Lm == 0) return -1;
@@ -811,7 +811,7 @@ void lba_destroy(lba_engine *e) {
     delete e;
 }
 
-int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile int32_t *stop) {
+int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile uint8_t *stop) {
     if (!e || !p || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return ORBX_EINVAL;
     LBA_CHK(hipSetDevice(e->device));
     hipStream_t s = e->stream;

@@ -1,0 +1,150 @@
+// C++ host layer over the orbslam2_amd C-ABI, mirroring the reference classes the HIP path
+// replaces (same names, argument meaning and call order; OpenCV types swapped for PODs so
+// this header builds without OpenCV). INTEGRATION.md shows the cv::Mat adapters that drop
+// these into the reference tree unchanged for Tracking.cc / LocalMapping.cc.
+//
+//   orbslam2_amd::ORBextractor   <- ORB_SLAM2::ORBextractor (include/ORBextractor.h:80-216)
+//   orbslam2_amd::ORBmatcher     <- ORB_SLAM2::ORBmatcher   (include/ORBmatcher.h:57-65)
+//   orbslam2_amd::ComputeStereoMatches <- Frame::ComputeStereoMatches (Frame.cc:831-1128)
+//   orbslam2_amd::Optimizer::LocalBundleAdjustment <- Optimizer.h:112 (graph supplied flat)
+//
+// Error behaviour: the reference has no error path (it asserts / returns silently); a GPU
+// failure here throws std::runtime_error -- there is no CPU fallback.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "orbslam2_amd.h"
+
+namespace orbslam2_amd {
+
+using KeyPoint = orbx_kp;   // cv::KeyPoint memory layout: pt.x, pt.y, size, angle, response, octave, class_id
+
+struct ImageU8 {            // cv::Mat CV_8UC1 view
+    const uint8_t *data = nullptr;
+    int cols = 0, rows = 0;
+    int step = 0;           // bytes per row
+};
+
+inline void check(int rc, const char *what) {
+    if (rc != ORBX_OK) throw std::runtime_error(std::string("orbslam2_amd: ") + what + " failed (" + std::to_string(rc) + ")");
+}
+
+class ORBextractor {
+public:
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+        : nfeatures_(nfeatures), nlevels_(nlevels), scaleFactor_(scaleFactor) {
+        orbx_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, 0};
+        check(orbx_create(&p, &h_), "orbx_create");
+    }
+    ~ORBextractor() { orbx_destroy(h_); }
+    ORBextractor(const ORBextractor &) = delete;
+    ORBextractor &operator=(const ORBextractor &) = delete;
+
+    // operator()(image, mask, keypoints, descriptors): descriptors is N x 32 bytes, row i
+    // belongs to keypoints[i]. Empty image -> returns with outputs untouched (:1547).
+    void operator()(const ImageU8 &image, std::vector<KeyPoint> &keypoints, std::vector<uint8_t> &descriptors) {
+        if (!image.data || image.cols == 0 || image.rows == 0) return;
+        const int cap = 2 * nfeatures_ + 512;
+        keypoints.resize(cap);
+        descriptors.resize((size_t)cap * 32);
+        int n = 0;
+        check(orbx_extract(h_, image.data, image.cols, image.rows, image.step, keypoints.data(), descriptors.data(), cap, &n),
+              "orbx_extract");
+        keypoints.resize(n);
+        descriptors.resize((size_t)n * 32);
+    }
+
+    int GetLevels() const { return nlevels_; }
+    float GetScaleFactor() const { return scaleFactor_; }
+    std::vector<float> GetScaleFactors() const { return levels()[0]; }
+    std::vector<float> GetInverseScaleFactors() const { return levels()[1]; }
+    std::vector<float> GetScaleSigmaSquares() const { return levels()[2]; }
+    std::vector<float> GetInverseScaleSigmaSquares() const { return levels()[3]; }
+
+    // mvImagePyramid[level] (host copy of the device level)
+    std::vector<uint8_t> ImagePyramidLevel(int level, int *cols, int *rows) {
+        check(orbx_pyramid_level(h_, 0, level, nullptr, cols, rows), "orbx_pyramid_level");
+        std::vector<uint8_t> out((size_t)(*cols) * (*rows));
+        check(orbx_pyramid_level(h_, 0, level, out.data(), nullptr, nullptr), "orbx_pyramid_level");
+        return out;
+    }
+
+    orbx_engine *engine() const { return h_; }
+
+private:
+    std::vector<std::vector<float>> levels() const {
+        std::vector<std::vector<float>> v(4, std::vector<float>(nlevels_));
+        int L = 0;
+        check(orbx_levels(h_, &L, v[0].data(), v[1].data(), v[2].data(), v[3].data(), nullptr), "orbx_levels");
+        return v;
+    }
+    orbx_engine *h_ = nullptr;
+    int nfeatures_, nlevels_;
+    float scaleFactor_;
+};
+
+// Frame::ComputeStereoMatches over the frame whose left/right images were last extracted by
+// `left` / `right` (mvKeys = left keypoints, N = their count).
+inline void ComputeStereoMatches(ORBextractor &left, ORBextractor &right, int N, float mbf, float mb,
+                                 std::vector<float> &mvuRight, std::vector<float> &mvDepth) {
+    mvuRight.assign(N, -1.0f);
+    mvDepth.assign(N, -1.0f);
+    check(orbm_stereo_match(left.engine(), right.engine(), mbf, mb, mvuRight.data(), mvDepth.data(), N),
+          "orbm_stereo_match");
+}
+
+class ORBmatcher {
+public:
+    static const int TH_LOW = 50, TH_HIGH = 100, HISTO_LENGTH = 30;
+    explicit ORBmatcher(float nnratio = 0.6f, bool checkOri = true) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
+    // DescriptorDistance (ORBmatcher.cc:2123-2143)
+    static int DescriptorDistance(const uint8_t *a, const uint8_t *b) {
+        int d = 0;
+        for (int i = 0; i < 32; i++) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+        return d;
+    }
+    // brute-force best / second-best scan on the GPU
+    static void HammingBest2(const std::vector<uint8_t> &q, const std::vector<uint8_t> &db, std::vector<int> &best,
+                             std::vector<int> &bestDist, std::vector<int> &secondDist) {
+        const int nq = (int)(q.size() / 32), ndb = (int)(db.size() / 32);
+        best.resize(nq); bestDist.resize(nq); secondDist.resize(nq);
+        check(orbm_hamming_best2(q.data(), nq, db.data(), ndb, best.data(), bestDist.data(), secondDist.data()),
+              "orbm_hamming_best2");
+    }
+    float mfNNratio;
+    bool mbCheckOrientation;
+};
+
+// Optimizer::LocalBundleAdjustment minus the map walk: the caller flattens the local
+// keyframes / fixed keyframes / local map points / observations into lba_problem
+// (Optimizer.cc:646-898 order) and applies the result (SetPose / SetWorldPos /
+// EraseMapPointMatch, :977-1048).
+class Optimizer {
+public:
+    static lba_result LocalBundleAdjustment(const lba_problem &graph, bool *pbStopFlag, std::vector<float> &poseTcw,
+                                            std::vector<float> &pointXw, std::vector<uint8_t> &edgeErase) {
+        static thread_local LbaHandle lba;
+        poseTcw.resize((size_t)graph.n_poses * 16);
+        pointXw.resize((size_t)graph.n_points * 3);
+        edgeErase.resize(graph.n_edges);
+        lba_result r{};
+        r.pose_Tcw = poseTcw.data();
+        r.point_Xw = pointXw.data();
+        r.edge_erase = edgeErase.data();
+        static_assert(sizeof(bool) == 1, "pbStopFlag is passed to the C-ABI as one byte");
+        check(lba_solve(lba.h, &graph, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag)), "lba_solve");
+        return r;
+    }
+
+private:
+    struct LbaHandle {
+        lba_engine *h = nullptr;
+        LbaHandle() { check(lba_create(&h), "lba_create"); }
+        ~LbaHandle() { lba_destroy(h); }
+    };
+};
+
+}  // namespace orbslam2_amd

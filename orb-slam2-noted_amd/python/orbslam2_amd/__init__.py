@@ -345,7 +345,7 @@ class LocalBundleAdjustment:
                "point_Xw": np.zeros((len(keep["point_id"]), 3), np.float32),
                "edge_erase": np.zeros(len(keep["edge_point"]), np.uint8)}
         R = LbaResult(out["pose_Tcw"].ctypes.data, out["point_Xw"].ctypes.data, out["edge_erase"].ctypes.data)
-        flag = C.c_int32(1 if stop else 0)
+        flag = C.c_uint8(1 if stop else 0)
         _check(lib().lba_solve(self._h, C.byref(P), C.byref(R), C.byref(flag)), "lba_solve")
         out["iterations"] = tuple(R.iterations)
         out["chi2"] = tuple(R.chi2)

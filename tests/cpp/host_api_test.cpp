@@ -1,0 +1,94 @@
+// C++ host-layer driver (orb-slam2-noted_amd/host/orbslam2_amd.hpp) used by
+// tests/test_host_cpp_gpu.py: reads raw inputs written by the test, runs the reference-named
+// classes, writes raw outputs for comparison with the CPU oracle.
+//   host_api_test extract <img.u8> <w> <h> <nfeat> <out.bin>
+//   host_api_test stereo <left.u8> <right.u8> <w> <h> <nfeat> <mbf> <mb> <out.bin>
+//   host_api_test lba <problem.bin> <out.bin>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <vector>
+
+#include "orbslam2_amd.hpp"
+
+using namespace orbslam2_amd;
+
+static std::vector<uint8_t> read_file(const char *path) {
+    std::ifstream f(path, std::ios::binary);
+    return std::vector<uint8_t>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+template <class T> static void put(std::ofstream &o, const std::vector<T> &v) {
+    const int64_t n = (int64_t)v.size();
+    o.write((const char *)&n, 8);
+    o.write((const char *)v.data(), sizeof(T) * v.size());
+}
+
+int main(int argc, char **argv) {
+    try {
+        if (argc >= 7 && !strcmp(argv[1], "extract")) {
+            auto img = read_file(argv[2]);
+            const int w = atoi(argv[3]), h = atoi(argv[4]), nf = atoi(argv[5]);
+            ORBextractor ex(nf, 1.2f, 8, 20, 7);
+            std::vector<KeyPoint> kps;
+            std::vector<uint8_t> desc;
+            ex(ImageU8{img.data(), w, h, w}, kps, desc);
+            std::ofstream o(argv[6], std::ios::binary);
+            put(o, kps);
+            put(o, desc);
+            std::vector<float> sf = ex.GetScaleFactors();
+            put(o, sf);
+            return 0;
+        }
+        if (argc >= 10 && !strcmp(argv[1], "stereo")) {
+            auto L = read_file(argv[2]), R = read_file(argv[3]);
+            const int w = atoi(argv[4]), h = atoi(argv[5]), nf = atoi(argv[6]);
+            const float mbf = (float)atof(argv[7]), mb = (float)atof(argv[8]);
+            ORBextractor exL(nf, 1.2f, 8, 20, 7), exR(nf, 1.2f, 8, 20, 7);
+            std::vector<KeyPoint> kL, kR;
+            std::vector<uint8_t> dL, dR;
+            exL(ImageU8{L.data(), w, h, w}, kL, dL);   // Frame.cc:144-153 (two extractors)
+            exR(ImageU8{R.data(), w, h, w}, kR, dR);
+            std::vector<float> uR, depth;
+            ComputeStereoMatches(exL, exR, (int)kL.size(), mbf, mb, uR, depth);
+            std::ofstream o(argv[9], std::ios::binary);
+            put(o, uR);
+            put(o, depth);
+            return 0;
+        }
+        if (argc >= 4 && !strcmp(argv[1], "lba")) {
+            auto b = read_file(argv[2]);
+            const int32_t *hdr = (const int32_t *)b.data();
+            const int np = hdr[0], nq = hdr[1], ne = hdr[2];
+            const uint8_t *p = b.data() + 12;
+            lba_problem g{};
+            g.n_poses = np; g.n_points = nq; g.n_edges = ne;
+            g.pose_id = (const int32_t *)p; p += 4 * np;
+            g.pose_fixed = p; p += np; p += (4 - (np % 4)) % 4;
+            g.pose_Tcw = (const float *)p; p += 4 * 16 * np;
+            g.pose_cam = (const float *)p; p += 4 * 5 * np;
+            g.point_id = (const int32_t *)p; p += 4 * nq;
+            g.point_Xw = (const float *)p; p += 4 * 3 * nq;
+            g.edge_point = (const int32_t *)p; p += 4 * ne;
+            g.edge_pose = (const int32_t *)p; p += 4 * ne;
+            g.edge_obs = (const float *)p; p += 4 * 3 * ne;
+            g.edge_inv_sigma2 = (const float *)p;
+            bool stop = false;
+            std::vector<float> T, X;
+            std::vector<uint8_t> erase;
+            Optimizer::LocalBundleAdjustment(g, &stop, T, X, erase);
+            std::ofstream o(argv[3], std::ios::binary);
+            put(o, T);
+            put(o, X);
+            put(o, erase);
+            return 0;
+        }
+    } catch (const std::exception &e) {
+        std::cerr << e.what() << "\n";
+        return 2;
+    }
+    std::cerr << "usage: host_api_test extract|stereo|lba ...\n";
+    return 1;
+}
