@@ -77,11 +77,8 @@ def bench_localba(amd, args, dist, world, with_cpu):
     for _ in range(args.lba_steps):
         r = lba.solve(prob)
     dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    from orbslam2_amd import dist as odist
+    dt = odist.max_over_ranks(dt, "cuda", dist)
     res = {"localba_kf_per_s": round(world * args.lba_steps / dt, 3),
            "localba": {"ms_per_call": round(1000 * dt / args.lba_steps, 3), "edges": int(len(prob["edge_point"])),
                        "keyframes": 20, "map_points": 3000, "lm_iterations": list(r["iterations"]),
@@ -144,12 +141,11 @@ def main():
     import orbslam2_amd as amd
     amd.set_device(local_rank)
 
+    from orbslam2_amd import dist as odist
     B = args.batch
     # shared read-only state: ORB params + camera, broadcast once from rank 0 over RCCL
-    shared = torch.tensor([NFEAT, 1.2, 8, 20, 7, KITTI_BF, KITTI_FX, W, H], dtype=torch.float64, device="cuda")
-    if dist is not None:
-        dist.broadcast(shared, src=0)
-    nf, sf, nl, ith, mth, bf, fx, w, h = shared.tolist()
+    nf, sf, nl, ith, mth, bf, fx, w, h = odist.broadcast_shared(
+        [NFEAT, 1.2, 8, 20, 7, KITTI_BF, KITTI_FX, W, H] if rank == 0 else [0] * 9, "cuda", dist)
     mb = float(np.float32(bf) / np.float32(fx))
 
     pool = make_pool(args.pool, 2 + 100 * rank)
@@ -192,10 +188,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = ex.profile_read() if not args.no_profile else {}
     ex.profile(False)
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = odist.max_over_ranks(elapsed, "cuda", dist)
 
     # sanity: the batch produced keypoints and stereo matches
     k0, _ = ex.fetch(0)

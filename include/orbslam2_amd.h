@@ -141,7 +141,9 @@ typedef struct {
     uint8_t *edge_erase;         /* [n_edges] out: 1 = pair in vToErase (Optimizer.cc:977-1008) */
     int32_t iterations[2];       /* LM iterations run in optimize(5) / optimize(10) */
     double chi2[2];              /* active robust chi2 after each phase */
-    int32_t stopped;             /* 1 = *stop was set (early return / phase 2 skipped) */
+    int32_t stopped;             /* 2 = *stop set before optimising: early return, outputs =
+                                    inputs, nothing to write back (Optimizer.cc:902-904);
+                                    1 = set after phase 1: phase 2 skipped (:913-917) */
 } lba_result;
 
 typedef struct lba_engine lba_engine;

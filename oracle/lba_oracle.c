@@ -612,7 +612,7 @@ int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint
     res->stopped = 0;
     int rc = 0;
     if (stop && *stop) {                  /* Optimizer.cc:902-904: return before optimising */
-        res->stopped = 1;
+        res->stopped = 2;
         memcpy(res->pose_Tcw, pr->pose_Tcw, sizeof(float) * 16 * g.np);
         memcpy(res->point_Xw, pr->point_Xw, sizeof(float) * 3 * g.nq);
         memset(res->edge_erase, 0, g.ne);

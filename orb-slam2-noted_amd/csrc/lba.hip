@@ -820,7 +820,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     r->chi2[0] = r->chi2[1] = 0;
     r->stopped = 0;
     if (stop && *stop) {  // Optimizer.cc:902-904: return before optimising, nothing written back
-        r->stopped = 1;
+        r->stopped = 2;
         std::memcpy(r->pose_Tcw, p->pose_Tcw, sizeof(float) * 16 * np);
         std::memcpy(r->point_Xw, p->point_Xw, sizeof(float) * 3 * nq);
         std::memset(r->edge_erase, 0, ne);

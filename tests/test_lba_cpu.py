@@ -22,5 +22,5 @@ def test_lba_oracle_converges(oracle_mod):
 def test_lba_oracle_stop_flag(oracle_mod):
     prob = synth.localba_problem(seed=7, n_kf=8, n_points=300)
     r = oracle_mod.lba_solve(prob, stop=True)
-    assert r["stopped"] == 1
+    assert r["stopped"] == 2
     assert np.array_equal(r["pose_Tcw"], prob["pose_Tcw"].reshape(-1, 16))

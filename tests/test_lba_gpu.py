@@ -40,7 +40,7 @@ def test_lba_matches_oracle(amd, oracle_mod, seed, n_kf, n_pts):
 def test_lba_stop_flag(amd, oracle_mod):
     prob = synth.localba_problem(seed=7, n_kf=8, n_points=300)
     got = amd.LocalBundleAdjustment().solve(prob, stop=True)
-    assert got["stopped"] == 1 and got["iterations"] == (0, 0)
+    assert got["stopped"] == 2 and got["iterations"] == (0, 0)
     assert np.array_equal(got["pose_Tcw"], prob["pose_Tcw"].reshape(-1, 16))
     assert got["edge_erase"].sum() == 0
 
