@@ -97,6 +97,42 @@ def bench_localba(amd, args, dist, world, with_cpu):
     return res
 
 
+def bench_rgbd(amd, args, dist, world):
+    """C3: TUM-like RGB-D 640x480 stream, ORBextractor(1000) + UndistortKeyPoints +
+    ComputeStereoFromRGBD + SearchForInitialization(F_t-1, F_t, 100), frames resident in HBM."""
+    import torch
+    from orbslam2_amd import synth
+    from orbslam2_amd import dist as odist
+    T = args.rgbd_batch
+    K = [517.306408, 516.469215, 318.643040, 255.313989]
+    D = [0.262383, -0.953104, -0.005358, 0.002628, 1.163314]
+    pool = [synth.rgbd_frame(480, 640, t) for t in range(8)]
+    g = torch.from_numpy(np.stack([pool[t % 8][0] for t in range(T)])).cuda()
+    d = torch.from_numpy(np.stack([pool[t % 8][1] for t in range(T)])).cuda()
+    torch.cuda.synchronize()
+    ex = amd.BatchExtractor(1000)
+    ex.reserve(640, 480, T)
+
+    def step():
+        ex.extract_device(g.data_ptr(), T, 640, 480, 640, 640 * 480)
+        ex.rgbd_device(d.data_ptr(), 640 * 480, 640, K, D, 40.0)
+        ex.search_init_device(T - 1, 0, 1, 1, 1, K, D, 100, 0.9, True)
+
+    for _ in range(2):
+        step()
+    amd.device_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.rgbd_steps):
+        step()
+    amd.device_sync()
+    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    n, m, _ = ex.search_init_fetch(0)
+    return {"c3_rgbd_frames_per_s": round(world * T * args.rgbd_steps / dt, 2),
+            "c3": {"frames_per_step": T, "ms_per_step": round(1000 * dt / args.rgbd_steps, 3),
+                   "search_init_matches_pair0": int(n),
+                   "bytes_per_frame": 640 * 480 + 1000 * 60 + 1000 * 12}}
+
+
 def load_traffic(kernel: str, batch: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
     f = ROOT / "profiles" / "pmc_traffic.json"
@@ -125,6 +161,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--lba-steps", type=int, default=10, help="timed LocalBA calls (C4 graph)")
     ap.add_argument("--no-lba", action="store_true")
+    ap.add_argument("--rgbd-batch", type=int, default=256)
+    ap.add_argument("--rgbd-steps", type=int, default=10)
+    ap.add_argument("--no-rgbd", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -233,6 +272,8 @@ def main():
                            "traffic": traffic, "avg_launch_ms": round(tot / n, 4),
                            "algorithmic_bytes_per_launch": BYTES_PER_STEREO_FRAME * B}
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
+    if not args.no_rgbd:
+        out.update(bench_rgbd(amd, args, dist, world))
     if not args.no_lba:
         out.update(bench_localba(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -110,6 +110,34 @@ int orbm_stereo_fetch(orbx_engine *e, int pair, float *u_right, float *depth, in
 int orbm_hamming_best2(const uint8_t *q, int nq, const uint8_t *db, int ndb, int *best_idx,
                        int *best_d, int *second_d);
 
+/* -------- RGB-D frame + frame-to-frame matching (C3) -------- */
+
+/* Frame::UndistortKeyPoints (Frame.cc:725-776, cv::undistortPoints with K = {fx, fy, cx, cy}
+ * and dist = {k1, k2, p1, p2, k3}; k1 == 0 -> copy) + Frame::ComputeStereoFromRGBD
+ * (Frame.cc:1131-1169: depth read at the distorted keypoint, uR = xUn - mbf / d) for the
+ * last extraction of `e` (image 0). depth is the CV_32F depth map (metres), dpitch floats per
+ * row. Outputs mvKeysUn[n], mvuRight[n], mvDepth[n]. */
+int orbf_rgbd(orbx_engine *e, const float *depth, int dpitch, const float K[4], const float dist[5],
+              float mbf, orbx_kp *keys_un, float *u_right, float *depth_out, int n);
+/* Same for every image of the last device batch: depth image i at d_depth + i*depth_stride
+ * floats. Results stay on device (fetch with orbf_rgbd_fetch). */
+int orbf_rgbd_batch_device(orbx_engine *e, const float *d_depth, size_t depth_stride, int dpitch,
+                           const float K[4], const float dist[5], float mbf, void *stream);
+int orbf_rgbd_fetch(orbx_engine *e, int image, orbx_kp *keys_un, float *u_right, float *depth_out,
+                    int cap);
+
+/* ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+ * (ORBmatcher.h:169, ORBmatcher.cc:580-748) with ORBmatcher(nnratio, checkOri), over pairs of
+ * images of the last device batch: F1 = image f1_base + f1_step*p, F2 = f2_base + f2_step*p,
+ * using their undistorted keypoints (orbf_rgbd_batch_device) and the Frame grid of F2
+ * (Frame.cc:398-698, bounds from ComputeImageBounds with K/dist). vbPrevMatched starts at F1's
+ * undistorted keypoints (Tracking::MonocularInitialization). Greedy order kept exactly. */
+int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int f1_step, int f2_base,
+                                  int f2_step, const float K[4], const float dist[5], int window,
+                                  float nnratio, int check_ori, void *stream);
+int orbm_search_init_fetch(orbx_engine *e, int pair, int *matches12, float *prev_xy, int cap,
+                           int *nmatches);
+
 /* -------- local bundle adjustment (replaces Optimizer::LocalBundleAdjustment) -------- */
 
 /* The graph Optimizer::LocalBundleAdjustment (Optimizer.cc:646-898) builds from the map,

@@ -1,0 +1,493 @@
+// MI355X-native per-frame front end around the extractor (C3 config):
+//   * Frame::UndistortKeyPoints (Frame.cc:725-776; cv::undistortPoints) +
+//     Frame::ComputeStereoFromRGBD (Frame.cc:1131-1169)        -> rgbd_kernel
+//   * Frame grid (AssignFeaturesToGrid / PosInGrid / GetFeaturesInArea, Frame.cc:398-698)
+//     as a per-frame sorted (cell, index) key list             -> grid_sort_kernel
+//   * ORBmatcher::SearchForInitialization (ORBmatcher.cc:580-748) + ComputeThreeMaxima
+//     (:2076-2118): windowed candidates and Hamming distances are wave-parallel, the greedy
+//     claim / evict order of the reference is kept by walking F1 keypoints in index order
+//                                                              -> search_init_kernel
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "orb_device.h"
+#include "orb_engine.h"
+
+using namespace orbamd;
+
+#define FR_CHK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "orbslam2_amd: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return ORBX_EDEVICE;                                                    \
+        }                                                                           \
+    } while (0)
+
+namespace orbframe {
+
+constexpr int GRID_COLS = 64, GRID_ROWS = 48;   // Frame.h:55-60
+
+struct Camera {
+    double fx, fy, cx, cy;
+    double k[5];      // k1 k2 p1 p2 k3
+    int distorted;    // mDistCoef.at<float>(0) != 0
+    float mbf;
+};
+
+// cv::undistortPoints(src, dst, K, dist, noArray(), K): 5 fixed iterations in double
+__host__ __device__ inline void undistort_point(const Camera &c, float u, float v, float *uo, float *vo) {
+    const double ifx = 1. / c.fx, ify = 1. / c.fy;
+    double x = u, y = v;
+    x = (x - c.cx) * ifx;
+    y = (y - c.cy) * ify;
+    const double x0 = x, y0 = y;
+    for (int j = 0; j < 5; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = 1. / (1 + ((c.k[4] * r2 + c.k[1]) * r2 + c.k[0]) * r2);
+        const double deltaX = 2 * c.k[2] * x * y + c.k[3] * (r2 + 2 * x * x);
+        const double deltaY = c.k[2] * (r2 + 2 * y * y) + 2 * c.k[3] * x * y;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    *uo = (float)(c.fx * x + c.cx);
+    *vo = (float)(c.fy * y + c.cy);
+}
+
+// one thread per keypoint of every image in the batch
+__global__ __launch_bounds__(256) void rgbd_kernel(Camera cam, const orbx_kp *kps, const int *cnt, int cap,
+                                                   const float *depth, long long depth_stride, int dpitch,
+                                                   orbx_kp *kun, float *u_right, float *dep_out) {
+    const int i = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+    if (i >= cap) return;
+    const long long o = (long long)b * cap + i;
+    if (i >= cnt[b]) return;
+    orbx_kp kp = kps[o];
+    orbx_kp ku = kp;
+    if (cam.distorted) undistort_point(cam, kp.x, kp.y, &ku.x, &ku.y);
+    kun[o] = ku;
+    float uR = -1, dd = -1;
+    const float d = depth[(long long)b * depth_stride + (long long)(int)kp.y * dpitch + (int)kp.x];
+    if (d > 0) {
+        dd = d;
+        uR = ku.x - cam.mbf / d;
+    }
+    u_right[o] = uR;
+    dep_out[o] = dd;
+}
+
+struct GridParams {
+    float minX, maxX, minY, maxY, invW, invH;
+};
+
+// Per frame: keys (cell << 16 | index) of keypoints that fall in the grid, sorted -> the
+// candidate order of GetFeaturesInArea (ix, then iy, then insertion order).
+__global__ __launch_bounds__(256) void grid_sort_kernel(GridParams gp, const orbx_kp *kun, const int *cnt,
+                                                        int cap, int sort_cap, uint32_t *keys, int *nkeys) {
+    extern __shared__ uint32_t sk[];
+    const int b = blockIdx.x;
+    const int n = min(cnt[b], cap);
+    for (int i = threadIdx.x; i < sort_cap; i += 256) {
+        uint32_t key = 0xFFFFFFFFu;
+        if (i < n) {
+            const orbx_kp k = kun[(long long)b * cap + i];
+            const int px = (int)roundf((k.x - gp.minX) * gp.invW);   // PosInGrid (Frame.cc:682-698)
+            const int py = (int)roundf((k.y - gp.minY) * gp.invH);
+            if (!(px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS))
+                key = ((uint32_t)(px * GRID_ROWS + py) << 16) | (uint32_t)i;
+        }
+        sk[i] = key;
+    }
+    __syncthreads();
+    for (int k = 2; k <= sort_cap; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < sort_cap; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t x = sk[i], y = sk[ixj];
+                    const bool asc = (i & k) == 0;
+                    if (asc ? (x > y) : (x < y)) { sk[i] = y; sk[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    __shared__ int valid;
+    if (threadIdx.x == 0) valid = 0;
+    __syncthreads();
+    int mine = 0;
+    for (int i = threadIdx.x; i < sort_cap; i += 256) {
+        keys[(long long)b * sort_cap + i] = sk[i];
+        mine += sk[i] != 0xFFFFFFFFu;
+    }
+    atomicAdd(&valid, mine);
+    __syncthreads();
+    if (threadIdx.x == 0) nkeys[b] = valid;
+}
+
+__device__ inline int lower_bound_u32(const uint32_t *a, int n, uint32_t v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (a[m] < v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+__device__ inline int hamming32(const uint8_t *a, const uint8_t *b) {
+    const uint4 *pa = (const uint4 *)a, *pb = (const uint4 *)b;
+    const uint4 x0 = pa[0], x1 = pa[1], y0 = pb[0], y1 = pb[1];
+    return __popc(x0.x ^ y0.x) + __popc(x0.y ^ y0.y) + __popc(x0.z ^ y0.z) + __popc(x0.w ^ y0.w) +
+           __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
+}
+
+struct SearchArgs {
+    // F1 = image f1_base + f1_step * p, F2 = image f2_base + f2_step * p
+    int f1_base, f1_step, f2_base, f2_step;
+    const orbx_kp *kun;
+    const uint8_t *desc;
+    const int *cnt;
+    int cap, sort_cap;
+    const uint32_t *keys;   // grid-sorted keys per image
+    const int *nkeys;
+    GridParams gp;
+    float r, nnratio;
+    int check_ori;
+};
+
+// One wave per (F1, F2) pair. LDS: F2 sorted keys, vMatchedDistance, vnMatches21.
+__global__ __launch_bounds__(64) void search_init_kernel(SearchArgs a, float *prev_xy, int *m12, int *nmatch) {
+    extern __shared__ int lds[];
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int i1img = a.f1_base + a.f1_step * p, i2img = a.f2_base + a.f2_step * p;
+    const int N1 = min(a.cnt[i1img], a.cap), N2 = min(a.cnt[i2img], a.cap);
+    const int nk = a.nkeys[i2img];
+    uint32_t *sk = (uint32_t *)lds;
+    int *vMD = lds + a.sort_cap;
+    int *v21 = vMD + a.cap;
+    __shared__ int run_pre[65];
+    __shared__ int run_lo[64];
+    __shared__ int8_t bin_of[4096];
+    const uint32_t *gk = a.keys + (long long)i2img * a.sort_cap;
+    for (int i = lane; i < nk; i += 64) sk[i] = gk[i];
+    for (int i = lane; i < N2; i += 64) { vMD[i] = INT_MAX; v21[i] = -1; }
+    const orbx_kp *K1 = a.kun + (long long)i1img * a.cap, *K2 = a.kun + (long long)i2img * a.cap;
+    const uint8_t *D1 = a.desc + (long long)i1img * a.cap * 32, *D2 = a.desc + (long long)i2img * a.cap * 32;
+    float *pxy = prev_xy + (long long)p * a.cap * 2;
+    int *M12 = m12 + (long long)p * a.cap;
+    for (int i = lane; i < N1; i += 64) { M12[i] = -1; if (i < 4096) bin_of[i] = -1; }
+    __syncthreads();
+    int nmatches = 0;
+    const float r = a.r;
+    for (int i1 = 0; i1 < N1; i1++) {
+        const orbx_kp kp1 = K1[i1];
+        if (kp1.octave > 0) continue;
+        const float x = pxy[2 * i1], y = pxy[2 * i1 + 1];
+        // GetFeaturesInArea (Frame.cc:590-671) cell window
+        const int cMinX = (int)floorf((x - a.gp.minX - r) * a.gp.invW);
+        const int nMinCellX = max(0, cMinX);
+        if (nMinCellX >= GRID_COLS) continue;
+        const int nMaxCellX = min(GRID_COLS - 1, (int)ceilf((x - a.gp.minX + r) * a.gp.invW));
+        if (nMaxCellX < 0) continue;
+        const int nMinCellY = max(0, (int)floorf((y - a.gp.minY - r) * a.gp.invH));
+        if (nMinCellY >= GRID_ROWS) continue;
+        const int nMaxCellY = min(GRID_ROWS - 1, (int)ceilf((y - a.gp.minY + r) * a.gp.invH));
+        if (nMaxCellY < 0) continue;
+        const int nx = nMaxCellX - nMinCellX + 1;
+        int len = 0, lo = 0;
+        if (lane < nx) {
+            const int ix = nMinCellX + lane;
+            const uint32_t k0 = (uint32_t)(ix * GRID_ROWS + nMinCellY) << 16;
+            const uint32_t k1 = ((uint32_t)(ix * GRID_ROWS + nMaxCellY) << 16) | 0xFFFFu;
+            lo = lower_bound_u32(sk, nk, k0);
+            len = lower_bound_u32(sk, nk, k1 + 1u) - lo;
+            if (k1 == 0xFFFFFFFFu) len = nk - lo;
+        }
+        // exclusive prefix of run lengths over lanes
+        int incl = len;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += v;
+        }
+        run_pre[lane] = incl - len;
+        run_lo[lane] = lo;
+        if (lane == 63) run_pre[64] = incl;
+        __syncthreads();
+        const int total = run_pre[64];
+        unsigned long long best = ~0ull;   // (dist << 32) | candidate position
+        int bestcnt = 0;                   // how many candidates have the best distance
+        int second = INT_MAX;
+        // per-lane partial: best key, count of its distance, second distinct-or-dup
+        int ldist = INT_MAX, lcnt = 0, lsec = INT_MAX;
+        unsigned lpos = 0xFFFFFFFFu;
+        for (int base = 0; base < total; base += 64) {
+            const int c = base + lane;
+            if (c < total) {
+                int rr = 0;  // run containing c
+                int hi = min(nx, 64) - 1;
+                while (rr < hi) {
+                    const int m = (rr + hi + 1) >> 1;
+                    if (run_pre[m] <= c) rr = m; else hi = m - 1;
+                }
+                const int pos = run_lo[rr] + (c - run_pre[rr]);
+                const int i2 = (int)(sk[pos] & 0xFFFFu);
+                const orbx_kp kp2 = K2[i2];
+                const bool lvl_ok = !(kp2.octave < 0) && !(kp2.octave > 0);   // minLevel = maxLevel = 0
+                if (lvl_ok && fabsf(kp2.x - x) < r && fabsf(kp2.y - y) < r) {
+                    const int dist = hamming32(D1 + (long long)i1 * 32, D2 + (long long)i2 * 32);
+                    if (!(vMD[i2] <= dist)) {
+                        if (dist < ldist) { lsec = ldist == INT_MAX ? lsec : min(lsec, ldist); ldist = dist; lpos = (unsigned)c; lcnt = 1; }
+                        else if (dist == ldist) { lcnt++; lsec = min(lsec, dist); }
+                        else lsec = min(lsec, dist);
+                    }
+                }
+            }
+        }
+        // wave merge: best = min (dist, pos); second = min over the multiset minus best
+        for (int off = 32; off > 0; off >>= 1) {
+            const int od = __shfl_xor(ldist, off, 64), oc = __shfl_xor(lcnt, off, 64), os = __shfl_xor(lsec, off, 64);
+            const unsigned op = (unsigned)__shfl_xor((int)lpos, off, 64);
+            int nd, nc, ns;
+            unsigned np;
+            if (od < ldist || (od == ldist && op < lpos)) {
+                nd = od; np = op;
+            } else {
+                nd = ldist; np = lpos;
+            }
+            if (od == ldist) nc = oc + lcnt; else nc = od < ldist ? oc : lcnt;
+            ns = min(lsec, os);
+            if (od != ldist) ns = min(ns, max(od, ldist) == INT_MAX ? INT_MAX : max(od, ldist));
+            ldist = nd; lpos = np; lcnt = nc; lsec = ns;
+        }
+        (void)best; (void)bestcnt; (void)second;
+        const int bestDist = ldist;
+        const int bestDist2 = lcnt >= 2 ? ldist : lsec;
+        if (lane == 0 && bestDist != INT_MAX && bestDist <= 50 && bestDist < (float)bestDist2 * a.nnratio) {
+            int cc = (int)lpos;
+            int rr = 0, hi = min(nx, 64) - 1;
+            while (rr < hi) {
+                const int m = (rr + hi + 1) >> 1;
+                if (run_pre[m] <= cc) rr = m; else hi = m - 1;
+            }
+            const int bestIdx2 = (int)(sk[run_lo[rr] + (cc - run_pre[rr])] & 0xFFFFu);
+            if (v21[bestIdx2] >= 0) { M12[v21[bestIdx2]] = -1; nmatches--; }
+            M12[i1] = bestIdx2;
+            v21[bestIdx2] = i1;
+            vMD[bestIdx2] = bestDist;
+            nmatches++;
+            if (a.check_ori) {
+                float rot = kp1.angle - K2[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * (30 / 360.0f));
+                if (bin == 30) bin = 0;
+                if (i1 < 4096) bin_of[i1] = (int8_t)bin;
+            }
+        }
+        __syncthreads();
+    }
+    if (a.check_ori) {   // ComputeThreeMaxima over the acceptance events, prune other bins
+        __shared__ int hist[30];
+        if (lane < 30) hist[lane] = 0;
+        __syncthreads();
+        for (int i = lane; i < min(N1, 4096); i += 64)
+            if (bin_of[i] >= 0) atomicAdd(&hist[bin_of[i]], 1);
+        __syncthreads();
+        if (lane == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < 30; i++) {
+                const int s = hist[i];
+                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+                else if (s > max3) { max3 = s; ind3 = i; }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            for (int i = 0; i < min(N1, 4096); i++) {
+                const int bb = bin_of[i];
+                if (bb < 0 || bb == ind1 || bb == ind2 || bb == ind3) continue;
+                if (M12[i] >= 0) { M12[i] = -1; nmatches--; }
+            }
+        }
+        __syncthreads();
+    }
+    if (lane == 0) nmatch[p] = nmatches;
+    __syncthreads();
+    for (int i = lane; i < N1; i += 64)
+        if (M12[i] >= 0) { pxy[2 * i] = K2[M12[i]].x; pxy[2 * i + 1] = K2[M12[i]].y; }
+}
+
+__global__ __launch_bounds__(256) void init_prev_xy(const orbx_kp *kun, const int *cnt, int cap, int f1_base,
+                                                    int f1_step, float *prev_xy) {
+    const int i = blockIdx.x * 256 + threadIdx.x, p = blockIdx.y;
+    if (i >= cap) return;
+    const int img = f1_base + f1_step * p;
+    float *o = prev_xy + ((long long)p * cap + i) * 2;
+    if (i < cnt[img]) {
+        const orbx_kp k = kun[(long long)img * cap + i];
+        o[0] = k.x; o[1] = k.y;   // mvbPrevMatched[i] = mvKeysUn[i].pt (Tracking.cc)
+    }
+}
+
+static Camera make_camera(const float K[4], const float dist[5], float mbf) {
+    Camera c;
+    c.fx = K[0]; c.fy = K[1]; c.cx = K[2]; c.cy = K[3];
+    for (int i = 0; i < 5; i++) c.k[i] = dist[i];
+    c.distorted = dist[0] != 0.0f;
+    c.mbf = mbf;
+    return c;
+}
+
+// Frame::ComputeImageBounds (Frame.cc:780-830) + grid element inverses (Frame.cc:183-185)
+static GridParams make_grid(const Camera &c, int cols, int rows) {
+    GridParams g;
+    if (c.distorted) {
+        float u[4], v[4];
+        const float in[8] = {0.f, 0.f, (float)cols, 0.f, 0.f, (float)rows, (float)cols, (float)rows};
+        for (int i = 0; i < 4; i++) undistort_point(c, in[2 * i], in[2 * i + 1], &u[i], &v[i]);
+        g.minX = std::min(u[0], u[2]);
+        g.maxX = std::max(u[1], u[3]);
+        g.minY = std::min(v[0], v[1]);
+        g.maxY = std::max(v[2], v[3]);
+    } else {
+        g.minX = 0.0f; g.maxX = (float)cols; g.minY = 0.0f; g.maxY = (float)rows;
+    }
+    g.invW = (float)GRID_COLS / (g.maxX - g.minX);
+    g.invH = (float)GRID_ROWS / (g.maxY - g.minY);
+    return g;
+}
+
+}  // namespace orbframe
+
+using namespace orbframe;
+
+struct orbf_state {
+    DevBuf kun, uR, dep, keys, nkeys, prev, m12, nmatch, depth_in;
+};
+
+static orbf_state &fstate(orbx_engine *e) {
+    // per-engine frame buffers live in a side table keyed by engine pointer
+    static std::vector<std::pair<orbx_engine *, orbf_state *>> tab;
+    for (auto &t : tab) if (t.first == e) return *t.second;
+    tab.push_back({e, new orbf_state()});
+    return *tab.back().second;
+}
+
+extern "C" {
+
+int orbf_rgbd_batch_device(orbx_engine *e, const float *d_depth, size_t depth_stride, int dpitch,
+                           const float K[4], const float dist[5], float mbf, void *stream) {
+    if (!e || !d_depth || !K || !dist) return ORBX_EINVAL;
+    if (e->last_n < 1) return ORBX_ESTATE;
+    orbf_state &S = fstate(e);
+    const int cap = e->g.out_base[e->g.nlevels], n = e->last_n;
+    if (S.kun.ensure(sizeof(orbx_kp) * (size_t)n * cap) || S.uR.ensure(4 * (size_t)n * cap) || S.dep.ensure(4 * (size_t)n * cap))
+        return ORBX_EDEVICE;
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    const Camera cam = make_camera(K, dist, mbf);
+    int ph = prof_begin(e, s);
+    rgbd_kernel<<<dim3((cap + 255) / 256, n), 256, 0, s>>>(cam, e->d_kps.as<orbx_kp>(), e->d_cnt.as<int>(), cap, d_depth,
+                                                           (long long)depth_stride, dpitch, S.kun.as<orbx_kp>(),
+                                                           S.uR.as<float>(), S.dep.as<float>());
+    prof_end(e, s, ph, "rgbd_kernel");
+    FR_CHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbf_rgbd(orbx_engine *e, const float *depth, int dpitch, const float K[4], const float dist[5], float mbf,
+              orbx_kp *keys_un, float *u_right, float *depth_out, int n) {
+    if (!e || !depth || n < 0) return ORBX_EINVAL;
+    if (e->last_n < 1) return ORBX_ESTATE;
+    orbf_state &S = fstate(e);
+    if (S.depth_in.ensure(sizeof(float) * (size_t)dpitch * e->H)) return ORBX_EDEVICE;
+    FR_CHK(hipMemcpyAsync(S.depth_in.p, depth, sizeof(float) * (size_t)dpitch * e->H, hipMemcpyHostToDevice, e->stream));
+    int rc = orbf_rgbd_batch_device(e, S.depth_in.as<float>(), 0, dpitch, K, dist, mbf, e->stream);
+    if (rc) return rc;
+    FR_CHK(hipStreamSynchronize(e->stream));
+    int cnt = 0;
+    FR_CHK(hipMemcpy(&cnt, e->d_cnt.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (cnt != n) return ORBX_EINVAL;
+    if (n > 0) {
+        if (keys_un) FR_CHK(hipMemcpy(keys_un, S.kun.p, sizeof(orbx_kp) * n, hipMemcpyDeviceToHost));
+        if (u_right) FR_CHK(hipMemcpy(u_right, S.uR.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        if (depth_out) FR_CHK(hipMemcpy(depth_out, S.dep.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    }
+    return ORBX_OK;
+}
+
+int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int f1_step, int f2_base, int f2_step,
+                                  const float K[4], const float dist[5], int window, float nnratio, int check_ori,
+                                  void *stream) {
+    if (!e || n_pairs <= 0 || !K || !dist) return ORBX_EINVAL;
+    orbf_state &S = fstate(e);
+    if (!S.kun.p) return ORBX_ESTATE;  // needs orbf_rgbd*: undistorted keypoints
+    const int n = e->last_n, cap = e->g.out_base[e->g.nlevels];
+    if (f1_base + f1_step * (n_pairs - 1) >= n || f2_base + f2_step * (n_pairs - 1) >= n) return ORBX_EINVAL;
+    int sort_cap = 1;
+    while (sort_cap < cap) sort_cap <<= 1;
+    if (cap > 4096 || sort_cap > 4096) return ORBX_EINVAL;
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    const Camera cam = make_camera(K, dist, 0.f);
+    const GridParams gp = make_grid(cam, e->W, e->H);
+    if (S.keys.ensure(4 * (size_t)n * sort_cap) || S.nkeys.ensure(4 * (size_t)n) ||
+        S.prev.ensure(8 * (size_t)n_pairs * cap) || S.m12.ensure(4 * (size_t)n_pairs * cap) ||
+        S.nmatch.ensure(4 * (size_t)n_pairs))
+        return ORBX_EDEVICE;
+    int ph = prof_begin(e, s);
+    grid_sort_kernel<<<n, 256, 4 * sort_cap, s>>>(gp, S.kun.as<orbx_kp>(), e->d_cnt.as<int>(), cap, sort_cap,
+                                                  S.keys.as<uint32_t>(), S.nkeys.as<int>());
+    prof_end(e, s, ph, "grid_sort_kernel");
+    init_prev_xy<<<dim3((cap + 255) / 256, n_pairs), 256, 0, s>>>(S.kun.as<orbx_kp>(), e->d_cnt.as<int>(), cap, f1_base,
+                                                                  f1_step, S.prev.as<float>());
+    SearchArgs a;
+    a.f1_base = f1_base; a.f1_step = f1_step; a.f2_base = f2_base; a.f2_step = f2_step;
+    a.kun = S.kun.as<orbx_kp>();
+    a.desc = e->d_desc.as<uint8_t>();
+    a.cnt = e->d_cnt.as<int>();
+    a.cap = cap;
+    a.sort_cap = sort_cap;
+    a.keys = S.keys.as<uint32_t>();
+    a.nkeys = S.nkeys.as<int>();
+    a.gp = gp;
+    a.r = (float)window;
+    a.nnratio = nnratio;
+    a.check_ori = check_ori;
+    ph = prof_begin(e, s);
+    search_init_kernel<<<n_pairs, 64, 4 * (sort_cap + 2 * cap), s>>>(a, S.prev.as<float>(), S.m12.as<int>(),
+                                                                    S.nmatch.as<int>());
+    prof_end(e, s, ph, "search_init_kernel");
+    FR_CHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbm_search_init_fetch(orbx_engine *e, int pair, int *matches12, float *prev_xy, int cap, int *nmatches) {
+    if (!e) return ORBX_EINVAL;
+    orbf_state &S = fstate(e);
+    if (!S.m12.p) return ORBX_ESTATE;
+    const int kc = e->g.out_base[e->g.nlevels];
+    if (cap < kc) return ORBX_ECAP;
+    FR_CHK(hipDeviceSynchronize());
+    if (matches12) FR_CHK(hipMemcpy(matches12, S.m12.as<int>() + (size_t)pair * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
+    if (prev_xy) FR_CHK(hipMemcpy(prev_xy, S.prev.as<float>() + (size_t)pair * kc * 2, 8 * (size_t)kc, hipMemcpyDeviceToHost));
+    if (nmatches) FR_CHK(hipMemcpy(nmatches, S.nmatch.as<int>() + pair, 4, hipMemcpyDeviceToHost));
+    return ORBX_OK;
+}
+
+int orbf_rgbd_fetch(orbx_engine *e, int image, orbx_kp *keys_un, float *u_right, float *depth_out, int cap) {
+    if (!e) return ORBX_EINVAL;
+    orbf_state &S = fstate(e);
+    if (!S.kun.p) return ORBX_ESTATE;
+    const int kc = e->g.out_base[e->g.nlevels];
+    if (cap < kc) return ORBX_ECAP;
+    FR_CHK(hipDeviceSynchronize());
+    if (keys_un) FR_CHK(hipMemcpy(keys_un, S.kun.as<orbx_kp>() + (size_t)image * kc, sizeof(orbx_kp) * kc, hipMemcpyDeviceToHost));
+    if (u_right) FR_CHK(hipMemcpy(u_right, S.uR.as<float>() + (size_t)image * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
+    if (depth_out) FR_CHK(hipMemcpy(depth_out, S.dep.as<float>() + (size_t)image * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
+    return ORBX_OK;
+}
+
+}  // extern "C"

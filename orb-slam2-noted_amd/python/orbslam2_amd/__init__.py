@@ -67,6 +67,11 @@ SIGNATURES = [
     ("orbslam2_amd_device_sync", _I, []),
     ("orbslam2_amd_set_device", _I, [_I]),
     ("orbx_profile", _I, [_P, _I]),
+    ("orbf_rgbd", _I, [_P, _P, _I, _P, _P, _F, _P, _P, _P, _I]),
+    ("orbf_rgbd_batch_device", _I, [_P, _P, C.c_size_t, _I, _P, _P, _F, _P]),
+    ("orbf_rgbd_fetch", _I, [_P, _I, _P, _P, _P, _I]),
+    ("orbm_search_init_batch_device", _I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _F, _I, _P]),
+    ("orbm_search_init_fetch", _I, [_P, _I, _P, _P, _I, _P]),
     ("lba_create", _I, [C.POINTER(C.c_void_p)]),
     ("lba_destroy", None, [_P]),
     ("lba_solve", _I, [_P, _P, _P, _P]),
@@ -255,12 +260,53 @@ class BatchExtractor(ORBextractor):
         _check(lib().orbm_stereo_match_batch_device(self._h, n_pairs, mbf, mb, C.c_void_p(stream or 0)),
                "orbm_stereo_match_batch_device")
 
+    def rgbd_device(self, d_depth: int, depth_stride: int, dpitch: int, K, dist, mbf: float, stream=None):
+        Ka, Da = np.asarray(K, np.float32), np.asarray(dist, np.float32)
+        _check(lib().orbf_rgbd_batch_device(self._h, C.c_void_p(d_depth), depth_stride, dpitch, _p(Ka), _p(Da),
+                                            mbf, C.c_void_p(stream or 0)), "orbf_rgbd_batch_device")
+
+    def rgbd_fetch(self, image: int):
+        cap = max(64, self.nfeatures * 2 + 512)
+        ku = np.zeros(cap, KP_DTYPE)
+        u = np.zeros(cap, np.float32)
+        d = np.zeros(cap, np.float32)
+        _check(lib().orbf_rgbd_fetch(self._h, image, _p(ku), _p(u), _p(d), cap), "orbf_rgbd_fetch")
+        return ku, u, d
+
+    def search_init_device(self, n_pairs, f1_base, f1_step, f2_base, f2_step, K, dist, window=100,
+                           nnratio=0.9, check_ori=True, stream=None):
+        Ka, Da = np.asarray(K, np.float32), np.asarray(dist, np.float32)
+        _check(lib().orbm_search_init_batch_device(self._h, n_pairs, f1_base, f1_step, f2_base, f2_step, _p(Ka),
+                                                   _p(Da), window, nnratio, 1 if check_ori else 0,
+                                                   C.c_void_p(stream or 0)), "orbm_search_init_batch_device")
+
+    def search_init_fetch(self, pair: int):
+        cap = max(64, self.nfeatures * 2 + 512)
+        m = np.zeros(cap, np.int32)
+        xy = np.zeros(2 * cap, np.float32)
+        n = C.c_int()
+        _check(lib().orbm_search_init_fetch(self._h, pair, _p(m), _p(xy), cap, C.byref(n)), "orbm_search_init_fetch")
+        return n.value, m, xy.reshape(-1, 2)
+
     def stereo_fetch(self, pair: int):
         cap = max(64, self.nfeatures * 2 + 512)
         u = np.zeros(cap, np.float32)
         d = np.zeros(cap, np.float32)
         _check(lib().orbm_stereo_fetch(self._h, pair, _p(u), _p(d), cap), "orbm_stereo_fetch")
         return u, d
+
+
+def compute_stereo_from_rgbd(ex: ORBextractor, n: int, depth: np.ndarray, K, dist, mbf: float):
+    """UndistortKeyPoints + ComputeStereoFromRGBD for the extractor's last image ->
+    (mvKeysUn, mvuRight, mvDepth)."""
+    depth = np.ascontiguousarray(depth, np.float32)
+    Ka, Da = np.asarray(K, np.float32), np.asarray(dist, np.float32)
+    ku = np.zeros(max(n, 1), KP_DTYPE)
+    u = np.zeros(max(n, 1), np.float32)
+    d = np.zeros(max(n, 1), np.float32)
+    _check(lib().orbf_rgbd(ex.handle, _p(depth), depth.shape[1], _p(Ka), _p(Da), mbf, _p(ku), _p(u), _p(d), n),
+           "orbf_rgbd")
+    return ku[:n], u[:n], d[:n]
 
 
 def compute_stereo_matches(left: ORBextractor, right: ORBextractor, n_left: int, mbf: float, mb: float):

@@ -1,0 +1,72 @@
+"""GPU C3 path vs the CPU oracle: UndistortKeyPoints + ComputeStereoFromRGBD (Frame.cc:725-776,
+1131-1169) and SearchForInitialization over consecutive frames (ORBmatcher.cc:580-748) with
+the TUM1 camera (Examples/RGB-D/TUM1.yaml). Bit-exact keypoints / depths / match indices."""
+import numpy as np
+import pytest
+
+from orbslam2_amd import synth
+
+pytestmark = pytest.mark.gpu
+K_TUM = [517.306408, 516.469215, 318.643040, 255.313989]
+D_TUM = [0.262383, -0.953104, -0.005358, 0.002628, 1.163314]
+BF_TUM = 40.0
+
+
+def _oracle_frame(oracle_mod, gray, depth, K, D):
+    ex = oracle_mod.Extractor(1000)
+    k, d = ex.extract(gray)
+    if D[0] != 0:
+        xy = oracle_mod.undistort_points(np.stack([k["x"], k["y"]], 1), K, D)
+        ku = k.copy()
+        ku["x"], ku["y"] = xy[:, 0], xy[:, 1]
+    else:
+        ku = k.copy()
+    u, dep = oracle_mod.stereo_from_rgbd(k, ku, depth, BF_TUM)
+    return k, d, ku, u, dep
+
+
+@pytest.mark.parametrize("dist", [D_TUM, [0, 0, 0, 0, 0]])
+def test_rgbd_and_search_init(amd, oracle_mod, dist):
+    import torch
+    T = 4
+    frames = [synth.rgbd_frame(480, 640, t) for t in range(T)]
+    grays = np.stack([f[0] for f in frames])
+    depths = np.stack([f[1] for f in frames])
+    dg = torch.from_numpy(grays).cuda()
+    dd = torch.from_numpy(depths).cuda()
+    ex = amd.BatchExtractor(1000)
+    ex.reserve(640, 480, T)
+    torch.cuda.synchronize()
+    ex.extract_device(dg.data_ptr(), T, 640, 480, 640, 640 * 480)
+    ex.rgbd_device(dd.data_ptr(), 640 * 480, 640, K_TUM, dist, BF_TUM)
+    ex.search_init_device(T - 1, 0, 1, 1, 1, K_TUM, dist, 100, 0.9, True)
+    bounds = oracle_mod.image_bounds(640, 480, K_TUM, dist)
+    ref = [_oracle_frame(oracle_mod, grays[t], depths[t], K_TUM, dist) for t in range(T)]
+    for t in range(T):
+        k, d, ku, u, dep = ref[t]
+        gku, gu, gd = ex.rgbd_fetch(t)
+        n = len(k)
+        assert gku[:n].tobytes() == ku.tobytes(), f"keysUn frame {t}"
+        assert gu[:n].tobytes() == u.tobytes() and gd[:n].tobytes() == dep.tobytes(), f"depth frame {t}"
+    for p in range(T - 1):
+        k1, d1, ku1, _, _ = ref[p]
+        k2, d2, ku2, _, _ = ref[p + 1]
+        G1 = oracle_mod.Grid(ku1, d1, bounds)
+        G2 = oracle_mod.Grid(ku2, d2, bounds)
+        prev = np.stack([ku1["x"], ku1["y"]], 1)
+        nm, m12, prev_out = oracle_mod.search_for_initialization(G1, G2, prev, 100, 0.9, True)
+        gn, gm, gxy = ex.search_init_fetch(p)
+        n1 = len(k1)
+        assert nm > 20, "consecutive synthetic frames should match"
+        np.testing.assert_array_equal(gm[:n1], m12)
+        assert gn == nm
+        assert gxy[:n1].tobytes() == prev_out.tobytes()
+
+
+def test_rgbd_host_path(amd, oracle_mod):
+    gray, depth = synth.rgbd_frame(480, 640, 5)
+    ex = amd.ORBextractor(1000)
+    k, _ = ex(gray)
+    ku, u, d = amd.compute_stereo_from_rgbd(ex, len(k), depth, K_TUM, D_TUM, BF_TUM)
+    rk, rd, rku, ru, rdep = _oracle_frame(oracle_mod, gray, depth, K_TUM, D_TUM)
+    assert ku.tobytes() == rku.tobytes() and u.tobytes() == ru.tobytes() and d.tobytes() == rdep.tobytes()
