@@ -28,6 +28,7 @@ struct ExtractGeom {
     int lw[ORBX_MAXL], lh[ORBX_MAXL];
     long long pyr_off[ORBX_MAXL];   // level >= 1 offset inside an image's pyramid block
     long long blur_off[ORBX_MAXL];  // offset inside an image's blurred block (all levels)
+    int bp[ORBX_MAXL];              // blurred / strength-map row pitch (lw rounded up to 16)
     long long pyr_stride, blur_stride;
     int in_pitch;
     long long in_stride;
@@ -47,6 +48,7 @@ struct ExtractGeom {
     int ini_th, min_th, resize_mode;
     int rz_col_off[ORBX_MAXL], rz_row_off[ORBX_MAXL], rz_simd_end[ORBX_MAXL];
     int blur_tiles_x[ORBX_MAXL], blur_tiles_y[ORBX_MAXL], blur_tile_base[ORBX_MAXL + 1];
+    int nms_sm_words, nms_wave_words;  // per-wavefront LDS of the cell NMS kernel (u32 words)
 };
 
 struct DevBuf {
@@ -73,7 +75,7 @@ struct orbx_engine {
     orbamd::ExtractGeom g{};
     std::vector<orbamd::CellDesc> cells;
     // device buffers
-    orbamd::DevBuf d_cells, d_rz, d_pattern, d_in, d_pyr, d_blur, d_cell_cnt, d_cell_keys,
+    orbamd::DevBuf d_mmap, d_cells, d_rz, d_pattern, d_in, d_pyr, d_blur, d_cell_cnt, d_cell_keys,
         d_qt, d_qt_nodes, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt;
     // stereo
     orbamd::DevBuf d_st_sorted, d_st_res, d_st_u, d_st_depth, d_st_dist;

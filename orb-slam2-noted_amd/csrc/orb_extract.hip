@@ -91,148 +91,37 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 }
 
 // ------------------------------------------------------------------------------------
-// K2: per-cell FAST-9/16 with 3x3 NMS inside the cell ROI and the dual-threshold retry
-// (ORBextractor.cc:1084-1153 + cv::FAST). One wavefront per cell, ROI
-// staged in LDS. Keypoints are emitted row-major (the order cv::FAST pushes them).
+// K2: fused FAST strength map + GaussianBlur over 128x16 tiles of every level.
+//
+// cornerScore<16> (OpenCV fast_score.cpp) returns max(th, M) - 1 where
+//   M = max over the 16 circular 9-arcs of max(min_arc(v - ring), min_arc(ring - v)),
+// and the FAST-9 test at threshold th is exactly M > th (the pre-tests of
+// FAST_t are necessary conditions of the 9-arc test). M is therefore pixel-intrinsic: one
+// pass computes it once per pixel for both thresholds of the per-cell retry
+// (ORBextractor.cc:1122-1135), and the cell kernel (K2b) applies threshold, NMS and order.
+//
+// One 256-thread workgroup per tile, one 24x136 LDS halo tile (reflect-101) feeding both:
+//  1. staging: aligned dword loads + v_alignbyte (per-byte reflection only at edges);
+//  2. FAST pre-filter: every 9-arc holds two adjacent compass pixels (ring 0/4/8/12), so
+//     max over adjacent compass pairs of min(d) (darker) / min(-d) (brighter) bounds M
+//     from above; packed int16 pairs, 8 pixels per thread. Pixels whose bound exceeds
+//     the lower threshold join a per-wavefront candidate list (~12 % of the pixels of
+//     textured imagery; ~1.4 % are corners);
+//  3. exact M for the candidates only (v_min3/v_max3 9-arc windows) into an LDS strength
+//     tile; every other pixel stores 0 -- thr_score(0, th) == thr_score(M, th) for every
+//     M <= min(thresholds), so K2b sees the scores of the dense map;
+//  4. cv::GaussianBlur(9x9, sigma 2) of ORBextractor.cc:1617-1625 (bit-exact fixed-point
+//     path, SURVEY.md A.3 -- exact integer row sums, Q16 column sums, (acc + 2^15) >> 16):
+//     row pass with v_dot4_u32_u8 on byte quads, stored vertically pair-interleaved (rows
+//     2p, 2p+1 in one dword) so the column pass runs on v_dot2_u32_u16.
+// Blurred level and strength map use the row pitch g.bp[l] (16-byte aligned) so both are
+// written with dword / dwordx2 stores.
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ bool has9(uint32_t m) {
-    uint32_t m32 = m | (m << 16);
-    uint32_t t = m32 & (m32 >> 1);
-    t &= t >> 2;
-    t &= t >> 4;
-    t &= m32 >> 8;
-    return (t & 0xFFFFu) != 0;
-}
+#define FB_TW 128
+#define FB_TH 16
+#define FB_LW (FB_TW + 8)   // LDS tile row bytes
+#define FB_LD (FB_LW / 4)   // LDS tile row dwords
 
-// cornerScore<16> (OpenCV fast_score.cpp), d[k] = v - ring[k].
-__device__ __forceinline__ int corner_score16(const int *d, int threshold) {
-    int a0 = threshold;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int a = min(d[k + 1], d[k + 2]);
-        a = min(a, d[k + 3]);
-        if (a <= a0) continue;
-        a = min(a, d[k + 4]);
-        a = min(a, d[k + 5]);
-        a = min(a, d[k + 6]);
-        a = min(a, d[k + 7]);
-        a = min(a, d[k + 8]);
-        a0 = max(a0, min(a, d[k]));
-        a0 = max(a0, min(a, d[k + 9]));
-    }
-    int b0 = -a0;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int b = max(d[k + 1], d[k + 2]);
-        b = max(b, d[k + 3]);
-        b = max(b, d[k + 4]);
-        b = max(b, d[k + 5]);
-        if (b >= b0) continue;
-        b = max(b, d[k + 6]);
-        b = max(b, d[k + 7]);
-        b = max(b, d[k + 8]);
-        b0 = min(b0, max(b, d[k]));
-        b0 = min(b0, max(b, d[k + 9]));
-    }
-    return -b0 - 1;
-}
-
-__device__ __forceinline__ int fast_pixel_score(const uint8_t *t, int i, int j, int th) {
-    // ring offsets (dx, dy) of OpenCV's offsets16, extended to 25 by wrapping
-    const int8_t RX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-    const int8_t RY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-    const int v = t[i * ORBX_TMAX + j];
-    int d[25];
-    uint32_t dk = 0, br = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        int p = t[(i + RY[k]) * ORBX_TMAX + j + RX[k]];
-        d[k] = v - p;
-        dk |= (uint32_t)(p < v - th) << k;
-        br |= (uint32_t)(p > v + th) << k;
-    }
-    if (!has9(dk) && !has9(br)) return 0;
-#pragma unroll
-    for (int k = 16; k < 25; k++) d[k] = d[k - 16];
-    return corner_score16(d, th) & 0xFF;  // stored as uchar (fast.cpp curr[j])
-}
-
-__global__ __launch_bounds__(64) void fast_cells_kernel(ExtractGeom g, const CellDesc *cells,
-                                                        const uint8_t *in, const uint8_t *pyr,
-                                                        int *cell_cnt, uint32_t *cell_keys) {
-    __shared__ uint8_t tile[ORBX_TMAX * ORBX_TMAX];
-    __shared__ uint8_t score[ORBX_TMAX * ORBX_TMAX];
-    const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
-    const CellDesc cd = cells[c];
-    int pitch;
-    const uint8_t *img = level_ptr(g, in, pyr, b, cd.level, &pitch);
-    const int rh = cd.rh, rw = cd.rw;
-    const uint8_t *src = img + (long long)cd.r0 * pitch + cd.c0;
-    for (int i = lane; i < rh * rw; i += 64) {
-        const int r = i / rw, cc = i - r * rw;
-        tile[r * ORBX_TMAX + cc] = src[(long long)r * pitch + cc];
-    }
-    const int dh = rh - 6, dwid = rw - 6;
-    const int ndet = (dh > 0 && dwid > 0) ? dh * dwid : 0;
-    int th = g.ini_th;
-    int total = 0;
-    for (int pass = 0; pass < 2; pass++) {
-        th = min(max(th, 0), 255);
-        for (int i = lane; i < ORBX_TMAX * ORBX_TMAX; i += 64) score[i] = 0;
-        __syncthreads();
-        for (int idx = lane; idx < ndet; idx += 64) {
-            const int i = 3 + idx / dwid, j = 3 + idx % dwid;
-            score[i * ORBX_TMAX + j] = (uint8_t)fast_pixel_score(tile, i, j, th);
-        }
-        __syncthreads();
-        total = 0;
-        for (int base = 0; base < ndet; base += 64) {
-            const int idx = base + lane;
-            bool keep = false;
-            if (idx < ndet) {
-                const int i = 3 + idx / dwid, j = 3 + idx % dwid;
-                const uint8_t *s = score + i * ORBX_TMAX + j;
-                const int v = s[0];
-                keep = v > s[1] && v > s[-1] && v > s[-ORBX_TMAX - 1] && v > s[-ORBX_TMAX] &&
-                       v > s[-ORBX_TMAX + 1] && v > s[ORBX_TMAX - 1] && v > s[ORBX_TMAX] &&
-                       v > s[ORBX_TMAX + 1];
-            }
-            total += __popcll(__ballot(keep));
-        }
-        if (total > 0) break;
-        th = g.min_th;
-    }
-    uint32_t *out = cell_keys + ((long long)b * g.ncell_total + c) * g.cell_cap;
-    int written = 0;
-    if (total > 0) {
-        for (int base = 0; base < ndet; base += 64) {
-            const int idx = base + lane;
-            bool keep = false;
-            int i = 0, j = 0, v = 0;
-            if (idx < ndet) {
-                i = 3 + idx / dwid;
-                j = 3 + idx % dwid;
-                const uint8_t *s = score + i * ORBX_TMAX + j;
-                v = s[0];
-                keep = v > s[1] && v > s[-1] && v > s[-ORBX_TMAX - 1] && v > s[-ORBX_TMAX] &&
-                       v > s[-ORBX_TMAX + 1] && v > s[ORBX_TMAX - 1] && v > s[ORBX_TMAX] &&
-                       v > s[ORBX_TMAX + 1];
-            }
-            const unsigned long long m = __ballot(keep);
-            const int rank = __popcll(m & ((1ull << lane) - 1ull));
-            if (keep && written + rank < g.cell_cap)
-                out[written + rank] = pack_key(j + cd.offx, i + cd.offy, v);
-            written += __popcll(m);
-        }
-    }
-    if (lane == 0) cell_cnt[(long long)b * g.ncell_total + c] = min(written, g.cell_cap);
-}
-
-// ------------------------------------------------------------------------------------
-// K3: cv::GaussianBlur(9x9, sigma 2, REFLECT_101) on each level (ORBextractor.cc:1617-1625;
-// bit-exact fixed-point path). 64x16 output tiles, (16+8)x(64+8) LDS halo,
-// exact integer row sums then Q16 column sums.
-// ------------------------------------------------------------------------------------
 __device__ __forceinline__ int refl101(int i, int n) {
     if (n == 1) return 0;
     while (i < 0 || i >= n) {
@@ -242,44 +131,318 @@ __device__ __forceinline__ int refl101(int i, int n) {
     return i;
 }
 
-__global__ __launch_bounds__(256) void blur_kernel(ExtractGeom g, const uint8_t *in,
-                                                   const uint8_t *pyr, uint8_t *blur) {
-    __shared__ uint8_t tin[24][72];
-    __shared__ int trow[24][64];
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 vmin2(s16x2 a, s16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ s16x2 vmax2(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
+
+// bytes j, j+1 of the little-endian 16-byte segment w[0..3], zero-extended into int16 lanes
+__device__ __forceinline__ s16x2 byte_pair(const uint32_t *w, int j) {
+    const int k = j & 3, d = j >> 2;
+    const uint32_t r = k < 3 ? __builtin_amdgcn_perm(0u, w[d], 0x0c000c00u | ((uint32_t)(k + 1) << 16) | (uint32_t)k)
+                             : __builtin_amdgcn_perm(w[d + 1], w[d], 0x0c040c03u);
+    return __builtin_bit_cast(s16x2, r);
+}
+
+// dword of image bytes [x, x+4) of row `rowp` (x .. x+3 inside the row) from aligned loads
+__device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *pa = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t lo = pa[0];
+    const uint32_t hi = sh ? pa[1] : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// order LDS traffic between lanes of one wavefront (LDS executes a wave's ops in order)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long bal) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+}
+
+__global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
+                                                        uint8_t *blur, uint8_t *mmap) {
+    __shared__ uint32_t tin[(FB_TH + 8) * FB_LD];
+    __shared__ uint32_t trowp[((FB_TH + 8) / 2) * FB_TW];
+    __shared__ uint32_t mt[FB_TH * FB_TW / 4];
+    __shared__ uint16_t clist[4][512];
     const int b = blockIdx.y;
     int t = blockIdx.x, l = 0;
     while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
     t -= g.blur_tile_base[l];
     const int tx = t % g.blur_tiles_x[l], ty = t / g.blur_tiles_x[l];
-    const int w = g.lw[l], h = g.lh[l];
-    const int x0 = tx * 64, y0 = ty * 16;
+    const int w = g.lw[l], h = g.lh[l], bp = g.bp[l];
+    const int x0 = tx * FB_TW, y0 = ty * FB_TH;
     int pitch;
     const uint8_t *src = level_ptr(g, in, pyr, b, l, &pitch);
-    for (int i = threadIdx.x; i < 24 * 72; i += 256) {
-        const int r = i / 72, cc = i % 72;
-        const int sy = refl101(y0 + r - 4, h), sx = refl101(x0 + cc - 4, w);
-        tin[r][cc] = src[(long long)sy * pitch + sx];
+    // 1. stage rows y0-4 .. y0+19, cols x0-4 .. x0+131
+    for (int i = threadIdx.x; i < (FB_TH + 8) * FB_LD; i += 256) {
+        const int rr = i / FB_LD, j = i - rr * FB_LD;
+        const uint8_t *rowp = src + (long long)refl101(y0 + rr - 4, h) * pitch;
+        const int xs = x0 - 4 + 4 * j;
+        uint32_t v;
+        if (xs >= 0 && xs + 3 < w) {
+            v = load_u32_unaligned(rowp + xs);
+        } else {
+            v = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) v |= (uint32_t)rowp[refl101(xs + e, w)] << (8 * e);
+        }
+        tin[i] = v;
     }
     __syncthreads();
-    const int K[9] = {7, 17, 32, 46, 52, 46, 32, 17, 7};
-    for (int i = threadIdx.x; i < 24 * 64; i += 256) {
-        const int r = i / 64, cc = i % 64;
-        int acc = 0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;  // pixels (y0 + r, x0 + cb + i)
+    const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
+    const int tlo = min(th_a, th_b);
+    // 2. FAST pre-filter
+    int ncand = 0;
+    {
+        uint32_t S[4], C[4], N[4];  // tile cols cb .. cb+15 (image x0+cb-4 .. x0+cb+11)
 #pragma unroll
-        for (int k = 0; k < 9; k++) acc += K[k] * tin[r][cc + k];
-        trow[r][cc] = acc;
+        for (int k = 0; k < 4; k++) {
+            N[k] = tin[(r + 1) * FB_LD + (cb >> 2) + k];
+            C[k] = tin[(r + 4) * FB_LD + (cb >> 2) + k];
+            S[k] = tin[(r + 7) * FB_LD + (cb >> 2) + k];
+        }
+        const s16x2 th1 = {(short)(tlo + 1), (short)(tlo + 1)};
+        uint32_t cand = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const s16x2 c = byte_pair(C, 4 + 2 * q);
+            const s16x2 d0 = c - byte_pair(S, 4 + 2 * q);    // ring 0  (0, +3)
+            const s16x2 d4 = c - byte_pair(C, 7 + 2 * q);    // ring 4  (+3, 0)
+            const s16x2 d8 = c - byte_pair(N, 4 + 2 * q);    // ring 8  (0, -3)
+            const s16x2 d12 = c - byte_pair(C, 1 + 2 * q);   // ring 12 (-3, 0)
+            const s16x2 a = vmax2(vmax2(vmin2(d0, d4), vmin2(d4, d8)), vmax2(vmin2(d8, d12), vmin2(d12, d0)));
+            const s16x2 bb = vmin2(vmin2(vmax2(d0, d4), vmax2(d4, d8)), vmin2(vmax2(d8, d12), vmax2(d12, d0)));
+            const uint32_t u = __builtin_bit_cast(uint32_t, vmax2(a, -bb) - th1);  // lane >= 0 <=> bound > tlo
+            cand |= (((~u >> 15) & 1u) | ((~u >> 30) & 2u)) << (2 * q);
+        }
+        const int y = y0 + r, xb = x0 + cb;
+        if (y < 3 || y >= h - 3) cand = 0;
+        const int lo = max(3 - xb, 0), hi = min(w - 3 - xb, 8);
+        cand &= hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+        mt[r * (FB_TW / 4) + (cb >> 2)] = 0u;
+        mt[r * (FB_TW / 4) + (cb >> 2) + 1] = 0u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const bool f = (cand >> i) & 1u;
+            const unsigned long long bal = __ballot(f);
+            if (f) clist[wv][ncand + lane_rank(bal)] = (uint16_t)((r << 7) | (cb + i));
+            ncand += __popcll(bal);
+        }
+    }
+    // 4a. blur row pass: tile rows (2p, 2p+1) x output cols 4cg .. 4cg+3
+    {
+        const uint32_t K0123 = 7u | 17u << 8 | 32u << 16 | 46u << 24;
+        const uint32_t K4567 = 52u | 46u << 8 | 32u << 16 | 17u << 24;
+        for (int task = threadIdx.x; task < ((FB_TH + 8) / 2) * (FB_TW / 4); task += 256) {
+            const int p = task / (FB_TW / 4), cg = task % (FB_TW / 4);
+            uint32_t o[2][4];
+#pragma unroll
+            for (int rr = 0; rr < 2; rr++) {
+                const uint32_t *row = tin + (2 * p + rr) * FB_LD + cg;
+                const uint32_t D0 = row[0], D1 = row[1], D2 = row[2];
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    const uint32_t Wa = s ? __builtin_amdgcn_alignbyte(D1, D0, s) : D0;
+                    const uint32_t Wb = s ? __builtin_amdgcn_alignbyte(D2, D1, s) : D1;
+                    uint32_t acc = __builtin_amdgcn_udot4(Wa, K0123, 0u, false);
+                    acc = __builtin_amdgcn_udot4(Wb, K4567, acc, false);
+                    o[rr][s] = __builtin_amdgcn_udot4(D2, 7u << (8 * s), acc, false);
+                }
+            }
+            uint4 v;
+            v.x = o[0][0] | o[1][0] << 16;
+            v.y = o[0][1] | o[1][1] << 16;
+            v.z = o[0][2] | o[1][2] << 16;
+            v.w = o[0][3] | o[1][3] << 16;
+            *(uint4 *)&trowp[p * FB_TW + 4 * cg] = v;
+        }
     }
     __syncthreads();
-    uint8_t *dst = blur + (long long)b * g.blur_stride + g.blur_off[l];
-    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
-        const int r = i / 64, cc = i % 64;
-        const int y = y0 + r, x = x0 + cc;
-        if (y >= h || x >= w) continue;
-        uint32_t acc = 0;
+    // 3. exact M for this wavefront's candidates
+    {
+        const uint8_t *t8 = (const uint8_t *)tin;
+        uint8_t *m8 = (uint8_t *)mt;
+        const int RX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+        const int RY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+        for (int base = 0; base < ncand; base += 64) {
+            if (base + lane < ncand) {
+                const int e = clist[wv][base + lane];
+                const int rr = e >> 7, cx = e & 127;
+                const uint8_t *pc = t8 + (rr + 4) * FB_LW + cx + 4;
+                const int v = pc[0];
+                int d[16];
 #pragma unroll
-        for (int k = 0; k < 9; k++) acc += (uint32_t)K[k] * (uint32_t)trow[r + k][cc];
-        dst[(long long)y * w + x] = (uint8_t)min((int)((acc + 32768u) >> 16), 255);
+                for (int k = 0; k < 16; k++) d[k] = v - (int)pc[RY[k] * FB_LW + RX[k]];
+                int n3[16], x3[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    n3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+                    x3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+                }
+                int A = -256, Bm = 256;
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    A = max(A, min(min(n3[k], n3[(k + 3) & 15]), n3[(k + 6) & 15]));    // darker 9-arc
+                    Bm = min(Bm, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15])); // brighter 9-arc
+                }
+                m8[rr * FB_TW + cx] = (uint8_t)max(max(A, -Bm), 0);
+            }
+        }
     }
+    // 4b. blur column pass: output rows 2rp, 2rp+1 x cols 4cg .. 4cg+3
+    {
+        const int rp = threadIdx.x >> 5, cg = threadIdx.x & 31;
+        uint4 P[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) P[k] = *(const uint4 *)&trowp[(rp + k) * FB_TW + 4 * cg];
+        const uint32_t KE[5] = {7u | 17u << 16, 32u | 46u << 16, 52u | 46u << 16, 32u | 17u << 16, 7u};
+        const uint32_t KO[5] = {7u << 16, 17u | 32u << 16, 46u | 52u << 16, 46u | 32u << 16, 17u | 7u << 16};
+        uint32_t be = 0, bo = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            uint32_t ae = 32768u, ao = 32768u;
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const uint32_t pv = c == 0 ? P[k].x : c == 1 ? P[k].y : c == 2 ? P[k].z : P[k].w;
+                ae = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, pv), __builtin_bit_cast(u16x2, KE[k]), ae, false);
+                ao = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, pv), __builtin_bit_cast(u16x2, KO[k]), ao, false);
+            }
+            be |= (ae >> 16) << (8 * c);
+            bo |= (ao >> 16) << (8 * c);
+        }
+        uint8_t *dst = blur + (long long)b * g.blur_stride + g.blur_off[l];
+        const int x = x0 + 4 * cg;
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int y = y0 + 2 * rp + e;
+            const uint32_t val = e ? bo : be;
+            if (y >= h || x >= w) continue;
+            uint8_t *o = dst + (long long)y * bp + x;
+            if (x + 3 < w) {
+                *(uint32_t *)o = val;
+            } else {
+                for (int k = 0; k < w - x; k++) o[k] = (uint8_t)(val >> (8 * k));
+            }
+        }
+    }
+    wave_lds_sync();
+    // strength map rows (written by this wavefront's lanes above)
+    {
+        const int y = y0 + r, x = x0 + cb;
+        if (y < h && x < w) {
+            uint8_t *o = mmap + (long long)b * g.blur_stride + g.blur_off[l] + (long long)y * bp + x;
+            const uint32_t m0 = mt[r * (FB_TW / 4) + (cb >> 2)], m1 = mt[r * (FB_TW / 4) + (cb >> 2) + 1];
+            if (x + 7 < w) {
+                *(uint2 *)o = make_uint2(m0, m1);
+            } else {
+                for (int k = 0; k < w - x; k++) o[k] = (uint8_t)((k < 4 ? m0 : m1) >> (8 * (k & 3)));
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// K2b: per-cell threshold + 3x3 NMS + row-major emission on the strength map
+// (ORBextractor.cc:1084-1153 with cv::FAST's per-ROI semantics): score = M > th ? M - 1 : 0
+// inside the cell's detection region [3, rh-3) x [3, rw-3), 0 outside (neighbours in the
+// adjacent cell never suppress), retry at minThFAST when the cell is empty at iniThFAST.
+// One wavefront per cell, four cells per workgroup. The region is staged with dword loads;
+// the few pixels with M > min(thresholds) are compacted in row-major order (ballot ranks),
+// and only those run the 3x3 test at both thresholds.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int thr_score(int m, int th) { return m > th ? m - 1 : 0; }
+
+#define NMS_P 68   // LDS row pitch of the staged region (bytes)
+
+__global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const CellDesc *cells, const uint8_t *mmap,
+                                                       int *cell_cnt, uint32_t *cell_keys) {
+    extern __shared__ uint32_t nms_lds[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c = blockIdx.x * 4 + wv, b = blockIdx.y;
+    if (c >= g.ncell_total) return;
+    uint32_t *sm32 = nms_lds + wv * g.nms_wave_words;
+    uint8_t *sm = (uint8_t *)sm32;
+    uint16_t *lst = (uint16_t *)(sm32 + g.nms_sm_words);
+    const CellDesc cd = cells[c];
+    const int l = cd.level, bp = g.bp[l];
+    const int dh = cd.rh - 6, dwid = cd.rw - 6;
+    const int ndet = (dh > 0 && dwid > 0) ? dh * dwid : 0;
+    // region rows r0+2 .. r0+rh-3, cols c0+2 .. c0+rw-3 (detection region + 1); sm(0,0) = (r0+2, c0+2)
+    const uint8_t *base = mmap + (long long)b * g.blur_stride + g.blur_off[l] + (long long)(cd.r0 + 2) * bp + cd.c0 + 2;
+    const int qw = (dwid + 2 + 3) >> 2;
+    for (int i = lane; i < (dh + 2) * qw && ndet > 0; i += 64) {
+        const int rr = i / qw, j = i - rr * qw;
+        sm32[rr * (NMS_P / 4) + j] = load_u32_unaligned(base + (long long)rr * bp + 4 * j);
+    }
+    wave_lds_sync();
+    // zero the one-pixel frame: neighbours outside the detection region score 0
+    for (int i = lane; i < 2 * (dwid + 2) + 2 * dh && ndet > 0; i += 64) {
+        int rr, cc;
+        if (i < dwid + 2) { rr = 0; cc = i; }
+        else if (i < 2 * (dwid + 2)) { rr = dh + 1; cc = i - (dwid + 2); }
+        else { const int k = i - 2 * (dwid + 2); rr = 1 + (k >> 1); cc = (k & 1) ? dwid + 1 : 0; }
+        sm[rr * NMS_P + cc] = 0;
+    }
+    const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
+    const int tlo = min(th_a, th_b);
+    wave_lds_sync();
+    int nl = 0;
+    for (int b0 = 0; b0 < ndet; b0 += 64) {
+        const int idx = b0 + lane;
+        bool f = false;
+        if (idx < ndet) {
+            const int i = idx / dwid, j = idx - i * dwid;
+            f = sm[(i + 1) * NMS_P + j + 1] > tlo;
+        }
+        const unsigned long long bal = __ballot(f);
+        if (f) lst[nl + lane_rank(bal)] = (uint16_t)idx;
+        nl += __popcll(bal);
+    }
+    wave_lds_sync();
+    auto keep_at = [&](int idx, int th, int *score) {
+        const int i = idx / dwid, j = idx - i * dwid;
+        const uint8_t *s = sm + (i + 1) * NMS_P + j + 1;
+        const int v = thr_score(s[0], th);
+        *score = v;
+        return v > thr_score(s[1], th) && v > thr_score(s[-1], th) && v > thr_score(s[-NMS_P - 1], th) &&
+               v > thr_score(s[-NMS_P], th) && v > thr_score(s[-NMS_P + 1], th) && v > thr_score(s[NMS_P - 1], th) &&
+               v > thr_score(s[NMS_P], th) && v > thr_score(s[NMS_P + 1], th);
+    };
+    int total = 0;
+    for (int b0 = 0; b0 < nl; b0 += 64) {
+        int v;
+        const bool k = b0 + lane < nl && keep_at(lst[b0 + lane], th_a, &v);
+        total += __popcll(__ballot(k));
+    }
+    const int th = total > 0 ? th_a : th_b;
+    uint32_t *out = cell_keys + ((long long)b * g.ncell_total + c) * g.cell_cap;
+    int written = 0;
+    for (int b0 = 0; b0 < nl; b0 += 64) {
+        int v = 0, idx = 0;
+        bool k = false;
+        if (b0 + lane < nl) {
+            idx = lst[b0 + lane];
+            k = keep_at(idx, th, &v);
+        }
+        const unsigned long long m = __ballot(k);
+        const int rank = (int)lane_rank(m);
+        if (k && written + rank < g.cell_cap) {
+            const int i = idx / dwid, j = idx - i * dwid;
+            out[written + rank] = pack_key(j + 3 + cd.offx, i + 3 + cd.offy, v);
+        }
+        written += __popcll(m);
+    }
+    if (lane == 0) cell_cnt[(long long)b * g.ncell_total + c] = min(written, g.cell_cap);
 }
 
 // ------------------------------------------------------------------------------------
@@ -727,7 +890,7 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
     float sa, ca;
     glibc_sincosf(angle * factorPI, &sa, &ca);
     const float a = ca, bs = sa;
-    const int bw = g.lw[l];
+    const int bw = g.bp[l];
     const uint8_t *bc = blur + (long long)b * g.blur_stride + g.blur_off[l] + (long long)y * bw + x;
     unsigned long long words[4];
 #pragma unroll
@@ -846,8 +1009,9 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             if (g.lw[l] < 40 || g.lh[l] < 40) return ORBX_EINVAL;
             g.pyr_off[l] = l == 0 ? 0 : pyr;
             if (l > 0) pyr += ((long long)g.lw[l] * g.lh[l] + 63) & ~63LL;
+            g.bp[l] = (g.lw[l] + 15) & ~15;
             g.blur_off[l] = blur;
-            blur += ((long long)g.lw[l] * g.lh[l] + 63) & ~63LL;
+            blur += ((long long)g.bp[l] * g.lh[l] + 63) & ~63LL;
             g.scale[l] = e->scale[l];
             g.scaled_patch[l] = (int)(31 * e->scale[l]);
         }
@@ -899,6 +1063,13 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             (void)ncl;
         }
         g.cell_base[L] = (int)e->cells.size();
+        int max_rh = 0, max_det = 0;
+        for (const CellDesc &cd : e->cells) {
+            max_rh = std::max(max_rh, (int)cd.rh);
+            max_det = std::max(max_det, std::max(cd.rh - 6, 0) * std::max(cd.rw - 6, 0));
+        }
+        g.nms_sm_words = std::max(max_rh - 4, 1) * (NMS_P / 4);
+        g.nms_wave_words = (g.nms_sm_words + (max_det + 1) / 2 + 3) & ~3;
         g.ncell_total = g.cell_base[L];
         g.cell_cap = cell_cap;
         g.out_base[0] = 0;
@@ -950,8 +1121,8 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         // blur tiles
         g.blur_tile_base[0] = 0;
         for (int l = 0; l < L; l++) {
-            g.blur_tiles_x[l] = (g.lw[l] + 63) / 64;
-            g.blur_tiles_y[l] = (g.lh[l] + 15) / 16;
+            g.blur_tiles_x[l] = (g.lw[l] + FB_TW - 1) / FB_TW;
+            g.blur_tiles_y[l] = (g.lh[l] + FB_TH - 1) / FB_TH;
             g.blur_tile_base[l + 1] = g.blur_tile_base[l] + g.blur_tiles_x[l] * g.blur_tiles_y[l];
         }
         if (e->d_cells.ensure(sizeof(CellDesc) * e->cells.size())) return ORBX_EDEVICE;
@@ -963,6 +1134,7 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
     }
     const long long B = max_images;
     if (e->d_pyr.ensure(B * g.pyr_stride) || e->d_blur.ensure(B * g.blur_stride) ||
+        e->d_mmap.ensure(B * g.blur_stride) ||
         e->d_cell_cnt.ensure(sizeof(int) * B * g.ncell_total) ||
         e->d_cell_keys.ensure(sizeof(uint32_t) * B * g.ncell_total * g.cell_cap) ||
         e->d_qt.ensure(sizeof(uint32_t) * B * g.qt_off[g.nlevels]) ||
@@ -991,12 +1163,13 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     }
     prof_end(e, s, ph, "resize_level_kernel");
     ph = prof_begin(e, s);
-    fast_cells_kernel<<<dim3(g.ncell_total, n), 64, 0, s>>>(g, e->d_cells.as<CellDesc>(), d_imgs, pyr,
-                                                          e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
-    prof_end(e, s, ph, "fast_cells_kernel");
+    fast_blur_kernel<<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
+                                                                   e->d_mmap.as<uint8_t>());
+    prof_end(e, s, ph, "fast_blur_kernel");
     ph = prof_begin(e, s);
-    blur_kernel<<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>());
-    prof_end(e, s, ph, "blur_kernel");
+    fast_nms_kernel<<<dim3((g.ncell_total + 3) / 4, n), 256, 16 * (size_t)g.nms_wave_words, s>>>(g, e->d_cells.as<CellDesc>(), e->d_mmap.as<uint8_t>(),
+                                                        e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
+    prof_end(e, s, ph, "fast_nms_kernel");
     ph = prof_begin(e, s);
     size_t lds = 8 * (size_t)ORBX_QT_KL;
     if (g.qt_nodes_in_lds) lds += 2 * sizeof(QNode) * g.node_cap + 16 * (size_t)g.node_pow2;
@@ -1060,7 +1233,7 @@ void orbx_destroy(orbx_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    orbamd::DevBuf *bufs[] = {&e->d_cells, &e->d_rz, &e->d_pattern, &e->d_in, &e->d_pyr, &e->d_blur,
+    orbamd::DevBuf *bufs[] = {&e->d_mmap, &e->d_cells, &e->d_rz, &e->d_pattern, &e->d_in, &e->d_pyr, &e->d_blur,
                               &e->d_cell_cnt, &e->d_cell_keys, &e->d_qt, &e->d_qt_nodes, &e->d_sel,
                               &e->d_sel_cnt, &e->d_kps, &e->d_desc, &e->d_cnt, &e->d_st_sorted,
                               &e->d_st_res, &e->d_st_u, &e->d_st_depth, &e->d_st_dist};
