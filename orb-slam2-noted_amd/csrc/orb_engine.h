@@ -11,7 +11,6 @@
 #define ORBX_MAXL 16
 #define ORBX_TMAX 66          // max FAST cell ROI side (hCell + 6, wCell + 6)
 #define ORBX_QT_THREADS 256   // quadtree workgroup
-#define ORBX_QT_KL 4096       // per-workgroup LDS key capacity (x2 ping-pong)
 
 namespace orbamd {
 
@@ -43,6 +42,7 @@ struct ExtractGeom {
     int node_pow2;                     // next pow2 >= node_cap
     long long qt_node_stride;          // u32 words of global node scratch per (image, level)
     int qt_nodes_in_lds;
+    int qt_kl;                         // LDS key capacity (candidates) of the quadtree workgroup
     float scale[ORBX_MAXL];
     int scaled_patch[ORBX_MAXL];
     int ini_th, min_th, resize_mode;

@@ -462,86 +462,83 @@ __global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const Cell
 // ------------------------------------------------------------------------------------
 struct QNode {
     int16_t x0, y0, x1, y1;
-    int s;      // segment start | buffer bit << 30
+    int s;      // segment start in the current key buffer
     int n;      // key count
     int id;     // creation id
 };
 
-__device__ __forceinline__ int qnode_start(const QNode &q) { return q.s & 0x3FFFFFFF; }
-__device__ __forceinline__ int qnode_buf(const QNode &q) { return (q.s >> 30) & 1; }
+// per-node scratch of one split round
+// quadrant counters: 4 x u32 fields in two u64 (q0 | q1 << 32, q2 | q3 << 32); plain u64
+// adds never carry across fields for counts < 2^32
+struct QCnt {
+    unsigned long long a, b;
+    __device__ QCnt &operator+=(const QCnt &o) { a += o.a; b += o.b; return *this; }
+    __device__ QCnt operator-(const QCnt &o) const { return {a - o.a, b - o.b}; }
+    __device__ QCnt operator+(const QCnt &o) const { return {a + o.a, b + o.b}; }
+    __device__ int f(int k) const { return (int)(uint32_t)((k < 2 ? a : b) >> (32 * (k & 1))); }
+};
+__device__ __forceinline__ QCnt qone(int k) {
+    const unsigned long long v = 1ull << (32 * (k & 1));
+    return k < 2 ? QCnt{v, 0ull} : QCnt{0ull, v};
+}
+
+// per-node scratch of one split round
+struct QTmp {
+    QCnt pstart, pend;   // quadrant prefix at the node's segment start / end
+    int16_t cm[4];       // child k: >= 0 next-round node, < 0 leaf -> outrec[-1 - cm]
+    int keep;            // -1 divided; else next-array index of the node kept undivided
+    int pad;
+};
+
+__device__ __forceinline__ void qnode_mid(const QNode &q, int *mx, int *my) {
+    *mx = q.x0 + ((q.x1 - q.x0 + 1) >> 1);   // x0 + ceil((x1 - x0) / 2), DivideNode :612-613
+    *my = q.y0 + ((q.y1 - q.y0 + 1) >> 1);
+}
 
 __device__ __forceinline__ int quadrant(uint32_t k, int midx, int midy) {
     return (key_x(k) >= midx ? 1 : 0) + (key_y(k) >= midy ? 2 : 0);
 }
 
 struct QShared {
-    int live, next_id, n_out, n_next, n_act, prev_size, cross;
-    int tot[4];
-    int root_cnt[64], root_start[64], root_fill[64];
+    int live, next_id, n_out, n_next, n_act, cross, lim_mu;
+    int root_cnt[64], root_start[64], root_fill[64], root_node[64], root_out[64];
     int wcnt[4][64];
-    int scan[ORBX_QT_THREADS];
+    QCnt wsum[2][4];
 };
 
-// block-wide exclusive scan of one int per thread; returns exclusive prefix, *total = sum
-__device__ __forceinline__ int block_excl_scan(QShared &S, int v, int *total) {
-    const int tid = threadIdx.x;
-    S.scan[tid] = v;
+// block-wide exclusive scan of one value per thread; two LDS slots alternate so
+// back-to-back scans need one barrier each
+__device__ __forceinline__ unsigned long long shfl_up64(unsigned long long v, int off) { return __shfl_up(v, off, 64); }
+
+__device__ __forceinline__ QCnt block_scan(QShared &S, QCnt v, QCnt *total, int &par) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    QCnt incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const QCnt t{shfl_up64(incl.a, off), shfl_up64(incl.b, off)};
+        if (lane >= off) incl += t;
+    }
+    if (lane == 63) S.wsum[par][wv] = incl;
     __syncthreads();
-    for (int off = 1; off < ORBX_QT_THREADS; off <<= 1) {
-        int add = tid >= off ? S.scan[tid - off] : 0;
-        __syncthreads();
-        S.scan[tid] += add;
-        __syncthreads();
+    QCnt base{0ull, 0ull}, tot{0ull, 0ull};
+#pragma unroll
+    for (int w = 0; w < ORBX_QT_THREADS / 64; w++) {
+        const QCnt s = S.wsum[par][w];
+        if (w < wv) base += s;
+        tot += s;
     }
-    const int incl = S.scan[tid];
-    *total = S.scan[ORBX_QT_THREADS - 1];
-    __syncthreads();
-    return incl - v;
+    par ^= 1;
+    *total = tot;
+    return base + incl - v;
 }
 
-// counts of the four children of node q (no writes)
-__device__ __forceinline__ void qnode_counts(const QNode &q, uint32_t *const K[2], int c[4]) {
-    const int hx = (int)ceilf((float)(q.x1 - q.x0) / 2);
-    const int hy = (int)ceilf((float)(q.y1 - q.y0) / 2);
-    const int midx = q.x0 + hx, midy = q.y0 + hy;
-    const uint32_t *src = K[qnode_buf(q)] + qnode_start(q);
-    c[0] = c[1] = c[2] = c[3] = 0;
-    for (int i = 0; i < q.n; i++) c[quadrant(src[i], midx, midy)]++;
-}
-
-// DivideNode (:610-682): stable 4-way partition into the other buffer, children boxes
-__device__ __forceinline__ void qnode_divide(const QNode &q, uint32_t *const K[2], int c[4],
-                                             QNode ch[4]) {
-    const int hx = (int)ceilf((float)(q.x1 - q.x0) / 2);
-    const int hy = (int)ceilf((float)(q.y1 - q.y0) / 2);
-    const int midx = q.x0 + hx, midy = q.y0 + hy;
-    const int s = qnode_start(q), bsrc = qnode_buf(q), bdst = bsrc ^ 1;
-    const uint32_t *src = K[bsrc] + s;
-    uint32_t *dst = K[bdst] + s;
-    c[0] = c[1] = c[2] = c[3] = 0;
-    for (int i = 0; i < q.n; i++) c[quadrant(src[i], midx, midy)]++;
-    int pos[4] = {0, c[0], c[0] + c[1], c[0] + c[1] + c[2]};
-    for (int k = 0; k < 4; k++) {
-        ch[k].s = (s + pos[k]) | (bdst << 30);
-        ch[k].n = c[k];
-    }
-    for (int i = 0; i < q.n; i++) {
-        const uint32_t k = src[i];
-        dst[pos[quadrant(k, midx, midy)]++] = k;
-    }
-    ch[0].x0 = q.x0; ch[0].y0 = q.y0; ch[0].x1 = (int16_t)midx; ch[0].y1 = (int16_t)midy;
-    ch[1].x0 = (int16_t)midx; ch[1].y0 = q.y0; ch[1].x1 = q.x1; ch[1].y1 = (int16_t)midy;
-    ch[2].x0 = q.x0; ch[2].y0 = (int16_t)midy; ch[2].x1 = (int16_t)midx; ch[2].y1 = q.y1;
-    ch[3].x0 = (int16_t)midx; ch[3].y0 = (int16_t)midy; ch[3].x1 = q.x1; ch[3].y1 = q.y1;
-}
-
-// first key with maximal response (strict >, :1028-1036)
-__device__ __forceinline__ uint32_t qnode_best(const QNode &q, uint32_t *const K[2]) {
-    const uint32_t *src = K[qnode_buf(q)] + qnode_start(q);
-    uint32_t best = src[0];
-    for (int i = 1; i < q.n; i++)
-        if (key_score(src[i]) > key_score(best)) best = src[i];
-    return best;
+// scalar form (one u64 lane)
+__device__ __forceinline__ unsigned long long block_scan64(QShared &S, unsigned long long v,
+                                                           unsigned long long *total, int &par) {
+    QCnt tot;
+    const QCnt r = block_scan(S, QCnt{v, 0ull}, &tot, par);
+    *total = tot.a;
+    return r.a;
 }
 
 // bitonic sort of n (pow2) u64 values, descending
@@ -561,63 +558,170 @@ __device__ void block_sort_desc(unsigned long long *a, int n) {
     }
 }
 
-// One split round over `na` nodes taken from cur[] in the given order (perm: optional
-// index list; reverse: process cur[na-1-t]). limit = number of leading nodes (in processing
-// order) that are actually divided; the rest are left as leftovers. Children with one key
-// go to outrec (leaf), multi-key children to nxt[] in creation order.
-__device__ void qt_split(QShared &S, const QNode *cur, int na, bool reverse,
-                         const unsigned long long *order, int limit, QNode *nxt,
-                         unsigned long long *outrec, uint32_t *const K[2], int rec_cap,
-                         int nxt_cap) {
-    for (int cb = 0; cb < na; cb += ORBX_QT_THREADS) {
-        const int t = cb + (int)threadIdx.x;
-        const bool valid = t < na;
-        const bool divide = valid && t < limit;
-        QNode q{};
-        if (valid) {
-            const int idx = order ? (int)(order[t] & 0xFFFF) : (reverse ? na - 1 - t : t);
-            q = cur[idx];
-        }
-        int c[4] = {0, 0, 0, 0};
-        QNode ch[4];
-        if (divide) qnode_divide(q, K, c, ch);
+// Quadtree working set of one (image, level)
+struct QT {
+    QNode *cur, *nxt;
+    QTmp *tmp;
+    unsigned long long *outrec, *sortbuf;
+    uint32_t *K[2];
+    int16_t *NO[2];   // node index of each key position (-1: not in a live multi-key node)
+    int src;          // buffer holding the live nodes' keys
+    int M, NP, NC;
+    // buffer selection by select (no dynamically indexed private arrays -> no scratch)
+    __device__ uint32_t *keys(int i) const { return i ? K[1] : K[0]; }
+    __device__ int16_t *nodes_of(int i) const { return i ? NO[1] : NO[0]; }
+};
+
+// S1: quadrant prefix of every live key in buffer order; segment start / end prefixes per
+// node. Thread tid owns the contiguous key run [tid*R, tid*R + R). Returns the run's base.
+__device__ QCnt qt_prefix(QShared &S, QT &Q, int &par) {
+    const int R = (Q.M + ORBX_QT_THREADS - 1) / ORBX_QT_THREADS;
+    const int i0 = threadIdx.x * R, i1 = min(i0 + R, Q.M);
+    const uint32_t *K = Q.keys(Q.src);
+    const int16_t *NO = Q.nodes_of(Q.src);
+    QCnt run{0ull, 0ull};
+    for (int i = i0; i < i1; i++) {
+        const int nd = NO[i];
+        if (nd < 0) continue;
+        int mx, my;
+        qnode_mid(Q.cur[nd], &mx, &my);
+        run += qone(quadrant(K[i], mx, my));
+    }
+    QCnt tot;
+    const QCnt base = block_scan(S, run, &tot, par);
+    QCnt p = base;
+    for (int i = i0; i < i1; i++) {
+        const int nd = NO[i];
+        if (nd < 0) continue;
+        int mx, my;
+        qnode_mid(Q.cur[nd], &mx, &my);
+        if (i == 0 || NO[i - 1] != nd) Q.tmp[nd].pstart = p;
+        p += qone(quadrant(K[i], mx, my));
+        if (i == Q.M - 1 || NO[i + 1] != nd) Q.tmp[nd].pend = p;
+    }
+    __syncthreads();
+    return base;
+}
+
+// S3: one split round over `na` live nodes in processing order (order: 0 ascending,
+// 1 descending, 2 Q.sortbuf); nodes at positions >= limit are kept undivided (final phase).
+// Children get consecutive ids in processing order and n1..n4 order; multi-key children
+// (then kept nodes) form the next array in that order, single-key children become leaves.
+__device__ void qt_assign(QShared &S, QT &Q, int na, int order, int limit, int &par) {
+    const int Rn = (na + ORBX_QT_THREADS - 1) / ORBX_QT_THREADS;
+    const int t0 = threadIdx.x * Rn, t1 = min(t0 + Rn, na);
+    auto node_at = [&](int t) { return order == 2 ? (int)(Q.sortbuf[t] & 0xFFFF) : order == 1 ? na - 1 - t : t; };
+    unsigned long long run = 0;
+    for (int t = t0; t < t1 && t < limit; t++) {
+        const QTmp &T = Q.tmp[node_at(t)];
+        const QCnt c = T.pend - T.pstart;
         int ne = 0, mu = 0, si = 0;
-        for (int k = 0; k < 4; k++) { ne += c[k] > 0; mu += c[k] > 1; si += c[k] == 1; }
-        const bool left = valid && !divide;  // leftover (final phase)
-        int tot_ne, tot_mu, tot_si, tot_left;
-        const int pre_ne = block_excl_scan(S, ne, &tot_ne);
-        const int pre_mu = block_excl_scan(S, mu, &tot_mu);
-        const int pre_si = block_excl_scan(S, si + (left ? 1 : 0), &tot_si);
-        const int ndiv = block_excl_scan(S, divide ? 1 : 0, &tot_left);
-        (void)ndiv;
-        if (divide) {
-            int id = S.next_id + pre_ne, m = S.n_next + pre_mu, o = S.n_out + pre_si;
-            for (int k = 0; k < 4; k++) {
-                if (c[k] == 0) continue;
-                ch[k].id = id++;
-                if (c[k] == 1) {
-                    const uint32_t key = K[qnode_buf(ch[k])][qnode_start(ch[k])];
-                    if (o < rec_cap) outrec[o] = ((unsigned long long)(uint32_t)(ch[k].id + 0x40000000) << 32) | key;
-                    o++;
-                } else {
-                    if (m < nxt_cap) nxt[m] = ch[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { const int ck = c.f(k); ne += ck > 0; mu += ck > 1; si += ck == 1; }
+        run += (unsigned long long)ne | (unsigned long long)mu << 16 | (unsigned long long)si << 32;
+    }
+    unsigned long long tot;
+    const unsigned long long pre = block_scan64(S, run, &tot, par);
+    const int tot_ne = (int)(tot & 0xFFFF), tot_mu = (int)((tot >> 16) & 0xFFFF), tot_si = (int)(tot >> 32);
+    int id = S.next_id + (int)(pre & 0xFFFF);
+    int m = S.n_next + (int)((pre >> 16) & 0xFFFF);
+    int o = S.n_out + (int)(pre >> 32);
+    for (int t = t0; t < t1; t++) {
+        const int nd = node_at(t);
+        QTmp &T = Q.tmp[nd];
+        if (t >= limit) {
+            const int km = S.n_next + tot_mu + (t - limit);
+            T.keep = km < Q.NC ? km : -1;   // (never exceeds NC: the list stays below N + 4)
+            if (km < Q.NC) Q.nxt[km] = Q.cur[nd];
+            continue;
+        }
+        T.keep = -1;
+        const QNode q = Q.cur[nd];
+        const QCnt c = T.pend - T.pstart;
+        int mx, my;
+        qnode_mid(q, &mx, &my);
+        int cs = q.s;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int ck = c.f(k);
+            int16_t cmk = 0;
+            if (ck > 0) {
+                const int cid = id++;
+                if (ck > 1) {
+                    QNode ch;
+                    ch.x0 = (k & 1) ? (int16_t)mx : q.x0;
+                    ch.x1 = (k & 1) ? q.x1 : (int16_t)mx;
+                    ch.y0 = (k & 2) ? (int16_t)my : q.y0;
+                    ch.y1 = (k & 2) ? q.y1 : (int16_t)my;
+                    ch.s = cs;
+                    ch.n = ck;
+                    ch.id = cid;
+                    if (m < Q.NC) Q.nxt[m] = ch;
+                    cmk = (int16_t)(m < Q.NC ? m : -32768);
                     m++;
+                } else {
+                    if (o < Q.NP) Q.outrec[o] = (unsigned long long)(uint32_t)(cid + 0x40000000) << 32;
+                    cmk = (int16_t)(o < Q.NP ? -1 - o : -32768);
+                    o++;
                 }
             }
-        } else if (left) {
-            const int o = S.n_out + pre_si;
-            if (o < rec_cap)
-                outrec[o] = ((unsigned long long)(uint32_t)(q.id + 0x40000000) << 32) | qnode_best(q, K);
+            T.cm[k] = cmk;
+            cs += ck;
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            S.next_id += tot_ne;
-            S.n_next += tot_mu;
-            S.n_out += tot_si;
-            S.live += tot_ne - tot_left;
-        }
-        __syncthreads();
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int ndiv = min(limit, na);
+        S.next_id += tot_ne;
+        S.n_out += tot_si;
+        S.live += tot_ne - ndiv;
+        S.n_act = min(S.n_next + tot_mu + (na - ndiv), Q.NC);
+    }
+}
+
+// S4: move every live key to its child's segment in the other buffer (stable), record its
+// next-round node; leaves receive their key.
+__device__ void qt_move(QShared &S, QT &Q, QCnt base) {
+    const int R = (Q.M + ORBX_QT_THREADS - 1) / ORBX_QT_THREADS;
+    const int i0 = threadIdx.x * R, i1 = min(i0 + R, Q.M);
+    const int s = Q.src, d = s ^ 1;
+    const uint32_t *Ks = Q.keys(s);
+    const int16_t *Ns = Q.nodes_of(s);
+    uint32_t *Kd = Q.keys(d);
+    int16_t *Nd = Q.nodes_of(d);
+    QCnt p = base;
+    for (int i = i0; i < i1; i++) {
+        const int nd = Ns[i];
+        if (nd < 0) { Nd[i] = -1; continue; }
+        const uint32_t key = Ks[i];
+        const QNode q = Q.cur[nd];
+        int mx, my;
+        qnode_mid(q, &mx, &my);
+        const int k = quadrant(key, mx, my);
+        const QTmp &T = Q.tmp[nd];
+        if (T.keep >= 0) {
+            Kd[i] = key;
+            Nd[i] = (int16_t)T.keep;
+        } else {
+            const QCnt c = T.pend - T.pstart;
+            int pos = q.s + (p - T.pstart).f(k);
+            for (int j = 0; j < k; j++) pos += c.f(j);
+            Kd[pos] = key;
+            const int cmk = T.cm[k];
+            if (cmk >= 0) {
+                Nd[pos] = (int16_t)cmk;
+            } else {
+                Nd[pos] = -1;
+                if (cmk != -32768) Q.outrec[-1 - cmk] |= key;
+            }
+        }
+        p += qone(k);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) S.n_next = 0;
+    Q.src = d;
+    QNode *t = Q.cur; Q.cur = Q.nxt; Q.nxt = t;
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
@@ -629,68 +733,93 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     const int cb0 = g.cell_base[l], ncell = g.cell_base[l + 1] - cb0;
     const int N = g.N[l], nIni = g.nIni[l];
     const int NC = g.node_cap, NP = g.node_pow2;
+    int par = 0;
+    QT Q;
+    Q.NC = NC; Q.NP = NP;
     // ---- LDS / global carving
     unsigned char *lds = qt_lds;
-    QNode *nodes0, *nodes1;
-    unsigned long long *outrec, *sortbuf;
-    if (g.qt_nodes_in_lds) {
-        nodes0 = (QNode *)lds; lds += sizeof(QNode) * NC;
-        nodes1 = (QNode *)lds; lds += sizeof(QNode) * NC;
-        outrec = (unsigned long long *)lds; lds += 8 * NP;
-        sortbuf = (unsigned long long *)lds; lds += 8 * NP;
-    } else {
-        unsigned char *gn = qt_nodes + ((long long)b * g.nlevels + l) * g.qt_node_stride * 4;
-        nodes0 = (QNode *)gn; gn += sizeof(QNode) * NC;
-        nodes1 = (QNode *)gn; gn += sizeof(QNode) * NC;
-        outrec = (unsigned long long *)gn; gn += 8 * NP;
-        sortbuf = (unsigned long long *)gn;
+    {
+        unsigned char *p = g.qt_nodes_in_lds ? lds : qt_nodes + ((long long)b * g.nlevels + l) * g.qt_node_stride * 4;
+        Q.outrec = (unsigned long long *)p; p += 8 * NP;
+        Q.sortbuf = (unsigned long long *)p; p += 8 * NP;
+        Q.tmp = (QTmp *)p; p += sizeof(QTmp) * NC;
+        Q.cur = (QNode *)p; p += sizeof(QNode) * NC;
+        Q.nxt = (QNode *)p; p += sizeof(QNode) * NC;
+        if (g.qt_nodes_in_lds) lds = p;
     }
-    uint32_t *ldskeys = (uint32_t *)lds;
     // ---- 1. gather candidates in cell (row-major) order -> M
     const int *cnt = cell_cnt + (long long)b * g.ncell_total + cb0;
     int M = 0;
     for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS) {
         const int c = c0 + tid;
-        const int v = c < ncell ? cnt[c] : 0;
-        int tot;
-        block_excl_scan(S, v, &tot);
-        M += tot;
+        unsigned long long tot;
+        block_scan64(S, c < ncell ? (unsigned)cnt[c] : 0u, &tot, par);
+        M += (int)tot;
     }
-    uint32_t *K0, *K1;
-    if (M <= ORBX_QT_KL) { K0 = ldskeys; K1 = ldskeys + ORBX_QT_KL; }
-    else {
+    Q.M = M;
+    if (M <= g.qt_kl) {
+        Q.K[0] = (uint32_t *)lds;
+        Q.K[1] = Q.K[0] + g.qt_kl;
+        Q.NO[0] = (int16_t *)(Q.K[1] + g.qt_kl);
+        Q.NO[1] = Q.NO[0] + g.qt_kl;
+    } else {
         uint32_t *gk = qt_keys + (long long)b * g.qt_off[g.nlevels] + g.qt_off[l];
-        K0 = gk; K1 = gk + (g.qt_off[l + 1] - g.qt_off[l]) / 2;
+        const long long cap = (g.qt_off[l + 1] - g.qt_off[l]) / 3;
+        Q.K[0] = gk;
+        Q.K[1] = gk + cap;
+        Q.NO[0] = (int16_t *)(gk + 2 * cap);
+        Q.NO[1] = Q.NO[0] + cap;
     }
-    uint32_t *const K[2] = {K0, K1};
     {
         int base = 0;
         for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS) {
             const int c = c0 + tid;
             const int v = c < ncell ? cnt[c] : 0;
-            int tot;
-            const int pre = block_excl_scan(S, v, &tot);
+            unsigned long long tot;
+            const int pre = (int)block_scan64(S, (unsigned)v, &tot, par);
             if (c < ncell) {
                 const uint32_t *src = cell_keys + ((long long)b * g.ncell_total + cb0 + c) * g.cell_cap;
-                for (int i = 0; i < v; i++) K0[base + pre + i] = src[i];
+                for (int i = 0; i < v; i++) Q.K[0][base + pre + i] = src[i];
             }
-            base += tot;
+            base += (int)tot;
         }
     }
-    // ---- 2. roots (:700-745): stable counting partition into K1
+    // ---- 2. roots (:700-745): stable counting partition into buffer 1
     const float hX = g.hX[l];
     if (tid < 64) { S.root_cnt[tid] = 0; S.root_fill[tid] = 0; }
-    if (tid == 0) { S.live = 0; S.next_id = nIni; S.n_out = 0; S.n_next = 0; }
     __syncthreads();
     for (int i = tid; i < M; i += ORBX_QT_THREADS) {
-        int r = (int)((float)key_x(K0[i]) / hX);
-        r = min(r, nIni - 1);
+        const int r = min((int)((float)key_x(Q.K[0][i]) / hX), nIni - 1);
         atomicAdd(&S.root_cnt[r], 1);
     }
     __syncthreads();
     if (tid == 0) {
-        int a = 0;
-        for (int r = 0; r < nIni; r++) { S.root_start[r] = a; a += S.root_cnt[r]; }
+        const int H = g.maxBY[l] - 16;
+        int a = 0, na = 0, no = 0, live = 0;
+        for (int r = 0; r < nIni; r++) {
+            const int n = S.root_cnt[r];
+            S.root_start[r] = a;
+            S.root_node[r] = -1;
+            S.root_out[r] = -1;
+            a += n;
+            if (n == 0) continue;
+            live++;
+            if (n == 1) {
+                S.root_out[r] = no++;
+            } else {
+                QNode q;
+                q.x0 = (int16_t)(int)(hX * (float)r);
+                q.x1 = (int16_t)(int)(hX * (float)(r + 1));
+                q.y0 = 0;
+                q.y1 = (int16_t)H;
+                q.s = S.root_start[r];
+                q.n = n;
+                q.id = -1 - r;
+                S.root_node[r] = na;
+                Q.cur[na++] = q;
+            }
+        }
+        S.live = live; S.n_out = no; S.n_act = na; S.next_id = nIni; S.n_next = 0;
     }
     __syncthreads();
     const int lane = tid & 63, wv = tid >> 6;
@@ -698,7 +827,7 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         const int i = cs + tid;
         int r = -1;
         uint32_t key = 0;
-        if (i < M) { key = K0[i]; r = min((int)((float)key_x(key) / hX), nIni - 1); }
+        if (i < M) { key = Q.K[0][i]; r = min((int)((float)key_x(key) / hX), nIni - 1); }
         int my_rank = 0;
         for (int rr = 0; rr < nIni; rr++) {
             const unsigned long long m = __ballot(r == rr);
@@ -709,7 +838,9 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         if (r >= 0) {
             int pos = S.root_start[r] + S.root_fill[r] + my_rank;
             for (int w = 0; w < wv; w++) pos += S.wcnt[w][r];
-            K1[pos] = key;
+            Q.K[1][pos] = key;
+            Q.NO[1][pos] = (int16_t)S.root_node[r];
+            if (S.root_out[r] >= 0) Q.outrec[S.root_out[r]] = ((unsigned long long)(uint32_t)(-1 - r + 0x40000000) << 32) | key;
         }
         __syncthreads();
         if (tid < nIni) {
@@ -719,118 +850,98 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         }
         __syncthreads();
     }
-    if (tid == 0) {
-        const int H = g.maxBY[l] - 16;
-        int na = 0, live = 0, no = 0;
-        for (int r = 0; r < nIni; r++) {
-            const int n = S.root_cnt[r];
-            if (n == 0) continue;
-            live++;
-            if (n == 1) {
-                outrec[no++] = ((unsigned long long)(uint32_t)(-1 - r + 0x40000000) << 32) | K1[S.root_start[r]];
-            } else {
-                QNode q;
-                q.x0 = (int16_t)(int)(hX * (float)r);
-                q.x1 = (int16_t)(int)(hX * (float)(r + 1));
-                q.y0 = 0;
-                q.y1 = (int16_t)H;
-                q.s = S.root_start[r] | (1 << 30);
-                q.n = n;
-                q.id = -1 - r;
-                nodes0[na++] = q;
-            }
-        }
-        S.live = live; S.n_out = no; S.n_act = na;
-    }
-    __syncthreads();
-    // ---- 3. phase-1 rounds (:772-913)
-    QNode *cur = nodes0, *nxt = nodes1;
-    bool reverse = false;  // roots are processed in ascending order (push_back'ed)
-    bool finished = false;
-    bool final_phase = false;
+    Q.src = 1;
+    // ---- 3. phase-1 rounds (:772-913): every live node divided, roots ascending, then
+    //         the previous round's multi-key children in reverse creation order
+    int order = 0;
+    bool finished = false, final_phase = false;
     while (!finished) {
-        const int prev = S.live;
-        const int na = S.n_act;
-        if (tid == 0) S.n_next = 0;
-        __syncthreads();
-        qt_split(S, cur, na, reverse, nullptr, na, nxt, outrec, K, NP, NC);
-        QNode *tmp = cur; cur = nxt; nxt = tmp;
-        reverse = true;
-        if (tid == 0) S.n_act = S.n_next;
-        __syncthreads();
+        const int prev = S.live, na = S.n_act;
+        const QCnt base = qt_prefix(S, Q, par);
+        qt_assign(S, Q, na, order, na, par);
+        qt_move(S, Q, base);
+        order = 1;
         const int live = S.live, nToExpand = S.n_act;
         if (live >= N || live == prev) finished = true;
         else if (live + nToExpand * 3 > N) { final_phase = true; finished = true; }
     }
-    // ---- 4. final phase (:914-997)
+    // ---- 4. final phase (:914-997): nodes by (size, id) descending; divide until the
+    //         list reaches N
     if (final_phase) {
         bool done = false;
         while (!done) {
-            const int prev = S.live;
-            const int na = S.n_act;
-            for (int i = tid; i < NP; i += ORBX_QT_THREADS) {
-                unsigned long long v = 0;
-                if (i < na) {
-                    const QNode &q = cur[i];
-                    v = ((unsigned long long)(uint32_t)q.n << 40) | ((unsigned long long)(uint32_t)(q.id & 0xFFFFFF) << 16) | (unsigned)i;
-                }
-                sortbuf[i] = v;
-            }
-            __syncthreads();
+            const int prev = S.live, na = S.n_act;
+            const QCnt base = qt_prefix(S, Q, par);
             int np2 = 1;
             while (np2 < na) np2 <<= 1;
-            block_sort_desc(sortbuf, np2);
-            // first sorted position whose split brings the size to >= N
+            for (int i = tid; i < np2; i += ORBX_QT_THREADS) {
+                unsigned long long v = 0;
+                if (i < na) {
+                    const QNode &q = Q.cur[i];
+                    v = ((unsigned long long)(uint32_t)q.n << 40) | ((unsigned long long)(uint32_t)(q.id & 0xFFFFFF) << 16) | (unsigned)i;
+                }
+                Q.sortbuf[i] = v;
+            }
             if (tid == 0) S.cross = na;
             __syncthreads();
-            int run = S.live;
-            for (int cb = 0; cb < na; cb += ORBX_QT_THREADS) {
-                const int t = cb + tid;
-                int delta = 0;
-                if (t < na) {
-                    int c[4];
-                    qnode_counts(cur[sortbuf[t] & 0xFFFF], K, c);
-                    delta = (c[0] > 0) + (c[1] > 0) + (c[2] > 0) + (c[3] > 0) - 1;
+            block_sort_desc(Q.sortbuf, np2);
+            // first sorted position whose split brings the size to >= N
+            {
+                const int Rn = (na + ORBX_QT_THREADS - 1) / ORBX_QT_THREADS;
+                const int t0 = tid * Rn, t1 = min(t0 + Rn, na);
+                int run = 0;
+                for (int t = t0; t < t1; t++) {
+                    const QTmp &T = Q.tmp[Q.sortbuf[t] & 0xFFFF];
+                    const QCnt c = T.pend - T.pstart;
+                    run += (c.f(0) > 0) + (c.f(1) > 0) + (c.f(2) > 0) + (c.f(3) > 0) - 1;
                 }
-                int tot;
-                const int pre = block_excl_scan(S, delta, &tot);
-                if (t < na && run + pre + delta >= N) atomicMin(&S.cross, t);
-                run += tot;
-                __syncthreads();
+                unsigned long long tot;
+                int acc = S.live + (int)block_scan64(S, (unsigned long long)(long long)run, &tot, par);
+                for (int t = t0; t < t1; t++) {
+                    const QTmp &T = Q.tmp[Q.sortbuf[t] & 0xFFFF];
+                    const QCnt c = T.pend - T.pstart;
+                    acc += (c.f(0) > 0) + (c.f(1) > 0) + (c.f(2) > 0) + (c.f(3) > 0) - 1;
+                    if (acc >= N) { atomicMin(&S.cross, t); break; }
+                }
             }
+            __syncthreads();
             const int limit = min(S.cross + 1, na);
-            if (tid == 0) S.n_next = 0;
-            __syncthreads();
-            qt_split(S, cur, na, false, sortbuf, limit, nxt, outrec, K, NP, NC);
-            QNode *tmp = cur; cur = nxt; nxt = tmp;
-            if (tid == 0) S.n_act = S.n_next;
-            __syncthreads();
+            qt_assign(S, Q, na, 2, limit, par);
+            qt_move(S, Q, base);
             if (S.live >= N || S.live == prev) done = true;
         }
     }
-    // ---- 5. leftover multi-key nodes -> first max response; output in list order
+    // ---- 5. every remaining multi-key node -> its first key of maximal response (:1028)
     {
         const int na = S.n_act;
-        for (int cb = 0; cb < na; cb += ORBX_QT_THREADS) {
-            const int t = cb + tid;
-            int tot;
-            const int pre = block_excl_scan(S, t < na ? 1 : 0, &tot);
-            if (t < na && S.n_out + pre < NP) {
-                const QNode &q = cur[t];
-                outrec[S.n_out + pre] = ((unsigned long long)(uint32_t)(q.id + 0x40000000) << 32) | qnode_best(q, K);
-            }
-            __syncthreads();
-            if (tid == 0) S.n_out += tot;
-            __syncthreads();
+        const int R = (M + ORBX_QT_THREADS - 1) / ORBX_QT_THREADS;
+        const int i0 = tid * R, i1 = min(i0 + R, M);
+        unsigned *best = (unsigned *)Q.sortbuf;
+        for (int i = tid; i < na; i += ORBX_QT_THREADS) best[i] = 0u;
+        __syncthreads();
+        for (int i = i0; i < i1; i++) {
+            const int nd = Q.nodes_of(Q.src)[i];
+            if (nd >= 0) atomicMax(&best[nd], ((unsigned)key_score(Q.keys(Q.src)[i]) << 24) | (0xFFFFFFu - (unsigned)i));
         }
+        __syncthreads();
+        for (int t = tid; t < na; t += ORBX_QT_THREADS) {
+            const int o = S.n_out + t;
+            if (o < NP) {
+                const uint32_t key = Q.keys(Q.src)[0xFFFFFF - (best[t] & 0xFFFFFF)];
+                Q.outrec[o] = ((unsigned long long)(uint32_t)(Q.cur[t].id + 0x40000000) << 32) | key;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) S.n_out += na;
+        __syncthreads();
     }
     const int nout = min(S.n_out, NP);
-    for (int i = nout + tid; i < NP; i += ORBX_QT_THREADS) outrec[i] = 0;
+    for (int i = nout + tid; i < NP; i += ORBX_QT_THREADS) Q.outrec[i] = 0;
     __syncthreads();
-    block_sort_desc(outrec, NP);
+    block_sort_desc(Q.outrec, NP);
     const int ncap = min(nout, g.out_cap[l]);
     uint32_t *dst = sel + (long long)b * g.out_base[g.nlevels] + g.out_base[l];
-    for (int i = tid; i < ncap; i += ORBX_QT_THREADS) dst[i] = (uint32_t)(outrec[i] & 0xFFFFFFFFull);
+    for (int i = tid; i < ncap; i += ORBX_QT_THREADS) dst[i] = (uint32_t)(Q.outrec[i] & 0xFFFFFFFFull);
     if (tid == 0) sel_cnt[b * g.nlevels + l] = ncap;
 }
 
@@ -1077,7 +1188,7 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         for (int l = 0; l < L; l++) {
             g.qt_off[l] = qt;
             const long long mcap = (long long)(g.cell_base[l + 1] - g.cell_base[l]) * cell_cap;
-            qt += 2 * mcap;
+            qt += 3 * mcap;   // K0, K1, node index (2 x int16) -- global fallback
             maxM_total = std::max<long long>(maxM_total, mcap);
         }
         g.qt_off[L] = qt;
@@ -1085,9 +1196,14 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         int np2 = 1;
         while (np2 < g.node_cap) np2 <<= 1;
         g.node_pow2 = np2;
-        const size_t node_bytes = 2 * sizeof(QNode) * g.node_cap + 16 * (size_t)np2;
-        g.qt_nodes_in_lds = node_bytes + 8 * ORBX_QT_KL <= 96 * 1024 ? 1 : 0;
+        if (g.node_cap > 32767 || maxM_total >= (1 << 24)) return ORBX_EINVAL;  // int16 node ids, 24-bit positions
+        const size_t node_bytes = (2 * sizeof(QNode) + sizeof(QTmp)) * g.node_cap + 16 * (size_t)np2;
+        g.qt_nodes_in_lds = node_bytes <= 48 * 1024 ? 1 : 0;
         g.qt_node_stride = (long long)((node_bytes + 15) / 16) * 4;
+        // keys (2 x u32) + node index (2 x int16) per candidate in LDS up to ~78 KB per workgroup
+        // (two workgroups per CU); larger levels run on the global scratch
+        const long long kl_bytes = 78 * 1024 - (g.qt_nodes_in_lds ? (long long)node_bytes : 0);
+        g.qt_kl = (int)std::max<long long>(256, (kl_bytes / 12) & ~63LL);
         g.ini_th = e->p.ini_th_fast;
         g.min_th = e->p.min_th_fast;
         g.resize_mode = e->p.resize_mode;
@@ -1171,8 +1287,8 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
                                                         e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
     prof_end(e, s, ph, "fast_nms_kernel");
     ph = prof_begin(e, s);
-    size_t lds = 8 * (size_t)ORBX_QT_KL;
-    if (g.qt_nodes_in_lds) lds += 2 * sizeof(QNode) * g.node_cap + 16 * (size_t)g.node_pow2;
+    size_t lds = 12 * (size_t)g.qt_kl;
+    if (g.qt_nodes_in_lds) lds += (2 * sizeof(QNode) + sizeof(QTmp)) * g.node_cap + 16 * (size_t)g.node_pow2;
     quadtree_kernel<<<dim3(L, n), ORBX_QT_THREADS, lds, s>>>(
         g, e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>(), e->d_qt.as<uint32_t>(),
         e->d_qt_nodes.as<unsigned char>(), e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>());

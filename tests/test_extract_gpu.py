@@ -74,7 +74,7 @@ def test_extract_empty_image(amd):
     assert len(k) == 0
 
 
-@pytest.mark.parametrize("nf,levels", [(500, 4), (3000, 8), (1200, 6)])
+@pytest.mark.parametrize("nf,levels", [(500, 4), (3000, 8), (1200, 6), (8000, 8)])
 def test_extract_param_sweep(amd, oracle_mod, nf, levels):
     img = synth.textured_image(480, 752, 21 + nf)
     ex = amd.ORBextractor(nf, 1.2, levels, 20, 7)
