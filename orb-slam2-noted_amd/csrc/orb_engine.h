@@ -75,7 +75,7 @@ struct orbx_engine {
     orbamd::ExtractGeom g{};
     std::vector<orbamd::CellDesc> cells;
     // device buffers
-    orbamd::DevBuf d_mmap, d_cells, d_rz, d_pattern, d_in, d_pyr, d_blur, d_cell_cnt, d_cell_keys,
+    orbamd::DevBuf d_mmap, d_cells, d_rz, d_rzr, d_pattern, d_in, d_pyr, d_blur, d_cell_cnt, d_cell_keys,
         d_qt, d_qt_nodes, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt;
     // stereo
     orbamd::DevBuf d_st_sorted, d_st_res, d_st_u, d_st_depth, d_st_dist;

@@ -20,6 +20,9 @@ namespace orbamd {
 
 static __constant__ int8_t c_pattern[1024];  // bit_pattern_31_ (ORBextractor.cc:209-467) as data
 static __constant__ int c_umax[16];
+// IC_Angle byte weights per (|v|, dword w) of the row segment u = 4w-16 .. 4w-13:
+// x = (u + 16) where |u| <= umax[|v|] else 0, y = 1 / 0 mask (built from umax on the host)
+static __constant__ uint2 c_icw[16 * 8];
 
 #define HIPCHK(x)                                                                   \
     do {                                                                            \
@@ -52,7 +55,7 @@ int DevBuf::ensure(size_t n) {
 __device__ __forceinline__ const uint8_t *level_ptr(const ExtractGeom &g, const uint8_t *in,
                                                     const uint8_t *pyr, int b, int l, int *pitch) {
     if (l == 0) { *pitch = g.in_pitch; return in + (long long)b * g.in_stride; }
-    *pitch = g.lw[l];
+    *pitch = g.bp[l];
     return pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
 }
 
@@ -60,23 +63,24 @@ __device__ __forceinline__ const uint8_t *level_ptr(const ExtractGeom &g, const 
 // K1: cv::resize(INTER_LINEAR) of level l-1 into level l (ComputePyramid :1686-1691,
 // SURVEY.md A.2). Column/row coefficient tables are precomputed on the host with the
 // reference's float/double arithmetic; the kernel does the exact integer math.
+// Each thread produces 4 consecutive pixels of one row: the row pair is a wave-uniform
+// (scalar) load, the 4 source columns span <= 8 bytes (scale <= 2) and come from two
+// dword loads per source row; the result is one dword store (pyramid pitch is 16-aligned).
+// Column table entry: x = sx | a0 << 16, y = a1 | (sx1 - sx) << 16.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, const int4 *rz,
-                                                           const uint8_t *in, uint8_t *pyr) {
-    const int dw = g.lw[l], dh = g.lh[l];
-    const int b = blockIdx.z, dy = blockIdx.y;
-    const int dx = blockIdx.x * 256 + threadIdx.x;
-    if (dx >= dw || dy >= dh) return;
-    int sp;
-    const uint8_t *src = level_ptr(g, in, pyr, b, l - 1, &sp);
-    uint8_t *dst = pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
-    const int4 cx = rz[g.rz_col_off[l] + dx];   // sx, sx1, a0, a1
-    const int4 ry = rz[g.rz_row_off[l] + dy];   // r0, r1, b0, b1
-    const uint8_t *p0 = src + (long long)ry.x * sp, *p1 = src + (long long)ry.y * sp;
-    const int S0 = p0[cx.x] * cx.z + p0[cx.y] * cx.w;
-    const int S1 = p1[cx.x] * cx.z + p1[cx.y] * cx.w;
+// dword of image bytes [x, x+4) of row `rowp` (x .. x+3 inside the row) from aligned loads
+__device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *pa = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t lo = pa[0];
+    const uint32_t hi = sh ? pa[1] : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+__device__ __forceinline__ int resize_px(int S0, int S1, int4 ry, bool simd) {
     int v;
-    if (dx < g.rz_simd_end[l]) {  // SSE2 VResizeLinearVec_32s8u lane arithmetic
+    if (simd) {  // SSE2 VResizeLinearVec_32s8u lane arithmetic
         int x0 = S0 >> 4, y0 = S1 >> 4;
         x0 = min(max(x0, -32768), 32767);
         y0 = min(max(y0, -32768), 32767);
@@ -84,10 +88,54 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
         t = min(max(t, -32768), 32767);
         t = min(max(t + 2, -32768), 32767) >> 2;
         v = t;
-    } else {                      // FixedPtCast<int, uchar, 22>
+    } else {     // FixedPtCast<int, uchar, 22>
         v = (S0 * ry.z + S1 * ry.w + (1 << 21)) >> 22;
     }
-    dst[(long long)dy * dw + dx] = (uint8_t)min(max(v, 0), 255);
+    return min(max(v, 0), 255);
+}
+
+__global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, const int2 *cxt, const int4 *ryt,
+                                                           const uint8_t *in, uint8_t *pyr) {
+    const int dw = g.lw[l];
+    const int b = blockIdx.z, dy = blockIdx.y;
+    const int dx0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (dx0 >= dw) return;
+    int sp;
+    const uint8_t *src = level_ptr(g, in, pyr, b, l - 1, &sp);
+    uint8_t *dst = pyr + (long long)b * g.pyr_stride + g.pyr_off[l] + (long long)dy * g.bp[l];
+    const int4 ry = ryt[dy];   // r0, r1, b0, b1 (uniform over the block)
+    const uint8_t *p0 = src + (long long)ry.x * sp, *p1 = src + (long long)ry.y * sp;
+    const int n = min(4, dw - dx0);
+    int2 c[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) c[k] = cxt[min(dx0 + k, dw - 1)];
+    const int sx0 = c[0].x & 0xFFFF;
+    const int sw = g.lw[l - 1];
+    unsigned long long R0, R1;
+    if (sx0 + 8 <= sw) {
+        R0 = load_u32_unaligned(p0 + sx0) | (unsigned long long)load_u32_unaligned(p0 + sx0 + 4) << 32;
+        R1 = load_u32_unaligned(p1 + sx0) | (unsigned long long)load_u32_unaligned(p1 + sx0 + 4) << 32;
+    } else {
+        R0 = R1 = 0;
+        for (int e = 0; e < 8 && sx0 + e < sw; e++) {
+            R0 |= (unsigned long long)p0[sx0 + e] << (8 * e);
+            R1 |= (unsigned long long)p1[sx0 + e] << (8 * e);
+        }
+    }
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int o = (c[k].x & 0xFFFF) - sx0, o1 = o + (c[k].y >> 16);
+        const int a0 = c[k].x >> 16, a1 = c[k].y & 0xFFFF;
+        const int S0 = (int)((R0 >> (8 * o)) & 0xFF) * a0 + (int)((R0 >> (8 * o1)) & 0xFF) * a1;
+        const int S1 = (int)((R1 >> (8 * o)) & 0xFF) * a0 + (int)((R1 >> (8 * o1)) & 0xFF) * a1;
+        out |= (uint32_t)resize_px(S0, S1, ry, dx0 + k < g.rz_simd_end[l]) << (8 * k);
+    }
+    if (n == 4) {
+        *(uint32_t *)(dst + dx0) = out;
+    } else {
+        for (int k = 0; k < n; k++) dst[dx0 + k] = (uint8_t)(out >> (8 * k));
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -143,16 +191,6 @@ __device__ __forceinline__ s16x2 byte_pair(const uint32_t *w, int j) {
     const uint32_t r = k < 3 ? __builtin_amdgcn_perm(0u, w[d], 0x0c000c00u | ((uint32_t)(k + 1) << 16) | (uint32_t)k)
                              : __builtin_amdgcn_perm(w[d + 1], w[d], 0x0c040c03u);
     return __builtin_bit_cast(s16x2, r);
-}
-
-// dword of image bytes [x, x+4) of row `rowp` (x .. x+3 inside the row) from aligned loads
-__device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t *pa = (const uint32_t *)(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t lo = pa[0];
-    const uint32_t hi = sh ? pa[1] : 0u;
-    return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
 // order LDS traffic between lanes of one wavefront (LDS executes a wave's ops in order)
@@ -981,16 +1019,21 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
     const int x = key_x(key) + 16, y = key_y(key) + 16;  // + minBorderX/Y (:1177-1186)
     int pitch;
     const uint8_t *img = level_ptr(g, in, pyr, b, l, &pitch);
-    // IC_Angle over the circular patch (|u| <= umax[|v|])
-    const uint8_t *center = img + (long long)y * pitch + x;
+    // IC_Angle over the circular patch (|u| <= umax[|v|]): rows v = -15..15 as 8 dwords
+    // (u = -16..15), sum_u u*p = sum (u+16)*p - 16 * sum p with v_dot4_u32_u8 (exact integers)
+    const uint8_t *rowc = img + (long long)y * pitch + x - 16;
     int m01 = 0, m10 = 0;
-    for (int t = lane; t < 31 * 31; t += 64) {
-        const int v = t / 31 - 15, u = t % 31 - 15;
-        const int av = v < 0 ? -v : v;
-        if ((u < 0 ? -u : u) <= c_umax[av]) {
-            const int p = center[(long long)v * pitch + u];
-            m10 += u * p;
-            m01 += v * p;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int j = lane + 64 * k;
+        if (j < 31 * 8) {
+            const int v = (j >> 3) - 15, w = j & 7;
+            const uint2 wt = c_icw[(v < 0 ? -v : v) * 8 + w];
+            const uint32_t P = load_u32_unaligned(rowc + (long long)v * pitch + 4 * w);
+            const int su = (int)__builtin_amdgcn_udot4(P, wt.x, 0u, false);
+            const int sm = (int)__builtin_amdgcn_udot4(P, wt.y, 0u, false);
+            m10 += su - 16 * sm;
+            m01 += v * sm;
         }
     }
     m10 = wave_sum(m10);
@@ -1119,8 +1162,8 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             g.lh[l] = host_round((float)H * e->inv_scale[l]);
             if (g.lw[l] < 40 || g.lh[l] < 40) return ORBX_EINVAL;
             g.pyr_off[l] = l == 0 ? 0 : pyr;
-            if (l > 0) pyr += ((long long)g.lw[l] * g.lh[l] + 63) & ~63LL;
             g.bp[l] = (g.lw[l] + 15) & ~15;
+            if (l > 0) pyr += ((long long)g.bp[l] * g.lh[l] + 63) & ~63LL;
             g.blur_off[l] = blur;
             blur += ((long long)g.bp[l] * g.lh[l] + 63) & ~63LL;
             g.scale[l] = e->scale[l];
@@ -1208,32 +1251,36 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         g.min_th = e->p.min_th_fast;
         g.resize_mode = e->p.resize_mode;
         // resize coefficient tables
-        std::vector<int4> rz;
+        std::vector<int2> rzc;
+        std::vector<int4> rzr;
         for (int l = 1; l < L; l++) {
             const int sw = g.lw[l - 1], sh = g.lh[l - 1], dw = g.lw[l], dh = g.lh[l];
             const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
-            g.rz_col_off[l] = (int)rz.size();
+            if (scale_x > 2.0) return ORBX_EINVAL;   // 4 outputs span <= 8 source bytes
+            auto satS = [](float v) { int r = host_round(v); return std::min(std::max(r, -32768), 32767); };
+            g.rz_col_off[l] = (int)rzc.size();
             for (int dx = 0; dx < dw; dx++) {
                 float fx = (float)((dx + 0.5) * scale_x - 0.5);
                 int sx = (int)std::floor(fx);
                 fx -= sx;
                 if (sx < 0) { fx = 0; sx = 0; }
                 if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
-                auto satS = [](float v) { int r = host_round(v); return std::min(std::max(r, -32768), 32767); };
-                rz.push_back(make_int4(sx, std::min(sx + 1, sw - 1), satS((1.f - fx) * 2048), satS(fx * 2048)));
+                const int a0 = satS((1.f - fx) * 2048), a1 = satS(fx * 2048);
+                const int sx1 = std::min(sx + 1, sw - 1);
+                rzc.push_back(make_int2(sx | (a0 << 16), a1 | ((sx1 - sx) << 16)));
             }
-            g.rz_row_off[l] = (int)rz.size();
+            g.rz_row_off[l] = (int)rzr.size();
             for (int dy = 0; dy < dh; dy++) {
                 float fy = (float)((dy + 0.5) * scale_y - 0.5);
                 int sy = (int)std::floor(fy);
                 fy -= sy;
-                auto satS = [](float v) { int r = host_round(v); return std::min(std::max(r, -32768), 32767); };
                 auto clip = [sh](int y) { return y >= 0 ? (y < sh ? y : sh - 1) : 0; };
-                rz.push_back(make_int4(clip(sy), clip(sy + 1), satS((1.f - fy) * 2048), satS(fy * 2048)));
+                rzr.push_back(make_int4(clip(sy), clip(sy + 1), satS((1.f - fy) * 2048), satS(fy * 2048)));
             }
             g.rz_simd_end[l] = e->p.resize_mode ? simd_end_for(dw) : 0;
         }
-        if (rz.empty()) rz.push_back(make_int4(0, 0, 0, 0));
+        if (rzc.empty()) rzc.push_back(make_int2(0, 0));
+        if (rzr.empty()) rzr.push_back(make_int4(0, 0, 0, 0));
         // blur tiles
         g.blur_tile_base[0] = 0;
         for (int l = 0; l < L; l++) {
@@ -1243,8 +1290,9 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         }
         if (e->d_cells.ensure(sizeof(CellDesc) * e->cells.size())) return ORBX_EDEVICE;
         HIPCHK(hipMemcpy(e->d_cells.p, e->cells.data(), sizeof(CellDesc) * e->cells.size(), hipMemcpyHostToDevice));
-        if (e->d_rz.ensure(sizeof(int4) * rz.size())) return ORBX_EDEVICE;
-        HIPCHK(hipMemcpy(e->d_rz.p, rz.data(), sizeof(int4) * rz.size(), hipMemcpyHostToDevice));
+        if (e->d_rz.ensure(sizeof(int2) * rzc.size()) || e->d_rzr.ensure(sizeof(int4) * rzr.size())) return ORBX_EDEVICE;
+        HIPCHK(hipMemcpy(e->d_rz.p, rzc.data(), sizeof(int2) * rzc.size(), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->d_rzr.p, rzr.data(), sizeof(int4) * rzr.size(), hipMemcpyHostToDevice));
         e->W = W; e->H = H;
         e->max_images = 0;
     }
@@ -1274,8 +1322,9 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     uint8_t *pyr = e->d_pyr.as<uint8_t>();
     int ph = prof_begin(e, s);
     for (int l = 1; l < L; l++) {
-        dim3 grid((g.lw[l] + 255) / 256, g.lh[l], n);
-        resize_level_kernel<<<grid, 256, 0, s>>>(g, l, e->d_rz.as<int4>(), d_imgs, pyr);
+        dim3 grid((g.lw[l] + 1023) / 1024, g.lh[l], n);
+        resize_level_kernel<<<grid, 256, 0, s>>>(g, l, e->d_rz.as<int2>() + g.rz_col_off[l],
+                                                 e->d_rzr.as<int4>() + g.rz_row_off[l], d_imgs, pyr);
     }
     prof_end(e, s, ph, "resize_level_kernel");
     ph = prof_begin(e, s);
@@ -1335,8 +1384,20 @@ int orbx_create(const orbx_params *p, orbx_engine **out) {
     if (hipGetDevice(&e->device) != hipSuccess) { delete e; return ORBX_EDEVICE; }
     compute_tables(e);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return ORBX_EDEVICE; }
+    uint2 icw[16 * 8];
+    for (int av = 0; av < 16; av++) {
+        for (int w = 0; w < 8; w++) {
+            uint32_t wu = 0, wm = 0;
+            for (int b = 0; b < 4; b++) {
+                const int u = 4 * w + b - 16;
+                if (std::abs(u) <= e->umax[av]) { wu |= (uint32_t)(u + 16) << (8 * b); wm |= 1u << (8 * b); }
+            }
+            icw[av * 8 + w] = make_uint2(wu, wm);
+        }
+    }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), e->pattern, 1024) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_umax), e->umax, sizeof(e->umax)) != hipSuccess) {
+        hipMemcpyToSymbol(HIP_SYMBOL(c_umax), e->umax, sizeof(e->umax)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_icw), icw, sizeof(icw)) != hipSuccess) {
         (void)hipStreamDestroy(e->stream);
         delete e;
         return ORBX_EDEVICE;
@@ -1349,7 +1410,7 @@ void orbx_destroy(orbx_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    orbamd::DevBuf *bufs[] = {&e->d_mmap, &e->d_cells, &e->d_rz, &e->d_pattern, &e->d_in, &e->d_pyr, &e->d_blur,
+    orbamd::DevBuf *bufs[] = {&e->d_mmap, &e->d_cells, &e->d_rz, &e->d_rzr, &e->d_pattern, &e->d_in, &e->d_pyr, &e->d_blur,
                               &e->d_cell_cnt, &e->d_cell_keys, &e->d_qt, &e->d_qt_nodes, &e->d_sel,
                               &e->d_sel_cnt, &e->d_kps, &e->d_desc, &e->d_cnt, &e->d_st_sorted,
                               &e->d_st_res, &e->d_st_u, &e->d_st_depth, &e->d_st_dist};
@@ -1488,8 +1549,8 @@ int orbx_pyramid_level(orbx_engine *e, int image, int level, uint8_t *dst, int *
     if (level == 0) {
         HIPCHK(hipMemcpy2D(dst, lw, e->last_in + image * e->last_stride, e->last_pitch, lw, lh, hipMemcpyDeviceToHost));
     } else {
-        HIPCHK(hipMemcpy(dst, e->d_pyr.as<uint8_t>() + image * e->g.pyr_stride + e->g.pyr_off[level],
-                         (size_t)lw * lh, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy2D(dst, lw, e->d_pyr.as<uint8_t>() + image * e->g.pyr_stride + e->g.pyr_off[level],
+                           e->g.bp[level], lw, lh, hipMemcpyDeviceToHost));
     }
     return ORBX_OK;
 }

@@ -56,7 +56,7 @@ struct StereoArgs {
 __device__ __forceinline__ const uint8_t *side_level(const ExtractGeom &g, const StereoSide &s, int img,
                                                      int l, int *pitch) {
     if (l == 0) { *pitch = s.in_pitch; return s.in + (long long)img * s.in_stride; }
-    *pitch = g.lw[l];
+    *pitch = g.bp[l];
     return s.pyr + (long long)img * g.pyr_stride + g.pyr_off[l];
 }
 
