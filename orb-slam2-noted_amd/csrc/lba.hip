@@ -13,7 +13,8 @@
 //   lba_syrk_mfma     Hpp - Y Y^T on FP64 matrix cores (v_mfma_f64_16x16x4f64), one wave per
 //                     16x16 upper tile per K slice, partial slabs reduced in fixed order
 //   lba_schur_reduce  Hschur = Hpp + lambda I - sum(slabs), b_schur = b_p - Y w
-//   lba_chol_solve    dense Cholesky of the <=126x126 Schur matrix in LDS + two solves
+//   lba_chol_small    dense Cholesky of the Schur matrix (6P <= 128) in LDS + two solves;
+//   lba_chol_panel/_update/_solve_blocked  blocked Cholesky (MFMA trailing update) above
 //   lba_backsub       x_l = Dinv (b_l - Hpl^T x_p)
 //   lba_update        T <- exp(x_p) T (SE3Quat::exp, left-multiplied), X <- X + x_l
 //   lba_errors        trial residuals (kept as g2o's stale _error) + robust chi2 + scale
@@ -43,8 +44,9 @@
 
 namespace lbaamd {
 
-constexpr int kMaxPoses = 21;        // 6 * 21 = 126 <= 128 (one Schur matrix in LDS)
-constexpr int kNP = 128;             // padded Schur dimension
+constexpr int kSmallNP = 128;        // Schur dimension factored in one workgroup's LDS
+constexpr int kMaxPoses = 2048;      // 6 * 2048 = 12288: Hs 1.2 GB, far beyond any LocalBA window
+constexpr int kCB = 32;              // blocked Cholesky panel width (Schur dimension > kSmallNP)
 constexpr int kRedBlocks = 16384;    // partial-sum region stride (blocks) for scalar reductions
 
 struct Quat { double x, y, z, w; };
@@ -171,14 +173,15 @@ struct Graph {
     double *Hll, *bl;      // [Lm][9], [Lm][3]
     double *Hpp, *bp;      // [P][36], [P][6]
     double *Dinv;          // [Lm][9]
-    double *Y;             // [kNP][Kpad] row-major
+    double *Y;             // [NP][Kpad] row-major
     double *w;             // [Kpad]
-    double *slab;          // [S][kNP][kNP]
-    double *Hs, *bs;       // [kNP][kNP], [kNP]
+    double *slab;          // [S][NP][NP]
+    double *Hs, *bs;       // [NP][NP], [NP]
     double *x;             // [6P + 3Lm]
     double *partial;       // [4][kRedBlocks]
     double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok
     int Kpad, S;
+    int NP;                // Schur dimension 6P padded to a multiple of kCB
 };
 
 __device__ inline void edge_error(const Graph &g, const EdgeDev &e, const Pose *T, const double *X, double err[3]) {
@@ -461,18 +464,19 @@ __global__ __launch_bounds__(64) void lba_syrk_mfma(Graph g, int ntile, int kchu
         const double a = ya[k], b = yb[k];
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
     }
-    double *out = g.slab + (long long)s * kNP * kNP;
+    const long long NP = g.NP;
+    double *out = g.slab + (long long)s * NP * NP;
     // C/D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * reg
     for (int r = 0; r < 4; r++) {
         const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
-        out[(long long)row * kNP + col] = acc[r];
+        out[(long long)row * NP + col] = acc[r];
     }
 }
 
 __global__ __launch_bounds__(256) void lba_schur_reduce(Graph g, double lambda) {
     const int n6 = 6 * g.P;
     const int r = blockIdx.x;  // row
-    const long long K = g.Kpad;
+    const long long K = g.Kpad, NP = g.NP;
     // b_schur[r] = b_p[r] - (Y w)[r]
     __shared__ double sh[256];
     double acc = 0;
@@ -488,23 +492,37 @@ __global__ __launch_bounds__(256) void lba_schur_reduce(Graph g, double lambda) 
     for (int c = threadIdx.x; c < n6; c += 256) {
         const int lo = min(r, c), hi = max(r, c);   // slabs hold upper tiles
         double v = 0;
-        for (int s = 0; s < g.S; s++) v += g.slab[(long long)s * kNP * kNP + (long long)lo * kNP + hi];
+        for (int s = 0; s < g.S; s++) v += g.slab[(long long)s * NP * NP + (long long)lo * NP + hi];
         double h = 0;
         if (r / 6 == c / 6) h = g.Hpp[36 * (r / 6) + 6 * (r % 6) + (c % 6)];
         if (r == c) h += lambda;
-        g.Hs[(long long)r * kNP + c] = h - v;
+        g.Hs[(long long)r * NP + c] = h - v;
     }
 }
 
-// dense Cholesky of the n6 x n6 Schur matrix in LDS + forward / back substitution
-// (replaces LinearSolverEigen's SimplicialLDLT; failure -> the trial is rejected,
-// optimization_algorithm_levenberg.cpp:126-127)
-__global__ __launch_bounds__(256) void lba_chol_solve(Graph g) {
-    extern __shared__ double A[];   // n6 x (n6 + 1), column n6 = right-hand side
+// Dense Cholesky of the n6 x n6 Schur matrix + forward / back substitution (replaces
+// LinearSolverEigen's SimplicialLDLT, linear_solver_eigen.h:94-124; a non-positive pivot ->
+// ok = 0 and the LM trial is rejected, optimization_algorithm_levenberg.cpp:126-127).
+//
+// n6 <= kSmallNP: one 1024-thread workgroup, matrix in LDS, right-looking column sweep.
+// The scaled column j is copied to `col` so the rank-1 trailing update reads two broadcast
+// vectors; the update is spread over a 32 x 32 thread grid with fixed strides (no div/mod).
+// The two triangular solves run in wave 0 with the right-hand side in registers (lanes own
+// rows lane and lane + 64), the solved value broadcast by a cross-lane shuffle.
+__device__ inline double wave_bcast2(double v0, double v1, int k) {
+    const double a = __shfl(v0, k & 63), b = __shfl(v1, k & 63);
+    return (k < 64) ? a : b;
+}
+
+__global__ __launch_bounds__(1024) void lba_chol_small(Graph g) {
+    extern __shared__ double A[];   // n x ld
+    __shared__ double col[kSmallNP];
     const int n = 6 * g.P, ld = n + 1, tid = threadIdx.x;
-    for (int i = tid; i < n * n; i += 256) A[(i / n) * ld + i % n] = g.Hs[(long long)(i / n) * kNP + i % n];
-    for (int i = tid; i < n; i += 256) A[i * ld + n] = g.bs[i];
+    const long long NP = g.NP;
+    for (int r = tid >> 5; r < n; r += 32)
+        for (int c = tid & 31; c <= r; c += 32) A[r * ld + c] = g.Hs[r * NP + c];
     __syncthreads();
+    const int ty = tid >> 5, tx = tid & 31;
     for (int j = 0; j < n; j++) {
         const double d = A[j * ld + j];
         if (!(d > 0)) {                 // uniform: every thread read the same value
@@ -512,32 +530,169 @@ __global__ __launch_bounds__(256) void lba_chol_solve(Graph g) {
             return;
         }
         const double ljj = sqrt(d);
-        for (int i = j + 1 + tid; i < n; i += 256) A[i * ld + j] /= ljj;
+        for (int i = j + 1 + tid; i < n; i += 1024) {
+            const double v = A[i * ld + j] / ljj;
+            A[i * ld + j] = v;
+            col[i] = v;
+        }
         __syncthreads();
         if (tid == 0) A[j * ld + j] = ljj;
-        const int m = n - j - 1;
-        for (int t = tid; t < m * m; t += 256) {
-            const int r = j + 1 + t / m, c = j + 1 + t % m;
-            if (c <= r) A[r * ld + c] -= A[r * ld + j] * A[c * ld + j];
+        for (int r = j + 1 + ty; r < n; r += 32) {
+            const double lr = col[r];
+            for (int c = j + 1 + tx; c <= r; c += 32) A[r * ld + c] -= lr * col[c];
         }
         __syncthreads();
     }
-    for (int k = 0; k < n; k++) {       // L y = b (column sweep)
-        const double yk = A[k * ld + n] / A[k * ld + k];
-        __syncthreads();
-        if (tid == 0) A[k * ld + n] = yk;
-        for (int i = k + 1 + tid; i < n; i += 256) A[i * ld + n] -= A[i * ld + k] * yk;
-        __syncthreads();
+    if (tid >= 64) return;
+    const int lane = tid;
+    double y0 = lane < n ? g.bs[lane] : 0.0, y1 = lane + 64 < n ? g.bs[lane + 64] : 0.0;
+    for (int k = 0; k < n; k++) {       // L y = b
+        const double yk = wave_bcast2(y0, y1, k) / A[k * ld + k];
+        if (lane == k) y0 = yk;
+        else if (lane > k && lane < n) y0 -= A[lane * ld + k] * yk;
+        if (lane + 64 == k) y1 = yk;
+        else if (lane + 64 > k && lane + 64 < n) y1 -= A[(lane + 64) * ld + k] * yk;
     }
     for (int k = n - 1; k >= 0; k--) {  // L^T x = y
-        const double xk = A[k * ld + n] / A[k * ld + k];
+        const double xk = wave_bcast2(y0, y1, k) / A[k * ld + k];
+        if (lane == k) y0 = xk;
+        else if (lane < k) y0 -= A[k * ld + lane] * xk;
+        if (lane + 64 == k) y1 = xk;
+        else if (lane + 64 < k) y1 -= A[k * ld + lane + 64] * xk;
+    }
+    if (lane < n) g.x[lane] = y0;
+    if (lane + 64 < n) g.x[lane + 64] = y1;
+    if (lane == 0) g.scalars[4] = 1;
+}
+
+// n6 > kSmallNP: blocked right-looking Cholesky in place on Hs (lower triangle), panel
+// width kCB = 32. Per panel kb: lba_chol_panel factors the diagonal block in LDS (every
+// workgroup redundantly; workgroup 0 stores it) and solves 256 rows of the panel below it
+// per workgroup (one thread per row, forward substitution against L_kk); lba_chol_update
+// subtracts L_panel L_panel^T from the trailing lower tiles on FP64 MFMA (one wave per
+// 16 x 16 tile, K = 32 = 8 x v_mfma_f64_16x16x4f64).
+__global__ __launch_bounds__(256) void lba_chol_panel(Graph g, int kb) {
+    __shared__ double D[kCB][kCB + 1];
+    const int n = 6 * g.P, tid = threadIdx.x;
+    const long long NP = g.NP;
+    const int nb = min(kCB, n - kb);
+    for (int t = tid; t < kCB * kCB; t += 256) {
+        const int r = t >> 5, c = t & 31;
+        D[r][c] = (r < nb && c < nb && c <= r) ? g.Hs[(kb + r) * NP + kb + c] : 0.0;
+    }
+    __syncthreads();
+    for (int j = 0; j < nb; j++) {      // unblocked factor of the diagonal block
+        const double d = D[j][j];       // uniform after the barrier
+        if (!(d > 0)) {
+            if (tid == 0 && blockIdx.x == 0) g.scalars[4] = 0;
+            break;
+        }
+        const double ljj = sqrt(d);
         __syncthreads();
-        if (tid == 0) A[k * ld + n] = xk;
-        for (int i = tid; i < k; i += 256) A[i * ld + n] -= A[k * ld + i] * xk;
+        if (tid > j && tid < nb) D[tid][j] /= ljj;
+        if (tid == j) D[j][j] = ljj;
+        __syncthreads();
+        if (tid > j && tid < nb) {
+            const double v = D[tid][j];
+            for (int c = j + 1; c <= tid; c++) D[tid][c] -= v * D[c][j];
+        }
         __syncthreads();
     }
-    for (int i = tid; i < n; i += 256) g.x[i] = A[i * ld + n];
-    if (tid == 0) g.scalars[4] = 1;
+    if (blockIdx.x == 0)
+        for (int t = tid; t < kCB * kCB; t += 256) {
+            const int r = t >> 5, c = t & 31;
+            if (r < nb && c <= r) g.Hs[(kb + r) * NP + kb + c] = D[r][c];
+        }
+    const int row = kb + nb + blockIdx.x * 256 + tid;
+    if (row >= n) return;
+    double a[kCB];
+    double *Ar = g.Hs + row * NP + kb;
+#pragma unroll
+    for (int c = 0; c < kCB; c++) a[c] = c < nb ? Ar[c] : 0.0;
+#pragma unroll
+    for (int c = 0; c < kCB; c++) {     // x L_kk^T = a  ->  forward substitution
+        if (c < nb) {
+            double v = a[c];
+#pragma unroll
+            for (int k = 0; k < c; k++) v -= a[k] * D[c][k];
+            a[c] = v / D[c][c];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < kCB; c++) if (c < nb) Ar[c] = a[c];
+}
+
+__global__ __launch_bounds__(64) void lba_chol_update(Graph g, int kb, int ntile) {
+    // lower 16 x 16 tiles (I >= J) of the trailing matrix, rows / cols >= kb + kCB
+    const int lane = threadIdx.x;
+    int t = blockIdx.x, I = 0;
+    while (t > I) { t -= I + 1; I++; }
+    const int J = t;
+    const long long NP = g.NP;
+    const int base = kb + kCB;
+    const double *la = g.Hs + (base + 16 * I + (lane & 15)) * NP + kb;
+    const double *lb = g.Hs + (base + 16 * J + (lane & 15)) * NP + kb;
+    double4_t acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < kCB; k += 4) {
+        const int kk = k + (lane >> 4);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(la[kk], lb[kk], acc, 0, 0, 0);
+    }
+    for (int r = 0; r < 4; r++) {
+        const int row = base + 16 * I + (lane >> 4) + 4 * r, c = base + 16 * J + (lane & 15);
+        if (c <= row) g.Hs[row * NP + c] -= acc[r];
+    }
+}
+
+// triangular solves on the blocked factor: one 1024-thread workgroup, rhs in LDS; wave 0
+// solves each 32-row diagonal block serially, then every thread updates the remaining rows.
+__global__ __launch_bounds__(1024) void lba_chol_solve_blocked(Graph g) {
+    extern __shared__ double y[];
+    const int n = 6 * g.P, tid = threadIdx.x;
+    const long long NP = g.NP;
+    const double *L = g.Hs;
+    for (int i = tid; i < n; i += 1024) y[i] = g.bs[i];
+    __syncthreads();
+    for (int kb = 0; kb < n; kb += kCB) {
+        const int nb = min(kCB, n - kb);
+        if (tid < 64) {
+            double v = tid < nb ? y[kb + tid] : 0.0;
+            for (int k = 0; k < nb; k++) {
+                const double yk = __shfl(v, k) / L[(kb + k) * NP + kb + k];
+                if (tid == k) v = yk;
+                else if (tid > k && tid < nb) v -= L[(kb + tid) * NP + kb + k] * yk;
+            }
+            if (tid < nb) y[kb + tid] = v;
+        }
+        __syncthreads();
+        for (int r = kb + nb + tid; r < n; r += 1024) {
+            double v = y[r];
+            const double *Lr = L + r * NP + kb;
+            for (int k = 0; k < nb; k++) v -= Lr[k] * y[kb + k];
+            y[r] = v;
+        }
+        __syncthreads();
+    }
+    for (int kb = ((n - 1) / kCB) * kCB; kb >= 0; kb -= kCB) {
+        const int nb = min(kCB, n - kb);
+        if (tid < 64) {
+            double v = tid < nb ? y[kb + tid] : 0.0;
+            for (int k = nb - 1; k >= 0; k--) {
+                const double xk = __shfl(v, k) / L[(kb + k) * NP + kb + k];
+                if (tid == k) v = xk;
+                else if (tid < k) v -= L[(kb + k) * NP + kb + tid] * xk;
+            }
+            if (tid < nb) y[kb + tid] = v;
+        }
+        __syncthreads();
+        for (int r = tid; r < kb; r += 1024) {
+            double v = y[r];
+            for (int k = 0; k < nb; k++) v -= L[(kb + k) * NP + r] * y[kb + k];
+            y[r] = v;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += 1024) g.x[i] = y[i];
 }
 
 __global__ void lba_set_ok(Graph g) { g.scalars[4] = 1; }
@@ -744,7 +899,20 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
                 const int kchunk = (((g.Kpad + g.S - 1) / g.S + 3) / 4) * 4;  // S * kchunk >= Kpad
                 lba_syrk_mfma<<<dim3(npair, g.S), 64, 0, s>>>(g, ntile, kchunk);
                 lba_schur_reduce<<<n6, 256, 0, s>>>(g, lambda);
-                lba_chol_solve<<<1, 256, sizeof(double) * n6 * (n6 + 1), s>>>(g);
+                if (n6 <= kSmallNP) {
+                    lba_chol_small<<<1, 1024, sizeof(double) * n6 * (n6 + 1), s>>>(g);
+                } else {
+                    lba_set_ok<<<1, 1, 0, s>>>(g);
+                    for (int kb = 0; kb < n6; kb += kCB) {
+                        const int rows = n6 - kb - kCB;
+                        lba_chol_panel<<<std::max(1, (rows + 255) / 256), 256, 0, s>>>(g, kb);
+                        if (rows > 0) {
+                            const int nt = (rows + 15) / 16;
+                            lba_chol_update<<<nt * (nt + 1) / 2, 64, 0, s>>>(g, kb, nt);
+                        }
+                    }
+                    lba_chol_solve_blocked<<<1, 1024, sizeof(double) * n6, s>>>(g);
+                }
             } else {
                 lba_set_ok<<<1, 1, 0, s>>>(g);
             }
@@ -887,14 +1055,17 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.pt_start = e->pt_start.as<int>(); g.pt_items = e->pt_items.as<int>();
         g.ps_start = e->ps_start.as<int>(); g.ps_items = e->ps_items.as<int>();
         g.Kpad = std::max(4, ((3 * A.Lm + 3) / 4) * 4);
-        g.S = std::max(1, std::min(64, g.Kpad / 256));
+        g.NP = std::max(kCB, ((6 * A.P + kCB - 1) / kCB) * kCB);
+        const size_t NP = (size_t)g.NP;
+        // K slices of the SYRK: enough waves to fill the chip, slabs capped at ~1 GB
+        g.S = std::max(1, std::min({64, g.Kpad / 256, (int)std::max<size_t>(1, (size_t(1) << 27) / (NP * NP))}));
         if (e->con.ensure(sizeof(double) * 36 * std::max(nact, 1)) || e->hpl.ensure(sizeof(double) * 18 * std::max(nact, 1)) ||
             e->Hll.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) || e->bl.ensure(sizeof(double) * 3 * std::max(A.Lm, 1)) ||
             e->Hpp.ensure(sizeof(double) * 36 * std::max(A.P, 1)) || e->bp.ensure(sizeof(double) * 6 * std::max(A.P, 1)) ||
             e->Dinv.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) ||
-            e->Y.ensure(sizeof(double) * kNP * (size_t)g.Kpad) || e->w.ensure(sizeof(double) * g.Kpad) ||
-            e->slab.ensure(sizeof(double) * (size_t)g.S * kNP * kNP) || e->Hs.ensure(sizeof(double) * kNP * kNP) ||
-            e->bs.ensure(sizeof(double) * kNP) || e->x.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)) ||
+            e->Y.ensure(sizeof(double) * NP * (size_t)g.Kpad) || e->w.ensure(sizeof(double) * g.Kpad) ||
+            e->slab.ensure(sizeof(double) * (size_t)g.S * NP * NP) || e->Hs.ensure(sizeof(double) * NP * NP) ||
+            e->bs.ensure(sizeof(double) * NP) || e->x.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)) ||
             e->bfull.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)))
             return -1;
         g.con = e->con.as<double>(); g.hpl = e->hpl.as<double>();
@@ -903,9 +1074,10 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.Dinv = e->Dinv.as<double>(); g.Y = e->Y.as<double>(); g.w = e->w.as<double>();
         g.slab = e->slab.as<double>(); g.Hs = e->Hs.as<double>(); g.bs = e->bs.as<double>();
         g.x = e->x.as<double>();
-        if (hipMemsetAsync(g.Y, 0, sizeof(double) * kNP * (size_t)g.Kpad, s) != hipSuccess ||
+        if (hipMemsetAsync(g.Y, 0, sizeof(double) * NP * (size_t)g.Kpad, s) != hipSuccess ||
             hipMemsetAsync(g.w, 0, sizeof(double) * g.Kpad, s) != hipSuccess ||
-            hipMemsetAsync(g.slab, 0, sizeof(double) * (size_t)g.S * kNP * kNP, s) != hipSuccess ||
+            hipMemsetAsync(g.slab, 0, sizeof(double) * (size_t)g.S * NP * NP, s) != hipSuccess ||
+            hipMemsetAsync(g.Hs, 0, sizeof(double) * NP * NP, s) != hipSuccess ||
             hipMemsetAsync(g.x, 0, sizeof(double) * (6 * A.P + 3 * A.Lm + 8), s) != hipSuccess)
             return -1;
         // trial buffers start equal to the current estimate (inactive vertices never change)
