@@ -133,6 +133,57 @@ def bench_rgbd(amd, args, dist, world):
                    "bytes_per_frame": 640 * 480 + 1000 * 60 + 1000 * 12}}
 
 
+def bench_track(amd, args, dist, world, with_cpu):
+    """§8f rank 1: per-frame tracking matchers on B independent (frame, local map) problems
+    resident in HBM: Frame::isInFrustum + SearchByProjection(F, vpMapPoints, th=1) (as in
+    Tracking::SearchLocalPoints) + SearchByProjection(CurrentFrame, LastFrame, 15, stereo)
+    (TrackWithMotionModel). 2000 keypoints, 3000 local map points, 1500 last-frame keypoints
+    per frame (synth.tracking_problem)."""
+    from orbslam2_amd import synth
+    from orbslam2_amd import dist as odist
+    B = args.track_batch
+    probs = [synth.tracking_problem(300 + i, motion=("forward", "backward", "static")[i % 3]) for i in range(8)]
+    t = amd.Tracker()
+    t.reserve(B, 2000, 3000)
+    for s in range(B):
+        t.stage(s, probs[s % len(probs)])
+
+    def step():
+        t.run_local_batch(B, 0.5, 1.0, 0.8)
+        t.run_frame_batch(B, 15.0, False, True)
+
+    for _ in range(2):
+        step()
+    amd.device_sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.track_steps):
+        step()
+    amd.device_sync()
+    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    nm, _, _ = t.fetch(0, 2000)
+    res = {"track_frames_per_s": round(world * B * args.track_steps / dt, 2),
+           "track": {"frames_per_step": B, "ms_per_step": round(1000 * dt / args.track_steps, 3),
+                     "keypoints": 2000, "map_points": 3000, "last_keypoints": 1500,
+                     "frame_matches_slot0": int(nm)}}
+    t.close()
+    if with_cpu:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 3.0:
+            p = probs[n % len(probs)]
+            oracle.search_local_points(p, 0.5, 1.0, 0.8)
+            oracle.search_by_projection_frame(p, 15.0, False, True)
+            n += 1
+        cdt = time.perf_counter() - t0
+        res["track"]["cpu_baseline"] = {"value": round(n / cdt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+                                        "sample": f"{n} frames (8 distinct problems), oracle, single thread, {cdt:.1f} s"}
+    return res
+
+
 def load_traffic(kernel: str, batch: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
     f = ROOT / "profiles" / "pmc_traffic.json"
@@ -164,6 +215,9 @@ def main():
     ap.add_argument("--rgbd-batch", type=int, default=256)
     ap.add_argument("--rgbd-steps", type=int, default=10)
     ap.add_argument("--no-rgbd", action="store_true")
+    ap.add_argument("--track-batch", type=int, default=256)
+    ap.add_argument("--track-steps", type=int, default=10)
+    ap.add_argument("--no-track", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -274,6 +328,8 @@ def main():
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
     if not args.no_rgbd:
         out.update(bench_rgbd(amd, args, dist, world))
+    if not args.no_track:
+        out.update(bench_track(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if not args.no_lba:
         out.update(bench_localba(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

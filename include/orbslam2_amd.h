@@ -138,6 +138,88 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
 int orbm_search_init_fetch(orbx_engine *e, int pair, int *matches12, float *prev_xy, int cap,
                            int *nmatches);
 
+/* -------- tracking matchers (replace Frame::isInFrustum and the two per-frame
+ * ORBmatcher::SearchByProjection overloads used by Tracking) -------- */
+
+/* The Frame members the tracking matchers read (include/Frame.h:195-300). Host pointers. */
+typedef struct {
+    int32_t n;                   /* N */
+    const orbx_kp *keys_un;      /* mvKeysUn[N] (octave / angle equal mvKeys') */
+    const float *u_right;        /* mvuRight[N]; < 0 = no stereo */
+    const uint8_t *desc;         /* mDescriptors, N x 32 */
+    float Tcw[12];               /* mTcw rows 0..2 = [Rcw | tcw], CV_32F */
+    float Ow[3];                 /* mOw (Frame::UpdatePoseMatrices, Frame.cc:453-473) */
+    float fx, fy, cx, cy, mbf, mb;
+    float min_x, max_x, min_y, max_y;   /* mnMinX .. mnMaxY (Frame::ComputeImageBounds) */
+    int32_t nlevels;             /* mnScaleLevels */
+    float log_scale_factor;      /* mfLogScaleFactor = log(mfScaleFactor) */
+    float scale_factors[16];     /* mvScaleFactors */
+} orbt_frame;
+
+#define ORBT_MP_BAD 1            /* MapPoint::isBad() */
+#define ORBT_MP_HAS_OBS 2        /* MapPoint::Observations() > 0 */
+#define ORBT_MP_IN_FRAME 4       /* mnLastFrameSeen == CurrentFrame.mnId (Tracking.cc:1749-1769) */
+
+/* The map points a matcher reads (MapPoint getters). Host pointers. */
+typedef struct {
+    int32_t n;
+    const float *Xw;             /* [n][3] GetWorldPos() */
+    const float *normal;         /* [n][3] GetNormal() */
+    const float *min_dist;       /* [n] mfMinDistance (GetMinDistanceInvariance = 0.8f * this) */
+    const float *max_dist;       /* [n] mfMaxDistance (GetMaxDistanceInvariance = 1.2f * this) */
+    const uint8_t *desc;         /* [n][32] GetDescriptor() */
+    const uint8_t *flags;        /* [n] ORBT_MP_* */
+} orbt_mappoints;
+
+/* MapPoint tracking members written by Frame::isInFrustum (Frame.cc:556-574). Any pointer
+ * may be NULL. */
+typedef struct {
+    uint8_t *in_view;            /* mbTrackInView */
+    float *proj_x, *proj_y, *proj_xr, *view_cos;   /* mTrackProjX/Y/XR, mTrackViewCos */
+    int32_t *level;              /* mnTrackScaleLevel */
+} orbt_view;
+
+typedef struct orbt_engine orbt_engine;
+
+int orbt_create(orbt_engine **out);
+void orbt_destroy(orbt_engine *e);
+
+/* Tracking::SearchLocalPoints (Tracking.cc:1745-1810) minus the MapPoint counters:
+ * mbTrackInView = !(flags & (BAD | IN_FRAME)) && Frame::isInFrustum(pMP, view_cos_limit)
+ * (Frame.cc:490-578, PredictScale MapPoint.cc:612-626), then
+ * ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th) (ORBmatcher.h:82,
+ * ORBmatcher.cc:78-176) with the reference's greedy claim order (map points in order; a
+ * keypoint owned by a map point with Observations() > 0 is skipped by later ones).
+ * kp_blocked[N] (may be NULL): 1 where F.mvpMapPoints[idx] holds a point with
+ * Observations() > 0 on entry. owner[N] out: map point index assigned to keypoint idx, or
+ * -1 = untouched. view may be NULL. */
+int orbt_search_local_points(orbt_engine *e, const orbt_frame *F, const orbt_mappoints *M,
+                             float view_cos_limit, float th, float nnratio, const uint8_t *kp_blocked,
+                             orbt_view *view, int32_t *owner, int32_t *nmatches);
+
+/* ORBmatcher(nnratio, check_ori).SearchByProjection(CurrentFrame, LastFrame, th, bMono)
+ * (ORBmatcher.h:102, ORBmatcher.cc:1741-1904; Tracking::TrackWithMotionModel). last_mp[i]
+ * = index into M of LastFrame.mvpMapPoints[i] (-1 = NULL); last_outlier[i] = mvbOutlier[i]
+ * (may be NULL). owner[cur->n] out: -1 untouched, >= 0 map point index assigned, -2 =
+ * assigned and then cleared by the rotation-consistency check (mvpMapPoints[idx] = NULL).
+ * *nmatches = the reference's return value. */
+int orbt_search_by_projection_frame(orbt_engine *e, const orbt_frame *cur, const orbt_frame *last,
+                                    const int32_t *last_mp, const uint8_t *last_outlier,
+                                    const orbt_mappoints *M, float th, int mono, int check_ori,
+                                    const uint8_t *kp_blocked, int32_t *owner, int32_t *nmatches);
+
+/* Batched device-resident form (throughput path): stage independent problems into slots
+ * (host -> HBM), run one launch chain over all slots, fetch per slot. `last`, `last_mp`,
+ * `last_outlier` may be NULL when only orbt_run_local_batch is used. */
+int orbt_reserve(orbt_engine *e, int n_slots, int cap_kp, int cap_mp);
+int orbt_stage(orbt_engine *e, int slot, const orbt_frame *F, const orbt_mappoints *M,
+               const orbt_frame *last, const int32_t *last_mp, const uint8_t *last_outlier,
+               const uint8_t *kp_blocked);
+int orbt_run_local_batch(orbt_engine *e, int n_slots, float view_cos_limit, float th, float nnratio,
+                         void *stream);
+int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int check_ori, void *stream);
+int orbt_fetch(orbt_engine *e, int slot, orbt_view *view, int32_t *owner, int32_t *nmatches);
+
 /* -------- local bundle adjustment (replaces Optimizer::LocalBundleAdjustment) -------- */
 
 /* The graph Optimizer::LocalBundleAdjustment (Optimizer.cc:646-898) builds from the map,

@@ -331,3 +331,97 @@ def lba_solve(prob: dict, stop: bool = False):
     out["chi2"] = tuple(R.chi2)
     out["stopped"] = R.stopped
     return out
+
+
+# ---- tracking matchers (track_oracle.c): Frame::isInFrustum + both per-frame
+# ORBmatcher::SearchByProjection overloads. Problems are the dicts of synth.tracking_problem.
+class OrbtFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("keys_un", C.c_void_p), ("u_right", C.c_void_p), ("desc", C.c_void_p),
+                ("Tcw", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("mb", C.c_float),
+                ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float),
+                ("nlevels", C.c_int32), ("log_scale_factor", C.c_float), ("scale_factors", C.c_float * 16)]
+
+
+class OrbtMapPoints(C.Structure):
+    _fields_ = [("n", C.c_int32), ("Xw", C.c_void_p), ("normal", C.c_void_p), ("min_dist", C.c_void_p),
+                ("max_dist", C.c_void_p), ("desc", C.c_void_p), ("flags", C.c_void_p)]
+
+
+class OrbtView(C.Structure):
+    _fields_ = [("in_view", C.c_void_p), ("proj_x", C.c_void_p), ("proj_y", C.c_void_p),
+                ("proj_xr", C.c_void_p), ("view_cos", C.c_void_p), ("level", C.c_void_p)]
+
+
+def make_orbt_frame(fr: dict):
+    keep = {"keys_un": np.ascontiguousarray(fr["keys_un"], KP_DTYPE),
+            "u_right": np.ascontiguousarray(fr["u_right"], np.float32),
+            "desc": np.ascontiguousarray(fr["desc"], np.uint8)}
+    F = OrbtFrame()
+    F.n = len(keep["keys_un"])
+    F.keys_un, F.u_right, F.desc = (keep[k].ctypes.data for k in ("keys_un", "u_right", "desc"))
+    F.Tcw[:] = [float(v) for v in np.asarray(fr["Tcw"], np.float32).reshape(-1)[:12]]
+    F.Ow[:] = [float(v) for v in np.asarray(fr["Ow"], np.float32)]
+    for k in ("fx", "fy", "cx", "cy", "mbf", "mb", "min_x", "max_x", "min_y", "max_y", "log_scale_factor"):
+        setattr(F, k, float(fr[k]))
+    F.nlevels = int(fr["nlevels"])
+    sf = np.zeros(16, np.float32)
+    sf[: F.nlevels] = fr["scale_factors"]
+    F.scale_factors[:] = [float(v) for v in sf]
+    return F, keep
+
+
+def make_orbt_map(mp: dict):
+    keep = {"Xw": np.ascontiguousarray(mp["Xw"], np.float32), "normal": np.ascontiguousarray(mp["normal"], np.float32),
+            "min_dist": np.ascontiguousarray(mp["min_dist"], np.float32),
+            "max_dist": np.ascontiguousarray(mp["max_dist"], np.float32),
+            "desc": np.ascontiguousarray(mp["desc"], np.uint8), "flags": np.ascontiguousarray(mp["flags"], np.uint8)}
+    M = OrbtMapPoints(len(keep["Xw"]), *(keep[k].ctypes.data for k in ("Xw", "normal", "min_dist", "max_dist", "desc",
+                                                                        "flags")))
+    return M, keep
+
+
+def logf(x: float) -> float:
+    L = lib()
+    L.orc_logf.argtypes = [C.c_float]
+    L.orc_logf.restype = C.c_float
+    return L.orc_logf(x)
+
+
+def search_local_points(prob: dict, cos_limit=0.5, th=1.0, nnratio=0.8):
+    """Tracking::SearchLocalPoints core: isInFrustum + SearchByProjection(F, vpMapPoints, th)."""
+    L = lib()
+    L.orc_search_local_points.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_void_p,
+                                          C.c_void_p, C.c_void_p]
+    F, k1 = make_orbt_frame(prob["frame"])
+    M, k2 = make_orbt_map(prob["map"])
+    n, m = F.n, M.n
+    view = {"in_view": np.zeros(max(m, 1), np.uint8), "proj_x": np.zeros(max(m, 1), np.float32),
+            "proj_y": np.zeros(max(m, 1), np.float32), "proj_xr": np.zeros(max(m, 1), np.float32),
+            "view_cos": np.zeros(max(m, 1), np.float32), "level": np.zeros(max(m, 1), np.int32)}
+    V = OrbtView(*(view[k].ctypes.data for k in ("in_view", "proj_x", "proj_y", "proj_xr", "view_cos", "level")))
+    owner = np.zeros(max(n, 1), np.int32)
+    blk = prob.get("kp_blocked")
+    blk = np.ascontiguousarray(blk, np.uint8) if blk is not None else None
+    nm = L.orc_search_local_points(C.byref(F), C.byref(M), cos_limit, th, nnratio,
+                                   blk.ctypes.data if blk is not None else None, C.byref(V), owner.ctypes.data)
+    return nm, owner[:n], {k: v[:m] for k, v in view.items()}
+
+
+def search_by_projection_frame(prob: dict, th=15.0, mono=False, check_ori=True):
+    """ORBmatcher(0.9, checkOri).SearchByProjection(CurrentFrame, LastFrame, th, bMono)."""
+    L = lib()
+    L.orc_search_by_projection_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                 C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    F, k1 = make_orbt_frame(prob["frame"])
+    Lf, k2 = make_orbt_frame(prob["last"])
+    M, k3 = make_orbt_map(prob["map"])
+    last_mp = np.ascontiguousarray(prob["last_mp"], np.int32)
+    last_out = np.ascontiguousarray(prob["last_outlier"], np.uint8)
+    owner = np.zeros(max(F.n, 1), np.int32)
+    blk = prob.get("kp_blocked")
+    blk = np.ascontiguousarray(blk, np.uint8) if blk is not None else None
+    nm = L.orc_search_by_projection_frame(C.byref(F), C.byref(Lf), last_mp.ctypes.data, last_out.ctypes.data,
+                                          C.byref(M), th, 1 if mono else 0, 1 if check_ori else 0,
+                                          blk.ctypes.data if blk is not None else None, owner.ctypes.data)
+    return nm, owner[: F.n]

@@ -1,0 +1,299 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY (see orb_oracle.h). Never linked into the product.
+ *
+ * Single-threaded C restatement of the per-frame tracking matchers of ORB-SLAM2-noted:
+ *   Frame::isInFrustum            src/Frame.cc:490-578
+ *   MapPoint::PredictScale        src/MapPoint.cc:612-626 (Frame overload)
+ *   ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
+ *                                 src/ORBmatcher.cc:78-176 (+ RadiusByViewingCos :179-191)
+ *   ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
+ *                                 src/ORBmatcher.cc:1741-1904
+ *   Tracking::SearchLocalPoints   src/Tracking.cc:1745-1810 (the in-view selection)
+ *
+ * Float semantics pinned (SURVEY.md Appendix A + A.8 in DESIGN.md):
+ *   - cv::Mat float products R*X + t (3x3 * 3x1 + 3x1): OpenCV's small-matrix gemm path,
+ *     float products summed left to right in float, then the float add of t;
+ *   - cv::norm(float 3-vector): double sum of squares, sqrt in double, stored as float;
+ *   - Mat::dot(float 3-vectors): double products summed left to right;
+ *   - log(float) resolves to std::log(float) = glibc logf (`using namespace std` from
+ *     DBoW2/TemplatedVocabulary.h:36); restated here as glibc 2.35's table algorithm and
+ *     pinned exhaustively by oracle/tools/check_logf.c (0 mismatches over every positive
+ *     float);
+ *   - `1.0 / z` with float z is a double division rounded to float (ORBmatcher.cc:1794);
+ *   - round(float) = roundf (half away from zero), ceil(float) = ceilf.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "orb_oracle.h"
+#include "track_oracle.h"
+
+/* ---- glibc 2.35 logf (sysdeps/ieee754/flt-32/e_logf.c, e_logf_data.c), restated ---- */
+static const double LOGF_INVC[16] = {
+    0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
+    0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0,  0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
+    0x1.0953f419900a7p+0, 0x1p+0,               0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1,
+    0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
+static const double LOGF_LOGC[16] = {
+    -0x1.57bf7808caadep-2, -0x1.2bef0a7c06ddbp-2, -0x1.01eae7f513a67p-2, -0x1.b31d8a68224e9p-3,
+    -0x1.6574f0ac07758p-3, -0x1.1aa2bc79c81p-3,   -0x1.a4e76ce8c0e5ep-4, -0x1.1973c5a611cccp-4,
+    -0x1.252f438e10c1ep-5, 0x0p+0,                0x1.aa5aa5df25984p-5,  0x1.c5e53aa362eb4p-4,
+    0x1.526e57720db08p-3,  0x1.bc2860d22477p-3,   0x1.1058bc8a07ee1p-2,  0x1.4043057b6ee09p-2};
+static const double LOGF_A[3] = {-0x1.00ea348b88334p-2, 0x1.5575b0be00b6ap-2, -0x1.ffffef20a4123p-2};
+static const double LOGF_LN2 = 0x1.62e42fefa39efp-1;
+
+float orc_logf(float x) {
+    uint32_t ix;
+    memcpy(&ix, &x, 4);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        if (ix * 2 == 0) return -INFINITY;
+        if (ix == 0x7f800000u) return x;
+        if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return NAN;
+        float y = x * 0x1p23f;               /* subnormal: normalise */
+        memcpy(&ix, &y, 4);
+        ix -= 23u << 23;
+    }
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> (23 - 4)) % 16);
+    const int k = (int32_t)tmp >> 23;
+    const uint32_t iz = ix - (tmp & (0x1ffu << 23));
+    float zf;
+    memcpy(&zf, &iz, 4);
+    const double z = zf;
+    const double r = z * LOGF_INVC[i] - 1;
+    const double y0 = LOGF_LOGC[i] + (double)k * LOGF_LN2;
+    const double r2 = r * r;
+    double y = LOGF_A[1] * r + LOGF_A[2];
+    y = LOGF_A[0] * r2 + y;
+    y = y * r2 + (y0 + r);
+    return (float)y;
+}
+
+/* R * X + t as cv::Mat CV_32F expressions evaluate it (pinned, see header) */
+static void mat_rx_t(const float T[12], const float X[3], float o[3]) {
+    for (int i = 0; i < 3; i++) {
+        const float *R = T + 4 * i;
+        float s = R[0] * X[0];
+        s = s + R[1] * X[1];
+        s = s + R[2] * X[2];
+        o[i] = s + R[3];
+    }
+}
+
+void orc_is_in_frustum(const orbt_frame *F, const orbt_mappoints *M, int i, float viewingCosLimit,
+                       uint8_t *in_view, float *px, float *py, float *pxr, float *vcos, int *lvl) {
+    *in_view = 0;
+    const float *P = M->Xw + 3 * i;
+    float Pc[3];
+    mat_rx_t(F->Tcw, P, Pc);
+    const float PcX = Pc[0], PcY = Pc[1], PcZ = Pc[2];
+    if (PcZ < 0.0f) return;                                        /* Frame.cc:509 */
+    const float invz = 1.0f / PcZ;
+    const float u = F->fx * PcX * invz + F->cx;
+    const float v = F->fy * PcY * invz + F->cy;
+    if (u < F->min_x || u > F->max_x) return;
+    if (v < F->min_y || v > F->max_y) return;
+    const float maxDistance = 1.2f * M->max_dist[i];               /* MapPoint.cc:555-559 */
+    const float minDistance = 0.8f * M->min_dist[i];
+    const float PO[3] = {P[0] - F->Ow[0], P[1] - F->Ow[1], P[2] - F->Ow[2]};
+    double ss = 0;
+    for (int k = 0; k < 3; k++) { const double t = PO[k]; ss += t * t; }
+    const float dist = (float)sqrt(ss);                           /* cv::norm */
+    if (dist < minDistance || dist > maxDistance) return;
+    const float *Pn = M->normal + 3 * i;
+    double dot = 0;
+    for (int k = 0; k < 3; k++) dot += (double)PO[k] * Pn[k];     /* Mat::dot */
+    const float viewCos = (float)(dot / dist);
+    if (viewCos < viewingCosLimit) return;
+    /* MapPoint::PredictScale(dist, Frame*) */
+    const float ratio = M->max_dist[i] / dist;
+    int nScale = (int)ceilf(orc_logf(ratio) / F->log_scale_factor);
+    if (nScale < 0) nScale = 0;
+    else if (nScale >= F->nlevels) nScale = F->nlevels - 1;
+    *in_view = 1;
+    *px = u;
+    *pxr = u - F->mbf * invz;
+    *py = v;
+    *lvl = nScale;
+    *vcos = viewCos;
+}
+
+static int frame_grid(const orbt_frame *F, orc_frame_grid *g) {
+    return orc_grid_build(g, (const orc_kp *)F->keys_un, F->desc, F->n, F->min_x, F->max_x, F->min_y,
+                          F->max_y);
+}
+
+int orc_search_local_points(const orbt_frame *F, const orbt_mappoints *M, float viewCosLimit, float th,
+                            float nnratio, const uint8_t *kp_blocked, orbt_view *view, int32_t *owner) {
+    const int TH_HIGH = 100;
+    const int N = F->n;
+    orc_frame_grid g;
+    frame_grid(F, &g);
+    uint8_t *blocked = (uint8_t *)calloc((size_t)N + 1, 1);
+    if (kp_blocked) memcpy(blocked, kp_blocked, (size_t)N);
+    int *cand = (int *)malloc(sizeof(int) * ((size_t)N + 1));
+    for (int k = 0; k < N; k++) owner[k] = -1;
+    const int bFactor = th != 1.0f;
+    int nmatches = 0;
+    for (int m = 0; m < M->n; m++) {
+        uint8_t inv = 0;
+        float px = 0, py = 0, pxr = 0, vc = 0;
+        int lvl = 0;
+        /* Tracking::SearchLocalPoints: points matched in this frame keep mbTrackInView
+         * false, bad points are skipped, the rest go through isInFrustum(pMP, 0.5) */
+        if (!(M->flags[m] & (ORBT_MP_BAD | ORBT_MP_IN_FRAME)))
+            orc_is_in_frustum(F, M, m, viewCosLimit, &inv, &px, &py, &pxr, &vc, &lvl);
+        if (view) {
+            if (view->in_view) view->in_view[m] = inv;
+            if (view->proj_x) view->proj_x[m] = inv ? px : 0;
+            if (view->proj_y) view->proj_y[m] = inv ? py : 0;
+            if (view->proj_xr) view->proj_xr[m] = inv ? pxr : 0;
+            if (view->view_cos) view->view_cos[m] = inv ? vc : 0;
+            if (view->level) view->level[m] = inv ? lvl : 0;
+        }
+        if (!inv) continue;
+        if (M->flags[m] & ORBT_MP_BAD) continue;
+        /* ORBmatcher::SearchByProjection(F, vpMapPoints, th), ORBmatcher.cc:78-176 */
+        float r = (vc > 0.998) ? 2.5f : 4.0f;                      /* RadiusByViewingCos */
+        if (bFactor) r *= th;
+        const float rs = r * F->scale_factors[lvl];
+        const int nc = orc_features_in_area(&g, px, py, rs, lvl - 1, lvl, cand, N + 1);
+        if (nc == 0) continue;
+        const uint8_t *dMP = M->desc + 32 * (size_t)m;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int idx = cand[c];
+            if (blocked[idx]) continue;
+            if (F->u_right[idx] > 0) {
+                const float er = fabsf(pxr - F->u_right[idx]);
+                if (er > rs) continue;
+            }
+            const int dist = orc_descriptor_distance(dMP, F->desc + 32 * (size_t)idx);
+            if (dist < bestDist) {
+                bestDist2 = bestDist; bestDist = dist;
+                bestLevel2 = bestLevel; bestLevel = F->keys_un[idx].octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = F->keys_un[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
+            owner[bestIdx] = m;
+            blocked[bestIdx] = (M->flags[m] & ORBT_MP_HAS_OBS) ? 1 : 0;
+            nmatches++;
+        }
+    }
+    free(cand); free(blocked);
+    orc_grid_free(&g);
+    return nmatches;
+}
+
+static void three_maxima30(const int *counts, int *ind1, int *ind2, int *ind3) {
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < 30; i++) {
+        const int s = counts[i];
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; *ind3 = *ind2; *ind2 = *ind1; *ind1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; *ind3 = *ind2; *ind2 = i; }
+        else if (s > max3) { max3 = s; *ind3 = i; }
+    }
+    if (max2 < 0.1f * (float)max1) { *ind2 = -1; *ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { *ind3 = -1; }
+}
+
+int orc_search_by_projection_frame(const orbt_frame *cur, const orbt_frame *last, const int32_t *last_mp,
+                                   const uint8_t *last_outlier, const orbt_mappoints *M, float th, int bMono,
+                                   int checkOri, const uint8_t *kp_blocked, int32_t *owner) {
+    const int TH_HIGH = 100, HISTO_LENGTH = 30;
+    const int N = cur->n;
+    orc_frame_grid g;
+    frame_grid(cur, &g);
+    uint8_t *blocked = (uint8_t *)calloc((size_t)N + 1, 1);
+    if (kp_blocked) memcpy(blocked, kp_blocked, (size_t)N);
+    int *cand = (int *)malloc(sizeof(int) * ((size_t)N + 1));
+    int *hist_bin = (int *)malloc(sizeof(int) * ((size_t)last->n + 1));
+    int *hist_idx = (int *)malloc(sizeof(int) * ((size_t)last->n + 1));
+    int nhist = 0;
+    for (int k = 0; k < N; k++) owner[k] = -1;
+    const float factor = HISTO_LENGTH / 360.0f;
+    /* twc = -Rcw^T tcw (small-matrix gemm with GEMM_1_T, alpha -1); tlc = Rlw twc + tlw */
+    float twc[3];
+    for (int i = 0; i < 3; i++) {
+        float s = cur->Tcw[i] * cur->Tcw[3];
+        s = s + cur->Tcw[4 + i] * cur->Tcw[7];
+        s = s + cur->Tcw[8 + i] * cur->Tcw[11];
+        twc[i] = -s;
+    }
+    float tlc[3];
+    mat_rx_t(last->Tcw, twc, tlc);
+    const int bForward = tlc[2] > cur->mb && !bMono;
+    const int bBackward = -tlc[2] > cur->mb && !bMono;
+    int nmatches = 0;
+    for (int i = 0; i < last->n; i++) {
+        const int m = last_mp[i];
+        if (m < 0) continue;
+        if (last_outlier && last_outlier[i]) continue;
+        float x3Dc[3];
+        mat_rx_t(cur->Tcw, M->Xw + 3 * (size_t)m, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        if (invzc < 0) continue;
+        const float u = cur->fx * xc * invzc + cur->cx;
+        const float v = cur->fy * yc * invzc + cur->cy;
+        if (u < cur->min_x || u > cur->max_x) continue;
+        if (v < cur->min_y || v > cur->max_y) continue;
+        const int nLastOctave = last->keys_un[i].octave;
+        const float radius = th * cur->scale_factors[nLastOctave];
+        int nc;
+        if (bForward) nc = orc_features_in_area(&g, u, v, radius, nLastOctave, -1, cand, N + 1);
+        else if (bBackward) nc = orc_features_in_area(&g, u, v, radius, 0, nLastOctave, cand, N + 1);
+        else nc = orc_features_in_area(&g, u, v, radius, nLastOctave - 1, nLastOctave + 1, cand, N + 1);
+        if (nc == 0) continue;
+        const uint8_t *dMP = M->desc + 32 * (size_t)m;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = cand[c];
+            if (blocked[i2]) continue;
+            if (cur->u_right[i2] > 0) {
+                const float ur = u - cur->mbf * invzc;
+                const float er = fabsf(ur - cur->u_right[i2]);
+                if (er > radius) continue;
+            }
+            const int dist = orc_descriptor_distance(dMP, cur->desc + 32 * (size_t)i2);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        }
+        if (bestDist <= TH_HIGH) {
+            owner[bestIdx2] = m;
+            blocked[bestIdx2] = (M->flags[m] & ORBT_MP_HAS_OBS) ? 1 : 0;
+            nmatches++;
+            if (checkOri) {
+                float rot = last->keys_un[i].angle - cur->keys_un[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == HISTO_LENGTH) bin = 0;
+                hist_bin[nhist] = bin;
+                hist_idx[nhist] = bestIdx2;
+                nhist++;
+            }
+        }
+    }
+    if (checkOri) {
+        int counts[30] = {0};
+        for (int k = 0; k < nhist; k++) counts[hist_bin[k]]++;
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima30(counts, &ind1, &ind2, &ind3);
+        for (int k = 0; k < nhist; k++) {
+            const int b = hist_bin[k];
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            owner[hist_idx[k]] = -2;                            /* mvpMapPoints[..] = NULL */
+            nmatches--;
+        }
+    }
+    free(cand); free(blocked); free(hist_bin); free(hist_idx);
+    orc_grid_free(&g);
+    return nmatches;
+}

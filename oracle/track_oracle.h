@@ -1,0 +1,24 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY. CPU restatement of the per-frame tracking matchers
+ * (Frame::isInFrustum, both ORBmatcher::SearchByProjection overloads used by Tracking) and
+ * glibc logf (see track_oracle.c). Uses the orbt_* POD types of the C-ABI header (types
+ * only; nothing of the product library is linked).
+ */
+#ifndef TRACK_ORACLE_H
+#define TRACK_ORACLE_H
+#include "../include/orbslam2_amd.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+float orc_logf(float x);
+void orc_is_in_frustum(const orbt_frame *F, const orbt_mappoints *M, int i, float viewingCosLimit,
+                       uint8_t *in_view, float *px, float *py, float *pxr, float *vcos, int *lvl);
+int orc_search_local_points(const orbt_frame *F, const orbt_mappoints *M, float viewCosLimit, float th,
+                            float nnratio, const uint8_t *kp_blocked, orbt_view *view, int32_t *owner);
+int orc_search_by_projection_frame(const orbt_frame *cur, const orbt_frame *last, const int32_t *last_mp,
+                                   const uint8_t *last_outlier, const orbt_mappoints *M, float th, int bMono,
+                                   int checkOri, const uint8_t *kp_blocked, int32_t *owner);
+#ifdef __cplusplus
+}
+#endif
+#endif

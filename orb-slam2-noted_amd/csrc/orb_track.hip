@@ -1,0 +1,831 @@
+// MI355X-native per-frame tracking matchers:
+//   Frame::isInFrustum                        Frame.cc:490-578 (+ MapPoint::PredictScale
+//                                             MapPoint.cc:612-626, glibc logf restated)
+//   ORBmatcher::SearchByProjection(F, vpMapPoints, th)      ORBmatcher.cc:78-176
+//   ORBmatcher::SearchByProjection(CurrentFrame, LastFrame, th, bMono)  ORBmatcher.cc:1741-1904
+//
+// Both matchers are greedy: map points (resp. last-frame keypoints) are visited in order and
+// a keypoint claimed by a map point with Observations() > 0 is skipped by every later one.
+// Everything that does not depend on the claims runs fully parallel, one thread per map
+// point (resp. last keypoint), in the *_cand kernels: frustum test, grid window, level /
+// stereo filters, Hamming distances, and the K smallest candidates by (distance, candidate
+// position) -- the (best, second) pair of the reference's sequential update is exactly the
+// two smallest (distance, position) keys among the unclaimed candidates. The *_resolve
+// kernels replay the claim order per frame (one workgroup per frame, map-point records staged
+// through LDS, the claim set in LDS); when claims remove too many of a point's K kept
+// candidates the point's window is rescanned with the claim set (exact fallback).
+//
+// Frames are batched in slots (one (frame, map) problem per slot) for throughput; the
+// single-frame C-ABI entry points use slot 0.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "orb_device.h"
+#include "orb_engine.h"
+
+using namespace orbamd;
+
+#define TR_CHK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "orbslam2_amd track: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return ORBX_EDEVICE;                                                    \
+        }                                                                           \
+    } while (0)
+
+namespace orbtrack {
+
+constexpr int GRID_COLS = 64, GRID_ROWS = 48;   // Frame.h:55-60
+constexpr int NCELL = GRID_COLS * GRID_ROWS;
+constexpr int TOPK = 4;                          // kept candidates per map point
+constexpr int TH_HIGH = 100, HISTO_LENGTH = 30;  // ORBmatcher.cc:56-58
+constexpr int kMaxKp = 8192;                     // grid keys sorted in LDS; idx fits 16 bits
+
+struct FrameDev {
+    int n, n_mp, n_last;
+    float Tcw[12];
+    float Ow[3];
+    float fx, fy, cx, cy, mbf, mb;
+    float min_x, max_x, min_y, max_y, inv_w, inv_h;
+    int nlevels;
+    float log_scale;
+    float scale[16];
+    float lTcw[12];   // last frame pose (frame-to-frame matcher)
+};
+
+// per-slot device arrays (slot stride = cap)
+struct Slots {
+    const FrameDev *fr;
+    const orbx_kp *kun;      // [S][cap_kp]
+    const float *uR;         // [S][cap_kp]
+    const uint8_t *desc;     // [S][cap_kp][32]
+    const uint8_t *blocked;  // [S][cap_kp]
+    const uint32_t *keys;    // [S][sort_cap] sorted (cell << 16 | idx)
+    const int *cell_start;   // [S][NCELL + 1]
+    const orbx_kp *lkun;     // [S][cap_kp] last frame
+    const int *last_mp;      // [S][cap_kp]
+    const uint8_t *last_out; // [S][cap_kp]
+    const float *Xw, *nrm, *mind, *maxd;   // [S][cap_mp][3] / [S][cap_mp]
+    const uint8_t *mdesc, *mflags;         // [S][cap_mp][32] / [S][cap_mp]
+    int cap_kp, cap_mp, sort_cap;
+};
+
+struct Cand {   // K smallest candidate keys of one query (sorted ascending)
+    uint32_t key[TOPK];   // dist << 16 | candidate position; 0xFFFFFFFF = empty
+    uint16_t idx[TOPK];
+    int8_t oct[TOPK];
+    int8_t bin[TOPK];     // rotation-histogram bin (frame-to-frame only)
+};
+
+// ---- glibc 2.35 logf, restated (bit-identical to libm over every positive float: oracle pin
+// oracle/tools/check_logf.c); std::log(float) of MapPoint::PredictScale
+__constant__ double kLogfInvc[16] = {
+    0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
+    0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0,  0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
+    0x1.0953f419900a7p+0, 0x1p+0,               0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1,
+    0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
+__constant__ double kLogfLogc[16] = {
+    -0x1.57bf7808caadep-2, -0x1.2bef0a7c06ddbp-2, -0x1.01eae7f513a67p-2, -0x1.b31d8a68224e9p-3,
+    -0x1.6574f0ac07758p-3, -0x1.1aa2bc79c81p-3,   -0x1.a4e76ce8c0e5ep-4, -0x1.1973c5a611cccp-4,
+    -0x1.252f438e10c1ep-5, 0x0p+0,                0x1.aa5aa5df25984p-5,  0x1.c5e53aa362eb4p-4,
+    0x1.526e57720db08p-3,  0x1.bc2860d22477p-3,   0x1.1058bc8a07ee1p-2,  0x1.4043057b6ee09p-2};
+
+__device__ inline float glibc_logf(float x) {
+    uint32_t ix = __float_as_uint(x);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        if (ix * 2 == 0) return -INFINITY;
+        if (ix == 0x7f800000u) return x;
+        if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return NAN;
+        ix = __float_as_uint(x * 0x1p23f) - (23u << 23);
+    }
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> 19) & 15);
+    const int k = (int32_t)tmp >> 23;
+    const uint32_t iz = ix - (tmp & (0x1ffu << 23));
+    const double z = (double)__uint_as_float(iz);
+    const double r = z * kLogfInvc[i] - 1;
+    const double y0 = kLogfLogc[i] + (double)k * 0x1.62e42fefa39efp-1;
+    const double r2 = r * r;
+    double y = 0x1.5575b0be00b6ap-2 * r + -0x1.ffffef20a4123p-2;
+    y = -0x1.00ea348b88334p-2 * r2 + y;
+    y = y * r2 + (y0 + r);
+    return (float)y;
+}
+
+// R * X + t with cv::Mat CV_32F semantics (float products summed left to right, then + t)
+__device__ inline void mat_rx_t(const float *T, const float *X, float o[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        float s = T[4 * i] * X[0];
+        s = s + T[4 * i + 1] * X[1];
+        s = s + T[4 * i + 2] * X[2];
+        o[i] = s + T[4 * i + 3];
+    }
+}
+
+__device__ inline int hamming32(const uint8_t *a, const uint8_t *b) {
+    const uint4 *pa = (const uint4 *)a, *pb = (const uint4 *)b;
+    const uint4 x0 = pa[0], x1 = pa[1], y0 = pb[0], y1 = pb[1];
+    return __popc(x0.x ^ y0.x) + __popc(x0.y ^ y0.y) + __popc(x0.z ^ y0.z) + __popc(x0.w ^ y0.w) +
+           __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
+}
+
+__device__ inline void cand_insert(Cand &c, uint32_t key, int idx, int oct, int bin) {
+    if (key >= c.key[TOPK - 1]) return;
+    int p = TOPK - 1;
+    while (p > 0 && c.key[p - 1] > key) {
+        c.key[p] = c.key[p - 1]; c.idx[p] = c.idx[p - 1]; c.oct[p] = c.oct[p - 1]; c.bin[p] = c.bin[p - 1];
+        p--;
+    }
+    c.key[p] = key; c.idx[p] = (uint16_t)idx; c.oct[p] = (int8_t)oct; c.bin[p] = (int8_t)bin;
+}
+
+// Frame::GetFeaturesInArea (Frame.cc:590-671) window: returns false if empty.
+__device__ inline bool grid_window(const FrameDev &f, float x, float y, float r, int &x0, int &x1, int &y0,
+                                   int &y1) {
+    x0 = max(0, (int)floorf((x - f.min_x - r) * f.inv_w));
+    if (x0 >= GRID_COLS) return false;
+    x1 = min(GRID_COLS - 1, (int)ceilf((x - f.min_x + r) * f.inv_w));
+    if (x1 < 0) return false;
+    y0 = max(0, (int)floorf((y - f.min_y - r) * f.inv_h));
+    if (y0 >= GRID_ROWS) return false;
+    y1 = min(GRID_ROWS - 1, (int)ceilf((y - f.min_y + r) * f.inv_h));
+    if (y1 < 0) return false;
+    return true;
+}
+
+// Scan the window in the reference's candidate order (ix, iy, insertion order) applying the
+// static filters; `claimed` (may be null) adds the dynamic claim filter (rescan fallback).
+// Returns the number of candidates that passed; keeps the K smallest (dist, position) keys.
+template <bool kLocal>
+__device__ int scan_window(const Slots &S, int s, const FrameDev &f, float x, float y, float r, int minL,
+                           int maxL, const uint8_t *qdesc, float xr, float er_r, const uint8_t *claimed,
+                           float last_angle, Cand &c) {
+#pragma unroll
+    for (int k = 0; k < TOPK; k++) { c.key[k] = 0xFFFFFFFFu; c.idx[k] = 0; c.oct[k] = -1; c.bin[k] = -1; }
+    int cx0, cx1, cy0, cy1;
+    if (!grid_window(f, x, y, r, cx0, cx1, cy0, cy1)) return 0;
+    const bool bCheckLevels = (minL > 0) || (maxL >= 0);
+    const uint32_t *keys = S.keys + (long long)s * S.sort_cap;
+    const int *cs = S.cell_start + (long long)s * (NCELL + 1);
+    const long long kb = (long long)s * S.cap_kp;
+    const uint8_t *blocked = S.blocked + kb;
+    int pos = 0, n = 0;
+    for (int ix = cx0; ix <= cx1; ix++) {
+        const int a = cs[ix * GRID_ROWS + cy0], b = cs[ix * GRID_ROWS + cy1 + 1];
+        for (int t = a; t < b; t++) {
+            const int idx = (int)(keys[t] & 0xFFFFu);
+            const orbx_kp kp = S.kun[kb + idx];
+            if (bCheckLevels) {
+                if (kp.octave < minL) continue;
+                if (maxL >= 0 && kp.octave > maxL) continue;
+            }
+            const float distx = kp.x - x, disty = kp.y - y;
+            if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+            const int p = pos++;                       // position in vIndices order
+            if (blocked[idx]) continue;
+            if (claimed && claimed[idx]) continue;
+            const float ur = S.uR[kb + idx];
+            if (ur > 0) {
+                const float er = fabsf(xr - ur);
+                if (er > er_r) continue;
+            }
+            const int dist = hamming32(qdesc, S.desc + (kb + idx) * 32);
+            int bin = -1;
+            if (!kLocal) {
+                float rot = last_angle - kp.angle;     // ORBmatcher.cc:1872-1878
+                if (rot < 0.0f) rot += 360.0f;
+                bin = (int)roundf(rot * (HISTO_LENGTH / 360.0f));
+                if (bin == HISTO_LENGTH) bin = 0;
+            }
+            n++;
+            cand_insert(c, ((uint32_t)dist << 16) | (uint32_t)p, idx, kp.octave, bin);
+        }
+    }
+    return n;
+}
+
+// ---- grid: sorted (cell << 16 | idx) keys + CSR cell starts, one workgroup per slot
+__global__ __launch_bounds__(1024) void track_grid_kernel(Slots S, uint32_t *keys_out, int *cell_start) {
+    extern __shared__ uint32_t sk[];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const FrameDev &f = S.fr[s];
+    const int n = f.n, sc = S.sort_cap;
+    const long long kb = (long long)s * S.cap_kp;
+    for (int i = tid; i < sc; i += 1024) {
+        uint32_t key = 0xFFFFFFFFu;
+        if (i < n) {
+            const orbx_kp k = S.kun[kb + i];
+            const int px = (int)roundf((k.x - f.min_x) * f.inv_w);   // PosInGrid (Frame.cc:682-698)
+            const int py = (int)roundf((k.y - f.min_y) * f.inv_h);
+            if (!(px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS))
+                key = ((uint32_t)(px * GRID_ROWS + py) << 16) | (uint32_t)i;
+        }
+        sk[i] = key;
+    }
+    __syncthreads();
+    for (int k = 2; k <= sc; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < sc; i += 1024) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t x = sk[i], y = sk[ixj];
+                    const bool asc = (i & k) == 0;
+                    if (asc ? (x > y) : (x < y)) { sk[i] = y; sk[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    uint32_t *ko = keys_out + (long long)s * sc;
+    for (int i = tid; i < sc; i += 1024) ko[i] = sk[i];
+    int *cso = cell_start + (long long)s * (NCELL + 1);
+    for (int c = tid; c <= NCELL; c += 1024) {   // lower_bound(c << 16)
+        const uint32_t v = (uint32_t)c << 16;
+        int lo = 0, hi = sc;
+        while (lo < hi) {
+            const int m = (lo + hi) >> 1;
+            if (sk[m] < v) lo = m + 1; else hi = m;
+        }
+        cso[c] = lo;
+    }
+}
+
+struct ViewOut {
+    uint8_t *in_view;
+    float *px, *py, *pxr, *vcos;
+    int *level;
+};
+
+// ---- SearchLocalPoints candidates: one thread per (slot, map point)
+__global__ __launch_bounds__(256) void track_local_cand_kernel(Slots S, float cos_limit, float th, ViewOut V,
+                                                               Cand *cand, int *ncand) {
+    const int m = blockIdx.x * 256 + threadIdx.x, s = blockIdx.y;
+    const FrameDev &f = S.fr[s];
+    if (m >= f.n_mp) return;
+    const long long mb = (long long)s * S.cap_mp + m;
+    const uint8_t flags = S.mflags[mb];
+    uint8_t inv = 0;
+    float u = 0, v = 0, uxr = 0, viewCos = 0;
+    int nScale = 0;
+    if (!(flags & (ORBT_MP_BAD | ORBT_MP_IN_FRAME))) {
+        // Frame::isInFrustum (Frame.cc:490-578)
+        const float *P = S.Xw + mb * 3;
+        float Pc[3];
+        mat_rx_t(f.Tcw, P, Pc);
+        bool ok = !(Pc[2] < 0.0f);
+        if (ok) {
+            const float invz = 1.0f / Pc[2];
+            u = f.fx * Pc[0] * invz + f.cx;
+            v = f.fy * Pc[1] * invz + f.cy;
+            ok = !(u < f.min_x || u > f.max_x) && !(v < f.min_y || v > f.max_y);
+            if (ok) {
+                const float maxDistance = 1.2f * S.maxd[mb], minDistance = 0.8f * S.mind[mb];
+                const float PO[3] = {P[0] - f.Ow[0], P[1] - f.Ow[1], P[2] - f.Ow[2]};
+                double ss = 0;
+                for (int k = 0; k < 3; k++) { const double t = PO[k]; ss = ss + t * t; }
+                const float dist = (float)sqrt(ss);                       // cv::norm
+                ok = !(dist < minDistance || dist > maxDistance);
+                if (ok) {
+                    const float *Pn = S.nrm + mb * 3;
+                    double dot = 0;
+                    for (int k = 0; k < 3; k++) dot = dot + (double)PO[k] * (double)Pn[k];   // Mat::dot
+                    viewCos = (float)(dot / (double)dist);
+                    ok = !(viewCos < cos_limit);
+                    if (ok) {
+                        const float ratio = S.maxd[mb] / dist;            // PredictScale
+                        nScale = (int)ceilf(glibc_logf(ratio) / f.log_scale);
+                        if (nScale < 0) nScale = 0;
+                        else if (nScale >= f.nlevels) nScale = f.nlevels - 1;
+                        uxr = u - f.mbf * invz;
+                        inv = 1;
+                    }
+                }
+            }
+        }
+    }
+    if (V.in_view) V.in_view[mb] = inv;
+    if (V.px) V.px[mb] = inv ? u : 0.f;
+    if (V.py) V.py[mb] = inv ? v : 0.f;
+    if (V.pxr) V.pxr[mb] = inv ? uxr : 0.f;
+    if (V.vcos) V.vcos[mb] = inv ? viewCos : 0.f;
+    if (V.level) V.level[mb] = inv ? nScale : 0;
+    Cand c;
+    int nc = 0;
+    if (inv) {
+        // ORBmatcher::SearchByProjection(F, vpMapPoints, th), ORBmatcher.cc:78-176
+        float r = (viewCos > 0.998) ? 2.5f : 4.0f;                        // RadiusByViewingCos
+        if (th != 1.0f) r *= th;
+        const float rs = r * f.scale[nScale];
+        nc = scan_window<true>(S, s, f, u, v, rs, nScale - 1, nScale, S.mdesc + mb * 32, uxr, rs, nullptr, 0.f, c);
+    } else {
+#pragma unroll
+        for (int k = 0; k < TOPK; k++) { c.key[k] = 0xFFFFFFFFu; c.idx[k] = 0; c.oct[k] = -1; c.bin[k] = -1; }
+    }
+    cand[mb] = c;
+    ncand[mb] = inv ? nc : -1;
+}
+
+constexpr int kChunk = 256;
+
+// ---- SearchLocalPoints claim replay: one workgroup per slot
+__global__ __launch_bounds__(256) void track_local_resolve_kernel(Slots S, float th, float nnratio, ViewOut V,
+                                                                  const Cand *cand, const int *ncand, int *owner,
+                                                                  int *nmatch) {
+    extern __shared__ uint8_t claimed[];   // [cap_kp]
+    __shared__ Cand sc[kChunk];
+    __shared__ int snc[kChunk];
+    __shared__ uint8_t sfl[kChunk];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const FrameDev &f = S.fr[s];
+    const long long kb = (long long)s * S.cap_kp, mb0 = (long long)s * S.cap_mp;
+    for (int i = tid; i < f.n; i += 256) { claimed[i] = S.blocked[kb + i]; owner[kb + i] = -1; }
+    __syncthreads();
+    int nm = 0;
+    for (int c0 = 0; c0 < f.n_mp; c0 += kChunk) {
+        const int cn = min(kChunk, f.n_mp - c0);
+        for (int i = tid; i < cn; i += 256) {
+            sc[i] = cand[mb0 + c0 + i];
+            snc[i] = ncand[mb0 + c0 + i];
+            sfl[i] = S.mflags[mb0 + c0 + i];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int i = 0; i < cn; i++) {
+                const int nc = snc[i];
+                if (nc <= 0) continue;                 // not in view / no candidate
+                int b = -1, b2 = -1, found = 0;
+                for (int k = 0; k < TOPK && found < 2; k++) {
+                    if (sc[i].key[k] == 0xFFFFFFFFu) break;
+                    if (claimed[sc[i].idx[k]]) continue;
+                    if (found == 0) b = k; else b2 = k;
+                    found++;
+                }
+                Cand full;
+                const Cand *use = &sc[i];
+                if (found < 2 && nc > TOPK) {          // exact fallback: rescan with the claims
+                    const int m = c0 + i;
+                    const long long mb = mb0 + m;
+                    const float vc = V.vcos[mb];
+                    const int lvl = V.level[mb];
+                    float r = (vc > 0.998) ? 2.5f : 4.0f;
+                    if (th != 1.0f) r *= th;
+                    const float rs = r * f.scale[lvl];
+                    scan_window<true>(S, s, f, V.px[mb], V.py[mb], rs, lvl - 1, lvl, S.mdesc + mb * 32, V.pxr[mb], rs,
+                                      claimed, 0.f, full);
+                    use = &full;
+                    b = full.key[0] != 0xFFFFFFFFu ? 0 : -1;
+                    b2 = full.key[1] != 0xFFFFFFFFu ? 1 : -1;
+                }
+                if (b < 0) continue;
+                const int bestDist = (int)(use->key[b] >> 16);
+                const int bestLevel = use->oct[b];
+                const int bestDist2 = b2 >= 0 ? (int)(use->key[b2] >> 16) : 256;
+                const int bestLevel2 = b2 >= 0 ? use->oct[b2] : -1;
+                if (bestDist <= TH_HIGH) {
+                    if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
+                    const int idx = use->idx[b];
+                    owner[kb + idx] = c0 + i;
+                    claimed[idx] = (sfl[i] & ORBT_MP_HAS_OBS) ? 1 : 0;
+                    nm++;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) nmatch[s] = nm;
+}
+
+// ---- SearchByProjection(CurrentFrame, LastFrame): one thread per (slot, last keypoint)
+__global__ __launch_bounds__(256) void track_frame_cand_kernel(Slots S, float th, int mono, Cand *cand,
+                                                               int *ncand) {
+    const int i = blockIdx.x * 256 + threadIdx.x, s = blockIdx.y;
+    const FrameDev &f = S.fr[s];
+    if (i >= f.n_last) return;
+    const long long lb = (long long)s * S.cap_kp + i;
+    Cand c;
+#pragma unroll
+    for (int k = 0; k < TOPK; k++) { c.key[k] = 0xFFFFFFFFu; c.idx[k] = 0; c.oct[k] = -1; c.bin[k] = -1; }
+    int nc = -1;
+    const int m = S.last_mp[lb];
+    if (m >= 0 && !S.last_out[lb]) {
+        // twc = -Rcw^T tcw; tlc = Rlw twc + tlw (ORBmatcher.cc:1757-1771)
+        float twc[3];
+        for (int k = 0; k < 3; k++) {
+            float t = f.Tcw[k] * f.Tcw[3];
+            t = t + f.Tcw[4 + k] * f.Tcw[7];
+            t = t + f.Tcw[8 + k] * f.Tcw[11];
+            twc[k] = -t;
+        }
+        float tlc[3];
+        mat_rx_t(f.lTcw, twc, tlc);
+        const bool bForward = tlc[2] > f.mb && !mono;
+        const bool bBackward = -tlc[2] > f.mb && !mono;
+        const long long mb = (long long)s * S.cap_mp + m;
+        float x3Dc[3];
+        mat_rx_t(f.Tcw, S.Xw + mb * 3, x3Dc);
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        nc = 0;
+        if (!(invzc < 0)) {
+            const float u = f.fx * x3Dc[0] * invzc + f.cx;
+            const float v = f.fy * x3Dc[1] * invzc + f.cy;
+            if (!(u < f.min_x || u > f.max_x) && !(v < f.min_y || v > f.max_y)) {
+                const orbx_kp lk = S.lkun[lb];
+                const int nLastOctave = lk.octave;
+                const float radius = th * f.scale[nLastOctave];
+                int minL, maxL;
+                if (bForward) { minL = nLastOctave; maxL = -1; }
+                else if (bBackward) { minL = 0; maxL = nLastOctave; }
+                else { minL = nLastOctave - 1; maxL = nLastOctave + 1; }
+                const float ur = u - f.mbf * invzc;
+                nc = scan_window<false>(S, s, f, u, v, radius, minL, maxL, S.mdesc + mb * 32, ur, radius, nullptr,
+                                        lk.angle, c);
+            }
+        }
+    }
+    cand[lb] = c;
+    ncand[lb] = nc;
+}
+
+__global__ __launch_bounds__(256) void track_frame_resolve_kernel(Slots S, float th, int mono, int check_ori,
+                                                                  const Cand *cand, const int *ncand, int *owner,
+                                                                  int *nmatch, int *hist_idx, int8_t *hist_bin) {
+    extern __shared__ uint8_t claimed[];   // [cap_kp]
+    __shared__ Cand sc[kChunk];
+    __shared__ int snc[kChunk];
+    __shared__ int smp[kChunk];
+    __shared__ int counts[HISTO_LENGTH];
+    __shared__ int s_nh, s_nm, s_top[3];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const FrameDev &f = S.fr[s];
+    const long long kb = (long long)s * S.cap_kp;
+    for (int i = tid; i < f.n; i += 256) { claimed[i] = S.blocked[kb + i]; owner[kb + i] = -1; }
+    if (tid < HISTO_LENGTH) counts[tid] = 0;
+    __syncthreads();
+    int nm = 0, nh = 0;
+    int *HI = hist_idx + kb;
+    int8_t *HB = hist_bin + kb;
+    for (int c0 = 0; c0 < f.n_last; c0 += kChunk) {
+        const int cn = min(kChunk, f.n_last - c0);
+        for (int i = tid; i < cn; i += 256) {
+            sc[i] = cand[kb + c0 + i];
+            snc[i] = ncand[kb + c0 + i];
+            smp[i] = S.last_mp[kb + c0 + i];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int i = 0; i < cn; i++) {
+                const int nc = snc[i];
+                if (nc <= 0) continue;
+                int b = -1;
+                for (int k = 0; k < TOPK; k++) {
+                    if (sc[i].key[k] == 0xFFFFFFFFu) break;
+                    if (!claimed[sc[i].idx[k]]) { b = k; break; }
+                }
+                Cand full;
+                const Cand *use = &sc[i];
+                if (b < 0 && nc > TOPK) {              // exact fallback: rescan with the claims
+                    const long long lb = kb + c0 + i;
+                    const int m = smp[i];
+                    const long long mb = (long long)s * S.cap_mp + m;
+                    float twc[3];
+                    for (int k = 0; k < 3; k++) {
+                        float t = f.Tcw[k] * f.Tcw[3];
+                        t = t + f.Tcw[4 + k] * f.Tcw[7];
+                        t = t + f.Tcw[8 + k] * f.Tcw[11];
+                        twc[k] = -t;
+                    }
+                    float tlc[3];
+                    mat_rx_t(f.lTcw, twc, tlc);
+                    const bool bForward = tlc[2] > f.mb && !mono;
+                    const bool bBackward = -tlc[2] > f.mb && !mono;
+                    float x3Dc[3];
+                    mat_rx_t(f.Tcw, S.Xw + mb * 3, x3Dc);
+                    const float invzc = (float)(1.0 / (double)x3Dc[2]);
+                    const float u = f.fx * x3Dc[0] * invzc + f.cx;
+                    const float v = f.fy * x3Dc[1] * invzc + f.cy;
+                    const orbx_kp lk = S.lkun[lb];
+                    const int o = lk.octave;
+                    const float radius = th * f.scale[o];
+                    const int minL = bForward ? o : (bBackward ? 0 : o - 1);
+                    const int maxL = bForward ? -1 : (bBackward ? o : o + 1);
+                    scan_window<false>(S, s, f, u, v, radius, minL, maxL, S.mdesc + mb * 32, u - f.mbf * invzc, radius,
+                                       claimed, lk.angle, full);
+                    use = &full;
+                    b = full.key[0] != 0xFFFFFFFFu ? 0 : -1;
+                }
+                if (b < 0) continue;
+                const int bestDist = (int)(use->key[b] >> 16);
+                if (bestDist <= TH_HIGH) {
+                    const int idx = use->idx[b];
+                    const int m = smp[i];
+                    owner[kb + idx] = m;
+                    claimed[idx] = (S.mflags[(long long)s * S.cap_mp + m] & ORBT_MP_HAS_OBS) ? 1 : 0;
+                    nm++;
+                    if (check_ori) {
+                        HI[nh] = idx;
+                        HB[nh] = use->bin[b];
+                        counts[use->bin[b]]++;
+                        nh++;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        s_nh = nh;
+        s_nm = nm;
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        if (check_ori) {   // ComputeThreeMaxima (ORBmatcher.cc:2076-2118)
+            int max1 = 0, max2 = 0, max3 = 0;
+            for (int i = 0; i < HISTO_LENGTH; i++) {
+                const int v = counts[i];
+                if (v > max1) { max3 = max2; max2 = max1; max1 = v; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (v > max2) { max3 = max2; max2 = v; ind3 = ind2; ind2 = i; }
+                else if (v > max3) { max3 = v; ind3 = i; }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+        }
+        s_top[0] = ind1; s_top[1] = ind2; s_top[2] = ind3;
+    }
+    __syncthreads();
+    if (check_ori) {
+        // mvpMapPoints[rotHist[bin][j]] = NULL for bins outside the top three
+        int removed = 0;
+        for (int k = tid; k < s_nh; k += 256) {
+            const int b = HB[k];
+            if (b == s_top[0] || b == s_top[1] || b == s_top[2]) continue;
+            owner[kb + HI[k]] = -2;
+            removed++;
+        }
+        atomicAdd(&s_nm, -removed);
+        __syncthreads();
+    }
+    if (tid == 0) nmatch[s] = s_nm;
+}
+
+}  // namespace orbtrack
+
+using namespace orbtrack;
+
+struct orbt_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int nslots = 0, cap_kp = 0, cap_mp = 0, sort_cap = 0;
+    DevBuf fr, kun, uR, desc, blocked, keys, cell_start, lkun, last_mp, last_out;
+    DevBuf Xw, nrm, mind, maxd, mdesc, mflags;
+    DevBuf in_view, px, py, pxr, vcos, level, cand, ncand, owner, nmatch, hist_idx, hist_bin;
+    std::vector<FrameDev> hfr;
+};
+
+namespace {
+
+Slots make_slots(orbt_engine *e) {
+    Slots S;
+    S.fr = e->fr.as<FrameDev>();
+    S.kun = e->kun.as<orbx_kp>(); S.uR = e->uR.as<float>(); S.desc = e->desc.as<uint8_t>();
+    S.blocked = e->blocked.as<uint8_t>(); S.keys = e->keys.as<uint32_t>(); S.cell_start = e->cell_start.as<int>();
+    S.lkun = e->lkun.as<orbx_kp>(); S.last_mp = e->last_mp.as<int>(); S.last_out = e->last_out.as<uint8_t>();
+    S.Xw = e->Xw.as<float>(); S.nrm = e->nrm.as<float>(); S.mind = e->mind.as<float>(); S.maxd = e->maxd.as<float>();
+    S.mdesc = e->mdesc.as<uint8_t>(); S.mflags = e->mflags.as<uint8_t>();
+    S.cap_kp = e->cap_kp; S.cap_mp = e->cap_mp; S.sort_cap = e->sort_cap;
+    return S;
+}
+
+ViewOut make_view(orbt_engine *e) {
+    ViewOut V;
+    V.in_view = e->in_view.as<uint8_t>(); V.px = e->px.as<float>(); V.py = e->py.as<float>();
+    V.pxr = e->pxr.as<float>(); V.vcos = e->vcos.as<float>(); V.level = e->level.as<int>();
+    return V;
+}
+
+int max_n(orbt_engine *e, int which, int n) {
+    int m = 0;
+    for (int s = 0; s < n; s++) m = std::max(m, which == 0 ? e->hfr[s].n_mp : e->hfr[s].n_last);
+    return m;
+}
+
+hipStream_t pick(orbt_engine *e, void *stream) { return stream ? (hipStream_t)stream : e->stream; }
+
+int grid(orbt_engine *e, int n, hipStream_t st) {
+    track_grid_kernel<<<n, 1024, sizeof(uint32_t) * e->sort_cap, st>>>(make_slots(e), e->keys.as<uint32_t>(),
+                                                                        e->cell_start.as<int>());
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+void fill_frame(FrameDev &d, const orbt_frame *F) {
+    d.n = F->n;
+    std::memcpy(d.Tcw, F->Tcw, sizeof d.Tcw);
+    std::memcpy(d.Ow, F->Ow, sizeof d.Ow);
+    d.fx = F->fx; d.fy = F->fy; d.cx = F->cx; d.cy = F->cy; d.mbf = F->mbf; d.mb = F->mb;
+    d.min_x = F->min_x; d.max_x = F->max_x; d.min_y = F->min_y; d.max_y = F->max_y;
+    // Frame.cc:183-184 (static_cast<float>(FRAME_GRID_COLS) / static_cast<float>(mnMaxX - mnMinX))
+    d.inv_w = (float)GRID_COLS / (F->max_x - F->min_x);
+    d.inv_h = (float)GRID_ROWS / (F->max_y - F->min_y);
+    d.nlevels = F->nlevels;
+    d.log_scale = F->log_scale_factor;
+    std::memcpy(d.scale, F->scale_factors, sizeof d.scale);
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbt_create(orbt_engine **out) {
+    if (!out) return ORBX_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORBX_EDEVICE;
+    orbt_engine *e = new orbt_engine();
+    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return ORBX_EDEVICE;
+    }
+    *out = e;
+    return ORBX_OK;
+}
+
+void orbt_destroy(orbt_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
+    DevBuf *bufs[] = {&e->fr, &e->kun, &e->uR, &e->desc, &e->blocked, &e->keys, &e->cell_start, &e->lkun, &e->last_mp,
+                      &e->last_out, &e->Xw, &e->nrm, &e->mind, &e->maxd, &e->mdesc, &e->mflags, &e->in_view, &e->px,
+                      &e->py, &e->pxr, &e->vcos, &e->level, &e->cand, &e->ncand, &e->owner, &e->nmatch, &e->hist_idx,
+                      &e->hist_bin};
+    for (DevBuf *b : bufs) b->release();
+    delete e;
+}
+
+int orbt_reserve(orbt_engine *e, int n_slots, int cap_kp, int cap_mp) {
+    if (!e || n_slots <= 0 || cap_kp < 0 || cap_mp < 0 || cap_kp > kMaxKp) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    cap_kp = std::max(cap_kp, 1);
+    cap_mp = std::max(cap_mp, 1);
+    int sc = 64;
+    while (sc < cap_kp) sc <<= 1;
+    const size_t S = (size_t)n_slots, K = (size_t)cap_kp, M = (size_t)cap_mp;
+    if (e->fr.ensure(sizeof(FrameDev) * S) || e->kun.ensure(sizeof(orbx_kp) * S * K) || e->uR.ensure(4 * S * K) ||
+        e->desc.ensure(32 * S * K) || e->blocked.ensure(S * K) || e->keys.ensure(4 * S * (size_t)sc) ||
+        e->cell_start.ensure(4 * S * (NCELL + 1)) || e->lkun.ensure(sizeof(orbx_kp) * S * K) ||
+        e->last_mp.ensure(4 * S * K) || e->last_out.ensure(S * K) || e->Xw.ensure(12 * S * M) ||
+        e->nrm.ensure(12 * S * M) || e->mind.ensure(4 * S * M) || e->maxd.ensure(4 * S * M) ||
+        e->mdesc.ensure(32 * S * M) || e->mflags.ensure(S * M) || e->in_view.ensure(S * M) || e->px.ensure(4 * S * M) ||
+        e->py.ensure(4 * S * M) || e->pxr.ensure(4 * S * M) || e->vcos.ensure(4 * S * M) || e->level.ensure(4 * S * M) ||
+        e->cand.ensure(sizeof(Cand) * S * std::max(K, M)) || e->ncand.ensure(4 * S * std::max(K, M)) ||
+        e->owner.ensure(4 * S * K) || e->nmatch.ensure(4 * S) || e->hist_idx.ensure(4 * S * K) ||
+        e->hist_bin.ensure(S * K))
+        return ORBX_EDEVICE;
+    e->nslots = n_slots;
+    e->cap_kp = cap_kp;
+    e->cap_mp = cap_mp;
+    e->sort_cap = sc;
+    e->hfr.assign(n_slots, FrameDev{});
+    return ORBX_OK;
+}
+
+int orbt_stage(orbt_engine *e, int slot, const orbt_frame *F, const orbt_mappoints *M, const orbt_frame *last,
+               const int32_t *last_mp, const uint8_t *last_outlier, const uint8_t *kp_blocked) {
+    if (!e || !F || !M || slot < 0 || slot >= e->nslots) return ORBX_EINVAL;
+    if (F->n < 0 || F->n > e->cap_kp || M->n < 0 || M->n > e->cap_mp) return ORBX_ECAP;
+    if (last && (last->n < 0 || last->n > e->cap_kp || !last_mp)) return ORBX_EINVAL;
+    if (F->nlevels < 1 || F->nlevels > 16) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    hipStream_t st = e->stream;
+    FrameDev &d = e->hfr[slot];
+    d = FrameDev{};
+    fill_frame(d, F);
+    d.n_mp = M->n;
+    d.n_last = last ? last->n : 0;
+    if (last) std::memcpy(d.lTcw, last->Tcw, sizeof d.lTcw);
+    // validate indices the kernels dereference
+    for (int i = 0; i < F->n; i++) {
+        const int o = F->keys_un[i].octave;
+        if (o < 0 || o >= F->nlevels) return ORBX_EINVAL;
+    }
+    if (last)
+        for (int i = 0; i < last->n; i++) {
+            if (last_mp[i] >= M->n) return ORBX_EINVAL;
+            const int o = last->keys_un[i].octave;
+            if (last_mp[i] >= 0 && (o < 0 || o >= F->nlevels)) return ORBX_EINVAL;
+        }
+    const size_t K = (size_t)e->cap_kp, Mc = (size_t)e->cap_mp, s = (size_t)slot;
+    auto up = [&](DevBuf &b, size_t off, const void *src, size_t bytes) -> bool {
+        return bytes == 0 || hipMemcpyAsync((char *)b.p + off, src, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+    };
+    const int n = F->n, m = M->n;
+    bool ok = up(e->fr, sizeof(FrameDev) * s, &d, sizeof(FrameDev)) &&
+              up(e->kun, sizeof(orbx_kp) * s * K, F->keys_un, sizeof(orbx_kp) * n) &&
+              up(e->uR, 4 * s * K, F->u_right, 4 * (size_t)n) && up(e->desc, 32 * s * K, F->desc, 32 * (size_t)n) &&
+              up(e->Xw, 12 * s * Mc, M->Xw, 12 * (size_t)m) && up(e->nrm, 12 * s * Mc, M->normal, 12 * (size_t)m) &&
+              up(e->mind, 4 * s * Mc, M->min_dist, 4 * (size_t)m) && up(e->maxd, 4 * s * Mc, M->max_dist, 4 * (size_t)m) &&
+              up(e->mdesc, 32 * s * Mc, M->desc, 32 * (size_t)m) && up(e->mflags, s * Mc, M->flags, (size_t)m);
+    if (!ok) return ORBX_EDEVICE;
+    if (kp_blocked) ok = up(e->blocked, s * K, kp_blocked, (size_t)n);
+    else ok = hipMemsetAsync((char *)e->blocked.p + s * K, 0, (size_t)n, st) == hipSuccess;
+    if (ok && last) {
+        ok = up(e->lkun, sizeof(orbx_kp) * s * K, last->keys_un, sizeof(orbx_kp) * (size_t)last->n) &&
+             up(e->last_mp, 4 * s * K, last_mp, 4 * (size_t)last->n);
+        if (ok) {
+            if (last_outlier) ok = up(e->last_out, s * K, last_outlier, (size_t)last->n);
+            else ok = hipMemsetAsync((char *)e->last_out.p + s * K, 0, (size_t)last->n, st) == hipSuccess;
+        }
+    }
+    if (!ok) return ORBX_EDEVICE;
+    TR_CHK(hipStreamSynchronize(st));   // host arrays may be freed by the caller on return
+    return ORBX_OK;
+}
+
+int orbt_run_local_batch(orbt_engine *e, int n_slots, float view_cos_limit, float th, float nnratio, void *stream) {
+    if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    hipStream_t st = pick(e, stream);
+    if (grid(e, n_slots, st)) return ORBX_EDEVICE;
+    const int mm = std::max(1, max_n(e, 0, n_slots));
+    track_local_cand_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), view_cos_limit, th,
+                                                                             make_view(e), e->cand.as<Cand>(),
+                                                                             e->ncand.as<int>());
+    track_local_resolve_kernel<<<n_slots, 256, e->cap_kp, st>>>(make_slots(e), th, nnratio, make_view(e),
+                                                                e->cand.as<Cand>(), e->ncand.as<int>(),
+                                                                e->owner.as<int>(), e->nmatch.as<int>());
+    TR_CHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int check_ori, void *stream) {
+    if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    hipStream_t st = pick(e, stream);
+    if (grid(e, n_slots, st)) return ORBX_EDEVICE;
+    const int nl = std::max(1, max_n(e, 1, n_slots));
+    track_frame_cand_kernel<<<dim3((nl + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, mono,
+                                                                             e->cand.as<Cand>(), e->ncand.as<int>());
+    track_frame_resolve_kernel<<<n_slots, 256, e->cap_kp, st>>>(make_slots(e), th, mono, check_ori, e->cand.as<Cand>(),
+                                                                e->ncand.as<int>(), e->owner.as<int>(),
+                                                                e->nmatch.as<int>(), e->hist_idx.as<int>(),
+                                                                e->hist_bin.as<int8_t>());
+    TR_CHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbt_fetch(orbt_engine *e, int slot, orbt_view *view, int32_t *owner, int32_t *nmatches) {
+    if (!e || slot < 0 || slot >= e->nslots) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    hipStream_t st = e->stream;
+    TR_CHK(hipDeviceSynchronize());
+    const FrameDev &d = e->hfr[slot];
+    const size_t K = (size_t)e->cap_kp, M = (size_t)e->cap_mp, s = (size_t)slot, m = (size_t)d.n_mp;
+    auto dn = [&](void *dst, const DevBuf &b, size_t off, size_t bytes) -> bool {
+        return !dst || bytes == 0 || hipMemcpyAsync(dst, (const char *)b.p + off, bytes, hipMemcpyDeviceToHost, st) == hipSuccess;
+    };
+    bool ok = dn(owner, e->owner, 4 * s * K, 4 * (size_t)d.n) && dn(nmatches, e->nmatch, 4 * s, 4);
+    if (ok && view)
+        ok = dn(view->in_view, e->in_view, s * M, m) && dn(view->proj_x, e->px, 4 * s * M, 4 * m) &&
+             dn(view->proj_y, e->py, 4 * s * M, 4 * m) && dn(view->proj_xr, e->pxr, 4 * s * M, 4 * m) &&
+             dn(view->view_cos, e->vcos, 4 * s * M, 4 * m) && dn(view->level, e->level, 4 * s * M, 4 * m);
+    if (!ok) return ORBX_EDEVICE;
+    TR_CHK(hipStreamSynchronize(st));
+    return ORBX_OK;
+}
+
+int orbt_search_local_points(orbt_engine *e, const orbt_frame *F, const orbt_mappoints *M, float view_cos_limit,
+                             float th, float nnratio, const uint8_t *kp_blocked, orbt_view *view, int32_t *owner,
+                             int32_t *nmatches) {
+    if (!e || !F || !M || !owner) return ORBX_EINVAL;
+    if (e->nslots < 1 || e->cap_kp < F->n || e->cap_mp < M->n) {
+        const int rc = orbt_reserve(e, std::max(1, e->nslots), std::max(e->cap_kp, F->n), std::max(e->cap_mp, M->n));
+        if (rc) return rc;
+    }
+    int rc = orbt_stage(e, 0, F, M, nullptr, nullptr, nullptr, kp_blocked);
+    if (rc) return rc;
+    rc = orbt_run_local_batch(e, 1, view_cos_limit, th, nnratio, nullptr);
+    if (rc) return rc;
+    return orbt_fetch(e, 0, view, owner, nmatches);
+}
+
+int orbt_search_by_projection_frame(orbt_engine *e, const orbt_frame *cur, const orbt_frame *last,
+                                    const int32_t *last_mp, const uint8_t *last_outlier, const orbt_mappoints *M,
+                                    float th, int mono, int check_ori, const uint8_t *kp_blocked, int32_t *owner,
+                                    int32_t *nmatches) {
+    if (!e || !cur || !last || !last_mp || !M || !owner) return ORBX_EINVAL;
+    const int need_kp = std::max(cur->n, last->n);
+    if (e->nslots < 1 || e->cap_kp < need_kp || e->cap_mp < M->n) {
+        const int rc = orbt_reserve(e, std::max(1, e->nslots), std::max(e->cap_kp, need_kp), std::max(e->cap_mp, M->n));
+        if (rc) return rc;
+    }
+    int rc = orbt_stage(e, 0, cur, M, last, last_mp, last_outlier, kp_blocked);
+    if (rc) return rc;
+    rc = orbt_run_frame_batch(e, 1, th, mono, check_ori, nullptr);
+    if (rc) return rc;
+    return orbt_fetch(e, 0, nullptr, owner, nmatches);
+}
+
+}  // extern "C"

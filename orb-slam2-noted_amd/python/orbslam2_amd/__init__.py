@@ -76,6 +76,15 @@ SIGNATURES = [
     ("lba_destroy", None, [_P]),
     ("lba_solve", _I, [_P, _P, _P, _P]),
     ("orbx_profile_read", _I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+    ("orbt_create", _I, [C.POINTER(C.c_void_p)]),
+    ("orbt_destroy", None, [_P]),
+    ("orbt_search_local_points", _I, [_P, _P, _P, _F, _F, _F, _P, _P, _P, _P]),
+    ("orbt_search_by_projection_frame", _I, [_P, _P, _P, _P, _P, _P, _F, _I, _I, _P, _P, _P]),
+    ("orbt_reserve", _I, [_P, _I, _I, _I]),
+    ("orbt_stage", _I, [_P, _I, _P, _P, _P, _P, _P, _P]),
+    ("orbt_run_local_batch", _I, [_P, _I, _F, _F, _F, _P]),
+    ("orbt_run_frame_batch", _I, [_P, _I, _F, _I, _I, _P]),
+    ("orbt_fetch", _I, [_P, _I, _P, _P, _P]),
 ]
 
 
@@ -397,3 +406,144 @@ class LocalBundleAdjustment:
         out["chi2"] = tuple(R.chi2)
         out["stopped"] = R.stopped
         return out
+
+
+# ---- tracking matchers (orbt_*): Frame::isInFrustum + ORBmatcher::SearchByProjection --------
+class OrbtFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("keys_un", C.c_void_p), ("u_right", C.c_void_p), ("desc", C.c_void_p),
+                ("Tcw", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("mb", C.c_float),
+                ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float),
+                ("nlevels", C.c_int32), ("log_scale_factor", C.c_float), ("scale_factors", C.c_float * 16)]
+
+
+class OrbtMapPoints(C.Structure):
+    _fields_ = [("n", C.c_int32), ("Xw", C.c_void_p), ("normal", C.c_void_p), ("min_dist", C.c_void_p),
+                ("max_dist", C.c_void_p), ("desc", C.c_void_p), ("flags", C.c_void_p)]
+
+
+class OrbtView(C.Structure):
+    _fields_ = [("in_view", C.c_void_p), ("proj_x", C.c_void_p), ("proj_y", C.c_void_p),
+                ("proj_xr", C.c_void_p), ("view_cos", C.c_void_p), ("level", C.c_void_p)]
+
+
+def _orbt_frame(fr: dict):
+    keep = {"keys_un": np.ascontiguousarray(fr["keys_un"]).view(KP_DTYPE),
+            "u_right": np.ascontiguousarray(fr["u_right"], np.float32),
+            "desc": np.ascontiguousarray(fr["desc"], np.uint8)}
+    F = OrbtFrame()
+    F.n = len(keep["keys_un"])
+    F.keys_un, F.u_right, F.desc = (keep[k].ctypes.data for k in ("keys_un", "u_right", "desc"))
+    F.Tcw[:] = [float(v) for v in np.asarray(fr["Tcw"], np.float32).reshape(-1)[:12]]
+    F.Ow[:] = [float(v) for v in np.asarray(fr["Ow"], np.float32)]
+    for k in ("fx", "fy", "cx", "cy", "mbf", "mb", "min_x", "max_x", "min_y", "max_y", "log_scale_factor"):
+        setattr(F, k, float(fr[k]))
+    F.nlevels = int(fr["nlevels"])
+    sf = np.zeros(16, np.float32)
+    sf[: F.nlevels] = fr["scale_factors"]
+    F.scale_factors[:] = [float(v) for v in sf]
+    return F, keep
+
+
+def _orbt_map(mp: dict):
+    keep = {k: np.ascontiguousarray(mp[k], np.uint8 if k in ("desc", "flags") else np.float32)
+            for k in ("Xw", "normal", "min_dist", "max_dist", "desc", "flags")}
+    M = OrbtMapPoints(len(keep["Xw"]), *(keep[k].ctypes.data for k in ("Xw", "normal", "min_dist", "max_dist",
+                                                                        "desc", "flags")))
+    return M, keep
+
+
+class Tracker:
+    """The per-frame tracking matchers of ORBmatcher (ORBmatcher.h:82,102) plus
+    Frame::isInFrustum, on the GPU. Problems are dicts shaped like synth.tracking_problem:
+    {"frame", "map", "last", "last_mp", "last_outlier", "kp_blocked"}."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        _check(lib().orbt_create(C.byref(h)), "orbt_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _blk(prob):
+        b = prob.get("kp_blocked")
+        return np.ascontiguousarray(b, np.uint8) if b is not None else None
+
+    def search_local_points(self, prob: dict, cos_limit=0.5, th=1.0, nnratio=0.8):
+        F, k1 = _orbt_frame(prob["frame"])
+        M, k2 = _orbt_map(prob["map"])
+        n, m = F.n, M.n
+        view = {"in_view": np.zeros(max(m, 1), np.uint8), "proj_x": np.zeros(max(m, 1), np.float32),
+                "proj_y": np.zeros(max(m, 1), np.float32), "proj_xr": np.zeros(max(m, 1), np.float32),
+                "view_cos": np.zeros(max(m, 1), np.float32), "level": np.zeros(max(m, 1), np.int32)}
+        V = OrbtView(*(view[k].ctypes.data for k in ("in_view", "proj_x", "proj_y", "proj_xr", "view_cos", "level")))
+        owner = np.zeros(max(n, 1), np.int32)
+        nm = C.c_int32()
+        blk = self._blk(prob)
+        _check(lib().orbt_search_local_points(self._h, C.byref(F), C.byref(M), cos_limit, th, nnratio,
+                                              blk.ctypes.data if blk is not None else None, C.byref(V),
+                                              owner.ctypes.data, C.byref(nm)), "orbt_search_local_points")
+        return nm.value, owner[:n], {k: v[:m] for k, v in view.items()}
+
+    def search_by_projection_frame(self, prob: dict, th=15.0, mono=False, check_ori=True):
+        F, k1 = _orbt_frame(prob["frame"])
+        Lf, k2 = _orbt_frame(prob["last"])
+        M, k3 = _orbt_map(prob["map"])
+        last_mp = np.ascontiguousarray(prob["last_mp"], np.int32)
+        last_out = np.ascontiguousarray(prob["last_outlier"], np.uint8)
+        owner = np.zeros(max(F.n, 1), np.int32)
+        nm = C.c_int32()
+        blk = self._blk(prob)
+        _check(lib().orbt_search_by_projection_frame(self._h, C.byref(F), C.byref(Lf), last_mp.ctypes.data,
+                                                     last_out.ctypes.data, C.byref(M), th, 1 if mono else 0,
+                                                     1 if check_ori else 0,
+                                                     blk.ctypes.data if blk is not None else None,
+                                                     owner.ctypes.data, C.byref(nm)),
+               "orbt_search_by_projection_frame")
+        return nm.value, owner[: F.n]
+
+    # batched device-resident path (bench.py)
+    def reserve(self, n_slots: int, cap_kp: int, cap_mp: int):
+        _check(lib().orbt_reserve(self._h, n_slots, cap_kp, cap_mp), "orbt_reserve")
+
+    def stage(self, slot: int, prob: dict):
+        F, k1 = _orbt_frame(prob["frame"])
+        Lf, k2 = _orbt_frame(prob["last"])
+        M, k3 = _orbt_map(prob["map"])
+        last_mp = np.ascontiguousarray(prob["last_mp"], np.int32)
+        last_out = np.ascontiguousarray(prob["last_outlier"], np.uint8)
+        blk = self._blk(prob)
+        _check(lib().orbt_stage(self._h, slot, C.byref(F), C.byref(M), C.byref(Lf), last_mp.ctypes.data,
+                                last_out.ctypes.data, blk.ctypes.data if blk is not None else None), "orbt_stage")
+
+    def run_local_batch(self, n_slots: int, cos_limit=0.5, th=1.0, nnratio=0.8, stream=None):
+        _check(lib().orbt_run_local_batch(self._h, n_slots, cos_limit, th, nnratio, stream), "orbt_run_local_batch")
+
+    def run_frame_batch(self, n_slots: int, th=15.0, mono=False, check_ori=True, stream=None):
+        _check(lib().orbt_run_frame_batch(self._h, n_slots, th, 1 if mono else 0, 1 if check_ori else 0, stream),
+               "orbt_run_frame_batch")
+
+    def fetch(self, slot: int, n_kp: int, n_mp: int = 0):
+        owner = np.zeros(max(n_kp, 1), np.int32)
+        nm = C.c_int32()
+        view = None
+        V = None
+        if n_mp:
+            view = {"in_view": np.zeros(n_mp, np.uint8), "proj_x": np.zeros(n_mp, np.float32),
+                    "proj_y": np.zeros(n_mp, np.float32), "proj_xr": np.zeros(n_mp, np.float32),
+                    "view_cos": np.zeros(n_mp, np.float32), "level": np.zeros(n_mp, np.int32)}
+            V = OrbtView(*(view[k].ctypes.data for k in ("in_view", "proj_x", "proj_y", "proj_xr", "view_cos",
+                                                         "level")))
+        _check(lib().orbt_fetch(self._h, slot, C.byref(V) if V is not None else None, owner.ctypes.data,
+                                C.byref(nm)), "orbt_fetch")
+        return nm.value, owner[:n_kp], view

@@ -225,3 +225,158 @@ def localba_problem(seed: int = 4, n_kf: int = 20, n_points: int = 3000, stereo_
         "truth_Tcw": np.array(Tcw_true, np.float64),
         "truth_Xw": np.array(pts, np.float64),
     }
+
+
+# ---------------------------------------------------------------------------------------
+# Tracking matchers: one current frame + a local map (+ the last
+# frame for the motion-model matcher). Keypoints are synthetic (not extracted): projections
+# of map points with pixel noise sigma = scale[octave], descriptors = the map point's with
+# 0..60 flipped bits, plus clones competing for the same keypoints (exercises the greedy
+# claim order) and uniformly random distractors. Octaves ~ features per level.
+# ---------------------------------------------------------------------------------------
+TRACK_KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+MP_BAD, MP_HAS_OBS, MP_IN_FRAME = 1, 2, 4
+
+
+def _flip_bits(rng, d: np.ndarray, k: int) -> np.ndarray:
+    d = d.copy()
+    for b in rng.choice(256, size=k, replace=False):
+        d[b >> 3] ^= np.uint8(1 << (b & 7))
+    return d
+
+
+def _pose_dict(R: np.ndarray, t: np.ndarray):
+    Rf = R.astype(np.float32)
+    tf = t.astype(np.float32)
+    T = np.concatenate([Rf, tf[:, None]], axis=1).astype(np.float32)
+    Ow = (-(Rf.astype(np.float64).T @ tf.astype(np.float64))).astype(np.float32)
+    return T, Ow
+
+
+def tracking_problem(seed: int = 5, n_kp: int = 2000, n_mp: int = 3000, W: int = 1241, H: int = 376,
+                     stereo: bool = True, motion: str = "forward", clone_frac: float = 0.15,
+                     n_last: int = 1500):
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = (np.float32(v) for v in KITTI_CAM)
+    mb = np.float32(bf / fx)
+    nl = 8
+    sf = np.ones(nl, np.float32)
+    for i in range(1, nl):
+        sf[i] = np.float32(sf[i - 1] * np.float32(1.2))
+    feat = np.array([434, 362, 302, 251, 209, 175, 145, 122], np.float64)
+    oct_p = feat / feat.sum()
+    Rcw = _small_rot(rng, 2.0)
+    tcw = rng.normal(0, 0.3, 3)
+    Tcw, Ow = _pose_dict(Rcw, tcw)
+    Rwc = Rcw.T
+    n_true = int(n_mp * (1 - clone_frac))
+    # map points: projections (some outside the image), depth 3..45 m (some behind)
+    u = rng.uniform(-30, W + 30, n_true)
+    v = rng.uniform(-30, H + 30, n_true)
+    z = rng.uniform(3, 45, n_true)
+    z[rng.random(n_true) < 0.03] *= -1
+    Pc = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    Xw = (Pc - tcw) @ Rcw            # Rwc (Pc - tcw)
+    octv = rng.choice(nl, size=n_true, p=oct_p)
+    Ocw = -Rwc @ tcw
+    dist = np.linalg.norm(Xw - Ocw, axis=1)
+    maxd = dist * (1.2 ** octv) * rng.uniform(0.92, 1.08, n_true)
+    maxd[rng.random(n_true) < 0.04] *= 0.3                         # out of the scale range
+    # viewing direction of a reference keyframe: mostly close, some beyond 60 degrees
+    ref = Ocw + rng.normal(0, 0.5, (n_true, 3))
+    nrm = Xw - ref
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    wild = rng.random(n_true) < 0.08
+    nrm[wild] = rng.normal(size=(int(wild.sum()), 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    mdesc = rng.integers(0, 256, (n_true, 32), dtype=np.uint8)
+    # clones: another map point at nearly the same place with a similar descriptor
+    n_clone = n_mp - n_true
+    src = rng.integers(0, n_true, n_clone)
+    Xw = np.concatenate([Xw, Xw[src] + rng.normal(0, 0.02, (n_clone, 3))])
+    nrm = np.concatenate([nrm, nrm[src]])
+    maxd = np.concatenate([maxd, maxd[src]])
+    octv = np.concatenate([octv, octv[src]])
+    mdesc = np.concatenate([mdesc, np.stack([_flip_bits(rng, mdesc[s], int(rng.integers(0, 30))) for s in src])
+                            if n_clone else np.zeros((0, 32), np.uint8)])
+    perm = rng.permutation(n_mp)
+    Xw, nrm, maxd, octv, mdesc = Xw[perm], nrm[perm], maxd[perm], octv[perm], mdesc[perm]
+    mind = maxd / sf[nl - 1]
+    flags = np.where(rng.random(n_mp) < 0.9, MP_HAS_OBS, 0).astype(np.uint8)
+    flags[rng.random(n_mp) < 0.03] |= MP_BAD
+    flags[rng.random(n_mp) < 0.05] |= MP_IN_FRAME
+    # keypoints
+    kps, kdesc, kur, kgen = [], [], [], []
+    Pcm = Xw @ Rcw.T + tcw
+    for m in range(n_mp):
+        if len(kps) >= int(0.75 * n_kp) or Pcm[m, 2] <= 0.1 or rng.random() < 0.3:
+            continue
+        uu = fx * Pcm[m, 0] / Pcm[m, 2] + cx
+        vv = fy * Pcm[m, 1] / Pcm[m, 2] + cy
+        for _ in range(1 + int(rng.random() < 0.2)):             # sometimes two detections
+            o = int(np.clip(octv[m] + rng.integers(-1, 2), 0, nl - 1))
+            s = float(sf[o])
+            x = uu + rng.normal(0, s)
+            y = vv + rng.normal(0, s)
+            if not (0 <= x < W and 0 <= y < H):
+                continue
+            kps.append((x, y, 31 * s, rng.uniform(0, 360), 0, o, -1))
+            kdesc.append(_flip_bits(rng, mdesc[m], int(rng.integers(0, 60))))
+            ur = x - bf / Pcm[m, 2] + rng.normal(0, 0.5) if (stereo and rng.random() < 0.6) else -1.0
+            kur.append(ur)
+            kgen.append(m)
+    while len(kps) < n_kp:
+        o = int(rng.choice(nl, p=oct_p))
+        kps.append((rng.uniform(0, W), rng.uniform(0, H), 31 * float(sf[o]), rng.uniform(0, 360), 0, o, -1))
+        kdesc.append(rng.integers(0, 256, 32, dtype=np.uint8))
+        kur.append(float(rng.uniform(0, W)) if (stereo and rng.random() < 0.5) else -1.0)
+        kgen.append(-1)
+    kps = kps[:n_kp]
+    order = rng.permutation(len(kps))
+    keys = np.array([kps[i] for i in order], TRACK_KP_DTYPE)
+    kdesc = np.stack([kdesc[i] for i in order]).astype(np.uint8)
+    kur = np.array([kur[i] for i in order], np.float32)
+    kgen = np.array([kgen[i] for i in order], np.int64)
+    frame = {"keys_un": keys, "u_right": kur, "desc": kdesc, "Tcw": Tcw, "Ow": Ow, "fx": fx, "fy": fy, "cx": cx,
+             "cy": cy, "mbf": bf, "mb": mb, "min_x": 0.0, "max_x": float(W), "min_y": 0.0, "max_y": float(H),
+             "nlevels": nl, "log_scale_factor": np.float32(np.log(np.float32(1.2))), "scale_factors": sf}
+    mp = {"Xw": Xw.astype(np.float32), "normal": nrm.astype(np.float32), "min_dist": mind.astype(np.float32),
+          "max_dist": maxd.astype(np.float32), "desc": mdesc, "flags": flags}
+    # last frame (motion model): the camera 1 m behind / ahead / in place along its optical axis
+    shift = {"forward": 1.0, "backward": -1.0, "static": 0.2}[motion]
+    Rlw = Rcw @ _small_rot(rng, 1.0)
+    Olw = Ocw - shift * Rwc[:, 2]
+    tlw = -Rlw @ Olw
+    lTcw, lOw = _pose_dict(Rlw, tlw)
+    nL = n_last
+    last_mp = np.full(nL, -1, np.int32)
+    pick = rng.choice(n_mp, size=min(n_mp, int(0.8 * nL)), replace=False)
+    slots = rng.choice(nL, size=len(pick), replace=False)
+    last_mp[slots] = pick
+    lk = np.zeros(nL, TRACK_KP_DTYPE)
+    lk["x"] = rng.uniform(0, W, nL)
+    lk["y"] = rng.uniform(0, H, nL)
+    lk["octave"] = rng.choice(nl, size=nL, p=oct_p)
+    lk["octave"][slots] = np.clip(octv[pick] + rng.integers(-1, 2, len(pick)), 0, nl - 1)
+    lk["angle"] = rng.uniform(0, 360, nL).astype(np.float32)
+    lk["size"] = 31.0
+    lk["class_id"] = -1
+    # a consistent in-plane rotation (12 +- 3 deg) between the last and the current keypoint of
+    # the same map point for most matches, random for the rest (rotation-histogram check)
+    first_kp = {}
+    for i, g in enumerate(kgen):
+        if g >= 0 and g not in first_kp:
+            first_kp[int(g)] = i
+    for i in slots:
+        j = first_kp.get(int(last_mp[i]))
+        if j is not None and rng.random() < 0.8:
+            lk["angle"][i] = np.float32((float(keys["angle"][j]) + 12.0 + rng.normal(0, 3)) % 360.0)
+    last = {"keys_un": lk, "u_right": np.full(nL, -1, np.float32), "desc": np.zeros((nL, 32), np.uint8),
+            "Tcw": lTcw, "Ow": lOw, **{k: frame[k] for k in ("fx", "fy", "cx", "cy", "mbf", "mb", "min_x", "max_x",
+                                                               "min_y", "max_y", "nlevels", "log_scale_factor",
+                                                               "scale_factors")}}
+    last_out = (rng.random(nL) < 0.05).astype(np.uint8)
+    kp_blocked = (rng.random(len(keys)) < 0.05).astype(np.uint8)
+    return {"frame": frame, "map": mp, "last": last, "last_mp": last_mp, "last_outlier": last_out,
+            "kp_blocked": kp_blocked}
