@@ -67,7 +67,7 @@ struct Slots {
     const float *uR;         // [S][cap_kp]
     const uint8_t *desc;     // [S][cap_kp][32]
     const uint8_t *blocked;  // [S][cap_kp]
-    const uint32_t *keys;    // [S][sort_cap] sorted (cell << 16 | idx)
+    const float4 *grec;      // [S][sort_cap] grid-sorted {x, y, uR, idx | octave << 16 | blocked << 24}
     const int *cell_start;   // [S][NCELL + 1]
     const orbx_kp *lkun;     // [S][cap_kp] last frame
     const int *last_mp;      // [S][cap_kp]
@@ -174,26 +174,26 @@ __device__ int scan_window(const Slots &S, int s, const FrameDev &f, float x, fl
     int cx0, cx1, cy0, cy1;
     if (!grid_window(f, x, y, r, cx0, cx1, cy0, cy1)) return 0;
     const bool bCheckLevels = (minL > 0) || (maxL >= 0);
-    const uint32_t *keys = S.keys + (long long)s * S.sort_cap;
+    const float4 *rec = S.grec + (long long)s * S.sort_cap;
     const int *cs = S.cell_start + (long long)s * (NCELL + 1);
     const long long kb = (long long)s * S.cap_kp;
-    const uint8_t *blocked = S.blocked + kb;
     int pos = 0, n = 0;
     for (int ix = cx0; ix <= cx1; ix++) {
         const int a = cs[ix * GRID_ROWS + cy0], b = cs[ix * GRID_ROWS + cy1 + 1];
         for (int t = a; t < b; t++) {
-            const int idx = (int)(keys[t] & 0xFFFFu);
-            const orbx_kp kp = S.kun[kb + idx];
+            const float4 g = rec[t];
+            const uint32_t pk = __float_as_uint(g.w);
+            const int idx = (int)(pk & 0xFFFFu), oct = (int)((pk >> 16) & 0xFF);
             if (bCheckLevels) {
-                if (kp.octave < minL) continue;
-                if (maxL >= 0 && kp.octave > maxL) continue;
+                if (oct < minL) continue;
+                if (maxL >= 0 && oct > maxL) continue;
             }
-            const float distx = kp.x - x, disty = kp.y - y;
+            const float distx = g.x - x, disty = g.y - y;
             if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
             const int p = pos++;                       // position in vIndices order
-            if (blocked[idx]) continue;
+            if (pk >> 24) continue;                    // owned on entry by a point with observations
             if (claimed && claimed[idx]) continue;
-            const float ur = S.uR[kb + idx];
+            const float ur = g.z;
             if (ur > 0) {
                 const float er = fabsf(xr - ur);
                 if (er > er_r) continue;
@@ -201,20 +201,20 @@ __device__ int scan_window(const Slots &S, int s, const FrameDev &f, float x, fl
             const int dist = hamming32(qdesc, S.desc + (kb + idx) * 32);
             int bin = -1;
             if (!kLocal) {
-                float rot = last_angle - kp.angle;     // ORBmatcher.cc:1872-1878
+                float rot = last_angle - S.kun[kb + idx].angle;   // ORBmatcher.cc:1872-1878
                 if (rot < 0.0f) rot += 360.0f;
                 bin = (int)roundf(rot * (HISTO_LENGTH / 360.0f));
                 if (bin == HISTO_LENGTH) bin = 0;
             }
             n++;
-            cand_insert(c, ((uint32_t)dist << 16) | (uint32_t)p, idx, kp.octave, bin);
+            cand_insert(c, ((uint32_t)dist << 16) | (uint32_t)p, idx, oct, bin);
         }
     }
     return n;
 }
 
 // ---- grid: sorted (cell << 16 | idx) keys + CSR cell starts, one workgroup per slot
-__global__ __launch_bounds__(1024) void track_grid_kernel(Slots S, uint32_t *keys_out, int *cell_start) {
+__global__ __launch_bounds__(1024) void track_grid_kernel(Slots S, float4 *rec_out, int *cell_start) {
     extern __shared__ uint32_t sk[];
     const int s = blockIdx.x, tid = threadIdx.x;
     const FrameDev &f = S.fr[s];
@@ -244,8 +244,19 @@ __global__ __launch_bounds__(1024) void track_grid_kernel(Slots S, uint32_t *key
             }
             __syncthreads();
         }
-    uint32_t *ko = keys_out + (long long)s * sc;
-    for (int i = tid; i < sc; i += 1024) ko[i] = sk[i];
+    float4 *ro = rec_out + (long long)s * sc;
+    for (int i = tid; i < sc; i += 1024) {
+        const uint32_t key = sk[i];
+        float4 g = make_float4(0.f, 0.f, -1.f, __uint_as_float(0xFFFFFFFFu));
+        if (key != 0xFFFFFFFFu) {
+            const int idx = (int)(key & 0xFFFFu);
+            const orbx_kp k = S.kun[kb + idx];
+            const uint32_t pk = (uint32_t)idx | ((uint32_t)(k.octave & 0xFF) << 16) |
+                                ((uint32_t)(S.blocked[kb + idx] ? 1 : 0) << 24);
+            g = make_float4(k.x, k.y, S.uR[kb + idx], __uint_as_float(pk));
+        }
+        ro[i] = g;
+    }
     int *cso = cell_start + (long long)s * (NCELL + 1);
     for (int c = tid; c <= NCELL; c += 1024) {   // lower_bound(c << 16)
         const uint32_t v = (uint32_t)c << 16;
@@ -333,219 +344,264 @@ __global__ __launch_bounds__(256) void track_local_cand_kernel(Slots S, float co
     ncand[mb] = inv ? nc : -1;
 }
 
-constexpr int kChunk = 256;
+// ---- claim replay, one wave per slot, speculative 64-query windows.
+// Each lane decides one query of the window against the claim set as of the window start
+// and records the candidates it examined (its kept entries up to the decision). An earlier
+// lane that claims -- with a map point that has observations -- a keypoint a later lane
+// examined invalidates that later lane and everything after it; the valid prefix is
+// committed and the window restarts at the first invalid lane. A lane whose kept entries
+// are exhausted by claims (fallback) is a window barrier, rescanned exactly with the claims.
+// Result = the reference's strictly sequential order.
+constexpr int kNoTag = 1 << 30;
 
-// ---- SearchLocalPoints claim replay: one workgroup per slot
-__global__ __launch_bounds__(256) void track_local_resolve_kernel(Slots S, float th, float nnratio, ViewOut V,
-                                                                  const Cand *cand, const int *ncand, int *owner,
-                                                                  int *nmatch) {
-    extern __shared__ uint8_t claimed[];   // [cap_kp]
-    __shared__ Cand sc[kChunk];
-    __shared__ int snc[kChunk];
-    __shared__ uint8_t sfl[kChunk];
-    const int s = blockIdx.x, tid = threadIdx.x;
-    const FrameDev &f = S.fr[s];
-    const long long kb = (long long)s * S.cap_kp, mb0 = (long long)s * S.cap_mp;
-    for (int i = tid; i < f.n; i += 256) { claimed[i] = S.blocked[kb + i]; owner[kb + i] = -1; }
-    __syncthreads();
-    int nm = 0;
-    for (int c0 = 0; c0 < f.n_mp; c0 += kChunk) {
-        const int cn = min(kChunk, f.n_mp - c0);
-        for (int i = tid; i < cn; i += 256) {
-            sc[i] = cand[mb0 + c0 + i];
-            snc[i] = ncand[mb0 + c0 + i];
-            sfl[i] = S.mflags[mb0 + c0 + i];
-        }
-        __syncthreads();
-        if (tid == 0) {
-            for (int i = 0; i < cn; i++) {
-                const int nc = snc[i];
-                if (nc <= 0) continue;                 // not in view / no candidate
-                int b = -1, b2 = -1, found = 0;
-                for (int k = 0; k < TOPK && found < 2; k++) {
-                    if (sc[i].key[k] == 0xFFFFFFFFu) break;
-                    if (claimed[sc[i].idx[k]]) continue;
-                    if (found == 0) b = k; else b2 = k;
-                    found++;
-                }
-                Cand full;
-                const Cand *use = &sc[i];
-                if (found < 2 && nc > TOPK) {          // exact fallback: rescan with the claims
-                    const int m = c0 + i;
-                    const long long mb = mb0 + m;
-                    const float vc = V.vcos[mb];
-                    const int lvl = V.level[mb];
-                    float r = (vc > 0.998) ? 2.5f : 4.0f;
-                    if (th != 1.0f) r *= th;
-                    const float rs = r * f.scale[lvl];
-                    scan_window<true>(S, s, f, V.px[mb], V.py[mb], rs, lvl - 1, lvl, S.mdesc + mb * 32, V.pxr[mb], rs,
-                                      claimed, 0.f, full);
-                    use = &full;
-                    b = full.key[0] != 0xFFFFFFFFu ? 0 : -1;
-                    b2 = full.key[1] != 0xFFFFFFFFu ? 1 : -1;
-                }
-                if (b < 0) continue;
-                const int bestDist = (int)(use->key[b] >> 16);
-                const int bestLevel = use->oct[b];
-                const int bestDist2 = b2 >= 0 ? (int)(use->key[b2] >> 16) : 256;
-                const int bestLevel2 = b2 >= 0 ? use->oct[b2] : -1;
-                if (bestDist <= TH_HIGH) {
-                    if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
-                    const int idx = use->idx[b];
-                    owner[kb + idx] = c0 + i;
-                    claimed[idx] = (sfl[i] & ORBT_MP_HAS_OBS) ? 1 : 0;
-                    nm++;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    if (tid == 0) nmatch[s] = nm;
+__device__ inline float local_radius(float vc, int lvl, float th, const FrameDev &f) {
+    float r = (vc > 0.998) ? 2.5f : 4.0f;                            // RadiusByViewingCos
+    if (th != 1.0f) r *= th;
+    return r * f.scale[lvl];
 }
 
-// ---- SearchByProjection(CurrentFrame, LastFrame): one thread per (slot, last keypoint)
+__global__ __launch_bounds__(64) void track_local_resolve_kernel(Slots S, float th, float nnratio, ViewOut V,
+                                                                 const Cand *cand, const int *ncand, int *owner,
+                                                                 int *nmatch) {
+    extern __shared__ uint8_t lds[];
+    uint8_t *claimed = lds;                                 // [cap_kp]
+    int *tag = (int *)(lds + ((S.cap_kp + 15) & ~15));       // [cap_kp] lowest claiming lane
+    const int s = blockIdx.x, lane = threadIdx.x;
+    const FrameDev &f = S.fr[s];
+    const long long kb = (long long)s * S.cap_kp, mb0 = (long long)s * S.cap_mp;
+    for (int i = lane; i < f.n; i += 64) { claimed[i] = S.blocked[kb + i]; tag[i] = kNoTag; owner[kb + i] = -1; }
+    __syncthreads();
+    int nm = 0, base = 0;
+    while (base < f.n_mp) {
+        const int q = base + lane;
+        const bool live = q < f.n_mp;
+        Cand c;
+        int nc = -1;
+        uint8_t fl = 0;
+        if (live) { c = cand[mb0 + q]; nc = ncand[mb0 + q]; fl = S.mflags[mb0 + q]; }
+        int b = -1, b2 = -1, found = 0, last_ex = -1;
+        if (nc > 0) {
+            for (int k = 0; k < TOPK && found < 2; k++) {
+                if (c.key[k] == 0xFFFFFFFFu) break;
+                last_ex = k;
+                if (claimed[c.idx[k]]) continue;
+                if (found == 0) b = k; else b2 = k;
+                found++;
+            }
+        }
+        const bool fallback = nc > TOPK && found < 2;
+        bool accept = false;
+        if (nc > 0 && !fallback && b >= 0) {
+            const int bestDist = (int)(c.key[b] >> 16), bestLevel = c.oct[b];
+            const int bestDist2 = b2 >= 0 ? (int)(c.key[b2] >> 16) : 256, bestLevel2 = b2 >= 0 ? c.oct[b2] : -1;
+            accept = bestDist <= TH_HIGH && !(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2);
+        }
+        const bool obs = (fl & ORBT_MP_HAS_OBS) != 0;
+        const int idx = b >= 0 ? c.idx[b] : 0;
+        if (accept && obs) atomicMin(&tag[idx], lane);
+        __syncthreads();
+        bool conflict = false;
+        for (int k = 0; k <= last_ex; k++) conflict |= tag[c.idx[k]] < lane;
+        const unsigned long long stop = __ballot(live && (conflict || fallback));
+        const int cut = stop ? __ffsll((long long)stop) - 1 : 64;
+        __syncthreads();
+        if (accept && obs) tag[idx] = kNoTag;
+        const bool commit = accept && lane < cut;
+        if (commit) {
+            atomicMax(&owner[kb + idx], q);   // later map points overwrite observation-less owners
+            if (obs) claimed[idx] = 1;
+        }
+        nm += __popcll(__ballot(commit));
+        __syncthreads();
+        if (cut < 64 && base + cut < f.n_mp && ((stop >> cut) & 1)) {
+            // the barrier lane: conflict -> re-decide in the next window; fallback -> rescan now
+            bool is_fb = __shfl(fallback ? 1 : 0, cut) != 0;
+            if (is_fb) {
+                if (lane == 0) {
+                    const int qq = base + cut;
+                    const long long mb = mb0 + qq;
+                    const int lvl = V.level[mb];
+                    const float rs = local_radius(V.vcos[mb], lvl, th, f);
+                    Cand full;
+                    scan_window<true>(S, s, f, V.px[mb], V.py[mb], rs, lvl - 1, lvl, S.mdesc + mb * 32, V.pxr[mb], rs,
+                                      claimed, 0.f, full);
+                    if (full.key[0] != 0xFFFFFFFFu) {
+                        const int bd = (int)(full.key[0] >> 16), bl = full.oct[0];
+                        const int bd2 = full.key[1] != 0xFFFFFFFFu ? (int)(full.key[1] >> 16) : 256;
+                        const int bl2 = full.key[1] != 0xFFFFFFFFu ? full.oct[1] : -1;
+                        if (bd <= TH_HIGH && !(bl == bl2 && (float)bd > nnratio * (float)bd2)) {
+                            const int id = full.idx[0];
+                            owner[kb + id] = qq;
+                            if (S.mflags[mb] & ORBT_MP_HAS_OBS) claimed[id] = 1;
+                            nm++;
+                        }
+                    }
+                }
+                nm = __shfl(nm, 0);
+                __syncthreads();
+                base += cut + 1;
+            } else {
+                base += cut;
+            }
+        } else {
+            base += 64;
+        }
+    }
+    if (lane == 0) nmatch[s] = nm;
+}
+
+// ---- SearchByProjection(CurrentFrame, LastFrame) query of last keypoint i (ORBmatcher.cc:1786-1870);
+// `claimed` != null adds the claim filter (resolve fallback). Returns -1 if not projected.
+__device__ int frame_query(const Slots &S, int s, const FrameDev &f, int i, float th, int mono,
+                           const uint8_t *claimed, Cand &c) {
+#pragma unroll
+    for (int k = 0; k < TOPK; k++) { c.key[k] = 0xFFFFFFFFu; c.idx[k] = 0; c.oct[k] = -1; c.bin[k] = -1; }
+    const long long lb = (long long)s * S.cap_kp + i;
+    const int m = S.last_mp[lb];
+    if (m < 0 || S.last_out[lb]) return -1;
+    // twc = -Rcw^T tcw; tlc = Rlw twc + tlw (ORBmatcher.cc:1757-1771)
+    float twc[3];
+    for (int k = 0; k < 3; k++) {
+        float t = f.Tcw[k] * f.Tcw[3];
+        t = t + f.Tcw[4 + k] * f.Tcw[7];
+        t = t + f.Tcw[8 + k] * f.Tcw[11];
+        twc[k] = -t;
+    }
+    float tlc[3];
+    mat_rx_t(f.lTcw, twc, tlc);
+    const bool bForward = tlc[2] > f.mb && !mono;
+    const bool bBackward = -tlc[2] > f.mb && !mono;
+    const long long mb = (long long)s * S.cap_mp + m;
+    float x3Dc[3];
+    mat_rx_t(f.Tcw, S.Xw + mb * 3, x3Dc);
+    const float invzc = (float)(1.0 / (double)x3Dc[2]);
+    if (invzc < 0) return 0;
+    const float u = f.fx * x3Dc[0] * invzc + f.cx;
+    const float v = f.fy * x3Dc[1] * invzc + f.cy;
+    if (u < f.min_x || u > f.max_x || v < f.min_y || v > f.max_y) return 0;
+    const orbx_kp lk = S.lkun[lb];
+    const int nLastOctave = lk.octave;
+    const float radius = th * f.scale[nLastOctave];
+    int minL, maxL;
+    if (bForward) { minL = nLastOctave; maxL = -1; }
+    else if (bBackward) { minL = 0; maxL = nLastOctave; }
+    else { minL = nLastOctave - 1; maxL = nLastOctave + 1; }
+    const float ur = u - f.mbf * invzc;
+    return scan_window<false>(S, s, f, u, v, radius, minL, maxL, S.mdesc + mb * 32, ur, radius, claimed, lk.angle, c);
+}
+
+// one thread per (slot, last keypoint)
 __global__ __launch_bounds__(256) void track_frame_cand_kernel(Slots S, float th, int mono, Cand *cand,
                                                                int *ncand) {
     const int i = blockIdx.x * 256 + threadIdx.x, s = blockIdx.y;
     const FrameDev &f = S.fr[s];
     if (i >= f.n_last) return;
-    const long long lb = (long long)s * S.cap_kp + i;
     Cand c;
-#pragma unroll
-    for (int k = 0; k < TOPK; k++) { c.key[k] = 0xFFFFFFFFu; c.idx[k] = 0; c.oct[k] = -1; c.bin[k] = -1; }
-    int nc = -1;
-    const int m = S.last_mp[lb];
-    if (m >= 0 && !S.last_out[lb]) {
-        // twc = -Rcw^T tcw; tlc = Rlw twc + tlw (ORBmatcher.cc:1757-1771)
-        float twc[3];
-        for (int k = 0; k < 3; k++) {
-            float t = f.Tcw[k] * f.Tcw[3];
-            t = t + f.Tcw[4 + k] * f.Tcw[7];
-            t = t + f.Tcw[8 + k] * f.Tcw[11];
-            twc[k] = -t;
-        }
-        float tlc[3];
-        mat_rx_t(f.lTcw, twc, tlc);
-        const bool bForward = tlc[2] > f.mb && !mono;
-        const bool bBackward = -tlc[2] > f.mb && !mono;
-        const long long mb = (long long)s * S.cap_mp + m;
-        float x3Dc[3];
-        mat_rx_t(f.Tcw, S.Xw + mb * 3, x3Dc);
-        const float invzc = (float)(1.0 / (double)x3Dc[2]);
-        nc = 0;
-        if (!(invzc < 0)) {
-            const float u = f.fx * x3Dc[0] * invzc + f.cx;
-            const float v = f.fy * x3Dc[1] * invzc + f.cy;
-            if (!(u < f.min_x || u > f.max_x) && !(v < f.min_y || v > f.max_y)) {
-                const orbx_kp lk = S.lkun[lb];
-                const int nLastOctave = lk.octave;
-                const float radius = th * f.scale[nLastOctave];
-                int minL, maxL;
-                if (bForward) { minL = nLastOctave; maxL = -1; }
-                else if (bBackward) { minL = 0; maxL = nLastOctave; }
-                else { minL = nLastOctave - 1; maxL = nLastOctave + 1; }
-                const float ur = u - f.mbf * invzc;
-                nc = scan_window<false>(S, s, f, u, v, radius, minL, maxL, S.mdesc + mb * 32, ur, radius, nullptr,
-                                        lk.angle, c);
-            }
-        }
-    }
+    const int nc = frame_query(S, s, f, i, th, mono, nullptr, c);
+    const long long lb = (long long)s * S.cap_kp + i;
     cand[lb] = c;
     ncand[lb] = nc;
 }
 
-__global__ __launch_bounds__(256) void track_frame_resolve_kernel(Slots S, float th, int mono, int check_ori,
-                                                                  const Cand *cand, const int *ncand, int *owner,
-                                                                  int *nmatch, int *hist_idx, int8_t *hist_bin) {
-    extern __shared__ uint8_t claimed[];   // [cap_kp]
-    __shared__ Cand sc[kChunk];
-    __shared__ int snc[kChunk];
-    __shared__ int smp[kChunk];
+__global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float th, int mono, int check_ori,
+                                                                 const Cand *cand, const int *ncand, int *owner,
+                                                                 int *nmatch, int *hist_idx, int8_t *hist_bin) {
+    extern __shared__ uint8_t lds[];
+    uint8_t *claimed = lds;                                 // [cap_kp]
+    int *tag = (int *)(lds + ((S.cap_kp + 15) & ~15));       // [cap_kp]
+    int *wl = tag + S.cap_kp;                                // [cap_kp] last committed writer lane
     __shared__ int counts[HISTO_LENGTH];
-    __shared__ int s_nh, s_nm, s_top[3];
-    const int s = blockIdx.x, tid = threadIdx.x;
+    const int s = blockIdx.x, lane = threadIdx.x;
     const FrameDev &f = S.fr[s];
-    const long long kb = (long long)s * S.cap_kp;
-    for (int i = tid; i < f.n; i += 256) { claimed[i] = S.blocked[kb + i]; owner[kb + i] = -1; }
-    if (tid < HISTO_LENGTH) counts[tid] = 0;
+    const long long kb = (long long)s * S.cap_kp, mb0 = (long long)s * S.cap_mp;
+    for (int i = lane; i < f.n; i += 64) {
+        claimed[i] = S.blocked[kb + i]; tag[i] = kNoTag; wl[i] = -1; owner[kb + i] = -1;
+    }
+    if (lane < HISTO_LENGTH) counts[lane] = 0;
     __syncthreads();
-    int nm = 0, nh = 0;
+    int nm = 0, nh = 0, base = 0;
     int *HI = hist_idx + kb;
     int8_t *HB = hist_bin + kb;
-    for (int c0 = 0; c0 < f.n_last; c0 += kChunk) {
-        const int cn = min(kChunk, f.n_last - c0);
-        for (int i = tid; i < cn; i += 256) {
-            sc[i] = cand[kb + c0 + i];
-            snc[i] = ncand[kb + c0 + i];
-            smp[i] = S.last_mp[kb + c0 + i];
-        }
-        __syncthreads();
-        if (tid == 0) {
-            for (int i = 0; i < cn; i++) {
-                const int nc = snc[i];
-                if (nc <= 0) continue;
-                int b = -1;
-                for (int k = 0; k < TOPK; k++) {
-                    if (sc[i].key[k] == 0xFFFFFFFFu) break;
-                    if (!claimed[sc[i].idx[k]]) { b = k; break; }
-                }
-                Cand full;
-                const Cand *use = &sc[i];
-                if (b < 0 && nc > TOPK) {              // exact fallback: rescan with the claims
-                    const long long lb = kb + c0 + i;
-                    const int m = smp[i];
-                    const long long mb = (long long)s * S.cap_mp + m;
-                    float twc[3];
-                    for (int k = 0; k < 3; k++) {
-                        float t = f.Tcw[k] * f.Tcw[3];
-                        t = t + f.Tcw[4 + k] * f.Tcw[7];
-                        t = t + f.Tcw[8 + k] * f.Tcw[11];
-                        twc[k] = -t;
-                    }
-                    float tlc[3];
-                    mat_rx_t(f.lTcw, twc, tlc);
-                    const bool bForward = tlc[2] > f.mb && !mono;
-                    const bool bBackward = -tlc[2] > f.mb && !mono;
-                    float x3Dc[3];
-                    mat_rx_t(f.Tcw, S.Xw + mb * 3, x3Dc);
-                    const float invzc = (float)(1.0 / (double)x3Dc[2]);
-                    const float u = f.fx * x3Dc[0] * invzc + f.cx;
-                    const float v = f.fy * x3Dc[1] * invzc + f.cy;
-                    const orbx_kp lk = S.lkun[lb];
-                    const int o = lk.octave;
-                    const float radius = th * f.scale[o];
-                    const int minL = bForward ? o : (bBackward ? 0 : o - 1);
-                    const int maxL = bForward ? -1 : (bBackward ? o : o + 1);
-                    scan_window<false>(S, s, f, u, v, radius, minL, maxL, S.mdesc + mb * 32, u - f.mbf * invzc, radius,
-                                       claimed, lk.angle, full);
-                    use = &full;
-                    b = full.key[0] != 0xFFFFFFFFu ? 0 : -1;
-                }
-                if (b < 0) continue;
-                const int bestDist = (int)(use->key[b] >> 16);
-                if (bestDist <= TH_HIGH) {
-                    const int idx = use->idx[b];
-                    const int m = smp[i];
-                    owner[kb + idx] = m;
-                    claimed[idx] = (S.mflags[(long long)s * S.cap_mp + m] & ORBT_MP_HAS_OBS) ? 1 : 0;
-                    nm++;
-                    if (check_ori) {
-                        HI[nh] = idx;
-                        HB[nh] = use->bin[b];
-                        counts[use->bin[b]]++;
-                        nh++;
-                    }
-                }
+    while (base < f.n_last) {
+        const int q = base + lane;
+        const bool live = q < f.n_last;
+        Cand c;
+        int nc = -1, m = -1;
+        if (live) { c = cand[kb + q]; nc = ncand[kb + q]; m = S.last_mp[kb + q]; }
+        int b = -1, last_ex = -1;
+        if (nc > 0)
+            for (int k = 0; k < TOPK; k++) {
+                if (c.key[k] == 0xFFFFFFFFu) break;
+                last_ex = k;
+                if (!claimed[c.idx[k]]) { b = k; break; }
             }
+        const bool fallback = nc > TOPK && b < 0;
+        const bool accept = nc > 0 && !fallback && b >= 0 && (int)(c.key[b] >> 16) <= TH_HIGH;
+        const bool obs = m >= 0 && (S.mflags[mb0 + m] & ORBT_MP_HAS_OBS) != 0;
+        const int idx = b >= 0 ? c.idx[b] : 0;
+        if (accept && obs) atomicMin(&tag[idx], lane);
+        __syncthreads();
+        bool conflict = false;
+        for (int k = 0; k <= last_ex; k++) conflict |= tag[c.idx[k]] < lane;
+        const unsigned long long stop = __ballot(live && (conflict || fallback));
+        const int cut = stop ? __ffsll((long long)stop) - 1 : 64;
+        __syncthreads();
+        if (accept && obs) tag[idx] = kNoTag;
+        const bool commit = accept && lane < cut;
+        if (commit) {
+            // CurrentFrame.mvpMapPoints[bestIdx2] = pMP: the last committed lane wins
+            atomicMax(&wl[idx], lane);
+            if (obs) claimed[idx] = 1;
         }
         __syncthreads();
+        if (commit && wl[idx] == lane) owner[kb + idx] = m;
+        __syncthreads();
+        if (commit) wl[idx] = -1;
+        const unsigned long long cm = __ballot(commit);
+        if (commit && check_ori) {   // rotHist push order = query order
+            const int slot = nh + __popcll(cm & ((1ull << lane) - 1));
+            HI[slot] = idx;
+            HB[slot] = c.bin[b];
+            atomicAdd(&counts[c.bin[b]], 1);
+        }
+        nm += __popcll(cm);
+        if (check_ori) nh += __popcll(cm);
+        __syncthreads();
+        if (cut < 64 && base + cut < f.n_last && ((stop >> cut) & 1)) {
+            const bool is_fb = __shfl(fallback ? 1 : 0, cut) != 0;
+            if (is_fb) {
+                if (lane == 0) {
+                    const int qq = base + cut;
+                    Cand full;
+                    frame_query(S, s, f, qq, th, mono, claimed, full);
+                    if (full.key[0] != 0xFFFFFFFFu && (int)(full.key[0] >> 16) <= TH_HIGH) {
+                        const int id = full.idx[0], mm = S.last_mp[kb + qq];
+                        owner[kb + id] = mm;
+                        if (S.mflags[mb0 + mm] & ORBT_MP_HAS_OBS) claimed[id] = 1;
+                        nm++;
+                        if (check_ori) {
+                            HI[nh] = id;
+                            HB[nh] = full.bin[0];
+                            counts[full.bin[0]]++;
+                            nh++;
+                        }
+                    }
+                }
+                nm = __shfl(nm, 0);
+                nh = __shfl(nh, 0);
+                __syncthreads();
+                base += cut + 1;
+            } else {
+                base += cut;
+            }
+        } else {
+            base += 64;
+        }
     }
-    if (tid == 0) {
-        s_nh = nh;
-        s_nm = nm;
-        int ind1 = -1, ind2 = -1, ind3 = -1;
-        if (check_ori) {   // ComputeThreeMaxima (ORBmatcher.cc:2076-2118)
-            int max1 = 0, max2 = 0, max3 = 0;
+    if (check_ori) {
+        __shared__ int top[3];
+        if (lane == 0) {   // ComputeThreeMaxima (ORBmatcher.cc:2076-2118)
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < HISTO_LENGTH; i++) {
                 const int v = counts[i];
                 if (v > max1) { max3 = max2; max2 = max1; max1 = v; ind3 = ind2; ind2 = ind1; ind1 = i; }
@@ -554,23 +610,20 @@ __global__ __launch_bounds__(256) void track_frame_resolve_kernel(Slots S, float
             }
             if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
             else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            top[0] = ind1; top[1] = ind2; top[2] = ind3;
         }
-        s_top[0] = ind1; s_top[1] = ind2; s_top[2] = ind3;
-    }
-    __syncthreads();
-    if (check_ori) {
-        // mvpMapPoints[rotHist[bin][j]] = NULL for bins outside the top three
+        __syncthreads();
         int removed = 0;
-        for (int k = tid; k < s_nh; k += 256) {
-            const int b = HB[k];
-            if (b == s_top[0] || b == s_top[1] || b == s_top[2]) continue;
+        for (int k = lane; k < nh; k += 64) {   // mvpMapPoints[rotHist[bin][j]] = NULL outside the top three
+            const int bb = HB[k];
+            if (bb == top[0] || bb == top[1] || bb == top[2]) continue;
             owner[kb + HI[k]] = -2;
             removed++;
         }
-        atomicAdd(&s_nm, -removed);
-        __syncthreads();
+        for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);
+        nm -= removed;
     }
-    if (tid == 0) nmatch[s] = s_nm;
+    if (lane == 0) nmatch[s] = nm;
 }
 
 }  // namespace orbtrack
@@ -593,7 +646,7 @@ Slots make_slots(orbt_engine *e) {
     Slots S;
     S.fr = e->fr.as<FrameDev>();
     S.kun = e->kun.as<orbx_kp>(); S.uR = e->uR.as<float>(); S.desc = e->desc.as<uint8_t>();
-    S.blocked = e->blocked.as<uint8_t>(); S.keys = e->keys.as<uint32_t>(); S.cell_start = e->cell_start.as<int>();
+    S.blocked = e->blocked.as<uint8_t>(); S.grec = e->keys.as<float4>(); S.cell_start = e->cell_start.as<int>();
     S.lkun = e->lkun.as<orbx_kp>(); S.last_mp = e->last_mp.as<int>(); S.last_out = e->last_out.as<uint8_t>();
     S.Xw = e->Xw.as<float>(); S.nrm = e->nrm.as<float>(); S.mind = e->mind.as<float>(); S.maxd = e->maxd.as<float>();
     S.mdesc = e->mdesc.as<uint8_t>(); S.mflags = e->mflags.as<uint8_t>();
@@ -614,10 +667,12 @@ int max_n(orbt_engine *e, int which, int n) {
     return m;
 }
 
+size_t resolve_lds(const orbt_engine *e) { return ((e->cap_kp + 15) & ~15) + 2 * sizeof(int) * e->cap_kp; }
+
 hipStream_t pick(orbt_engine *e, void *stream) { return stream ? (hipStream_t)stream : e->stream; }
 
 int grid(orbt_engine *e, int n, hipStream_t st) {
-    track_grid_kernel<<<n, 1024, sizeof(uint32_t) * e->sort_cap, st>>>(make_slots(e), e->keys.as<uint32_t>(),
+    track_grid_kernel<<<n, 1024, sizeof(uint32_t) * e->sort_cap, st>>>(make_slots(e), e->keys.as<float4>(),
                                                                         e->cell_start.as<int>());
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
@@ -674,7 +729,7 @@ int orbt_reserve(orbt_engine *e, int n_slots, int cap_kp, int cap_mp) {
     while (sc < cap_kp) sc <<= 1;
     const size_t S = (size_t)n_slots, K = (size_t)cap_kp, M = (size_t)cap_mp;
     if (e->fr.ensure(sizeof(FrameDev) * S) || e->kun.ensure(sizeof(orbx_kp) * S * K) || e->uR.ensure(4 * S * K) ||
-        e->desc.ensure(32 * S * K) || e->blocked.ensure(S * K) || e->keys.ensure(4 * S * (size_t)sc) ||
+        e->desc.ensure(32 * S * K) || e->blocked.ensure(S * K) || e->keys.ensure(16 * S * (size_t)sc) ||
         e->cell_start.ensure(4 * S * (NCELL + 1)) || e->lkun.ensure(sizeof(orbx_kp) * S * K) ||
         e->last_mp.ensure(4 * S * K) || e->last_out.ensure(S * K) || e->Xw.ensure(12 * S * M) ||
         e->nrm.ensure(12 * S * M) || e->mind.ensure(4 * S * M) || e->maxd.ensure(4 * S * M) ||
@@ -753,7 +808,7 @@ int orbt_run_local_batch(orbt_engine *e, int n_slots, float view_cos_limit, floa
     track_local_cand_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), view_cos_limit, th,
                                                                              make_view(e), e->cand.as<Cand>(),
                                                                              e->ncand.as<int>());
-    track_local_resolve_kernel<<<n_slots, 256, e->cap_kp, st>>>(make_slots(e), th, nnratio, make_view(e),
+    track_local_resolve_kernel<<<n_slots, 64, resolve_lds(e), st>>>(make_slots(e), th, nnratio, make_view(e),
                                                                 e->cand.as<Cand>(), e->ncand.as<int>(),
                                                                 e->owner.as<int>(), e->nmatch.as<int>());
     TR_CHK(hipGetLastError());
@@ -768,7 +823,7 @@ int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int ch
     const int nl = std::max(1, max_n(e, 1, n_slots));
     track_frame_cand_kernel<<<dim3((nl + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, mono,
                                                                              e->cand.as<Cand>(), e->ncand.as<int>());
-    track_frame_resolve_kernel<<<n_slots, 256, e->cap_kp, st>>>(make_slots(e), th, mono, check_ori, e->cand.as<Cand>(),
+    track_frame_resolve_kernel<<<n_slots, 64, resolve_lds(e), st>>>(make_slots(e), th, mono, check_ori, e->cand.as<Cand>(),
                                                                 e->ncand.as<int>(), e->owner.as<int>(),
                                                                 e->nmatch.as<int>(), e->hist_idx.as<int>(),
                                                                 e->hist_bin.as<int8_t>());
