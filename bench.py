@@ -184,6 +184,48 @@ def bench_track(amd, args, dist, world, with_cpu):
     return res
 
 
+def bench_pose(amd, args, dist, world, with_cpu):
+    """§8f rank 2: Optimizer::PoseOptimization on B independent frames resident in HBM
+    (800 map-point matches each, 60 % stereo, 15 % outliers; synth.pose_problem), the whole
+    4-round LM solve on the GPU, one workgroup per frame."""
+    from orbslam2_amd import synth
+    from orbslam2_amd import dist as odist
+    B = args.pose_batch
+    probs = [synth.pose_problem(500 + i, n=800) for i in range(8)]
+    po = amd.PoseOptimizer()
+    po.reserve(B, 800)
+    for s in range(B):
+        po.stage(s, probs[s % len(probs)])
+    for _ in range(2):
+        po.run_batch(B)
+    amd.device_sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.pose_steps):
+        po.run_batch(B)
+    amd.device_sync()
+    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    r = po.fetch(0, 800)
+    res = {"pose_frames_per_s": round(world * B * args.pose_steps / dt, 2),
+           "pose": {"frames_per_step": B, "ms_per_step": round(1000 * dt / args.pose_steps, 3), "edges": 800,
+                    "inliers_slot0": int(r["n_inliers"]), "lm_iterations_slot0": list(r["iterations"]),
+                    "dtype": "f64"}}
+    po.close()
+    if with_cpu:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 3.0:
+            oracle.pose_optimization(probs[n % len(probs)])
+            n += 1
+        cdt = time.perf_counter() - t0
+        res["pose"]["cpu_baseline"] = {"value": round(n / cdt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+                                       "sample": f"{n} frames (8 distinct problems), oracle, single thread, {cdt:.1f} s"}
+    return res
+
+
 def load_traffic(kernel: str, batch: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
     f = ROOT / "profiles" / "pmc_traffic.json"
@@ -218,6 +260,9 @@ def main():
     ap.add_argument("--track-batch", type=int, default=256)
     ap.add_argument("--track-steps", type=int, default=10)
     ap.add_argument("--no-track", action="store_true")
+    ap.add_argument("--pose-batch", type=int, default=256)
+    ap.add_argument("--pose-steps", type=int, default=10)
+    ap.add_argument("--no-pose", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -330,6 +375,8 @@ def main():
         out.update(bench_rgbd(amd, args, dist, world))
     if not args.no_track:
         out.update(bench_track(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
+    if not args.no_pose:
+        out.update(bench_pose(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if not args.no_lba:
         out.update(bench_localba(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

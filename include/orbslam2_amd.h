@@ -220,6 +220,43 @@ int orbt_run_local_batch(orbt_engine *e, int n_slots, float view_cos_limit, floa
 int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int check_ori, void *stream);
 int orbt_fetch(orbt_engine *e, int slot, orbt_view *view, int32_t *owner, int32_t *nmatches);
 
+/* -------- pose-only optimisation (replaces Optimizer::PoseOptimization) -------- */
+
+/* The edges Optimizer::PoseOptimization (Optimizer.h:105, Optimizer.cc:375-622) builds from a
+ * Frame: one per keypoint i with pFrame->mvpMapPoints[i] != NULL, in keypoint order
+ * (the caller compacts them; edge k <-> keypoint i_k). obs = (mvKeysUn[i].pt, mvuRight[i]):
+ * uR < 0 -> EdgeSE3ProjectXYZOnlyPose (mono), else EdgeStereoSE3ProjectXYZOnlyPose. */
+typedef struct {
+    int32_t n;                   /* edges */
+    const float *Xw;             /* [n][3] MapPoint::GetWorldPos() */
+    const float *obs;            /* [n][3] u, v, uR */
+    const float *inv_sigma2;     /* [n] mvInvLevelSigma2[mvKeysUn[i].octave] */
+    float Tcw[16];               /* pFrame->mTcw (row-major, CV_32F), the start of every round */
+    float fx, fy, cx, cy, bf;    /* Frame::fx.. and mbf */
+} orbp_frame;
+
+typedef struct {
+    float Tcw[16];               /* pFrame->SetPose(...) value (unchanged input if < 3 edges) */
+    uint8_t *outlier;            /* [n] out: pFrame->mvbOutlier[i_k] */
+    int32_t n_inliers;           /* the return value: nInitialCorrespondences - nBad (0 if < 3) */
+    int32_t iterations[4];       /* LM iterations per round (-1 = round not run) */
+} orbp_result;
+
+typedef struct orbp_engine orbp_engine;
+
+int orbp_create(orbp_engine **out);
+void orbp_destroy(orbp_engine *e);
+/* Optimizer::PoseOptimization(Frame*): four rounds of optimize(10) from the frame's pose with
+ * Huber kernels in rounds 0-2, outliers (chi2 > 5.991 mono / 7.815 stereo on g2o's last
+ * _error) moved to level 1 between rounds. The whole Levenberg-Marquardt loop runs on the GPU
+ * (one workgroup per frame, no host round trips). */
+int orbp_pose_optimization(orbp_engine *e, const orbp_frame *f, orbp_result *r);
+/* Batched device-resident form: stage frames into slots, one launch solves every slot. */
+int orbp_reserve(orbp_engine *e, int n_slots, int cap_edges);
+int orbp_stage(orbp_engine *e, int slot, const orbp_frame *f);
+int orbp_run_batch(orbp_engine *e, int n_slots, void *stream);
+int orbp_fetch(orbp_engine *e, int slot, orbp_result *r);
+
 /* -------- local bundle adjustment (replaces Optimizer::LocalBundleAdjustment) -------- */
 
 /* The graph Optimizer::LocalBundleAdjustment (Optimizer.cc:646-898) builds from the map,

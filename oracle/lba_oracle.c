@@ -655,3 +655,271 @@ int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint
     free(g.T); free(g.X); free(g.E); free(g.pose_hidx); free(g.point_hidx); free(g.hpose); free(g.hpoint);
     return rc;
 }
+
+/* ==========================================================================================
+ * Optimizer::PoseOptimization (Optimizer.cc:375-622): one VertexSE3Expmap, unary edges
+ * EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose (types_six_dof_expmap.h:143-205,
+ * .cpp:266-364), BlockSolver_6_3 over LinearSolverDense (linear_solver_dense.h:60-118:
+ * Eigen::LDLT with diagonal pivoting, restated below), OptimizationAlgorithmLevenberg as above.
+ * ========================================================================================*/
+typedef struct {
+    double Xw[3], obs[3], info, delta, dsqr;
+    double err[3];
+    int stereo, level, robust;
+} pedge_t;
+
+typedef struct { double fx, fy, cx, cy, bf; } pcam_t;
+
+/* computeError: _error = obs - cam_project(T.map(Xw)) */
+static void pedge_error(const se3 *T, const pcam_t *c, pedge_t *e) {
+    double p[3];
+    se3_map(T, e->Xw, p);
+    if (!e->stereo) {                          /* project2d then * f + c */
+        const double u = p[0] / p[2], v = p[1] / p[2];
+        e->err[0] = e->obs[0] - (u * c->fx + c->cx);
+        e->err[1] = e->obs[1] - (v * c->fy + c->cy);
+        e->err[2] = 0;
+    } else {                                   /* float invz, double bf member (:325-332) */
+        const float invz = (float)(1.0 / p[2]);
+        const double r0 = p[0] * invz * c->fx + c->cx;
+        const double r1 = p[1] * invz * c->fy + c->cy;
+        const double r2 = r0 - c->bf * invz;
+        e->err[0] = e->obs[0] - r0;
+        e->err[1] = e->obs[1] - r1;
+        e->err[2] = e->obs[2] - r2;
+    }
+}
+
+static double pedge_chi2(const pedge_t *e) {
+    double s = e->err[0] * e->info * e->err[0] + e->err[1] * e->info * e->err[1];
+    if (e->stereo) s += e->err[2] * e->info * e->err[2];
+    return s;
+}
+
+static double pedge_rho(const pedge_t *e, double chi, double *w) {
+    if (!e->robust) { *w = 1.0; return chi; }
+    if (chi <= e->dsqr) { *w = 1.0; return chi; }
+    const double s = sqrt(chi);
+    *w = e->delta / s;
+    return 2 * s * e->delta - e->dsqr;
+}
+
+/* linearizeOplus (:283-301, :337-362) */
+static void pedge_jacobian(const se3 *T, const pcam_t *c, const pedge_t *e, double J[18]) {
+    double p[3];
+    se3_map(T, e->Xw, p);
+    const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
+    const double fx = c->fx, fy = c->fy;
+    J[0] = x * y * invz_2 * fx; J[1] = -(1 + (x * x * invz_2)) * fx; J[2] = y * invz * fx;
+    J[3] = -invz * fx; J[4] = 0; J[5] = x * invz_2 * fx;
+    J[6] = (1 + y * y * invz_2) * fy; J[7] = -x * y * invz_2 * fy; J[8] = -x * invz * fy;
+    J[9] = 0; J[10] = -invz * fy; J[11] = y * invz_2 * fy;
+    if (e->stereo) {
+        J[12] = J[0] - c->bf * y * invz_2; J[13] = J[1] + c->bf * x * invz_2; J[14] = J[2];
+        J[15] = J[3]; J[16] = 0; J[17] = J[5] - c->bf * invz_2;
+    }
+}
+
+/* Eigen::LDLT<MatrixXd> (lower, diagonal pivoting) compute + solve, restated; returns 0 when
+ * !isPositive() */
+int orc_ldlt_solve6(const double Hin[36], const double b[6], double x[6]) {
+    double m[36];
+    int tr[6];
+    memcpy(m, Hin, sizeof(m));
+    const int n = 6;
+    int sign = 0;   /* 0 zero, 1 positive-semidef, 2 negative-semidef, 3 indefinite */
+    for (int k = 0; k < n; k++) {
+        int big = k;
+        double bv = fabs(m[7 * k]);
+        for (int i = k + 1; i < n; i++)
+            if (fabs(m[7 * i]) > bv) { bv = fabs(m[7 * i]); big = i; }
+        tr[k] = big;
+        if (big != k) {
+            for (int j = 0; j < k; j++) { double t = m[6 * k + j]; m[6 * k + j] = m[6 * big + j]; m[6 * big + j] = t; }
+            for (int i = big + 1; i < n; i++) { double t = m[6 * i + k]; m[6 * i + k] = m[6 * i + big]; m[6 * i + big] = t; }
+            double t = m[7 * k]; m[7 * k] = m[7 * big]; m[7 * big] = t;
+            for (int i = k + 1; i < big; i++) {
+                double t2 = m[6 * i + k];
+                m[6 * i + k] = m[6 * big + i];
+                m[6 * big + i] = t2;
+            }
+        }
+        double temp[6];
+        if (k > 0) {
+            for (int j = 0; j < k; j++) temp[j] = m[7 * j] * m[6 * k + j];
+            double s = 0;
+            for (int j = 0; j < k; j++) s += m[6 * k + j] * temp[j];
+            m[7 * k] -= s;
+            for (int i = k + 1; i < n; i++) {
+                double t = 0;
+                for (int j = 0; j < k; j++) t += m[6 * i + j] * temp[j];
+                m[6 * i + k] -= t;
+            }
+        }
+        const double akk = m[7 * k];
+        const int valid = fabs(akk) > 0;
+        if (k == 0 && !valid) return 0;
+        if (valid)
+            for (int i = k + 1; i < n; i++) m[6 * i + k] /= akk;
+        if (sign == 1) { if (akk < 0) sign = 3; }
+        else if (sign == 2) { if (akk > 0) sign = 3; }
+        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    }
+    if (!(sign == 1 || sign == 0)) return 0;
+    /* solve: x = P^T L^-T D^+ L^-1 P b */
+    double y[6];
+    memcpy(y, b, sizeof(y));
+    for (int k = 0; k < n; k++) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < i; j++) y[i] -= m[6 * i + j] * y[j];
+    const double tol = DBL_MIN;
+    for (int i = 0; i < n; i++) y[i] = fabs(m[7 * i]) > tol ? y[i] / m[7 * i] : 0.0;
+    for (int i = n - 1; i >= 0; i--)
+        for (int j = i + 1; j < n; j++) y[i] -= m[6 * j + i] * y[j];
+    for (int k = n - 1; k >= 0; k--) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+    memcpy(x, y, sizeof(y));
+    return 1;
+}
+
+/* SparseOptimizer::optimize(iterations) on the single pose vertex; returns iterations run
+ * (-1 when no edge is active: "0 vertices to optimize") */
+static int pose_optimize(se3 *T, const pcam_t *c, pedge_t *E, int n, int iterations) {
+    int nact = 0;
+    for (int k = 0; k < n; k++) nact += E[k].level == 0;
+    if (nact == 0) return -1;
+    double lambda = 0, ni = 2;
+    int nBad = 0, it = 0;
+    for (int i = 0; i < iterations; i++) {
+        double H[36], b[6];
+        double currentChi = 0;
+        for (int k = 0; k < n; k++)
+            if (E[k].level == 0) { pedge_error(T, c, &E[k]); double w; currentChi += pedge_rho(&E[k], pedge_chi2(&E[k]), &w); }
+        const double iniChi = currentChi;
+        memset(H, 0, sizeof(H));
+        memset(b, 0, sizeof(b));
+        for (int k = 0; k < n; k++) {            /* BaseUnaryEdge::constructQuadraticForm */
+            pedge_t *e = &E[k];
+            if (e->level != 0) continue;
+            double J[18], w;
+            pedge_jacobian(T, c, e, J);
+            pedge_rho(e, pedge_chi2(e), &w);
+            const int D = e->stereo ? 3 : 2;
+            for (int a = 0; a < 6; a++) {
+                double s = 0;
+                for (int r = 0; r < D; r++) s += J[6 * r + a] * (e->info * e->err[r]);
+                b[a] -= w * s;
+                for (int cc = 0; cc < 6; cc++) {
+                    double h = 0;
+                    for (int r = 0; r < D; r++) h += J[6 * r + a] * (w * e->info) * J[6 * r + cc];
+                    H[6 * a + cc] += h;
+                }
+            }
+        }
+        if (i == 0) {                            /* computeLambdaInit */
+            double mx = 0;
+            for (int a = 0; a < 6; a++) mx = fmax(fabs(H[7 * a]), mx);
+            lambda = 1e-5 * mx;
+            ni = 2;
+            nBad = 0;
+        }
+        double rho = 0, tempChi;
+        int qmax = 0;
+        do {
+            const se3 save = *T;                 /* push */
+            double Hl[36], x[6];
+            memcpy(Hl, H, sizeof(H));
+            for (int a = 0; a < 6; a++) Hl[7 * a] += lambda;
+            const int ok2 = orc_ldlt_solve6(Hl, b, x);
+            se3 d = se3_exp(x);
+            *T = se3_mul(&d, T);
+            tempChi = 0;
+            for (int k = 0; k < n; k++)
+                if (E[k].level == 0) { pedge_error(T, c, &E[k]); double w; tempChi += pedge_rho(&E[k], pedge_chi2(&E[k]), &w); }
+            if (!ok2) tempChi = DBL_MAX;
+            rho = currentChi - tempChi;
+            double scale = 0;
+            for (int a = 0; a < 6; a++) scale += x[a] * (lambda * x[a] + b[a]);
+            scale += 1e-3;
+            rho /= scale;
+            if (rho > 0 && isfinite(tempChi)) {
+                double alpha = 1. - pow((2 * rho - 1), 3);
+                alpha = fmin(alpha, 2. / 3.);
+                lambda *= fmax(1. / 3., alpha);
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                *T = save;                       /* pop (the edges keep the trial _error) */
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10);
+        it++;
+        int ok = 1;
+        if (qmax == 10 || rho == 0) ok = 0;
+        else {
+            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++; else nBad = 0;
+            if (nBad >= 3) ok = 0;
+        }
+        if (!ok) break;
+    }
+    return it;
+}
+
+int pose_oracle_optimize(const orbp_frame *f, orbp_result *r) {
+    const int n = f->n;
+    memcpy(r->Tcw, f->Tcw, sizeof(r->Tcw));
+    for (int k = 0; k < 4; k++) r->iterations[k] = -1;
+    for (int k = 0; k < n; k++) r->outlier[k] = 0;    /* mvbOutlier[i] = false at edge creation */
+    if (n < 3) { r->n_inliers = 0; return 0; }
+    pcam_t c = {f->fx, f->fy, f->cx, f->cy, f->bf};
+    pedge_t *E = (pedge_t *)calloc((size_t)n + 1, sizeof(pedge_t));
+    const float deltaMono = (float)sqrt(5.991), deltaStereo = (float)sqrt(7.815);
+    for (int k = 0; k < n; k++) {
+        pedge_t *e = &E[k];
+        for (int j = 0; j < 3; j++) e->Xw[j] = f->Xw[3 * k + j];
+        e->stereo = f->obs[3 * k + 2] >= 0;
+        e->obs[0] = f->obs[3 * k]; e->obs[1] = f->obs[3 * k + 1]; e->obs[2] = e->stereo ? f->obs[3 * k + 2] : 0;
+        e->info = f->inv_sigma2[k];
+        e->delta = e->stereo ? deltaStereo : deltaMono;
+        e->dsqr = e->delta * e->delta;
+        e->robust = 1;
+        e->level = 0;
+    }
+    /* Converter::toSE3Quat(pFrame->mTcw) */
+    se3 T0;
+    {
+        const float *m = f->Tcw;
+        const double R[9] = {m[0], m[1], m[2], m[4], m[5], m[6], m[8], m[9], m[10]};
+        T0.r = quat_from_R(R);
+        T0.t[0] = m[3]; T0.t[1] = m[7]; T0.t[2] = m[11];
+        quat_normalize_g2o(&T0.r);
+    }
+    const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
+    se3 T = T0;
+    int nBad = 0;
+    for (int it = 0; it < 4; it++) {
+        T = T0;                                       /* vSE3->setEstimate(toSE3Quat(mTcw)) */
+        r->iterations[it] = pose_optimize(&T, &c, E, n, 10);
+        nBad = 0;
+        for (int k = 0; k < n; k++) {
+            pedge_t *e = &E[k];
+            if (r->outlier[k]) pedge_error(&T, &c, e);
+            const float chi2 = (float)pedge_chi2(e);
+            if (chi2 > (e->stereo ? chi2Stereo : chi2Mono)) { r->outlier[k] = 1; e->level = 1; nBad++; }
+            else { r->outlier[k] = 0; e->level = 0; }
+            if (it == 2) e->robust = 0;
+        }
+        if (n < 10) break;                            /* optimizer.edges().size() < 10 */
+    }
+    double R[9];
+    quat_to_R(T.r, R);
+    for (int a = 0; a < 3; a++) {
+        for (int b2 = 0; b2 < 3; b2++) r->Tcw[4 * a + b2] = (float)R[3 * a + b2];
+        r->Tcw[4 * a + 3] = (float)T.t[a];
+    }
+    r->Tcw[12] = 0; r->Tcw[13] = 0; r->Tcw[14] = 0; r->Tcw[15] = 1;
+    r->n_inliers = n - nBad;
+    free(E);
+    return 0;
+}

@@ -425,3 +425,37 @@ def search_by_projection_frame(prob: dict, th=15.0, mono=False, check_ori=True):
                                           C.byref(M), th, 1 if mono else 0, 1 if check_ori else 0,
                                           blk.ctypes.data if blk is not None else None, owner.ctypes.data)
     return nm, owner[: F.n]
+
+
+# ---- Optimizer::PoseOptimization (lba_oracle.c pose_oracle_optimize)
+class OrbpFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("Xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p),
+                ("Tcw", C.c_float * 16), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("bf", C.c_float)]
+
+
+class OrbpResult(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 16), ("outlier", C.c_void_p), ("n_inliers", C.c_int32),
+                ("iterations", C.c_int32 * 4)]
+
+
+def make_orbp_frame(prob: dict):
+    keep = {k: np.ascontiguousarray(prob[k], np.float32) for k in ("Xw", "obs", "inv_sigma2")}
+    F = OrbpFrame()
+    F.n = len(keep["Xw"])
+    F.Xw, F.obs, F.inv_sigma2 = (keep[k].ctypes.data for k in ("Xw", "obs", "inv_sigma2"))
+    F.Tcw[:] = [float(v) for v in np.asarray(prob["Tcw"], np.float32).reshape(-1)]
+    F.fx, F.fy, F.cx, F.cy, F.bf = (float(v) for v in prob["cam"])
+    return F, keep
+
+
+def pose_optimization(prob: dict):
+    L = lib()
+    L.pose_oracle_optimize.argtypes = [C.c_void_p, C.c_void_p]
+    F, keep = make_orbp_frame(prob)
+    out = np.zeros(max(F.n, 1), np.uint8)
+    R = OrbpResult()
+    R.outlier = out.ctypes.data
+    L.pose_oracle_optimize(C.byref(F), C.byref(R))
+    return {"Tcw": np.array(R.Tcw[:], np.float32).reshape(4, 4), "outlier": out[: F.n].copy(),
+            "n_inliers": R.n_inliers, "iterations": tuple(R.iterations)}

@@ -85,6 +85,13 @@ SIGNATURES = [
     ("orbt_run_local_batch", _I, [_P, _I, _F, _F, _F, _P]),
     ("orbt_run_frame_batch", _I, [_P, _I, _F, _I, _I, _P]),
     ("orbt_fetch", _I, [_P, _I, _P, _P, _P]),
+    ("orbp_create", _I, [C.POINTER(C.c_void_p)]),
+    ("orbp_destroy", None, [_P]),
+    ("orbp_pose_optimization", _I, [_P, _P, _P]),
+    ("orbp_reserve", _I, [_P, _I, _I]),
+    ("orbp_stage", _I, [_P, _I, _P]),
+    ("orbp_run_batch", _I, [_P, _I, _P]),
+    ("orbp_fetch", _I, [_P, _I, _P]),
 ]
 
 
@@ -547,3 +554,80 @@ class Tracker:
         _check(lib().orbt_fetch(self._h, slot, C.byref(V) if V is not None else None, owner.ctypes.data,
                                 C.byref(nm)), "orbt_fetch")
         return nm.value, owner[:n_kp], view
+
+
+# ---- Optimizer::PoseOptimization (orbp_*) ----------------------------------------------------
+class OrbpFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("Xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p),
+                ("Tcw", C.c_float * 16), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("bf", C.c_float)]
+
+
+class OrbpResult(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 16), ("outlier", C.c_void_p), ("n_inliers", C.c_int32),
+                ("iterations", C.c_int32 * 4)]
+
+
+def _orbp_frame(prob: dict):
+    keep = {k: np.ascontiguousarray(prob[k], np.float32) for k in ("Xw", "obs", "inv_sigma2")}
+    F = OrbpFrame()
+    F.n = len(keep["Xw"])
+    F.Xw, F.obs, F.inv_sigma2 = (keep[k].ctypes.data for k in ("Xw", "obs", "inv_sigma2"))
+    F.Tcw[:] = [float(v) for v in np.asarray(prob["Tcw"], np.float32).reshape(-1)]
+    F.fx, F.fy, F.cx, F.cy, F.bf = (float(v) for v in prob["cam"])
+    return F, keep
+
+
+class PoseOptimizer:
+    """Optimizer::PoseOptimization (Optimizer.h:105) on the GPU: the whole 4-round
+    Levenberg-Marquardt solve in one workgroup per frame. Problems are dicts shaped like
+    synth.pose_problem: {"Xw", "obs", "inv_sigma2", "Tcw", "cam"}."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        _check(lib().orbp_create(C.byref(h)), "orbp_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _result(n):
+        out = np.zeros(max(n, 1), np.uint8)
+        R = OrbpResult()
+        R.outlier = out.ctypes.data
+        return R, out
+
+    @staticmethod
+    def _pack(R, out, n):
+        return {"Tcw": np.array(R.Tcw[:], np.float32).reshape(4, 4), "outlier": out[:n].copy(),
+                "n_inliers": R.n_inliers, "iterations": tuple(R.iterations)}
+
+    def optimize(self, prob: dict) -> dict:
+        F, keep = _orbp_frame(prob)
+        R, out = self._result(F.n)
+        _check(lib().orbp_pose_optimization(self._h, C.byref(F), C.byref(R)), "orbp_pose_optimization")
+        return self._pack(R, out, F.n)
+
+    def reserve(self, n_slots: int, cap_edges: int):
+        _check(lib().orbp_reserve(self._h, n_slots, cap_edges), "orbp_reserve")
+
+    def stage(self, slot: int, prob: dict):
+        F, keep = _orbp_frame(prob)
+        _check(lib().orbp_stage(self._h, slot, C.byref(F)), "orbp_stage")
+
+    def run_batch(self, n_slots: int, stream=None):
+        _check(lib().orbp_run_batch(self._h, n_slots, stream), "orbp_run_batch")
+
+    def fetch(self, slot: int, n: int) -> dict:
+        R, out = self._result(n)
+        _check(lib().orbp_fetch(self._h, slot, C.byref(R)), "orbp_fetch")
+        return self._pack(R, out, n)

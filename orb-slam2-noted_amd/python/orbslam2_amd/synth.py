@@ -380,3 +380,47 @@ def tracking_problem(seed: int = 5, n_kp: int = 2000, n_mp: int = 3000, W: int =
     kp_blocked = (rng.random(len(keys)) < 0.05).astype(np.uint8)
     return {"frame": frame, "map": mp, "last": last, "last_mp": last_mp, "last_outlier": last_out,
             "kp_blocked": kp_blocked}
+
+
+# ---------------------------------------------------------------------------------------
+# Optimizer::PoseOptimization: one frame's map-point matches. KITTI
+# camera; points 3..45 m in front; observations = projections of the true pose with noise
+# sigma = scale[octave] (uR from the true depth for stereo edges), `outlier_frac` of them
+# moved 8..60 px; the starting pose is the true one perturbed by ~1 deg / 10 cm (a motion-
+# model prediction).
+# ---------------------------------------------------------------------------------------
+def pose_problem(seed: int = 7, n: int = 600, stereo_frac: float = 0.6, outlier_frac: float = 0.15,
+                 W: int = 1241, H: int = 376, rot_deg: float = 1.0, trans_m: float = 0.1):
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = KITTI_CAM
+    sf = np.float32(1.2) ** np.arange(8, dtype=np.float32)
+    inv_s2 = (np.float32(1) / (sf * sf)).astype(np.float32)
+    feat = np.array([434, 362, 302, 251, 209, 175, 145, 122], np.float64)
+    Rt = _small_rot(rng, 3.0)
+    tt = rng.normal(0, 1.0, 3)
+    u = rng.uniform(0, W, n)
+    v = rng.uniform(0, H, n)
+    z = rng.uniform(3, 45, n)
+    Pc = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    Xw = (Pc - tt) @ Rt
+    octv = rng.choice(8, size=n, p=feat / feat.sum())
+    s = sf[octv].astype(np.float64)
+    ou = u + rng.normal(0, 1, n) * s
+    ov = v + rng.normal(0, 1, n) * s
+    ur = ou - bf / z + rng.normal(0, 1, n) * s
+    st = rng.random(n) < stereo_frac
+    bad = rng.random(n) < outlier_frac
+    ang = rng.uniform(0, 2 * np.pi, int(bad.sum()))
+    mag = rng.uniform(8, 60, int(bad.sum()))
+    ou[bad] += mag * np.cos(ang)
+    ov[bad] += mag * np.sin(ang)
+    obs = np.stack([ou, ov, np.where(st, ur, -1.0)], 1).astype(np.float32)
+    R0 = Rt @ _small_rot(rng, rot_deg)
+    t0 = tt + rng.normal(0, trans_m, 3)
+    T = np.eye(4, dtype=np.float32)
+    T[:3, :3] = R0
+    T[:3, 3] = t0
+    return {"Xw": Xw.astype(np.float32), "obs": obs, "inv_sigma2": inv_s2[octv].astype(np.float32),
+            "Tcw": T, "cam": (np.float32(fx), np.float32(fy), np.float32(cx), np.float32(cy), np.float32(bf)),
+            "true_Tcw": np.concatenate([np.concatenate([Rt, tt[:, None]], 1), [[0, 0, 0, 1]]]).astype(np.float32),
+            "is_outlier": bad}
