@@ -180,38 +180,46 @@ __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
         const int D = e.stereo ? 3 : 2;
         const double wW = r1 * e.info;
         double omr[3];
-        for (int i = 0; i < D; i++) omr[i] = -(e.info * err[i]) * r1;
+        _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) omr[i] = -(e.info * err[i]) * r1;
         double *c = g.con + (long long)s * 36;
         int u = 0;
+#pragma unroll
         for (int a = 0; a < 3; a++)
+#pragma unroll
             for (int b = a; b < 3; b++) {
                 double h = 0;
-                for (int i = 0; i < D; i++) h += Jp[3 * i + a] * wW * Jp[3 * i + b];
+                _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jp[3 * i + a] * wW * Jp[3 * i + b];
                 c[u++] = h;
             }
+#pragma unroll
         for (int a = 0; a < 3; a++) {
             double v = 0;
-            for (int i = 0; i < D; i++) v += Jp[3 * i + a] * omr[i];
+            _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) v += Jp[3 * i + a] * omr[i];
             c[6 + a] = v;
         }
         if (g.pose_hidx[e.pose] >= 0) {
             u = 9;
+#pragma unroll
             for (int a = 0; a < 6; a++)
+#pragma unroll
                 for (int b = a; b < 6; b++) {
                     double h = 0;
-                    for (int i = 0; i < D; i++) h += Jt[6 * i + a] * wW * Jt[6 * i + b];
+                    _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jt[6 * i + a] * wW * Jt[6 * i + b];
                     c[u++] = h;
                 }
+#pragma unroll
             for (int a = 0; a < 6; a++) {
                 double v = 0;
-                for (int i = 0; i < D; i++) v += Jt[6 * i + a] * omr[i];
+                _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) v += Jt[6 * i + a] * omr[i];
                 c[30 + a] = v;
             }
             double *hp = g.hpl + (long long)s * 18;
+#pragma unroll
             for (int a = 0; a < 6; a++)
+#pragma unroll
                 for (int b = 0; b < 3; b++) {
                     double h = 0;
-                    for (int i = 0; i < D; i++) h += Jt[6 * i + a] * wW * Jp[3 * i + b];
+                    _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jt[6 * i + a] * wW * Jp[3 * i + b];
                     hp[3 * a + b] = h;
                 }
         }

@@ -119,9 +119,9 @@ __device__ inline void block_reduce(double *v, double *red, double (*wsum)[kRed]
 }
 
 // Eigen::LDLT<MatrixXd> (lower, diagonal pivoting) + solve; false when !isPositive()
-__device__ bool ldlt_solve6(const double *Hin, const double *b, double *x) {
-    double m[36];
-    int tr[6];
+// m (36), tr (6), y (6): workspace with data-dependent indexing -> LDS, not scratch
+__device__ bool ldlt_solve6(const double *Hin, const double *b, double *x, double *m, int *tr, double *y,
+                            double *temp) {
     for (int i = 0; i < 36; i++) m[i] = Hin[i];
     int sign = 0;
     for (int k = 0; k < 6; k++) {
@@ -136,7 +136,6 @@ __device__ bool ldlt_solve6(const double *Hin, const double *b, double *x) {
             const double t = m[7 * k]; m[7 * k] = m[7 * big]; m[7 * big] = t;
             for (int i = k + 1; i < big; i++) { const double t2 = m[6 * i + k]; m[6 * i + k] = m[6 * big + i]; m[6 * big + i] = t2; }
         }
-        double temp[6];
         if (k > 0) {
             for (int j = 0; j < k; j++) temp[j] = m[7 * j] * m[6 * k + j];
             double s = 0;
@@ -158,7 +157,6 @@ __device__ bool ldlt_solve6(const double *Hin, const double *b, double *x) {
         else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
     }
     if (!(sign == 1 || sign == 0)) return false;
-    double y[6];
     for (int i = 0; i < 6; i++) y[i] = b[i];
     for (int k = 0; k < 6; k++) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
     for (int i = 0; i < 6; i++)
@@ -176,6 +174,8 @@ struct Shared {
     double red[kRed];
     double wsum[4][kRed];
     double H[36], b[6];
+    double Hl[36], work[36], y[6], temp[6], x[6];
+    int tr[6];
     double lambda, ni, currentChi, iniChi, rho;
     int qmax, nBad, stop, cnt;
 };
@@ -212,17 +212,23 @@ __device__ void accumulate(const PoseSlots &P, int s, const FrameHdr &h, const P
             J[9] = 0; J[10] = -invz * h.fy; J[11] = y * invz_2 * h.fy;
             J[12] = J[0] - h.bf * y * invz_2; J[13] = J[1] + h.bf * x * invz_2; J[14] = J[2];
             J[15] = J[3]; J[16] = 0; J[17] = J[5] - h.bf * invz_2;
-            const int D = stereo ? 3 : 2;
-            int u = 1;   // lower triangle (the part Eigen::LDLT reads), row-major
+            // lower triangle (the part Eigen::LDLT reads), row-major; constant register indices
+            const double W = w * info;
+            int u = 1;
+#pragma unroll
             for (int a = 0; a < 6; a++)
+#pragma unroll
                 for (int c = 0; c <= a; c++) {
-                    double hh = 0;
-                    for (int r = 0; r < D; r++) hh += J[6 * r + a] * (w * info) * J[6 * r + c];
+                    double hh = J[a] * W * J[c];
+                    hh += J[6 + a] * W * J[6 + c];
+                    if (stereo) hh += J[12 + a] * W * J[12 + c];
                     v[u++] += hh;
                 }
+#pragma unroll
             for (int a = 0; a < 6; a++) {
-                double t = 0;
-                for (int r = 0; r < D; r++) t += J[6 * r + a] * (info * e[r]);
+                double t = J[a] * (info * e[0]);
+                t += J[6 + a] * (info * e[1]);
+                if (stereo) t += J[12 + a] * (info * e[2]);
                 v[22 + a] -= w * t;
             }
         }
@@ -242,8 +248,18 @@ __device__ int optimize(const PoseSlots &P, int s, const FrameHdr &h, bool robus
     __syncthreads();
     if (sh.cnt == 0) return -1;
     int it = 0;
+#ifdef ORBP_PROFILE
+    long long t_lin = 0, t_solve = 0, t_trial = 0, t_acc = 0, t0;
+#define PT0() t0 = clock64()
+#define PT1(v) v += clock64() - t0
+#else
+#define PT0()
+#define PT1(v)
+#endif
     for (int i = 0; i < iterations; i++) {
+        PT0();
         accumulate(P, s, h, sh.T, robust, true, sh);
+        PT1(t_lin);
         if (tid == 0) {
             sh.currentChi = sh.iniChi = sh.red[0];
             int u = 1;
@@ -261,23 +277,26 @@ __device__ int optimize(const PoseSlots &P, int s, const FrameHdr &h, bool robus
         }
         __syncthreads();
         bool ok2 = true;
-        double x[6];
         do {
+            PT0();
             if (tid == 0) {
-                double Hl[36];
-                for (int k = 0; k < 36; k++) Hl[k] = sh.H[k];
-                for (int a = 0; a < 6; a++) Hl[7 * a] += sh.lambda;
-                ok2 = ldlt_solve6(Hl, sh.b, x);
-                sh.T2 = pose_oplus(sh.T, x);           // VertexSE3Expmap::oplusImpl
+                for (int k = 0; k < 36; k++) sh.Hl[k] = sh.H[k];
+                for (int a = 0; a < 6; a++) sh.Hl[7 * a] += sh.lambda;
+                ok2 = ldlt_solve6(sh.Hl, sh.b, sh.x, sh.work, sh.tr, sh.y, sh.temp);
+                sh.T2 = pose_oplus(sh.T, sh.x);           // VertexSE3Expmap::oplusImpl
             }
             __syncthreads();
+            PT1(t_solve);
+            PT0();
             accumulate(P, s, h, sh.T2, robust, false, sh);
+            PT1(t_trial);
+            PT0();
             if (tid == 0) {
                 double tempChi = sh.red[0];
                 if (!ok2) tempChi = DBL_MAX;
                 double rho = sh.currentChi - tempChi;
                 double scale = 0;
-                for (int a = 0; a < 6; a++) scale += x[a] * (sh.lambda * x[a] + sh.b[a]);
+                for (int a = 0; a < 6; a++) scale += sh.x[a] * (sh.lambda * sh.x[a] + sh.b[a]);
                 scale += 1e-3;
                 rho /= scale;
                 if (rho > 0 && isfinite(tempChi)) {
@@ -295,6 +314,7 @@ __device__ int optimize(const PoseSlots &P, int s, const FrameHdr &h, bool robus
                 sh.qmax++;
             }
             __syncthreads();
+            PT1(t_acc);
         } while (sh.rho < 0 && sh.qmax < 10);
         it++;
         if (tid == 0) {
@@ -309,6 +329,9 @@ __device__ int optimize(const PoseSlots &P, int s, const FrameHdr &h, bool robus
         __syncthreads();
         if (sh.stop) break;
     }
+#ifdef ORBP_PROFILE
+    if (tid == 0 && blockIdx.x == 0) printf("orbp prof: it=%d lin=%lld solve=%lld trial=%lld accept=%lld cycles\n", it, t_lin, t_solve, t_trial, t_acc);
+#endif
     return it;
 }
 

@@ -138,14 +138,59 @@ __device__ inline int hamming32(const uint8_t *a, const uint8_t *b) {
            __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
 }
 
+// insert into the sorted K-list; every index is a compile-time constant (unrolled compare-and-
+// swap), so the list stays in registers instead of scratch memory
 __device__ inline void cand_insert(Cand &c, uint32_t key, int idx, int oct, int bin) {
     if (key >= c.key[TOPK - 1]) return;
-    int p = TOPK - 1;
-    while (p > 0 && c.key[p - 1] > key) {
-        c.key[p] = c.key[p - 1]; c.idx[p] = c.idx[p - 1]; c.oct[p] = c.oct[p - 1]; c.bin[p] = c.bin[p - 1];
-        p--;
+    c.key[TOPK - 1] = key; c.idx[TOPK - 1] = (uint16_t)idx; c.oct[TOPK - 1] = (int8_t)oct; c.bin[TOPK - 1] = (int8_t)bin;
+#pragma unroll
+    for (int p = TOPK - 1; p > 0; p--) {
+        if (c.key[p] < c.key[p - 1]) {
+            const uint32_t k = c.key[p]; c.key[p] = c.key[p - 1]; c.key[p - 1] = k;
+            const uint16_t i = c.idx[p]; c.idx[p] = c.idx[p - 1]; c.idx[p - 1] = i;
+            const int8_t o = c.oct[p]; c.oct[p] = c.oct[p - 1]; c.oct[p - 1] = o;
+            const int8_t b = c.bin[p]; c.bin[p] = c.bin[p - 1]; c.bin[p - 1] = b;
+        }
     }
-    c.key[p] = key; c.idx[p] = (uint16_t)idx; c.oct[p] = (int8_t)oct; c.bin[p] = (int8_t)bin;
+}
+
+// the first `want` (1 or 2) unclaimed entries of a K-list, constant-index scan
+struct Pick {
+    int found, last_ex;          // entries found; index of the last entry examined
+    uint32_t key0, key1;
+    int idx0, idx1, oct0, oct1, bin0;
+};
+
+__device__ inline Pick pick_unclaimed(const Cand &c, const uint8_t *claimed, int want) {
+    Pick r;
+    r.found = 0; r.last_ex = -1;
+    r.key0 = r.key1 = 0xFFFFFFFFu;
+    r.idx0 = r.idx1 = 0; r.oct0 = r.oct1 = -1; r.bin0 = -1;
+    bool done = false;
+#pragma unroll
+    for (int k = 0; k < TOPK; k++) {
+        if (!done && c.key[k] != 0xFFFFFFFFu) {
+            r.last_ex = k;
+            if (!claimed[c.idx[k]]) {
+                if (r.found == 0) { r.key0 = c.key[k]; r.idx0 = c.idx[k]; r.oct0 = c.oct[k]; r.bin0 = c.bin[k]; }
+                else { r.key1 = c.key[k]; r.idx1 = c.idx[k]; r.oct1 = c.oct[k]; }
+                r.found++;
+                if (r.found == want) done = true;
+            }
+        } else {
+            done = true;
+        }
+    }
+    return r;
+}
+
+// any kept entry in [0, last_ex] claimed (tag < lane) by an earlier lane of the window
+__device__ inline bool examined_conflict(const Cand &c, int last_ex, const int *tag, int lane) {
+    bool conflict = false;
+#pragma unroll
+    for (int k = 0; k < TOPK; k++)
+        if (k <= last_ex) conflict |= tag[c.idx[k]] < lane;
+    return conflict;
 }
 
 // Frame::GetFeaturesInArea (Frame.cc:590-671) window: returns false if empty.
@@ -379,29 +424,21 @@ __global__ __launch_bounds__(64) void track_local_resolve_kernel(Slots S, float 
         int nc = -1;
         uint8_t fl = 0;
         if (live) { c = cand[mb0 + q]; nc = ncand[mb0 + q]; fl = S.mflags[mb0 + q]; }
-        int b = -1, b2 = -1, found = 0, last_ex = -1;
-        if (nc > 0) {
-            for (int k = 0; k < TOPK && found < 2; k++) {
-                if (c.key[k] == 0xFFFFFFFFu) break;
-                last_ex = k;
-                if (claimed[c.idx[k]]) continue;
-                if (found == 0) b = k; else b2 = k;
-                found++;
-            }
-        }
-        const bool fallback = nc > TOPK && found < 2;
+        Pick pk;
+        pk.found = 0; pk.last_ex = -1; pk.key0 = pk.key1 = 0xFFFFFFFFu; pk.idx0 = 0; pk.oct0 = pk.oct1 = -1;
+        if (nc > 0) pk = pick_unclaimed(c, claimed, 2);
+        const bool fallback = nc > TOPK && pk.found < 2;
         bool accept = false;
-        if (nc > 0 && !fallback && b >= 0) {
-            const int bestDist = (int)(c.key[b] >> 16), bestLevel = c.oct[b];
-            const int bestDist2 = b2 >= 0 ? (int)(c.key[b2] >> 16) : 256, bestLevel2 = b2 >= 0 ? c.oct[b2] : -1;
+        if (nc > 0 && !fallback && pk.found >= 1) {
+            const int bestDist = (int)(pk.key0 >> 16), bestLevel = pk.oct0;
+            const int bestDist2 = pk.found >= 2 ? (int)(pk.key1 >> 16) : 256, bestLevel2 = pk.found >= 2 ? pk.oct1 : -1;
             accept = bestDist <= TH_HIGH && !(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2);
         }
         const bool obs = (fl & ORBT_MP_HAS_OBS) != 0;
-        const int idx = b >= 0 ? c.idx[b] : 0;
+        const int idx = pk.idx0;
         if (accept && obs) atomicMin(&tag[idx], lane);
         __syncthreads();
-        bool conflict = false;
-        for (int k = 0; k <= last_ex; k++) conflict |= tag[c.idx[k]] < lane;
+        const bool conflict = nc > 0 && examined_conflict(c, pk.last_ex, tag, lane);
         const unsigned long long stop = __ballot(live && (conflict || fallback));
         const int cut = stop ? __ffsll((long long)stop) - 1 : 64;
         __syncthreads();
@@ -528,21 +565,16 @@ __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float 
         Cand c;
         int nc = -1, m = -1;
         if (live) { c = cand[kb + q]; nc = ncand[kb + q]; m = S.last_mp[kb + q]; }
-        int b = -1, last_ex = -1;
-        if (nc > 0)
-            for (int k = 0; k < TOPK; k++) {
-                if (c.key[k] == 0xFFFFFFFFu) break;
-                last_ex = k;
-                if (!claimed[c.idx[k]]) { b = k; break; }
-            }
-        const bool fallback = nc > TOPK && b < 0;
-        const bool accept = nc > 0 && !fallback && b >= 0 && (int)(c.key[b] >> 16) <= TH_HIGH;
+        Pick pk;
+        pk.found = 0; pk.last_ex = -1; pk.key0 = 0xFFFFFFFFu; pk.idx0 = 0; pk.bin0 = -1;
+        if (nc > 0) pk = pick_unclaimed(c, claimed, 1);
+        const bool fallback = nc > TOPK && pk.found < 1;
+        const bool accept = nc > 0 && !fallback && pk.found >= 1 && (int)(pk.key0 >> 16) <= TH_HIGH;
         const bool obs = m >= 0 && (S.mflags[mb0 + m] & ORBT_MP_HAS_OBS) != 0;
-        const int idx = b >= 0 ? c.idx[b] : 0;
+        const int idx = pk.idx0;
         if (accept && obs) atomicMin(&tag[idx], lane);
         __syncthreads();
-        bool conflict = false;
-        for (int k = 0; k <= last_ex; k++) conflict |= tag[c.idx[k]] < lane;
+        const bool conflict = nc > 0 && examined_conflict(c, pk.last_ex, tag, lane);
         const unsigned long long stop = __ballot(live && (conflict || fallback));
         const int cut = stop ? __ffsll((long long)stop) - 1 : 64;
         __syncthreads();
@@ -561,8 +593,8 @@ __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float 
         if (commit && check_ori) {   // rotHist push order = query order
             const int slot = nh + __popcll(cm & ((1ull << lane) - 1));
             HI[slot] = idx;
-            HB[slot] = c.bin[b];
-            atomicAdd(&counts[c.bin[b]], 1);
+            HB[slot] = (int8_t)pk.bin0;
+            atomicAdd(&counts[pk.bin0], 1);
         }
         nm += __popcll(cm);
         if (check_ori) nh += __popcll(cm);

@@ -38,16 +38,33 @@ __host__ __device__ inline void quat_from_R_norm(const double m[9], double q[4])
         c[1] = (m[2] - m[6]) * t;
         c[2] = (m[3] - m[1]) * t;
     } else {
+        // branches spelled out per pivot i (j = i+1, k = i+2 mod 3) so no array is indexed
+        // dynamically (a dynamically indexed local lands in scratch memory on the GPU)
         int i = 0;
         if (m[4] > m[0]) i = 1;
-        if (m[8] > m[4 * i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(m[4 * i] - m[4 * j] - m[4 * k] + 1.0);
-        c[i] = 0.5 * t;
-        t = 0.5 / t;
-        w = (m[3 * k + j] - m[3 * j + k]) * t;
-        c[j] = (m[3 * j + i] + m[3 * i + j]) * t;
-        c[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+        if (m[8] > (i == 0 ? m[0] : m[4])) i = 2;
+        if (i == 0) {        // j = 1, k = 2
+            t = sqrt(m[0] - m[4] - m[8] + 1.0);
+            c[0] = 0.5 * t;
+            t = 0.5 / t;
+            w = (m[7] - m[5]) * t;
+            c[1] = (m[3] + m[1]) * t;
+            c[2] = (m[6] + m[2]) * t;
+        } else if (i == 1) { // j = 2, k = 0
+            t = sqrt(m[4] - m[8] - m[0] + 1.0);
+            c[1] = 0.5 * t;
+            t = 0.5 / t;
+            w = (m[2] - m[6]) * t;
+            c[2] = (m[7] + m[5]) * t;
+            c[0] = (m[1] + m[3]) * t;
+        } else {             // j = 0, k = 1
+            t = sqrt(m[8] - m[0] - m[4] + 1.0);
+            c[2] = 0.5 * t;
+            t = 0.5 / t;
+            w = (m[3] - m[1]) * t;
+            c[0] = (m[2] + m[6]) * t;
+            c[1] = (m[5] + m[7]) * t;
+        }
     }
     if (w < 0) { c[0] = -c[0]; c[1] = -c[1]; c[2] = -c[2]; w = -w; }
     const double n = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2] + w * w);
