@@ -101,70 +101,109 @@ __device__ inline double huber(double chi, bool stereo, bool robust, double &w) 
     return 2 * s * delta - dsqr;
 }
 
-// sum-reduce v[0..kRed) over the workgroup into red[] (every thread reads the result)
+// sum-reduce v[0..N) over the workgroup into red[] (every thread reads the result)
+template <int N>
 __device__ inline void block_reduce(double *v, double *red, double (*wsum)[kRed]) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < kRed; k++) {
+    for (int k = 0; k < N; k++) {
         double x = v[k];
+#pragma unroll
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
         v[k] = x;
     }
     if (lane == 0)
-        for (int k = 0; k < kRed; k++) wsum[wv][k] = v[k];
+#pragma unroll
+        for (int k = 0; k < N; k++) wsum[wv][k] = v[k];
     __syncthreads();
-    if (threadIdx.x < kRed) red[threadIdx.x] = ((wsum[0][threadIdx.x] + wsum[1][threadIdx.x]) + wsum[2][threadIdx.x]) +
-                                               wsum[3][threadIdx.x];
+    if (threadIdx.x < N) red[threadIdx.x] = ((wsum[0][threadIdx.x] + wsum[1][threadIdx.x]) + wsum[2][threadIdx.x]) +
+                                            wsum[3][threadIdx.x];
     __syncthreads();
 }
 
-// Eigen::LDLT<MatrixXd> (lower, diagonal pivoting) + solve; false when !isPositive()
-// m (36), tr (6), y (6): workspace with data-dependent indexing -> LDS, not scratch
-__device__ bool ldlt_solve6(const double *Hin, const double *b, double *x, double *m, int *tr, double *y,
-                            double *temp) {
-    for (int i = 0; i < 36; i++) m[i] = Hin[i];
+// Eigen::LDLT<MatrixXd> (lower, diagonal pivoting) + solve; false when !isPositive().
+// Register-resident: the matrix is kept fully symmetric (every lower-triangle write is
+// mirrored), so Eigen's partial lower-triangle swap of pivot k <-> big equals a full symmetric
+// row + column swap, done with compile-time indices and selects on the runtime `big`. Same
+// operation sequence as the oracle's restatement (oracle/lba_oracle.c orc_ldlt_solve6).
+__device__ bool ldlt_solve6(const double *Hin, const double *b, double *x) {
+    double a[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j < 6; j++) a[i][j] = i >= j ? Hin[6 * i + j] : Hin[6 * j + i];
+    int tr[6];
     int sign = 0;
+    bool fail = false;
+#pragma unroll
     for (int k = 0; k < 6; k++) {
         int big = k;
-        double bv = fabs(m[7 * k]);
+        double bv = fabs(a[k][k]);
+#pragma unroll
         for (int i = k + 1; i < 6; i++)
-            if (fabs(m[7 * i]) > bv) { bv = fabs(m[7 * i]); big = i; }
+            if (fabs(a[i][i]) > bv) { bv = fabs(a[i][i]); big = i; }
         tr[k] = big;
-        if (big != k) {
-            for (int j = 0; j < k; j++) { const double t = m[6 * k + j]; m[6 * k + j] = m[6 * big + j]; m[6 * big + j] = t; }
-            for (int i = big + 1; i < 6; i++) { const double t = m[6 * i + k]; m[6 * i + k] = m[6 * i + big]; m[6 * i + big] = t; }
-            const double t = m[7 * k]; m[7 * k] = m[7 * big]; m[7 * big] = t;
-            for (int i = k + 1; i < big; i++) { const double t2 = m[6 * i + k]; m[6 * i + k] = m[6 * big + i]; m[6 * big + i] = t2; }
-        }
-        if (k > 0) {
-            for (int j = 0; j < k; j++) temp[j] = m[7 * j] * m[6 * k + j];
-            double s = 0;
-            for (int j = 0; j < k; j++) s += m[6 * k + j] * temp[j];
-            m[7 * k] -= s;
-            for (int i = k + 1; i < 6; i++) {
-                double t = 0;
-                for (int j = 0; j < k; j++) t += m[6 * i + j] * temp[j];
-                m[6 * i + k] -= t;
+#pragma unroll
+        for (int r = k + 1; r < 6; r++) {
+            if (r == big) {
+#pragma unroll
+                for (int j = 0; j < 6; j++) { const double t = a[k][j]; a[k][j] = a[r][j]; a[r][j] = t; }
+#pragma unroll
+                for (int i = 0; i < 6; i++) { const double t = a[i][k]; a[i][k] = a[i][r]; a[i][r] = t; }
             }
         }
-        const double akk = m[7 * k];
+        if (k > 0) {
+            double temp[6];
+#pragma unroll
+            for (int j = 0; j < k; j++) temp[j] = a[j][j] * a[k][j];
+            double s = 0;
+#pragma unroll
+            for (int j = 0; j < k; j++) s += a[k][j] * temp[j];
+            a[k][k] -= s;
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) {
+                double t = 0;
+#pragma unroll
+                for (int j = 0; j < k; j++) t += a[i][j] * temp[j];
+                a[i][k] -= t;
+                a[k][i] = a[i][k];
+            }
+        }
+        const double akk = a[k][k];
         const bool valid = fabs(akk) > 0;
-        if (k == 0 && !valid) return false;
+        if (k == 0 && !valid) fail = true;
         if (valid)
-            for (int i = k + 1; i < 6; i++) m[6 * i + k] /= akk;
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) { a[i][k] /= akk; a[k][i] = a[i][k]; }
         if (sign == 1) { if (akk < 0) sign = 3; }
         else if (sign == 2) { if (akk > 0) sign = 3; }
         else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
     }
-    if (!(sign == 1 || sign == 0)) return false;
+    if (fail || !(sign == 1 || sign == 0)) return false;
+    double y[6];
+#pragma unroll
     for (int i = 0; i < 6; i++) y[i] = b[i];
-    for (int k = 0; k < 6; k++) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+#pragma unroll
+        for (int r = k + 1; r < 6; r++)
+            if (r == tr[k]) { const double t = y[k]; y[k] = y[r]; y[r] = t; }
+#pragma unroll
     for (int i = 0; i < 6; i++)
-        for (int j = 0; j < i; j++) y[i] -= m[6 * i + j] * y[j];
-    for (int i = 0; i < 6; i++) y[i] = fabs(m[7 * i]) > DBL_MIN ? y[i] / m[7 * i] : 0.0;
+#pragma unroll
+        for (int j = 0; j < i; j++) y[i] -= a[i][j] * y[j];
+#pragma unroll
+    for (int i = 0; i < 6; i++) y[i] = fabs(a[i][i]) > DBL_MIN ? y[i] / a[i][i] : 0.0;
+#pragma unroll
     for (int i = 5; i >= 0; i--)
-        for (int j = i + 1; j < 6; j++) y[i] -= m[6 * j + i] * y[j];
-    for (int k = 5; k >= 0; k--) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+#pragma unroll
+        for (int j = i + 1; j < 6; j++) y[i] -= a[j][i] * y[j];
+#pragma unroll
+    for (int k = 5; k >= 0; k--)
+#pragma unroll
+        for (int r = k + 1; r < 6; r++)
+            if (r == tr[k]) { const double t = y[k]; y[k] = y[r]; y[r] = t; }
+#pragma unroll
     for (int i = 0; i < 6; i++) x[i] = y[i];
     return true;
 }
@@ -174,14 +213,14 @@ struct Shared {
     double red[kRed];
     double wsum[4][kRed];
     double H[36], b[6];
-    double Hl[36], work[36], y[6], temp[6], x[6];
-    int tr[6];
+    double Hl[36], x[6];
     double lambda, ni, currentChi, iniChi, rho;
     int qmax, nBad, stop, cnt;
 };
 
 // errors of the active edges at `T` (+ the robust chi2 partial; + H/b partials if `lin`)
-__device__ void accumulate(const PoseSlots &P, int s, const FrameHdr &h, const Pose &T, bool robust, bool lin,
+template <bool lin>
+__device__ void accumulate(const PoseSlots &P, int s, const FrameHdr &h, const Pose &T, bool robust,
                            Shared &sh) {
     double v[kRed];
 #pragma unroll
@@ -198,7 +237,7 @@ __device__ void accumulate(const PoseSlots &P, int s, const FrameHdr &h, const P
         const double info = ob.w;
         double w;
         v[0] += huber(edge_chi2(e, info, stereo), stereo, robust, w);
-        if (lin) {
+        if constexpr (lin) {
             // linearizeOplus (types_six_dof_expmap.cpp:283-301, 337-362)
             const double X[3] = {xw.x, xw.y, xw.z};
             double p[3];
@@ -233,7 +272,8 @@ __device__ void accumulate(const PoseSlots &P, int s, const FrameHdr &h, const P
             }
         }
     }
-    block_reduce(v, sh.red, sh.wsum);
+    if constexpr (lin) block_reduce<kRed>(v, sh.red, sh.wsum);
+    else block_reduce<1>(v, sh.red, sh.wsum);
 }
 
 // SparseOptimizer::optimize(iterations) + OptimizationAlgorithmLevenberg::solve on the pose
@@ -258,7 +298,7 @@ __device__ int optimize(const PoseSlots &P, int s, const FrameHdr &h, bool robus
 #endif
     for (int i = 0; i < iterations; i++) {
         PT0();
-        accumulate(P, s, h, sh.T, robust, true, sh);
+        accumulate<true>(P, s, h, sh.T, robust, sh);
         PT1(t_lin);
         if (tid == 0) {
             sh.currentChi = sh.iniChi = sh.red[0];
@@ -282,13 +322,13 @@ __device__ int optimize(const PoseSlots &P, int s, const FrameHdr &h, bool robus
             if (tid == 0) {
                 for (int k = 0; k < 36; k++) sh.Hl[k] = sh.H[k];
                 for (int a = 0; a < 6; a++) sh.Hl[7 * a] += sh.lambda;
-                ok2 = ldlt_solve6(sh.Hl, sh.b, sh.x, sh.work, sh.tr, sh.y, sh.temp);
+                ok2 = ldlt_solve6(sh.Hl, sh.b, sh.x);
                 sh.T2 = pose_oplus(sh.T, sh.x);           // VertexSE3Expmap::oplusImpl
             }
             __syncthreads();
             PT1(t_solve);
             PT0();
-            accumulate(P, s, h, sh.T2, robust, false, sh);
+            accumulate<false>(P, s, h, sh.T2, robust, sh);
             PT1(t_trial);
             PT0();
             if (tid == 0) {
