@@ -226,6 +226,56 @@ def bench_pose(amd, args, dist, world, with_cpu):
     return res
 
 
+def bench_bow(amd, args, dist, world, with_cpu):
+    """§8f rank 3: Frame::ComputeBoW = DBoW2 transform(levelsup 4) of B frames x 2000
+    descriptors resident in HBM against a k=10, L=6 vocabulary (1.11 M nodes, ORBvoc.txt
+    shape; synthetic, synth.vocabulary)."""
+    import torch
+    from orbslam2_amd import synth
+    from orbslam2_amd import dist as odist
+    B, N = args.bow_batch, 2000
+    voc = synth.vocabulary(11, 10, 6)
+    feats = [synth.bow_features(voc, 700 + i, N) for i in range(8)]
+    V = amd.Vocabulary(voc)
+    buf = np.stack([feats[i % 8] for i in range(B)])
+    d = torch.from_numpy(buf).cuda()
+    c = torch.full((B,), N, dtype=torch.int32).cuda()
+    torch.cuda.synchronize()
+
+    def step():
+        V.transform_batch_device(d.data_ptr(), c.data_ptr(), B, N, N * 32, 4)
+
+    for _ in range(2):
+        step()
+    amd.device_sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.bow_steps):
+        step()
+    amd.device_sync()
+    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    r = V.batch_fetch(0, N)
+    res = {"bow_frames_per_s": round(world * B * args.bow_steps / dt, 2),
+           "bow": {"frames_per_step": B, "ms_per_step": round(1000 * dt / args.bow_steps, 3), "features": N,
+                   "vocabulary": "k=10 L=6 (1111111 nodes)", "words_frame0": int(len(r["words"])),
+                   "fv_nodes_frame0": int(len(r["fv_nodes"]))}}
+    V.close()
+    if with_cpu:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+        O = oracle.Vocabulary(voc)
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 3.0:
+            O.transform(feats[n % 8], 4)
+            n += 1
+        cdt = time.perf_counter() - t0
+        res["bow"]["cpu_baseline"] = {"value": round(n / cdt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+                                      "sample": f"{n} frames x {N} descriptors, oracle, single thread, {cdt:.1f} s"}
+    return res
+
+
 def load_traffic(kernel: str, batch: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
     f = ROOT / "profiles" / "pmc_traffic.json"
@@ -263,6 +313,9 @@ def main():
     ap.add_argument("--pose-batch", type=int, default=256)
     ap.add_argument("--pose-steps", type=int, default=10)
     ap.add_argument("--no-pose", action="store_true")
+    ap.add_argument("--bow-batch", type=int, default=256)
+    ap.add_argument("--bow-steps", type=int, default=10)
+    ap.add_argument("--no-bow", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -377,6 +430,8 @@ def main():
         out.update(bench_track(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if not args.no_pose:
         out.update(bench_pose(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
+    if not args.no_bow:
+        out.update(bench_bow(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if not args.no_lba:
         out.update(bench_localba(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

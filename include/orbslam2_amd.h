@@ -220,6 +220,40 @@ int orbt_run_local_batch(orbt_engine *e, int n_slots, float view_cos_limit, floa
 int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int check_ori, void *stream);
 int orbt_fetch(orbt_engine *e, int slot, orbt_view *view, int32_t *owner, int32_t *nmatches);
 
+/* -------- bag of words (replaces Frame::ComputeBoW -> DBoW2 TemplatedVocabulary::transform) -------- */
+
+/* A DBoW2 TemplatedVocabulary<FORB::TDescriptor, FORB> (Thirdparty/DBoW2/DBoW2/
+ * TemplatedVocabulary.h) in the order loadFromTextFile (:1385-1460) builds it: node 0 is the
+ * root, node i >= 1 is the i-th node line of the text file (parent id, isLeaf, 32 descriptor
+ * bytes, weight); children keep file order; word ids are given to leaves in file order.
+ * scoring = ScoringType (L1_NORM = 0 .. DOT_PRODUCT = 5), weighting = WeightingType
+ * (TF_IDF = 0, TF, IDF, BINARY). ORBvoc.txt is k = 10, L = 6, L1_NORM, TF_IDF. */
+typedef struct orbv_vocab orbv_vocab;
+
+int orbv_create(int k, int L, int scoring, int weighting, int n_nodes, const int32_t *parent,
+                const uint8_t *is_leaf, const uint8_t *desc, const double *weight, orbv_vocab **out);
+/* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1385-1460). */
+int orbv_load_text(const char *path, orbv_vocab **out);
+void orbv_destroy(orbv_vocab *v);
+/* nodes / words / k / L of a loaded vocabulary (any pointer may be NULL) */
+int orbv_info(const orbv_vocab *v, int *n_nodes, int *n_words, int *k, int *L);
+
+/* TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup)
+ * (TemplatedVocabulary.h:1125-1209, per-feature descent :1226-1286; Frame::ComputeBoW calls it
+ * with levelsup = 4, Frame.cc:704-719) on n descriptors (N x 32, host). Outputs:
+ *   BowVector     words[n_words] ascending with values[n_words] (after the scoring's norm);
+ *   FeatureVector fv_nodes[n_fv] ascending, the features of fv_nodes[j] are
+ *                 fv_features[fv_start[j] .. fv_start[j+1]) in increasing index order.
+ * Capacities: words / values / fv_nodes n entries, fv_start n + 1, fv_features n. */
+int orbv_transform(orbv_vocab *v, const uint8_t *desc, int n, int levelsup, uint32_t *words, double *values,
+                   int32_t *n_words, uint32_t *fv_nodes, int32_t *fv_start, int32_t *fv_features, int32_t *n_fv);
+/* Batched device-resident form: descriptors of frame f at d_desc + f * frame_stride (N x 32
+ * bytes, counts in d_counts[f] <= cap); results stay on the device, fetched per frame. */
+int orbv_transform_batch_device(orbv_vocab *v, const uint8_t *d_desc, const int32_t *d_counts, int n_frames,
+                                int cap, size_t frame_stride, int levelsup, void *stream);
+int orbv_batch_fetch(orbv_vocab *v, int frame, uint32_t *words, double *values, int32_t *n_words,
+                     uint32_t *fv_nodes, int32_t *fv_start, int32_t *fv_features, int32_t *n_fv);
+
 /* -------- pose-only optimisation (replaces Optimizer::PoseOptimization) -------- */
 
 /* The edges Optimizer::PoseOptimization (Optimizer.h:105, Optimizer.cc:375-622) builds from a

@@ -459,3 +459,57 @@ def pose_optimization(prob: dict):
     L.pose_oracle_optimize(C.byref(F), C.byref(R))
     return {"Tcw": np.array(R.Tcw[:], np.float32).reshape(4, 4), "outlier": out[: F.n].copy(),
             "n_inliers": R.n_inliers, "iterations": tuple(R.iterations)}
+
+
+# ---- DBoW2 vocabulary transform (bow_oracle.c)
+class OrcVocab(C.Structure):
+    _fields_ = [("k", C.c_int), ("L", C.c_int), ("scoring", C.c_int), ("weighting", C.c_int), ("n_nodes", C.c_int),
+                ("n_words", C.c_int), ("child_start", C.c_void_p), ("children", C.c_void_p), ("desc", C.c_void_p),
+                ("weight", C.c_void_p), ("word_id", C.c_void_p)]
+
+
+class Vocabulary:
+    """Oracle TemplatedVocabulary (from synth.vocabulary arrays or a text file)."""
+
+    def __init__(self, voc: dict | None = None, path: str | None = None):
+        L = lib()
+        L.orc_vocab_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p]
+        L.orc_vocab_load_text.argtypes = [C.c_void_p, C.c_char_p]
+        L.orc_vocab_free.argtypes = [C.c_void_p]
+        L.orc_bow_transform.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        self.v = OrcVocab()
+        if path is not None:
+            rc = L.orc_vocab_load_text(C.byref(self.v), str(path).encode())
+        else:
+            par = np.ascontiguousarray(voc["parent"], np.int32)
+            leaf = np.ascontiguousarray(voc["is_leaf"], np.uint8)
+            desc = np.ascontiguousarray(voc["desc"], np.uint8)
+            w = np.ascontiguousarray(voc["weight"], np.float64)
+            rc = L.orc_vocab_build(C.byref(self.v), voc["k"], voc["L"], voc["scoring"], voc["weighting"], len(par),
+                                   par.ctypes.data, leaf.ctypes.data, desc.ctypes.data, w.ctypes.data)
+        if rc != 0:
+            raise ValueError("bad vocabulary")
+
+    def __del__(self):
+        try:
+            lib().orc_vocab_free(C.byref(self.v))
+        except Exception:
+            pass
+
+    def transform(self, desc: np.ndarray, levelsup: int = 4):
+        desc = np.ascontiguousarray(desc, np.uint8)
+        n = len(desc)
+        m = max(n, 1)
+        words = np.zeros(m, np.uint32)
+        vals = np.zeros(m, np.float64)
+        fvn = np.zeros(m, np.uint32)
+        fvs = np.zeros(m + 1, np.int32)
+        fvf = np.zeros(m, np.int32)
+        nw, nf = C.c_int(), C.c_int()
+        lib().orc_bow_transform(C.byref(self.v), desc.ctypes.data, n, levelsup, words.ctypes.data, vals.ctypes.data,
+                                C.byref(nw), fvn.ctypes.data, fvs.ctypes.data, fvf.ctypes.data, C.byref(nf))
+        return {"words": words[: nw.value].copy(), "values": vals[: nw.value].copy(),
+                "fv_nodes": fvn[: nf.value].copy(), "fv_start": fvs[: nf.value + 1].copy(),
+                "fv_features": fvf[: fvs[nf.value]].copy()}

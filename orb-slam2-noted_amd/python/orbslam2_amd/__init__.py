@@ -92,6 +92,13 @@ SIGNATURES = [
     ("orbp_stage", _I, [_P, _I, _P]),
     ("orbp_run_batch", _I, [_P, _I, _P]),
     ("orbp_fetch", _I, [_P, _I, _P]),
+    ("orbv_create", _I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, C.POINTER(C.c_void_p)]),
+    ("orbv_load_text", _I, [C.c_char_p, C.POINTER(C.c_void_p)]),
+    ("orbv_destroy", None, [_P]),
+    ("orbv_info", _I, [_P, _P, _P, _P, _P]),
+    ("orbv_transform", _I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    ("orbv_transform_batch_device", _I, [_P, _P, _P, _I, _I, C.c_size_t, _I, _P]),
+    ("orbv_batch_fetch", _I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
 ]
 
 
@@ -631,3 +638,73 @@ class PoseOptimizer:
         R, out = self._result(n)
         _check(lib().orbp_fetch(self._h, slot, C.byref(R)), "orbp_fetch")
         return self._pack(R, out, n)
+
+
+# ---- DBoW2 vocabulary transform (orbv_*): Frame::ComputeBoW ---------------------------------
+class Vocabulary:
+    """ORBVocabulary (DBoW2 TemplatedVocabulary<FORB>) resident in HBM. Built from the arrays
+    of synth.vocabulary or loaded from a DBoW2 text file (loadFromTextFile format).
+    ``transform(desc, levelsup=4)`` = Frame::ComputeBoW -> (BowVector, FeatureVector)."""
+
+    def __init__(self, voc: dict | None = None, path: str | None = None):
+        h = C.c_void_p()
+        if path is not None:
+            _check(lib().orbv_load_text(str(path).encode(), C.byref(h)), "orbv_load_text")
+        else:
+            par = np.ascontiguousarray(voc["parent"], np.int32)
+            leaf = np.ascontiguousarray(voc["is_leaf"], np.uint8)
+            desc = np.ascontiguousarray(voc["desc"], np.uint8)
+            w = np.ascontiguousarray(voc["weight"], np.float64)
+            _check(lib().orbv_create(voc["k"], voc["L"], voc["scoring"], voc["weighting"], len(par), par.ctypes.data,
+                                     leaf.ctypes.data, desc.ctypes.data, w.ctypes.data, C.byref(h)), "orbv_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        vals = [C.c_int() for _ in range(4)]
+        _check(lib().orbv_info(self._h, *[C.byref(v) for v in vals]), "orbv_info")
+        return dict(zip(("n_nodes", "n_words", "k", "L"), (v.value for v in vals)))
+
+    @staticmethod
+    def _bufs(n):
+        m = max(n, 1)
+        return (np.zeros(m, np.uint32), np.zeros(m, np.float64), np.zeros(m, np.uint32), np.zeros(m + 1, np.int32),
+                np.zeros(m, np.int32))
+
+    @staticmethod
+    def _pack(b, nw, nf):
+        words, vals, fvn, fvs, fvf = b
+        return {"words": words[:nw].copy(), "values": vals[:nw].copy(), "fv_nodes": fvn[:nf].copy(),
+                "fv_start": fvs[: nf + 1].copy(), "fv_features": fvf[: fvs[nf]].copy()}
+
+    def transform(self, desc: np.ndarray, levelsup: int = 4) -> dict:
+        desc = np.ascontiguousarray(desc, np.uint8)
+        n = len(desc)
+        b = self._bufs(n)
+        nw, nf = C.c_int32(), C.c_int32()
+        _check(lib().orbv_transform(self._h, desc.ctypes.data if n else None, n, levelsup, *(x.ctypes.data for x in b[:2]),
+                                    C.byref(nw), *(x.ctypes.data for x in b[2:]), C.byref(nf)), "orbv_transform")
+        return self._pack(b, nw.value, nf.value)
+
+    def transform_batch_device(self, d_desc: int, d_counts: int, n_frames: int, cap: int, frame_stride: int,
+                               levelsup: int = 4, stream=None):
+        _check(lib().orbv_transform_batch_device(self._h, C.c_void_p(d_desc), C.c_void_p(d_counts), n_frames, cap,
+                                                 frame_stride, levelsup, stream), "orbv_transform_batch_device")
+
+    def batch_fetch(self, frame: int, cap: int) -> dict:
+        b = self._bufs(cap)
+        nw, nf = C.c_int32(), C.c_int32()
+        _check(lib().orbv_batch_fetch(self._h, frame, b[0].ctypes.data, b[1].ctypes.data, C.byref(nw),
+                                      b[2].ctypes.data, b[3].ctypes.data, b[4].ctypes.data, C.byref(nf)),
+               "orbv_batch_fetch")
+        return self._pack(b, nw.value, nf.value)

@@ -424,3 +424,57 @@ def pose_problem(seed: int = 7, n: int = 600, stereo_frac: float = 0.6, outlier_
             "Tcw": T, "cam": (np.float32(fx), np.float32(fy), np.float32(cx), np.float32(cy), np.float32(bf)),
             "true_Tcw": np.concatenate([np.concatenate([Rt, tt[:, None]], 1), [[0, 0, 0, 1]]]).astype(np.float32),
             "is_outlier": bad}
+
+
+# ---------------------------------------------------------------------------------------
+# DBoW2 vocabulary. ORBvoc.txt is not in the reference tree
+# (.MISSING_LARGE_BLOBS), so a synthetic vocabulary of the same shape is generated: a full
+# k-ary tree of depth L in breadth-first node order (DBoW2's saveToTextFile order), each child
+# descriptor = its parent's with each bit flipped with probability p_level (coarse-to-fine
+# clusters), leaf weights = IDF-like values in [0.5, 8] with `stop_frac` stopped (weight 0)
+# words, internal weights 0; scoring L1_NORM, weighting TF_IDF (ORBvoc.txt header 10 6 0 0).
+# ---------------------------------------------------------------------------------------
+def vocabulary(seed: int = 11, k: int = 10, L: int = 6, stop_frac: float = 0.02):
+    rng = np.random.default_rng(seed)
+    sizes = [k ** l for l in range(L + 1)]
+    n = sum(sizes)
+    parent = np.full(n, -1, np.int32)
+    desc = np.zeros((n, 32), np.uint8)
+    leaf = np.zeros(n, np.uint8)
+    weight = np.zeros(n, np.float64)
+    desc[0] = rng.integers(0, 256, 32, dtype=np.uint8)
+    start_prev, start = 0, 1
+    for l in range(1, L + 1):
+        m = sizes[l]
+        parent[start:start + m] = np.repeat(np.arange(start_prev, start_prev + sizes[l - 1], dtype=np.int32), k)
+        p = 0.35 / (1.0 + 0.6 * (l - 1))
+        flips = np.packbits(rng.random((m, 256)) < p, axis=1, bitorder="little")
+        desc[start:start + m] = desc[parent[start:start + m]] ^ flips
+        start_prev, start = start, start + m
+    leaf[n - sizes[L]:] = 1
+    w = rng.uniform(0.5, 8.0, sizes[L])
+    w[rng.random(sizes[L]) < stop_frac] = 0.0
+    weight[n - sizes[L]:] = w
+    return {"k": k, "L": L, "scoring": 0, "weighting": 0, "parent": parent, "is_leaf": leaf, "desc": desc,
+            "weight": weight}
+
+
+def vocabulary_text(voc: dict) -> str:
+    """TemplatedVocabulary::saveToTextFile layout (TemplatedVocabulary.h:1479-1530)."""
+    lines = [f"{voc['k']} {voc['L']} {voc['scoring']} {voc['weighting']}"]
+    for i in range(1, len(voc["parent"])):
+        d = " ".join(str(int(b)) for b in voc["desc"][i])
+        lines.append(f"{int(voc['parent'][i])} {int(voc['is_leaf'][i])} {d} {float(voc['weight'][i])!r}")
+    return "\n".join(lines) + "\n"
+
+
+def bow_features(voc: dict, seed: int, n: int = 2000, noise_bits: int = 24, random_frac: float = 0.2):
+    """Descriptors near random leaves (each bit flipped w.p. noise_bits/256) plus random ones."""
+    rng = np.random.default_rng(seed)
+    leaves = np.nonzero(voc["is_leaf"])[0]
+    pick = rng.choice(leaves, size=n)
+    flips = np.packbits(rng.random((n, 256)) < noise_bits / 256.0, axis=1, bitorder="little")
+    d = voc["desc"][pick] ^ flips
+    r = rng.random(n) < random_frac
+    d[r] = rng.integers(0, 256, (int(r.sum()), 32), dtype=np.uint8)
+    return np.ascontiguousarray(d)
