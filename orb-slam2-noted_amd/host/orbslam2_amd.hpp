@@ -7,11 +7,17 @@
 //   orbslam2_amd::ORBmatcher     <- ORB_SLAM2::ORBmatcher   (include/ORBmatcher.h:57-65)
 //   orbslam2_amd::ComputeStereoMatches <- Frame::ComputeStereoMatches (Frame.cc:831-1128)
 //   orbslam2_amd::Optimizer::LocalBundleAdjustment <- Optimizer.h:112 (graph supplied flat)
+//   orbslam2_amd::Optimizer::PoseOptimization     <- Optimizer.h:105 (edges supplied flat)
+//   orbslam2_amd::ORBmatcher::SearchByProjection   <- ORBmatcher.h:82 (+ Frame::isInFrustum),
+//                                                     ORBmatcher.h:102 (motion model)
+//   orbslam2_amd::ORBVocabulary                    <- DBoW2 TemplatedVocabulary<FORB>:
+//                                                     loadFromTextFile + transform (ComputeBoW)
 //
 // Error behaviour: the reference has no error path (it asserts / returns silently); a GPU
 // failure here throws std::runtime_error -- there is no CPU fallback.
 #pragma once
 #include <cstdint>
+#include <map>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -114,8 +120,84 @@ public:
         check(orbm_hamming_best2(q.data(), nq, db.data(), ndb, best.data(), bestDist.data(), secondDist.data()),
               "orbm_hamming_best2");
     }
+    // SearchByProjection(Frame&, const vector<MapPoint*>&, th) with the in-view selection of
+    // Tracking::SearchLocalPoints (isInFrustum(pMP, 0.5)); owner[i] = index into M assigned to
+    // keypoint i, -1 untouched. inView (optional) = mbTrackInView per map point.
+    int SearchByProjection(const orbt_frame &F, const orbt_mappoints &M, float th, const uint8_t *blocked,
+                           std::vector<int32_t> &owner, std::vector<uint8_t> *inView = nullptr) {
+        owner.assign(F.n, -1);
+        std::vector<uint8_t> iv(M.n);
+        orbt_view v{iv.data(), nullptr, nullptr, nullptr, nullptr, nullptr};
+        int32_t nm = 0;
+        check(orbt_search_local_points(track(), &F, &M, 0.5f, th, mfNNratio, blocked, &v, owner.data(), &nm),
+              "orbt_search_local_points");
+        if (inView) *inView = iv;
+        return nm;
+    }
+    // SearchByProjection(CurrentFrame, LastFrame, th, bMono); owner[i] == -2: set to NULL by
+    // the rotation-consistency check.
+    int SearchByProjection(const orbt_frame &cur, const orbt_frame &last, const int32_t *lastMp,
+                           const uint8_t *lastOutlier, const orbt_mappoints &M, float th, bool bMono,
+                           std::vector<int32_t> &owner) {
+        owner.assign(cur.n, -1);
+        int32_t nm = 0;
+        check(orbt_search_by_projection_frame(track(), &cur, &last, lastMp, lastOutlier, &M, th, bMono ? 1 : 0,
+                                              mbCheckOrientation ? 1 : 0, nullptr, owner.data(), &nm),
+              "orbt_search_by_projection_frame");
+        return nm;
+    }
     float mfNNratio;
     bool mbCheckOrientation;
+
+private:
+    static orbt_engine *track() {
+        struct H {
+            orbt_engine *h = nullptr;
+            H() { check(orbt_create(&h), "orbt_create"); }
+            ~H() { orbt_destroy(h); }
+        };
+        static thread_local H h;
+        return h.h;
+    }
+};
+
+// DBoW2 TemplatedVocabulary<FORB::TDescriptor, FORB> (ORBVocabulary.h) resident in HBM.
+using BowVector = std::map<uint32_t, double>;                        // DBoW2::BowVector
+using FeatureVector = std::map<uint32_t, std::vector<unsigned int>>; // DBoW2::FeatureVector
+
+class ORBVocabulary {
+public:
+    ORBVocabulary() = default;
+    ~ORBVocabulary() { orbv_destroy(h_); }
+    ORBVocabulary(const ORBVocabulary &) = delete;
+    ORBVocabulary &operator=(const ORBVocabulary &) = delete;
+    bool loadFromTextFile(const std::string &filename) {
+        orbv_destroy(h_);
+        h_ = nullptr;
+        return orbv_load_text(filename.c_str(), &h_) == ORBX_OK;
+    }
+    // transform(features, BowVector&, FeatureVector&, levelsup): Frame::ComputeBoW uses 4
+    void transform(const uint8_t *desc, int n, BowVector &v, FeatureVector &fv, int levelsup) const {
+        v.clear();
+        fv.clear();
+        std::vector<uint32_t> words(n + 1), nodes(n + 1);
+        std::vector<double> vals(n + 1);
+        std::vector<int32_t> start(n + 2), feats(n + 1);
+        int32_t nw = 0, nf = 0;
+        check(orbv_transform(h_, desc, n, levelsup, words.data(), vals.data(), &nw, nodes.data(), start.data(),
+                             feats.data(), &nf), "orbv_transform");
+        for (int j = 0; j < nw; j++) v.emplace_hint(v.end(), words[j], vals[j]);
+        for (int j = 0; j < nf; j++)
+            fv.emplace_hint(fv.end(), nodes[j], std::vector<unsigned int>(feats.begin() + start[j], feats.begin() + start[j + 1]));
+    }
+    size_t size() const {
+        int nw = 0;
+        if (h_) orbv_info(h_, nullptr, &nw, nullptr, nullptr);
+        return (size_t)nw;
+    }
+
+private:
+    orbv_vocab *h_ = nullptr;
 };
 
 // Optimizer::LocalBundleAdjustment minus the map walk: the caller flattens the local
@@ -137,6 +219,24 @@ public:
         static_assert(sizeof(bool) == 1, "pbStopFlag is passed to the C-ABI as one byte");
         check(lba_solve(lba.h, &graph, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag)), "lba_solve");
         return r;
+    }
+
+    // PoseOptimization(Frame*): edges = the frame's keypoints with a map point, in keypoint
+    // order (Optimizer.cc:412-531). Returns nInitialCorrespondences - nBad; Tcw = SetPose
+    // value, outlier[k] = mvbOutlier of edge k.
+    static int PoseOptimization(const orbp_frame &f, float Tcw[16], std::vector<uint8_t> &outlier) {
+        struct H {
+            orbp_engine *h = nullptr;
+            H() { check(orbp_create(&h), "orbp_create"); }
+            ~H() { orbp_destroy(h); }
+        };
+        static thread_local H eng;
+        outlier.assign(f.n, 0);
+        orbp_result r{};
+        r.outlier = outlier.data();
+        check(orbp_pose_optimization(eng.h, &f, &r), "orbp_pose_optimization");
+        for (int i = 0; i < 16; i++) Tcw[i] = r.Tcw[i];
+        return r.n_inliers;
     }
 
 private:

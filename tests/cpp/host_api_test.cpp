@@ -4,6 +4,8 @@
 //   host_api_test extract <img.u8> <w> <h> <nfeat> <out.bin>
 //   host_api_test stereo <left.u8> <right.u8> <w> <h> <nfeat> <mbf> <mb> <out.bin>
 //   host_api_test lba <problem.bin> <out.bin>
+//   host_api_test pose <edges.bin> <out.bin>
+//   host_api_test bow <vocab.txt> <desc.u8> <n> <levelsup> <out.bin>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -85,10 +87,55 @@ int main(int argc, char **argv) {
             put(o, erase);
             return 0;
         }
+        if (argc >= 4 && !strcmp(argv[1], "pose")) {
+            auto b = read_file(argv[2]);   // int32 n | float Tcw[16] | float cam[5] | Xw[n][3] | obs[n][3] | isg[n]
+            const int n = *(const int32_t *)b.data();
+            const float *p = (const float *)(b.data() + 4);
+            orbp_frame f{};
+            f.n = n;
+            for (int i = 0; i < 16; i++) f.Tcw[i] = p[i];
+            f.fx = p[16]; f.fy = p[17]; f.cx = p[18]; f.cy = p[19]; f.bf = p[20];
+            f.Xw = p + 21;
+            f.obs = p + 21 + 3 * n;
+            f.inv_sigma2 = p + 21 + 6 * n;
+            std::vector<float> T(16);
+            std::vector<uint8_t> out;
+            const int nin = Optimizer::PoseOptimization(f, T.data(), out);
+            std::ofstream o(argv[3], std::ios::binary);
+            put(o, T);
+            put(o, out);
+            put(o, std::vector<int32_t>{nin});
+            return 0;
+        }
+        if (argc >= 7 && !strcmp(argv[1], "bow")) {
+            ORBVocabulary voc;
+            if (!voc.loadFromTextFile(argv[2])) throw std::runtime_error("loadFromTextFile");
+            auto d = read_file(argv[3]);
+            const int n = atoi(argv[4]), levelsup = atoi(argv[5]);
+            BowVector v;
+            FeatureVector fv;
+            voc.transform(d.data(), n, v, fv, levelsup);
+            std::vector<uint32_t> words, nodes;
+            std::vector<double> vals;
+            std::vector<int32_t> start{0}, feats;
+            for (auto &kv : v) { words.push_back(kv.first); vals.push_back(kv.second); }
+            for (auto &kv : fv) {
+                nodes.push_back(kv.first);
+                for (unsigned i : kv.second) feats.push_back((int32_t)i);
+                start.push_back((int32_t)feats.size());
+            }
+            std::ofstream o(argv[6], std::ios::binary);
+            put(o, words);
+            put(o, vals);
+            put(o, nodes);
+            put(o, start);
+            put(o, feats);
+            return 0;
+        }
     } catch (const std::exception &e) {
         std::cerr << e.what() << "\n";
         return 2;
     }
-    std::cerr << "usage: host_api_test extract|stereo|lba ...\n";
+    std::cerr << "usage: host_api_test extract|stereo|lba|pose|bow ...\n";
     return 1;
 }

@@ -79,3 +79,30 @@ def test_cpp_localba(tmp_path, oracle_mod):
     assert rel(T.reshape(-1, 16).astype(np.float64), ref["pose_Tcw"]) < 1e-4
     assert rel(X.reshape(-1, 3).astype(np.float64), ref["point_Xw"]) < 1e-4
     assert np.array_equal(er, ref["edge_erase"])
+
+
+def test_cpp_pose_optimization(tmp_path, oracle_mod):
+    p = synth.pose_problem(21, n=500)
+    n = len(p["Xw"])
+    blob = (np.array([n], np.int32).tobytes() + np.asarray(p["Tcw"], np.float32).tobytes() +
+            np.array(p["cam"], np.float32).tobytes() + p["Xw"].astype(np.float32).tobytes() +
+            p["obs"].astype(np.float32).tobytes() + p["inv_sigma2"].astype(np.float32).tobytes())
+    (tmp_path / "e.bin").write_bytes(blob)
+    _run("pose", tmp_path / "e.bin", tmp_path / "o.bin")
+    T, out, nin = _read(tmp_path / "o.bin", [np.float32, np.uint8, np.int32])
+    ref = oracle_mod.pose_optimization(p)
+    assert int(nin[0]) == ref["n_inliers"] and np.array_equal(out, ref["outlier"])
+    assert np.abs(T.reshape(4, 4).astype(np.float64) - ref["Tcw"]).max() < 1e-4
+
+
+def test_cpp_bow_text_vocabulary(tmp_path, oracle_mod):
+    voc = synth.vocabulary(31, 8, 4)
+    (tmp_path / "voc.txt").write_text(synth.vocabulary_text(voc))
+    d = synth.bow_features(voc, 5, 1200)
+    (tmp_path / "d.u8").write_bytes(d.tobytes())
+    _run("bow", tmp_path / "voc.txt", tmp_path / "d.u8", len(d), 4, tmp_path / "o.bin")
+    words, vals, nodes, start, feats = _read(tmp_path / "o.bin", [np.uint32, np.float64, np.uint32, np.int32, np.int32])
+    ref = oracle_mod.Vocabulary(voc).transform(d, 4)
+    assert words.tobytes() == ref["words"].tobytes() and vals.tobytes() == ref["values"].tobytes()
+    assert nodes.tobytes() == ref["fv_nodes"].tobytes() and start.tobytes() == ref["fv_start"].tobytes()
+    assert feats.tobytes() == ref["fv_features"].tobytes()
