@@ -276,6 +276,54 @@ def bench_bow(amd, args, dist, world, with_cpu):
     return res
 
 
+def bench_bowmatch(amd, args, dist, world, with_cpu):
+    """§8f rank 4: ORBmatcher::SearchByBoW(KF, F) (TrackReferenceKeyFrame, nnratio 0.7) +
+    SearchForTriangulation(KF1, KF2) (CreateNewMapPoints) on B keyframe pairs resident in HBM,
+    2000 keypoints each (synth.bow_match_problem)."""
+    from orbslam2_amd import synth
+    from orbslam2_amd import dist as odist
+    B = args.bowmatch_batch
+    probs = [synth.bow_match_problem(900 + i, n=2000) for i in range(8)]
+    m = amd.BowMatcher()
+    m.reserve(B, 2000)
+    for s in range(B):
+        m.stage(s, probs[s % len(probs)])
+
+    def step():
+        m.run_bow_batch(B, 0.7, True)
+        m.run_tri_batch(B, False, True)
+
+    for _ in range(2):
+        step()
+    amd.device_sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.bowmatch_steps):
+        step()
+    amd.device_sync()
+    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    pairs0 = m.fetch(0, True, 2000)
+    res = {"bowmatch_pairs_per_s": round(world * B * args.bowmatch_steps / dt, 2),
+           "bowmatch": {"pairs_per_step": B, "ms_per_step": round(1000 * dt / args.bowmatch_steps, 3),
+                        "keypoints": 2000, "triangulation_pairs_slot0": int(len(pairs0))}}
+    m.close()
+    if with_cpu:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 3.0:
+            p = probs[n % len(probs)]
+            oracle.search_by_bow(p, 0.7, True)
+            oracle.search_for_triangulation(p)
+            n += 1
+        cdt = time.perf_counter() - t0
+        res["bowmatch"]["cpu_baseline"] = {"value": round(n / cdt, 2), "unit": "pairs/s", "cores": 1, "kind": "port",
+                                           "sample": f"{n} keyframe pairs (8 distinct), oracle, single thread, {cdt:.1f} s"}
+    return res
+
+
 def load_traffic(kernel: str, batch: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
     f = ROOT / "profiles" / "pmc_traffic.json"
@@ -316,6 +364,9 @@ def main():
     ap.add_argument("--bow-batch", type=int, default=256)
     ap.add_argument("--bow-steps", type=int, default=10)
     ap.add_argument("--no-bow", action="store_true")
+    ap.add_argument("--bowmatch-batch", type=int, default=256)
+    ap.add_argument("--bowmatch-steps", type=int, default=10)
+    ap.add_argument("--no-bowmatch", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -432,6 +483,8 @@ def main():
         out.update(bench_pose(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if not args.no_bow:
         out.update(bench_bow(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
+    if not args.no_bowmatch:
+        out.update(bench_bowmatch(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if not args.no_lba:
         out.update(bench_localba(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -254,6 +254,58 @@ int orbv_transform_batch_device(orbv_vocab *v, const uint8_t *d_desc, const int3
 int orbv_batch_fetch(orbv_vocab *v, int frame, uint32_t *words, double *values, int32_t *n_words,
                      uint32_t *fv_nodes, int32_t *fv_start, int32_t *fv_features, int32_t *n_fv);
 
+/* -------- BoW-guided matchers (replace ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) and
+ * ORBmatcher::SearchForTriangulation) -------- */
+
+/* A KeyFrame (or Frame) as the BoW matchers read it (include/KeyFrame.h). Host pointers. */
+typedef struct {
+    int32_t n;                   /* N */
+    const orbx_kp *keys_un;      /* mvKeysUn (angle / octave / pt) */
+    const float *u_right;        /* mvuRight */
+    const uint8_t *desc;         /* mDescriptors, N x 32 */
+    const int32_t *mp;           /* GetMapPoint(i) as an index into the caller's point table, -1 = NULL */
+    const uint8_t *mp_bad;       /* [N] 1 if that map point isBad() (may be NULL = none bad) */
+    int32_t n_fv;                /* mFeatVec: n_fv nodes ascending, features of node j are */
+    const uint32_t *fv_nodes;    /*   fv_features[fv_start[j] .. fv_start[j+1]) */
+    const int32_t *fv_start;
+    const int32_t *fv_features;
+    float fx, fy, cx, cy;        /* KeyFrame calibration */
+    int32_t nlevels;
+    float scale_factors[16];     /* mvScaleFactors */
+    float level_sigma2[16];      /* mvLevelSigma2 */
+} orbb_keyframe;
+
+typedef struct orbb_engine orbb_engine;
+int orbb_create(orbb_engine **out);
+void orbb_destroy(orbb_engine *e);
+
+/* ORBmatcher(nnratio, check_ori).SearchByBoW(pKF, F, vpMapPointMatches) (ORBmatcher.h:148,
+ * ORBmatcher.cc:236-353; Tracking::TrackReferenceKeyFrame / Relocalization). matches[F.n] out:
+ * the KF map-point index matched to frame keypoint i, -1 = NULL. Feature-vector nodes are
+ * independent (a frame keypoint belongs to one node), so each shared node is one wavefront
+ * that keeps the reference's greedy order inside the node. */
+int orbb_search_by_bow(orbb_engine *e, const orbb_keyframe *kf, const orbb_keyframe *f, float nnratio,
+                       int check_ori, int32_t *matches, int32_t *nmatches);
+
+/* ORBmatcher(0.6, check_ori).SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+ * (ORBmatcher.h:181, ORBmatcher.cc:915-1089; LocalMapping::CreateNewMapPoints). F12 row-major
+ * CV_32F (LocalMapping::ComputeF12), Cw1 = pKF1->GetCameraCenter(), T2w = pKF2 [R2w | t2w]
+ * rows. pairs[2 * k] = idx1, pairs[2 * k + 1] = idx2 of the k-th vMatchedPairs entry (idx1
+ * ascending); capacity kf1->n pairs. */
+int orbb_search_for_triangulation(orbb_engine *e, const orbb_keyframe *kf1, const orbb_keyframe *kf2,
+                                  const float F12[9], const float Cw1[3], const float T2w[12], int only_stereo,
+                                  int check_ori, int32_t *pairs, int32_t *npairs);
+/* Batched device-resident form: stage (a, b) pairs into slots -- SearchByBoW reads a = KeyFrame,
+ * b = Frame; SearchForTriangulation a = KF1, b = KF2 (F12 / Cw1 / T2w may be NULL for
+ * SearchByBoW) -- run one launch chain over all slots, fetch per slot (tri = 0: matches[b.n],
+ * tri = 1: pairs[2 * n]). */
+int orbb_reserve(orbb_engine *e, int n_slots, int cap_kp);
+int orbb_stage(orbb_engine *e, int slot, const orbb_keyframe *a, const orbb_keyframe *b, const float F12[9],
+               const float Cw1[3], const float T2w[12]);
+int orbb_run_bow_batch(orbb_engine *e, int n_slots, float nnratio, int check_ori, void *stream);
+int orbb_run_tri_batch(orbb_engine *e, int n_slots, int only_stereo, int check_ori, void *stream);
+int orbb_fetch(orbb_engine *e, int slot, int tri, int32_t *out, int32_t *n);
+
 /* -------- pose-only optimisation (replaces Optimizer::PoseOptimization) -------- */
 
 /* The edges Optimizer::PoseOptimization (Optimizer.h:105, Optimizer.cc:375-622) builds from a

@@ -513,3 +513,57 @@ class Vocabulary:
         return {"words": words[: nw.value].copy(), "values": vals[: nw.value].copy(),
                 "fv_nodes": fvn[: nf.value].copy(), "fv_start": fvs[: nf.value + 1].copy(),
                 "fv_features": fvf[: fvs[nf.value]].copy()}
+
+
+# ---- BoW-guided matchers (track_oracle.c)
+class OrbbKeyFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("keys_un", C.c_void_p), ("u_right", C.c_void_p), ("desc", C.c_void_p),
+                ("mp", C.c_void_p), ("mp_bad", C.c_void_p), ("n_fv", C.c_int32), ("fv_nodes", C.c_void_p),
+                ("fv_start", C.c_void_p), ("fv_features", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("nlevels", C.c_int32), ("scale_factors", C.c_float * 16),
+                ("level_sigma2", C.c_float * 16)]
+
+
+def make_orbb_keyframe(k: dict):
+    keep = {"keys_un": np.ascontiguousarray(k["keys_un"], KP_DTYPE), "u_right": np.ascontiguousarray(k["u_right"], np.float32),
+            "desc": np.ascontiguousarray(k["desc"], np.uint8), "mp": np.ascontiguousarray(k["mp"], np.int32),
+            "mp_bad": np.ascontiguousarray(k["mp_bad"], np.uint8), "fv_nodes": np.ascontiguousarray(k["fv_nodes"], np.uint32),
+            "fv_start": np.ascontiguousarray(k["fv_start"], np.int32),
+            "fv_features": np.ascontiguousarray(k["fv_features"], np.int32)}
+    K = OrbbKeyFrame()
+    K.n = len(keep["keys_un"])
+    for f in ("keys_un", "u_right", "desc", "mp", "mp_bad", "fv_nodes", "fv_start", "fv_features"):
+        setattr(K, f, keep[f].ctypes.data)
+    K.n_fv = len(keep["fv_nodes"])
+    K.fx, K.fy, K.cx, K.cy = (float(k[f]) for f in ("fx", "fy", "cx", "cy"))
+    K.nlevels = int(k["nlevels"])
+    for f in ("scale_factors", "level_sigma2"):
+        a = np.zeros(16, np.float32)
+        a[: K.nlevels] = k[f]
+        getattr(K, f)[:] = [float(x) for x in a]
+    return K, keep
+
+
+def search_by_bow(prob: dict, nnratio=0.7, check_ori=True):
+    L = lib()
+    L.orc_search_by_bow.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_int, C.c_void_p]
+    A, k1 = make_orbb_keyframe(prob["A"])
+    B, k2 = make_orbb_keyframe(prob["B"])
+    out = np.zeros(max(B.n, 1), np.int32)
+    nm = L.orc_search_by_bow(C.byref(A), C.byref(B), nnratio, 1 if check_ori else 0, out.ctypes.data)
+    return nm, out[: B.n]
+
+
+def search_for_triangulation(prob: dict, only_stereo=False, check_ori=True):
+    L = lib()
+    L.orc_search_for_triangulation.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                               C.c_int, C.c_void_p]
+    A, k1 = make_orbb_keyframe(prob["A"])
+    B, k2 = make_orbb_keyframe(prob["B"])
+    F12 = np.ascontiguousarray(prob["F12"], np.float32)
+    Cw = np.ascontiguousarray(prob["Cw1"], np.float32)
+    T2w = np.ascontiguousarray(prob["T2w"], np.float32)
+    pairs = np.zeros((max(A.n, 1), 2), np.int32)
+    npairs = L.orc_search_for_triangulation(C.byref(A), C.byref(B), F12.ctypes.data, Cw.ctypes.data, T2w.ctypes.data,
+                                            1 if only_stereo else 0, 1 if check_ori else 0, pairs.ctypes.data)
+    return pairs[:npairs].copy()

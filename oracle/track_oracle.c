@@ -297,3 +297,154 @@ int orc_search_by_projection_frame(const orbt_frame *cur, const orbt_frame *last
     orc_grid_free(&g);
     return nmatches;
 }
+
+/* ==========================================================================================
+ * BoW-guided matchers: ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+ * (ORBmatcher.cc:236-353) and ORBmatcher::SearchForTriangulation (ORBmatcher.cc:915-1089,
+ * CheckDistEpipolarLine :211-231). FeatureVector = sorted node arrays; the reference's
+ * while loop with lower_bound visits exactly the nodes present in both.
+ * ========================================================================================*/
+static int fv_find(const orbb_keyframe *k, uint32_t node) {
+    int lo = 0, hi = k->n_fv;
+    while (lo < hi) { const int m = (lo + hi) >> 1; if (k->fv_nodes[m] < node) lo = m + 1; else hi = m; }
+    return (lo < k->n_fv && k->fv_nodes[lo] == node) ? lo : -1;
+}
+
+static void three_maxima_n(const int *counts, int *ind1, int *ind2, int *ind3) { three_maxima30(counts, ind1, ind2, ind3); }
+
+int orc_search_by_bow(const orbb_keyframe *kf, const orbb_keyframe *F, float nnratio, int checkOri, int32_t *matches) {
+    const int TH_LOW = 50, HISTO_LENGTH = 30;
+    const float factor = HISTO_LENGTH / 360.0f;
+    for (int i = 0; i < F->n; i++) matches[i] = -1;
+    int *hb = (int *)malloc(sizeof(int) * ((size_t)F->n + 1)), *hi = (int *)malloc(sizeof(int) * ((size_t)F->n + 1));
+    int nh = 0, nmatches = 0;
+    for (int a = 0; a < kf->n_fv; a++) {
+        const int b = fv_find(F, kf->fv_nodes[a]);
+        if (b < 0) continue;
+        for (int u = kf->fv_start[a]; u < kf->fv_start[a + 1]; u++) {
+            const int realIdxKF = kf->fv_features[u];
+            const int pMP = kf->mp[realIdxKF];
+            if (pMP < 0) continue;
+            if (kf->mp_bad && kf->mp_bad[realIdxKF]) continue;
+            const uint8_t *dKF = kf->desc + 32 * (size_t)realIdxKF;
+            int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+            for (int w = F->fv_start[b]; w < F->fv_start[b + 1]; w++) {
+                const int realIdxF = F->fv_features[w];
+                if (matches[realIdxF] >= 0) continue;
+                const int dist = orc_descriptor_distance(dKF, F->desc + 32 * (size_t)realIdxF);
+                if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = realIdxF; }
+                else if (dist < bestDist2) bestDist2 = dist;
+            }
+            if (bestDist1 <= TH_LOW) {
+                if ((float)bestDist1 < nnratio * (float)bestDist2) {
+                    matches[bestIdxF] = pMP;
+                    if (checkOri) {
+                        float rot = kf->keys_un[realIdxKF].angle - F->keys_un[bestIdxF].angle;
+                        if (rot < 0.0) rot += 360.0f;
+                        int bin = (int)roundf(rot * factor);
+                        if (bin == HISTO_LENGTH) bin = 0;
+                        hb[nh] = bin; hi[nh] = bestIdxF; nh++;
+                    }
+                    nmatches++;
+                }
+            }
+        }
+    }
+    if (checkOri) {
+        int counts[30] = {0};
+        for (int k = 0; k < nh; k++) counts[hb[k]]++;
+        int i1 = -1, i2 = -1, i3 = -1;
+        three_maxima_n(counts, &i1, &i2, &i3);
+        for (int k = 0; k < nh; k++) {
+            if (hb[k] == i1 || hb[k] == i2 || hb[k] == i3) continue;
+            matches[hi[k]] = -1;
+            nmatches--;
+        }
+    }
+    free(hb); free(hi);
+    return nmatches;
+}
+
+static int check_dist_epipolar(const orc_kp *kp1, const orc_kp *kp2, const float F12[9], const orbb_keyframe *kf2) {
+    const float a = kp1->x * F12[0] + kp1->y * F12[3] + F12[6];
+    const float b = kp1->x * F12[1] + kp1->y * F12[4] + F12[7];
+    const float c = kp1->x * F12[2] + kp1->y * F12[5] + F12[8];
+    const float num = a * kp2->x + b * kp2->y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return 0;
+    const float dsqr = num * num / den;
+    return dsqr < 3.84 * kf2->level_sigma2[kp2->octave];
+}
+
+int orc_search_for_triangulation(const orbb_keyframe *kf1, const orbb_keyframe *kf2, const float F12[9],
+                                 const float Cw[3], const float T2w[12], int bOnlyStereo, int checkOri,
+                                 int32_t *pairs) {
+    const int TH_LOW = 50, HISTO_LENGTH = 30;
+    const float factor = HISTO_LENGTH / 360.0f;
+    float C2[3];
+    mat_rx_t(T2w, Cw, C2);
+    const float invz = 1.0f / C2[2];
+    const float ex = kf2->fx * C2[0] * invz + kf2->cx;
+    const float ey = kf2->fy * C2[1] * invz + kf2->cy;
+    uint8_t *matched2 = (uint8_t *)calloc((size_t)kf2->n + 1, 1);
+    int *m12 = (int *)malloc(sizeof(int) * ((size_t)kf1->n + 1));
+    for (int i = 0; i < kf1->n; i++) m12[i] = -1;
+    int *hb = (int *)malloc(sizeof(int) * ((size_t)kf1->n + 1)), *hi = (int *)malloc(sizeof(int) * ((size_t)kf1->n + 1));
+    int nh = 0, nmatches = 0;
+    for (int a = 0; a < kf1->n_fv; a++) {
+        const int b = fv_find(kf2, kf1->fv_nodes[a]);
+        if (b < 0) continue;
+        for (int u = kf1->fv_start[a]; u < kf1->fv_start[a + 1]; u++) {
+            const int idx1 = kf1->fv_features[u];
+            if (kf1->mp[idx1] >= 0) continue;                     /* GetMapPoint(idx1) != NULL */
+            const int bStereo1 = kf1->u_right[idx1] >= 0;
+            if (bOnlyStereo && !bStereo1) continue;
+            const orc_kp *kp1 = (const orc_kp *)&kf1->keys_un[idx1];
+            const uint8_t *d1 = kf1->desc + 32 * (size_t)idx1;
+            int bestDist = TH_LOW, bestIdx2 = -1;
+            for (int w = kf2->fv_start[b]; w < kf2->fv_start[b + 1]; w++) {
+                const int idx2 = kf2->fv_features[w];
+                if (matched2[idx2] || kf2->mp[idx2] >= 0) continue;
+                const int bStereo2 = kf2->u_right[idx2] >= 0;
+                if (bOnlyStereo && !bStereo2) continue;
+                const int dist = orc_descriptor_distance(d1, kf2->desc + 32 * (size_t)idx2);
+                if (dist > TH_LOW || dist > bestDist) continue;
+                const orc_kp *kp2 = (const orc_kp *)&kf2->keys_un[idx2];
+                if (!bStereo1 && !bStereo2) {
+                    const float distex = ex - kp2->x, distey = ey - kp2->y;
+                    if (distex * distex + distey * distey < 100 * kf2->scale_factors[kp2->octave]) continue;
+                }
+                if (check_dist_epipolar(kp1, kp2, F12, kf2)) { bestIdx2 = idx2; bestDist = dist; }
+            }
+            if (bestIdx2 >= 0) {
+                m12[idx1] = bestIdx2;
+                matched2[bestIdx2] = 1;
+                nmatches++;
+                if (checkOri) {
+                    float rot = kp1->angle - kf2->keys_un[bestIdx2].angle;
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == HISTO_LENGTH) bin = 0;
+                    hb[nh] = bin; hi[nh] = idx1; nh++;
+                }
+            }
+        }
+    }
+    if (checkOri) {
+        int counts[30] = {0};
+        for (int k = 0; k < nh; k++) counts[hb[k]]++;
+        int i1 = -1, i2 = -1, i3 = -1;
+        three_maxima_n(counts, &i1, &i2, &i3);
+        for (int k = 0; k < nh; k++) {
+            if (hb[k] == i1 || hb[k] == i2 || hb[k] == i3) continue;
+            matched2[m12[hi[k]]] = 0;
+            m12[hi[k]] = -1;
+            nmatches--;
+        }
+    }
+    int np = 0;
+    for (int i = 0; i < kf1->n; i++)
+        if (m12[i] >= 0) { pairs[2 * np] = i; pairs[2 * np + 1] = m12[i]; np++; }
+    free(matched2); free(m12); free(hb); free(hi);
+    return np;
+}

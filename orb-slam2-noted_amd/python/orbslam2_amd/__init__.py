@@ -99,6 +99,15 @@ SIGNATURES = [
     ("orbv_transform", _I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     ("orbv_transform_batch_device", _I, [_P, _P, _P, _I, _I, C.c_size_t, _I, _P]),
     ("orbv_batch_fetch", _I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    ("orbb_create", _I, [C.POINTER(C.c_void_p)]),
+    ("orbb_destroy", None, [_P]),
+    ("orbb_search_by_bow", _I, [_P, _P, _P, _F, _I, _P, _P]),
+    ("orbb_search_for_triangulation", _I, [_P, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
+    ("orbb_reserve", _I, [_P, _I, _I]),
+    ("orbb_stage", _I, [_P, _I, _P, _P, _P, _P, _P]),
+    ("orbb_run_bow_batch", _I, [_P, _I, _F, _I, _P]),
+    ("orbb_run_tri_batch", _I, [_P, _I, _I, _I, _P]),
+    ("orbb_fetch", _I, [_P, _I, _I, _P, _P]),
 ]
 
 
@@ -708,3 +717,100 @@ class Vocabulary:
                                       b[2].ctypes.data, b[3].ctypes.data, b[4].ctypes.data, C.byref(nf)),
                "orbv_batch_fetch")
         return self._pack(b, nw.value, nf.value)
+
+
+# ---- BoW-guided matchers (orbb_*): SearchByBoW(KF, F) + SearchForTriangulation -------------
+class OrbbKeyFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("keys_un", C.c_void_p), ("u_right", C.c_void_p), ("desc", C.c_void_p),
+                ("mp", C.c_void_p), ("mp_bad", C.c_void_p), ("n_fv", C.c_int32), ("fv_nodes", C.c_void_p),
+                ("fv_start", C.c_void_p), ("fv_features", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("nlevels", C.c_int32), ("scale_factors", C.c_float * 16),
+                ("level_sigma2", C.c_float * 16)]
+
+
+def _orbb_keyframe(k: dict):
+    keep = {"keys_un": np.ascontiguousarray(k["keys_un"]).view(KP_DTYPE),
+            "u_right": np.ascontiguousarray(k["u_right"], np.float32), "desc": np.ascontiguousarray(k["desc"], np.uint8),
+            "mp": np.ascontiguousarray(k["mp"], np.int32), "mp_bad": np.ascontiguousarray(k["mp_bad"], np.uint8),
+            "fv_nodes": np.ascontiguousarray(k["fv_nodes"], np.uint32),
+            "fv_start": np.ascontiguousarray(k["fv_start"], np.int32),
+            "fv_features": np.ascontiguousarray(k["fv_features"], np.int32)}
+    K = OrbbKeyFrame()
+    K.n = len(keep["keys_un"])
+    for f in ("keys_un", "u_right", "desc", "mp", "mp_bad", "fv_nodes", "fv_start", "fv_features"):
+        setattr(K, f, keep[f].ctypes.data)
+    K.n_fv = len(keep["fv_nodes"])
+    K.fx, K.fy, K.cx, K.cy = (float(k[f]) for f in ("fx", "fy", "cx", "cy"))
+    K.nlevels = int(k["nlevels"])
+    for f in ("scale_factors", "level_sigma2"):
+        a = np.zeros(16, np.float32)
+        a[: K.nlevels] = k[f]
+        getattr(K, f)[:] = [float(x) for x in a]
+    return K, keep
+
+
+class BowMatcher:
+    """ORBmatcher::SearchByBoW(KeyFrame*, Frame&) and SearchForTriangulation on the GPU.
+    Problems are dicts shaped like synth.bow_match_problem: {"A", "B", "F12", "Cw1", "T2w"}."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        _check(lib().orbb_create(C.byref(h)), "orbb_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def search_by_bow(self, prob: dict, nnratio=0.7, check_ori=True):
+        A, k1 = _orbb_keyframe(prob["A"])
+        B, k2 = _orbb_keyframe(prob["B"])
+        out = np.zeros(max(B.n, 1), np.int32)
+        nm = C.c_int32()
+        _check(lib().orbb_search_by_bow(self._h, C.byref(A), C.byref(B), nnratio, 1 if check_ori else 0,
+                                        out.ctypes.data, C.byref(nm)), "orbb_search_by_bow")
+        return nm.value, out[: B.n]
+
+    def search_for_triangulation(self, prob: dict, only_stereo=False, check_ori=True):
+        A, k1 = _orbb_keyframe(prob["A"])
+        B, k2 = _orbb_keyframe(prob["B"])
+        g = {k: np.ascontiguousarray(prob[k], np.float32) for k in ("F12", "Cw1", "T2w")}
+        pairs = np.zeros((max(A.n, 1), 2), np.int32)
+        n = C.c_int32()
+        _check(lib().orbb_search_for_triangulation(self._h, C.byref(A), C.byref(B), g["F12"].ctypes.data,
+                                                   g["Cw1"].ctypes.data, g["T2w"].ctypes.data, 1 if only_stereo else 0,
+                                                   1 if check_ori else 0, pairs.ctypes.data, C.byref(n)),
+               "orbb_search_for_triangulation")
+        return pairs[: n.value].copy()
+
+    def reserve(self, n_slots: int, cap_kp: int):
+        _check(lib().orbb_reserve(self._h, n_slots, cap_kp), "orbb_reserve")
+
+    def stage(self, slot: int, prob: dict):
+        A, k1 = _orbb_keyframe(prob["A"])
+        B, k2 = _orbb_keyframe(prob["B"])
+        g = {k: np.ascontiguousarray(prob[k], np.float32) for k in ("F12", "Cw1", "T2w")}
+        _check(lib().orbb_stage(self._h, slot, C.byref(A), C.byref(B), g["F12"].ctypes.data, g["Cw1"].ctypes.data,
+                                g["T2w"].ctypes.data), "orbb_stage")
+
+    def run_bow_batch(self, n_slots: int, nnratio=0.7, check_ori=True, stream=None):
+        _check(lib().orbb_run_bow_batch(self._h, n_slots, nnratio, 1 if check_ori else 0, stream), "orbb_run_bow_batch")
+
+    def run_tri_batch(self, n_slots: int, only_stereo=False, check_ori=True, stream=None):
+        _check(lib().orbb_run_tri_batch(self._h, n_slots, 1 if only_stereo else 0, 1 if check_ori else 0, stream),
+               "orbb_run_tri_batch")
+
+    def fetch(self, slot: int, tri: bool, n_out: int):
+        out = np.zeros(max(2 * n_out, 1), np.int32)
+        n = C.c_int32()
+        _check(lib().orbb_fetch(self._h, slot, 1 if tri else 0, out.ctypes.data, C.byref(n)), "orbb_fetch")
+        if tri:
+            return out[: 2 * n.value].reshape(-1, 2).copy()
+        return n.value, out[:n_out].copy()

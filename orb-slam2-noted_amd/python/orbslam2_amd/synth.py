@@ -478,3 +478,92 @@ def bow_features(voc: dict, seed: int, n: int = 2000, noise_bits: int = 24, rand
     r = rng.random(n) < random_frac
     d[r] = rng.integers(0, 256, (int(r.sum()), 32), dtype=np.uint8)
     return np.ascontiguousarray(d)
+
+
+# ---------------------------------------------------------------------------------------
+# BoW-guided matchers: two keyframes A, B of a common scene (KITTI
+# camera, B ~0.8 m ahead of A). Keypoints of the same 3D point share a base descriptor
+# (0..40 flipped bits), a consistent in-plane rotation (+10 deg) and, mostly, a FeatureVector
+# node (node = point id mod 100 -- the level-2 nodes of a k=10 vocabulary at levelsup 4);
+# distractor keypoints fill up to n. A's keypoints carry map points (some bad) for
+# SearchByBoW; both frames carry some for SearchForTriangulation. F12 / Cw1 / T2w follow
+# LocalMapping::ComputeF12 and KeyFrame::GetCameraCenter.
+# ---------------------------------------------------------------------------------------
+def _fv_from_nodes(nodes: np.ndarray):
+    order = np.lexsort((np.arange(len(nodes)), nodes))
+    sn = nodes[order]
+    uniq, start = np.unique(sn, return_index=True)
+    return (uniq.astype(np.uint32), np.append(start, len(nodes)).astype(np.int32), order.astype(np.int32))
+
+
+def bow_match_problem(seed: int = 3, n: int = 2000, n_points: int = 1600, stereo_frac: float = 0.5,
+                      mp_frac_a: float = 0.6, mp_frac_b: float = 0.3, W: int = 1241, H: int = 376):
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = (np.float32(v) for v in KITTI_CAM)
+    sf = np.float32(1.2) ** np.arange(8, dtype=np.float32)
+    s2 = (sf * sf).astype(np.float32)
+    feat = np.array([434, 362, 302, 251, 209, 175, 145, 122], np.float64)
+    oct_p = feat / feat.sum()
+    Ra = _small_rot(rng, 2.0)
+    ta = rng.normal(0, 0.5, 3)
+    Rb = Ra @ _small_rot(rng, 2.0)
+    Ca = -Ra.T @ ta
+    Cb = Ca + Ra.T @ np.array([rng.normal(0, 0.1), rng.normal(0, 0.05), 0.8])
+    tb = -Rb @ Cb
+    z = rng.uniform(4, 40, n_points)
+    u = rng.uniform(0, W, n_points)
+    v = rng.uniform(0, H, n_points)
+    Pa = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    Pw = (Pa - ta) @ Ra
+    base = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    ang = rng.uniform(0, 360, n_points)
+    node = (np.arange(n_points) % 100).astype(np.int64)
+
+    def frame(R, t, dang, frac, mp_frac):
+        kps, desc, ur, nodes, mp = [], [], [], [], []
+        Pc = Pw @ R.T + t
+        for p in range(n_points):
+            if rng.random() > frac or Pc[p, 2] <= 0.5:
+                continue
+            uu = fx * Pc[p, 0] / Pc[p, 2] + cx
+            vv = fy * Pc[p, 1] / Pc[p, 2] + cy
+            o = int(rng.choice(8, p=oct_p))
+            s = float(sf[o])
+            x, y = uu + rng.normal(0, 0.7 * s), vv + rng.normal(0, 0.7 * s)
+            if not (0 <= x < W and 0 <= y < H):
+                continue
+            kps.append((x, y, 31 * s, (ang[p] + dang + rng.normal(0, 2)) % 360, 0, o, -1))
+            desc.append(_flip_bits(rng, base[p], int(rng.integers(0, 40))))
+            ur.append(x - bf / Pc[p, 2] if rng.random() < stereo_frac else -1.0)
+            nodes.append(node[p] if rng.random() < 0.9 else int(rng.integers(0, 100)))
+            mp.append(p if rng.random() < mp_frac else -1)
+        while len(kps) < n:
+            o = int(rng.choice(8, p=oct_p))
+            kps.append((rng.uniform(0, W), rng.uniform(0, H), 31 * float(sf[o]), rng.uniform(0, 360), 0, o, -1))
+            desc.append(rng.integers(0, 256, 32, dtype=np.uint8))
+            ur.append(float(rng.uniform(0, W)) if rng.random() < stereo_frac else -1.0)
+            nodes.append(int(rng.integers(0, 100)))
+            mp.append(int(rng.integers(0, n_points)) if rng.random() < mp_frac * 0.5 else -1)
+        perm = rng.permutation(len(kps))[:n]
+        keys = np.array([kps[i] for i in perm], TRACK_KP_DTYPE)
+        fvn, fvs, fvf = _fv_from_nodes(np.array([nodes[i] for i in perm], np.int64))
+        mpa = np.array([mp[i] for i in perm], np.int32)
+        return {"keys_un": keys, "desc": np.stack([desc[i] for i in perm]).astype(np.uint8),
+                "u_right": np.array([ur[i] for i in perm], np.float32), "mp": mpa,
+                "mp_bad": ((rng.random(len(perm)) < 0.05) & (mpa >= 0)).astype(np.uint8),
+                "fv_nodes": fvn, "fv_start": fvs, "fv_features": fvf, "fx": fx, "fy": fy, "cx": cx, "cy": cy,
+                "nlevels": 8, "scale_factors": sf, "level_sigma2": s2}
+
+    A = frame(Ra, ta, 0.0, 0.85, mp_frac_a)
+    B = frame(Rb, tb, -10.0, 0.85, mp_frac_b)
+    # LocalMapping::ComputeF12 (float): F12 = K1^-T [t12]x R12 K2^-1
+    R1, t1, R2, t2 = Ra.astype(np.float32), ta.astype(np.float32), Rb.astype(np.float32), tb.astype(np.float32)
+    R12 = R1 @ R2.T
+    t12 = -R1 @ R2.T @ t2 + t1
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]], np.float32)
+    K = np.array([[fx, 0, cx], [0, fy, cy], [0, 0, 1]], np.float32)
+    Kinv = np.linalg.inv(K.astype(np.float64)).astype(np.float32)
+    F12 = (Kinv.T @ tx @ R12 @ Kinv).astype(np.float32)
+    T2w = np.concatenate([R2, t2[:, None]], 1).astype(np.float32)
+    Cw1 = (-(R1.astype(np.float64).T @ t1.astype(np.float64))).astype(np.float32)
+    return {"A": A, "B": B, "F12": F12, "Cw1": Cw1, "T2w": T2w}
