@@ -163,10 +163,19 @@ def bench_track(amd, args, dist, world, with_cpu):
     amd.device_sync()
     dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
     nm, _, _ = t.fetch(0, 2000)
+    # ORBmatcher::Fuse(pKF, vpMapPoints, 3) search half over the same (keyframe, 3000 points)
+    t.run_fuse_batch(B, 3.0)
+    amd.device_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.track_steps):
+        t.run_fuse_batch(B, 3.0)
+    amd.device_sync()
+    fdt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
     res = {"track_frames_per_s": round(world * B * args.track_steps / dt, 2),
            "track": {"frames_per_step": B, "ms_per_step": round(1000 * dt / args.track_steps, 3),
                      "keypoints": 2000, "map_points": 3000, "last_keypoints": 1500,
-                     "frame_matches_slot0": int(nm)}}
+                     "frame_matches_slot0": int(nm)},
+           "fuse_keyframes_per_s": round(world * B * args.track_steps / fdt, 2)}
     t.close()
     if with_cpu:
         sys.path.insert(0, str(ROOT / "oracle"))

@@ -154,6 +154,7 @@ typedef struct {
     int32_t nlevels;             /* mnScaleLevels */
     float log_scale_factor;      /* mfLogScaleFactor = log(mfScaleFactor) */
     float scale_factors[16];     /* mvScaleFactors */
+    float inv_level_sigma2[16];  /* mvInvLevelSigma2 (read by orbt_fuse_candidates) */
 } orbt_frame;
 
 #define ORBT_MP_BAD 1            /* MapPoint::isBad() */
@@ -208,6 +209,19 @@ int orbt_search_by_projection_frame(orbt_engine *e, const orbt_frame *cur, const
                                     const orbt_mappoints *M, float th, int mono, int check_ori,
                                     const uint8_t *kp_blocked, int32_t *owner, int32_t *nmatches);
 
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th) (ORBmatcher.h:208, ORBmatcher.cc:1139-1278; th = 3 from
+ * LocalMapping::SearchInNeighbors) -- the search half. `kf` is the KeyFrame (pose, calibration,
+ * bounds, grid keypoints, mvuRight, descriptors, mvScaleFactors, mvInvLevelSigma2); flags
+ * ORBT_MP_IN_FRAME = pMP->IsInKeyFrame(pKF). For every other non-bad point: projection,
+ * IsInImage, scale-invariance and viewing-angle gates, PredictScale(dist, pKF), window,
+ * level and chi2 (5.99 / 7.8) gates, first minimum Hamming distance -> best_idx[m] (-1 = no
+ * candidate) and best_dist[m]. The search of a point does not depend on the map updates of
+ * earlier points, so all points run in parallel; the caller applies the reference's updates
+ * (Replace / AddObservation, :1245-1271) in point order for best_dist <= 50, re-checking
+ * isBad / IsInKeyFrame, exactly as the reference loop does. */
+int orbt_fuse_candidates(orbt_engine *e, const orbt_frame *kf, const orbt_mappoints *M, float th,
+                         int32_t *best_idx, int32_t *best_dist);
+
 /* Batched device-resident form (throughput path): stage independent problems into slots
  * (host -> HBM), run one launch chain over all slots, fetch per slot. `last`, `last_mp`,
  * `last_outlier` may be NULL when only orbt_run_local_batch is used. */
@@ -218,6 +232,8 @@ int orbt_stage(orbt_engine *e, int slot, const orbt_frame *F, const orbt_mappoin
 int orbt_run_local_batch(orbt_engine *e, int n_slots, float view_cos_limit, float th, float nnratio,
                          void *stream);
 int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int check_ori, void *stream);
+int orbt_run_fuse_batch(orbt_engine *e, int n_slots, float th, void *stream);
+int orbt_fetch_fuse(orbt_engine *e, int slot, int32_t *best_idx, int32_t *best_dist);
 int orbt_fetch(orbt_engine *e, int slot, orbt_view *view, int32_t *owner, int32_t *nmatches);
 
 /* -------- bag of words (replaces Frame::ComputeBoW -> DBoW2 TemplatedVocabulary::transform) -------- */

@@ -340,7 +340,8 @@ class OrbtFrame(C.Structure):
                 ("Tcw", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float), ("fy", C.c_float),
                 ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("mb", C.c_float),
                 ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float),
-                ("nlevels", C.c_int32), ("log_scale_factor", C.c_float), ("scale_factors", C.c_float * 16)]
+                ("nlevels", C.c_int32), ("log_scale_factor", C.c_float), ("scale_factors", C.c_float * 16),
+                ("inv_level_sigma2", C.c_float * 16)]
 
 
 class OrbtMapPoints(C.Structure):
@@ -368,6 +369,10 @@ def make_orbt_frame(fr: dict):
     sf = np.zeros(16, np.float32)
     sf[: F.nlevels] = fr["scale_factors"]
     F.scale_factors[:] = [float(v) for v in sf]
+    isg = np.zeros(16, np.float32)
+    isg[: F.nlevels] = fr["inv_level_sigma2"] if "inv_level_sigma2" in fr else \
+        (np.float32(1) / (np.asarray(fr["scale_factors"], np.float32) ** 2)).astype(np.float32)
+    F.inv_level_sigma2[:] = [float(v) for v in isg]
     return F, keep
 
 
@@ -567,3 +572,15 @@ def search_for_triangulation(prob: dict, only_stereo=False, check_ori=True):
     npairs = L.orc_search_for_triangulation(C.byref(A), C.byref(B), F12.ctypes.data, Cw.ctypes.data, T2w.ctypes.data,
                                             1 if only_stereo else 0, 1 if check_ori else 0, pairs.ctypes.data)
     return pairs[:npairs].copy()
+
+
+def fuse_candidates(prob: dict, th=3.0):
+    """ORBmatcher::Fuse(pKF, vpMapPoints, th) search half: (best_idx, best_dist) per map point."""
+    L = lib()
+    L.orc_fuse_candidates.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]
+    F, k1 = make_orbt_frame(prob["frame"])
+    M, k2 = make_orbt_map(prob["map"])
+    bi = np.zeros(max(M.n, 1), np.int32)
+    bd = np.zeros(max(M.n, 1), np.int32)
+    L.orc_fuse_candidates(C.byref(F), C.byref(M), th, bi.ctypes.data, bd.ctypes.data)
+    return bi[: M.n], bd[: M.n]

@@ -448,3 +448,68 @@ int orc_search_for_triangulation(const orbb_keyframe *kf1, const orbb_keyframe *
     free(matched2); free(m12); free(hb); free(hi);
     return np;
 }
+
+/* ==========================================================================================
+ * ORBmatcher::Fuse(KeyFrame*, const vector<MapPoint*>&, th), search half (ORBmatcher.cc:
+ * 1139-1240; KeyFrame::IsInImage KeyFrame.cc:841-844, KeyFrame::GetFeaturesInArea :794-838,
+ * MapPoint::PredictScale(dist, KeyFrame*) MapPoint.cc:584-606).
+ * ========================================================================================*/
+void orc_fuse_candidates(const orbt_frame *kf, const orbt_mappoints *M, float th, int32_t *best_idx,
+                         int32_t *best_dist) {
+    orc_frame_grid g;
+    frame_grid(kf, &g);
+    int *cand = (int *)malloc(sizeof(int) * ((size_t)kf->n + 1));
+    for (int i = 0; i < M->n; i++) {
+        best_idx[i] = -1;
+        best_dist[i] = 256;
+        if (M->flags[i] & (ORBT_MP_BAD | ORBT_MP_IN_FRAME)) continue;   /* isBad() || IsInKeyFrame(pKF) */
+        const float *P = M->Xw + 3 * (size_t)i;
+        float p3Dc[3];
+        mat_rx_t(kf->Tcw, P, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+        const float u = kf->fx * x + kf->cx, v = kf->fy * y + kf->cy;
+        if (!(u >= kf->min_x && u < kf->max_x && v >= kf->min_y && v < kf->max_y)) continue;   /* IsInImage */
+        const float ur = u - kf->mbf * invz;
+        const float maxDistance = 1.2f * M->max_dist[i], minDistance = 0.8f * M->min_dist[i];
+        const float PO[3] = {P[0] - kf->Ow[0], P[1] - kf->Ow[1], P[2] - kf->Ow[2]};
+        double ss = 0;
+        for (int k = 0; k < 3; k++) { const double t = PO[k]; ss += t * t; }
+        const float dist3D = (float)sqrt(ss);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float *Pn = M->normal + 3 * (size_t)i;
+        double dot = 0;
+        for (int k = 0; k < 3; k++) dot += (double)PO[k] * Pn[k];
+        if (dot < 0.5 * dist3D) continue;
+        const float ratio = M->max_dist[i] / dist3D;
+        int nPredictedLevel = (int)ceilf(orc_logf(ratio) / kf->log_scale_factor);
+        if (nPredictedLevel < 0) nPredictedLevel = 0;
+        else if (nPredictedLevel >= kf->nlevels) nPredictedLevel = kf->nlevels - 1;
+        const float radius = th * kf->scale_factors[nPredictedLevel];
+        const int nc = orc_features_in_area(&g, u, v, radius, -1, -1, cand, kf->n + 1);
+        const uint8_t *dMP = M->desc + 32 * (size_t)i;
+        int bestDist = 256, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int idx = cand[c];
+            const orbx_kp *kp = &kf->keys_un[idx];
+            const int kpLevel = kp->octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            if (kf->u_right[idx] >= 0) {
+                const float ex = u - kp->x, ey = v - kp->y, er = ur - kf->u_right[idx];
+                const float e2 = ex * ex + ey * ey + er * er;
+                if (e2 * kf->inv_level_sigma2[kpLevel] > 7.8) continue;
+            } else {
+                const float ex = u - kp->x, ey = v - kp->y;
+                const float e2 = ex * ex + ey * ey;
+                if (e2 * kf->inv_level_sigma2[kpLevel] > 5.99) continue;
+            }
+            const int dist = orc_descriptor_distance(dMP, kf->desc + 32 * (size_t)idx);
+            if (dist < bestDist) { bestDist = dist; bestIdx = idx; }
+        }
+        best_idx[i] = bestIdx;
+        best_dist[i] = bestDist;
+    }
+    free(cand);
+    orc_grid_free(&g);
+}

@@ -22,6 +22,8 @@ int orc_search_by_bow(const orbb_keyframe *kf, const orbb_keyframe *F, float nnr
 int orc_search_for_triangulation(const orbb_keyframe *kf1, const orbb_keyframe *kf2, const float F12[9],
                                  const float Cw[3], const float T2w[12], int bOnlyStereo, int checkOri,
                                  int32_t *pairs);
+void orc_fuse_candidates(const orbt_frame *kf, const orbt_mappoints *M, float th, int32_t *best_idx,
+                         int32_t *best_dist);
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,7 @@ struct FrameDev {
     int nlevels;
     float log_scale;
     float scale[16];
+    float inv_s2[16];  // mvInvLevelSigma2 (Fuse)
     float lTcw[12];   // last frame pose (frame-to-frame matcher)
 };
 
@@ -658,6 +659,84 @@ __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float 
     if (lane == 0) nmatch[s] = nm;
 }
 
+// ---- ORBmatcher::Fuse(pKF, vpMapPoints, th) search half (ORBmatcher.cc:1139-1240): one thread
+// per (slot, map point); no claims -- every point's best keypoint is independent
+__global__ __launch_bounds__(256) void track_fuse_kernel(Slots S, float th, int *best_idx, int *best_dist) {
+    const int m = blockIdx.x * 256 + threadIdx.x, s = blockIdx.y;
+    const FrameDev &f = S.fr[s];
+    if (m >= f.n_mp) return;
+    const long long mb = (long long)s * S.cap_mp + m;
+    int bestIdx = -1, bestDist = 256;
+    if (!(S.mflags[mb] & (ORBT_MP_BAD | ORBT_MP_IN_FRAME))) {   // isBad() || IsInKeyFrame(pKF)
+        const float *P = S.Xw + mb * 3;
+        float p3Dc[3];
+        mat_rx_t(f.Tcw, P, p3Dc);
+        bool ok = !(p3Dc[2] < 0.0f);
+        float u = 0, v = 0, ur = 0;
+        int lvl = 0;
+        if (ok) {
+            const float invz = 1 / p3Dc[2];
+            const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+            u = f.fx * x + f.cx;
+            v = f.fy * y + f.cy;
+            ok = u >= f.min_x && u < f.max_x && v >= f.min_y && v < f.max_y;   // KeyFrame::IsInImage
+            ur = u - f.mbf * invz;
+        }
+        if (ok) {
+            const float maxDistance = 1.2f * S.maxd[mb], minDistance = 0.8f * S.mind[mb];
+            const float PO[3] = {P[0] - f.Ow[0], P[1] - f.Ow[1], P[2] - f.Ow[2]};
+            double ss = 0;
+            for (int k = 0; k < 3; k++) { const double t = PO[k]; ss = ss + t * t; }
+            const float dist3D = (float)sqrt(ss);
+            ok = !(dist3D < minDistance || dist3D > maxDistance);
+            if (ok) {
+                const float *Pn = S.nrm + mb * 3;
+                double dot = 0;
+                for (int k = 0; k < 3; k++) dot = dot + (double)PO[k] * (double)Pn[k];
+                ok = !(dot < 0.5 * (double)dist3D);
+                if (ok) {   // MapPoint::PredictScale(dist3D, pKF)
+                    const float ratio = S.maxd[mb] / dist3D;
+                    lvl = (int)ceilf(glibc_logf(ratio) / f.log_scale);
+                    if (lvl < 0) lvl = 0;
+                    else if (lvl >= f.nlevels) lvl = f.nlevels - 1;
+                }
+            }
+        }
+        int cx0, cx1, cy0, cy1;
+        const float radius = th * f.scale[lvl];
+        if (ok && grid_window(f, u, v, radius, cx0, cx1, cy0, cy1)) {
+            const float4 *rec = S.grec + (long long)s * S.sort_cap;
+            const int *cs = S.cell_start + (long long)s * (NCELL + 1);
+            const long long kb = (long long)s * S.cap_kp;
+            const uint8_t *dMP = S.mdesc + mb * 32;
+            for (int ix = cx0; ix <= cx1; ix++) {
+                const int a = cs[ix * GRID_ROWS + cy0], b = cs[ix * GRID_ROWS + cy1 + 1];
+                for (int t = a; t < b; t++) {
+                    const float4 g = rec[t];
+                    const float distx = g.x - u, disty = g.y - v;
+                    if (!(fabsf(distx) < radius && fabsf(disty) < radius)) continue;
+                    const uint32_t pk = __float_as_uint(g.w);
+                    const int idx = (int)(pk & 0xFFFFu), kpLevel = (int)((pk >> 16) & 0xFF);
+                    if (kpLevel < lvl - 1 || kpLevel > lvl) continue;
+                    const float ex = u - g.x, ey = v - g.y;
+                    if (g.z >= 0) {
+                        const float er = ur - g.z;
+                        const float e2 = ex * ex + ey * ey + er * er;
+                        if ((double)(e2 * f.inv_s2[kpLevel]) > 7.8) continue;
+                    } else {
+                        const float e2 = ex * ex + ey * ey;
+                        if ((double)(e2 * f.inv_s2[kpLevel]) > 5.99) continue;
+                    }
+                    const int dist = hamming32(dMP, S.desc + (kb + idx) * 32);
+                    if (dist < bestDist) { bestDist = dist; bestIdx = idx; }
+                }
+            }
+        }
+    }
+    best_idx[mb] = bestIdx;
+    best_dist[mb] = bestDist;
+}
+
 }  // namespace orbtrack
 
 using namespace orbtrack;
@@ -668,7 +747,7 @@ struct orbt_engine {
     int nslots = 0, cap_kp = 0, cap_mp = 0, sort_cap = 0;
     DevBuf fr, kun, uR, desc, blocked, keys, cell_start, lkun, last_mp, last_out;
     DevBuf Xw, nrm, mind, maxd, mdesc, mflags;
-    DevBuf in_view, px, py, pxr, vcos, level, cand, ncand, owner, nmatch, hist_idx, hist_bin;
+    DevBuf in_view, px, py, pxr, vcos, level, cand, ncand, owner, nmatch, hist_idx, hist_bin, fuse_idx, fuse_dist;
     std::vector<FrameDev> hfr;
 };
 
@@ -721,6 +800,7 @@ void fill_frame(FrameDev &d, const orbt_frame *F) {
     d.nlevels = F->nlevels;
     d.log_scale = F->log_scale_factor;
     std::memcpy(d.scale, F->scale_factors, sizeof d.scale);
+    std::memcpy(d.inv_s2, F->inv_level_sigma2, sizeof d.inv_s2);
 }
 
 }  // namespace
@@ -747,7 +827,7 @@ void orbt_destroy(orbt_engine *e) {
     DevBuf *bufs[] = {&e->fr, &e->kun, &e->uR, &e->desc, &e->blocked, &e->keys, &e->cell_start, &e->lkun, &e->last_mp,
                       &e->last_out, &e->Xw, &e->nrm, &e->mind, &e->maxd, &e->mdesc, &e->mflags, &e->in_view, &e->px,
                       &e->py, &e->pxr, &e->vcos, &e->level, &e->cand, &e->ncand, &e->owner, &e->nmatch, &e->hist_idx,
-                      &e->hist_bin};
+                      &e->hist_bin, &e->fuse_idx, &e->fuse_dist};
     for (DevBuf *b : bufs) b->release();
     delete e;
 }
@@ -769,7 +849,7 @@ int orbt_reserve(orbt_engine *e, int n_slots, int cap_kp, int cap_mp) {
         e->py.ensure(4 * S * M) || e->pxr.ensure(4 * S * M) || e->vcos.ensure(4 * S * M) || e->level.ensure(4 * S * M) ||
         e->cand.ensure(sizeof(Cand) * S * std::max(K, M)) || e->ncand.ensure(4 * S * std::max(K, M)) ||
         e->owner.ensure(4 * S * K) || e->nmatch.ensure(4 * S) || e->hist_idx.ensure(4 * S * K) ||
-        e->hist_bin.ensure(S * K))
+        e->hist_bin.ensure(S * K) || e->fuse_idx.ensure(4 * S * M) || e->fuse_dist.ensure(4 * S * M))
         return ORBX_EDEVICE;
     e->nslots = n_slots;
     e->cap_kp = cap_kp;
@@ -913,6 +993,42 @@ int orbt_search_by_projection_frame(orbt_engine *e, const orbt_frame *cur, const
     rc = orbt_run_frame_batch(e, 1, th, mono, check_ori, nullptr);
     if (rc) return rc;
     return orbt_fetch(e, 0, nullptr, owner, nmatches);
+}
+
+int orbt_run_fuse_batch(orbt_engine *e, int n_slots, float th, void *stream) {
+    if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    hipStream_t st = pick(e, stream);
+    if (grid(e, n_slots, st)) return ORBX_EDEVICE;
+    const int mm = std::max(1, max_n(e, 0, n_slots));
+    track_fuse_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, e->fuse_idx.as<int>(),
+                                                                       e->fuse_dist.as<int>());
+    TR_CHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbt_fetch_fuse(orbt_engine *e, int slot, int32_t *best_idx, int32_t *best_dist) {
+    if (!e || slot < 0 || slot >= e->nslots) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    TR_CHK(hipDeviceSynchronize());
+    const size_t M = (size_t)e->cap_mp, s = (size_t)slot, m = (size_t)e->hfr[slot].n_mp;
+    if (m && best_idx) TR_CHK(hipMemcpy(best_idx, (char *)e->fuse_idx.p + 4 * s * M, 4 * m, hipMemcpyDeviceToHost));
+    if (m && best_dist) TR_CHK(hipMemcpy(best_dist, (char *)e->fuse_dist.p + 4 * s * M, 4 * m, hipMemcpyDeviceToHost));
+    return ORBX_OK;
+}
+
+int orbt_fuse_candidates(orbt_engine *e, const orbt_frame *kf, const orbt_mappoints *M, float th, int32_t *best_idx,
+                         int32_t *best_dist) {
+    if (!e || !kf || !M || !best_idx || !best_dist) return ORBX_EINVAL;
+    if (e->nslots < 1 || e->cap_kp < kf->n || e->cap_mp < M->n) {
+        const int rc = orbt_reserve(e, std::max(1, e->nslots), std::max(e->cap_kp, kf->n), std::max(e->cap_mp, M->n));
+        if (rc) return rc;
+    }
+    int rc = orbt_stage(e, 0, kf, M, nullptr, nullptr, nullptr, nullptr);
+    if (rc) return rc;
+    rc = orbt_run_fuse_batch(e, 1, th, nullptr);
+    if (rc) return rc;
+    return orbt_fetch_fuse(e, 0, best_idx, best_dist);
 }
 
 }  // extern "C"

@@ -85,6 +85,9 @@ SIGNATURES = [
     ("orbt_run_local_batch", _I, [_P, _I, _F, _F, _F, _P]),
     ("orbt_run_frame_batch", _I, [_P, _I, _F, _I, _I, _P]),
     ("orbt_fetch", _I, [_P, _I, _P, _P, _P]),
+    ("orbt_fuse_candidates", _I, [_P, _P, _P, _F, _P, _P]),
+    ("orbt_run_fuse_batch", _I, [_P, _I, _F, _P]),
+    ("orbt_fetch_fuse", _I, [_P, _I, _P, _P]),
     ("orbp_create", _I, [C.POINTER(C.c_void_p)]),
     ("orbp_destroy", None, [_P]),
     ("orbp_pose_optimization", _I, [_P, _P, _P]),
@@ -437,7 +440,8 @@ class OrbtFrame(C.Structure):
                 ("Tcw", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float), ("fy", C.c_float),
                 ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("mb", C.c_float),
                 ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float),
-                ("nlevels", C.c_int32), ("log_scale_factor", C.c_float), ("scale_factors", C.c_float * 16)]
+                ("nlevels", C.c_int32), ("log_scale_factor", C.c_float), ("scale_factors", C.c_float * 16),
+                ("inv_level_sigma2", C.c_float * 16)]
 
 
 class OrbtMapPoints(C.Structure):
@@ -465,6 +469,10 @@ def _orbt_frame(fr: dict):
     sf = np.zeros(16, np.float32)
     sf[: F.nlevels] = fr["scale_factors"]
     F.scale_factors[:] = [float(v) for v in sf]
+    isg = np.zeros(16, np.float32)
+    isg[: F.nlevels] = fr["inv_level_sigma2"] if "inv_level_sigma2" in fr else \
+        (np.float32(1) / (np.asarray(fr["scale_factors"], np.float32) ** 2)).astype(np.float32)
+    F.inv_level_sigma2[:] = [float(v) for v in isg]
     return F, keep
 
 
@@ -534,6 +542,25 @@ class Tracker:
                                                      owner.ctypes.data, C.byref(nm)),
                "orbt_search_by_projection_frame")
         return nm.value, owner[: F.n]
+
+    def fuse_candidates(self, prob: dict, th=3.0):
+        """ORBmatcher::Fuse(pKF, vpMapPoints, th) search half; prob["frame"] is the KeyFrame."""
+        F, k1 = _orbt_frame(prob["frame"])
+        M, k2 = _orbt_map(prob["map"])
+        bi = np.zeros(max(M.n, 1), np.int32)
+        bd = np.zeros(max(M.n, 1), np.int32)
+        _check(lib().orbt_fuse_candidates(self._h, C.byref(F), C.byref(M), th, bi.ctypes.data, bd.ctypes.data),
+               "orbt_fuse_candidates")
+        return bi[: M.n], bd[: M.n]
+
+    def run_fuse_batch(self, n_slots: int, th=3.0, stream=None):
+        _check(lib().orbt_run_fuse_batch(self._h, n_slots, th, stream), "orbt_run_fuse_batch")
+
+    def fetch_fuse(self, slot: int, n_mp: int):
+        bi = np.zeros(max(n_mp, 1), np.int32)
+        bd = np.zeros(max(n_mp, 1), np.int32)
+        _check(lib().orbt_fetch_fuse(self._h, slot, bi.ctypes.data, bd.ctypes.data), "orbt_fetch_fuse")
+        return bi[:n_mp], bd[:n_mp]
 
     # batched device-resident path (bench.py)
     def reserve(self, n_slots: int, cap_kp: int, cap_mp: int):

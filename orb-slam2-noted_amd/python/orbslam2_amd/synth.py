@@ -340,7 +340,8 @@ def tracking_problem(seed: int = 5, n_kp: int = 2000, n_mp: int = 3000, W: int =
     kgen = np.array([kgen[i] for i in order], np.int64)
     frame = {"keys_un": keys, "u_right": kur, "desc": kdesc, "Tcw": Tcw, "Ow": Ow, "fx": fx, "fy": fy, "cx": cx,
              "cy": cy, "mbf": bf, "mb": mb, "min_x": 0.0, "max_x": float(W), "min_y": 0.0, "max_y": float(H),
-             "nlevels": nl, "log_scale_factor": np.float32(np.log(np.float32(1.2))), "scale_factors": sf}
+             "nlevels": nl, "log_scale_factor": np.float32(np.log(np.float32(1.2))), "scale_factors": sf,
+             "inv_level_sigma2": (np.float32(1) / (sf * sf)).astype(np.float32)}
     mp = {"Xw": Xw.astype(np.float32), "normal": nrm.astype(np.float32), "min_dist": mind.astype(np.float32),
           "max_dist": maxd.astype(np.float32), "desc": mdesc, "flags": flags}
     # last frame (motion model): the camera 1 m behind / ahead / in place along its optical axis
@@ -375,7 +376,7 @@ def tracking_problem(seed: int = 5, n_kp: int = 2000, n_mp: int = 3000, W: int =
     last = {"keys_un": lk, "u_right": np.full(nL, -1, np.float32), "desc": np.zeros((nL, 32), np.uint8),
             "Tcw": lTcw, "Ow": lOw, **{k: frame[k] for k in ("fx", "fy", "cx", "cy", "mbf", "mb", "min_x", "max_x",
                                                                "min_y", "max_y", "nlevels", "log_scale_factor",
-                                                               "scale_factors")}}
+                                                               "scale_factors", "inv_level_sigma2")}}
     last_out = (rng.random(nL) < 0.05).astype(np.uint8)
     kp_blocked = (rng.random(len(keys)) < 0.05).astype(np.uint8)
     return {"frame": frame, "map": mp, "last": last, "last_mp": last_mp, "last_outlier": last_out,

@@ -107,3 +107,28 @@ def test_crowd_fallback_rescan(tracker, oracle_mod):
         nm_r, own_r = oracle_mod.search_by_projection_frame(p, th=15.0, check_ori=ori)
         nm_g, own_g = tracker.search_by_projection_frame(p, th=15.0, check_ori=ori)
         assert nm_g == nm_r and np.array_equal(own_g, own_r)
+
+
+@pytest.mark.parametrize("seed,n_kp,n_mp,th", [(31, 2000, 3000, 3.0), (32, 1000, 1500, 3.0), (33, 4000, 6000, 5.0),
+                                               (34, 300, 200, 1.0)])
+def test_fuse_candidates(tracker, oracle_mod, seed, n_kp, n_mp, th):
+    """ORBmatcher::Fuse(pKF, vpMapPoints, th) search half (ORBmatcher.cc:1139-1240)."""
+    p = synth.tracking_problem(seed, n_kp=n_kp, n_mp=n_mp)
+    bi_r, bd_r = oracle_mod.fuse_candidates(p, th)
+    bi_g, bd_g = tracker.fuse_candidates(p, th)
+    assert np.array_equal(bi_g, bi_r) and np.array_equal(bd_g, bd_r)
+    assert (bd_r <= 50).sum() > 20
+
+
+def test_fuse_batched(amd, oracle_mod):
+    t = amd.Tracker()
+    probs = [synth.tracking_problem(40 + s, n_kp=1200 + 100 * s, n_mp=1500 + 200 * s) for s in range(5)]
+    t.reserve(len(probs), 1700, 2500)
+    for s, p in enumerate(probs):
+        t.stage(s, p)
+    t.run_fuse_batch(len(probs), 3.0)
+    for s, p in enumerate(probs):
+        bi, bd = t.fetch_fuse(s, len(p["map"]["Xw"]))
+        bi_r, bd_r = oracle_mod.fuse_candidates(p, 3.0)
+        assert np.array_equal(bi, bi_r) and np.array_equal(bd, bd_r)
+    t.close()
