@@ -29,6 +29,11 @@ CASES = [
     ("kitti_sse", 376, 1241, 2000, 1, 5),
     ("tum", 480, 640, 1000, 0, 3),
     ("tum_b", 480, 640, 1000, 0, 11),
+    ("kitti_04", 370, 1226, 2000, 0, 21),    # KITTI04-12.yaml resolution
+    ("euroc", 480, 752, 1200, 0, 22),        # EuRoC.yaml
+    ("qvga", 240, 320, 500, 0, 23),
+    ("fullhd", 1080, 1920, 4000, 0, 24),
+    ("odd", 333, 517, 800, 1, 25),
 ]
 
 
