@@ -16,6 +16,28 @@ namespace orbamd {
 
 __device__ __forceinline__ int cv_round_f(float v) { return (int)__builtin_rintf(v); }
 
+// XCD-aware workgroup remap (cdna_hip_programming.md §5.5 T1, bijective form). Workgroups are
+// dealt round-robin over the 8 XCDs (each with a private L2); remapping the linear id so every
+// XCD works one contiguous range of the grid keeps an image's pyramid / blurred pixels in one
+// L2 instead of eight. A pure speed choice: any placement gives the same results.
+__device__ __forceinline__ unsigned xcd_linear() {
+    const unsigned nwg = gridDim.x * gridDim.y * gridDim.z;
+    const unsigned orig = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const unsigned q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+__device__ __forceinline__ void xcd_remap2(int &bx, int &by) {
+    const unsigned w = xcd_linear();
+    bx = (int)(w % gridDim.x);
+    by = (int)(w / gridDim.x);
+}
+__device__ __forceinline__ void xcd_remap3(int &bx, int &by, int &bz) {
+    const unsigned w = xcd_linear();
+    bx = (int)(w % gridDim.x);
+    by = (int)((w / gridDim.x) % gridDim.y);
+    bz = (int)(w / (gridDim.x * gridDim.y));
+}
+
 __device__ __forceinline__ float fast_atan2_deg(float y, float x) {
     const float kR2D = (float)(180.0 / 3.1415926535897932384626433832795);
     const float p1 = 0.9997878412794807f * kR2D;

@@ -97,7 +97,7 @@ __device__ __forceinline__ int resize_px(int S0, int S1, int4 ry, bool simd) {
 __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, const int2 *cxt, const int4 *ryt,
                                                            const uint8_t *in, uint8_t *pyr) {
     const int dw = g.lw[l];
-    const int b = blockIdx.z, dy = blockIdx.y;
+    const int b = blockIdx.z, dy = blockIdx.y;   // streaming: the XCD remap measured no gain here
     const int dx0 = (blockIdx.x * 256 + threadIdx.x) * 4;
     if (dx0 >= dw) return;
     int sp;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     __shared__ uint32_t trowp[((FB_TH + 8) / 2) * FB_TW];
     __shared__ uint32_t mt[FB_TH * FB_TW / 4];
     __shared__ uint16_t clist[4][512];
-    const int b = blockIdx.y;
+    const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
     int t = blockIdx.x, l = 0;
     while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
     t -= g.blur_tile_base[l];
@@ -406,7 +406,9 @@ __global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const Cell
                                                        int *cell_cnt, uint32_t *cell_keys) {
     extern __shared__ uint32_t nms_lds[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c = blockIdx.x * 4 + wv, b = blockIdx.y;
+    int bxr, b;
+    xcd_remap2(bxr, b);
+    const int c = bxr * 4 + wv;
     if (c >= g.ncell_total) return;
     uint32_t *sm32 = nms_lds + wv * g.nms_wave_words;
     uint8_t *sm = (uint8_t *)sm32;
@@ -767,7 +769,9 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     unsigned char *qt_nodes, uint32_t *sel, int *sel_cnt) {
     extern __shared__ __align__(16) unsigned char qt_lds[];
     __shared__ QShared S;
-    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    int l, b;
+    xcd_remap2(l, b);
+    const int tid = threadIdx.x;
     const int cb0 = g.cell_base[l], ncell = g.cell_base[l + 1] - cb0;
     const int N = g.N[l], nIni = g.nIni[l];
     const int NC = g.node_cap, NP = g.node_pow2;
@@ -999,8 +1003,9 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
                                                        const uint32_t *sel, const int *sel_cnt,
                                                        orbx_kp *kps, uint8_t *desc, int *cnt) {
     const int lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int b = blockIdx.y;
+    int bxr, b;
+    xcd_remap2(bxr, b);
+    const int slot = bxr * 4 + (threadIdx.x >> 6);
     const int L = g.nlevels, cap = g.out_base[L];
     if (slot >= cap) return;
     int l = 0;

@@ -99,7 +99,9 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
                                                          const unsigned long long *sorted,
                                                          float *u_right, float *depth, int *sad) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int iL = blockIdx.x * 4 + wv, p = blockIdx.y;
+    int bxr, p;
+    xcd_remap2(bxr, p);
+    const int iL = bxr * 4 + wv;
     if (iL >= a.cap) return;
     const int imgL = a.L.img_base + a.L.img_step * p, imgR = a.R.img_base + a.R.img_step * p;
     const int nL = min(a.L.cnt[imgL], a.cap), nR = min(a.R.cnt[imgR], a.cap);
