@@ -13,7 +13,8 @@
 //   lba_syrk_mfma     Hpp - Y Y^T on FP64 matrix cores (v_mfma_f64_16x16x4f64), one wave per
 //                     16x16 upper tile per K slice, partial slabs reduced in fixed order
 //   lba_schur_reduce  Hschur = Hpp + lambda I - sum(slabs), b_schur = b_p - Y w
-//   lba_chol_small    dense Cholesky of the Schur matrix (6P <= 128) in LDS + two solves;
+//   lba_chol_tiled    dense Cholesky of the Schur matrix (6P <= 128) in LDS, 16-column panels
+//                     with FP64 MFMA trailing updates, + two solves;
 //   lba_chol_panel/_update/_solve_blocked  blocked Cholesky (MFMA trailing update) above
 //   lba_backsub       x_l = Dinv (b_l - Hpl^T x_p)
 //   lba_update        T <- exp(x_p) T (SE3Quat::exp, left-multiplied), X <- X + x_l
@@ -420,65 +421,198 @@ __global__ __launch_bounds__(256) void lba_schur_reduce(Graph g, double lambda) 
 // LinearSolverEigen's SimplicialLDLT, linear_solver_eigen.h:94-124; a non-positive pivot ->
 // ok = 0 and the LM trial is rejected, optimization_algorithm_levenberg.cpp:126-127).
 //
-// n6 <= kSmallNP: one 1024-thread workgroup, matrix in LDS, right-looking column sweep.
-// The scaled column j is copied to `col` so the rank-1 trailing update reads two broadcast
-// vectors; the update is spread over a 32 x 32 thread grid with fixed strides (no div/mod).
-// The two triangular solves run in wave 0 with the right-hand side in registers (lanes own
-// rows lane and lane + 64), the solved value broadcast by a cross-lane shuffle.
-__device__ inline double wave_bcast2(double v0, double v1, int k) {
-    const double a = __shfl(v0, k & 63), b = __shfl(v1, k & 63);
-    return (k < 64) ? a : b;
+// n6 <= kSmallNP: the Schur system [Hs bs; bs^T 0] (the right-hand side appended as row n,
+// padded to N2 = 16 * ceil((n + 1) / 16) with identity rows) factored in LDS by one
+// 512-thread workgroup, right-looking over 16-column panels:
+//   1. wave 0 factors the 16 x 16 diagonal tile in registers (lane i = row i; L[c][j] and the
+//      pivot are DPP row broadcasts, one reciprocal square root per column) and inverts it
+//      (lane c = column c of L_kk^-1, kept in LDS for the back substitution);
+//   2. the panel below, L_ik = A_ik L_kk^-T, on FP64 MFMA (v_mfma_f64_16x16x4f64), one wave
+//      per 16-row tile;
+//   3. the trailing lower tiles A_ij -= L_ik L_jk^T on FP64 MFMA, one wave per tile.
+// The appended row comes out as y^T with L y = bs (forward substitution for free); the back
+// substitution L^T x = y runs block by block: x_K = L_KK^-T y_K (wave 0), then every earlier
+// row subtracts L_K^T x_K in parallel. Rows >= n are treated as unit pivots. 3 barriers per
+// panel + 2 per back-substitution block.
+// value of lane C of each 16-lane row, v_mov_b32_dpp row_newbcast (no LDS, no SGPR trip)
+template <int C> __device__ __forceinline__ double row_bcast(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)b, 0x150 + C, 0xF, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(b >> 32), 0x150 + C, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-__global__ __launch_bounds__(1024) void lba_chol_small(Graph g) {
-    extern __shared__ double A[];   // n x ld
-    __shared__ double col[kSmallNP];
-    const int n = 6 * g.P, ld = n + 1, tid = threadIdx.x;
+template <int J, int C> __device__ __forceinline__ void chol16_update(double (&row)[16], double (&li)[16]) {
+    if constexpr (C < 16) {
+        const double l = row_bcast<C>(row[J]);   // L[C][J]
+        row[C] = __builtin_fma(-row[J], l, row[C]);
+        li[C] = __builtin_fma(-l, li[J], li[C]);
+        chol16_update<J, C + 1>(row, li);
+    }
+}
+
+// Lane i (of each 16-lane row) holds row i of the tile; column J is pivoted, scaled by the
+// reciprocal square root (v_rsq_f64 + 2 Newton steps) and subtracted from columns > J.
+// li carries column i of L^-1 by forward substitution, fed by the same broadcasts.
+// Pivots at J >= lim (rows >= n: padding and the appended right-hand side) are forced to 1.
+template <int J> __device__ __forceinline__ void chol16_factor(double (&row)[16], double (&li)[16], int i, int lim,
+                                                               bool &bad) {
+    if constexpr (J < 16) {
+        double d = row_bcast<J>(row[J]);
+        if (J >= lim) d = 1.0;
+        bad |= !(d > 0);
+        const double h = 0.5 * d;
+        double y = __builtin_amdgcn_rsq(d);
+        y = __builtin_fma(y, __builtin_fma(-(h * y), y, 0.5), y);
+        y = __builtin_fma(y, __builtin_fma(-(h * y), y, 0.5), y);
+        row[J] = i == J ? d * y : row[J] * y;
+        li[J] = (i == J ? 1.0 + li[J] : li[J]) * y;   // li[J] held -sum L[J][k] li[k]
+        chol16_update<J, J + 1>(row, li);
+        chol16_factor<J + 1>(row, li, i, lim, bad);
+    }
+}
+
+__host__ __device__ constexpr int chol_tiled_dim(int n) { return 16 * ((n + 16) / 16); }
+__host__ __device__ constexpr size_t chol_tiled_lds(int n) {
+    return sizeof(double) * ((size_t)chol_tiled_dim(n) * (chol_tiled_dim(n) + 1) + (size_t)(chol_tiled_dim(n) / 16) * 16 * 17 +
+                             2 * (size_t)chol_tiled_dim(n));
+}
+
+__global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
+    extern __shared__ double A[];   // N2 x LDA, then Linv[NT][16][17], y[N2], x[N2]
+    __shared__ int fail;
+    const int n = 6 * g.P, N2 = chol_tiled_dim(n), NT = N2 / 16, LDA = N2 + 1;
+    double *Linv = A + N2 * LDA, *yv = Linv + NT * 16 * 17, *xv = yv + N2;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const long long NP = g.NP;
-    for (int r = tid >> 5; r < n; r += 32)
-        for (int c = tid & 31; c <= r; c += 32) A[r * ld + c] = g.Hs[r * NP + c];
+#ifdef LBA_PROFILE
+    long long t_diag = 0, t_trsm = 0, t_trail = 0, t0 = clock64(), ta;
+#define LBA_T(acc) do { __syncthreads(); const long long tb = clock64(); acc += tb - ta; ta = tb; } while (0)
+#else
+#define LBA_T(acc) do {} while (0)
+#endif
+    // load: lower triangle of Hs, bs as row n, identity padding; 128 rows per pass (16 per
+    // wave, lanes along the row; N2 <= kSmallNP = 128), 32 loads in flight per thread
+    for (int rb = 0; rb < N2; rb += 128) {
+        double v[16][2];
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int r = rb + wv + 8 * u, c = lane + 64 * h;
+                v[u][h] = 0.0;
+                if (r < N2 && c <= r) {
+                    if (r < n) v[u][h] = g.Hs[r * NP + c];
+                    else if (r == n) v[u][h] = c < n ? g.bs[c] : 0.0;
+                    else v[u][h] = r == c ? 1.0 : 0.0;
+                }
+            }
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int r = rb + wv + 8 * u, c = lane + 64 * h;
+                if (r < N2 && c <= r) A[r * LDA + c] = v[u][h];
+            }
+    }
+    if (tid == 0) fail = 0;
     __syncthreads();
-    const int ty = tid >> 5, tx = tid & 31;
-    for (int j = 0; j < n; j++) {
-        const double d = A[j * ld + j];
-        if (!(d > 0)) {                 // uniform: every thread read the same value
+#ifdef LBA_PROFILE
+    const long long t_load = clock64() - t0;
+    ta = clock64();
+#endif
+    for (int K = 0; K < NT; K++) {
+        const int k0 = 16 * K;
+        double *LK = Linv + K * 16 * 17;
+        if (wv == 0) {   // 1. diagonal tile: factor + inverse
+            const int i = lane & 15;
+            double row[16], li[16];   // li: column i of L_kk^-1
+#pragma unroll
+            for (int c = 0; c < 16; c++) row[c] = c <= i ? A[(k0 + i) * LDA + k0 + c] : 0.0;
+#pragma unroll
+            for (int r = 0; r < 16; r++) li[r] = 0.0;
+            bool bad = false;
+            chol16_factor<0>(row, li, i, n - k0, bad);
+            // every 16-lane row computed the same tile: all lanes store (same values), so the
+            // compiler cannot sink the li chain into a lane < 16 branch and keep every
+            // broadcast live until there
+#pragma unroll
+            for (int c = 0; c < 16; c++) A[(k0 + i) * LDA + k0 + c] = row[c];
+#pragma unroll
+            for (int r = 0; r < 16; r++) LK[r * 17 + i] = li[r];
+            if (lane == 0 && bad) fail = 1;
+        }
+        __syncthreads();
+        LBA_T(t_diag);
+        if (fail) {   // uniform after the barrier
             if (tid == 0) g.scalars[4] = 0;
             return;
         }
-        const double ljj = sqrt(d);
-        for (int i = j + 1 + tid; i < n; i += 1024) {
-            const double v = A[i * ld + j] / ljj;
-            A[i * ld + j] = v;
-            col[i] = v;
+        const int r0 = k0 + 16, m = NT - K - 1;
+        for (int I = wv; I < m; I += 8) {   // 2. panel: L_ik = A_ik L_kk^-T
+            const int ri = r0 + 16 * I;
+            double4_t acc = {0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 16; kk += 4) {
+                const double a = A[(ri + (lane & 15)) * LDA + k0 + kk + (lane >> 4)];
+                const double b = LK[(lane & 15) * 17 + kk + (lane >> 4)];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) A[(ri + (lane >> 4) + 4 * q) * LDA + k0 + (lane & 15)] = acc[q];
         }
         __syncthreads();
-        if (tid == 0) A[j * ld + j] = ljj;
-        for (int r = j + 1 + ty; r < n; r += 32) {
-            const double lr = col[r];
-            for (int c = j + 1 + tx; c <= r; c += 32) A[r * ld + c] -= lr * col[c];
+        LBA_T(t_trsm);
+        const int ntile = m * (m + 1) / 2;
+        for (int t = wv; t < ntile; t += 8) {   // 3. trailing lower tiles
+            int I = 0, u = t;
+            while (u > I) { u -= I + 1; I++; }
+            const int J = u;
+            const int ri = r0 + 16 * I, cj = r0 + 16 * J;
+            double4_t acc;
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc[q] = A[(ri + (lane >> 4) + 4 * q) * LDA + cj + (lane & 15)];
+#pragma unroll
+            for (int kk = 0; kk < 16; kk += 4) {
+                const double a = -A[(ri + (lane & 15)) * LDA + k0 + kk + (lane >> 4)];
+                const double b = A[(cj + (lane & 15)) * LDA + k0 + kk + (lane >> 4)];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) A[(ri + (lane >> 4) + 4 * q) * LDA + cj + (lane & 15)] = acc[q];
+        }
+        __syncthreads();
+        LBA_T(t_trail);
+    }
+#ifdef LBA_PROFILE
+    const long long ts = clock64();
+#endif
+    // back substitution L^T x = y, y = row n of the factor
+    for (int j = tid; j < n; j += 512) yv[j] = A[n * LDA + j];
+    __syncthreads();
+    for (int K = (n - 1) / 16; K >= 0; K--) {
+        const int k0 = 16 * K, kn = min(16, n - k0);
+        if (tid < kn) {   // x_K = L_KK^-T y_K over the rows < n
+            const double *LK = Linv + K * 16 * 17;
+            double s = 0.0;
+            for (int r = tid; r < kn; r++) s += LK[r * 17 + tid] * yv[k0 + r];
+            xv[k0 + tid] = s;
+        }
+        __syncthreads();
+        for (int j = tid; j < k0; j += 512) {
+            double s = yv[j];
+            for (int k = 0; k < kn; k++) s -= A[(k0 + k) * LDA + j] * xv[k0 + k];
+            yv[j] = s;
         }
         __syncthreads();
     }
-    if (tid >= 64) return;
-    const int lane = tid;
-    double y0 = lane < n ? g.bs[lane] : 0.0, y1 = lane + 64 < n ? g.bs[lane + 64] : 0.0;
-    for (int k = 0; k < n; k++) {       // L y = b
-        const double yk = wave_bcast2(y0, y1, k) / A[k * ld + k];
-        if (lane == k) y0 = yk;
-        else if (lane > k && lane < n) y0 -= A[lane * ld + k] * yk;
-        if (lane + 64 == k) y1 = yk;
-        else if (lane + 64 > k && lane + 64 < n) y1 -= A[(lane + 64) * ld + k] * yk;
-    }
-    for (int k = n - 1; k >= 0; k--) {  // L^T x = y
-        const double xk = wave_bcast2(y0, y1, k) / A[k * ld + k];
-        if (lane == k) y0 = xk;
-        else if (lane < k) y0 -= A[k * ld + lane] * xk;
-        if (lane + 64 == k) y1 = xk;
-        else if (lane + 64 < k) y1 -= A[k * ld + lane + 64] * xk;
-    }
-    if (lane < n) g.x[lane] = y0;
-    if (lane + 64 < n) g.x[lane + 64] = y1;
-    if (lane == 0) g.scalars[4] = 1;
+    for (int j = tid; j < n; j += 512) g.x[j] = xv[j];
+    if (tid == 0) g.scalars[4] = 1;
+#ifdef LBA_PROFILE
+    if (tid == 0)
+        printf("LBAPROF n=%d load=%lld diag=%lld trsm=%lld trail=%lld solve=%lld\n", n, t_load, t_diag, t_trsm, t_trail,
+               clock64() - ts);
+#endif
 }
 
 // n6 > kSmallNP: blocked right-looking Cholesky in place on Hs (lower triangle), panel
@@ -816,7 +950,7 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
                 lba_syrk_mfma<<<dim3(npair, g.S), 64, 0, s>>>(g, ntile, kchunk);
                 lba_schur_reduce<<<n6, 256, 0, s>>>(g, lambda);
                 if (n6 <= kSmallNP) {
-                    lba_chol_small<<<1, 1024, sizeof(double) * n6 * (n6 + 1), s>>>(g);
+                    lba_chol_tiled<<<1, 512, chol_tiled_lds(n6), s>>>(g);
                 } else {
                     lba_set_ok<<<1, 1, 0, s>>>(g);
                     for (int kb = 0; kb < n6; kb += kCB) {
