@@ -6,21 +6,25 @@
 //                     3x9 Jacobians, per-edge quadratic-form pieces (Hpl block kept)
 //   lba_reduce_points one thread per landmark: Hll (3x3), b_l  (edges of a point are a CSR
 //                     segment -> deterministic order)
-//   lba_reduce_poses  one workgroup per free pose: Hpp (6x6), b_p tree reduction
-// per LM trial:
-//   lba_schur_points  one thread per landmark: Dinv = (Hll + lambda I)^-1 (Eigen cofactor
-//                     inverse), L = chol(Dinv), Y_l = Hpl_l L, w_l = L^T b_l
-//   lba_syrk_mfma     Hpp - Y Y^T on FP64 matrix cores (v_mfma_f64_16x16x4f64), one wave per
-//                     16x16 upper tile per K slice, partial slabs reduced in fixed order
-//   lba_schur_reduce  Hschur = Hpp + lambda I - sum(slabs), b_schur = b_p - Y w
-//   lba_chol_tiled    dense Cholesky of the Schur matrix (6P <= 128) in LDS, 16-column panels
-//                     with FP64 MFMA trailing updates, + two solves;
-//   lba_chol_panel/_update/_solve_blocked  blocked Cholesky (MFMA trailing update) above
-//   lba_backsub       x_l = Dinv (b_l - Hpl^T x_p)
-//   lba_update        T <- exp(x_p) T (SE3Quat::exp, left-multiplied), X <- X + x_l
-//   lba_errors        trial residuals (kept as g2o's stale _error) + robust chi2 + scale
+//   lba_reduce_poses  one 1024-thread workgroup per free pose: Hpp (6x6), b_p, fixed-order sums
+// per LM trial (6 kernels for 6P <= 128):
+//   lba_prep_slots    finishes the linearisation's chi2 / maxDiagonal reductions (first lambda
+//                     on the device); one thread per active edge: its 6x3 block of Y = Hpl L
+//                     with L = chol(Dinv); one thread per landmark: Dinv = (Hll + lambda I)^-1
+//                     (Eigen cofactor inverse), w_l = L^T b_l
+//   lba_syrk_mfma     Y [Y; w]^T on FP64 matrix cores (v_mfma_f64_16x16x4f64), Y stored
+//                     transposed, one 4-wave workgroup per 16x16 upper tile per K slice,
+//                     partial slabs reduced in fixed order
+//   lba_schur_reduce  Hschur = Hpp + lambda I - sum(slabs), b_schur = b_p - Y w (one workgroup
+//                     per row: the 1.2 MB of slabs is read by n6 CUs, not one)
+//   lba_chol_tiled    (6P <= 128) dense Cholesky in LDS over 16-column panels (DPP diagonal
+//                     tiles, FP64 MFMA panel / trailing updates) + the two solves
+//   lba_chol_panel/_update/_solve_blocked  blocked Cholesky for 6P > 128
+//   lba_update        x_l = Dinv (b_l - Hpl^T x_p), T <- exp(x_p) T (SE3Quat::exp,
+//                     left-multiplied), X <- X + x_l, computeScale block sums
+//   lba_errors        trial residuals (kept as g2o's stale _error) + robust chi2 block sums
 // The LM accept/reject/lambda logic (optimization_algorithm_levenberg.cpp:61-164) runs on
-// the host with one 3-double readback per trial.
+// the host with one readback per trial (flags + the block sums, summed in block order).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -76,21 +80,24 @@ struct Graph {
     int P, Lm;
     const int *pt_start, *pt_items;  // per active point: active slots (all edges of the point)
     const int *ps_start, *ps_items;  // per free pose: active slots
+    const int *slot_pt, *slot_ph;    // per active slot: hessian point / pose index (-1 fixed)
     // system
     double *con;           // [nact][36] per-slot Hll(6) bl(3) Hpp(21) bp(6)
     double *hpl;           // [nact][18]
     double *Hll, *bl;      // [Lm][9], [Lm][3]
     double *Hpp, *bp;      // [P][36], [P][6]
     double *Dinv;          // [Lm][9]
-    double *Y;             // [NP][Kpad] row-major
-    double *w;             // [Kpad]
-    double *slab;          // [S][NP][NP]
+    double *Lc;            // [Lm][6] chol(Dinv): L00 L10 L20 L11 L21 L22
+    double *Y;             // [Kpad][NPW] (point columns major: Y^T); column wrow = w
+    double *w;             // = Y + wrow, stride NPW
+    double *slab;          // [S][NP][NPW], NPW = NP + 16 (column wrow: partial Y w)
     double *Hs, *bs;       // [NP][NP], [NP]
     double *x;             // [6P + 3Lm]
     double *partial;       // [4][kRedBlocks]
-    double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok
+    double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok, lambda
     int Kpad, S;
     int NP;                // Schur dimension 6P padded to a multiple of kCB
+    int NPW, wrow;         // slab leading dimension; Y row holding w (16 * ceil(6P / 16))
 };
 
 __device__ inline void edge_error(const Graph &g, const EdgeDev &e, const Pose *T, const double *X, double err[3]) {
@@ -233,10 +240,18 @@ __global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
     double dmax = 0;
     if (l < g.Lm) {
         double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-        for (int i = g.pt_start[l]; i < g.pt_start[l + 1]; i++) {
-            const double *c = g.con + (long long)g.pt_items[i] * 36;
-            for (int k = 0; k < 6; k++) h[k] += c[k];
-            for (int k = 0; k < 3; k++) b[k] += c[6 + k];
+        const int i0 = g.pt_start[l], i1 = g.pt_start[l + 1];
+        for (int i = i0; i < i1; i += 4) {   // 4 slot indices in flight, summed in order
+            int sl[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) sl[u] = i + u < i1 ? g.pt_items[i + u] : -1;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (sl[u] < 0) continue;
+                const double *c = g.con + (long long)sl[u] * 36;
+                for (int k = 0; k < 6; k++) h[k] += c[k];
+                for (int k = 0; k < 3; k++) b[k] += c[6 + k];
+            }
         }
         double *H = g.Hll + 9 * l;
         H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
@@ -255,63 +270,46 @@ __global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
     if (threadIdx.x == 0) g.partial[kRedBlocks + blockIdx.x] = sh[0];
 }
 
-__global__ __launch_bounds__(256) void lba_reduce_poses(Graph g) {
-    const int i = blockIdx.x;
-    double acc[27];
-    for (int k = 0; k < 27; k++) acc[k] = 0;
-    for (int t = g.ps_start[i] + (int)threadIdx.x; t < g.ps_start[i + 1]; t += 256) {
-        const double *c = g.con + (long long)g.ps_items[t] * 36 + 9;
-        for (int k = 0; k < 27; k++) acc[k] += c[k];
+// one 1024-thread workgroup per free pose: 32 slot groups x 32 lanes, lane k < 27 of a group
+// accumulates component k (Hpp upper 21 + b_p 6) of every 32nd slot, coalesced 216-byte slot
+// reads; the 32 group partials are summed in LDS in fixed order
+__global__ __launch_bounds__(1024) void lba_reduce_poses(Graph g) {
+    const int i = blockIdx.x, k = threadIdx.x & 31, grp = threadIdx.x >> 5;
+    const int t0 = g.ps_start[i], t1 = g.ps_start[i + 1];
+    double acc = 0;
+    if (k < 27) {
+        int t = t0 + grp;
+        for (; t + 96 < t1; t += 128) {   // 4 slots in flight
+            const int s0 = g.ps_items[t], s1 = g.ps_items[t + 32], s2 = g.ps_items[t + 64], s3 = g.ps_items[t + 96];
+            const double v0 = g.con[(long long)s0 * 36 + 9 + k], v1 = g.con[(long long)s1 * 36 + 9 + k];
+            const double v2 = g.con[(long long)s2 * 36 + 9 + k], v3 = g.con[(long long)s3 * 36 + 9 + k];
+            acc += v0; acc += v1; acc += v2; acc += v3;
+        }
+        for (; t < t1; t += 32) acc += g.con[(long long)g.ps_items[t] * 36 + 9 + k];
     }
-    __shared__ double sh[27][256];
-    for (int k = 0; k < 27; k++) sh[k][threadIdx.x] = acc[k];
+    __shared__ double sh[32][33];
+    sh[grp][k] = acc;
     __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s)
-            for (int k = 0; k < 27; k++) sh[k][threadIdx.x] += sh[k][threadIdx.x + s];
-        __syncthreads();
+    if (threadIdx.x < 27) {
+        double v = 0;
+        for (int q = 0; q < 32; q++) v += sh[q][threadIdx.x];
+        sh[0][threadIdx.x] = v;   // row 0 entry threadIdx.x is read only by this thread above
     }
+    __syncthreads();
     if (threadIdx.x < 36) {
         const int a = threadIdx.x / 6, b = threadIdx.x % 6;
         const int lo = min(a, b), hi = max(a, b);
         const int u = lo * 6 - lo * (lo - 1) / 2 + (hi - lo);   // packed upper index
-        g.Hpp[36 * i + threadIdx.x] = sh[u][0];
+        g.Hpp[36 * i + threadIdx.x] = sh[0][u];
     }
-    if (threadIdx.x < 6) g.bp[6 * i + threadIdx.x] = sh[21 + threadIdx.x][0];
+    if (threadIdx.x < 6) g.bp[6 * i + threadIdx.x] = sh[0][21 + threadIdx.x];
     if (threadIdx.x == 0) {
         double m = 0;
         for (int a = 0; a < 6; a++) {
             const int u = a * 6 - a * (a - 1) / 2;
-            m = fmax(m, fabs(sh[u][0]));
+            m = fmax(m, fabs(sh[0][u]));
         }
         g.partial[2 * kRedBlocks + i] = m;
-    }
-}
-
-// final scalar reductions: mode 0 -> chi2 (sum) + maxdiag (max); mode 1 -> tempChi + scale
-__global__ __launch_bounds__(256) void lba_finish(Graph g, int mode, int n0, int n1, int n2) {
-    __shared__ double sa[256], sb[256];
-    double a = 0, b = 0;
-    for (int i = threadIdx.x; i < n0; i += 256) a += g.partial[i];
-    if (mode == 0) {
-        for (int i = threadIdx.x; i < n1; i += 256) b = fmax(b, g.partial[kRedBlocks + i]);
-        for (int i = threadIdx.x; i < n2; i += 256) b = fmax(b, g.partial[2 * kRedBlocks + i]);
-    } else {
-        for (int i = threadIdx.x; i < n1; i += 256) b += g.partial[kRedBlocks + i];
-    }
-    sa[threadIdx.x] = a;
-    sb[threadIdx.x] = b;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            sa[threadIdx.x] += sa[threadIdx.x + s];
-            sb[threadIdx.x] = mode == 0 ? fmax(sb[threadIdx.x], sb[threadIdx.x + s]) : sb[threadIdx.x] + sb[threadIdx.x + s];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        if (mode == 0) { g.scalars[0] = sa[0]; g.scalars[1] = sb[0]; }
-        else { g.scalars[2] = sa[0]; g.scalars[3] = sb[0]; }
     }
 }
 
@@ -327,89 +325,133 @@ __device__ inline void inv3(const double m[9], double o[9]) {
     o[6] = c20 * id; o[7] = (m[1] * m[6] - m[0] * m[7]) * id; o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
 }
 
-__global__ __launch_bounds__(256) void lba_schur_points(Graph g, double lambda) {
-    const int l = blockIdx.x * 256 + threadIdx.x;
-    if (l >= g.Lm) return;
+// (Hll + lambda I)^-1 (Eigen cofactor inverse) and L = chol(Dinv) of one landmark
+__device__ inline void point_factor(const Graph &g, int l, double lambda, double Di[9], double L[6]) {
     double D[9];
     for (int k = 0; k < 9; k++) D[k] = g.Hll[9 * l + k];
     D[0] += lambda; D[4] += lambda; D[8] += lambda;
-    double Di[9];
     inv3(D, Di);
-    for (int k = 0; k < 9; k++) g.Dinv[9 * l + k] = Di[k];
     // Dinv = L L^T (symmetrised)
     const double a00 = Di[0], a10 = 0.5 * (Di[3] + Di[1]), a11 = Di[4];
     const double a20 = 0.5 * (Di[6] + Di[2]), a21 = 0.5 * (Di[7] + Di[5]), a22 = Di[8];
-    const double L00 = sqrt(a00), L10 = a10 / L00, L20 = a20 / L00;
-    const double L11 = sqrt(a11 - L10 * L10), L21 = (a21 - L20 * L10) / L11;
-    const double L22 = sqrt(a22 - L20 * L20 - L21 * L21);
-    const double *b = g.bl + 3 * l;
-    const long long K = g.Kpad, c0 = 3LL * l;
-    g.w[c0] = L00 * b[0] + L10 * b[1] + L20 * b[2];
-    g.w[c0 + 1] = L11 * b[1] + L21 * b[2];
-    g.w[c0 + 2] = L22 * b[2];
-    for (int i = g.pt_start[l]; i < g.pt_start[l + 1]; i++) {
-        const int s = g.pt_items[i];
-        const int ph = g.pose_hidx[g.E[g.act[s]].pose];
-        if (ph < 0) continue;
-        const double *B = g.hpl + (long long)s * 18;
+    L[0] = sqrt(a00); L[1] = a10 / L[0]; L[2] = a20 / L[0];
+    L[3] = sqrt(a11 - L[1] * L[1]); L[4] = (a21 - L[2] * L[1]) / L[3];
+    L[5] = sqrt(a22 - L[2] * L[2] - L[4] * L[4]);
+}
+
+// First kernel of an LM trial (setLambda + the landmark half of the Schur complement).
+// Threads [0, nact): the 6x3 block Y = Hpl L of one active edge (its pose's rows, its point's
+// columns of Y^T); threads [nact, nact + Lm): Dinv and w = L^T b_l of one landmark. The edge
+// threads refactor their landmark (same arithmetic, so the same bits) instead of waiting for
+// a separate landmark pass.
+// mode 1: block 0 also finishes the linearisation's chi2 reduction -> scalars[0];
+// mode 2 (first trial of the first iteration): every block reduces chi2 and maxDiagonal and
+// uses lambda = tau * maxDiagonal (tau = 1e-5, optimization_algorithm_levenberg.cpp:179-191);
+// otherwise lambda = lambda_arg. Block 0 publishes lambda in scalars[5].
+__global__ __launch_bounds__(256) void lba_prep_slots(Graph g, double lambda_arg, int mode, int n0, int n1, int n2) {
+    double lambda = lambda_arg;
+    if (mode == 2 || (mode == 1 && blockIdx.x == 0)) {   // uniform per block
+        __shared__ double sa[256], sb[256];
+        double a = 0, b = 0;
+        for (int i = threadIdx.x; i < n0; i += 256) a += g.partial[i];
+        for (int i = threadIdx.x; i < n1; i += 256) b = fmax(b, g.partial[kRedBlocks + i]);
+        for (int i = threadIdx.x; i < n2; i += 256) b = fmax(b, g.partial[2 * kRedBlocks + i]);
+        sa[threadIdx.x] = a;
+        sb[threadIdx.x] = b;
+        __syncthreads();
+        for (int s = 128; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) {
+                sa[threadIdx.x] += sa[threadIdx.x + s];
+                sb[threadIdx.x] = fmax(sb[threadIdx.x], sb[threadIdx.x + s]);
+            }
+            __syncthreads();
+        }
+        if (mode == 2) lambda = 1e-5 * sb[0];
+        if (blockIdx.x == 0 && threadIdx.x == 0) { g.scalars[0] = sa[0]; g.scalars[1] = sb[0]; }
+    }
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t == 0) g.scalars[5] = lambda;
+    const long long W = g.NPW;
+    double Di[9], L[6];
+    if (t < g.nact) {
+        const int ph = g.slot_ph[t];
+        if (ph < 0) return;
+        const int l = g.slot_pt[t];
+        point_factor(g, l, lambda, Di, L);
+        const double *B = g.hpl + (long long)t * 18;
+        double *y = g.Y + 3LL * l * W + 6 * ph;   // Y^T rows 3l..3l+2, columns 6ph..6ph+5
+#pragma unroll
         for (int r = 0; r < 6; r++) {
             const double b0 = B[3 * r], b1 = B[3 * r + 1], b2 = B[3 * r + 2];
-            double *yr = g.Y + (long long)(6 * ph + r) * K + c0;
-            yr[0] = b0 * L00 + b1 * L10 + b2 * L20;
-            yr[1] = b1 * L11 + b2 * L21;
-            yr[2] = b2 * L22;
+            y[r] = b0 * L[0] + b1 * L[1] + b2 * L[2];
+            y[W + r] = b1 * L[3] + b2 * L[4];
+            y[2 * W + r] = b2 * L[5];
         }
+    } else if (t < g.nact + g.Lm) {
+        const int l = t - g.nact;
+        point_factor(g, l, lambda, Di, L);
+        for (int k = 0; k < 9; k++) g.Dinv[9 * l + k] = Di[k];
+        const double *b = g.bl + 3 * l;
+        const long long c0 = 3LL * l;
+        g.w[c0 * W] = L[0] * b[0] + L[1] * b[1] + L[2] * b[2];
+        g.w[(c0 + 1) * W] = L[3] * b[1] + L[4] * b[2];
+        g.w[(c0 + 2) * W] = L[5] * b[2];
     }
 }
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
-// Y Y^T on FP64 MFMA: one wave per (upper tile pair, K slice); slab[s] = partial tile sums
-__global__ __launch_bounds__(64) void lba_syrk_mfma(Graph g, int ntile, int kchunk) {
-    const int lane = threadIdx.x;
+// Y [Y; w]^T on FP64 MFMA: one 4-wave workgroup per (upper tile pair, K slice), the waves
+// interleaving 4-column steps of the slice and summing in LDS; slab[s] = partial tile sums.
+// Tile pairs run over ntile + 1 tile rows (the last one holds w) without the (w, w) tile.
+__global__ __launch_bounds__(256) void lba_syrk_mfma(Graph g, int ntile1, int kchunk) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int pair = blockIdx.x, I = 0;
-    while (pair >= ntile - I) { pair -= ntile - I; I++; }
+    while (pair >= ntile1 - I) { pair -= ntile1 - I; I++; }
     const int J = I + pair;
     const int s = blockIdx.y;
-    const long long K = g.Kpad;
+    const long long K = g.Kpad, W = g.NPW;
     const int k0 = s * kchunk, k1 = min((int)K, k0 + kchunk);
-    const double *ya = g.Y + (long long)(16 * I + (lane & 15)) * K;
-    const double *yb = g.Y + (long long)(16 * J + (lane & 15)) * K;
+    // Y^T layout: one load instruction = 4 k-rows x 16 consecutive columns (4 full lines)
+    const double *ya = g.Y + 16 * I + (lane & 15) + (lane >> 4) * W;
+    const double *yb = g.Y + 16 * J + (lane & 15) + (lane >> 4) * W;
     double4_t acc = {0, 0, 0, 0};
-    for (int kk = k0; kk < k1; kk += 4) {  // (k1 - k0) % 4 == 0: every lane runs every step
-        const int k = kk + (lane >> 4);
-        const double a = ya[k], b = yb[k];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    int kk = k0 + 4 * wv;   // K % 4 == 0: every lane runs every step
+    for (; kk + 48 < k1; kk += 64) {   // 4 steps (8 loads) in flight
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) { a[u] = ya[(kk + 16 * u) * W]; b[u] = yb[(kk + 16 * u) * W]; }
+#pragma unroll
+        for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
     }
-    const long long NP = g.NP;
-    double *out = g.slab + (long long)s * NP * NP;
+    for (; kk < k1; kk += 16) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[kk * W], yb[kk * W], acc, 0, 0, 0);
+    __shared__ double red[3][4][64];
+    if (wv > 0)
+        for (int r = 0; r < 4; r++) red[wv - 1][r][lane] = acc[r];
+    __syncthreads();
+    if (wv > 0) return;
+    const long long NPW = g.NPW;
+    double *out = g.slab + (long long)s * g.NP * NPW;
     // C/D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * reg
     for (int r = 0; r < 4; r++) {
         const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
-        out[(long long)row * NP + col] = acc[r];
+        out[(long long)row * NPW + col] = ((acc[r] + red[0][r][lane]) + red[1][r][lane]) + red[2][r][lane];
     }
 }
-
-__global__ __launch_bounds__(256) void lba_schur_reduce(Graph g, double lambda) {
+__global__ __launch_bounds__(256) void lba_schur_reduce(Graph g) {
+    const double lambda = g.scalars[5];
     const int n6 = 6 * g.P;
     const int r = blockIdx.x;  // row
-    const long long K = g.Kpad, NP = g.NP;
-    // b_schur[r] = b_p[r] - (Y w)[r]
-    __shared__ double sh[256];
-    double acc = 0;
-    const double *yr = g.Y + (long long)r * K;
-    for (long long k = threadIdx.x; k < K; k += 256) acc += yr[k] * g.w[k];
-    sh[threadIdx.x] = acc;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
-        __syncthreads();
+    const long long NP = g.NP, NPW = g.NPW, SL = NP * NPW;
+    if (threadIdx.x == 0) {   // b_schur[r] = b_p[r] - (Y w)[r]
+        double v = 0;
+        for (int s = 0; s < g.S; s++) v += g.slab[s * SL + (long long)r * NPW + g.wrow];
+        g.bs[r] = g.bp[r] - v;
     }
-    if (threadIdx.x == 0) g.bs[r] = g.bp[r] - sh[0];
     for (int c = threadIdx.x; c < n6; c += 256) {
         const int lo = min(r, c), hi = max(r, c);   // slabs hold upper tiles
         double v = 0;
-        for (int s = 0; s < g.S; s++) v += g.slab[(long long)s * NP * NP + (long long)lo * NP + hi];
+        for (int s = 0; s < g.S; s++) v += g.slab[s * SL + (long long)lo * NPW + hi];
         double h = 0;
         if (r / 6 == c / 6) h = g.Hpp[36 * (r / 6) + 6 * (r % 6) + (c % 6)];
         if (r == c) h += lambda;
@@ -484,13 +526,13 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
     const int n = 6 * g.P, N2 = chol_tiled_dim(n), NT = N2 / 16, LDA = N2 + 1;
     double *Linv = A + N2 * LDA, *yv = Linv + NT * 16 * 17, *xv = yv + N2;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const long long NP = g.NP;
 #ifdef LBA_PROFILE
     long long t_diag = 0, t_trsm = 0, t_trail = 0, t0 = clock64(), ta;
 #define LBA_T(acc) do { __syncthreads(); const long long tb = clock64(); acc += tb - ta; ta = tb; } while (0)
 #else
 #define LBA_T(acc) do {} while (0)
 #endif
+    const long long NP = g.NP;
     // load: lower triangle of Hs, bs as row n, identity padding; 128 rows per pass (16 per
     // wave, lanes along the row; N2 <= kSmallNP = 128), 32 loads in flight per thread
     for (int rb = 0; rb < N2; rb += 128) {
@@ -747,45 +789,52 @@ __global__ __launch_bounds__(1024) void lba_chol_solve_blocked(Graph g) {
 
 __global__ void lba_set_ok(Graph g) { g.scalars[4] = 1; }
 
-__global__ __launch_bounds__(256) void lba_backsub(Graph g) {
-    const int l = blockIdx.x * 256 + threadIdx.x;
-    if (l >= g.Lm) return;
-    double c[3] = {g.bl[3 * l], g.bl[3 * l + 1], g.bl[3 * l + 2]};
-    for (int i = g.pt_start[l]; i < g.pt_start[l + 1]; i++) {
-        const int s = g.pt_items[i];
-        const int ph = g.pose_hidx[g.E[g.act[s]].pose];
-        if (ph < 0) continue;
-        const double *B = g.hpl + (long long)s * 18;
-        const double *xp = g.x + 6 * ph;
-        for (int cc = 0; cc < 3; cc++) {
-            double v = 0;
-            for (int a = 0; a < 6; a++) v += B[3 * a + cc] * (-xp[a]);
-            c[cc] += v;
-        }
-    }
-    const double *Di = g.Dinv + 9 * l;
-    double *xl = g.x + 6 * g.P + 3 * l;
-    for (int a = 0; a < 3; a++) xl[a] = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
-}
-
-__global__ __launch_bounds__(256) void lba_update(Graph g, double lambda, const double *b_full) {
+// landmark back substitution x_l = Dinv (b_l - Hpl^T x_p) fused with the update
+// T <- exp(x_p) T (SE3Quat::exp, left-multiplied), X <- X + x_l into the trial buffers and the
+// computeScale pieces x (lambda x + b) of the thread's own entries, block sums -> part[]
+__global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
     const int t = blockIdx.x * 256 + threadIdx.x;
+    const double lambda = g.scalars[5];
     double sc = 0;
     if (t < g.P) {
         const int v = g.hpose[t];
-        g.T2[v] = pose_oplus(g.T[v], g.x + 6 * t);
+        const double *xp = g.x + 6 * t;
+        g.T2[v] = pose_oplus(g.T[v], xp);
+        for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + g.bp[6 * t + k]);
     } else if (t < g.P + g.Lm) {
         const int l = t - g.P, v = g.hpoint[l];
-        const double *dx = g.x + 6 * g.P + 3 * l;
-        for (int k = 0; k < 3; k++) g.X2[3 * v + k] = g.X[3 * v + k] + dx[k];
+        double c[3] = {g.bl[3 * l], g.bl[3 * l + 1], g.bl[3 * l + 2]};
+        const int i0 = g.pt_start[l], i1 = g.pt_start[l + 1];
+        for (int i = i0; i < i1; i += 4) {   // 4 edges' index chains in flight, applied in order
+            int sl[4], ph[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) sl[u] = i + u < i1 ? g.pt_items[i + u] : -1;
+#pragma unroll
+            for (int u = 0; u < 4; u++) ph[u] = sl[u] >= 0 ? g.slot_ph[sl[u]] : -1;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (ph[u] < 0) continue;
+                const double *B = g.hpl + (long long)sl[u] * 18;
+                const double *xp = g.x + 6 * ph[u];
+                for (int cc = 0; cc < 3; cc++) {
+                    double v = 0;
+                    for (int a = 0; a < 6; a++) v += B[3 * a + cc] * (-xp[a]);
+                    c[cc] += v;
+                }
+            }
+        }
+        const double *Di = g.Dinv + 9 * l;
+        double *xl = g.x + 6 * g.P + 3 * l;
+        for (int a = 0; a < 3; a++) {
+            const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
+            xl[a] = xa;
+            g.X2[3 * v + a] = g.X[3 * v + a] + xa;
+            sc += xa * (lambda * xa + g.bl[3 * l + a]);
+        }
     }
-    // computeScale pieces: x (lambda x + b) over this thread's entries
-    const int nx = 6 * g.P + 3 * g.Lm;
-    for (int j = t; j < nx; j += gridDim.x * 256) sc += g.x[j] * (lambda * g.x[j] + b_full[j]);
-    block_sum_to(sc, g.partial + kRedBlocks + blockIdx.x);
+    block_sum_to(sc, part + blockIdx.x);
 }
-
-__global__ __launch_bounds__(256) void lba_errors(Graph g) {
+__global__ __launch_bounds__(256) void lba_errors(Graph g, double *part) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     double r0 = 0;
     if (s < g.nact) {
@@ -799,7 +848,7 @@ __global__ __launch_bounds__(256) void lba_errors(Graph g) {
         r0 = chi;
         if (e.robust) huber(e, chi, r0, r1);
     }
-    block_sum_to(r0, g.partial + blockIdx.x);
+    block_sum_to(r0, part + blockIdx.x);
 }
 
 // outlier test of Optimizer.cc:925-962 / 977-1008: chi2 (stale _error) + depth sign
@@ -817,12 +866,6 @@ __global__ __launch_bounds__(256) void lba_outliers(const EdgeDev *E, const doub
 }
 
 // b vector in hessian order for computeScale: [b_p (6P) | b_l (3Lm)]
-__global__ __launch_bounds__(256) void lba_gather_b(Graph g, double *b_full) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    const int n6 = 6 * g.P;
-    if (t < n6) b_full[t] = g.bp[t];
-    else if (t < n6 + 3 * g.Lm) b_full[t] = g.bl[t - n6];
-}
 
 }  // namespace lbaamd
 
@@ -848,8 +891,8 @@ struct lba_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     DBuf T, T2, X, X2, E, err, act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items,
-        ps_start, ps_items, con, hpl, Hll, bl, Hpp, bp, Dinv, Y, w, slab, Hs, bs, x, partial,
-        scalars, bfull, flags;
+        ps_start, ps_items, slot_pt, slot_ph, con, hpl, Hll, bl, Hpp, bp, Dinv, Lc, Y, slab, Hs, bs, x, partial,
+        scalars, flags;
     double *h_scalars = nullptr;  // pinned
 };
 
@@ -865,7 +908,7 @@ struct HostGraph {
 
 struct ActiveSet {
     int P = 0, Lm = 0;
-    std::vector<int> act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items, ps_start, ps_items;
+    std::vector<int> act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items, ps_start, ps_items, slot_pt, slot_ph;
 };
 
 // SparseOptimizer::initializeOptimization(level) + buildIndexMapping + block structure
@@ -897,11 +940,15 @@ void build_active(const HostGraph &h, ActiveSet &A) {
     A.pt_items.assign(std::max(1, A.pt_start[A.Lm]), 0);
     A.ps_items.assign(std::max(1, A.ps_start[A.P]), 0);
     std::vector<int> fl(A.Lm, 0), fp(A.P, 0);
+    A.slot_pt.assign(std::max<size_t>(1, A.act.size()), 0);
+    A.slot_ph.assign(std::max<size_t>(1, A.act.size()), -1);
     for (int s = 0; s < (int)A.act.size(); s++) {
         const int k = A.act[s];
         const int l = A.point_hidx[h.edge_point[k]];
         A.pt_items[A.pt_start[l] + fl[l]++] = s;
         const int ph = A.pose_hidx[h.edge_pose[k]];
+        A.slot_pt[s] = l;
+        A.slot_ph[s] = ph;
         if (ph >= 0) A.ps_items[A.ps_start[ph] + fp[ph]++] = s;
     }
 }
@@ -926,29 +973,28 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
     double lambda = 0, ni = 2;
     int nBad = 0, it = 0;
     const int nact = (int)A.act.size();
-    const int n6 = 6 * A.P, nx = n6 + 3 * A.Lm;
-    const int ntile = std::max(1, (n6 + 15) / 16);
-    const int npair = ntile * (ntile + 1) / 2;
+    const int n6 = 6 * A.P;
+    const int ntile1 = std::max(1, (n6 + 15) / 16) + 1;        // + the w tile row
+    const int npair = ntile1 * (ntile1 + 1) / 2 - 1;           // without (w, w)
     for (int i = 0; i < iterations && !term(); i++) {
         lba_linearize<<<nblk(nact), 256, 0, s>>>(g);
         lba_reduce_points<<<nblk(A.Lm), 256, 0, s>>>(g);
-        if (A.P > 0) lba_reduce_poses<<<A.P, 256, 0, s>>>(g);
-        lba_finish<<<1, 256, 0, s>>>(g, 0, nblk(nact), nblk(A.Lm), A.P);
-        lba_gather_b<<<nblk(nx), 256, 0, s>>>(g, e->bfull.as<double>());
-        if (hipMemcpyAsync(e->h_scalars, g.scalars, 2 * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return -3;
-        double currentChi = e->h_scalars[0], iniChi = currentChi, tempChi;
-        if (i == 0) { lambda = 1e-5 * e->h_scalars[1]; ni = 2; nBad = 0; }
+        if (A.P > 0) lba_reduce_poses<<<A.P, 1024, 0, s>>>(g);
+        // no readback here: chi2 / maxDiagonal are finished by the trial's first kernel (the
+        // first lambda is formed there) and come back with the trial's scalars, one
+        // synchronisation per trial
+        double currentChi = 0, iniChi = 0, tempChi;
+        if (i == 0) { ni = 2; nBad = 0; }
         double rho = 0;
         int qmax = 0;
         do {
             // setLambda + Schur + solve + update + errors (push/pop = T/T2 double buffering)
-            lba_schur_points<<<nblk(A.Lm), 256, 0, s>>>(g, lambda);
+            const int mode = qmax > 0 ? 0 : (i == 0 ? 2 : 1);
+            lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, lambda, mode, nblk(nact), nblk(A.Lm), A.P);
             if (A.P > 0) {
                 const int kchunk = (((g.Kpad + g.S - 1) / g.S + 3) / 4) * 4;  // S * kchunk >= Kpad
-                lba_syrk_mfma<<<dim3(npair, g.S), 64, 0, s>>>(g, ntile, kchunk);
-                lba_schur_reduce<<<n6, 256, 0, s>>>(g, lambda);
+                lba_syrk_mfma<<<dim3(npair, g.S), 256, 0, s>>>(g, ntile1, kchunk);
+                lba_schur_reduce<<<n6, 256, 0, s>>>(g);   // slab sums: spread over n6 workgroups
                 if (n6 <= kSmallNP) {
                     lba_chol_tiled<<<1, 512, chol_tiled_lds(n6), s>>>(g);
                 } else {
@@ -966,17 +1012,26 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
             } else {
                 lba_set_ok<<<1, 1, 0, s>>>(g);
             }
-            lba_backsub<<<nblk(A.Lm), 256, 0, s>>>(g);
-            lba_update<<<nblk(A.P + A.Lm), 256, 0, s>>>(g, lambda, e->bfull.as<double>());
-            lba_errors<<<nblk(nact), 256, 0, s>>>(g);
-            lba_finish<<<1, 256, 0, s>>>(g, 1, nblk(nact), nblk(A.P + A.Lm), 0);
-            if (hipMemcpyAsync(e->h_scalars + 2, g.scalars + 2, 3 * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            // scalars[8..): the update's computeScale block sums, then the trial chi2 block sums,
+            // summed here in block order (one readback for the whole trial)
+            const int nbu = nblk(A.P + A.Lm), nbe = nblk(nact);
+            lba_update<<<nbu, 256, 0, s>>>(g, g.scalars + 8);
+            lba_errors<<<nbe, 256, 0, s>>>(g, g.scalars + 8 + nbu);
+            if (hipMemcpyAsync(e->h_scalars, g.scalars, (8 + nbu + nbe) * sizeof(double), hipMemcpyDeviceToHost, s) !=
+                    hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess)
                 return -3;
+            if (qmax == 0) {
+                currentChi = iniChi = e->h_scalars[0];
+                if (i == 0) lambda = 1e-5 * e->h_scalars[1];   // the value the device used
+            }
+            double sc_sum = 0, chi_sum = 0;
+            for (int b = 0; b < nbu; b++) sc_sum += e->h_scalars[8 + b];
+            for (int b = 0; b < nbe; b++) chi_sum += e->h_scalars[8 + nbu + b];
             const bool ok2 = e->h_scalars[4] != 0;
-            tempChi = ok2 ? e->h_scalars[2] : DBL_MAX;
+            tempChi = ok2 ? chi_sum : DBL_MAX;
             rho = currentChi - tempChi;
-            double scale = e->h_scalars[3] + 1e-3;
+            double scale = sc_sum + 1e-3;
             rho /= scale;
             if (rho > 0 && std::isfinite(tempChi)) {
                 double alpha = 1. - std::pow((2 * rho - 1), 3);
@@ -1013,7 +1068,7 @@ int lba_create(lba_engine **out) {
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORBX_EDEVICE;
     lba_engine *e = new lba_engine();
     if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void **)&e->h_scalars, 8 * sizeof(double)) != hipSuccess) {
+        hipHostMalloc((void **)&e->h_scalars, (8 + 2 * kRedBlocks) * sizeof(double)) != hipSuccess) {
         delete e;
         return ORBX_EDEVICE;
     }
@@ -1081,7 +1136,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     }
     if (upload(e->T, T, s) || upload(e->T2, T, s) || upload(e->X, X, s) || upload(e->X2, X, s) ||
         upload(e->E, E, s) || e->err.ensure(sizeof(double) * 3 * std::max(ne, 1)) ||
-        e->flags.ensure(std::max(ne, 1)) || e->scalars.ensure(8 * sizeof(double)) ||
+        e->flags.ensure(std::max(ne, 1)) || e->scalars.ensure((8 + 2 * kRedBlocks) * sizeof(double)) ||
         e->partial.ensure(sizeof(double) * 4 * kRedBlocks))
         return ORBX_EDEVICE;
     LBA_CHK(hipMemsetAsync(e->err.p, 0, sizeof(double) * 3 * std::max(ne, 1), s));
@@ -1095,7 +1150,8 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     auto setup = [&](ActiveSet &A) -> int {
         if (upload(e->act, A.act, s) || upload(e->pose_hidx, A.pose_hidx, s) || upload(e->point_hidx, A.point_hidx, s) ||
             upload(e->hpose, A.hpose, s) || upload(e->hpoint, A.hpoint, s) || upload(e->pt_start, A.pt_start, s) ||
-            upload(e->pt_items, A.pt_items, s) || upload(e->ps_start, A.ps_start, s) || upload(e->ps_items, A.ps_items, s))
+            upload(e->pt_items, A.pt_items, s) || upload(e->ps_start, A.ps_start, s) || upload(e->ps_items, A.ps_items, s) ||
+            upload(e->slot_pt, A.slot_pt, s) || upload(e->slot_ph, A.slot_ph, s))
             return -1;
         const int nact = (int)A.act.size();
         g.act = e->act.as<int>(); g.nact = nact;
@@ -1104,29 +1160,31 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.P = A.P; g.Lm = A.Lm;
         g.pt_start = e->pt_start.as<int>(); g.pt_items = e->pt_items.as<int>();
         g.ps_start = e->ps_start.as<int>(); g.ps_items = e->ps_items.as<int>();
+        g.slot_pt = e->slot_pt.as<int>(); g.slot_ph = e->slot_ph.as<int>();
         g.Kpad = std::max(4, ((3 * A.Lm + 3) / 4) * 4);
         g.NP = std::max(kCB, ((6 * A.P + kCB - 1) / kCB) * kCB);
-        const size_t NP = (size_t)g.NP;
-        // K slices of the SYRK: enough waves to fill the chip, slabs capped at ~1 GB
-        g.S = std::max(1, std::min({64, g.Kpad / 256, (int)std::max<size_t>(1, (size_t(1) << 27) / (NP * NP))}));
+        const size_t NP = (size_t)g.NP, NPW = NP + 16;
+        g.NPW = (int)NPW;
+        g.wrow = 16 * std::max(1, (6 * A.P + 15) / 16);
+        // K slices of the SYRK (4 waves each): enough waves to fill the chip, slabs capped at ~1 GB
+        g.S = std::max(1, std::min({16, g.Kpad / 1024, (int)std::max<size_t>(1, (size_t(1) << 27) / (NP * NPW))}));
         if (e->con.ensure(sizeof(double) * 36 * std::max(nact, 1)) || e->hpl.ensure(sizeof(double) * 18 * std::max(nact, 1)) ||
             e->Hll.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) || e->bl.ensure(sizeof(double) * 3 * std::max(A.Lm, 1)) ||
             e->Hpp.ensure(sizeof(double) * 36 * std::max(A.P, 1)) || e->bp.ensure(sizeof(double) * 6 * std::max(A.P, 1)) ||
-            e->Dinv.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) ||
-            e->Y.ensure(sizeof(double) * NP * (size_t)g.Kpad) || e->w.ensure(sizeof(double) * g.Kpad) ||
-            e->slab.ensure(sizeof(double) * (size_t)g.S * NP * NP) || e->Hs.ensure(sizeof(double) * NP * NP) ||
-            e->bs.ensure(sizeof(double) * NP) || e->x.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)) ||
-            e->bfull.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)))
+            e->Dinv.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) || e->Lc.ensure(sizeof(double) * 6 * std::max(A.Lm, 1)) ||
+            e->Y.ensure(sizeof(double) * NPW * (size_t)g.Kpad) ||
+            e->slab.ensure(sizeof(double) * (size_t)g.S * NP * NPW) || e->Hs.ensure(sizeof(double) * NP * NP) ||
+            e->bs.ensure(sizeof(double) * NP) || e->x.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)))
             return -1;
         g.con = e->con.as<double>(); g.hpl = e->hpl.as<double>();
         g.Hll = e->Hll.as<double>(); g.bl = e->bl.as<double>();
         g.Hpp = e->Hpp.as<double>(); g.bp = e->bp.as<double>();
-        g.Dinv = e->Dinv.as<double>(); g.Y = e->Y.as<double>(); g.w = e->w.as<double>();
+        g.Dinv = e->Dinv.as<double>(); g.Lc = e->Lc.as<double>(); g.Y = e->Y.as<double>();
+        g.w = g.Y + g.wrow;
         g.slab = e->slab.as<double>(); g.Hs = e->Hs.as<double>(); g.bs = e->bs.as<double>();
         g.x = e->x.as<double>();
-        if (hipMemsetAsync(g.Y, 0, sizeof(double) * NP * (size_t)g.Kpad, s) != hipSuccess ||
-            hipMemsetAsync(g.w, 0, sizeof(double) * g.Kpad, s) != hipSuccess ||
-            hipMemsetAsync(g.slab, 0, sizeof(double) * (size_t)g.S * NP * NP, s) != hipSuccess ||
+        if (hipMemsetAsync(g.Y, 0, sizeof(double) * NPW * (size_t)g.Kpad, s) != hipSuccess ||
+            hipMemsetAsync(g.slab, 0, sizeof(double) * (size_t)g.S * NP * NPW, s) != hipSuccess ||
             hipMemsetAsync(g.Hs, 0, sizeof(double) * NP * NP, s) != hipSuccess ||
             hipMemsetAsync(g.x, 0, sizeof(double) * (6 * A.P + 3 * A.Lm + 8), s) != hipSuccess)
             return -1;
