@@ -563,35 +563,39 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
     const long long t_load = clock64() - t0;
     ta = clock64();
 #endif
-    for (int K = 0; K < NT; K++) {
-        const int k0 = 16 * K;
+    // wave 0: factor + invert diagonal tile K (lane i of each 16-lane row = row i)
+    auto diag = [&](int K) {
+        const int k0 = 16 * K, i = lane & 15;
         double *LK = Linv + K * 16 * 17;
-        if (wv == 0) {   // 1. diagonal tile: factor + inverse
-            const int i = lane & 15;
-            double row[16], li[16];   // li: column i of L_kk^-1
+        double row[16], li[16];   // li: column i of L_kk^-1
 #pragma unroll
-            for (int c = 0; c < 16; c++) row[c] = c <= i ? A[(k0 + i) * LDA + k0 + c] : 0.0;
+        for (int c = 0; c < 16; c++) row[c] = c <= i ? A[(k0 + i) * LDA + k0 + c] : 0.0;
 #pragma unroll
-            for (int r = 0; r < 16; r++) li[r] = 0.0;
-            bool bad = false;
-            chol16_factor<0>(row, li, i, n - k0, bad);
-            // every 16-lane row computed the same tile: all lanes store (same values), so the
-            // compiler cannot sink the li chain into a lane < 16 branch and keep every
-            // broadcast live until there
+        for (int r = 0; r < 16; r++) li[r] = 0.0;
+        bool bad = false;
+        chol16_factor<0>(row, li, i, n - k0, bad);
+        // every 16-lane row computed the same tile: all lanes store (same values), so the
+        // compiler cannot sink the li chain into a lane < 16 branch and keep every broadcast
+        // live until there
 #pragma unroll
-            for (int c = 0; c < 16; c++) A[(k0 + i) * LDA + k0 + c] = row[c];
+        for (int c = 0; c < 16; c++) A[(k0 + i) * LDA + k0 + c] = row[c];
 #pragma unroll
-            for (int r = 0; r < 16; r++) LK[r * 17 + i] = li[r];
-            if (lane == 0 && bad) fail = 1;
-        }
-        __syncthreads();
-        LBA_T(t_diag);
+        for (int r = 0; r < 16; r++) LK[r * 17 + i] = li[r];
+        if (lane == 0 && bad) fail = 1;
+    };
+    if (wv == 0) diag(0);
+    __syncthreads();
+    LBA_T(t_diag);
+    // look-ahead: diagonal tile K + 1 is factored by wave 0 right after its own trailing
+    // update, while waves 1-7 update the rest of the trailing matrix; 2 barriers per panel
+    for (int K = 0; K < NT; K++) {
         if (fail) {   // uniform after the barrier
             if (tid == 0) g.scalars[4] = 0;
             return;
         }
-        const int r0 = k0 + 16, m = NT - K - 1;
-        for (int I = wv; I < m; I += 8) {   // 2. panel: L_ik = A_ik L_kk^-T
+        const int k0 = 16 * K, r0 = k0 + 16, m = NT - K - 1;
+        const double *LK = Linv + K * 16 * 17;
+        for (int I = wv; I < m; I += 8) {   // panel: L_ik = A_ik L_kk^-T
             const int ri = r0 + 16 * I;
             double4_t acc = {0, 0, 0, 0};
 #pragma unroll
@@ -605,8 +609,10 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
         }
         __syncthreads();
         LBA_T(t_trsm);
+        if (m == 0) break;
         const int ntile = m * (m + 1) / 2;
-        for (int t = wv; t < ntile; t += 8) {   // 3. trailing lower tiles
+        // trailing lower tiles; tile 0 = diagonal tile K + 1 -> wave 0, the rest -> waves 1-7
+        for (int t = wv == 0 ? 0 : wv; t < ntile; t += wv == 0 ? ntile : 7) {
             int I = 0, u = t;
             while (u > I) { u -= I + 1; I++; }
             const int J = u;
@@ -623,27 +629,34 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
 #pragma unroll
             for (int q = 0; q < 4; q++) A[(ri + (lane >> 4) + 4 * q) * LDA + cj + (lane & 15)] = acc[q];
         }
+        if (wv == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // own tile stores before reloading it
+            diag(K + 1);
+        }
         __syncthreads();
         LBA_T(t_trail);
     }
 #ifdef LBA_PROFILE
     const long long ts = clock64();
 #endif
-    // back substitution L^T x = y, y = row n of the factor
-    for (int j = tid; j < n; j += 512) yv[j] = A[n * LDA + j];
+    // back substitution L^T x = y, y = row n of the factor, zero past n: the padded rows of
+    // the last block then contribute exactly 0 and every block runs fixed 16-term sums
+    for (int j = tid; j < N2; j += 512) yv[j] = j < n ? A[n * LDA + j] : 0.0;
     __syncthreads();
     for (int K = (n - 1) / 16; K >= 0; K--) {
-        const int k0 = 16 * K, kn = min(16, n - k0);
-        if (tid < kn) {   // x_K = L_KK^-T y_K over the rows < n
+        const int k0 = 16 * K;
+        if (tid < 16) {   // x_K = L_KK^-T y_K
             const double *LK = Linv + K * 16 * 17;
             double s = 0.0;
-            for (int r = tid; r < kn; r++) s += LK[r * 17 + tid] * yv[k0 + r];
+#pragma unroll
+            for (int r = 0; r < 16; r++) s += LK[r * 17 + tid] * yv[k0 + r];   // LK[r][c] = 0 for r < c
             xv[k0 + tid] = s;
         }
         __syncthreads();
         for (int j = tid; j < k0; j += 512) {
             double s = yv[j];
-            for (int k = 0; k < kn; k++) s -= A[(k0 + k) * LDA + j] * xv[k0 + k];
+#pragma unroll
+            for (int k = 0; k < 16; k++) s -= A[(k0 + k) * LDA + j] * xv[k0 + k];
             yv[j] = s;
         }
         __syncthreads();
