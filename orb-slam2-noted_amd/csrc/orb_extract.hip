@@ -63,9 +63,9 @@ __device__ __forceinline__ const uint8_t *level_ptr(const ExtractGeom &g, const 
 // K1: cv::resize(INTER_LINEAR) of level l-1 into level l (ComputePyramid :1686-1691,
 // SURVEY.md A.2). Column/row coefficient tables are precomputed on the host with the
 // reference's float/double arithmetic; the kernel does the exact integer math.
-// Each thread produces 4 consecutive pixels of one row: the row pair is a wave-uniform
-// (scalar) load, the 4 source columns span <= 8 bytes (scale <= 2) and come from two
-// dword loads per source row; the result is one dword store (pyramid pitch is 16-aligned).
+// Each thread produces 4 consecutive pixels of RZ_RB consecutive rows: the 4 source columns
+// span <= 8 bytes (scale <= 2) and come from two unaligned-dword reads per source row; each
+// output row is one dword store (pyramid pitch is 16-aligned).
 // Column table entry: x = sx | a0 << 16, y = a1 | (sx1 - sx) << 16.
 // ------------------------------------------------------------------------------------
 // dword of image bytes [x, x+4) of row `rowp` (x .. x+3 inside the row) from aligned loads
@@ -94,47 +94,67 @@ __device__ __forceinline__ int resize_px(int S0, int S1, int4 ry, bool simd) {
     return min(max(v, 0), 255);
 }
 
+#define RZ_RB 4   // output rows per thread
+
 __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, const int2 *cxt, const int4 *ryt,
                                                            const uint8_t *in, uint8_t *pyr) {
-    const int dw = g.lw[l];
-    const int b = blockIdx.z, dy = blockIdx.y;   // streaming: the XCD remap measured no gain here
-    const int dx0 = (blockIdx.x * 256 + threadIdx.x) * 4;
-    if (dx0 >= dw) return;
+    // flat (row block, column group) tasks: no idle lanes at the right edge of narrow
+    // levels; RZ_RB rows per thread keep 4 * RZ_RB independent loads in flight (the level-1
+    // pass streams the input from HBM and was latency bound with one row per thread)
+    const int dw = g.lw[l], dh = g.lh[l];
+    const int b = blockIdx.y;   // streaming: the XCD remap measured no gain here
+    const int ncg = (dw + 3) >> 2;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int rb = t / ncg, cg = t - rb * ncg;
+    const int dy0 = rb * RZ_RB;
+    if (dy0 >= dh) return;
+    const int dx0 = 4 * cg;
     int sp;
     const uint8_t *src = level_ptr(g, in, pyr, b, l - 1, &sp);
-    uint8_t *dst = pyr + (long long)b * g.pyr_stride + g.pyr_off[l] + (long long)dy * g.bp[l];
-    const int4 ry = ryt[dy];   // r0, r1, b0, b1 (uniform over the block)
-    const uint8_t *p0 = src + (long long)ry.x * sp, *p1 = src + (long long)ry.y * sp;
+    uint8_t *dst = pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
     const int n = min(4, dw - dx0);
     int2 c[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) c[k] = cxt[min(dx0 + k, dw - 1)];
     const int sx0 = c[0].x & 0xFFFF;
     const int sw = g.lw[l - 1];
-    unsigned long long R0, R1;
-    if (sx0 + 8 <= sw) {
-        R0 = load_u32_unaligned(p0 + sx0) | (unsigned long long)load_u32_unaligned(p0 + sx0 + 4) << 32;
-        R1 = load_u32_unaligned(p1 + sx0) | (unsigned long long)load_u32_unaligned(p1 + sx0 + 4) << 32;
-    } else {
-        R0 = R1 = 0;
-        for (int e = 0; e < 8 && sx0 + e < sw; e++) {
-            R0 |= (unsigned long long)p0[sx0 + e] << (8 * e);
-            R1 |= (unsigned long long)p1[sx0 + e] << (8 * e);
+    const bool fast = sx0 + 8 <= sw;
+    int4 ry[RZ_RB];
+    unsigned long long R0[RZ_RB], R1[RZ_RB];
+#pragma unroll
+    for (int u = 0; u < RZ_RB; u++) {
+        ry[u] = ryt[min(dy0 + u, dh - 1)];   // r0, r1, b0, b1
+        const uint8_t *p0 = src + (long long)ry[u].x * sp, *p1 = src + (long long)ry[u].y * sp;
+        if (fast) {
+            R0[u] = load_u32_unaligned(p0 + sx0) | (unsigned long long)load_u32_unaligned(p0 + sx0 + 4) << 32;
+            R1[u] = load_u32_unaligned(p1 + sx0) | (unsigned long long)load_u32_unaligned(p1 + sx0 + 4) << 32;
+        } else {
+            R0[u] = R1[u] = 0;
+            for (int e = 0; e < 8 && sx0 + e < sw; e++) {
+                R0[u] |= (unsigned long long)p0[sx0 + e] << (8 * e);
+                R1[u] |= (unsigned long long)p1[sx0 + e] << (8 * e);
+            }
         }
     }
-    uint32_t out = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int o = (c[k].x & 0xFFFF) - sx0, o1 = o + (c[k].y >> 16);
-        const int a0 = c[k].x >> 16, a1 = c[k].y & 0xFFFF;
-        const int S0 = (int)((R0 >> (8 * o)) & 0xFF) * a0 + (int)((R0 >> (8 * o1)) & 0xFF) * a1;
-        const int S1 = (int)((R1 >> (8 * o)) & 0xFF) * a0 + (int)((R1 >> (8 * o1)) & 0xFF) * a1;
-        out |= (uint32_t)resize_px(S0, S1, ry, dx0 + k < g.rz_simd_end[l]) << (8 * k);
-    }
-    if (n == 4) {
-        *(uint32_t *)(dst + dx0) = out;
-    } else {
-        for (int k = 0; k < n; k++) dst[dx0 + k] = (uint8_t)(out >> (8 * k));
+    for (int u = 0; u < RZ_RB; u++) {
+        const int dy = dy0 + u;
+        if (dy >= dh) break;
+        uint32_t out = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int o = (c[k].x & 0xFFFF) - sx0, o1 = o + (c[k].y >> 16);
+            const int a0 = c[k].x >> 16, a1 = c[k].y & 0xFFFF;
+            const int S0 = (int)((R0[u] >> (8 * o)) & 0xFF) * a0 + (int)((R0[u] >> (8 * o1)) & 0xFF) * a1;
+            const int S1 = (int)((R1[u] >> (8 * o)) & 0xFF) * a0 + (int)((R1[u] >> (8 * o1)) & 0xFF) * a1;
+            out |= (uint32_t)resize_px(S0, S1, ry[u], dx0 + k < g.rz_simd_end[l]) << (8 * k);
+        }
+        uint8_t *drow = dst + (long long)dy * g.bp[l];
+        if (n == 4) {
+            *(uint32_t *)(drow + dx0) = out;
+        } else {
+            for (int k = 0; k < n; k++) drow[dx0 + k] = (uint8_t)(out >> (8 * k));
+        }
     }
 }
 
@@ -772,6 +792,14 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     int l, b;
     xcd_remap2(l, b);
     const int tid = threadIdx.x;
+#ifdef ORBX_QT_PROFILE
+    long long qt_t[8];
+    int qt_rounds = 0;
+    qt_t[0] = wall_clock64();
+#define QT_MARK(k) do { if (tid == 0) qt_t[k] = wall_clock64(); } while (0)
+#else
+#define QT_MARK(k) do {} while (0)
+#endif
     const int cb0 = g.cell_base[l], ncell = g.cell_base[l + 1] - cb0;
     const int N = g.N[l], nIni = g.nIni[l];
     const int NC = g.node_cap, NP = g.node_pow2;
@@ -826,6 +854,7 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
             base += (int)tot;
         }
     }
+    QT_MARK(1);
     // ---- 2. roots (:700-745): stable counting partition into buffer 1
     const float hX = g.hX[l];
     if (tid < 64) { S.root_cnt[tid] = 0; S.root_fill[tid] = 0; }
@@ -893,6 +922,7 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         __syncthreads();
     }
     Q.src = 1;
+    QT_MARK(2);
     // ---- 3. phase-1 rounds (:772-913): every live node divided, roots ascending, then
     //         the previous round's multi-key children in reverse creation order
     int order = 0;
@@ -903,10 +933,14 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         qt_assign(S, Q, na, order, na, par);
         qt_move(S, Q, base);
         order = 1;
+#ifdef ORBX_QT_PROFILE
+        qt_rounds++;
+#endif
         const int live = S.live, nToExpand = S.n_act;
         if (live >= N || live == prev) finished = true;
         else if (live + nToExpand * 3 > N) { final_phase = true; finished = true; }
     }
+    QT_MARK(3);
     // ---- 4. final phase (:914-997): nodes by (size, id) descending; divide until the
     //         list reaches N
     if (final_phase) {
@@ -950,9 +984,13 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
             const int limit = min(S.cross + 1, na);
             qt_assign(S, Q, na, 2, limit, par);
             qt_move(S, Q, base);
+#ifdef ORBX_QT_PROFILE
+            qt_rounds += 100;
+#endif
             if (S.live >= N || S.live == prev) done = true;
         }
     }
+    QT_MARK(4);
     // ---- 5. every remaining multi-key node -> its first key of maximal response (:1028)
     {
         const int na = S.n_act;
@@ -977,14 +1015,22 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         if (tid == 0) S.n_out += na;
         __syncthreads();
     }
+    QT_MARK(5);
     const int nout = min(S.n_out, NP);
     for (int i = nout + tid; i < NP; i += ORBX_QT_THREADS) Q.outrec[i] = 0;
     __syncthreads();
     block_sort_desc(Q.outrec, NP);
+    QT_MARK(6);
     const int ncap = min(nout, g.out_cap[l]);
     uint32_t *dst = sel + (long long)b * g.out_base[g.nlevels] + g.out_base[l];
     for (int i = tid; i < ncap; i += ORBX_QT_THREADS) dst[i] = (uint32_t)(Q.outrec[i] & 0xFFFFFFFFull);
     if (tid == 0) sel_cnt[b * g.nlevels + l] = ncap;
+#ifdef ORBX_QT_PROFILE
+    if (tid == 0 && b < 2)
+        printf("QTPROF b=%d l=%d M=%d NP=%d nout=%d rounds=%d lds=%d gather=%lld roots=%lld ph1=%lld final=%lld best=%lld sort=%lld\n", b, l, M,
+               NP, nout, qt_rounds, g.qt_nodes_in_lds, qt_t[1] - qt_t[0], qt_t[2] - qt_t[1], qt_t[3] - qt_t[2], qt_t[4] - qt_t[3],
+               qt_t[5] - qt_t[4], qt_t[6] - qt_t[5]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -1248,9 +1294,12 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         const size_t node_bytes = (2 * sizeof(QNode) + sizeof(QTmp)) * g.node_cap + 16 * (size_t)np2;
         g.qt_nodes_in_lds = node_bytes <= 48 * 1024 ? 1 : 0;
         g.qt_node_stride = (long long)((node_bytes + 15) / 16) * 4;
-        // keys (2 x u32) + node index (2 x int16) per candidate in LDS up to ~78 KB per workgroup
-        // (two workgroups per CU); larger levels run on the global scratch
-        const long long kl_bytes = 78 * 1024 - (g.qt_nodes_in_lds ? (long long)node_bytes : 0);
+        // keys (2 x u32) + node index (2 x int16) per candidate in LDS: dynamic + static
+        // (QShared) LDS stays within half of the CU's 160 KB so two workgroups share a CU (at
+        // 78 KB + QShared only one fit, and the 8 x batch workgroups ran in 8 serial waves);
+        // larger levels run on the global scratch
+        const long long kl_bytes = 80 * 1024 - (long long)sizeof(QShared) - 256 -
+                                   (g.qt_nodes_in_lds ? (long long)node_bytes : 0);
         g.qt_kl = (int)std::max<long long>(256, (kl_bytes / 12) & ~63LL);
         g.ini_th = e->p.ini_th_fast;
         g.min_th = e->p.min_th_fast;
@@ -1327,7 +1376,8 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     uint8_t *pyr = e->d_pyr.as<uint8_t>();
     int ph = prof_begin(e, s);
     for (int l = 1; l < L; l++) {
-        dim3 grid((g.lw[l] + 1023) / 1024, g.lh[l], n);
+        const long long tasks = (long long)((g.lw[l] + 3) / 4) * ((g.lh[l] + RZ_RB - 1) / RZ_RB);
+        dim3 grid((unsigned)((tasks + 255) / 256), n);
         resize_level_kernel<<<grid, 256, 0, s>>>(g, l, e->d_rz.as<int2>() + g.rz_col_off[l],
                                                  e->d_rzr.as<int4>() + g.rz_row_off[l], d_imgs, pyr);
     }
