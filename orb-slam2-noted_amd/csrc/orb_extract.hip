@@ -18,7 +18,7 @@ using namespace orbamd;
 
 namespace orbamd {
 
-static __constant__ int8_t c_pattern[1024];  // bit_pattern_31_ (ORBextractor.cc:209-467) as data
+static __constant__ __attribute__((aligned(16))) int8_t c_pattern[1024];  // bit_pattern_31_ (ORBextractor.cc:209-467) as data
 static __constant__ int c_umax[16];
 // IC_Angle byte weights per (|v|, dword w) of the row segment u = 4w-16 .. 4w-13:
 // x = (u + 16) where |u| <= umax[|v|] else 0, y = 1 / 0 mask (built from umax on the host)
@@ -439,10 +439,12 @@ __global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const Cell
     const int ndet = (dh > 0 && dwid > 0) ? dh * dwid : 0;
     // region rows r0+2 .. r0+rh-3, cols c0+2 .. c0+rw-3 (detection region + 1); sm(0,0) = (r0+2, c0+2)
     const uint8_t *base = mmap + (long long)b * g.blur_stride + g.blur_off[l] + (long long)(cd.r0 + 2) * bp + cd.c0 + 2;
-    const int qw = (dwid + 2 + 3) >> 2;
-    for (int i = lane; i < (dh + 2) * qw && ndet > 0; i += 64) {
-        const int rr = i / qw, j = i - rr * qw;
-        sm32[rr * (NMS_P / 4) + j] = load_u32_unaligned(base + (long long)rr * bp + 4 * j);
+    const int qw = (dwid + 2 + 3) >> 2;   // <= NMS_P / 4 = 17 dwords per row
+    {   // lane -> (row offset, dword) once per cell: no per-element integer division
+        const int rpi = 64 / qw, ro = lane / qw, jq = lane - ro * qw;
+        if (ro < rpi && ndet > 0)
+            for (int rr = ro; rr < dh + 2; rr += rpi)
+                sm32[rr * (NMS_P / 4) + jq] = load_u32_unaligned(base + (long long)rr * bp + 4 * jq);
     }
     wave_lds_sync();
     // zero the one-pixel frame: neighbours outside the detection region score 0
@@ -456,21 +458,35 @@ __global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const Cell
     const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
     const int tlo = min(th_a, th_b);
     wave_lds_sync();
+    // candidates in row-major order as (i << 8 | j): rows of the region map onto the lanes
+    // (64 / dwid rows per step, lane = row offset * dwid + j keeps row-major order)
     int nl = 0;
-    for (int b0 = 0; b0 < ndet; b0 += 64) {
-        const int idx = b0 + lane;
-        bool f = false;
-        if (idx < ndet) {
-            const int i = idx / dwid, j = idx - i * dwid;
-            f = sm[(i + 1) * NMS_P + j + 1] > tlo;
+    if (dwid <= 64 && dh < 256) {
+        const int rpi = 64 / max(dwid, 1), ro = lane / max(dwid, 1), j = lane - ro * max(dwid, 1);
+        for (int i0 = 0; i0 < dh && ndet > 0; i0 += rpi) {
+            const int i = i0 + ro;
+            const bool f = ro < rpi && i < dh && sm[(i + 1) * NMS_P + j + 1] > tlo;
+            const unsigned long long bal = __ballot(f);
+            if (f) lst[nl + lane_rank(bal)] = (uint16_t)((i << 8) | j);
+            nl += __popcll(bal);
         }
-        const unsigned long long bal = __ballot(f);
-        if (f) lst[nl + lane_rank(bal)] = (uint16_t)idx;
-        nl += __popcll(bal);
+    } else {
+        for (int b0 = 0; b0 < ndet; b0 += 64) {
+            const int idx = b0 + lane;
+            bool f = false;
+            int i = 0, j = 0;
+            if (idx < ndet) {
+                i = idx / dwid; j = idx - i * dwid;
+                f = sm[(i + 1) * NMS_P + j + 1] > tlo;
+            }
+            const unsigned long long bal = __ballot(f);
+            if (f) lst[nl + lane_rank(bal)] = (uint16_t)((i << 8) | j);   // dwid <= 64 above ->
+            nl += __popcll(bal);                                          // here j < NMS_P, i < 256
+        }
     }
     wave_lds_sync();
-    auto keep_at = [&](int idx, int th, int *score) {
-        const int i = idx / dwid, j = idx - i * dwid;
+    auto keep_at = [&](int e, int th, int *score) {
+        const int i = e >> 8, j = e & 0xFF;
         const uint8_t *s = sm + (i + 1) * NMS_P + j + 1;
         const int v = thr_score(s[0], th);
         *score = v;
@@ -497,7 +513,7 @@ __global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const Cell
         const unsigned long long m = __ballot(k);
         const int rank = (int)lane_rank(m);
         if (k && written + rank < g.cell_cap) {
-            const int i = idx / dwid, j = idx - i * dwid;
+            const int i = idx >> 8, j = idx & 0xFF;
             out[written + rank] = pack_key(j + 3 + cd.offx, i + 3 + cd.offy, v);
         }
         written += __popcll(m);
@@ -601,7 +617,10 @@ __device__ __forceinline__ unsigned long long block_scan64(QShared &S, unsigned 
     return r.a;
 }
 
-// bitonic sort of n (pow2) u64 values, descending
+// bitonic sort of n (pow2) u64 values, descending. Thread t owns elements t + 256 e, so a
+// stage with j < 64 pairs elements of the same wavefront: those stages are ordered with a
+// wavefront LDS fence; workgroup barriers only around the stages with j >= 64 (10 of the 45
+// stages at n = 512).
 __device__ void block_sort_desc(unsigned long long *a, int n) {
     for (int k = 2; k <= n; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
@@ -613,7 +632,11 @@ __device__ void block_sort_desc(unsigned long long *a, int n) {
                     if (desc ? (x < y) : (x > y)) { a[i] = y; a[ixj] = x; }
                 }
             }
-            __syncthreads();
+            // a stage with j >= 64 writes other wavefronts' elements: barrier after it, and
+            // before the next one that reads across wavefronts (and at the end)
+            const int jn = j > 1 ? j >> 1 : k;   // next stage's distance (k: next k's first)
+            if (j >= 64 || jn >= 64 || (j == 1 && k == n)) __syncthreads();
+            else wave_lds_sync();
         }
     }
 }
@@ -847,9 +870,17 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
             const int v = c < ncell ? cnt[c] : 0;
             unsigned long long tot;
             const int pre = (int)block_scan64(S, (unsigned)v, &tot, par);
-            if (c < ncell) {
+            if (c < ncell) {   // 4 loads in flight per step
                 const uint32_t *src = cell_keys + ((long long)b * g.ncell_total + cb0 + c) * g.cell_cap;
-                for (int i = 0; i < v; i++) Q.K[0][base + pre + i] = src[i];
+                uint32_t *dk = Q.K[0] + base + pre;
+                for (int i = 0; i < v; i += 4) {
+                    uint32_t t4[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) t4[u] = i + u < v ? src[i + u] : 0u;
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (i + u < v) dk[i + u] = t4[u];
+                }
             }
             base += (int)tot;
         }
@@ -1026,9 +1057,9 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     for (int i = tid; i < ncap; i += ORBX_QT_THREADS) dst[i] = (uint32_t)(Q.outrec[i] & 0xFFFFFFFFull);
     if (tid == 0) sel_cnt[b * g.nlevels + l] = ncap;
 #ifdef ORBX_QT_PROFILE
-    if (tid == 0 && b < 2)
-        printf("QTPROF b=%d l=%d M=%d NP=%d nout=%d rounds=%d lds=%d gather=%lld roots=%lld ph1=%lld final=%lld best=%lld sort=%lld\n", b, l, M,
-               NP, nout, qt_rounds, g.qt_nodes_in_lds, qt_t[1] - qt_t[0], qt_t[2] - qt_t[1], qt_t[3] - qt_t[2], qt_t[4] - qt_t[3],
+    if (tid == 0 && (b < 2 || (b & 31) == 0))
+        printf("QTPROF b=%d l=%d M=%d NP=%d nout=%d rounds=%d start=%lld end=%lld gather=%lld roots=%lld ph1=%lld final=%lld best=%lld sort=%lld\n", b, l, M,
+               NP, nout, qt_rounds, qt_t[0], wall_clock64(), qt_t[1] - qt_t[0], qt_t[2] - qt_t[1], qt_t[3] - qt_t[2], qt_t[4] - qt_t[3],
                qt_t[5] - qt_t[4], qt_t[6] - qt_t[5]);
 #endif
 }
@@ -1044,14 +1075,10 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-__global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint8_t *in,
-                                                       const uint8_t *pyr, const uint8_t *blur,
-                                                       const uint32_t *sel, const int *sel_cnt,
-                                                       orbx_kp *kps, uint8_t *desc, int *cnt) {
-    const int lane = threadIdx.x & 63;
-    int bxr, b;
-    xcd_remap2(bxr, b);
-    const int slot = bxr * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void describe_one(const ExtractGeom &g, const uint8_t *in, const uint8_t *pyr,
+                                             const uint8_t *blur, const uint32_t *sel, const int *sel_cnt,
+                                             orbx_kp *kps, uint8_t *desc, int *cnt, int slot, int b, int lane,
+                                             uint32_t *patch, const uint2 (&icw)[4], const uint32_t (&pat)[4]) {
     const int L = g.nlevels, cap = g.out_base[L];
     if (slot >= cap) return;
     int l = 0;
@@ -1079,7 +1106,7 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
         const int j = lane + 64 * k;
         if (j < 31 * 8) {
             const int v = (j >> 3) - 15, w = j & 7;
-            const uint2 wt = c_icw[(v < 0 ? -v : v) * 8 + w];
+            const uint2 wt = icw[k];
             const uint32_t P = load_u32_unaligned(rowc + (long long)v * pitch + 4 * w);
             const int su = (int)__builtin_amdgcn_udot4(P, wt.x, 0u, false);
             const int sm = (int)__builtin_amdgcn_udot4(P, wt.y, 0u, false);
@@ -1089,24 +1116,48 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
     }
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
-    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    // wave-uniform from here: keep the angle in an SGPR so sincosf's tables are scalar loads
+    const float angle = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fast_atan2_deg((float)m01, (float)m10))));
     // steered BRIEF on the blurred level
     const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
     float sa, ca;
     glibc_sincosf(angle * factorPI, &sa, &ca);
     const float a = ca, bs = sa;
     const int bw = g.bp[l];
-    const uint8_t *bc = blur + (long long)b * g.blur_stride + g.blur_off[l] + (long long)y * bw + x;
+    // the rotated pattern stays within +-18 pixels (|rot(p)| <= 13 sqrt 2): stage the 37 rows x
+    // 40 bytes around the keypoint (dword-aligned; the pitch is 16-aligned so every row has the
+    // same misalignment sh) into this wavefront's LDS with coalesced dword loads, then run
+    // the 512 byte tests from LDS instead of as scattered global gathers. Flat addresses as
+    // before (row * pitch + column), clamped into the blur buffer.
+    const long long lvl0 = (long long)b * g.blur_stride + g.blur_off[l];
+    const long long c0 = lvl0 + (long long)(y - 18) * bw + (x - 18);
+    const int sh = (int)(c0 & 3);
+    const long long a0 = c0 - sh, amax = (long long)g.nimg * g.blur_stride - 4;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        const int idx = lane + 64 * k;
+        if (idx < 370) {
+            const int rr = idx / 10, q = idx - rr * 10;
+            long long ad = a0 + (long long)rr * bw + 4 * q;
+            ad = ad < 0 ? 0 : (ad > amax ? amax & ~3LL : ad);
+            patch[idx] = *(const uint32_t *)(blur + ad);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint8_t *pc = (const uint8_t *)patch + 18 * 40 + 18 + sh;   // (dy, dx) -> pc[dy * 40 + dx]
     unsigned long long words[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) {
-        const int p = w * 64 + lane;
-        const float px0 = (float)c_pattern[4 * p], py0 = (float)c_pattern[4 * p + 1];
-        const float px1 = (float)c_pattern[4 * p + 2], py1 = (float)c_pattern[4 * p + 3];
-        const int t0 = bc[(long long)cv_round_f(px0 * bs + py0 * a) * bw + cv_round_f(px0 * a - py0 * bs)];
-        const int t1 = bc[(long long)cv_round_f(px1 * bs + py1 * a) * bw + cv_round_f(px1 * a - py1 * bs)];
+        const uint32_t pw = pat[w];   // pattern pair w * 64 + lane: x0 y0 x1 y1 as int8
+        const float px0 = (float)(int8_t)(pw & 0xFF), py0 = (float)(int8_t)((pw >> 8) & 0xFF);
+        const float px1 = (float)(int8_t)((pw >> 16) & 0xFF), py1 = (float)(int8_t)(pw >> 24);
+        const int t0 = pc[cv_round_f(px0 * bs + py0 * a) * 40 + cv_round_f(px0 * a - py0 * bs)];
+        const int t1 = pc[cv_round_f(px1 * bs + py1 * a) * 40 + cv_round_f(px1 * a - py1 * bs)];
         words[w] = __ballot(t0 < t1);
     }
+    __builtin_amdgcn_wave_barrier();   // patch reused by this wavefront's next slot
     const long long o = (long long)b * cap + off;
     if (lane == 0) {
         unsigned long long *d = (unsigned long long *)(desc + o * 32);
@@ -1123,6 +1174,32 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
         kp.class_id = -1;
         kps[o] = kp;
     }
+}
+
+// DESC_R consecutive slots per wavefront: fewer, longer-lived waves (the one-slot waves lived
+// ~2 us and the chip held ~7 of them per CU)
+#define DESC_R 4
+__global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint8_t *in,
+                                                       const uint8_t *pyr, const uint8_t *blur,
+                                                       const uint32_t *sel, const int *sel_cnt,
+                                                       orbx_kp *kps, uint8_t *desc, int *cnt) {
+    const int lane = threadIdx.x & 63;
+    int bxr, b;
+    xcd_remap2(bxr, b);
+    __shared__ uint32_t patch[4][372];
+    const int s0 = (bxr * 4 + (threadIdx.x >> 6)) * DESC_R;
+    // per-lane constants loaded once for the wavefront's DESC_R slots: IC_Angle weights of
+    // the lane's 4 (row, dword) cells and its 4 packed test pairs
+    uint2 icw[4];
+    uint32_t pat[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int j = min(lane + 64 * k, 31 * 8 - 1), v = (j >> 3) - 15;
+        icw[k] = c_icw[(v < 0 ? -v : v) * 8 + (j & 7)];
+        pat[k] = ((const uint32_t *)c_pattern)[k * 64 + lane];
+    }
+    for (int r = 0; r < DESC_R; r++)
+        describe_one(g, in, pyr, blur, sel, sel_cnt, kps, desc, cnt, s0 + r, b, lane, patch[threadIdx.x >> 6], icw, pat);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1399,7 +1476,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     prof_end(e, s, ph, "quadtree_kernel");
     const int cap = g.out_base[L];
     ph = prof_begin(e, s);
-    describe_kernel<<<dim3((cap + 3) / 4, n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
+    describe_kernel<<<dim3((cap + 4 * DESC_R - 1) / (4 * DESC_R), n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
                                                           e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>(),
                                                           e->d_kps.as<orbx_kp>(), e->d_desc.as<uint8_t>(),
                                                           e->d_cnt.as<int>());

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
         // candidates: right keypoints whose band [floor(y-r), ceil(y+r)] contains `row`
         const unsigned long long *srt = sorted + (long long)p * a.sort_cap;
         const float ylo = (float)row - a.rmax - 2.0f;
-        int lo = 0, hi = nR;  // first entry with y >= ylo
+        int lo = 0, hi = nR;  // first entry with y >= ylo (uniform: scalar loads)
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (__uint_as_float((unsigned)(srt[mid] >> 32)) < ylo) lo = mid + 1; else hi = mid;
