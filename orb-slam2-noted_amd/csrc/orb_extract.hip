@@ -230,6 +230,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     __shared__ uint32_t trowp[((FB_TH + 8) / 2) * FB_TW];
     __shared__ uint32_t mt[FB_TH * FB_TW / 4];
     __shared__ uint16_t clist[4][512];
+    __shared__ int ccount[4];
     const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
     int t = blockIdx.x, l = 0;
     while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
@@ -239,7 +240,21 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     const int x0 = tx * FB_TW, y0 = ty * FB_TH;
     int pitch;
     const uint8_t *src = level_ptr(g, in, pyr, b, l, &pitch);
-    // 1. stage rows y0-4 .. y0+19, cols x0-4 .. x0+131
+#ifdef FB_PROFILE
+    long long fbt[8];
+#define FBP(k) do { fbt[k] = clock64(); } while (0)
+    FBP(0);
+#else
+#define FBP(k) do {} while (0)
+#endif
+    // 1. stage rows y0-4 .. y0+19, cols x0-4 .. x0+131 (interior tiles: no reflection tests)
+    if (y0 >= 4 && y0 + FB_TH + 4 <= h && x0 >= 4 && x0 + FB_TW + 4 <= w) {
+        const uint8_t *s0 = src + (long long)(y0 - 4) * pitch + (x0 - 4);
+        for (int i = threadIdx.x; i < (FB_TH + 8) * FB_LD; i += 256) {
+            const int rr = i / FB_LD, j = i - rr * FB_LD;
+            tin[i] = load_u32_unaligned(s0 + rr * pitch + 4 * j);
+        }
+    } else
     for (int i = threadIdx.x; i < (FB_TH + 8) * FB_LD; i += 256) {
         const int rr = i / FB_LD, j = i - rr * FB_LD;
         const uint8_t *rowp = src + (long long)refl101(y0 + rr - 4, h) * pitch;
@@ -259,6 +274,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;  // pixels (y0 + r, x0 + cb + i)
     const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
     const int tlo = min(th_a, th_b);
+    FBP(1);
     // 2. FAST pre-filter
     int ncand = 0;
     {
@@ -296,7 +312,9 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             if (f) clist[wv][ncand + lane_rank(bal)] = (uint16_t)((r << 7) | (cb + i));
             ncand += __popcll(bal);
         }
+        if (lane == 0) ccount[wv] = ncand;
     }
+    FBP(2);
     // 4a. blur row pass: tile rows (2p, 2p+1) x output cols 4cg .. 4cg+3
     {
         const uint32_t K0123 = 7u | 17u << 8 | 32u << 16 | 46u << 24;
@@ -325,16 +343,22 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             *(uint4 *)&trowp[p * FB_TW + 4 * cg] = v;
         }
     }
+    FBP(3);
     __syncthreads();
+    FBP(4);
     // 3. exact M for this wavefront's candidates
     {
         const uint8_t *t8 = (const uint8_t *)tin;
         uint8_t *m8 = (uint8_t *)mt;
         const int RX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
         const int RY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-        for (int base = 0; base < ncand; base += 64) {
-            if (base + lane < ncand) {
-                const int e = clist[wv][base + lane];
+        // the four wavefronts' lists pooled: wavefront wv takes pooled chunks wv, wv + 4, ...
+        // (~1 full 64-lane pass each instead of ~1.4 partly filled passes)
+        const int o1 = ccount[0], o2 = o1 + ccount[1], o3 = o2 + ccount[2], tot = o3 + ccount[3];
+        for (int base = 64 * wv; base < tot; base += 256) {
+            const int q = base + lane;
+            if (q < tot) {
+                const int e = q < o1 ? clist[0][q] : q < o2 ? clist[1][q - o1] : q < o3 ? clist[2][q - o2] : clist[3][q - o3];
                 const int rr = e >> 7, cx = e & 127;
                 const uint8_t *pc = t8 + (rr + 4) * FB_LW + cx + 4;
                 const int v = pc[0];
@@ -357,6 +381,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             }
         }
     }
+    FBP(5);
     // 4b. blur column pass: output rows 2rp, 2rp+1 x cols 4cg .. 4cg+3
     {
         const int rp = threadIdx.x >> 5, cg = threadIdx.x & 31;
@@ -393,8 +418,9 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             }
         }
     }
-    wave_lds_sync();
-    // strength map rows (written by this wavefront's lanes above)
+    __syncthreads();
+    FBP(7);
+    // strength map rows (exact M written by any wavefront of the workgroup)
     {
         const int y = y0 + r, x = x0 + cb;
         if (y < h && x < w) {
@@ -407,6 +433,12 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             }
         }
     }
+#ifdef FB_PROFILE
+    FBP(6);
+    if (threadIdx.x == 0 && blockIdx.y == 0 && (blockIdx.x % 97) == 0)
+        printf("FBPROF blk=%d l=%d stage=%lld pre=%lld rowblur=%lld bar=%lld exactM=%lld colblur=%lld store=%lld\n", blockIdx.x, l,
+               fbt[1] - fbt[0], fbt[2] - fbt[1], fbt[3] - fbt[2], fbt[4] - fbt[3], fbt[5] - fbt[4], fbt[7] - fbt[5], fbt[6] - fbt[7]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------
