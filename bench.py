@@ -333,8 +333,8 @@ def bench_bowmatch(amd, args, dist, world, with_cpu):
     return res
 
 
-def load_traffic(kernel: str, batch: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
+def load_pmc(kernel: str, batch: int, field: str = "hbm_bytes_per_launch"):
+    """Per-launch figure of `kernel` from the committed rocprofv3 PMC summary, if any."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None
@@ -342,10 +342,15 @@ def load_traffic(kernel: str, batch: int):
         d = json.loads(f.read_text())
         ent = d.get("kernels", {}).get(kernel)
         if ent and int(d.get("batch", -1)) == batch:
-            return ent.get("hbm_bytes_per_launch")
+            return ent.get(field)
     except Exception:
         return None
     return None
+
+
+# VALU issue ceiling: a wave64 VALU instruction occupies one 16-lane SIMD for 4 cycles;
+# 256 CUs x 4 SIMDs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
+VALU_SIMDS, VALU_CLOCK_HZ, VALU_CYCLES_PER_INST = 1024, 2.4e9, 4
 
 
 def main():
@@ -478,11 +483,16 @@ def main():
         name, (tot, n) = max(prof.items(), key=lambda kv: kv[1][0])
         avg_s = tot / n / 1000.0
         achieved = BYTES_PER_STEREO_FRAME * B / avg_s / 1e9
-        traffic = load_traffic(name, B)
+        traffic = load_pmc(name, B)
         out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 3),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                            "traffic": traffic, "avg_launch_ms": round(tot / n, 4),
                            "algorithmic_bytes_per_launch": BYTES_PER_STEREO_FRAME * B}
+        valu = load_pmc(name, B, "valu_insts_per_launch")
+        if valu:   # the ceiling this integer kernel actually sits against
+            out["roofline"]["valu_issue_frac"] = round(
+                valu * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (tot / n / 1e3), 4)
+            out["roofline"]["valu_insts_per_launch"] = valu
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
     if not args.no_rgbd:
         out.update(bench_rgbd(amd, args, dist, world))

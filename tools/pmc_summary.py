@@ -5,7 +5,9 @@ HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, following
 MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE (KB) reports half the bytes of wide coalesced
 reads (double it); WRITE_SIZE reads exact for streaming stores. Narrow/gather access widths
 are uncalibrated there, so the figure is an estimate; ratios between variants are exact.
-Usage: pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <batch> <out.json>
+Usage: pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <batch> <out.json> [<pmc_SQ_INSTS_VALU dir>]
+With the optional SQ_INSTS_VALU pass, each kernel also gets its VALU wave-instructions per
+launch (a wave64 VALU instruction occupies a 16-lane SIMD for 4 cycles).
 """
 import csv
 import json
@@ -32,6 +34,7 @@ def load(d: Path, counter: str):
 def main():
     fdir, wdir, batch, out = Path(sys.argv[1]), Path(sys.argv[2]), int(sys.argv[3]), Path(sys.argv[4])
     fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
+    valu = load(Path(sys.argv[5]), "SQ_INSTS_VALU") if len(sys.argv) > 5 else {}
     res = {}
     for k in sorted(set(fetch) | set(write)):
         fv, wv = fetch.get(k, []), write.get(k, [])
@@ -40,6 +43,8 @@ def main():
         res[k] = {"launches": max(len(fv), len(wv)), "FETCH_SIZE_KB": round(f_avg, 3),
                   "WRITE_SIZE_KB": round(w_avg, 3),
                   "hbm_bytes_per_launch": int((2 * f_avg + w_avg) * 1024)}
+        if valu.get(k):
+            res[k]["valu_insts_per_launch"] = int(sum(valu[k]) / len(valu[k]))
     doc = {"batch": batch, "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE read correction)",
            "kernels": res}
     out.write_text(json.dumps(doc, indent=1))
