@@ -67,7 +67,13 @@ def bench_localba(amd, args, dist, world, with_cpu):
     """C4: LocalBundleAdjustment on the synthetic 20 KF x 3000 MP graph; one LocalBA call per
     inserted keyframe (LocalMapping.cc:116-118) -> keyframes/s = calls/s, summed over ranks."""
     from orbslam2_amd import synth
-    prob = synth.localba_problem(seed=4)
+    from orbslam2_amd import dist as odist
+    # C5: rank 0 owns the map; its snapshot (poses, points, observations) reaches every rank
+    # in one RCCL broadcast over xGMI before timing (SURVEY.md §8e)
+    rank = dist.get_rank() if dist is not None else 0
+    prob = synth.localba_problem(seed=4) if rank == 0 else None
+    prob = odist.broadcast_map(prob, "cuda", dist)
+    map_bytes = int(sum(a.nbytes for a in prob.values()))
     lba = amd.LocalBundleAdjustment()
     for _ in range(2):
         r = lba.solve(prob)
@@ -77,12 +83,13 @@ def bench_localba(amd, args, dist, world, with_cpu):
     for _ in range(args.lba_steps):
         r = lba.solve(prob)
     dt = time.perf_counter() - t0
-    from orbslam2_amd import dist as odist
     dt = odist.max_over_ranks(dt, "cuda", dist)
     res = {"localba_kf_per_s": round(world * args.lba_steps / dt, 3),
            "localba": {"ms_per_call": round(1000 * dt / args.lba_steps, 3), "edges": int(len(prob["edge_point"])),
                        "keyframes": 20, "map_points": 3000, "lm_iterations": list(r["iterations"]),
-                       "dtype": "f64", "host_loop": "LM accept/reject on host, 1 readback per trial"}}
+                       "dtype": "f64", "host_loop": "LM accept/reject on host, 1 readback per trial",
+                       "map_snapshot_bytes": map_bytes,
+                       "map_source": "rank 0, RCCL broadcast" if dist is not None else "local"}}
     if with_cpu:
         sys.path.insert(0, str(ROOT / "oracle"))
         import oracle

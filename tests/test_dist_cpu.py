@@ -1,5 +1,6 @@
 """World-size-2 gloo run of the multi-GPU plumbing used by bench.py (CPU, no GPU):
-shared-state broadcast from rank 0, sequence sharding, max / sum over ranks."""
+shared-state broadcast from rank 0, map-snapshot broadcast (C5), sequence sharding,
+max / sum over ranks."""
 import os
 import socket
 
@@ -27,7 +28,11 @@ def _worker(rank, world, port, q):
     mine = list(odist.shard(8, world, rank))
     mx = odist.max_over_ranks(float(rank + 1), "cpu", dist)
     tot = odist.sum_over_ranks(float(len(mine)), "cpu", dist)
-    q.put((rank, got, mine, mx, tot))
+    from orbslam2_amd import synth
+    snap = synth.localba_problem(seed=4, n_kf=10, n_points=200) if rank == 0 else None
+    snap = odist.broadcast_map(snap, "cpu", dist)
+    digest = {k: (v.dtype.str, v.shape, v.tobytes()) for k, v in snap.items()}
+    q.put((rank, got, mine, mx, tot, digest))
     dist.destroy_process_group()
 
 
@@ -44,7 +49,12 @@ def test_gloo_world2(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     owned = []
-    for rank, got, mine, mx, tot in res:
+    from orbslam2_amd import synth
+    want = synth.localba_problem(seed=4, n_kf=10, n_points=200)
+    for rank, got, mine, mx, tot, digest in res:
+        assert sorted(digest) == sorted(want)
+        for k, a in want.items():   # map snapshot identical on every rank (dtype, shape, bytes)
+            assert digest[k] == (a.dtype.str, a.shape, a.tobytes()), k
         assert got == pytest.approx([2000, 1.2, 8, 20, 7, 386.1448, 718.856])
         assert mx == world
         assert tot == 8
