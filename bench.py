@@ -72,7 +72,7 @@ def bench_localba(amd, args, dist, world, with_cpu):
     # in one RCCL broadcast over xGMI before timing
     rank = dist.get_rank() if dist is not None else 0
     prob = synth.localba_problem(seed=4) if rank == 0 else None
-    prob = odist.broadcast_map(prob, "cuda", dist)
+    prob = odist.broadcast_map(prob, COLL_DEV, dist)
     map_bytes = int(sum(a.nbytes for a in prob.values()))
     lba = amd.LocalBundleAdjustment()
     for _ in range(2):
@@ -83,7 +83,7 @@ def bench_localba(amd, args, dist, world, with_cpu):
     for _ in range(args.lba_steps):
         r = lba.solve(prob)
     dt = time.perf_counter() - t0
-    dt = odist.max_over_ranks(dt, "cuda", dist)
+    dt = odist.max_over_ranks(dt, COLL_DEV, dist)
     res = {"localba_kf_per_s": round(world * args.lba_steps / dt, 3),
            "localba": {"ms_per_call": round(1000 * dt / args.lba_steps, 3), "edges": int(len(prob["edge_point"])),
                        "keyframes": 20, "map_points": 3000, "lm_iterations": list(r["iterations"]),
@@ -132,7 +132,7 @@ def bench_rgbd(amd, args, dist, world):
     for _ in range(args.rgbd_steps):
         step()
     amd.device_sync()
-    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    dt = odist.max_over_ranks(time.perf_counter() - t0, COLL_DEV, dist)
     n, m, _ = ex.search_init_fetch(0)
     return {"c3_rgbd_frames_per_s": round(world * T * args.rgbd_steps / dt, 2),
             "c3": {"frames_per_step": T, "ms_per_step": round(1000 * dt / args.rgbd_steps, 3),
@@ -168,7 +168,7 @@ def bench_track(amd, args, dist, world, with_cpu):
     for _ in range(args.track_steps):
         step()
     amd.device_sync()
-    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    dt = odist.max_over_ranks(time.perf_counter() - t0, COLL_DEV, dist)
     nm, _, _ = t.fetch(0, 2000)
     # ORBmatcher::Fuse(pKF, vpMapPoints, 3) search half over the same (keyframe, 3000 points)
     t.run_fuse_batch(B, 3.0)
@@ -177,7 +177,7 @@ def bench_track(amd, args, dist, world, with_cpu):
     for _ in range(args.track_steps):
         t.run_fuse_batch(B, 3.0)
     amd.device_sync()
-    fdt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    fdt = odist.max_over_ranks(time.perf_counter() - t0, COLL_DEV, dist)
     res = {"track_frames_per_s": round(world * B * args.track_steps / dt, 2),
            "track": {"frames_per_step": B, "ms_per_step": round(1000 * dt / args.track_steps, 3),
                      "keypoints": 2000, "map_points": 3000, "last_keypoints": 1500,
@@ -221,7 +221,7 @@ def bench_pose(amd, args, dist, world, with_cpu):
     for _ in range(args.pose_steps):
         po.run_batch(B)
     amd.device_sync()
-    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    dt = odist.max_over_ranks(time.perf_counter() - t0, COLL_DEV, dist)
     r = po.fetch(0, 800)
     res = {"pose_frames_per_s": round(world * B * args.pose_steps / dt, 2),
            "pose": {"frames_per_step": B, "ms_per_step": round(1000 * dt / args.pose_steps, 3), "edges": 800,
@@ -270,7 +270,7 @@ def bench_bow(amd, args, dist, world, with_cpu):
     for _ in range(args.bow_steps):
         step()
     amd.device_sync()
-    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    dt = odist.max_over_ranks(time.perf_counter() - t0, COLL_DEV, dist)
     r = V.batch_fetch(0, N)
     res = {"bow_frames_per_s": round(world * B * args.bow_steps / dt, 2),
            "bow": {"frames_per_step": B, "ms_per_step": round(1000 * dt / args.bow_steps, 3), "features": N,
@@ -318,7 +318,7 @@ def bench_bowmatch(amd, args, dist, world, with_cpu):
     for _ in range(args.bowmatch_steps):
         step()
     amd.device_sync()
-    dt = odist.max_over_ranks(time.perf_counter() - t0, "cuda", dist)
+    dt = odist.max_over_ranks(time.perf_counter() - t0, COLL_DEV, dist)
     pairs0 = m.fetch(0, True, 2000)
     res = {"bowmatch_pairs_per_s": round(world * B * args.bowmatch_steps / dt, 2),
            "bowmatch": {"pairs_per_step": B, "ms_per_step": round(1000 * dt / args.bowmatch_steps, 3),
@@ -359,6 +359,11 @@ def load_pmc(kernel: str, batch: int, field: str = "hbm_bytes_per_launch"):
 # 256 CUs x 4 SIMDs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
 VALU_SIMDS, VALU_CLOCK_HZ, VALU_CYCLES_PER_INST = 1024, 2.4e9, 4
 
+# collectives: RCCL ("nccl") on device tensors; ORBSLAM_DIST_BACKEND=gloo (CPU tensors) is
+# only for rehearsing the multi-rank path with several ranks sharing one GPU
+DIST_BACKEND = os.environ.get("ORBSLAM_DIST_BACKEND", "nccl")
+COLL_DEV = "cuda" if DIST_BACKEND == "nccl" else "cpu"
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -395,20 +400,24 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
-    torch.cuda.set_device(local_rank)
+    device = local_rank % max(torch.cuda.device_count(), 1)   # one GPU per rank (wraps only in rehearsals)
+    torch.cuda.set_device(device)
     torch.cuda.init()
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if DIST_BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(DIST_BACKEND)
     import orbslam2_amd as amd
-    amd.set_device(local_rank)
+    amd.set_device(device)
 
     from orbslam2_amd import dist as odist
     B = args.batch
     # shared read-only state: ORB params + camera, broadcast once from rank 0 over RCCL
     nf, sf, nl, ith, mth, bf, fx, w, h = odist.broadcast_shared(
-        [NFEAT, 1.2, 8, 20, 7, KITTI_BF, KITTI_FX, W, H] if rank == 0 else [0] * 9, "cuda", dist)
+        [NFEAT, 1.2, 8, 20, 7, KITTI_BF, KITTI_FX, W, H] if rank == 0 else [0] * 9, COLL_DEV, dist)
     mb = float(np.float32(bf) / np.float32(fx))
 
     pool = make_pool(args.pool, 2 + 100 * rank)
@@ -451,7 +460,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = ex.profile_read() if not args.no_profile else {}
     ex.profile(False)
-    elapsed = odist.max_over_ranks(elapsed, "cuda", dist)
+    elapsed = odist.max_over_ranks(elapsed, COLL_DEV, dist)
 
     # sanity: the batch produced keypoints and stereo matches
     k0, _ = ex.fetch(0)
