@@ -87,7 +87,7 @@ def bench_localba(amd, args, dist, world, with_cpu):
     res = {"localba_kf_per_s": round(world * args.lba_steps / dt, 3),
            "localba": {"ms_per_call": round(1000 * dt / args.lba_steps, 3), "edges": int(len(prob["edge_point"])),
                        "keyframes": 20, "map_points": 3000, "lm_iterations": list(r["iterations"]),
-                       "dtype": "f64", "host_loop": "LM accept/reject on host, 1 readback per trial",
+                       "dtype": "f64", "lm_control": "device-resident LM state (lba_decide), one host readback per chunk of trials",
                        "map_snapshot_bytes": map_bytes,
                        "map_source": "rank 0, RCCL broadcast" if dist is not None else "local"}}
     if with_cpu:

@@ -23,8 +23,14 @@
 //   lba_update        x_l = Dinv (b_l - Hpl^T x_p), T <- exp(x_p) T (SE3Quat::exp,
 //                     left-multiplied), X <- X + x_l, computeScale block sums
 //   lba_errors        trial residuals (kept as g2o's stale _error) + robust chi2 block sums
-// The LM accept/reject/lambda logic (optimization_algorithm_levenberg.cpp:61-164) runs on
-// the host with one readback per trial (flags + the block sums, summed in block order).
+//   lba_decide        the LM accept/reject/lambda logic (optimization_algorithm_levenberg.cpp
+//                     :61-164) and SparseOptimizer::optimize's stop rules on one thread: block
+//                     sums in block order, rho, lambda / nu, nBad; the accepted trial is copied
+//                     into the current estimate
+// The LM state lives on the device (LMState): every kernel of a trial slot reads it and
+// returns at once when the optimisation has finished (the linearisation kernels also when the
+// slot is a retry of the same iteration). The host enqueues slots in chunks and reads the
+// state back once per chunk instead of once per trial.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -56,6 +62,12 @@ constexpr int kSmallNP = 128;        // Schur dimension factored in one workgrou
 constexpr int kMaxPoses = 2048;      // 6 * 2048 = 12288: Hs 1.2 GB, far beyond any LocalBA window
 constexpr int kCB = 32;              // blocked Cholesky panel width (Schur dimension > kSmallNP)
 constexpr int kRedBlocks = 16384;    // partial-sum region stride (blocks) for scalar reductions
+
+// device-resident LM control (optimization_algorithm_levenberg.cpp:61-164 state)
+struct LMState {
+    double lambda, ni, currentChi, iniChi, rho, final_chi;
+    int qmax, nBad, it, iterations, done, newiter, accepted, pad;
+};
 
 struct EdgeDev {
     int point, pose;
@@ -95,6 +107,7 @@ struct Graph {
     double *x;             // [6P + 3Lm]
     double *partial;       // [4][kRedBlocks]
     double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok, lambda
+    LMState *lm;
     int Kpad, S;
     int NP;                // Schur dimension 6P padded to a multiple of kCB
     int NPW, wrow;         // slab leading dimension; Y row holding w (16 * ceil(6P / 16))
@@ -145,6 +158,7 @@ __device__ inline void block_sum_to(double v, double *dst) {
 
 // ---- linearize: errors + robust chi2 + per-edge quadratic-form pieces
 __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
+    if (g.lm->done || !g.lm->newiter) return;
     const int s = blockIdx.x * 256 + threadIdx.x;
     double rchi = 0;
     if (s < g.nact) {
@@ -236,6 +250,7 @@ __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
 }
 
 __global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
+    if (g.lm->done || !g.lm->newiter) return;
     const int l = blockIdx.x * 256 + threadIdx.x;
     double dmax = 0;
     if (l < g.Lm) {
@@ -274,6 +289,7 @@ __global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
 // accumulates component k (Hpp upper 21 + b_p 6) of every 32nd slot, coalesced 216-byte slot
 // reads; the 32 group partials are summed in LDS in fixed order
 __global__ __launch_bounds__(1024) void lba_reduce_poses(Graph g) {
+    if (g.lm->done || !g.lm->newiter) return;
     const int i = blockIdx.x, k = threadIdx.x & 31, grp = threadIdx.x >> 5;
     const int t0 = g.ps_start[i], t1 = g.ps_start[i + 1];
     double acc = 0;
@@ -347,9 +363,11 @@ __device__ inline void point_factor(const Graph &g, int l, double lambda, double
 // mode 1: block 0 also finishes the linearisation's chi2 reduction -> scalars[0];
 // mode 2 (first trial of the first iteration): every block reduces chi2 and maxDiagonal and
 // uses lambda = tau * maxDiagonal (tau = 1e-5, optimization_algorithm_levenberg.cpp:179-191);
-// otherwise lambda = lambda_arg. Block 0 publishes lambda in scalars[5].
-__global__ __launch_bounds__(256) void lba_prep_slots(Graph g, double lambda_arg, int mode, int n0, int n1, int n2) {
-    double lambda = lambda_arg;
+// otherwise lambda = the LM state's. Block 0 publishes lambda in scalars[5].
+__global__ __launch_bounds__(256) void lba_prep_slots(Graph g, int n0, int n1, int n2) {
+    if (g.lm->done) return;
+    const int mode = g.lm->newiter ? (g.lm->it == 0 ? 2 : 1) : 0;
+    double lambda = g.lm->lambda;
     if (mode == 2 || (mode == 1 && blockIdx.x == 0)) {   // uniform per block
         __shared__ double sa[256], sb[256];
         double a = 0, b = 0;
@@ -405,6 +423,7 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 // interleaving 4-column steps of the slice and summing in LDS; slab[s] = partial tile sums.
 // Tile pairs run over ntile + 1 tile rows (the last one holds w) without the (w, w) tile.
 __global__ __launch_bounds__(256) void lba_syrk_mfma(Graph g, int ntile1, int kchunk) {
+    if (g.lm->done) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int pair = blockIdx.x, I = 0;
     while (pair >= ntile1 - I) { pair -= ntile1 - I; I++; }
@@ -439,6 +458,7 @@ __global__ __launch_bounds__(256) void lba_syrk_mfma(Graph g, int ntile1, int kc
     }
 }
 __global__ __launch_bounds__(256) void lba_schur_reduce(Graph g) {
+    if (g.lm->done) return;
     const double lambda = g.scalars[5];
     const int n6 = 6 * g.P;
     const int r = blockIdx.x;  // row
@@ -523,6 +543,7 @@ __host__ __device__ constexpr size_t chol_tiled_lds(int n) {
 __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
     extern __shared__ double A[];   // N2 x LDA, then Linv[NT][16][17], y[N2], x[N2]
     __shared__ int fail;
+    if (g.lm->done) return;
     const int n = 6 * g.P, N2 = chol_tiled_dim(n), NT = N2 / 16, LDA = N2 + 1;
     double *Linv = A + N2 * LDA, *yv = Linv + NT * 16 * 17, *xv = yv + N2;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -678,6 +699,7 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
 // 16 x 16 tile, K = 32 = 8 x v_mfma_f64_16x16x4f64).
 __global__ __launch_bounds__(256) void lba_chol_panel(Graph g, int kb) {
     __shared__ double D[kCB][kCB + 1];
+    if (g.lm->done) return;
     const int n = 6 * g.P, tid = threadIdx.x;
     const long long NP = g.NP;
     const int nb = min(kCB, n - kb);
@@ -728,6 +750,7 @@ __global__ __launch_bounds__(256) void lba_chol_panel(Graph g, int kb) {
 }
 
 __global__ __launch_bounds__(64) void lba_chol_update(Graph g, int kb, int ntile) {
+    if (g.lm->done) return;
     // lower 16 x 16 tiles (I >= J) of the trailing matrix, rows / cols >= kb + kCB
     const int lane = threadIdx.x;
     int t = blockIdx.x, I = 0;
@@ -753,6 +776,7 @@ __global__ __launch_bounds__(64) void lba_chol_update(Graph g, int kb, int ntile
 // solves each 32-row diagonal block serially, then every thread updates the remaining rows.
 __global__ __launch_bounds__(1024) void lba_chol_solve_blocked(Graph g) {
     extern __shared__ double y[];
+    if (g.lm->done) return;
     const int n = 6 * g.P, tid = threadIdx.x;
     const long long NP = g.NP;
     const double *L = g.Hs;
@@ -800,12 +824,15 @@ __global__ __launch_bounds__(1024) void lba_chol_solve_blocked(Graph g) {
     for (int i = tid; i < n; i += 1024) g.x[i] = y[i];
 }
 
-__global__ void lba_set_ok(Graph g) { g.scalars[4] = 1; }
+__global__ void lba_set_ok(Graph g) {
+    if (!g.lm->done) g.scalars[4] = 1;
+}
 
 // landmark back substitution x_l = Dinv (b_l - Hpl^T x_p) fused with the update
 // T <- exp(x_p) T (SE3Quat::exp, left-multiplied), X <- X + x_l into the trial buffers and the
 // computeScale pieces x (lambda x + b) of the thread's own entries, block sums -> part[]
 __global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
+    if (g.lm->done) return;
     const int t = blockIdx.x * 256 + threadIdx.x;
     const double lambda = g.scalars[5];
     double sc = 0;
@@ -848,6 +875,7 @@ __global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
     block_sum_to(sc, part + blockIdx.x);
 }
 __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part) {
+    if (g.lm->done) return;
     const int s = blockIdx.x * 256 + threadIdx.x;
     double r0 = 0;
     if (s < g.nact) {
@@ -862,6 +890,77 @@ __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part) {
         if (e.robust) huber(e, chi, r0, r1);
     }
     block_sum_to(r0, part + blockIdx.x);
+}
+
+// SparseOptimizer::optimize(iterations) start: lambda / nu / nBad reset (levenberg.cpp:66-72)
+__global__ void lba_lm_init(Graph g, int iterations) {
+    LMState s{};
+    s.ni = 2;
+    s.iterations = iterations;
+    s.newiter = 1;
+    s.done = iterations <= 0;
+    *g.lm = s;
+}
+
+// End of one LM trial (optimization_algorithm_levenberg.cpp:96-164 + the ORB-SLAM2 stop rule
+// :155-161): thread 0 sums the update's computeScale block sums and the trial chi2 block sums
+// in block order, decides, and advances the state; an accepted trial becomes the current
+// estimate (copy T2 -> T, X2 -> X by the whole workgroup).
+__global__ __launch_bounds__(1024) void lba_decide(Graph g, int nbu, int nbe, int np, int nq) {
+    __shared__ int acc;
+    if (g.lm->done) return;
+    if (threadIdx.x == 0) {
+        LMState s = *g.lm;
+        const double *sc = g.scalars;
+        if (s.qmax == 0) {
+            s.currentChi = s.iniChi = sc[0];
+            if (s.it == 0) s.lambda = sc[5];   // tau * maxDiagonal, formed by lba_prep_slots
+        }
+        double sc_sum = 0, chi_sum = 0;
+        for (int b = 0; b < nbu; b++) sc_sum += sc[8 + b];
+        for (int b = 0; b < nbe; b++) chi_sum += sc[8 + nbu + b];
+        const double tempChi = sc[4] != 0 ? chi_sum : DBL_MAX;
+        double rho = s.currentChi - tempChi;
+        const double scale = sc_sum + 1e-3;
+        rho /= scale;
+        int a = 0;
+        if (rho > 0 && isfinite(tempChi)) {   // good step: discardTop
+            double alpha = 1. - pow((2 * rho - 1), 3.0);
+            alpha = fmin(alpha, 2. / 3.);
+            s.lambda *= fmax(1. / 3., alpha);
+            s.ni = 2;
+            s.currentChi = tempChi;
+            a = 1;
+        } else {                               // bad step: pop
+            s.lambda *= s.ni;
+            s.ni *= 2;
+        }
+        s.qmax++;
+        s.rho = rho;
+        s.accepted = a;
+        if (rho < 0 && s.qmax < 10) {
+            s.newiter = 0;                     // retry the same linearisation
+        } else {
+            s.it++;
+            s.final_chi = s.currentChi;
+            bool ok = true;
+            if (s.qmax == 10 || rho == 0) ok = false;
+            else {
+                if ((s.iniChi - s.currentChi) * 1e3 < s.iniChi) s.nBad++; else s.nBad = 0;
+                if (s.nBad >= 3) ok = false;
+            }
+            s.newiter = 1;
+            s.qmax = 0;
+            if (!ok || s.it >= s.iterations) s.done = 1;
+        }
+        *g.lm = s;
+        acc = a;
+    }
+    __syncthreads();
+    if (acc) {
+        for (int i = threadIdx.x; i < np; i += 1024) g.T[i] = g.T2[i];
+        for (int i = threadIdx.x; i < 3 * nq; i += 1024) g.X[i] = g.X2[i];
+    }
 }
 
 // outlier test of Optimizer.cc:925-962 / 977-1008: chi2 (stale _error) + depth sign
@@ -905,8 +1004,9 @@ struct lba_engine {
     hipStream_t stream = nullptr;
     DBuf T, T2, X, X2, E, err, act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items,
         ps_start, ps_items, slot_pt, slot_ph, con, hpl, Hll, bl, Hpp, bp, Dinv, Lc, Y, slab, Hs, bs, x, partial,
-        scalars, flags;
+        scalars, flags, lm;
     double *h_scalars = nullptr;  // pinned
+    LMState *h_lm = nullptr;      // pinned
 };
 
 namespace {
@@ -977,100 +1077,72 @@ int nblk(int n) { return std::max(1, (n + 255) / 256); }
 }  // namespace
 
 // One SparseOptimizer::optimize(iterations) on the device; returns iterations run.
-static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterations,
+// Trial slots (linearisation + setLambda/Schur/solve/update/errors + lba_decide) are enqueued
+// in chunks without host synchronisation; the device LM state turns the slots after the
+// last trial into no-ops. One state readback per chunk (the stop flag is polled there).
+static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterations, int np, int nq,
                         const volatile uint8_t *stop, double *final_chi) {
     hipStream_t s = e->stream;
     auto term = [&]() { return stop && *stop; };
     if (A.P + A.Lm == 0) return -1;
     if (A.P > kMaxPoses) return -2;
-    double lambda = 0, ni = 2;
-    int nBad = 0, it = 0;
     const int nact = (int)A.act.size();
     const int n6 = 6 * A.P;
     const int ntile1 = std::max(1, (n6 + 15) / 16) + 1;        // + the w tile row
     const int npair = ntile1 * (ntile1 + 1) / 2 - 1;           // without (w, w)
-    for (int i = 0; i < iterations && !term(); i++) {
+    const int nbu = nblk(A.P + A.Lm), nbe = nblk(nact);
+    auto slot = [&]() {
         lba_linearize<<<nblk(nact), 256, 0, s>>>(g);
         lba_reduce_points<<<nblk(A.Lm), 256, 0, s>>>(g);
         if (A.P > 0) lba_reduce_poses<<<A.P, 1024, 0, s>>>(g);
-        // no readback here: chi2 / maxDiagonal are finished by the trial's first kernel (the
-        // first lambda is formed there) and come back with the trial's scalars, one
-        // synchronisation per trial
-        double currentChi = 0, iniChi = 0, tempChi;
-        if (i == 0) { ni = 2; nBad = 0; }
-        double rho = 0;
-        int qmax = 0;
-        do {
-            // setLambda + Schur + solve + update + errors (push/pop = T/T2 double buffering)
-            const int mode = qmax > 0 ? 0 : (i == 0 ? 2 : 1);
-            lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, lambda, mode, nblk(nact), nblk(A.Lm), A.P);
-            if (A.P > 0) {
-                const int kchunk = (((g.Kpad + g.S - 1) / g.S + 3) / 4) * 4;  // S * kchunk >= Kpad
-                lba_syrk_mfma<<<dim3(npair, g.S), 256, 0, s>>>(g, ntile1, kchunk);
-                lba_schur_reduce<<<n6, 256, 0, s>>>(g);   // slab sums: spread over n6 workgroups
-                if (n6 <= kSmallNP) {
-                    lba_chol_tiled<<<1, 512, chol_tiled_lds(n6), s>>>(g);
-                } else {
-                    lba_set_ok<<<1, 1, 0, s>>>(g);
-                    for (int kb = 0; kb < n6; kb += kCB) {
-                        const int rows = n6 - kb - kCB;
-                        lba_chol_panel<<<std::max(1, (rows + 255) / 256), 256, 0, s>>>(g, kb);
-                        if (rows > 0) {
-                            const int nt = (rows + 15) / 16;
-                            lba_chol_update<<<nt * (nt + 1) / 2, 64, 0, s>>>(g, kb, nt);
-                        }
-                    }
-                    lba_chol_solve_blocked<<<1, 1024, sizeof(double) * n6, s>>>(g);
-                }
+        lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nblk(nact), nblk(A.Lm), A.P);
+        if (A.P > 0) {
+            const int kchunk = (((g.Kpad + g.S - 1) / g.S + 3) / 4) * 4;  // S * kchunk >= Kpad
+            lba_syrk_mfma<<<dim3(npair, g.S), 256, 0, s>>>(g, ntile1, kchunk);
+            lba_schur_reduce<<<n6, 256, 0, s>>>(g);   // slab sums: spread over n6 workgroups
+            if (n6 <= kSmallNP) {
+                lba_chol_tiled<<<1, 512, chol_tiled_lds(n6), s>>>(g);
             } else {
                 lba_set_ok<<<1, 1, 0, s>>>(g);
+                for (int kb = 0; kb < n6; kb += kCB) {
+                    const int rows = n6 - kb - kCB;
+                    lba_chol_panel<<<std::max(1, (rows + 255) / 256), 256, 0, s>>>(g, kb);
+                    if (rows > 0) {
+                        const int nt = (rows + 15) / 16;
+                        lba_chol_update<<<nt * (nt + 1) / 2, 64, 0, s>>>(g, kb, nt);
+                    }
+                }
+                lba_chol_solve_blocked<<<1, 1024, sizeof(double) * n6, s>>>(g);
             }
-            // scalars[8..): the update's computeScale block sums, then the trial chi2 block sums,
-            // summed here in block order (one readback for the whole trial)
-            const int nbu = nblk(A.P + A.Lm), nbe = nblk(nact);
-            lba_update<<<nbu, 256, 0, s>>>(g, g.scalars + 8);
-            lba_errors<<<nbe, 256, 0, s>>>(g, g.scalars + 8 + nbu);
-            if (hipMemcpyAsync(e->h_scalars, g.scalars, (8 + nbu + nbe) * sizeof(double), hipMemcpyDeviceToHost, s) !=
-                    hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess)
-                return -3;
-            if (qmax == 0) {
-                currentChi = iniChi = e->h_scalars[0];
-                if (i == 0) lambda = 1e-5 * e->h_scalars[1];   // the value the device used
-            }
-            double sc_sum = 0, chi_sum = 0;
-            for (int b = 0; b < nbu; b++) sc_sum += e->h_scalars[8 + b];
-            for (int b = 0; b < nbe; b++) chi_sum += e->h_scalars[8 + nbu + b];
-            const bool ok2 = e->h_scalars[4] != 0;
-            tempChi = ok2 ? chi_sum : DBL_MAX;
-            rho = currentChi - tempChi;
-            double scale = sc_sum + 1e-3;
-            rho /= scale;
-            if (rho > 0 && std::isfinite(tempChi)) {
-                double alpha = 1. - std::pow((2 * rho - 1), 3);
-                alpha = std::min(alpha, 2. / 3.);
-                lambda *= std::max(1. / 3., alpha);
-                ni = 2;
-                currentChi = tempChi;
-                std::swap(g.T, g.T2);     // discardTop: keep the trial estimate
-                std::swap(g.X, g.X2);
-            } else {
-                lambda *= ni;
-                ni *= 2;                  // pop: keep the current estimate
-            }
-            qmax++;
-        } while (rho < 0 && qmax < 10 && !term());
-        it++;
-        *final_chi = currentChi;
-        bool ok = true;
-        if (qmax == 10 || rho == 0) ok = false;
-        else {
-            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++; else nBad = 0;
-            if (nBad >= 3) ok = false;
+        } else {
+            lba_set_ok<<<1, 1, 0, s>>>(g);
         }
-        if (!ok) break;
+        // scalars[8..): the update's computeScale block sums, then the trial chi2 block sums
+        lba_update<<<nbu, 256, 0, s>>>(g, g.scalars + 8);
+        lba_errors<<<nbe, 256, 0, s>>>(g, g.scalars + 8 + nbu);
+        lba_decide<<<1, 1024, 0, s>>>(g, nbu, nbe, np, nq);
+    };
+    lba_lm_init<<<1, 1, 0, s>>>(g, iterations);
+    // first chunk: one trial per iteration plus one retry; then two slots per chunk
+    int chunk = iterations + 1, slots = 0;
+    LMState st{};
+    while (true) {
+        for (int k = 0; k < chunk; k++) slot();
+        slots += chunk;
+        if (hipMemcpyAsync(e->h_lm, g.lm, sizeof(LMState), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -3;
+        st = *e->h_lm;
+        if (st.done) break;
+        if (term()) {   // stop flag: the trial loop and the iteration loop end here
+            if (!st.newiter) { st.it++; st.final_chi = st.currentChi; }
+            break;
+        }
+        if (slots > 10 * iterations + 1) return -3;   // cannot happen: <= 10 trials per iteration
+        chunk = 2;
     }
-    return it;
+    *final_chi = st.final_chi;
+    return st.it;
 }
 
 extern "C" {
@@ -1081,7 +1153,8 @@ int lba_create(lba_engine **out) {
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORBX_EDEVICE;
     lba_engine *e = new lba_engine();
     if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void **)&e->h_scalars, (8 + 2 * kRedBlocks) * sizeof(double)) != hipSuccess) {
+        hipHostMalloc((void **)&e->h_scalars, (8 + 2 * kRedBlocks) * sizeof(double)) != hipSuccess ||
+        hipHostMalloc((void **)&e->h_lm, sizeof(LMState)) != hipSuccess) {
         delete e;
         return ORBX_EDEVICE;
     }
@@ -1094,6 +1167,7 @@ void lba_destroy(lba_engine *e) {
     (void)hipSetDevice(e->device);
     if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
     if (e->h_scalars) (void)hipHostFree(e->h_scalars);
+    if (e->h_lm) (void)hipHostFree(e->h_lm);
     delete e;
 }
 
@@ -1150,7 +1224,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     if (upload(e->T, T, s) || upload(e->T2, T, s) || upload(e->X, X, s) || upload(e->X2, X, s) ||
         upload(e->E, E, s) || e->err.ensure(sizeof(double) * 3 * std::max(ne, 1)) ||
         e->flags.ensure(std::max(ne, 1)) || e->scalars.ensure((8 + 2 * kRedBlocks) * sizeof(double)) ||
-        e->partial.ensure(sizeof(double) * 4 * kRedBlocks))
+        e->partial.ensure(sizeof(double) * 4 * kRedBlocks) || e->lm.ensure(sizeof(LMState)))
         return ORBX_EDEVICE;
     LBA_CHK(hipMemsetAsync(e->err.p, 0, sizeof(double) * 3 * std::max(ne, 1), s));
     Graph g{};
@@ -1160,6 +1234,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     g.err = e->err.as<double>();
     g.scalars = e->scalars.as<double>();
     g.partial = e->partial.as<double>();
+    g.lm = e->lm.as<LMState>();
     auto setup = [&](ActiveSet &A) -> int {
         if (upload(e->act, A.act, s) || upload(e->pose_hidx, A.pose_hidx, s) || upload(e->point_hidx, A.point_hidx, s) ||
             upload(e->hpose, A.hpose, s) || upload(e->hpoint, A.hpoint, s) || upload(e->pt_start, A.pt_start, s) ||
@@ -1210,7 +1285,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     ActiveSet A;
     build_active(h, A);
     if (setup(A)) return ORBX_EDEVICE;
-    r->iterations[0] = lba_optimize(e, g, A, 5, stop, &r->chi2[0]);
+    r->iterations[0] = lba_optimize(e, g, A, 5, np, nq, stop, &r->chi2[0]);
     if (r->iterations[0] < -1) return ORBX_EINVAL;
     const bool bDoMore = !(stop && *stop);
     std::vector<uint8_t> flag(std::max(ne, 1));
@@ -1226,7 +1301,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.E = e->E.as<EdgeDev>();
         build_active(h, A);
         if (setup(A)) return ORBX_EDEVICE;
-        r->iterations[1] = lba_optimize(e, g, A, 10, stop, &r->chi2[1]);
+        r->iterations[1] = lba_optimize(e, g, A, 10, np, nq, stop, &r->chi2[1]);
     } else {
         r->stopped = 1;
     }
