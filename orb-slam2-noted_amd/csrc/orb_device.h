@@ -121,4 +121,8 @@ __device__ __forceinline__ int key_y(uint32_t k) { return (int)(k >> 20); }
 
 __device__ __forceinline__ int wave_lane() { return (int)__lane_id(); }
 
+// wavefront index inside the workgroup as a wave-uniform (SGPR) value: lets the compiler keep
+// everything derived from it (slot / cell / keypoint ids, their loads and branches) scalar
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 }  // namespace orbamd

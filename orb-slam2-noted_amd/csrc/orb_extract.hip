@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         tin[i] = v;
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = wave_id();
     const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;  // pixels (y0 + r, x0 + cb + i)
     const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
     const int tlo = min(th_a, th_b);
@@ -457,7 +457,7 @@ __device__ __forceinline__ int thr_score(int m, int th) { return m > th ? m - 1 
 __global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const CellDesc *cells, const uint8_t *mmap,
                                                        int *cell_cnt, uint32_t *cell_keys) {
     extern __shared__ uint32_t nms_lds[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = wave_id();
     int bxr, b;
     xcd_remap2(bxr, b);
     const int c = bxr * 4 + wv;
@@ -619,7 +619,7 @@ struct QShared {
 __device__ __forceinline__ unsigned long long shfl_up64(unsigned long long v, int off) { return __shfl_up(v, off, 64); }
 
 __device__ __forceinline__ QCnt block_scan(QShared &S, QCnt v, QCnt *total, int &par) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = wave_id();
     QCnt incl = v;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1097,22 +1097,29 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
 }
 
 // ------------------------------------------------------------------------------------
-// K5: IC_Angle (:94-141) + computeOrbDescriptor (:153-204) + keypoint assembly
-// (:1603-1657). One wavefront per selected keypoint; the moments are exact integer
-// wave reductions, the 256 tests are packed with one ballot per 64 bits.
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+// exact integer wavefront sum on DPP (quad perms, half-row / row mirrors, row broadcasts
+// 15 / 31), result read from lane 63 -- no LDS traffic
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
-__device__ __forceinline__ void describe_one(const ExtractGeom &g, const uint8_t *in, const uint8_t *pyr,
-                                             const uint8_t *blur, const uint32_t *sel, const int *sel_cnt,
-                                             orbx_kp *kps, uint8_t *desc, int *cnt, int slot, int b, int lane,
-                                             uint32_t *patch, const uint2 (&icw)[4], const uint32_t (&pat)[4]) {
+// wave-uniform location of one output slot: level, output row, packed key
+struct DescSlot {
+    int valid, l, off;
+    uint32_t key;
+};
+
+__device__ __forceinline__ DescSlot desc_slot(const ExtractGeom &g, const uint32_t *sel, const int *sel_cnt, int *cnt,
+                                              int slot, int b, int lane) {
+    DescSlot d{0, 0, 0, 0u};
     const int L = g.nlevels, cap = g.out_base[L];
-    if (slot >= cap) return;
+    if (slot >= cap) return d;
     int l = 0;
     while (l + 1 < L && slot >= g.out_base[l + 1]) l++;
     const int idx = slot - g.out_base[l];
@@ -1122,116 +1129,161 @@ __device__ __forceinline__ void describe_one(const ExtractGeom &g, const uint8_t
         for (int k = 0; k < L; k++) tot += sc[k];
         cnt[b] = tot;
     }
-    if (idx >= sc[l]) return;
+    if (idx >= sc[l]) return d;
     int off = idx;
     for (int k = 0; k < l; k++) off += sc[k];
-    const uint32_t key = sel[(long long)b * cap + slot];
-    const int x = key_x(key) + 16, y = key_y(key) + 16;  // + minBorderX/Y (:1177-1186)
-    int pitch;
-    const uint8_t *img = level_ptr(g, in, pyr, b, l, &pitch);
-    // IC_Angle over the circular patch (|u| <= umax[|v|]): rows v = -15..15 as 8 dwords
-    // (u = -16..15), sum_u u*p = sum (u+16)*p - 16 * sum p with v_dot4_u32_u8 (exact integers)
-    const uint8_t *rowc = img + (long long)y * pitch + x - 16;
-    int m01 = 0, m10 = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int j = lane + 64 * k;
-        if (j < 31 * 8) {
-            const int v = (j >> 3) - 15, w = j & 7;
-            const uint2 wt = icw[k];
-            const uint32_t P = load_u32_unaligned(rowc + (long long)v * pitch + 4 * w);
-            const int su = (int)__builtin_amdgcn_udot4(P, wt.x, 0u, false);
-            const int sm = (int)__builtin_amdgcn_udot4(P, wt.y, 0u, false);
-            m10 += su - 16 * sm;
-            m01 += v * sm;
-        }
-    }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
-    // wave-uniform from here: keep the angle in an SGPR so sincosf's tables are scalar loads
-    const float angle = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fast_atan2_deg((float)m01, (float)m10))));
-    // steered BRIEF on the blurred level
-    const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
-    float sa, ca;
-    glibc_sincosf(angle * factorPI, &sa, &ca);
-    const float a = ca, bs = sa;
-    const int bw = g.bp[l];
-    // the rotated pattern stays within +-18 pixels (|rot(p)| <= 13 sqrt 2): stage the 37 rows x
-    // 40 bytes around the keypoint (dword-aligned; the pitch is 16-aligned so every row has the
-    // same misalignment sh) into this wavefront's LDS with coalesced dword loads, then run
-    // the 512 byte tests from LDS instead of as scattered global gathers. Flat addresses as
-    // before (row * pitch + column), clamped into the blur buffer.
-    const long long lvl0 = (long long)b * g.blur_stride + g.blur_off[l];
-    const long long c0 = lvl0 + (long long)(y - 18) * bw + (x - 18);
-    const int sh = (int)(c0 & 3);
-    const long long a0 = c0 - sh, amax = (long long)g.nimg * g.blur_stride - 4;
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-        const int idx = lane + 64 * k;
-        if (idx < 370) {
-            const int rr = idx / 10, q = idx - rr * 10;
-            long long ad = a0 + (long long)rr * bw + 4 * q;
-            ad = ad < 0 ? 0 : (ad > amax ? amax & ~3LL : ad);
-            patch[idx] = *(const uint32_t *)(blur + ad);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint8_t *pc = (const uint8_t *)patch + 18 * 40 + 18 + sh;   // (dy, dx) -> pc[dy * 40 + dx]
-    unsigned long long words[4];
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const uint32_t pw = pat[w];   // pattern pair w * 64 + lane: x0 y0 x1 y1 as int8
-        const float px0 = (float)(int8_t)(pw & 0xFF), py0 = (float)(int8_t)((pw >> 8) & 0xFF);
-        const float px1 = (float)(int8_t)((pw >> 16) & 0xFF), py1 = (float)(int8_t)(pw >> 24);
-        const int t0 = pc[cv_round_f(px0 * bs + py0 * a) * 40 + cv_round_f(px0 * a - py0 * bs)];
-        const int t1 = pc[cv_round_f(px1 * bs + py1 * a) * 40 + cv_round_f(px1 * a - py1 * bs)];
-        words[w] = __ballot(t0 < t1);
-    }
-    __builtin_amdgcn_wave_barrier();   // patch reused by this wavefront's next slot
-    const long long o = (long long)b * cap + off;
-    if (lane == 0) {
-        unsigned long long *d = (unsigned long long *)(desc + o * 32);
-        d[0] = words[0]; d[1] = words[1]; d[2] = words[2]; d[3] = words[3];
-        orbx_kp kp;
-        const float s = g.scale[l];
-        kp.x = (float)x;
-        kp.y = (float)y;
-        if (l != 0) { kp.x *= s; kp.y *= s; }  // :1642-1651
-        kp.size = (float)g.scaled_patch[l];
-        kp.angle = angle;
-        kp.response = (float)key_score(key);
-        kp.octave = l;
-        kp.class_id = -1;
-        kps[o] = kp;
-    }
+    d.valid = 1;
+    d.l = l;
+    d.off = off;
+    d.key = sel[(long long)b * cap + slot];
+    return d;
 }
 
-// DESC_R consecutive slots per wavefront: fewer, longer-lived waves (the one-slot waves lived
-// ~2 us and the chip held ~7 of them per CU)
+// K5: IC_Angle (:94-141) + computeOrbDescriptor (:153-204) + keypoint assembly
+// (:1603-1657) for DESC_R consecutive output slots per wavefront, in three phases:
+//  1. per slot: IC_Angle moments (v_dot4 over the lane's 4 row dwords, DPP wave sums) and the
+//     37 x 40 steered-BRIEF patch of the blurred level staged into the slot's LDS buffer --
+//     all global reads of the wavefront are issued before any result is needed;
+//  2. lanes 0..DESC_R-1 evaluate fastAtan2 and glibc sincosf for their slot in one pass;
+//  3. per slot: the 256 tests from LDS (pattern coordinates pre-converted to float once per
+//     wavefront), ballot bit-packing, output rows.
 #define DESC_R 4
 __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint8_t *in,
                                                        const uint8_t *pyr, const uint8_t *blur,
                                                        const uint32_t *sel, const int *sel_cnt,
                                                        orbx_kp *kps, uint8_t *desc, int *cnt) {
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wv = wave_id();
     int bxr, b;
     xcd_remap2(bxr, b);
-    __shared__ uint32_t patch[4][372];
-    const int s0 = (bxr * 4 + (threadIdx.x >> 6)) * DESC_R;
-    // per-lane constants loaded once for the wavefront's DESC_R slots: IC_Angle weights of
-    // the lane's 4 (row, dword) cells and its 4 packed test pairs
-    uint2 icw[4];
-    uint32_t pat[4];
+    __shared__ uint32_t patch[4][DESC_R][372];
+    const int s0 = (bxr * 4 + wv) * DESC_R;
+    DescSlot d[DESC_R];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int j = min(lane + 64 * k, 31 * 8 - 1), v = (j >> 3) - 15;
-        icw[k] = c_icw[(v < 0 ? -v : v) * 8 + (j & 7)];
-        pat[k] = ((const uint32_t *)c_pattern)[k * 64 + lane];
+    for (int r = 0; r < DESC_R; r++) d[r] = desc_slot(g, sel, sel_cnt, cnt, s0 + r, b, lane);
+    bool any = false;
+#pragma unroll
+    for (int r = 0; r < DESC_R; r++) any |= d[r].valid != 0;
+    if (!any) return;
+    // phase 1
+    int M10[DESC_R], M01[DESC_R], PSH[DESC_R];
+    const long long amax = (long long)g.nimg * g.blur_stride - 4;
+#pragma unroll
+    for (int r = 0; r < DESC_R; r++) {
+        M10[r] = M01[r] = PSH[r] = 0;
+        if (!d[r].valid) continue;
+        const int l = d[r].l;
+        const int x = key_x(d[r].key) + 16, y = key_y(d[r].key) + 16;  // + minBorderX/Y (:1177-1186)
+        int pitch;
+        const uint8_t *img = level_ptr(g, in, pyr, b, l, &pitch);
+        // IC_Angle over the circular patch (|u| <= umax[|v|]): rows v = -15..15 as 8 dwords
+        // (u = -16..15), sum_u u*p = sum (u+16)*p - 16 * sum p with v_dot4_u32_u8 (exact)
+        const uint8_t *rowc = img + (long long)y * pitch + x - 16;
+        int m01 = 0, m10 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int j = lane + 64 * k;
+            if (j < 31 * 8) {
+                const int v = (j >> 3) - 15, w = j & 7;
+                const uint2 wt = c_icw[(v < 0 ? -v : v) * 8 + w];
+                const uint32_t P = load_u32_unaligned(rowc + v * pitch + 4 * w);
+                const int su = (int)__builtin_amdgcn_udot4(P, wt.x, 0u, false);
+                const int sm = (int)__builtin_amdgcn_udot4(P, wt.y, 0u, false);
+                m10 += su - 16 * sm;
+                m01 += v * sm;
+            }
+        }
+        M10[r] = wave_sum_dpp(m10);
+        M01[r] = wave_sum_dpp(m01);
+        // the rotated pattern stays within +-18 pixels (|rot(p)| <= 13 sqrt 2): rows y-18 ..
+        // y+18, bytes x-18 .. x+21 as 10 aligned dwords per row (the pitch is 16-aligned, so
+        // every row has the same misalignment)
+        const int bw = g.bp[l];
+        const long long c0 = (long long)b * g.blur_stride + g.blur_off[l] + (long long)(y - 18) * bw + (x - 18);
+        const int sh = (int)(c0 & 3);
+        PSH[r] = sh;
+        const long long a0 = c0 - sh;
+        uint32_t *pt = patch[wv][r];
+        if (a0 >= 0 && a0 + 36LL * bw + 40 <= amax + 4) {   // wave-uniform: no clamping needed
+            const uint32_t *src = (const uint32_t *)(blur + a0);
+            const int bw4 = bw >> 2;
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                const int idx = lane + 64 * k;
+                if (idx < 370) {
+                    const int rr = idx / 10, q = idx - rr * 10;
+                    pt[idx] = src[rr * bw4 + q];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                const int idx = lane + 64 * k;
+                if (idx < 370) {
+                    const int rr = idx / 10, q = idx - rr * 10;
+                    long long ad = a0 + (long long)rr * bw + 4 * q;
+                    ad = ad < 0 ? 0 : (ad > amax ? amax & ~3LL : ad);
+                    pt[idx] = *(const uint32_t *)(blur + ad);
+                }
+            }
+        }
     }
-    for (int r = 0; r < DESC_R; r++)
-        describe_one(g, in, pyr, blur, sel, sel_cnt, kps, desc, cnt, s0 + r, b, lane, patch[threadIdx.x >> 6], icw, pat);
+    // phase 2: lane r computes slot r's angle = fastAtan2(m01, m10) and (float) cos / sin
+    float ang = 0.f, sa = 0.f, ca = 1.f;
+    if (lane < DESC_R) {
+        int m10 = M10[0], m01 = M01[0];
+#pragma unroll
+        for (int r = 1; r < DESC_R; r++) if (lane == r) { m10 = M10[r]; m01 = M01[r]; }
+        ang = fast_atan2_deg((float)m01, (float)m10);
+        const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+        glibc_sincosf(ang * factorPI, &sa, &ca);
+    }
+    // pattern coordinates of the lane's 4 test pairs as floats (int8 -> f32, exact)
+    float PX0[4], PY0[4], PX1[4], PY1[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const uint32_t pw = ((const uint32_t *)c_pattern)[w * 64 + lane];   // x0 y0 x1 y1 as int8
+        PX0[w] = (float)(int8_t)(pw & 0xFF);
+        PY0[w] = (float)(int8_t)((pw >> 8) & 0xFF);
+        PX1[w] = (float)(int8_t)((pw >> 16) & 0xFF);
+        PY1[w] = (float)(int8_t)(pw >> 24);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // phase 3
+    const int cap = g.out_base[g.nlevels];
+#pragma unroll
+    for (int r = 0; r < DESC_R; r++) {
+        if (!d[r].valid) continue;
+        const float angle = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), r));
+        const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), r));
+        const float bs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), r));
+        const uint8_t *pc = (const uint8_t *)patch[wv][r] + 18 * 40 + 18 + PSH[r];   // (dy, dx) -> pc[dy * 40 + dx]
+        unsigned long long words[4];
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const int t0 = pc[cv_round_f(PX0[w] * bs + PY0[w] * a) * 40 + cv_round_f(PX0[w] * a - PY0[w] * bs)];
+            const int t1 = pc[cv_round_f(PX1[w] * bs + PY1[w] * a) * 40 + cv_round_f(PX1[w] * a - PY1[w] * bs)];
+            words[w] = __ballot(t0 < t1);
+        }
+        if (lane == 0) {
+            const int l = d[r].l;
+            const long long o = (long long)b * cap + d[r].off;
+            unsigned long long *dd = (unsigned long long *)(desc + o * 32);
+            dd[0] = words[0]; dd[1] = words[1]; dd[2] = words[2]; dd[3] = words[3];
+            orbx_kp kp;
+            const float s = g.scale[l];
+            kp.x = (float)(key_x(d[r].key) + 16);
+            kp.y = (float)(key_y(d[r].key) + 16);
+            if (l != 0) { kp.x *= s; kp.y *= s; }  // :1642-1651
+            kp.size = (float)g.scaled_patch[l];
+            kp.angle = angle;
+            kp.response = (float)key_score(d[r].key);
+            kp.octave = l;
+            kp.class_id = -1;
+            kps[o] = kp;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void stereo_sort_right(StereoArgs a, unsigned 
 __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoArgs a,
                                                          const unsigned long long *sorted,
                                                          float *u_right, float *depth, int *sad) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = wave_id();
     int bxr, p;
     xcd_remap2(bxr, p);
     const int iL = bxr * 4 + wv;
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(256) void hamming_best2_kernel(const uint8_t *q, in
                                                             int ndb, int *best_idx, int *best_d,
                                                             int *second_d) {
     const int lane = threadIdx.x & 63;
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int i = blockIdx.x * 4 + wave_id();
     if (i >= nq) return;
     const uint8_t *qi = q + (long long)i * 32;
     // per-lane (best, second) over its strided subset in ascending index order, then a
