@@ -275,9 +275,14 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
     const int tlo = min(th_a, th_b);
     FBP(1);
-    // 2. FAST pre-filter
+    // 2. FAST pre-filter. Only pixels of the FAST detection region [19, w-19) x [19, h-19)
+    // (cell ROIs start at minBorder 16 and end at maxBorder = size - 16, cv::FAST detects in
+    // [3, roi - 3), ORBextractor.cc:1061-1135) can be keypoints: a wavefront whose 4 rows all
+    // lie outside skips the test, and candidates outside the region are dropped.
     int ncand = 0;
-    {
+    mt[r * (FB_TW / 4) + (cb >> 2)] = 0u;
+    mt[r * (FB_TW / 4) + (cb >> 2) + 1] = 0u;
+    if (y0 + 4 * wv + 3 >= 19 && y0 + 4 * wv < h - 19) {   // wave-uniform
         uint32_t S[4], C[4], N[4];  // tile cols cb .. cb+15 (image x0+cb-4 .. x0+cb+11)
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -300,11 +305,9 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             cand |= (((~u >> 15) & 1u) | ((~u >> 30) & 2u)) << (2 * q);
         }
         const int y = y0 + r, xb = x0 + cb;
-        if (y < 3 || y >= h - 3) cand = 0;
-        const int lo = max(3 - xb, 0), hi = min(w - 3 - xb, 8);
+        if (y < 19 || y >= h - 19) cand = 0;
+        const int lo = max(19 - xb, 0), hi = min(w - 19 - xb, 8);
         cand &= hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
-        mt[r * (FB_TW / 4) + (cb >> 2)] = 0u;
-        mt[r * (FB_TW / 4) + (cb >> 2) + 1] = 0u;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const bool f = (cand >> i) & 1u;
@@ -312,8 +315,8 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             if (f) clist[wv][ncand + lane_rank(bal)] = (uint16_t)((r << 7) | (cb + i));
             ncand += __popcll(bal);
         }
-        if (lane == 0) ccount[wv] = ncand;
     }
+    if (lane == 0) ccount[wv] = ncand;
     FBP(2);
     // 4a. blur row pass: tile rows (2p, 2p+1) x output cols 4cg .. 4cg+3
     {
