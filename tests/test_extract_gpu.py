@@ -110,6 +110,24 @@ def test_batch_device_matches_single(amd, oracle_mod):
         _assert_same_kps(ex.fetch(i), ref.extract(imgs[i]), f"batch[{i}]")
 
 
+def test_large_batch_matches_oracle(amd, oracle_mod):
+    """A bench-sized batch (160 images, more workgroups than the chip holds at once): every
+    image must still equal the oracle."""
+    import torch
+    h, w, n, k = 376, 1241, 160, 5
+    src = [synth.textured_image(h, w, 60 + i) for i in range(k)]
+    imgs = np.stack([src[i % k] for i in range(n)])
+    dev = torch.from_numpy(imgs).cuda()
+    ex = amd.BatchExtractor(2000, 1.2, 8, 20, 7)
+    ex.reserve(w, h, n)
+    torch.cuda.synchronize()
+    ex.extract_device(dev.data_ptr(), n, w, h, w, h * w)
+    ref = oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
+    want = [ref.extract(im) for im in src]
+    for i in range(n):
+        _assert_same_kps(ex.fetch(i), want[i % k], f"batch[{i}]")
+
+
 def test_golden_c1_c2_on_device(amd):
     """HIP path == committed golden fixtures (independent of the oracle at run time)."""
     from test_golden_cpu import load_c1, load_c2
