@@ -160,6 +160,7 @@ typedef struct {
 #define ORBT_MP_BAD 1            /* MapPoint::isBad() */
 #define ORBT_MP_HAS_OBS 2        /* MapPoint::Observations() > 0 */
 #define ORBT_MP_IN_FRAME 4       /* mnLastFrameSeen == CurrentFrame.mnId (Tracking.cc:1749-1769) */
+#define ORBT_MP_FOUND 8          /* in sAlreadyFound (ORBmatcher.cc:1951; Tracking::Relocalization) */
 
 /* The map points a matcher reads (MapPoint getters). Host pointers. */
 typedef struct {
@@ -209,6 +210,19 @@ int orbt_search_by_projection_frame(orbt_engine *e, const orbt_frame *cur, const
                                     const orbt_mappoints *M, float th, int mono, int check_ori,
                                     const uint8_t *kp_blocked, int32_t *owner, int32_t *nmatches);
 
+/* ORBmatcher(0.9, check_ori).SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+ * (ORBmatcher.h:116, ORBmatcher.cc:1922-2066; Tracking::Relocalization, th 10 / 3, ORBdist
+ * 100 / 64). `kf` carries pKF->mvKeysUn (angles); kf_mp[i] = index into M of
+ * pKF->GetMapPointMatches()[i] (-1 = NULL); M->flags ORBT_MP_FOUND = in sAlreadyFound.
+ * kp_blocked[cur->n] (may be NULL) = CurrentFrame.mvpMapPoints[i2] != NULL on entry; a keypoint
+ * claimed by an earlier point is skipped by later ones (greedy, point order). Frame pose,
+ * bounds, grid, scale tables are `cur`'s. owner / nmatches as for
+ * orbt_search_by_projection_frame. */
+int orbt_search_by_projection_keyframe(orbt_engine *e, const orbt_frame *cur, const orbt_frame *kf,
+                                       const int32_t *kf_mp, const orbt_mappoints *M, float th,
+                                       int orb_dist, int check_ori, const uint8_t *kp_blocked,
+                                       int32_t *owner, int32_t *nmatches);
+
 /* ORBmatcher::Fuse(pKF, vpMapPoints, th) (ORBmatcher.h:208, ORBmatcher.cc:1139-1278; th = 3 from
  * LocalMapping::SearchInNeighbors) -- the search half. `kf` is the KeyFrame (pose, calibration,
  * bounds, grid keypoints, mvuRight, descriptors, mvScaleFactors, mvInvLevelSigma2); flags
@@ -232,6 +246,8 @@ int orbt_stage(orbt_engine *e, int slot, const orbt_frame *F, const orbt_mappoin
 int orbt_run_local_batch(orbt_engine *e, int n_slots, float view_cos_limit, float th, float nnratio,
                          void *stream);
 int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int check_ori, void *stream);
+/* relocalisation matcher over staged slots: `last` = the keyframe, `last_mp` = its matches */
+int orbt_run_reloc_batch(orbt_engine *e, int n_slots, float th, int orb_dist, int check_ori, void *stream);
 int orbt_run_fuse_batch(orbt_engine *e, int n_slots, float th, void *stream);
 int orbt_fetch_fuse(orbt_engine *e, int slot, int32_t *best_idx, int32_t *best_dist);
 int orbt_fetch(orbt_engine *e, int slot, orbt_view *view, int32_t *owner, int32_t *nmatches);

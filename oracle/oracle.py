@@ -432,6 +432,24 @@ def search_by_projection_frame(prob: dict, th=15.0, mono=False, check_ori=True):
     return nm, owner[: F.n]
 
 
+def search_by_projection_keyframe(prob: dict, th=10.0, orb_dist=100, check_ori=True):
+    """ORBmatcher(0.9, checkOri).SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)."""
+    L = lib()
+    L.orc_search_by_projection_kf.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_int,
+                                              C.c_int, C.c_void_p, C.c_void_p]
+    F, k1 = make_orbt_frame(prob["frame"])
+    Kf, k2 = make_orbt_frame(prob["last"])
+    M, k3 = make_orbt_map(prob["map"])
+    kf_mp = np.ascontiguousarray(prob["last_mp"], np.int32)
+    owner = np.zeros(max(F.n, 1), np.int32)
+    blk = prob.get("kp_blocked")
+    blk = np.ascontiguousarray(blk, np.uint8) if blk is not None else None
+    nm = L.orc_search_by_projection_kf(C.byref(F), C.byref(Kf), kf_mp.ctypes.data, C.byref(M), th, int(orb_dist),
+                                       1 if check_ori else 0, blk.ctypes.data if blk is not None else None,
+                                       owner.ctypes.data)
+    return nm, owner[: F.n]
+
+
 # ---- Optimizer::PoseOptimization (lba_oracle.c pose_oracle_optimize)
 class OrbpFrame(C.Structure):
     _fields_ = [("n", C.c_int32), ("Xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p),

@@ -298,6 +298,92 @@ int orc_search_by_projection_frame(const orbt_frame *cur, const orbt_frame *last
     return nmatches;
 }
 
+/* ORBmatcher::SearchByProjection(Frame &CurrentFrame, KeyFrame *pKF, const set<MapPoint*>
+ * &sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1922-2066; Tracking::Relocalization). kf_mp[i] =
+ * index into M of pKF->GetMapPointMatches()[i] (-1 = NULL); ORBT_MP_FOUND marks sAlreadyFound.
+ * kp_blocked = CurrentFrame.mvpMapPoints[i2] != NULL on entry; every claim blocks the keypoint
+ * for later points (:2007-2008). No depth-sign test (:1959-1968). */
+int orc_search_by_projection_kf(const orbt_frame *cur, const orbt_frame *kf, const int32_t *kf_mp,
+                                const orbt_mappoints *M, float th, int ORBdist, int checkOri,
+                                const uint8_t *kp_blocked, int32_t *owner) {
+    const int HISTO_LENGTH = 30;
+    const int N = cur->n;
+    orc_frame_grid g;
+    frame_grid(cur, &g);
+    uint8_t *blocked = (uint8_t *)calloc((size_t)N + 1, 1);
+    if (kp_blocked) memcpy(blocked, kp_blocked, (size_t)N);
+    int *cand = (int *)malloc(sizeof(int) * ((size_t)N + 1));
+    int *hist_bin = (int *)malloc(sizeof(int) * ((size_t)kf->n + 1));
+    int *hist_idx = (int *)malloc(sizeof(int) * ((size_t)kf->n + 1));
+    int nhist = 0, nmatches = 0;
+    for (int k = 0; k < N; k++) owner[k] = -1;
+    const float factor = HISTO_LENGTH / 360.0f;
+    for (int i = 0; i < kf->n; i++) {
+        const int m = kf_mp[i];
+        if (m < 0) continue;
+        if (M->flags[m] & (ORBT_MP_BAD | ORBT_MP_FOUND)) continue;   /* isBad() || sAlreadyFound.count */
+        const float *P = M->Xw + 3 * (size_t)m;
+        float x3Dc[3];
+        mat_rx_t(cur->Tcw, P, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        const float u = cur->fx * xc * invzc + cur->cx;
+        const float v = cur->fy * yc * invzc + cur->cy;
+        if (u < cur->min_x || u > cur->max_x) continue;
+        if (v < cur->min_y || v > cur->max_y) continue;
+        const float PO[3] = {P[0] - cur->Ow[0], P[1] - cur->Ow[1], P[2] - cur->Ow[2]};
+        double ss = 0;
+        for (int k = 0; k < 3; k++) { const double t = PO[k]; ss += t * t; }
+        const float dist3D = (float)sqrt(ss);                         /* cv::norm */
+        const float maxDistance = 1.2f * M->max_dist[m], minDistance = 0.8f * M->min_dist[m];
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float ratio = M->max_dist[m] / dist3D;                  /* PredictScale(dist3D, &F) */
+        int nPredictedLevel = (int)ceilf(orc_logf(ratio) / cur->log_scale_factor);
+        if (nPredictedLevel < 0) nPredictedLevel = 0;
+        else if (nPredictedLevel >= cur->nlevels) nPredictedLevel = cur->nlevels - 1;
+        const float radius = th * cur->scale_factors[nPredictedLevel];
+        const int nc = orc_features_in_area(&g, u, v, radius, nPredictedLevel - 1, nPredictedLevel + 1, cand, N + 1);
+        if (nc == 0) continue;
+        const uint8_t *dMP = M->desc + 32 * (size_t)m;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = cand[c];
+            if (blocked[i2]) continue;
+            const int dist = orc_descriptor_distance(dMP, cur->desc + 32 * (size_t)i2);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        }
+        if (bestDist <= ORBdist && bestIdx2 >= 0) {
+            owner[bestIdx2] = m;
+            blocked[bestIdx2] = 1;
+            nmatches++;
+            if (checkOri) {
+                float rot = kf->keys_un[i].angle - cur->keys_un[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == HISTO_LENGTH) bin = 0;
+                hist_bin[nhist] = bin;
+                hist_idx[nhist] = bestIdx2;
+                nhist++;
+            }
+        }
+    }
+    if (checkOri) {
+        int counts[30] = {0};
+        for (int k = 0; k < nhist; k++) counts[hist_bin[k]]++;
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima30(counts, &ind1, &ind2, &ind3);
+        for (int k = 0; k < nhist; k++) {
+            const int b = hist_bin[k];
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            owner[hist_idx[k]] = -2;
+            nmatches--;
+        }
+    }
+    free(cand); free(blocked); free(hist_bin); free(hist_idx);
+    orc_grid_free(&g);
+    return nmatches;
+}
+
 /* ==========================================================================================
  * BoW-guided matchers: ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
  * (ORBmatcher.cc:236-353) and ORBmatcher::SearchForTriangulation (ORBmatcher.cc:915-1089,

@@ -18,6 +18,9 @@ int orc_search_local_points(const orbt_frame *F, const orbt_mappoints *M, float 
 int orc_search_by_projection_frame(const orbt_frame *cur, const orbt_frame *last, const int32_t *last_mp,
                                    const uint8_t *last_outlier, const orbt_mappoints *M, float th, int bMono,
                                    int checkOri, const uint8_t *kp_blocked, int32_t *owner);
+int orc_search_by_projection_kf(const orbt_frame *cur, const orbt_frame *kf, const int32_t *kf_mp,
+                                const orbt_mappoints *M, float th, int ORBdist, int checkOri,
+                                const uint8_t *kp_blocked, int32_t *owner);
 int orc_search_by_bow(const orbb_keyframe *kf, const orbb_keyframe *F, float nnratio, int checkOri, int32_t *matches);
 int orc_search_for_triangulation(const orbb_keyframe *kf1, const orbb_keyframe *kf2, const float F12[9],
                                  const float Cw[3], const float T2w[12], int bOnlyStereo, int checkOri,

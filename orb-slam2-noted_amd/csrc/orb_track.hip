@@ -3,6 +3,9 @@
 //                                             MapPoint.cc:612-626, glibc logf restated)
 //   ORBmatcher::SearchByProjection(F, vpMapPoints, th)      ORBmatcher.cc:78-176
 //   ORBmatcher::SearchByProjection(CurrentFrame, LastFrame, th, bMono)  ORBmatcher.cc:1741-1904
+//   ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+//                                             ORBmatcher.cc:1922-2066 (relocalisation; the
+//                                             keyframe takes the last frame's slot)
 //
 // Both matchers are greedy: map points (resp. last-frame keypoints) are visited in order and
 // a keypoint claimed by a map point with Observations() > 0 is skipped by every later one.
@@ -488,10 +491,46 @@ __global__ __launch_bounds__(64) void track_local_resolve_kernel(Slots S, float 
     if (lane == 0) nmatch[s] = nm;
 }
 
+constexpr int kModeMotion = 0, kModeReloc = 1;
+
+// ---- relocalisation query of keyframe keypoint i (ORBmatcher.cc:1944-2019): map point not bad
+// and not in sAlreadyFound, projection without a depth-sign test, scale-invariance gate,
+// PredictScale(dist3D, &CurrentFrame), window at levels [lvl - 1, lvl + 1], no stereo gate
+__device__ int reloc_query(const Slots &S, int s, const FrameDev &f, int i, float th, const uint8_t *claimed,
+                           Cand &c) {
+#pragma unroll
+    for (int k = 0; k < TOPK; k++) { c.key[k] = 0xFFFFFFFFu; c.idx[k] = 0; c.oct[k] = -1; c.bin[k] = -1; }
+    const long long lb = (long long)s * S.cap_kp + i;
+    const int m = S.last_mp[lb];
+    if (m < 0) return -1;
+    const long long mb = (long long)s * S.cap_mp + m;
+    if (S.mflags[mb] & (ORBT_MP_BAD | ORBT_MP_FOUND)) return -1;
+    const float *P = S.Xw + mb * 3;
+    float x3Dc[3];
+    mat_rx_t(f.Tcw, P, x3Dc);
+    const float invzc = (float)(1.0 / (double)x3Dc[2]);
+    const float u = f.fx * x3Dc[0] * invzc + f.cx;
+    const float v = f.fy * x3Dc[1] * invzc + f.cy;
+    if (u < f.min_x || u > f.max_x || v < f.min_y || v > f.max_y) return 0;
+    const float PO[3] = {P[0] - f.Ow[0], P[1] - f.Ow[1], P[2] - f.Ow[2]};
+    double ss = 0;
+    for (int k = 0; k < 3; k++) { const double t = PO[k]; ss = ss + t * t; }
+    const float dist3D = (float)sqrt(ss);                                   // cv::norm
+    const float maxDistance = 1.2f * S.maxd[mb], minDistance = 0.8f * S.mind[mb];
+    if (dist3D < minDistance || dist3D > maxDistance) return 0;
+    int lvl = (int)ceilf(glibc_logf(S.maxd[mb] / dist3D) / f.log_scale);    // PredictScale
+    if (lvl < 0) lvl = 0;
+    else if (lvl >= f.nlevels) lvl = f.nlevels - 1;
+    const float radius = th * f.scale[lvl];
+    return scan_window<false>(S, s, f, u, v, radius, lvl - 1, lvl + 1, S.mdesc + mb * 32, 0.f, INFINITY, claimed,
+                              S.lkun[lb].angle, c);
+}
+
 // ---- SearchByProjection(CurrentFrame, LastFrame) query of last keypoint i (ORBmatcher.cc:1786-1870);
 // `claimed` != null adds the claim filter (resolve fallback). Returns -1 if not projected.
 __device__ int frame_query(const Slots &S, int s, const FrameDev &f, int i, float th, int mono,
-                           const uint8_t *claimed, Cand &c) {
+                           const uint8_t *claimed, Cand &c, int mode = kModeMotion) {
+    if (mode == kModeReloc) return reloc_query(S, s, f, i, th, claimed, c);
 #pragma unroll
     for (int k = 0; k < TOPK; k++) { c.key[k] = 0xFFFFFFFFu; c.idx[k] = 0; c.oct[k] = -1; c.bin[k] = -1; }
     const long long lb = (long long)s * S.cap_kp + i;
@@ -529,19 +568,22 @@ __device__ int frame_query(const Slots &S, int s, const FrameDev &f, int i, floa
 }
 
 // one thread per (slot, last keypoint)
-__global__ __launch_bounds__(256) void track_frame_cand_kernel(Slots S, float th, int mono, Cand *cand,
+__global__ __launch_bounds__(256) void track_frame_cand_kernel(Slots S, float th, int mono, int mode, Cand *cand,
                                                                int *ncand) {
     const int i = blockIdx.x * 256 + threadIdx.x, s = blockIdx.y;
     const FrameDev &f = S.fr[s];
     if (i >= f.n_last) return;
     Cand c;
-    const int nc = frame_query(S, s, f, i, th, mono, nullptr, c);
+    const int nc = frame_query(S, s, f, i, th, mono, nullptr, c, mode);
     const long long lb = (long long)s * S.cap_kp + i;
     cand[lb] = c;
     ncand[lb] = nc;
 }
 
+// mode kModeMotion: accept <= TH_HIGH, a claim blocks later points only if the claiming point
+// has observations; kModeReloc: accept <= ORBdist (max_dist), every claim blocks (:2007-2008)
 __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float th, int mono, int check_ori,
+                                                                 int mode, int max_dist,
                                                                  const Cand *cand, const int *ncand, int *owner,
                                                                  int *nmatch, int *hist_idx, int8_t *hist_bin) {
     extern __shared__ uint8_t lds[];
@@ -570,8 +612,8 @@ __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float 
         pk.found = 0; pk.last_ex = -1; pk.key0 = 0xFFFFFFFFu; pk.idx0 = 0; pk.bin0 = -1;
         if (nc > 0) pk = pick_unclaimed(c, claimed, 1);
         const bool fallback = nc > TOPK && pk.found < 1;
-        const bool accept = nc > 0 && !fallback && pk.found >= 1 && (int)(pk.key0 >> 16) <= TH_HIGH;
-        const bool obs = m >= 0 && (S.mflags[mb0 + m] & ORBT_MP_HAS_OBS) != 0;
+        const bool accept = nc > 0 && !fallback && pk.found >= 1 && (int)(pk.key0 >> 16) <= max_dist;
+        const bool obs = m >= 0 && (mode == kModeReloc || (S.mflags[mb0 + m] & ORBT_MP_HAS_OBS) != 0);
         const int idx = pk.idx0;
         if (accept && obs) atomicMin(&tag[idx], lane);
         __syncthreads();
@@ -606,11 +648,11 @@ __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float 
                 if (lane == 0) {
                     const int qq = base + cut;
                     Cand full;
-                    frame_query(S, s, f, qq, th, mono, claimed, full);
-                    if (full.key[0] != 0xFFFFFFFFu && (int)(full.key[0] >> 16) <= TH_HIGH) {
+                    frame_query(S, s, f, qq, th, mono, claimed, full, mode);
+                    if (full.key[0] != 0xFFFFFFFFu && (int)(full.key[0] >> 16) <= max_dist) {
                         const int id = full.idx[0], mm = S.last_mp[kb + qq];
                         owner[kb + id] = mm;
-                        if (S.mflags[mb0 + mm] & ORBT_MP_HAS_OBS) claimed[id] = 1;
+                        if (mode == kModeReloc || (S.mflags[mb0 + mm] & ORBT_MP_HAS_OBS)) claimed[id] = 1;
                         nm++;
                         if (check_ori) {
                             HI[nh] = id;
@@ -933,12 +975,29 @@ int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int ch
     hipStream_t st = pick(e, stream);
     if (grid(e, n_slots, st)) return ORBX_EDEVICE;
     const int nl = std::max(1, max_n(e, 1, n_slots));
-    track_frame_cand_kernel<<<dim3((nl + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, mono,
+    track_frame_cand_kernel<<<dim3((nl + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, mono, kModeMotion,
                                                                              e->cand.as<Cand>(), e->ncand.as<int>());
-    track_frame_resolve_kernel<<<n_slots, 64, resolve_lds(e), st>>>(make_slots(e), th, mono, check_ori, e->cand.as<Cand>(),
+    track_frame_resolve_kernel<<<n_slots, 64, resolve_lds(e), st>>>(make_slots(e), th, mono, check_ori, kModeMotion,
+                                                                TH_HIGH, e->cand.as<Cand>(),
                                                                 e->ncand.as<int>(), e->owner.as<int>(),
                                                                 e->nmatch.as<int>(), e->hist_idx.as<int>(),
                                                                 e->hist_bin.as<int8_t>());
+    TR_CHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbt_run_reloc_batch(orbt_engine *e, int n_slots, float th, int orb_dist, int check_ori, void *stream) {
+    if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    hipStream_t st = pick(e, stream);
+    if (grid(e, n_slots, st)) return ORBX_EDEVICE;
+    const int nl = std::max(1, max_n(e, 1, n_slots));
+    track_frame_cand_kernel<<<dim3((nl + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, 0, kModeReloc,
+                                                                             e->cand.as<Cand>(), e->ncand.as<int>());
+    track_frame_resolve_kernel<<<n_slots, 64, resolve_lds(e), st>>>(make_slots(e), th, 0, check_ori, kModeReloc,
+                                                                orb_dist, e->cand.as<Cand>(), e->ncand.as<int>(),
+                                                                e->owner.as<int>(), e->nmatch.as<int>(),
+                                                                e->hist_idx.as<int>(), e->hist_bin.as<int8_t>());
     TR_CHK(hipGetLastError());
     return ORBX_OK;
 }
@@ -991,6 +1050,22 @@ int orbt_search_by_projection_frame(orbt_engine *e, const orbt_frame *cur, const
     int rc = orbt_stage(e, 0, cur, M, last, last_mp, last_outlier, kp_blocked);
     if (rc) return rc;
     rc = orbt_run_frame_batch(e, 1, th, mono, check_ori, nullptr);
+    if (rc) return rc;
+    return orbt_fetch(e, 0, nullptr, owner, nmatches);
+}
+
+int orbt_search_by_projection_keyframe(orbt_engine *e, const orbt_frame *cur, const orbt_frame *kf,
+                                       const int32_t *kf_mp, const orbt_mappoints *M, float th, int orb_dist,
+                                       int check_ori, const uint8_t *kp_blocked, int32_t *owner, int32_t *nmatches) {
+    if (!e || !cur || !kf || !kf_mp || !M || !owner) return ORBX_EINVAL;
+    const int need_kp = std::max(cur->n, kf->n);
+    if (e->nslots < 1 || e->cap_kp < need_kp || e->cap_mp < M->n) {
+        const int rc = orbt_reserve(e, std::max(1, e->nslots), std::max(e->cap_kp, need_kp), std::max(e->cap_mp, M->n));
+        if (rc) return rc;
+    }
+    int rc = orbt_stage(e, 0, cur, M, kf, kf_mp, nullptr, kp_blocked);
+    if (rc) return rc;
+    rc = orbt_run_reloc_batch(e, 1, th, orb_dist, check_ori, nullptr);
     if (rc) return rc;
     return orbt_fetch(e, 0, nullptr, owner, nmatches);
 }

@@ -84,6 +84,8 @@ SIGNATURES = [
     ("orbt_stage", _I, [_P, _I, _P, _P, _P, _P, _P, _P]),
     ("orbt_run_local_batch", _I, [_P, _I, _F, _F, _F, _P]),
     ("orbt_run_frame_batch", _I, [_P, _I, _F, _I, _I, _P]),
+    ("orbt_run_reloc_batch", _I, [_P, _I, _F, _I, _I, _P]),
+    ("orbt_search_by_projection_keyframe", _I, [_P, _P, _P, _P, _P, _F, _I, _I, _P, _P, _P]),
     ("orbt_fetch", _I, [_P, _I, _P, _P, _P]),
     ("orbt_fuse_candidates", _I, [_P, _P, _P, _F, _P, _P]),
     ("orbt_run_fuse_batch", _I, [_P, _I, _F, _P]),
@@ -542,6 +544,28 @@ class Tracker:
                                                      owner.ctypes.data, C.byref(nm)),
                "orbt_search_by_projection_frame")
         return nm.value, owner[: F.n]
+
+    def search_by_projection_keyframe(self, prob: dict, th=10.0, orb_dist=100, check_ori=True):
+        """ORBmatcher(0.9, checkOri).SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th,
+        ORBdist) (Tracking::Relocalization); prob["last"] / prob["last_mp"] are the keyframe and
+        its map point matches, map flags ORBT_MP_FOUND = sAlreadyFound."""
+        F, k1 = _orbt_frame(prob["frame"])
+        Kf, k2 = _orbt_frame(prob["last"])
+        M, k3 = _orbt_map(prob["map"])
+        kf_mp = np.ascontiguousarray(prob["last_mp"], np.int32)
+        owner = np.zeros(max(F.n, 1), np.int32)
+        nm = C.c_int32()
+        blk = self._blk(prob)
+        _check(lib().orbt_search_by_projection_keyframe(self._h, C.byref(F), C.byref(Kf), kf_mp.ctypes.data,
+                                                        C.byref(M), th, int(orb_dist), 1 if check_ori else 0,
+                                                        blk.ctypes.data if blk is not None else None,
+                                                        owner.ctypes.data, C.byref(nm)),
+               "orbt_search_by_projection_keyframe")
+        return nm.value, owner[: F.n]
+
+    def run_reloc_batch(self, n_slots: int, th=10.0, orb_dist=100, check_ori=True, stream=None):
+        _check(lib().orbt_run_reloc_batch(self._h, n_slots, th, int(orb_dist), 1 if check_ori else 0, stream),
+               "orbt_run_reloc_batch")
 
     def fuse_candidates(self, prob: dict, th=3.0):
         """ORBmatcher::Fuse(pKF, vpMapPoints, th) search half; prob["frame"] is the KeyFrame."""

@@ -236,7 +236,7 @@ def localba_problem(seed: int = 4, n_kf: int = 20, n_points: int = 3000, stereo_
 # ---------------------------------------------------------------------------------------
 TRACK_KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
-MP_BAD, MP_HAS_OBS, MP_IN_FRAME = 1, 2, 4
+MP_BAD, MP_HAS_OBS, MP_IN_FRAME, MP_FOUND = 1, 2, 4, 8
 
 
 def _flip_bits(rng, d: np.ndarray, k: int) -> np.ndarray:
@@ -568,3 +568,19 @@ def bow_match_problem(seed: int = 3, n: int = 2000, n_points: int = 1600, stereo
     T2w = np.concatenate([R2, t2[:, None]], 1).astype(np.float32)
     Cw1 = (-(R1.astype(np.float64).T @ t1.astype(np.float64))).astype(np.float32)
     return {"A": A, "B": B, "F12": F12, "Cw1": Cw1, "T2w": T2w}
+
+
+def reloc_problem(seed: int = 40, found_frac: float = 0.2, blocked_frac: float = 0.1, **kw):
+    """Tracking::Relocalization's projection search (ORBmatcher.cc:1922-2066): a tracking
+    problem whose last frame plays the candidate keyframe (its keypoint angles and map point
+    matches), ~found_frac of the map points in sAlreadyFound (MP_FOUND) and ~blocked_frac of
+    the current keypoints already holding a map point (kp_blocked)."""
+    p = tracking_problem(seed, **kw)
+    rng = np.random.default_rng(seed + 7919)
+    m = p["map"]
+    flags = np.array(m["flags"], np.uint8, copy=True)
+    flags[rng.random(len(flags)) < found_frac] |= MP_FOUND
+    p["map"] = dict(m, flags=flags)
+    n = len(p["frame"]["keys_un"])
+    p["kp_blocked"] = (rng.random(n) < blocked_frac).astype(np.uint8)
+    return p

@@ -75,3 +75,22 @@ def test_crowd_claims_in_order(oracle_mod):
     assert nm == 12 and own[:12].tolist() == list(range(12))
     nm, own = oracle_mod.search_by_projection_frame(p, th=15.0, check_ori=False)
     assert nm > 4 and own[0] == 0
+
+
+def test_reloc_projection_rules(oracle_mod):
+    """ORBmatcher.cc:1922-2066 invariants on the oracle: points in sAlreadyFound or bad never
+    match, keypoints holding a map point on entry are never reassigned, every claim is
+    exclusive (a keypoint is owned by one point), distances respect ORBdist."""
+    import numpy as np
+    from orbslam2_amd import synth
+    p = synth.reloc_problem(42)
+    flags = p["map"]["flags"]
+    for th, od in ((10.0, 100), (3.0, 64)):
+        nm, own = oracle_mod.search_by_projection_keyframe(p, th=th, orb_dist=od, check_ori=False)
+        got = own[own >= 0]
+        assert nm == len(got) > 50
+        assert len(np.unique(got)) == len(got)
+        assert not (flags[got] & (synth.MP_FOUND | synth.MP_BAD)).any()
+        assert (own[p["kp_blocked"] == 1] == -1).all()
+        d = np.unpackbits(p["map"]["desc"][got] ^ p["frame"]["desc"][own >= 0], axis=1).sum(1)
+        assert (d <= od).all()

@@ -53,6 +53,34 @@ def test_search_by_projection_frame(tracker, oracle_mod, seed, motion, mono, che
     assert (own_r >= 0).sum() > 20
 
 
+@pytest.mark.parametrize("seed,th,orb_dist,check_ori,stereo", [
+    (40, 10.0, 100, True, True), (41, 3.0, 64, True, True), (42, 10.0, 100, False, True),
+    (43, 10.0, 100, True, False), (44, 3.0, 64, False, False), (45, 20.0, 256, True, True)])
+def test_search_by_projection_keyframe(tracker, oracle_mod, seed, th, orb_dist, check_ori, stereo):
+    """Tracking::Relocalization's SearchByProjection(F, pKF, sAlreadyFound, th, ORBdist)
+    (ORBmatcher.cc:1922-2066): greedy claims by every point, sAlreadyFound filter."""
+    p = synth.reloc_problem(seed, stereo=stereo)
+    nm_r, own_r = oracle_mod.search_by_projection_keyframe(p, th=th, orb_dist=orb_dist, check_ori=check_ori)
+    nm_g, own_g = tracker.search_by_projection_keyframe(p, th=th, orb_dist=orb_dist, check_ori=check_ori)
+    assert nm_g == nm_r
+    assert np.array_equal(own_g, own_r)
+    assert (own_r >= 0).sum() > 20
+
+
+def test_reloc_batched_slots(amd, oracle_mod):
+    t = amd.Tracker()
+    probs = [synth.reloc_problem(200 + s, n_kp=1200 + 200 * s, n_mp=1800 + 300 * s) for s in range(5)]
+    t.reserve(len(probs), 2100, 3300)
+    for s, p in enumerate(probs):
+        t.stage(s, p)
+    t.run_reloc_batch(len(probs), th=10.0, orb_dist=100)
+    for s, p in enumerate(probs):
+        nm_g, own_g, _ = t.fetch(s, len(p["frame"]["keys_un"]))
+        nm_r, own_r = oracle_mod.search_by_projection_keyframe(p, th=10.0, orb_dist=100)
+        assert nm_g == nm_r and np.array_equal(own_g, own_r), s
+    t.close()
+
+
 def test_batched_slots(amd, oracle_mod):
     t = amd.Tracker()
     probs = [synth.tracking_problem(100 + s, n_kp=1500 + 100 * s, n_mp=2000 + 150 * s,
