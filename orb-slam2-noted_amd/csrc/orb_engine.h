@@ -69,6 +69,7 @@ struct orbx_engine {
     float scale[ORBX_MAXL]{}, inv_scale[ORBX_MAXL]{}, sigma2[ORBX_MAXL]{}, inv_sigma2[ORBX_MAXL]{};
     int nfeat[ORBX_MAXL]{};
     int umax[16]{};
+    int rz_rows[ORBX_MAXL]{};   // source rows per resize tile, per level
     int8_t pattern[1024]{};
     // geometry for the reserved image size
     int W = 0, H = 0, max_images = 0;

@@ -62,12 +62,21 @@ __device__ __forceinline__ const uint8_t *level_ptr(const ExtractGeom &g, const 
 // ------------------------------------------------------------------------------------
 // K1: cv::resize(INTER_LINEAR) of level l-1 into level l (ComputePyramid :1686-1691,
 // SURVEY.md A.2). Column/row coefficient tables are precomputed on the host with the
-// reference's float/double arithmetic; the kernel does the exact integer math.
-// Each thread produces 4 consecutive pixels of RZ_RB consecutive rows: the 4 source columns
-// span <= 8 bytes (scale <= 2) and come from two unaligned-dword reads per source row; each
-// output row is one dword store (pyramid pitch is 16-aligned).
+// reference's float/double arithmetic; the kernel does the exact integer math in OpenCV's
+// two passes (HResizeLinear: Q11 column sums per source row; VResizeLinear: row blend).
+// One workgroup per RZ_TW x RZ_TH output tile:
+//  1. horizontal pass over the tile's source rows [ry(y0).r0, ry(y1-1).r1] (each source row
+//     once, ~1.2 per output row): a thread owns 4 output columns, reads the <= 12 source
+//     bytes they span with 3 aligned dwords, picks each (p[sx], p[sx1]) pair with one
+//     v_perm and forms a0 p[sx] + a1 p[sx1] with one v_dot2_u32_u16 -> int sums in LDS;
+//  2. vertical pass: two ds_read_b128 per 4 output pixels, (S0 b0 + S1 b1 + 2^21) >> 22
+//     (FixedPtCast) or the SSE2 VResizeLinearVec_32s8u lane arithmetic for the columns
+//     OpenCV 3.2 vectorises (resize_mode 1), one dword store per 4 pixels.
 // Column table entry: x = sx | a0 << 16, y = a1 | (sx1 - sx) << 16.
 // ------------------------------------------------------------------------------------
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
 // dword of image bytes [x, x+4) of row `rowp` (x .. x+3 inside the row) from aligned loads
 __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
     const uintptr_t a = (uintptr_t)p;
@@ -78,76 +87,94 @@ __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
-__device__ __forceinline__ int resize_px(int S0, int S1, int4 ry, bool simd) {
-    int v;
-    if (simd) {  // SSE2 VResizeLinearVec_32s8u lane arithmetic
-        int x0 = S0 >> 4, y0 = S1 >> 4;
-        x0 = min(max(x0, -32768), 32767);
-        y0 = min(max(y0, -32768), 32767);
-        int t = ((x0 * (int)(int16_t)ry.z) >> 16) + ((y0 * (int)(int16_t)ry.w) >> 16);
-        t = min(max(t, -32768), 32767);
-        t = min(max(t + 2, -32768), 32767) >> 2;
-        v = t;
-    } else {     // FixedPtCast<int, uchar, 22>
-        v = (S0 * ry.z + S1 * ry.w + (1 << 21)) >> 22;
-    }
-    return min(max(v, 0), 255);
+__device__ __forceinline__ uint32_t resize_px_simd(int S0, int S1, int4 ry) {  // SSE2 lane arithmetic
+    int x0 = S0 >> 4, y0 = S1 >> 4;
+    x0 = min(max(x0, -32768), 32767);
+    y0 = min(max(y0, -32768), 32767);
+    int t = ((x0 * (int)(int16_t)ry.z) >> 16) + ((y0 * (int)(int16_t)ry.w) >> 16);
+    t = min(max(t, -32768), 32767);
+    t = min(max(t + 2, -32768), 32767) >> 2;
+    return (uint32_t)min(max(t, 0), 255);
 }
 
-#define RZ_RB 4   // output rows per thread
+#define RZ_TW 128   // output columns per tile (32 column groups of 4)
+#define RZ_TH 32    // output rows per tile
+#define RZ_HJ 6     // source rows per thread per load batch
 
-__global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, const int2 *cxt, const int4 *ryt,
-                                                           const uint8_t *in, uint8_t *pyr) {
-    // flat (row block, column group) tasks: no idle lanes at the right edge of narrow
-    // levels; RZ_RB rows per thread keep 4 * RZ_RB independent loads in flight (the level-1
-    // pass streams the input from HBM and was latency bound with one row per thread)
+template <bool SIMD>
+__global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, int tiles_x, const int2 *cxt,
+                                                           const int4 *ryt, const uint8_t *in, uint8_t *pyr) {
+    extern __shared__ uint4 rz_h[];   // [source row][32 column groups] horizontal sums
     const int dw = g.lw[l], dh = g.lh[l];
     const int b = blockIdx.y;   // streaming: the XCD remap measured no gain here
-    const int ncg = (dw + 3) >> 2;
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    const int rb = t / ncg, cg = t - rb * ncg;
-    const int dy0 = rb * RZ_RB;
-    if (dy0 >= dh) return;
-    const int dx0 = 4 * cg;
+    const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+    const int x0 = tx * RZ_TW, y0 = ty * RZ_TH, y1 = min(y0 + RZ_TH, dh);
+    const int sr0 = ryt[y0].x, nsr = ryt[y1 - 1].y - sr0 + 1;
     int sp;
     const uint8_t *src = level_ptr(g, in, pyr, b, l - 1, &sp);
-    uint8_t *dst = pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
-    const int n = min(4, dw - dx0);
-    int2 c[4];
+    const int cg = threadIdx.x & 31, dx0 = x0 + 4 * cg;
+    // 1. horizontal pass
+    {
+        int2 c[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) c[k] = cxt[min(dx0 + k, dw - 1)];
-    const int sx0 = c[0].x & 0xFFFF;
-    const int sw = g.lw[l - 1];
-    const bool fast = sx0 + 8 <= sw;
-    int4 ry[RZ_RB];
-    unsigned long long R0[RZ_RB], R1[RZ_RB];
+        for (int k = 0; k < 4; k++) c[k] = cxt[min(dx0 + k, dw - 1)];
+        const int sxa = c[0].x & 0xFFFF;
+        uint32_t coef[4];
+        int o[4], d[4];
 #pragma unroll
-    for (int u = 0; u < RZ_RB; u++) {
-        ry[u] = ryt[min(dy0 + u, dh - 1)];   // r0, r1, b0, b1
-        const uint8_t *p0 = src + (long long)ry[u].x * sp, *p1 = src + (long long)ry[u].y * sp;
-        if (fast) {
-            R0[u] = load_u32_unaligned(p0 + sx0) | (unsigned long long)load_u32_unaligned(p0 + sx0 + 4) << 32;
-            R1[u] = load_u32_unaligned(p1 + sx0) | (unsigned long long)load_u32_unaligned(p1 + sx0 + 4) << 32;
-        } else {
-            R0[u] = R1[u] = 0;
-            for (int e = 0; e < 8 && sx0 + e < sw; e++) {
-                R0[u] |= (unsigned long long)p0[sx0 + e] << (8 * e);
-                R1[u] |= (unsigned long long)p1[sx0 + e] << (8 * e);
+        for (int k = 0; k < 4; k++) {
+            o[k] = (c[k].x & 0xFFFF) - sxa;   // <= 3 * scale + 1 <= 7
+            d[k] = c[k].y >> 16;              // sx1 - sx (0 at the right border)
+            coef[k] = (uint32_t)(c[k].x >> 16) | (uint32_t)(c[k].y & 0xFFFF) << 16;
+        }
+        // all loads of a thread's source rows are issued before any use (6 rows x 3 dwords
+        // in flight; the level-1 pass streams the input image from HBM)
+        for (int jb = threadIdx.x >> 5; jb < nsr; jb += 8 * RZ_HJ) {
+            uint32_t D[RZ_HJ][3];
+            int mis[RZ_HJ];
+#pragma unroll
+            for (int u = 0; u < RZ_HJ; u++) {
+                const int j = jb + 8 * u;
+                if (j < nsr) {
+                    const uintptr_t a = (uintptr_t)(src + (long long)(sr0 + j) * sp + sxa);
+                    const uint32_t *pa = (const uint32_t *)(a & ~(uintptr_t)3);
+                    mis[u] = (int)(a & 3);
+                    D[u][0] = pa[0]; D[u][1] = pa[1]; D[u][2] = pa[2];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < RZ_HJ; u++) {
+                const int j = jb + 8 * u;
+                if (j >= nsr) break;
+                uint32_t hv[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int q = o[k] + mis[u];   // byte offset of p[sx] in D0..D2 (<= 10)
+                    const bool up = q > 6;
+                    const int qq = up ? q - 4 : q;
+                    const uint32_t pr = __builtin_amdgcn_perm(up ? D[u][2] : D[u][1], up ? D[u][1] : D[u][0],
+                                                              0x0c000c00u | (uint32_t)(qq + d[k]) << 16 | (uint32_t)qq);
+                    hv[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, pr), __builtin_bit_cast(u16x2, coef[k]), 0u, false);
+                }
+                rz_h[j * 32 + cg] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
             }
         }
     }
-#pragma unroll
-    for (int u = 0; u < RZ_RB; u++) {
-        const int dy = dy0 + u;
-        if (dy >= dh) break;
+    __syncthreads();
+    // 2. vertical pass
+    uint8_t *dst = pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
+    const int n = min(4, dw - dx0);
+    if (n <= 0) return;
+    for (int dy = y0 + (threadIdx.x >> 5); dy < y1; dy += 8) {
+        const int4 ry = ryt[dy];   // r0, r1, b0, b1
+        const uint4 A = rz_h[(ry.x - sr0) * 32 + cg], B = rz_h[(ry.y - sr0) * 32 + cg];
+        const uint32_t S0[4] = {A.x, A.y, A.z, A.w}, S1[4] = {B.x, B.y, B.z, B.w};
         uint32_t out = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int o = (c[k].x & 0xFFFF) - sx0, o1 = o + (c[k].y >> 16);
-            const int a0 = c[k].x >> 16, a1 = c[k].y & 0xFFFF;
-            const int S0 = (int)((R0[u] >> (8 * o)) & 0xFF) * a0 + (int)((R0[u] >> (8 * o1)) & 0xFF) * a1;
-            const int S1 = (int)((R1[u] >> (8 * o)) & 0xFF) * a0 + (int)((R1[u] >> (8 * o1)) & 0xFF) * a1;
-            out |= (uint32_t)resize_px(S0, S1, ry[u], dx0 + k < g.rz_simd_end[l]) << (8 * k);
+            uint32_t v = min((S0[k] * (uint32_t)ry.z + S1[k] * (uint32_t)ry.w + (1u << 21)) >> 22, 255u);
+            if (SIMD && dx0 + k < g.rz_simd_end[l]) v = resize_px_simd((int)S0[k], (int)S1[k], ry);
+            out |= v << (8 * k);
         }
         uint8_t *drow = dst + (long long)dy * g.bp[l];
         if (n == 4) {
@@ -199,8 +226,6 @@ __device__ __forceinline__ int refl101(int i, int n) {
     return i;
 }
 
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ s16x2 vmin2(s16x2 a, s16x2 b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ s16x2 vmax2(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
@@ -1496,6 +1521,14 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
                 rzr.push_back(make_int4(clip(sy), clip(sy + 1), satS((1.f - fy) * 2048), satS(fy * 2048)));
             }
             g.rz_simd_end[l] = e->p.resize_mode ? simd_end_for(dw) : 0;
+            // source rows one output tile spans (LDS of the horizontal pass)
+            int rows = 0;
+            for (int y0 = 0; y0 < dh; y0 += RZ_TH) {
+                const int y1 = std::min(y0 + RZ_TH, dh) - 1;
+                rows = std::max(rows, rzr[g.rz_row_off[l] + y1].y - rzr[g.rz_row_off[l] + y0].x + 1);
+            }
+            if (rows * 32 * (int)sizeof(uint4) > 64 * 1024) return ORBX_EINVAL;
+            e->rz_rows[l] = rows;
         }
         if (rzc.empty()) rzc.push_back(make_int2(0, 0));
         if (rzr.empty()) rzr.push_back(make_int4(0, 0, 0, 0));
@@ -1540,10 +1573,15 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     uint8_t *pyr = e->d_pyr.as<uint8_t>();
     int ph = prof_begin(e, s);
     for (int l = 1; l < L; l++) {
-        const long long tasks = (long long)((g.lw[l] + 3) / 4) * ((g.lh[l] + RZ_RB - 1) / RZ_RB);
-        dim3 grid((unsigned)((tasks + 255) / 256), n);
-        resize_level_kernel<<<grid, 256, 0, s>>>(g, l, e->d_rz.as<int2>() + g.rz_col_off[l],
-                                                 e->d_rzr.as<int4>() + g.rz_row_off[l], d_imgs, pyr);
+        const int tiles_x = (g.lw[l] + RZ_TW - 1) / RZ_TW, tiles_y = (g.lh[l] + RZ_TH - 1) / RZ_TH;
+        const size_t lds = sizeof(uint4) * 32 * (size_t)e->rz_rows[l];
+        const dim3 grid((unsigned)(tiles_x * tiles_y), n);
+        const int2 *cx = e->d_rz.as<int2>() + g.rz_col_off[l];
+        const int4 *ry = e->d_rzr.as<int4>() + g.rz_row_off[l];
+        if (g.resize_mode)
+            resize_level_kernel<true><<<grid, 256, lds, s>>>(g, l, tiles_x, cx, ry, d_imgs, pyr);
+        else
+            resize_level_kernel<false><<<grid, 256, lds, s>>>(g, l, tiles_x, cx, ry, d_imgs, pyr);
     }
     prof_end(e, s, ph, "resize_level_kernel");
     ph = prof_begin(e, s);
