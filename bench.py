@@ -44,23 +44,54 @@ def make_pool(n_pairs: int, seed0: int):
     return [synth.stereo_pair(H, W, seed0 + t) for t in range(n_pairs)]
 
 
+def host_cpu():
+    """(usable host threads, CPU model) of this box; the GPU box's CPU share is 16 threads."""
+    n = len(os.sched_getaffinity(0))
+    n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return max(1, n), model
+
+
 def cpu_baseline(pool, n_frames: int):
-    """Time the CPU oracle (test infrastructure) on n_frames stereo frames, one thread."""
+    """Time the CPU oracle (test infrastructure) on the C2 workload in SURVEY §8d's two modes:
+    throughput (a thread pool over the host's cores, independent frames; the reported value) and
+    single thread (one frame after another). The oracle's C calls release the GIL."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
+    from concurrent.futures import ThreadPoolExecutor
     oracle.build()
-    exL, exR = oracle.Extractor(NFEAT), oracle.Extractor(NFEAT)
     mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+
+    def run(k0, count):
+        exL, exR = oracle.Extractor(NFEAT), oracle.Extractor(NFEAT)
+        for i in range(k0, k0 + count):
+            L, R = pool[i % len(pool)]
+            kL, dL = exL.extract(L)
+            kR, dR = exR.extract(R)
+            oracle.stereo_matches(exL, exR, kL, dL, kR, dR, KITTI_BF, mb)
+
     t0 = time.perf_counter()
-    for i in range(n_frames):
-        L, R = pool[i % len(pool)]
-        kL, dL = exL.extract(L)
-        kR, dR = exR.extract(R)
-        oracle.stereo_matches(exL, exR, kL, dL, kR, dR, KITTI_BF, mb)
-    dt = time.perf_counter() - t0
-    return {"value": round(n_frames / dt, 3), "unit": "stereo frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n_frames} synthetic 1241x376 stereo frames (C2 generator, {len(pool)} distinct), "
-                      f"oracle extract L+R + ComputeStereoMatches, single thread, {dt:.1f} s"}
+    run(0, n_frames)
+    dt1 = time.perf_counter() - t0
+    threads, model = host_cpu()
+    per = max(2, n_frames // 2)
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(lambda k: run(k * per, per), range(threads)))
+        dtn = time.perf_counter() - t0
+    return {"value": round(threads * per / dtn, 3), "unit": "stereo frames/s", "cores": threads, "kind": "port",
+            "sample": f"{threads * per} synthetic 1241x376 stereo frames (C2 generator, {len(pool)} distinct), "
+                      f"oracle extract L+R + ComputeStereoMatches, {threads} threads x {per} frames, {dtn:.1f} s; "
+                      f"host CPU {model}",
+            "single_thread": {"value": round(n_frames / dt1, 3), "cores": 1,
+                              "sample": f"{n_frames} frames one after another, {dt1:.1f} s"}}
 
 
 def bench_localba(amd, args, dist, world, with_cpu):

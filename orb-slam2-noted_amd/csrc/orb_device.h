@@ -125,4 +125,11 @@ __device__ __forceinline__ int wave_lane() { return (int)__lane_id(); }
 // everything derived from it (slot / cell / keypoint ids, their loads and branches) scalar
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
+// order LDS traffic between lanes of one wavefront (LDS executes a wave's ops in order)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 }  // namespace orbamd

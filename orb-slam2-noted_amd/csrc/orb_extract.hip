@@ -227,8 +227,6 @@ __device__ __forceinline__ int refl101(int i, int n) {
 }
 
 
-__device__ __forceinline__ s16x2 vmin2(s16x2 a, s16x2 b) { return __builtin_elementwise_min(a, b); }
-__device__ __forceinline__ s16x2 vmax2(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
 
 // bytes j, j+1 of the little-endian 16-byte segment w[0..3], zero-extended into int16 lanes
 __device__ __forceinline__ s16x2 byte_pair(const uint32_t *w, int j) {
@@ -238,12 +236,6 @@ __device__ __forceinline__ s16x2 byte_pair(const uint32_t *w, int j) {
     return __builtin_bit_cast(s16x2, r);
 }
 
-// order LDS traffic between lanes of one wavefront (LDS executes a wave's ops in order)
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
@@ -315,18 +307,25 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             C[k] = tin[(r + 4) * FB_LD + (cb >> 2) + k];
             S[k] = tin[(r + 7) * FB_LD + (cb >> 2) + k];
         }
+        // Pixel passes the darker bound iff some adjacent compass pair (i, j) has both
+        // e = c - ring - (tlo + 1) >= 0, i.e. the sign bit of (e_i | e_j) is clear; ANDed over
+        // the 4 pairs, (e0|e4)&(e4|e8)&(e8|e12)&(e12|e0) == (e0 & e8) | (e4 & e12): one v_and
+        // + one v_and_or per direction for two pixels (brighter: f = ring - c - (tlo + 1)).
         const s16x2 th1 = {(short)(tlo + 1), (short)(tlo + 1)};
         uint32_t cand = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const s16x2 c = byte_pair(C, 4 + 2 * q);
-            const s16x2 d0 = c - byte_pair(S, 4 + 2 * q);    // ring 0  (0, +3)
-            const s16x2 d4 = c - byte_pair(C, 7 + 2 * q);    // ring 4  (+3, 0)
-            const s16x2 d8 = c - byte_pair(N, 4 + 2 * q);    // ring 8  (0, -3)
-            const s16x2 d12 = c - byte_pair(C, 1 + 2 * q);   // ring 12 (-3, 0)
-            const s16x2 a = vmax2(vmax2(vmin2(d0, d4), vmin2(d4, d8)), vmax2(vmin2(d8, d12), vmin2(d12, d0)));
-            const s16x2 bb = vmin2(vmin2(vmax2(d0, d4), vmax2(d4, d8)), vmin2(vmax2(d8, d12), vmax2(d12, d0)));
-            const uint32_t u = __builtin_bit_cast(uint32_t, vmax2(a, -bb) - th1);  // lane >= 0 <=> bound > tlo
+            const s16x2 cm = c - th1, cp = c + th1;
+            const s16x2 r0 = byte_pair(S, 4 + 2 * q);    // ring 0  (0, +3)
+            const s16x2 r4 = byte_pair(C, 7 + 2 * q);    // ring 4  (+3, 0)
+            const s16x2 r8 = byte_pair(N, 4 + 2 * q);    // ring 8  (0, -3)
+            const s16x2 r12 = byte_pair(C, 1 + 2 * q);   // ring 12 (-3, 0)
+            const uint32_t e0 = __builtin_bit_cast(uint32_t, cm - r0), e4 = __builtin_bit_cast(uint32_t, cm - r4);
+            const uint32_t e8 = __builtin_bit_cast(uint32_t, cm - r8), e12 = __builtin_bit_cast(uint32_t, cm - r12);
+            const uint32_t f0 = __builtin_bit_cast(uint32_t, r0 - cp), f4 = __builtin_bit_cast(uint32_t, r4 - cp);
+            const uint32_t f8 = __builtin_bit_cast(uint32_t, r8 - cp), f12 = __builtin_bit_cast(uint32_t, r12 - cp);
+            const uint32_t u = ((e0 & e8) | (e4 & e12)) & ((f0 & f8) | (f4 & f12));   // sign clear <=> candidate
             cand |= (((~u >> 15) & 1u) | ((~u >> 30) & 2u)) << (2 * q);
         }
         const int y = y0 + r, xb = x0 + cb;

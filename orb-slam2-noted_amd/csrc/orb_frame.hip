@@ -146,158 +146,220 @@ __device__ inline int hamming32(const uint8_t *a, const uint8_t *b) {
            __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
 }
 
+
+// SearchForInitialization in two phases.
+// Phase A (search_init_cand_kernel, one wavefront per F1 keypoint of octave 0, all pairs at
+// once): GetFeaturesInArea's candidates in its order (ix, iy, insertion; Frame.cc:631-666),
+// level and square-window filtered, with their Hamming distance and rotation bin, compacted
+// in order into a per-keypoint list: entry = i2 | dist << 16 | bin << 25. None of this
+// depends on the greedy state.
+// Phase B (search_init_resolve_kernel, one workgroup per pair): the greedy claim loop over i1
+// in index order (ORBmatcher.cc:614-712) on LDS state only -- vMatchedDistance filter, first
+// minimum and second distance by a wave min over (dist, position) keys, eviction of the
+// previous owner -- then ComputeThreeMaxima pruning (:2076-2118). The lists are staged into LDS
+// in chunks by all four wavefronts; wavefront 0 walks them.
 struct SearchArgs {
     // F1 = image f1_base + f1_step * p, F2 = image f2_base + f2_step * p
     int f1_base, f1_step, f2_base, f2_step;
     const orbx_kp *kun;
     const uint8_t *desc;
     const int *cnt;
-    int cap, sort_cap;
-    const uint32_t *keys;   // grid-sorted keys per image
+    int cap, sort_cap, cap0;   // cap0: level-0 keypoint capacity (list length bound)
+    const uint32_t *keys;      // grid-sorted keys per image
     const int *nkeys;
     GridParams gp;
     float r, nnratio;
     int check_ori;
+    uint32_t *list;            // [pair][cap0][cap0] candidate entries
+    int *lcnt;                 // [pair][cap0] entries per F1 keypoint
+    int stage_cap;             // LDS entry budget of phase B
 };
 
-// One wave per (F1, F2) pair. LDS: F2 sorted keys, vMatchedDistance, vnMatches21.
-__global__ __launch_bounds__(64) void search_init_kernel(SearchArgs a, float *prev_xy, int *m12, int *nmatch) {
-    extern __shared__ int lds[];
-    const int p = blockIdx.x, lane = threadIdx.x;
+__device__ __forceinline__ int rot_bin(float a1, float a2) {   // ORBmatcher.cc:700-707 (factor 30/360)
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * (30 / 360.0f));
+    if (bin == 30) bin = 0;
+    return bin;
+}
+
+__global__ __launch_bounds__(256) void search_init_cand_kernel(SearchArgs a, const float *prev_xy) {
+    __shared__ int run_pre_s[4][65];
+    __shared__ int run_lo_s[4][64];
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    const int p = blockIdx.y, i1 = blockIdx.x * 4 + wv;
+    if (i1 >= a.cap0) return;
     const int i1img = a.f1_base + a.f1_step * p, i2img = a.f2_base + a.f2_step * p;
-    const int N1 = min(a.cnt[i1img], a.cap), N2 = min(a.cnt[i2img], a.cap);
-    const int nk = a.nkeys[i2img];
-    uint32_t *sk = (uint32_t *)lds;
-    int *vMD = lds + a.sort_cap;
-    int *v21 = vMD + a.cap;
-    __shared__ int run_pre[65];
-    __shared__ int run_lo[64];
-    __shared__ int8_t bin_of[4096];
-    const uint32_t *gk = a.keys + (long long)i2img * a.sort_cap;
-    for (int i = lane; i < nk; i += 64) sk[i] = gk[i];
-    for (int i = lane; i < N2; i += 64) { vMD[i] = INT_MAX; v21[i] = -1; }
+    const int N1 = min(a.cnt[i1img], a.cap);
+    int *cnt_out = a.lcnt + (long long)p * a.cap0 + i1;
+    if (i1 >= N1) { if (lane == 0) *cnt_out = 0; return; }
     const orbx_kp *K1 = a.kun + (long long)i1img * a.cap, *K2 = a.kun + (long long)i2img * a.cap;
-    const uint8_t *D1 = a.desc + (long long)i1img * a.cap * 32, *D2 = a.desc + (long long)i2img * a.cap * 32;
-    float *pxy = prev_xy + (long long)p * a.cap * 2;
-    int *M12 = m12 + (long long)p * a.cap;
-    for (int i = lane; i < N1; i += 64) { M12[i] = -1; if (i < 4096) bin_of[i] = -1; }
-    __syncthreads();
-    int nmatches = 0;
+    const orbx_kp kp1 = K1[i1];
+    const float x = prev_xy[((long long)p * a.cap + i1) * 2], y = prev_xy[((long long)p * a.cap + i1) * 2 + 1];
     const float r = a.r;
-    for (int i1 = 0; i1 < N1; i1++) {
-        const orbx_kp kp1 = K1[i1];
-        if (kp1.octave > 0) continue;
-        const float x = pxy[2 * i1], y = pxy[2 * i1 + 1];
-        // GetFeaturesInArea (Frame.cc:590-671) cell window
-        const int cMinX = (int)floorf((x - a.gp.minX - r) * a.gp.invW);
-        const int nMinCellX = max(0, cMinX);
-        if (nMinCellX >= GRID_COLS) continue;
-        const int nMaxCellX = min(GRID_COLS - 1, (int)ceilf((x - a.gp.minX + r) * a.gp.invW));
-        if (nMaxCellX < 0) continue;
-        const int nMinCellY = max(0, (int)floorf((y - a.gp.minY - r) * a.gp.invH));
-        if (nMinCellY >= GRID_ROWS) continue;
-        const int nMaxCellY = min(GRID_ROWS - 1, (int)ceilf((y - a.gp.minY + r) * a.gp.invH));
-        if (nMaxCellY < 0) continue;
-        const int nx = nMaxCellX - nMinCellX + 1;
-        int len = 0, lo = 0;
-        if (lane < nx) {
-            const int ix = nMinCellX + lane;
-            const uint32_t k0 = (uint32_t)(ix * GRID_ROWS + nMinCellY) << 16;
-            const uint32_t k1 = ((uint32_t)(ix * GRID_ROWS + nMaxCellY) << 16) | 0xFFFFu;
-            lo = lower_bound_u32(sk, nk, k0);
-            len = lower_bound_u32(sk, nk, k1 + 1u) - lo;
-            if (k1 == 0xFFFFFFFFu) len = nk - lo;
-        }
-        // exclusive prefix of run lengths over lanes
-        int incl = len;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += v;
-        }
-        run_pre[lane] = incl - len;
-        run_lo[lane] = lo;
-        if (lane == 63) run_pre[64] = incl;
-        __syncthreads();
-        const int total = run_pre[64];
-        unsigned long long best = ~0ull;   // (dist << 32) | candidate position
-        int bestcnt = 0;                   // how many candidates have the best distance
-        int second = INT_MAX;
-        // per-lane partial: best key, count of its distance, second distinct-or-dup
-        int ldist = INT_MAX, lcnt = 0, lsec = INT_MAX;
-        unsigned lpos = 0xFFFFFFFFu;
-        for (int base = 0; base < total; base += 64) {
-            const int c = base + lane;
-            if (c < total) {
-                int rr = 0;  // run containing c
-                int hi = min(nx, 64) - 1;
-                while (rr < hi) {
-                    const int m = (rr + hi + 1) >> 1;
-                    if (run_pre[m] <= c) rr = m; else hi = m - 1;
-                }
-                const int pos = run_lo[rr] + (c - run_pre[rr]);
-                const int i2 = (int)(sk[pos] & 0xFFFFu);
-                const orbx_kp kp2 = K2[i2];
-                const bool lvl_ok = !(kp2.octave < 0) && !(kp2.octave > 0);   // minLevel = maxLevel = 0
-                if (lvl_ok && fabsf(kp2.x - x) < r && fabsf(kp2.y - y) < r) {
-                    const int dist = hamming32(D1 + (long long)i1 * 32, D2 + (long long)i2 * 32);
-                    if (!(vMD[i2] <= dist)) {
-                        if (dist < ldist) { lsec = ldist == INT_MAX ? lsec : min(lsec, ldist); ldist = dist; lpos = (unsigned)c; lcnt = 1; }
-                        else if (dist == ldist) { lcnt++; lsec = min(lsec, dist); }
-                        else lsec = min(lsec, dist);
-                    }
-                }
-            }
-        }
-        // wave merge: best = min (dist, pos); second = min over the multiset minus best
-        for (int off = 32; off > 0; off >>= 1) {
-            const int od = __shfl_xor(ldist, off, 64), oc = __shfl_xor(lcnt, off, 64), os = __shfl_xor(lsec, off, 64);
-            const unsigned op = (unsigned)__shfl_xor((int)lpos, off, 64);
-            int nd, nc, ns;
-            unsigned np;
-            if (od < ldist || (od == ldist && op < lpos)) {
-                nd = od; np = op;
-            } else {
-                nd = ldist; np = lpos;
-            }
-            if (od == ldist) nc = oc + lcnt; else nc = od < ldist ? oc : lcnt;
-            ns = min(lsec, os);
-            if (od != ldist) ns = min(ns, max(od, ldist) == INT_MAX ? INT_MAX : max(od, ldist));
-            ldist = nd; lpos = np; lcnt = nc; lsec = ns;
-        }
-        (void)best; (void)bestcnt; (void)second;
-        const int bestDist = ldist;
-        const int bestDist2 = lcnt >= 2 ? ldist : lsec;
-        if (lane == 0 && bestDist != INT_MAX && bestDist <= 50 && bestDist < (float)bestDist2 * a.nnratio) {
-            int cc = (int)lpos;
-            int rr = 0, hi = min(nx, 64) - 1;
+    // GetFeaturesInArea (Frame.cc:590-671) cell window
+    const int nMinCellX = max(0, (int)floorf((x - a.gp.minX - r) * a.gp.invW));
+    const int nMaxCellX = min(GRID_COLS - 1, (int)ceilf((x - a.gp.minX + r) * a.gp.invW));
+    const int nMinCellY = max(0, (int)floorf((y - a.gp.minY - r) * a.gp.invH));
+    const int nMaxCellY = min(GRID_ROWS - 1, (int)ceilf((y - a.gp.minY + r) * a.gp.invH));
+    if (kp1.octave > 0 || nMinCellX >= GRID_COLS || nMaxCellX < 0 || nMinCellY >= GRID_ROWS || nMaxCellY < 0) {
+        if (lane == 0) *cnt_out = 0;
+        return;
+    }
+    const int nk = a.nkeys[i2img];
+    const uint32_t *sk = a.keys + (long long)i2img * a.sort_cap;
+    int *run_pre = run_pre_s[wv], *run_lo = run_lo_s[wv];
+    const int nx = nMaxCellX - nMinCellX + 1;
+    int len = 0, lo = 0;
+    if (lane < nx) {
+        const int ix = nMinCellX + lane;
+        const uint32_t k0 = (uint32_t)(ix * GRID_ROWS + nMinCellY) << 16;
+        const uint32_t k1 = ((uint32_t)(ix * GRID_ROWS + nMaxCellY) << 16) | 0xFFFFu;
+        lo = lower_bound_u32(sk, nk, k0);
+        len = lower_bound_u32(sk, nk, k1 + 1u) - lo;
+        if (k1 == 0xFFFFFFFFu) len = nk - lo;
+    }
+    int incl = len;   // exclusive prefix of run lengths over lanes
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    run_pre[lane] = incl - len;
+    run_lo[lane] = lo;
+    if (lane == 63) run_pre[64] = incl;
+    wave_lds_sync();
+    const int total = run_pre[64];
+    const uint8_t *d1 = a.desc + ((long long)i1img * a.cap + i1) * 32;
+    const uint8_t *D2 = a.desc + (long long)i2img * a.cap * 32;
+    uint32_t *out = a.list + ((long long)p * a.cap0 + i1) * a.cap0;
+    int n = 0;
+    for (int base = 0; base < total; base += 64) {
+        const int c = base + lane;
+        bool keep = false;
+        uint32_t ent = 0;
+        if (c < total) {
+            int rr = 0, hi = min(nx, 64) - 1;   // run containing c
             while (rr < hi) {
                 const int m = (rr + hi + 1) >> 1;
-                if (run_pre[m] <= cc) rr = m; else hi = m - 1;
+                if (run_pre[m] <= c) rr = m; else hi = m - 1;
             }
-            const int bestIdx2 = (int)(sk[run_lo[rr] + (cc - run_pre[rr])] & 0xFFFFu);
-            if (v21[bestIdx2] >= 0) { M12[v21[bestIdx2]] = -1; nmatches--; }
-            M12[i1] = bestIdx2;
-            v21[bestIdx2] = i1;
-            vMD[bestIdx2] = bestDist;
-            nmatches++;
-            if (a.check_ori) {
-                float rot = kp1.angle - K2[bestIdx2].angle;
-                if (rot < 0.0) rot += 360.0f;
-                int bin = (int)roundf(rot * (30 / 360.0f));
-                if (bin == 30) bin = 0;
-                if (i1 < 4096) bin_of[i1] = (int8_t)bin;
+            const int i2 = (int)(sk[run_lo[rr] + (c - run_pre[rr])] & 0xFFFFu);
+            const orbx_kp kp2 = K2[i2];
+            // minLevel = maxLevel = 0 (ORBmatcher.cc:626) and the square window (Frame.cc:655)
+            if (!(kp2.octave < 0) && !(kp2.octave > 0) && fabsf(kp2.x - x) < r && fabsf(kp2.y - y) < r) {
+                const int dist = hamming32(d1, D2 + (long long)i2 * 32);
+                const int bin = a.check_ori ? rot_bin(kp1.angle, kp2.angle) : 0;
+                ent = (uint32_t)i2 | (uint32_t)dist << 16 | (uint32_t)bin << 25;
+                keep = true;
+            }
+        }
+        const unsigned long long bal = __ballot(keep);
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (keep && n + rank < a.cap0) out[n + rank] = ent;
+        n += __popcll(bal);
+    }
+    if (lane == 0) *cnt_out = min(n, a.cap0);
+}
+
+__device__ __forceinline__ void min2_merge(uint32_t &k1, uint32_t &k2, uint32_t o1, uint32_t o2) {
+    const uint32_t lo = min(k1, o1), hi = max(k1, o1);
+    k1 = lo;
+    k2 = min(hi, min(k2, o2));
+}
+
+__global__ __launch_bounds__(256) void search_init_resolve_kernel(SearchArgs a, float *prev_xy, int *m12, int *nmatch) {
+    extern __shared__ uint32_t rs_lds[];
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+    const int i1img = a.f1_base + a.f1_step * p, i2img = a.f2_base + a.f2_step * p;
+    const int N1 = min(a.cnt[i1img], a.cap);
+    const int n1s = min(N1, a.cap0);   // F1 keypoints with a list (octave 0 is a prefix)
+    // LDS: stage[stage_cap] u32 | pre[cap0 + 1] i32 | vMD[cap] u16 | v21[cap] i16 | M12[cap] i16 | bin[cap] i8
+    uint32_t *stage = rs_lds;
+    int *pre = (int *)(stage + a.stage_cap);
+    uint16_t *vMD = (uint16_t *)(pre + a.cap0 + 1);
+    int16_t *v21 = (int16_t *)(vMD + a.cap);
+    int16_t *M12 = v21 + a.cap;
+    int8_t *bin_of = (int8_t *)(M12 + a.cap);
+    for (int i = tid; i < a.cap; i += 256) { vMD[i] = 0xFFFF; v21[i] = -1; M12[i] = -1; bin_of[i] = -1; }
+    const int *lc = a.lcnt + (long long)p * a.cap0;
+    if (wv == 0) {   // exclusive prefix of list lengths
+        int carry = 0;
+        for (int b0 = 0; b0 < n1s; b0 += 64) {
+            const int v = b0 + lane < n1s ? lc[b0 + lane] : 0;
+            int incl = v;
+            for (int off = 1; off < 64; off <<= 1) {
+                const int t = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += t;
+            }
+            if (b0 + lane < n1s) pre[b0 + lane] = carry + incl - v;
+            carry += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) pre[n1s] = carry;
+    }
+    __syncthreads();
+    const uint32_t *L = a.list + (long long)p * a.cap0 * a.cap0;
+    int nmatches = 0;
+    for (int s0 = 0; s0 < n1s;) {
+        // chunk [s0, e0): as many lists as fit the stage (every list fits: cap0 <= stage_cap)
+        int lo = s0 + 1, hi = n1s;
+        while (lo < hi) {
+            const int m = (lo + hi + 1) >> 1;
+            if (pre[m] - pre[s0] <= a.stage_cap) lo = m; else hi = m - 1;
+        }
+        const int e0 = lo;
+        for (int i1 = s0 + wv; i1 < e0; i1 += 4) {
+            const int n = pre[i1 + 1] - pre[i1], o = pre[i1] - pre[s0];
+            for (int j = lane; j < n; j += 64) stage[o + j] = L[(long long)i1 * a.cap0 + j];
+        }
+        __syncthreads();
+        if (wv == 0) {
+            for (int i1 = s0; i1 < e0; i1++) {
+                const int n = pre[i1 + 1] - pre[i1], o = pre[i1] - pre[s0];
+                if (n == 0) continue;
+                uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;   // two smallest (dist << 12 | position)
+                for (int j = lane; j < n; j += 64) {
+                    const uint32_t ent = stage[o + j];
+                    const int i2 = (int)(ent & 0xFFFFu), dist = (int)((ent >> 16) & 0x1FFu);
+                    if (!((int)vMD[i2] <= dist)) min2_merge(k1, k2, (uint32_t)dist << 12 | (uint32_t)j, 0xFFFFFFFFu);
+                }
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint32_t o1 = (uint32_t)__shfl_xor((int)k1, off, 64), o2 = (uint32_t)__shfl_xor((int)k2, off, 64);
+                    min2_merge(k1, k2, o1, o2);
+                }
+                if (k1 == 0xFFFFFFFFu) continue;
+                const int bestDist = (int)(k1 >> 12);
+                const int bestDist2 = k2 == 0xFFFFFFFFu ? INT_MAX : (int)(k2 >> 12);
+                if (bestDist <= 50 && bestDist < (float)bestDist2 * a.nnratio) {   // TH_LOW, mfNNratio
+                    const uint32_t ent = stage[o + (int)(k1 & 0xFFFu)];
+                    const int bestIdx2 = (int)(ent & 0xFFFFu);
+                    const int prev = v21[bestIdx2];
+                    if (prev >= 0) nmatches--;
+                    nmatches++;
+                    if (lane == 0) {
+                        if (prev >= 0) M12[prev] = -1;
+                        M12[i1] = (int16_t)bestIdx2;
+                        v21[bestIdx2] = (int16_t)i1;
+                        vMD[bestIdx2] = (uint16_t)bestDist;
+                        if (a.check_ori) bin_of[i1] = (int8_t)(ent >> 25);
+                    }
+                    wave_lds_sync();
+                }
             }
         }
         __syncthreads();
+        s0 = e0;
     }
+    __shared__ int hist[30];
+    __shared__ int ind[3];
+    __shared__ int removed;
+    if (tid < 30) hist[tid] = 0;
+    if (tid == 0) removed = 0;
+    __syncthreads();
     if (a.check_ori) {   // ComputeThreeMaxima over the acceptance events, prune other bins
-        __shared__ int hist[30];
-        if (lane < 30) hist[lane] = 0;
-        __syncthreads();
-        for (int i = lane; i < min(N1, 4096); i += 64)
+        for (int i = tid; i < n1s; i += 256)
             if (bin_of[i] >= 0) atomicAdd(&hist[bin_of[i]], 1);
         __syncthreads();
-        if (lane == 0) {
+        if (tid == 0) {
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < 30; i++) {
                 const int s = hist[i];
@@ -307,18 +369,27 @@ __global__ __launch_bounds__(64) void search_init_kernel(SearchArgs a, float *pr
             }
             if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
             else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-            for (int i = 0; i < min(N1, 4096); i++) {
-                const int bb = bin_of[i];
-                if (bb < 0 || bb == ind1 || bb == ind2 || bb == ind3) continue;
-                if (M12[i] >= 0) { M12[i] = -1; nmatches--; }
-            }
+            ind[0] = ind1; ind[1] = ind2; ind[2] = ind3;
         }
         __syncthreads();
+        int mine = 0;
+        for (int i = tid; i < n1s; i += 256) {
+            const int bb = bin_of[i];
+            if (bb < 0 || bb == ind[0] || bb == ind[1] || bb == ind[2]) continue;
+            if (M12[i] >= 0) { M12[i] = -1; mine++; }
+        }
+        if (mine) atomicAdd(&removed, mine);
+        __syncthreads();
     }
-    if (lane == 0) nmatch[p] = nmatches;
-    __syncthreads();
-    for (int i = lane; i < N1; i += 64)
-        if (M12[i] >= 0) { pxy[2 * i] = K2[M12[i]].x; pxy[2 * i + 1] = K2[M12[i]].y; }
+    if (tid == 0) nmatch[p] = nmatches - removed;
+    const orbx_kp *K2 = a.kun + (long long)i2img * a.cap;
+    float *pxy = prev_xy + (long long)p * a.cap * 2;
+    int *out = m12 + (long long)p * a.cap;
+    for (int i = tid; i < N1; i += 256) {
+        const int m = i < n1s ? (int)M12[i] : -1;
+        out[i] = m;
+        if (m >= 0) { pxy[2 * i] = K2[m].x; pxy[2 * i + 1] = K2[m].y; }
+    }
 }
 
 __global__ __launch_bounds__(256) void init_prev_xy(const orbx_kp *kun, const int *cnt, int cap, int f1_base,
@@ -366,7 +437,7 @@ static GridParams make_grid(const Camera &c, int cols, int rows) {
 using namespace orbframe;
 
 struct orbf_state {
-    DevBuf kun, uR, dep, keys, nkeys, prev, m12, nmatch, depth_in;
+    DevBuf kun, uR, dep, keys, nkeys, prev, m12, nmatch, depth_in, list, lcnt;
 };
 
 static orbf_state &fstate(orbx_engine *e) {
@@ -429,7 +500,7 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
     if (f1_base + f1_step * (n_pairs - 1) >= n || f2_base + f2_step * (n_pairs - 1) >= n) return ORBX_EINVAL;
     int sort_cap = 1;
     while (sort_cap < cap) sort_cap <<= 1;
-    if (cap > 4096 || sort_cap > 4096) return ORBX_EINVAL;
+    if (cap > 4096 || sort_cap > 4096 || cap > 32767) return ORBX_EINVAL;
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
     const Camera cam = make_camera(K, dist, 0.f);
     const GridParams gp = make_grid(cam, e->W, e->H);
@@ -443,6 +514,8 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
     prof_end(e, s, ph, "grid_sort_kernel");
     init_prev_xy<<<dim3((cap + 255) / 256, n_pairs), 256, 0, s>>>(S.kun.as<orbx_kp>(), e->d_cnt.as<int>(), cap, f1_base,
                                                                   f1_step, S.prev.as<float>());
+    const int cap0 = e->g.out_cap[0];
+    if (S.list.ensure(4 * (size_t)n_pairs * cap0 * cap0) || S.lcnt.ensure(4 * (size_t)n_pairs * cap0)) return ORBX_EDEVICE;
     SearchArgs a;
     a.f1_base = f1_base; a.f1_step = f1_step; a.f2_base = f2_base; a.f2_step = f2_step;
     a.kun = S.kun.as<orbx_kp>();
@@ -450,15 +523,23 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
     a.cnt = e->d_cnt.as<int>();
     a.cap = cap;
     a.sort_cap = sort_cap;
+    a.cap0 = cap0;
     a.keys = S.keys.as<uint32_t>();
     a.nkeys = S.nkeys.as<int>();
     a.gp = gp;
     a.r = (float)window;
     a.nnratio = nnratio;
     a.check_ori = check_ori;
+    a.list = S.list.as<uint32_t>();
+    a.lcnt = S.lcnt.as<int>();
+    // phase B LDS: stage + prefix + vMD/v21/M12 (u16) + bins (i8); stage gets the rest of 60 KB
+    const size_t fixed = 4 * ((size_t)cap0 + 1) + 7 * (size_t)cap + 16;
+    a.stage_cap = (int)std::min<size_t>(16384, (60 * 1024 - fixed) / 4);
+    if (a.stage_cap < cap0) return ORBX_EINVAL;
+    const size_t lds = 4 * (size_t)a.stage_cap + fixed;
     ph = prof_begin(e, s);
-    search_init_kernel<<<n_pairs, 64, 4 * (sort_cap + 2 * cap), s>>>(a, S.prev.as<float>(), S.m12.as<int>(),
-                                                                    S.nmatch.as<int>());
+    search_init_cand_kernel<<<dim3((cap0 + 3) / 4, n_pairs), 256, 0, s>>>(a, S.prev.as<float>());
+    search_init_resolve_kernel<<<n_pairs, 256, lds, s>>>(a, S.prev.as<float>(), S.m12.as<int>(), S.nmatch.as<int>());
     prof_end(e, s, ph, "search_init_kernel");
     FR_CHK(hipGetLastError());
     return ORBX_OK;

@@ -70,3 +70,39 @@ def test_rgbd_host_path(amd, oracle_mod):
     ku, u, d = amd.compute_stereo_from_rgbd(ex, len(k), depth, K_TUM, D_TUM, BF_TUM)
     rk, rd, rku, ru, rdep = _oracle_frame(oracle_mod, gray, depth, K_TUM, D_TUM)
     assert ku.tobytes() == rku.tobytes() and u.tobytes() == ru.tobytes() and d.tobytes() == rdep.tobytes()
+
+
+@pytest.mark.parametrize("window,nnratio,check_ori,gap", [(50, 0.9, True, 1), (200, 0.9, True, 2),
+                                                          (100, 0.7, False, 1), (100, 0.95, True, 3)])
+def test_search_init_variants(amd, oracle_mod, window, nnratio, check_ori, gap):
+    """Two-phase GPU SearchForInitialization (candidate lists, then the greedy claim walk) vs the
+    oracle over windows, ratios, rotation check on/off and frames `gap` apart (larger motion,
+    more evictions)."""
+    import torch
+    T = 6
+    frames = [synth.rgbd_frame(480, 640, 10 + t) for t in range(T)]
+    grays = np.stack([f[0] for f in frames])
+    depths = np.stack([f[1] for f in frames])
+    dg = torch.from_numpy(grays).cuda()
+    dd = torch.from_numpy(depths).cuda()
+    ex = amd.BatchExtractor(1000)
+    ex.reserve(640, 480, T)
+    torch.cuda.synchronize()
+    ex.extract_device(dg.data_ptr(), T, 640, 480, 640, 640 * 480)
+    ex.rgbd_device(dd.data_ptr(), 640 * 480, 640, K_TUM, D_TUM, BF_TUM)
+    n_pairs = T - gap
+    ex.search_init_device(n_pairs, 0, 1, gap, 1, K_TUM, D_TUM, window, nnratio, check_ori)
+    bounds = oracle_mod.image_bounds(640, 480, K_TUM, D_TUM)
+    ref = [_oracle_frame(oracle_mod, grays[t], depths[t], K_TUM, D_TUM) for t in range(T)]
+    for p in range(n_pairs):
+        k1, d1, ku1, _, _ = ref[p]
+        k2, d2, ku2, _, _ = ref[p + gap]
+        G1 = oracle_mod.Grid(ku1, d1, bounds)
+        G2 = oracle_mod.Grid(ku2, d2, bounds)
+        prev = np.stack([ku1["x"], ku1["y"]], 1)
+        nm, m12, prev_out = oracle_mod.search_for_initialization(G1, G2, prev, window, nnratio, check_ori)
+        gn, gm, gxy = ex.search_init_fetch(p)
+        n1 = len(k1)
+        np.testing.assert_array_equal(gm[:n1], m12)
+        assert gn == nm
+        assert gxy[:n1].tobytes() == prev_out.tobytes()
