@@ -371,6 +371,51 @@ def bench_bowmatch(amd, args, dist, world, with_cpu):
     return res
 
 
+def bench_newpts(amd, args, dist, world, with_cpu):
+    """§8f rank 4: the triangulation loop of LocalMapping::CreateNewMapPoints on B (current
+    keyframe, neighbour) slots resident in HBM, ~1200 SearchForTriangulation pairs each
+    (synth.newpoints_problem, KITTI stereo and TUM RGB-D alternating)."""
+    from orbslam2_amd import synth
+    from orbslam2_amd import dist as odist
+    B = args.newpts_batch
+    probs = [synth.newpoints_problem(1100 + i, cam="kitti" if i % 2 == 0 else "tum") for i in range(8)]
+    m = amd.NewMapPoints()
+    m.reserve(B, 1500, max(len(p["pairs"]) for p in probs))
+    for s in range(B):
+        m.stage(s, probs[s % len(probs)])
+    n_pairs = sum(len(probs[s % len(probs)]["pairs"]) for s in range(B))
+    for _ in range(2):
+        m.run_batch(B)
+    amd.device_sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.newpts_steps):
+        m.run_batch(B)
+    amd.device_sync()
+    dt = odist.max_over_ranks(time.perf_counter() - t0, COLL_DEV, dist)
+    n0, _, _ = m.fetch(0, len(probs[0]["pairs"]))
+    res = {"newpts_matches_per_s": round(world * n_pairs * args.newpts_steps / dt, 1),
+           "newpts": {"slots_per_step": B, "matches_per_step": n_pairs,
+                      "ms_per_step": round(1000 * dt / args.newpts_steps, 4), "new_points_slot0": int(n0),
+                      "dtype": "f32 / f64 (OpenCV float Jacobi SVD with double norms)"}}
+    m.close()
+    if with_cpu:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+        n = k = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 3.0:
+            p = probs[k % len(probs)]
+            oracle.triangulate(p)
+            n += len(p["pairs"])
+            k += 1
+        cdt = time.perf_counter() - t0
+        res["newpts"]["cpu_baseline"] = {"value": round(n / cdt, 1), "unit": "matches/s", "cores": 1, "kind": "port",
+                                         "sample": f"{n} matches (8 distinct keyframe pairs), oracle, single thread, {cdt:.1f} s"}
+    return res
+
+
 def load_pmc(kernel: str, batch: int, field: str = "hbm_bytes_per_launch"):
     """Per-launch figure of `kernel` from the committed rocprofv3 PMC summary, if any."""
     f = ROOT / "profiles" / "pmc_traffic.json"
@@ -424,6 +469,9 @@ def main():
     ap.add_argument("--bowmatch-batch", type=int, default=256)
     ap.add_argument("--bowmatch-steps", type=int, default=10)
     ap.add_argument("--no-bowmatch", action="store_true")
+    ap.add_argument("--newpts-batch", type=int, default=256)
+    ap.add_argument("--newpts-steps", type=int, default=10)
+    ap.add_argument("--no-newpts", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -551,6 +599,8 @@ def main():
         out.update(bench_bow(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if not args.no_bowmatch:
         out.update(bench_bowmatch(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
+    if not args.no_newpts:
+        out.update(bench_newpts(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if not args.no_lba:
         out.update(bench_localba(amd, args, dist, world, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -375,6 +375,45 @@ int orbp_stage(orbp_engine *e, int slot, const orbp_frame *f);
 int orbp_run_batch(orbp_engine *e, int n_slots, void *stream);
 int orbp_fetch(orbp_engine *e, int slot, orbp_result *r);
 
+/* -------- new map points (replaces the triangulation loop of LocalMapping::CreateNewMapPoints) -------- */
+
+/* A KeyFrame as LocalMapping::CreateNewMapPoints (LocalMapping.cc:295-600) reads it. Host pointers. */
+typedef struct {
+    int32_t n;                   /* N */
+    const orbx_kp *keys;         /* mvKeys (KeyFrame::UnprojectStereo reads the distorted pt) */
+    const orbx_kp *keys_un;      /* mvKeysUn */
+    const float *u_right;        /* mvuRight */
+    const float *depth;          /* mvDepth */
+    float Tcw[12];               /* GetPose() rows 0..2 = [Rcw | tcw], CV_32F */
+    float Ow[3];                 /* GetCameraCenter() (= Twc translation, KeyFrame::SetPose) */
+    float fx, fy, cx, cy, invfx, invfy, mb, mbf;
+    int32_t nlevels;
+    float scale_factors[16];     /* mvScaleFactors */
+    float level_sigma2[16];      /* mvLevelSigma2 */
+} orbn_keyframe;
+
+typedef struct orbn_engine orbn_engine;
+int orbn_create(orbn_engine **out);
+void orbn_destroy(orbn_engine *e);
+
+/* The per-match body of LocalMapping::CreateNewMapPoints (LocalMapping.cc:396-600) for one
+ * (mpCurrentKeyFrame = kf1, pKF2 = kf2) neighbour: pairs[2k], pairs[2k+1] = vMatchedIndices[k]
+ * (orbb_search_for_triangulation's output). Parallax test, linear triangulation by
+ * cv::SVD(A, MODIFY_A | FULL_UV) (OpenCV's float Jacobi SVD) or KeyFrame::UnprojectStereo,
+ * positive depth, reprojection chi2 (5.991 / 7.8) in both keyframes, scale consistency with
+ * ratio_factor = 1.5f * mpCurrentKeyFrame->mfScaleFactor. ok[k] = 1 where the reference creates
+ * a MapPoint at x3d[3k..3k+2]; *nnew = their count. The baseline test and F12 before the
+ * matcher, and the MapPoint bookkeeping after, stay with the caller (per keyframe, not per
+ * match). */
+int orbn_triangulate(orbn_engine *e, const orbn_keyframe *kf1, const orbn_keyframe *kf2, const int32_t *pairs,
+                     int32_t npairs, float ratio_factor, float *x3d, uint8_t *ok, int32_t *nnew);
+/* Batched device-resident form: stage (kf1, kf2, pairs) into slots, one launch for all. */
+int orbn_reserve(orbn_engine *e, int n_slots, int cap_kp, int cap_pairs);
+int orbn_stage(orbn_engine *e, int slot, const orbn_keyframe *kf1, const orbn_keyframe *kf2, const int32_t *pairs,
+               int32_t npairs, float ratio_factor);
+int orbn_run_batch(orbn_engine *e, int n_slots, void *stream);
+int orbn_fetch(orbn_engine *e, int slot, float *x3d, uint8_t *ok, int32_t *nnew);
+
 /* -------- local bundle adjustment (replaces Optimizer::LocalBundleAdjustment) -------- */
 
 /* The graph Optimizer::LocalBundleAdjustment (Optimizer.cc:646-898) builds from the map,

@@ -602,3 +602,57 @@ def fuse_candidates(prob: dict, th=3.0):
     bd = np.zeros(max(M.n, 1), np.int32)
     L.orc_fuse_candidates(C.byref(F), C.byref(M), th, bi.ctypes.data, bd.ctypes.data)
     return bi[: M.n], bd[: M.n]
+
+
+# ---- new map points (newpts_oracle.c)
+class OrbnKeyFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("keys", C.c_void_p), ("keys_un", C.c_void_p), ("u_right", C.c_void_p),
+                ("depth", C.c_void_p), ("Tcw", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float),
+                ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("invfx", C.c_float), ("invfy", C.c_float),
+                ("mb", C.c_float), ("mbf", C.c_float), ("nlevels", C.c_int32), ("scale_factors", C.c_float * 16),
+                ("level_sigma2", C.c_float * 16)]
+
+
+def make_orbn_keyframe(k: dict):
+    keep = {"keys": np.ascontiguousarray(k["keys"], KP_DTYPE), "keys_un": np.ascontiguousarray(k["keys_un"], KP_DTYPE),
+            "u_right": np.ascontiguousarray(k["u_right"], np.float32), "depth": np.ascontiguousarray(k["depth"], np.float32)}
+    K = OrbnKeyFrame()
+    K.n = len(keep["keys_un"])
+    for f in ("keys", "keys_un", "u_right", "depth"):
+        setattr(K, f, keep[f].ctypes.data)
+    K.Tcw[:] = [float(x) for x in np.asarray(k["Tcw"], np.float32).reshape(-1)]
+    K.Ow[:] = [float(x) for x in np.asarray(k["Ow"], np.float32).reshape(-1)]
+    for f in ("fx", "fy", "cx", "cy", "invfx", "invfy", "mb", "mbf"):
+        setattr(K, f, float(k[f]))
+    K.nlevels = int(k["nlevels"])
+    for f in ("scale_factors", "level_sigma2"):
+        a = np.zeros(16, np.float32)
+        a[: K.nlevels] = k[f]
+        getattr(K, f)[:] = [float(x) for x in a]
+    return K, keep
+
+
+def triangulate(prob: dict):
+    """LocalMapping::CreateNewMapPoints' per-match body: (nnew, x3d[n][3], ok[n])."""
+    L = lib()
+    L.orc_triangulate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float, C.c_void_p, C.c_void_p]
+    A, k1 = make_orbn_keyframe(prob["kf1"])
+    B, k2 = make_orbn_keyframe(prob["kf2"])
+    pairs = np.ascontiguousarray(prob["pairs"], np.int32)
+    n = len(pairs)
+    x3d = np.zeros((max(n, 1), 3), np.float32)
+    ok = np.zeros(max(n, 1), np.uint8)
+    nnew = L.orc_triangulate(C.byref(A), C.byref(B), pairs.ctypes.data, n, float(prob["ratio_factor"]),
+                             x3d.ctypes.data, ok.ctypes.data)
+    return nnew, x3d[:n], ok[:n]
+
+
+def svd4_vt(A: np.ndarray):
+    """cv::SVD::compute(A 4x4 CV_32F, MODIFY_A | FULL_UV) -> (vt, w) as restated."""
+    L = lib()
+    L.orc_svd4_vt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    a = np.ascontiguousarray(A, np.float32).reshape(16)
+    vt = np.zeros(16, np.float32)
+    w = np.zeros(4, np.float32)
+    L.orc_svd4_vt(a.ctypes.data, vt.ctypes.data, w.ctypes.data)
+    return vt.reshape(4, 4), w

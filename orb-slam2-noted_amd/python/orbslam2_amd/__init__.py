@@ -113,6 +113,13 @@ SIGNATURES = [
     ("orbb_run_bow_batch", _I, [_P, _I, _F, _I, _P]),
     ("orbb_run_tri_batch", _I, [_P, _I, _I, _I, _P]),
     ("orbb_fetch", _I, [_P, _I, _I, _P, _P]),
+    ("orbn_create", _I, [C.POINTER(C.c_void_p)]),
+    ("orbn_destroy", None, [_P]),
+    ("orbn_triangulate", _I, [_P, _P, _P, _P, _I, _F, _P, _P, _P]),
+    ("orbn_reserve", _I, [_P, _I, _I, _I]),
+    ("orbn_stage", _I, [_P, _I, _P, _P, _P, _I, _F]),
+    ("orbn_run_batch", _I, [_P, _I, _P]),
+    ("orbn_fetch", _I, [_P, _I, _P, _P, _P]),
 ]
 
 
@@ -865,3 +872,88 @@ class BowMatcher:
         if tri:
             return out[: 2 * n.value].reshape(-1, 2).copy()
         return n.value, out[:n_out].copy()
+
+
+# ---- new map points (orbn_*): the triangulation loop of LocalMapping::CreateNewMapPoints ----
+class OrbnKeyFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("keys", C.c_void_p), ("keys_un", C.c_void_p), ("u_right", C.c_void_p),
+                ("depth", C.c_void_p), ("Tcw", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float),
+                ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("invfx", C.c_float), ("invfy", C.c_float),
+                ("mb", C.c_float), ("mbf", C.c_float), ("nlevels", C.c_int32), ("scale_factors", C.c_float * 16),
+                ("level_sigma2", C.c_float * 16)]
+
+
+def orbn_keyframe(k: dict):
+    """ctypes KeyFrame view of a synth.newpoints_problem keyframe dict (+ the arrays it points into)."""
+    keep = {"keys": np.ascontiguousarray(k["keys"]).view(KP_DTYPE),
+            "keys_un": np.ascontiguousarray(k["keys_un"]).view(KP_DTYPE),
+            "u_right": np.ascontiguousarray(k["u_right"], np.float32),
+            "depth": np.ascontiguousarray(k["depth"], np.float32)}
+    K = OrbnKeyFrame()
+    K.n = len(keep["keys_un"])
+    for f in ("keys", "keys_un", "u_right", "depth"):
+        setattr(K, f, keep[f].ctypes.data)
+    K.Tcw[:] = [float(x) for x in np.asarray(k["Tcw"], np.float32).reshape(-1)]
+    K.Ow[:] = [float(x) for x in np.asarray(k["Ow"], np.float32).reshape(-1)]
+    for f in ("fx", "fy", "cx", "cy", "invfx", "invfy", "mb", "mbf"):
+        setattr(K, f, float(k[f]))
+    K.nlevels = int(k["nlevels"])
+    for f in ("scale_factors", "level_sigma2"):
+        a = np.zeros(16, np.float32)
+        a[: K.nlevels] = k[f]
+        getattr(K, f)[:] = [float(x) for x in a]
+    return K, keep
+
+
+class NewMapPoints:
+    """LocalMapping::CreateNewMapPoints' per-match triangulation on the GPU. Problems are dicts
+    shaped like synth.newpoints_problem: {"kf1", "kf2", "pairs", "ratio_factor"}."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        _check(lib().orbn_create(C.byref(h)), "orbn_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbn_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def triangulate(self, prob: dict):
+        A, k1 = orbn_keyframe(prob["kf1"])
+        B, k2 = orbn_keyframe(prob["kf2"])
+        pairs = np.ascontiguousarray(prob["pairs"], np.int32)
+        n = len(pairs)
+        x3d = np.zeros((max(n, 1), 3), np.float32)
+        ok = np.zeros(max(n, 1), np.uint8)
+        nnew = C.c_int32()
+        _check(lib().orbn_triangulate(self._h, C.byref(A), C.byref(B), pairs.ctypes.data, n,
+                                      float(prob["ratio_factor"]), x3d.ctypes.data, ok.ctypes.data, C.byref(nnew)),
+               "orbn_triangulate")
+        return nnew.value, x3d[:n], ok[:n]
+
+    def reserve(self, n_slots: int, cap_kp: int, cap_pairs: int):
+        _check(lib().orbn_reserve(self._h, n_slots, cap_kp, cap_pairs), "orbn_reserve")
+
+    def stage(self, slot: int, prob: dict):
+        A, k1 = orbn_keyframe(prob["kf1"])
+        B, k2 = orbn_keyframe(prob["kf2"])
+        pairs = np.ascontiguousarray(prob["pairs"], np.int32)
+        _check(lib().orbn_stage(self._h, slot, C.byref(A), C.byref(B), pairs.ctypes.data, len(pairs),
+                                float(prob["ratio_factor"])), "orbn_stage")
+
+    def run_batch(self, n_slots: int, stream=None):
+        _check(lib().orbn_run_batch(self._h, n_slots, stream), "orbn_run_batch")
+
+    def fetch(self, slot: int, n_pairs: int):
+        x3d = np.zeros((max(n_pairs, 1), 3), np.float32)
+        ok = np.zeros(max(n_pairs, 1), np.uint8)
+        nnew = C.c_int32()
+        _check(lib().orbn_fetch(self._h, slot, x3d.ctypes.data, ok.ctypes.data, C.byref(nnew)), "orbn_fetch")
+        return nnew.value, x3d[:n_pairs], ok[:n_pairs]

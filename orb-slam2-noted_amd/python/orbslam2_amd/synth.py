@@ -584,3 +584,98 @@ def reloc_problem(seed: int = 40, found_frac: float = 0.2, blocked_frac: float =
     n = len(p["frame"]["keys_un"])
     p["kp_blocked"] = (rng.random(n) < blocked_frac).astype(np.uint8)
     return p
+
+
+# ---------------------------------------------------------------------------------------
+# New map points (LocalMapping::CreateNewMapPoints): the current
+# keyframe and one neighbour observing a shared cloud, keypoints = projections with pixel noise
+# 0.5 x scale[octave], stereo / RGB-D depth on a fraction of them, plus the matched pairs in
+# SearchForTriangulation's idx1 order with ~wrong_frac wrong partners (rejected by the
+# reprojection gates). cam = "kitti" (rectified stereo: mvKeys == mvKeysUn) or "tum" (RGB-D,
+# measured depth, mvKeys = distorted positions != mvKeysUn).
+# ---------------------------------------------------------------------------------------
+TUM1_CAM = (517.306408, 516.469215, 318.643040, 255.313989, 40.0)   # RGB-D/TUM1.yaml
+
+
+def newpoints_problem(seed: int = 21, n: int = 1500, n_points: int = 1400, stereo_frac: float = 0.6,
+                      baseline: float = 0.8, wrong_frac: float = 0.08, cam: str = "kitti", zmax: float = 60.0):
+    rng = np.random.default_rng(seed)
+    if cam == "kitti":
+        fx, fy, cx, cy, bf = (np.float32(v) for v in KITTI_CAM)
+        W, H = 1241, 376
+    else:
+        fx, fy, cx, cy, bf = (np.float32(v) for v in TUM1_CAM)
+        W, H = 640, 480
+    mb = np.float32(bf / fx)
+    sf = np.float32(1.2) ** np.arange(8, dtype=np.float32)
+    s2 = (sf * sf).astype(np.float32)
+    feat = np.array([434, 362, 302, 251, 209, 175, 145, 122], np.float64)
+    oct_p = feat / feat.sum()
+    R1 = _small_rot(rng, 2.0)
+    t1 = rng.normal(0, 0.5, 3)
+    C1 = -R1.T @ t1
+    C2 = C1 + R1.T @ np.array([rng.normal(0, 0.3), rng.normal(0, 0.05), baseline])
+    R2 = R1 @ _small_rot(rng, 3.0)
+    t2 = -R2 @ C2
+    z = np.where(rng.random(n_points) < 0.8, rng.uniform(2, 25, n_points), rng.uniform(25, zmax, n_points))
+    u = rng.uniform(0, W, n_points)
+    v = rng.uniform(0, H, n_points)
+    Pw = (np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1) - t1) @ R1
+
+    def keyframe(R, t):
+        Pc = Pw @ R.T + t
+        rows, owner = [], []
+        for p in range(n_points):
+            if Pc[p, 2] <= 0.5:
+                continue
+            o = int(rng.choice(8, p=oct_p))
+            s = float(sf[o])
+            x = fx * Pc[p, 0] / Pc[p, 2] + cx + rng.normal(0, 0.5 * s)
+            y = fy * Pc[p, 1] / Pc[p, 2] + cy + rng.normal(0, 0.5 * s)
+            if not (0 <= x < W and 0 <= y < H):
+                continue
+            if rng.random() < stereo_frac:
+                d = Pc[p, 2] * (1 + rng.normal(0, 0.01))
+                ur = x - bf / d
+            else:
+                d, ur = -1.0, -1.0
+            rows.append((x, y, o, ur, d))
+            owner.append(p)
+        while len(rows) < n:
+            o = int(rng.choice(8, p=oct_p))
+            rows.append((rng.uniform(0, W), rng.uniform(0, H), o, -1.0, -1.0))
+            owner.append(-1)
+        perm = rng.permutation(len(rows))[:n]
+        keys_un = np.zeros(n, TRACK_KP_DTYPE)
+        for i, j in enumerate(perm):
+            x, y, o, ur, d = rows[j]
+            keys_un[i] = (x, y, 31 * float(sf[o]), rng.uniform(0, 360), 0, o, -1)
+        keys = keys_un.copy()
+        if cam != "kitti":   # mvKeys: the distorted positions (UnprojectStereo reads them)
+            keys["x"] += rng.normal(0, 1.5, n).astype(np.float32)
+            keys["y"] += rng.normal(0, 1.5, n).astype(np.float32)
+        ur = np.array([rows[j][3] for j in perm], np.float32)
+        dep = np.array([rows[j][4] for j in perm], np.float32)
+        if cam != "kitti":   # RGB-D: uR = xUn - mbf / d (Frame::ComputeStereoFromRGBD)
+            ok = dep > 0
+            ur = np.where(ok, keys_un["x"] - bf / np.where(ok, dep, 1), -1).astype(np.float32)
+        else:                # stereo: depth = mbf / disparity
+            ok = ur >= 0
+            disp = keys_un["x"] - ur
+            dep = np.where(ok, bf / np.where(ok, disp, 1), -1).astype(np.float32)
+        T, Ow = _pose_dict(R, t)
+        kf = {"keys": keys, "keys_un": keys_un, "u_right": ur, "depth": dep, "Tcw": T.reshape(-1), "Ow": Ow,
+              "fx": fx, "fy": fy, "cx": cx, "cy": cy, "invfx": np.float32(1) / fx, "invfy": np.float32(1) / fy,
+              "mb": mb, "mbf": bf, "nlevels": 8, "scale_factors": sf, "level_sigma2": s2}
+        return kf, np.array([owner[j] for j in perm], np.int64)
+
+    k1, own1 = keyframe(R1, t1)
+    k2, own2 = keyframe(R2, t2)
+    where2 = {int(p): i for i, p in enumerate(own2) if p >= 0}
+    pairs = []
+    for i1 in range(n):
+        p = int(own1[i1])
+        if p >= 0 and p in where2:
+            pairs.append((i1, where2[p] if rng.random() >= wrong_frac else int(rng.integers(0, n))))
+    return {"kf1": k1, "kf2": k2, "pairs": np.array(pairs, np.int32).reshape(-1, 2),
+            "ratio_factor": np.float32(1.5) * np.float32(1.2)}
