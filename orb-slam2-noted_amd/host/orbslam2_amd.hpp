@@ -247,4 +247,29 @@ private:
     };
 };
 
+// LocalMapping::CreateNewMapPoints (LocalMapping.cc:295-600): per neighbour, the caller keeps
+// the baseline test, ComputeF12 and ORBmatcher::SearchForTriangulation (orbb_*), then
+// TriangulateMatches runs the per-match body on the GPU; ok[k] = 1 -> create the MapPoint at
+// x3D[3k..3k+2] with observations (idx1 in mpCurrentKeyFrame, idx2 in pKF2) as the reference does.
+class LocalMapping {
+public:
+    static int TriangulateMatches(const orbn_keyframe &kf1, const orbn_keyframe &kf2,
+                                  const std::vector<int32_t> &vMatchedIndices, float ratioFactor,
+                                  std::vector<float> &x3D, std::vector<uint8_t> &ok) {
+        struct H {
+            orbn_engine *h = nullptr;
+            H() { check(orbn_create(&h), "orbn_create"); }
+            ~H() { orbn_destroy(h); }
+        };
+        static thread_local H eng;
+        const int32_t n = (int32_t)(vMatchedIndices.size() / 2);
+        x3D.assign((size_t)n * 3, 0.0f);
+        ok.assign(n, 0);
+        int32_t nnew = 0;
+        check(orbn_triangulate(eng.h, &kf1, &kf2, vMatchedIndices.data(), n, ratioFactor, x3D.data(), ok.data(), &nnew),
+              "orbn_triangulate");
+        return nnew;
+    }
+};
+
 }  // namespace orbslam2_amd

@@ -6,6 +6,7 @@
 //   host_api_test lba <problem.bin> <out.bin>
 //   host_api_test pose <edges.bin> <out.bin>
 //   host_api_test bow <vocab.txt> <desc.u8> <n> <levelsup> <out.bin>
+//   host_api_test newpts <problem.bin> <out.bin>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -30,6 +31,50 @@ template <class T> static void put(std::ofstream &o, const std::vector<T> &v) {
 
 int main(int argc, char **argv) {
     try {
+        if (argc >= 4 && !strcmp(argv[1], "newpts")) {
+            // problem.bin: int32 n1, n2, npairs; float ratio; per keyframe: keys[n], keys_un[n]
+            // (28 B), u_right[n], depth[n], 23 floats (Tcw, Ow, fx fy cx cy invfx invfy mb mbf),
+            // int32 nlevels, float sf[16], s2[16]; then int32 pairs[npairs][2]
+            auto buf = read_file(argv[2]);
+            const uint8_t *q = buf.data();
+            auto take = [&q](void *dst, size_t bytes) { std::memcpy(dst, q, bytes); q += bytes; };
+            int32_t nk[2], np;
+            float ratio;
+            take(&nk[0], 4); take(&nk[1], 4); take(&np, 4); take(&ratio, 4);
+            std::vector<orbx_kp> keys[2], keysUn[2];
+            std::vector<float> ur[2], dep[2];
+            orbn_keyframe kf[2];
+            for (int i = 0; i < 2; i++) {
+                const size_t n = (size_t)nk[i];
+                keys[i].resize(n); keysUn[i].resize(n); ur[i].resize(n); dep[i].resize(n);
+                take(keys[i].data(), sizeof(orbx_kp) * n);
+                take(keysUn[i].data(), sizeof(orbx_kp) * n);
+                take(ur[i].data(), 4 * n);
+                take(dep[i].data(), 4 * n);
+                orbn_keyframe &k = kf[i];
+                k = orbn_keyframe{};
+                k.n = nk[i];
+                k.keys = keys[i].data(); k.keys_un = keysUn[i].data(); k.u_right = ur[i].data(); k.depth = dep[i].data();
+                float h[23];
+                take(h, sizeof h);
+                std::memcpy(k.Tcw, h, 48); std::memcpy(k.Ow, h + 12, 12);
+                k.fx = h[15]; k.fy = h[16]; k.cx = h[17]; k.cy = h[18]; k.invfx = h[19]; k.invfy = h[20];
+                k.mb = h[21]; k.mbf = h[22];
+                take(&k.nlevels, 4);
+                take(k.scale_factors, 64);
+                take(k.level_sigma2, 64);
+            }
+            std::vector<int32_t> pairs((size_t)np * 2);
+            take(pairs.data(), 8 * (size_t)np);
+            std::vector<float> x3d;
+            std::vector<uint8_t> ok;
+            const int nnew = LocalMapping::TriangulateMatches(kf[0], kf[1], pairs, ratio, x3d, ok);
+            std::ofstream o(argv[3], std::ios::binary);
+            put(o, std::vector<int32_t>{nnew});
+            put(o, x3d);
+            put(o, ok);
+            return 0;
+        }
         if (argc >= 7 && !strcmp(argv[1], "extract")) {
             auto img = read_file(argv[2]);
             const int w = atoi(argv[3]), h = atoi(argv[4]), nf = atoi(argv[5]);

@@ -106,3 +106,28 @@ def test_cpp_bow_text_vocabulary(tmp_path, oracle_mod):
     assert words.tobytes() == ref["words"].tobytes() and vals.tobytes() == ref["values"].tobytes()
     assert nodes.tobytes() == ref["fv_nodes"].tobytes() and start.tobytes() == ref["fv_start"].tobytes()
     assert feats.tobytes() == ref["fv_features"].tobytes()
+
+
+def test_host_local_mapping_triangulate(oracle_mod, tmp_path):
+    """LocalMapping::TriangulateMatches (host C++ over orbn_triangulate) vs the oracle."""
+    prob = synth.newpoints_problem(seed=41)
+    blob = [np.array([len(prob["kf1"]["keys"]), len(prob["kf2"]["keys"]), len(prob["pairs"])], np.int32).tobytes(),
+            np.float32(prob["ratio_factor"]).tobytes()]
+    for k in (prob["kf1"], prob["kf2"]):
+        blob += [np.ascontiguousarray(k["keys"]).view(KP).tobytes(), np.ascontiguousarray(k["keys_un"]).view(KP).tobytes(),
+                 np.asarray(k["u_right"], np.float32).tobytes(), np.asarray(k["depth"], np.float32).tobytes()]
+        hdr = np.concatenate([np.asarray(k["Tcw"], np.float32).reshape(-1), np.asarray(k["Ow"], np.float32),
+                              np.array([k[f] for f in ("fx", "fy", "cx", "cy", "invfx", "invfy", "mb", "mbf")], np.float32)])
+        blob += [hdr.astype(np.float32).tobytes(), np.int32(k["nlevels"]).tobytes()]
+        for f in ("scale_factors", "level_sigma2"):
+            a = np.zeros(16, np.float32)
+            a[: k["nlevels"]] = k[f]
+            blob.append(a.tobytes())
+    blob.append(np.ascontiguousarray(prob["pairs"], np.int32).tobytes())
+    (tmp_path / "p.bin").write_bytes(b"".join(blob))
+    subprocess.run([str(EXE), "newpts", str(tmp_path / "p.bin"), str(tmp_path / "o.bin")], check=True, timeout=120)
+    nnew, x3d, ok = _read(tmp_path / "o.bin", [np.int32, np.float32, np.uint8])
+    rn, rx, rok = oracle_mod.triangulate(prob)
+    assert int(nnew[0]) == rn
+    np.testing.assert_array_equal(ok, rok)
+    assert x3d.tobytes() == rx.reshape(-1).tobytes()
