@@ -446,7 +446,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="stereo frames per step")
+    ap.add_argument("--batch", type=int, default=256, help="stereo frames per step (B=64: 39.2k, 128: 42.7k, 256: 45.0k stereo fps)")
     ap.add_argument("--pool", type=int, default=8, help="distinct synthetic stereo pairs")
     ap.add_argument("--bufs", type=int, default=4, help="rotating resident input batches")
     ap.add_argument("--cpu-frames", type=int, default=96)
