@@ -327,15 +327,23 @@ int orbb_search_by_bow(orbb_engine *e, const orbb_keyframe *kf, const orbb_keyfr
 int orbb_search_for_triangulation(orbb_engine *e, const orbb_keyframe *kf1, const orbb_keyframe *kf2,
                                   const float F12[9], const float Cw1[3], const float T2w[12], int only_stereo,
                                   int check_ori, int32_t *pairs, int32_t *npairs);
+/* ORBmatcher(nnratio, check_ori).SearchByBoW(pKF1, pKF2, vpMatches12) (ORBmatcher.h:151,
+ * ORBmatcher.cc:760-903; LoopClosing::ComputeSim3 with ORBmatcher(0.75, true)). matches12[kf1->n]
+ * out: the kf2 map-point index (kf2->mp) matched to keypoint idx1 of kf1, -1 = NULL. Both
+ * sides need a map point that is not bad (mp_bad); KF2 keypoints are claimed (vbMatched2). */
+int orbb_search_by_bow_kf(orbb_engine *e, const orbb_keyframe *kf1, const orbb_keyframe *kf2, float nnratio,
+                          int check_ori, int32_t *matches12, int32_t *nmatches);
+
 /* Batched device-resident form: stage (a, b) pairs into slots -- SearchByBoW reads a = KeyFrame,
- * b = Frame; SearchForTriangulation a = KF1, b = KF2 (F12 / Cw1 / T2w may be NULL for
- * SearchByBoW) -- run one launch chain over all slots, fetch per slot (tri = 0: matches[b.n],
- * tri = 1: pairs[2 * n]). */
+ * b = Frame (or KeyFrame 2); SearchForTriangulation a = KF1, b = KF2 (F12 / Cw1 / T2w may be NULL
+ * for SearchByBoW) -- run one launch chain over all slots, fetch per slot (tri = 0:
+ * matches[b.n], tri = 1: pairs[2 * n], tri = 2: matches12[a.n] of orbb_run_bowkf_batch). */
 int orbb_reserve(orbb_engine *e, int n_slots, int cap_kp);
 int orbb_stage(orbb_engine *e, int slot, const orbb_keyframe *a, const orbb_keyframe *b, const float F12[9],
                const float Cw1[3], const float T2w[12]);
 int orbb_run_bow_batch(orbb_engine *e, int n_slots, float nnratio, int check_ori, void *stream);
 int orbb_run_tri_batch(orbb_engine *e, int n_slots, int only_stereo, int check_ori, void *stream);
+int orbb_run_bowkf_batch(orbb_engine *e, int n_slots, float nnratio, int check_ori, void *stream);
 int orbb_fetch(orbb_engine *e, int slot, int tri, int32_t *out, int32_t *n);
 
 /* -------- pose-only optimisation (replaces Optimizer::PoseOptimization) -------- */

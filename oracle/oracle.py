@@ -577,6 +577,17 @@ def search_by_bow(prob: dict, nnratio=0.7, check_ori=True):
     return nm, out[: B.n]
 
 
+def search_by_bow_kf(prob: dict, nnratio=0.75, check_ori=True):
+    """SearchByBoW(KeyFrame* pKF1 = A, KeyFrame* pKF2 = B): (nmatches, matches12[A.n])."""
+    L = lib()
+    L.orc_search_by_bow_kf.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_int, C.c_void_p]
+    A, k1 = make_orbb_keyframe(prob["A"])
+    B, k2 = make_orbb_keyframe(prob["B"])
+    out = np.zeros(max(A.n, 1), np.int32)
+    nm = L.orc_search_by_bow_kf(C.byref(A), C.byref(B), nnratio, 1 if check_ori else 0, out.ctypes.data)
+    return nm, out[: A.n]
+
+
 def search_for_triangulation(prob: dict, only_stereo=False, check_ori=True):
     L = lib()
     L.orc_search_for_triangulation.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,

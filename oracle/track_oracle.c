@@ -451,6 +451,66 @@ int orc_search_by_bow(const orbb_keyframe *kf, const orbb_keyframe *F, float nnr
     return nmatches;
 }
 
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+ * (src/ORBmatcher.cc:760-903; LoopClosing::ComputeSim3 with ORBmatcher(0.75, true)):
+ * matches12[idx1] = map point index of pKF2 matched to keypoint idx1 of pKF1, -1 = NULL.
+ * Differences to the (KF, F) overload: both sides need a non-bad map point, vbMatched2
+ * marks claimed KF2 keypoints, the distance gate is strict (bestDist1 < TH_LOW, :845) and the
+ * rotation histogram holds idx1. */
+int orc_search_by_bow_kf(const orbb_keyframe *k1, const orbb_keyframe *k2, float nnratio, int checkOri,
+                         int32_t *matches12) {
+    const int TH_LOW = 50, HISTO_LENGTH = 30;
+    const float factor = HISTO_LENGTH / 360.0f;
+    for (int i = 0; i < k1->n; i++) matches12[i] = -1;
+    uint8_t *matched2 = (uint8_t *)calloc((size_t)k2->n + 1, 1);
+    int *hb = (int *)malloc(sizeof(int) * ((size_t)k1->n + 1)), *hi = (int *)malloc(sizeof(int) * ((size_t)k1->n + 1));
+    int nh = 0, nmatches = 0;
+    for (int a = 0; a < k1->n_fv; a++) {
+        const int b = fv_find(k2, k1->fv_nodes[a]);
+        if (b < 0) continue;
+        for (int u = k1->fv_start[a]; u < k1->fv_start[a + 1]; u++) {
+            const int idx1 = k1->fv_features[u];
+            if (k1->mp[idx1] < 0) continue;                                     /* :802-806 */
+            if (k1->mp_bad && k1->mp_bad[idx1]) continue;
+            const uint8_t *d1 = k1->desc + 32 * (size_t)idx1;
+            int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+            for (int w = k2->fv_start[b]; w < k2->fv_start[b + 1]; w++) {
+                const int idx2 = k2->fv_features[w];
+                if (matched2[idx2] || k2->mp[idx2] < 0) continue;                /* :822-826 */
+                if (k2->mp_bad && k2->mp_bad[idx2]) continue;
+                const int dist = orc_descriptor_distance(d1, k2->desc + 32 * (size_t)idx2);
+                if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdx2 = idx2; }
+                else if (dist < bestDist2) bestDist2 = dist;
+            }
+            if (bestDist1 < TH_LOW && (float)bestDist1 < nnratio * (float)bestDist2) {   /* :845-864 */
+                matches12[idx1] = k2->mp[bestIdx2];
+                matched2[bestIdx2] = 1;
+                if (checkOri) {
+                    float rot = k1->keys_un[idx1].angle - k2->keys_un[bestIdx2].angle;
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == HISTO_LENGTH) bin = 0;
+                    hb[nh] = bin; hi[nh] = idx1; nh++;
+                }
+                nmatches++;
+            }
+        }
+    }
+    if (checkOri) {                                                              /* :882-900 */
+        int counts[30] = {0};
+        for (int k = 0; k < nh; k++) counts[hb[k]]++;
+        int i1 = -1, i2 = -1, i3 = -1;
+        three_maxima_n(counts, &i1, &i2, &i3);
+        for (int k = 0; k < nh; k++) {
+            if (hb[k] == i1 || hb[k] == i2 || hb[k] == i3) continue;
+            matches12[hi[k]] = -1;
+            nmatches--;
+        }
+    }
+    free(matched2); free(hb); free(hi);
+    return nmatches;
+}
+
 static int check_dist_epipolar(const orc_kp *kp1, const orc_kp *kp2, const float F12[9], const orbb_keyframe *kf2) {
     const float a = kp1->x * F12[0] + kp1->y * F12[3] + F12[6];
     const float b = kp1->x * F12[1] + kp1->y * F12[4] + F12[7];

@@ -1,6 +1,7 @@
 // MI355X-native BoW-guided matchers:
 //   ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)   ORBmatcher.cc:236-353
 //   ORBmatcher::SearchForTriangulation(KF1, KF2, F12, pairs, bOnlyStereo)  ORBmatcher.cc:915-1089
+//   ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)  ORBmatcher.cc:760-903
 //
 // Both walk the FeatureVector nodes the two frames share; a keypoint belongs to exactly one
 // node, so the greedy claims (vpMapPointMatches / vbMatched2) never cross nodes and every
@@ -50,7 +51,7 @@ struct Slots {
     const float *uA, *uB;
     const uint8_t *dA, *dB;     // [S][cap][32]
     const int *mpA, *mpB;
-    const uint8_t *badA;
+    const uint8_t *badA, *badB;
     const int *fA, *fB;         // FeatureVector features in node order [S][cap]
     const int4 *nodes;          // [S][cap] shared node ranges (a0, a1, b0, b1)
     int cap;
@@ -120,16 +121,19 @@ __device__ inline void mat_rx_t(const float *T, const float *X, float o[3]) {
 __global__ __launch_bounds__(256) void bm_init_kernel(Slots S, int tri, Work W) {
     const int s = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
     const PairHdr &h = S.hdr[s];
-    const int n = tri ? h.nA : h.nB;
+    const int n = tri ? h.nA : h.nB;   // tri != 0: output indexed by A's keypoints
     if (i < n) W.out[(long long)s * S.cap + i] = -1;
     if (i < HISTO_LENGTH) W.counts[s * HISTO_LENGTH + i] = 0;
     if (i == 0) { W.hist_n[s] = 0; W.nmatch[s] = 0; }
 }
 
-// one wavefront per (slot, shared node); blockIdx.x = node
-template <bool kTri>
+// one wavefront per (slot, shared node); blockIdx.x = node.
+// kMode 0 = SearchByBoW(KF, F), 1 = SearchForTriangulation, 2 = SearchByBoW(KF1, KF2)
+enum { BM_BOW = 0, BM_TRI = 1, BM_BOWKF = 2 };
+template <int kMode>
 __global__ __launch_bounds__(64) void bm_node_kernel(Slots S, float nnratio, int only_stereo, int check_ori, Work W) {
-    extern __shared__ uint8_t claimed[];   // B positions of this node
+    extern __shared__ uint8_t claimed[];   // B positions of this node (vbMatched2 / vpMapPointMatches)
+    constexpr bool kTri = kMode == BM_TRI;
     const int s = blockIdx.y, node = blockIdx.x, lane = threadIdx.x;
     const PairHdr &h = S.hdr[s];
     if (node >= h.n_nodes) return;
@@ -165,6 +169,7 @@ __global__ __launch_bounds__(64) void bm_node_kernel(Slots S, float nnratio, int
             const int ib = S.fB[kb + r.z + p];
             const long long gb = kb + ib;
             if (!kTri) {
+                if (kMode == BM_BOWKF && (S.mpB[gb] < 0 || S.badB[gb])) continue;   // :822-826
                 const unsigned long long key = ((unsigned long long)hamming32(da, S.dB + gb * 32) << 32) | (unsigned)p;
                 if (key < k1) { k2 = k1; k1 = key; } else if (key < k2) k2 = key;
             } else {
@@ -197,7 +202,8 @@ __global__ __launch_bounds__(64) void bm_node_kernel(Slots S, float nnratio, int
         if (!kTri) {
             wave_min2_u64(k1, k2);
             const int d1 = k1 == ~0ull ? 256 : (int)(k1 >> 32), d2 = k2 == ~0ull ? 256 : (int)(k2 >> 32);
-            if (d1 <= TH_LOW && (float)d1 < nnratio * (float)d2) win = (int)(unsigned)k1;
+            const bool gate = kMode == BM_BOWKF ? d1 < TH_LOW : d1 <= TH_LOW;   // :845 strict for (KF, KF)
+            if (gate && (float)d1 < nnratio * (float)d2) win = (int)(unsigned)k1;
         } else {
             k1 = wave_min_u64(k1);
             if (k1 != ~0ull) win = (int)(0xFFFFFFFFu - (unsigned)k1);
@@ -206,12 +212,13 @@ __global__ __launch_bounds__(64) void bm_node_kernel(Slots S, float nnratio, int
         const int ib = S.fB[kb + r.z + win];
         if (lane == 0) {
             claimed[win] = 1;
-            if (!kTri) W.out[kb + ib] = S.mpA[ga];                // vpMapPointMatches[bestIdxF] = pMP
-            else W.out[kb + ia] = ib;                             // vMatches12[idx1] = bestIdx2
+            if (kMode == BM_BOW) W.out[kb + ib] = S.mpA[ga];      // vpMapPointMatches[bestIdxF] = pMP
+            else if (kMode == BM_TRI) W.out[kb + ia] = ib;       // vMatches12[idx1] = bestIdx2
+            else W.out[kb + ia] = S.mpB[kb + ib];                 // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
             if (check_ori) {
                 const int bin = rot_bin(kp1.angle, S.kB[kb + ib].angle);
                 const int slot = atomicAdd(&W.hist_n[s], 1);
-                W.hist_idx[kb + slot] = kTri ? ia : ib;
+                W.hist_idx[kb + slot] = kMode == BM_BOW ? ib : ia;
                 W.hist_bin[kb + slot] = (int8_t)bin;
                 atomicAdd(&W.counts[s * HISTO_LENGTH + bin], 1);
             }
@@ -258,7 +265,7 @@ __global__ __launch_bounds__(256) void bm_finish_kernel(Slots S, int tri, int ch
     }
     __syncthreads();
     if (tid == 0) W.nmatch[s] -= s_removed;
-    if (!tri) return;
+    if (tri != 1) return;
     // vMatchedPairs in idx1 order: exclusive scan of (m12[i] >= 0)
     const int n = h.nA, per = (n + 255) / 256, lo = tid * per;
     int cnt = 0;
@@ -286,7 +293,7 @@ struct orbb_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     int nslots = 0, cap = 0;
-    DevBuf hdr, kA, kB, uA, uB, dA, dB, mpA, mpB, badA, fA, fB, nodes;
+    DevBuf hdr, kA, kB, uA, uB, dA, dB, mpA, mpB, badA, badB, fA, fB, nodes;
     DevBuf out, hidx, hbin, hn, counts, nmatch, pairs;
     std::vector<PairHdr> h;
 };
@@ -298,7 +305,7 @@ Slots make_slots(orbb_engine *e) {
     S.hdr = e->hdr.as<PairHdr>();
     S.kA = e->kA.as<orbx_kp>(); S.kB = e->kB.as<orbx_kp>(); S.uA = e->uA.as<float>(); S.uB = e->uB.as<float>();
     S.dA = e->dA.as<uint8_t>(); S.dB = e->dB.as<uint8_t>(); S.mpA = e->mpA.as<int>(); S.mpB = e->mpB.as<int>();
-    S.badA = e->badA.as<uint8_t>(); S.fA = e->fA.as<int>(); S.fB = e->fB.as<int>(); S.nodes = e->nodes.as<int4>();
+    S.badA = e->badA.as<uint8_t>(); S.badB = e->badB.as<uint8_t>(); S.fA = e->fA.as<int>(); S.fB = e->fB.as<int>(); S.nodes = e->nodes.as<int4>();
     S.cap = e->cap;
     return S;
 }
@@ -347,7 +354,7 @@ void orbb_destroy(orbb_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
-    DevBuf *bufs[] = {&e->hdr, &e->kA, &e->kB, &e->uA, &e->uB, &e->dA, &e->dB, &e->mpA, &e->mpB, &e->badA, &e->fA,
+    DevBuf *bufs[] = {&e->hdr, &e->kA, &e->kB, &e->uA, &e->uB, &e->dA, &e->dB, &e->mpA, &e->mpB, &e->badA, &e->badB, &e->fA,
                       &e->fB, &e->nodes, &e->out, &e->hidx, &e->hbin, &e->hn, &e->counts, &e->nmatch, &e->pairs};
     for (DevBuf *b : bufs) b->release();
     delete e;
@@ -359,7 +366,7 @@ int orbb_reserve(orbb_engine *e, int n_slots, int cap_kp) {
     const size_t S = (size_t)n_slots, C = (size_t)cap_kp;
     if (e->hdr.ensure(sizeof(PairHdr) * S) || e->kA.ensure(sizeof(orbx_kp) * S * C) || e->kB.ensure(sizeof(orbx_kp) * S * C) ||
         e->uA.ensure(4 * S * C) || e->uB.ensure(4 * S * C) || e->dA.ensure(32 * S * C) || e->dB.ensure(32 * S * C) ||
-        e->mpA.ensure(4 * S * C) || e->mpB.ensure(4 * S * C) || e->badA.ensure(S * C) || e->fA.ensure(4 * S * C) ||
+        e->mpA.ensure(4 * S * C) || e->mpB.ensure(4 * S * C) || e->badA.ensure(S * C) || e->badB.ensure(S * C) || e->fA.ensure(4 * S * C) ||
         e->fB.ensure(4 * S * C) || e->nodes.ensure(16 * S * C) || e->out.ensure(4 * S * C) || e->hidx.ensure(4 * S * C) ||
         e->hbin.ensure(S * C) || e->hn.ensure(4 * S) || e->counts.ensure(4 * S * HISTO_LENGTH) || e->nmatch.ensure(4 * S) ||
         e->pairs.ensure(8 * S * C))
@@ -413,12 +420,16 @@ int orbb_stage(orbb_engine *e, int slot, const orbb_keyframe *a, const orbb_keyf
         if (a->mp_bad) ok = up(e->badA, s * C, a->mp_bad, na);
         else ok = hipMemsetAsync((char *)e->badA.p + s * C, 0, na, st) == hipSuccess;
     }
+    if (ok) {
+        if (b->mp_bad) ok = up(e->badB, s * C, b->mp_bad, nbk);
+        else ok = hipMemsetAsync((char *)e->badB.p + s * C, 0, nbk, st) == hipSuccess;
+    }
     if (!ok) return ORBX_EDEVICE;
     BM_CHK(hipStreamSynchronize(st));
     return ORBX_OK;
 }
 
-static int run(orbb_engine *e, int n_slots, bool tri, float nnratio, int only_stereo, int check_ori, void *stream) {
+static int run(orbb_engine *e, int n_slots, int mode, float nnratio, int only_stereo, int check_ori, void *stream) {
     if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
     BM_CHK(hipSetDevice(e->device));
     hipStream_t st = stream ? (hipStream_t)stream : e->stream;
@@ -429,20 +440,26 @@ static int run(orbb_engine *e, int n_slots, bool tri, float nnratio, int only_st
     }
     const Slots S = make_slots(e);
     const Work W = make_work(e);
-    bm_init_kernel<<<dim3((std::max(maxn, HISTO_LENGTH) + 255) / 256, n_slots), 256, 0, st>>>(S, tri ? 1 : 0, W);
-    if (tri) bm_node_kernel<true><<<dim3(maxnodes, n_slots), 64, e->cap, st>>>(S, nnratio, only_stereo, check_ori, W);
-    else bm_node_kernel<false><<<dim3(maxnodes, n_slots), 64, e->cap, st>>>(S, nnratio, only_stereo, check_ori, W);
-    bm_finish_kernel<<<n_slots, 256, 0, st>>>(S, tri ? 1 : 0, check_ori, W);
+    bm_init_kernel<<<dim3((std::max(maxn, HISTO_LENGTH) + 255) / 256, n_slots), 256, 0, st>>>(S, mode, W);
+    const dim3 grid(maxnodes, n_slots);
+    if (mode == BM_TRI) bm_node_kernel<BM_TRI><<<grid, 64, e->cap, st>>>(S, nnratio, only_stereo, check_ori, W);
+    else if (mode == BM_BOWKF) bm_node_kernel<BM_BOWKF><<<grid, 64, e->cap, st>>>(S, nnratio, only_stereo, check_ori, W);
+    else bm_node_kernel<BM_BOW><<<grid, 64, e->cap, st>>>(S, nnratio, only_stereo, check_ori, W);
+    bm_finish_kernel<<<n_slots, 256, 0, st>>>(S, mode, check_ori, W);
     BM_CHK(hipGetLastError());
     return ORBX_OK;
 }
 
 int orbb_run_bow_batch(orbb_engine *e, int n_slots, float nnratio, int check_ori, void *stream) {
-    return run(e, n_slots, false, nnratio, 0, check_ori, stream);
+    return run(e, n_slots, BM_BOW, nnratio, 0, check_ori, stream);
 }
 
 int orbb_run_tri_batch(orbb_engine *e, int n_slots, int only_stereo, int check_ori, void *stream) {
-    return run(e, n_slots, true, 0.6f, only_stereo, check_ori, stream);
+    return run(e, n_slots, BM_TRI, 0.6f, only_stereo, check_ori, stream);
+}
+
+int orbb_run_bowkf_batch(orbb_engine *e, int n_slots, float nnratio, int check_ori, void *stream) {
+    return run(e, n_slots, BM_BOWKF, nnratio, 0, check_ori, stream);
 }
 
 int orbb_fetch(orbb_engine *e, int slot, int tri, int32_t *out, int32_t *n) {
@@ -451,8 +468,9 @@ int orbb_fetch(orbb_engine *e, int slot, int tri, int32_t *out, int32_t *n) {
     BM_CHK(hipDeviceSynchronize());
     const size_t C = (size_t)e->cap, s = (size_t)slot;
     BM_CHK(hipMemcpy(n, (char *)e->nmatch.p + 4 * s, 4, hipMemcpyDeviceToHost));
-    if (!tri) {
-        if (e->h[slot].nB) BM_CHK(hipMemcpy(out, (char *)e->out.p + 4 * s * C, 4 * (size_t)e->h[slot].nB, hipMemcpyDeviceToHost));
+    if (tri == 0 || tri == 2) {   // matches[b.n] (SearchByBoW(KF, F)) / matches12[a.n] (SearchByBoW(KF1, KF2))
+        const size_t m = (size_t)(tri == 0 ? e->h[slot].nB : e->h[slot].nA);
+        if (m) BM_CHK(hipMemcpy(out, (char *)e->out.p + 4 * s * C, 4 * m, hipMemcpyDeviceToHost));
     } else if (*n > 0) {
         BM_CHK(hipMemcpy(out, (char *)e->pairs.p + 8 * s * C, 8 * (size_t)*n, hipMemcpyDeviceToHost));
     }
@@ -470,6 +488,20 @@ int orbb_search_by_bow(orbb_engine *e, const orbb_keyframe *kf, const orbb_keyfr
     int rc = orbb_stage(e, 0, kf, f, nullptr, nullptr, nullptr);
     if (!rc) rc = orbb_run_bow_batch(e, 1, nnratio, check_ori, nullptr);
     if (!rc) rc = orbb_fetch(e, 0, 0, matches, nmatches);
+    return rc;
+}
+
+int orbb_search_by_bow_kf(orbb_engine *e, const orbb_keyframe *kf1, const orbb_keyframe *kf2, float nnratio, int check_ori,
+                          int32_t *matches12, int32_t *nmatches) {
+    if (!e || !kf1 || !kf2 || !matches12 || !nmatches) return ORBX_EINVAL;
+    const int need = std::max(1, std::max(kf1->n, kf2->n));
+    if (e->nslots < 1 || e->cap < need) {
+        const int rc = orbb_reserve(e, std::max(1, e->nslots), std::max(e->cap, need));
+        if (rc) return rc;
+    }
+    int rc = orbb_stage(e, 0, kf1, kf2, nullptr, nullptr, nullptr);
+    if (!rc) rc = orbb_run_bowkf_batch(e, 1, nnratio, check_ori, nullptr);
+    if (!rc) rc = orbb_fetch(e, 0, 2, matches12, nmatches);
     return rc;
 }
 

@@ -113,6 +113,8 @@ SIGNATURES = [
     ("orbb_run_bow_batch", _I, [_P, _I, _F, _I, _P]),
     ("orbb_run_tri_batch", _I, [_P, _I, _I, _I, _P]),
     ("orbb_fetch", _I, [_P, _I, _I, _P, _P]),
+    ("orbb_search_by_bow_kf", _I, [_P, _P, _P, _F, _I, _P, _P]),
+    ("orbb_run_bowkf_batch", _I, [_P, _I, _F, _I, _P]),
     ("orbn_create", _I, [C.POINTER(C.c_void_p)]),
     ("orbn_destroy", None, [_P]),
     ("orbn_triangulate", _I, [_P, _P, _P, _P, _I, _F, _P, _P, _P]),
@@ -836,6 +838,20 @@ class BowMatcher:
                                         out.ctypes.data, C.byref(nm)), "orbb_search_by_bow")
         return nm.value, out[: B.n]
 
+    def search_by_bow_kf(self, prob: dict, nnratio=0.75, check_ori=True):
+        """SearchByBoW(KeyFrame* pKF1 = A, KeyFrame* pKF2 = B) -> (nmatches, matches12[A.n])."""
+        A, k1 = _orbb_keyframe(prob["A"])
+        B, k2 = _orbb_keyframe(prob["B"])
+        out = np.zeros(max(A.n, 1), np.int32)
+        nm = C.c_int32()
+        _check(lib().orbb_search_by_bow_kf(self._h, C.byref(A), C.byref(B), nnratio, 1 if check_ori else 0,
+                                           out.ctypes.data, C.byref(nm)), "orbb_search_by_bow_kf")
+        return nm.value, out[: A.n]
+
+    def run_bowkf_batch(self, n_slots: int, nnratio=0.75, check_ori=True, stream=None):
+        _check(lib().orbb_run_bowkf_batch(self._h, n_slots, nnratio, 1 if check_ori else 0, stream),
+               "orbb_run_bowkf_batch")
+
     def search_for_triangulation(self, prob: dict, only_stereo=False, check_ori=True):
         A, k1 = _orbb_keyframe(prob["A"])
         B, k2 = _orbb_keyframe(prob["B"])
@@ -865,11 +881,14 @@ class BowMatcher:
         _check(lib().orbb_run_tri_batch(self._h, n_slots, 1 if only_stereo else 0, 1 if check_ori else 0, stream),
                "orbb_run_tri_batch")
 
-    def fetch(self, slot: int, tri: bool, n_out: int):
+    def fetch(self, slot: int, tri, n_out: int):
+        """tri: False / 0 = SearchByBoW(KF, F) matches, True / 1 = triangulation pairs,
+        2 = SearchByBoW(KF1, KF2) matches12."""
+        mode = int(tri)
         out = np.zeros(max(2 * n_out, 1), np.int32)
         n = C.c_int32()
-        _check(lib().orbb_fetch(self._h, slot, 1 if tri else 0, out.ctypes.data, C.byref(n)), "orbb_fetch")
-        if tri:
+        _check(lib().orbb_fetch(self._h, slot, mode, out.ctypes.data, C.byref(n)), "orbb_fetch")
+        if mode == 1:
             return out[: 2 * n.value].reshape(-1, 2).copy()
         return n.value, out[:n_out].copy()
 

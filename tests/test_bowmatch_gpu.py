@@ -61,3 +61,28 @@ def test_no_shared_nodes(bm, oracle_mod):
     q = dict(p, B=B)
     assert bm.search_by_bow(q)[0] == oracle_mod.search_by_bow(q)[0] == 0
     assert len(bm.search_for_triangulation(q)) == 0
+
+
+@pytest.mark.parametrize("seed,n,nnratio,ori,mpb", [(13, 2000, 0.75, True, 0.6), (14, 2000, 0.75, False, 0.8),
+                                                    (15, 1000, 0.9, True, 0.5), (16, 3000, 0.6, True, 0.7)])
+def test_search_by_bow_kf(bm, oracle_mod, seed, n, nnratio, ori, mpb):
+    """SearchByBoW(KeyFrame*, KeyFrame*) (ORBmatcher.cc:760-903, LoopClosing::ComputeSim3)."""
+    p = synth.bow_match_problem(seed, n=n, n_points=int(0.8 * n), mp_frac_b=mpb)
+    nm_r, m_r = oracle_mod.search_by_bow_kf(p, nnratio, ori)
+    nm_g, m_g = bm.search_by_bow_kf(p, nnratio, ori)
+    assert nm_g == nm_r and np.array_equal(m_g, m_r)
+    assert nm_r > 20
+
+
+def test_bow_kf_batched(amd, oracle_mod):
+    m = amd.BowMatcher()
+    probs = [synth.bow_match_problem(70 + s, n=900 + 150 * s, n_points=800 + 100 * s, mp_frac_b=0.6) for s in range(5)]
+    m.reserve(len(probs), 2000)
+    for s, p in enumerate(probs):
+        m.stage(s, p)
+    m.run_bowkf_batch(len(probs), 0.75, True)
+    for s, p in enumerate(probs):
+        nm, out = m.fetch(s, 2, len(p["A"]["keys_un"]))
+        nm_r, out_r = oracle_mod.search_by_bow_kf(p, 0.75, True)
+        assert nm == nm_r and np.array_equal(out, out_r)
+    m.close()
