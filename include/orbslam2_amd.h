@@ -236,6 +236,15 @@ int orbt_search_by_projection_keyframe(orbt_engine *e, const orbt_frame *cur, co
 int orbt_fuse_candidates(orbt_engine *e, const orbt_frame *kf, const orbt_mappoints *M, float th,
                          int32_t *best_idx, int32_t *best_dist);
 
+/* LoopClosing's ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (ORBmatcher.h:126,
+ * ORBmatcher.cc:431-560; LoopClosing::ComputeSim3 with th = 10). `kf` = pKF (its Tcw / Ow are ignored:
+ * the pose is Scw, row-major 4x4 CV_32F [sR | t], unscaled as the reference does), M = vpPoints
+ * (ORBT_MP_BAD = isBad()), matched[kf->n] in/out = vpMatched as indices into M (-1 = NULL, <= -2 =
+ * a map point outside vpPoints: the keypoint stays taken). Greedy in point order, every claim
+ * blocks later points, first minimum Hamming distance <= TH_LOW. *nmatches = the return value. */
+int orbt_search_by_projection_sim3(orbt_engine *e, const orbt_frame *kf, const float Scw[16],
+                                   const orbt_mappoints *M, int th, int32_t *matched, int32_t *nmatches);
+
 /* Batched device-resident form (throughput path): stage independent problems into slots
  * (host -> HBM), run one launch chain over all slots, fetch per slot. `last`, `last_mp`,
  * `last_outlier` may be NULL when only orbt_run_local_batch is used. */
@@ -249,6 +258,11 @@ int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int ch
 /* relocalisation matcher over staged slots: `last` = the keyframe, `last_mp` = its matches */
 int orbt_run_reloc_batch(orbt_engine *e, int n_slots, float th, int orb_dist, int check_ori, void *stream);
 int orbt_run_fuse_batch(orbt_engine *e, int n_slots, float th, void *stream);
+/* loop-closing projection search over slots staged with orbt_stage_sim3; orbt_fetch's owner[i] is
+ * the newly matched point of keypoint i (-1 = none: vpMatched[i] unchanged) */
+int orbt_stage_sim3(orbt_engine *e, int slot, const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M,
+                    const int32_t *matched);
+int orbt_run_sim3_batch(orbt_engine *e, int n_slots, int th, void *stream);
 int orbt_fetch_fuse(orbt_engine *e, int slot, int32_t *best_idx, int32_t *best_dist);
 int orbt_fetch(orbt_engine *e, int slot, orbt_view *view, int32_t *owner, int32_t *nmatches);
 

@@ -450,6 +450,19 @@ def search_by_projection_keyframe(prob: dict, th=10.0, orb_dist=100, check_ori=T
     return nm, owner[: F.n]
 
 
+def search_by_projection_sim3(prob: dict, th=10):
+    """LoopClosing's SearchByProjection(pKF = prob["frame"], Scw, vpPoints = prob["map"], vpMatched, th):
+    (nmatches, vpMatched out as point indices, -1 = NULL, -2 = a point outside vpPoints)."""
+    L = lib()
+    L.orc_search_by_projection_sim3.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    F, k1 = make_orbt_frame(prob["frame"])
+    M, k2 = make_orbt_map(prob["map"])
+    Scw = np.ascontiguousarray(prob["Scw"], np.float32).reshape(16)
+    matched = np.array(prob["matched"], np.int32, copy=True)
+    nm = L.orc_search_by_projection_sim3(C.byref(F), Scw.ctypes.data, C.byref(M), int(th), matched.ctypes.data)
+    return nm, matched[: F.n]
+
+
 # ---- Optimizer::PoseOptimization (lba_oracle.c pose_oracle_optimize)
 class OrbpFrame(C.Structure):
     _fields_ = [("n", C.c_int32), ("Xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p),

@@ -384,6 +384,87 @@ int orc_search_by_projection_kf(const orbt_frame *cur, const orbt_frame *kf, con
     return nmatches;
 }
 
+/* LoopClosing's SearchByProjection(KeyFrame* pKF, cv::Mat Scw, vpPoints, vpMatched, th)
+ * (src/ORBmatcher.cc:431-560). The Sim3 pose is unscaled as cv::Mat evaluates it:
+ * scw = (float)sqrt(row0 . row0) (Mat::dot in double), sRcw / scw and st / scw through
+ * convertTo(alpha = 1.0 / scw) in float (cvtScale_<float, float, float>), Ow = -Rcw^T tcw (float
+ * gemm). matched[kf->n] in/out = vpMatched as indices into M (-1 = NULL, <= -2 = a point outside
+ * vpPoints). Returns nmatches. */
+void orc_sim3_unscale(const float Scw[16], float Tcw[12], float Ow[3]) {
+    double d = 0;
+    for (int k = 0; k < 3; k++) d += (double)Scw[k] * Scw[k];
+    const float scw = (float)sqrt(d);
+    const float a = (float)(1.0 / (double)scw);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 4; c++) Tcw[4 * r + c] = Scw[4 * r + c] * a + 0.0f;
+    for (int i = 0; i < 3; i++) {
+        float t = Tcw[i] * Tcw[3];
+        t = t + Tcw[4 + i] * Tcw[7];
+        t = t + Tcw[8 + i] * Tcw[11];
+        Ow[i] = -t;
+    }
+}
+
+int orc_search_by_projection_sim3(const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M, int th,
+                                  int32_t *matched) {
+    const int TH_LOW = 50;
+    const int N = kf->n;
+    orbt_frame K = *kf;
+    orc_sim3_unscale(Scw, K.Tcw, K.Ow);
+    orc_frame_grid g;
+    frame_grid(&K, &g);
+    uint8_t *found = (uint8_t *)calloc((size_t)M->n + 1, 1);   /* spAlreadyFound */
+    for (int i = 0; i < N; i++)
+        if (matched[i] >= 0 && matched[i] < M->n) found[matched[i]] = 1;
+    int *cand = (int *)malloc(sizeof(int) * ((size_t)N + 1));
+    int nmatches = 0;
+    for (int m = 0; m < M->n; m++) {
+        if ((M->flags[m] & ORBT_MP_BAD) || found[m]) continue;                 /* :463 */
+        const float *P = M->Xw + 3 * (size_t)m;
+        float p3Dc[3];
+        mat_rx_t(K.Tcw, P, p3Dc);                                                /* :471 */
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+        const float u = K.fx * x + K.cx, v = K.fy * y + K.cy;
+        if (!(u >= K.min_x && u < K.max_x && v >= K.min_y && v < K.max_y)) continue;   /* KeyFrame::IsInImage */
+        const float maxDistance = 1.2f * M->max_dist[m], minDistance = 0.8f * M->min_dist[m];
+        const float PO[3] = {P[0] - K.Ow[0], P[1] - K.Ow[1], P[2] - K.Ow[2]};
+        double ss = 0;
+        for (int k = 0; k < 3; k++) { const double t = PO[k]; ss += t * t; }
+        const float dist = (float)sqrt(ss);
+        if (dist < minDistance || dist > maxDistance) continue;                 /* :499 */
+        const float *Pn = M->normal + 3 * (size_t)m;
+        double dot = 0;
+        for (int k = 0; k < 3; k++) dot += (double)PO[k] * Pn[k];
+        if (dot < 0.5 * (double)dist) continue;                                 /* :506 */
+        const float ratio = M->max_dist[m] / dist;                               /* PredictScale(dist, pKF) */
+        int nPredictedLevel = (int)ceilf(orc_logf(ratio) / K.log_scale_factor);
+        if (nPredictedLevel < 0) nPredictedLevel = 0;
+        else if (nPredictedLevel >= K.nlevels) nPredictedLevel = K.nlevels - 1;
+        const float radius = th * K.scale_factors[nPredictedLevel];
+        const int nc = orc_features_in_area(&g, u, v, radius, -1, -1, cand, N + 1);   /* KeyFrame version */
+        if (nc == 0) continue;
+        const uint8_t *dMP = M->desc + 32 * (size_t)m;
+        int bestDist = 256, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int idx = cand[c];
+            if (matched[idx] != -1) continue;                                   /* :531 vpMatched[idx] */
+            const int kpLevel = K.keys_un[idx].octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const int d = orc_descriptor_distance(dMP, K.desc + 32 * (size_t)idx);
+            if (d < bestDist) { bestDist = d; bestIdx = idx; }
+        }
+        if (bestDist <= TH_LOW) {                                                /* :552-556 */
+            matched[bestIdx] = m;
+            nmatches++;
+        }
+    }
+    free(cand); free(found);
+    orc_grid_free(&g);
+    return nmatches;
+}
+
 /* ==========================================================================================
  * BoW-guided matchers: ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
  * (ORBmatcher.cc:236-353) and ORBmatcher::SearchForTriangulation (ORBmatcher.cc:915-1089,

@@ -22,6 +22,9 @@ int orc_search_by_projection_kf(const orbt_frame *cur, const orbt_frame *kf, con
                                 const orbt_mappoints *M, float th, int ORBdist, int checkOri,
                                 const uint8_t *kp_blocked, int32_t *owner);
 int orc_search_by_bow(const orbb_keyframe *kf, const orbb_keyframe *F, float nnratio, int checkOri, int32_t *matches);
+void orc_sim3_unscale(const float Scw[16], float Tcw[12], float Ow[3]);
+int orc_search_by_projection_sim3(const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M, int th,
+                                  int32_t *matched);
 int orc_search_by_bow_kf(const orbb_keyframe *k1, const orbb_keyframe *k2, float nnratio, int checkOri,
                          int32_t *matches12);
 int orc_search_for_triangulation(const orbb_keyframe *kf1, const orbb_keyframe *kf2, const float F12[9],

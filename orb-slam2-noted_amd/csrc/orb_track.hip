@@ -6,6 +6,10 @@
 //   ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
 //                                             ORBmatcher.cc:1922-2066 (relocalisation; the
 //                                             keyframe takes the last frame's slot)
+//   ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
+//                                             ORBmatcher.cc:431-560 (loop closing: the
+//                                             keyframe takes the frame's slot, Sim3 pose
+//                                             unscaled on the host, queries = map points)
 //
 // Both matchers are greedy: map points (resp. last-frame keypoints) are visited in order and
 // a keypoint claimed by a map point with Observations() > 0 is skipped by every later one.
@@ -491,7 +495,7 @@ __global__ __launch_bounds__(64) void track_local_resolve_kernel(Slots S, float 
     if (lane == 0) nmatch[s] = nm;
 }
 
-constexpr int kModeMotion = 0, kModeReloc = 1;
+constexpr int kModeMotion = 0, kModeReloc = 1, kModeSim3 = 2;
 
 // ---- relocalisation query of keyframe keypoint i (ORBmatcher.cc:1944-2019): map point not bad
 // and not in sAlreadyFound, projection without a depth-sign test, scale-invariance gate,
@@ -526,11 +530,47 @@ __device__ int reloc_query(const Slots &S, int s, const FrameDev &f, int i, floa
                               S.lkun[lb].angle, c);
 }
 
+// ---- loop-closing query of map point m (ORBmatcher.cc:457-551): not bad and not already in
+// vpMatched (ORBT_MP_FOUND), depth sign test, KeyFrame::IsInImage, scale-invariance and
+// viewing-angle (PO.Pn >= 0.5 dist) gates, PredictScale(dist, pKF), KeyFrame::GetFeaturesInArea
+// window then levels [lvl - 1, lvl]; `f` holds pKF with the unscaled Sim3 pose [Rcw | tcw], Ow
+__device__ int sim3_query(const Slots &S, int s, const FrameDev &f, int m, float th, const uint8_t *claimed,
+                          Cand &c) {
+#pragma unroll
+    for (int k = 0; k < TOPK; k++) { c.key[k] = 0xFFFFFFFFu; c.idx[k] = 0; c.oct[k] = -1; c.bin[k] = -1; }
+    const long long mb = (long long)s * S.cap_mp + m;
+    if (S.mflags[mb] & (ORBT_MP_BAD | ORBT_MP_FOUND)) return -1;
+    const float *P = S.Xw + mb * 3;
+    float p3Dc[3];
+    mat_rx_t(f.Tcw, P, p3Dc);
+    if (p3Dc[2] < 0.0f) return 0;
+    const float invz = 1 / p3Dc[2];
+    const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+    const float u = f.fx * x + f.cx, v = f.fy * y + f.cy;
+    if (!(u >= f.min_x && u < f.max_x && v >= f.min_y && v < f.max_y)) return 0;   // KeyFrame::IsInImage
+    const float maxDistance = 1.2f * S.maxd[mb], minDistance = 0.8f * S.mind[mb];
+    const float PO[3] = {P[0] - f.Ow[0], P[1] - f.Ow[1], P[2] - f.Ow[2]};
+    double ss = 0;
+    for (int k = 0; k < 3; k++) { const double t = PO[k]; ss = ss + t * t; }
+    const float dist = (float)sqrt(ss);                                      // cv::norm
+    if (dist < minDistance || dist > maxDistance) return 0;
+    const float *Pn = S.nrm + mb * 3;
+    double dot = 0;
+    for (int k = 0; k < 3; k++) dot = dot + (double)PO[k] * (double)Pn[k];   // Mat::dot
+    if (dot < 0.5 * (double)dist) return 0;
+    int lvl = (int)ceilf(glibc_logf(S.maxd[mb] / dist) / f.log_scale);       // PredictScale(dist, pKF)
+    if (lvl < 0) lvl = 0;
+    else if (lvl >= f.nlevels) lvl = f.nlevels - 1;
+    const float radius = th * f.scale[lvl];
+    return scan_window<false>(S, s, f, u, v, radius, lvl - 1, lvl, S.mdesc + mb * 32, 0.f, INFINITY, claimed, 0.f, c);
+}
+
 // ---- SearchByProjection(CurrentFrame, LastFrame) query of last keypoint i (ORBmatcher.cc:1786-1870);
 // `claimed` != null adds the claim filter (resolve fallback). Returns -1 if not projected.
 __device__ int frame_query(const Slots &S, int s, const FrameDev &f, int i, float th, int mono,
                            const uint8_t *claimed, Cand &c, int mode = kModeMotion) {
     if (mode == kModeReloc) return reloc_query(S, s, f, i, th, claimed, c);
+    if (mode == kModeSim3) return sim3_query(S, s, f, i, th, claimed, c);
 #pragma unroll
     for (int k = 0; k < TOPK; k++) { c.key[k] = 0xFFFFFFFFu; c.idx[k] = 0; c.oct[k] = -1; c.bin[k] = -1; }
     const long long lb = (long long)s * S.cap_kp + i;
@@ -572,16 +612,17 @@ __global__ __launch_bounds__(256) void track_frame_cand_kernel(Slots S, float th
                                                                int *ncand) {
     const int i = blockIdx.x * 256 + threadIdx.x, s = blockIdx.y;
     const FrameDev &f = S.fr[s];
-    if (i >= f.n_last) return;
+    if (i >= (mode == kModeSim3 ? f.n_mp : f.n_last)) return;   // queries: last keypoints / map points
     Cand c;
     const int nc = frame_query(S, s, f, i, th, mono, nullptr, c, mode);
-    const long long lb = (long long)s * S.cap_kp + i;
+    const long long lb = (long long)s * (mode == kModeSim3 ? S.cap_mp : S.cap_kp) + i;
     cand[lb] = c;
     ncand[lb] = nc;
 }
 
 // mode kModeMotion: accept <= TH_HIGH, a claim blocks later points only if the claiming point
-// has observations; kModeReloc: accept <= ORBdist (max_dist), every claim blocks (:2007-2008)
+// has observations; kModeReloc: accept <= ORBdist (max_dist), every claim blocks (:2007-2008);
+// kModeSim3: queries are the map points themselves, accept <= TH_LOW, every claim blocks (:552-555)
 __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float th, int mono, int check_ori,
                                                                  int mode, int max_dist,
                                                                  const Cand *cand, const int *ncand, int *owner,
@@ -602,18 +643,21 @@ __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float 
     int nm = 0, nh = 0, base = 0;
     int *HI = hist_idx + kb;
     int8_t *HB = hist_bin + kb;
-    while (base < f.n_last) {
+    const bool sim3 = mode == kModeSim3;
+    const int nq = sim3 ? f.n_mp : f.n_last;
+    const long long qb = sim3 ? mb0 : kb;   // query record base
+    while (base < nq) {
         const int q = base + lane;
-        const bool live = q < f.n_last;
+        const bool live = q < nq;
         Cand c;
         int nc = -1, m = -1;
-        if (live) { c = cand[kb + q]; nc = ncand[kb + q]; m = S.last_mp[kb + q]; }
+        if (live) { c = cand[qb + q]; nc = ncand[qb + q]; m = sim3 ? q : S.last_mp[kb + q]; }
         Pick pk;
         pk.found = 0; pk.last_ex = -1; pk.key0 = 0xFFFFFFFFu; pk.idx0 = 0; pk.bin0 = -1;
         if (nc > 0) pk = pick_unclaimed(c, claimed, 1);
         const bool fallback = nc > TOPK && pk.found < 1;
         const bool accept = nc > 0 && !fallback && pk.found >= 1 && (int)(pk.key0 >> 16) <= max_dist;
-        const bool obs = m >= 0 && (mode == kModeReloc || (S.mflags[mb0 + m] & ORBT_MP_HAS_OBS) != 0);
+        const bool obs = m >= 0 && (mode != kModeMotion || (S.mflags[mb0 + m] & ORBT_MP_HAS_OBS) != 0);
         const int idx = pk.idx0;
         if (accept && obs) atomicMin(&tag[idx], lane);
         __syncthreads();
@@ -642,7 +686,7 @@ __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float 
         nm += __popcll(cm);
         if (check_ori) nh += __popcll(cm);
         __syncthreads();
-        if (cut < 64 && base + cut < f.n_last && ((stop >> cut) & 1)) {
+        if (cut < 64 && base + cut < nq && ((stop >> cut) & 1)) {
             const bool is_fb = __shfl(fallback ? 1 : 0, cut) != 0;
             if (is_fb) {
                 if (lane == 0) {
@@ -650,9 +694,9 @@ __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float 
                     Cand full;
                     frame_query(S, s, f, qq, th, mono, claimed, full, mode);
                     if (full.key[0] != 0xFFFFFFFFu && (int)(full.key[0] >> 16) <= max_dist) {
-                        const int id = full.idx[0], mm = S.last_mp[kb + qq];
+                        const int id = full.idx[0], mm = sim3 ? qq : S.last_mp[kb + qq];
                         owner[kb + id] = mm;
-                        if (mode == kModeReloc || (S.mflags[mb0 + mm] & ORBT_MP_HAS_OBS)) claimed[id] = 1;
+                        if (mode != kModeMotion || (S.mflags[mb0 + mm] & ORBT_MP_HAS_OBS)) claimed[id] = 1;
                         nm++;
                         if (check_ori) {
                             HI[nh] = id;
@@ -828,6 +872,24 @@ int grid(orbt_engine *e, int n, hipStream_t st) {
     track_grid_kernel<<<n, 1024, sizeof(uint32_t) * e->sort_cap, st>>>(make_slots(e), e->keys.as<float4>(),
                                                                         e->cell_start.as<int>());
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+// LoopClosing's Sim3 pose, unscaled as cv::Mat evaluates it (ORBmatcher.cc:442-446): scw =
+// (float)sqrt(row0 . row0) with Mat::dot in double; sRcw / scw, st / scw = convertTo(alpha =
+// 1.0 / scw) in float; Ow = -Rcw^T tcw (float gemm)
+void sim3_unscale(const float Scw[16], float Tcw[12], float Ow[3]) {
+    double d = 0;
+    for (int k = 0; k < 3; k++) d += (double)Scw[k] * Scw[k];
+    const float scw = (float)std::sqrt(d);
+    const float a = (float)(1.0 / (double)scw);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 4; c++) Tcw[4 * r + c] = Scw[4 * r + c] * a + 0.0f;
+    for (int i = 0; i < 3; i++) {
+        float t = Tcw[i] * Tcw[3];
+        t = t + Tcw[4 + i] * Tcw[7];
+        t = t + Tcw[8 + i] * Tcw[11];
+        Ow[i] = -t;
+    }
 }
 
 void fill_frame(FrameDev &d, const orbt_frame *F) {
@@ -1068,6 +1130,59 @@ int orbt_search_by_projection_keyframe(orbt_engine *e, const orbt_frame *cur, co
     rc = orbt_run_reloc_batch(e, 1, th, orb_dist, check_ori, nullptr);
     if (rc) return rc;
     return orbt_fetch(e, 0, nullptr, owner, nmatches);
+}
+
+int orbt_stage_sim3(orbt_engine *e, int slot, const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M,
+                    const int32_t *matched) {
+    if (!e || !kf || !Scw || !M || !matched || kf->n < 0 || M->n < 0) return ORBX_EINVAL;
+    orbt_frame K = *kf;
+    sim3_unscale(Scw, K.Tcw, K.Ow);
+    std::vector<uint8_t> flags(M->flags, M->flags + M->n), blocked((size_t)kf->n + 1);
+    for (auto &f : flags) f &= (uint8_t)~ORBT_MP_FOUND;
+    for (int i = 0; i < kf->n; i++) {
+        if (matched[i] >= M->n) return ORBX_EINVAL;
+        blocked[i] = matched[i] != -1;                          // vpMatched[idx] != NULL
+        if (matched[i] >= 0) flags[matched[i]] |= ORBT_MP_FOUND;   // spAlreadyFound
+    }
+    orbt_mappoints M2 = *M;
+    M2.flags = flags.data();
+    return orbt_stage(e, slot, &K, &M2, nullptr, nullptr, nullptr, blocked.data());
+}
+
+int orbt_run_sim3_batch(orbt_engine *e, int n_slots, int th, void *stream) {
+    if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    hipStream_t st = pick(e, stream);
+    if (grid(e, n_slots, st)) return ORBX_EDEVICE;
+    const int mm = std::max(1, max_n(e, 0, n_slots));
+    const float thf = (float)th;
+    track_frame_cand_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), thf, 0, kModeSim3,
+                                                                             e->cand.as<Cand>(), e->ncand.as<int>());
+    track_frame_resolve_kernel<<<n_slots, 64, resolve_lds(e), st>>>(make_slots(e), thf, 0, 0, kModeSim3, 50,
+                                                                e->cand.as<Cand>(), e->ncand.as<int>(),
+                                                                e->owner.as<int>(), e->nmatch.as<int>(),
+                                                                e->hist_idx.as<int>(), e->hist_bin.as<int8_t>());
+    TR_CHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbt_search_by_projection_sim3(orbt_engine *e, const orbt_frame *kf, const float Scw[16],
+                                   const orbt_mappoints *M, int th, int32_t *matched, int32_t *nmatches) {
+    if (!e || !kf || !Scw || !M || !matched || !nmatches) return ORBX_EINVAL;
+    if (e->nslots < 1 || e->cap_kp < kf->n || e->cap_mp < M->n) {
+        const int rc = orbt_reserve(e, std::max(1, e->nslots), std::max(e->cap_kp, kf->n), std::max(e->cap_mp, M->n));
+        if (rc) return rc;
+    }
+    int rc = orbt_stage_sim3(e, 0, kf, Scw, M, matched);
+    if (rc) return rc;
+    rc = orbt_run_sim3_batch(e, 1, th, nullptr);
+    if (rc) return rc;
+    std::vector<int32_t> owner((size_t)kf->n + 1);
+    rc = orbt_fetch(e, 0, nullptr, owner.data(), nmatches);
+    if (rc) return rc;
+    for (int i = 0; i < kf->n; i++)
+        if (owner[i] >= 0) matched[i] = owner[i];   // vpMatched[bestIdx] = pMP
+    return ORBX_OK;
 }
 
 int orbt_run_fuse_batch(orbt_engine *e, int n_slots, float th, void *stream) {

@@ -90,6 +90,9 @@ SIGNATURES = [
     ("orbt_fuse_candidates", _I, [_P, _P, _P, _F, _P, _P]),
     ("orbt_run_fuse_batch", _I, [_P, _I, _F, _P]),
     ("orbt_fetch_fuse", _I, [_P, _I, _P, _P]),
+    ("orbt_search_by_projection_sim3", _I, [_P, _P, _P, _P, _I, _P, _P]),
+    ("orbt_stage_sim3", _I, [_P, _I, _P, _P, _P, _P]),
+    ("orbt_run_sim3_batch", _I, [_P, _I, _I, _P]),
     ("orbp_create", _I, [C.POINTER(C.c_void_p)]),
     ("orbp_destroy", None, [_P]),
     ("orbp_pose_optimization", _I, [_P, _P, _P]),
@@ -575,6 +578,37 @@ class Tracker:
     def run_reloc_batch(self, n_slots: int, th=10.0, orb_dist=100, check_ori=True, stream=None):
         _check(lib().orbt_run_reloc_batch(self._h, n_slots, th, int(orb_dist), 1 if check_ori else 0, stream),
                "orbt_run_reloc_batch")
+
+    def search_by_projection_sim3(self, prob: dict, th=10):
+        """LoopClosing's SearchByProjection(pKF, Scw, vpPoints, vpMatched, th): prob = {"frame" (pKF),
+        "map" (vpPoints), "Scw" (4x4), "matched" (vpMatched as point indices, -1 NULL, -2 outside)}.
+        Returns (nmatches, vpMatched out)."""
+        F, k1 = _orbt_frame(prob["frame"])
+        M, k2 = _orbt_map(prob["map"])
+        Scw = np.ascontiguousarray(prob["Scw"], np.float32).reshape(16)
+        matched = np.array(prob["matched"], np.int32, copy=True)
+        nm = C.c_int32()
+        _check(lib().orbt_search_by_projection_sim3(self._h, C.byref(F), Scw.ctypes.data, C.byref(M), int(th),
+                                                    matched.ctypes.data, C.byref(nm)), "orbt_search_by_projection_sim3")
+        return nm.value, matched[: F.n]
+
+    def stage_sim3(self, slot: int, prob: dict):
+        F, k1 = _orbt_frame(prob["frame"])
+        M, k2 = _orbt_map(prob["map"])
+        Scw = np.ascontiguousarray(prob["Scw"], np.float32).reshape(16)
+        matched = np.ascontiguousarray(prob["matched"], np.int32)
+        _check(lib().orbt_stage_sim3(self._h, slot, C.byref(F), Scw.ctypes.data, C.byref(M), matched.ctypes.data),
+               "orbt_stage_sim3")
+
+    def run_sim3_batch(self, n_slots: int, th=10, stream=None):
+        _check(lib().orbt_run_sim3_batch(self._h, n_slots, int(th), stream), "orbt_run_sim3_batch")
+
+    def fetch_sim3(self, slot: int, prob: dict):
+        n = len(prob["frame"]["keys_un"])
+        nm, owner, _ = self.fetch(slot, n)
+        matched = np.array(prob["matched"], np.int32, copy=True)[:n]
+        matched[owner >= 0] = owner[owner >= 0]
+        return nm, matched
 
     def fuse_candidates(self, prob: dict, th=3.0):
         """ORBmatcher::Fuse(pKF, vpMapPoints, th) search half; prob["frame"] is the KeyFrame."""
