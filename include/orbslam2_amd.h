@@ -245,6 +245,23 @@ int orbt_fuse_candidates(orbt_engine *e, const orbt_frame *kf, const orbt_mappoi
 int orbt_search_by_projection_sim3(orbt_engine *e, const orbt_frame *kf, const float Scw[16],
                                    const orbt_mappoints *M, int th, int32_t *matched, int32_t *nmatches);
 
+/* LoopClosing's ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (ORBmatcher.h:215,
+ * ORBmatcher.cc:1321-1458; LoopClosing::SearchAndFuse th = 4) -- the search half: pose = Scw
+ * unscaled, flags ORBT_MP_IN_FRAME = in pKF->GetMapPoints(); best_idx[m] / best_dist[m] = the
+ * first minimum over the window at levels [l - 1, l] (-1 / INT_MAX = no candidate). The caller
+ * applies the reference's update for best_dist <= 50 (vpReplacePoint / AddObservation, :1439-1453). */
+int orbt_fuse_sim3_candidates(orbt_engine *e, const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M,
+                              float th, int32_t *best_idx, int32_t *best_dist);
+
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.h:197,
+ * ORBmatcher.cc:1472-1723; LoopClosing::ComputeSim3 th = 7.5): kf1_mp / kf2_mp =
+ * GetMapPointMatches() as indices into M (-1 = NULL), matches12[kf1->n] in/out = vpMatches12 (-1 =
+ * NULL). Both projection directions run in parallel (no claims), then the mutual-agreement check;
+ * *nfound = the return value. R12 row-major CV_32F, t12 CV_32F. */
+int orbt_search_by_sim3(orbt_engine *e, const orbt_frame *kf1, const int32_t *kf1_mp, const orbt_frame *kf2,
+                        const int32_t *kf2_mp, const orbt_mappoints *M, float s12, const float R12[9],
+                        const float t12[3], float th, int32_t *matches12, int32_t *nfound);
+
 /* Batched device-resident form (throughput path): stage independent problems into slots
  * (host -> HBM), run one launch chain over all slots, fetch per slot. `last`, `last_mp`,
  * `last_outlier` may be NULL when only orbt_run_local_batch is used. */
@@ -263,6 +280,16 @@ int orbt_run_fuse_batch(orbt_engine *e, int n_slots, float th, void *stream);
 int orbt_stage_sim3(orbt_engine *e, int slot, const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M,
                     const int32_t *matched);
 int orbt_run_sim3_batch(orbt_engine *e, int n_slots, int th, void *stream);
+/* Fuse(pKF, Scw, ...) search half over slots (fetch with orbt_fetch_fuse) */
+int orbt_stage_fuse_sim3(orbt_engine *e, int slot, const orbt_frame *kf, const float Scw[16],
+                         const orbt_mappoints *M);
+int orbt_run_fuse_sim3_batch(orbt_engine *e, int n_slots, float th, void *stream);
+/* SearchBySim3 pair k uses slots 2k and 2k + 1 (one per projection direction) */
+int orbt_stage_search_by_sim3(orbt_engine *e, int pair, const orbt_frame *kf1, const int32_t *kf1_mp,
+                              const orbt_frame *kf2, const int32_t *kf2_mp, const orbt_mappoints *M, float s12,
+                              const float R12[9], const float t12[3], const int32_t *matches12);
+int orbt_run_sim3_match_batch(orbt_engine *e, int n_pairs, float th, void *stream);
+int orbt_fetch_search_by_sim3(orbt_engine *e, int pair, const int32_t *kf2_mp, int32_t *matches12, int32_t *nfound);
 int orbt_fetch_fuse(orbt_engine *e, int slot, int32_t *best_idx, int32_t *best_dist);
 int orbt_fetch(orbt_engine *e, int slot, orbt_view *view, int32_t *owner, int32_t *nmatches);
 

@@ -463,6 +463,37 @@ def search_by_projection_sim3(prob: dict, th=10):
     return nm, matched[: F.n]
 
 
+def fuse_sim3_candidates(prob: dict, th=4.0):
+    """LoopClosing's Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) search half: (best_idx, best_dist)."""
+    L = lib()
+    L.orc_fuse_sim3_candidates.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p]
+    F, k1 = make_orbt_frame(prob["frame"])
+    M, k2 = make_orbt_map(prob["map"])
+    Scw = np.ascontiguousarray(prob["Scw"], np.float32).reshape(16)
+    bi = np.zeros(max(M.n, 1), np.int32)
+    bd = np.zeros(max(M.n, 1), np.int32)
+    L.orc_fuse_sim3_candidates(C.byref(F), Scw.ctypes.data, C.byref(M), th, bi.ctypes.data, bd.ctypes.data)
+    return bi[: M.n], bd[: M.n]
+
+
+def search_by_sim3(prob: dict, th=7.5):
+    """ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th): (nFound, matches12 out)."""
+    L = lib()
+    L.orc_search_by_sim3.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_void_p,
+                                     C.c_void_p, C.c_float, C.c_void_p]
+    F1, k1 = make_orbt_frame(prob["kf1"])
+    F2, k2 = make_orbt_frame(prob["kf2"])
+    M, k3 = make_orbt_map(prob["map"])
+    mp1 = np.ascontiguousarray(prob["kf1_mp"], np.int32)
+    mp2 = np.ascontiguousarray(prob["kf2_mp"], np.int32)
+    R12 = np.ascontiguousarray(prob["R12"], np.float32).reshape(9)
+    t12 = np.ascontiguousarray(prob["t12"], np.float32).reshape(3)
+    m12 = np.array(prob["matches12"], np.int32, copy=True)
+    nf = L.orc_search_by_sim3(C.byref(F1), mp1.ctypes.data, C.byref(F2), mp2.ctypes.data, C.byref(M), float(prob["s12"]),
+                              R12.ctypes.data, t12.ctypes.data, th, m12.ctypes.data)
+    return nf, m12[: F1.n]
+
+
 # ---- Optimizer::PoseOptimization (lba_oracle.c pose_oracle_optimize)
 class OrbpFrame(C.Structure):
     _fields_ = [("n", C.c_int32), ("Xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p),

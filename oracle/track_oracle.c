@@ -22,6 +22,7 @@
  *   - `1.0 / z` with float z is a double division rounded to float (ORBmatcher.cc:1794);
  *   - round(float) = roundf (half away from zero), ceil(float) = ceilf.
  */
+#include <limits.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -463,6 +464,159 @@ int orc_search_by_projection_sim3(const orbt_frame *kf, const float Scw[16], con
     free(cand); free(found);
     orc_grid_free(&g);
     return nmatches;
+}
+
+/* LoopClosing's Fuse(KeyFrame* pKF, cv::Mat Scw, vpPoints, th, vpReplacePoint) search half
+ * (src/ORBmatcher.cc:1321-1437): per point the first minimum Hamming distance in the window
+ * (bestDist starts at INT_MAX, :1414), levels [l - 1, l], no chi2 gate; invz = 1.0 / z in double
+ * (:1369). flags ORBT_MP_IN_FRAME = in pKF->GetMapPoints() (spAlreadyFound, :1339). */
+void orc_fuse_sim3_candidates(const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M, float th,
+                              int32_t *best_idx, int32_t *best_dist) {
+    const int N = kf->n;
+    orbt_frame K = *kf;
+    orc_sim3_unscale(Scw, K.Tcw, K.Ow);
+    orc_frame_grid g;
+    frame_grid(&K, &g);
+    int *cand = (int *)malloc(sizeof(int) * ((size_t)N + 1));
+    for (int m = 0; m < M->n; m++) {
+        best_idx[m] = -1;
+        best_dist[m] = INT_MAX;
+        if (M->flags[m] & (ORBT_MP_BAD | ORBT_MP_IN_FRAME)) continue;          /* :1353 */
+        const float *P = M->Xw + 3 * (size_t)m;
+        float p3Dc[3];
+        mat_rx_t(K.Tcw, P, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = (float)(1.0 / (double)p3Dc[2]);
+        const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+        const float u = K.fx * x + K.cx, v = K.fy * y + K.cy;
+        if (!(u >= K.min_x && u < K.max_x && v >= K.min_y && v < K.max_y)) continue;
+        const float maxDistance = 1.2f * M->max_dist[m], minDistance = 0.8f * M->min_dist[m];
+        const float PO[3] = {P[0] - K.Ow[0], P[1] - K.Ow[1], P[2] - K.Ow[2]};
+        double ss = 0;
+        for (int k = 0; k < 3; k++) { const double t = PO[k]; ss += t * t; }
+        const float dist3D = (float)sqrt(ss);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float *Pn = M->normal + 3 * (size_t)m;
+        double dot = 0;
+        for (int k = 0; k < 3; k++) dot += (double)PO[k] * Pn[k];
+        if (dot < 0.5 * (double)dist3D) continue;
+        int lvl = (int)ceilf(orc_logf(M->max_dist[m] / dist3D) / K.log_scale_factor);
+        if (lvl < 0) lvl = 0;
+        else if (lvl >= K.nlevels) lvl = K.nlevels - 1;
+        const float radius = th * K.scale_factors[lvl];
+        const int nc = orc_features_in_area(&g, u, v, radius, -1, -1, cand, N + 1);
+        const uint8_t *dMP = M->desc + 32 * (size_t)m;
+        int bestDist = INT_MAX, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int idx = cand[c];
+            const int kpLevel = K.keys_un[idx].octave;
+            if (kpLevel < lvl - 1 || kpLevel > lvl) continue;
+            const int d = orc_descriptor_distance(dMP, K.desc + 32 * (size_t)idx);
+            if (d < bestDist) { bestDist = d; bestIdx = idx; }
+        }
+        best_idx[m] = bestIdx;
+        best_dist[m] = bestDist;
+    }
+    free(cand);
+    orc_grid_free(&g);
+}
+
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (src/ORBmatcher.cc:1472-1723).
+ * Both keyframes' GetMapPointMatches() as indices into M; matches12[kf1->n] in/out (-1 = NULL).
+ * sR12 = s12 * R12, sR21 = (1.0 / s12) * R12.t() (MatExpr scale -> convertTo in float),
+ * t21 = -sR21 * t12 (float gemm). pKF1's intrinsics project in both directions (:1476-1479). */
+static int sim3_pass(const orbt_frame *src, const int32_t *mp_src, const uint8_t *already, const orbt_frame *dst,
+                     const orbt_frame *k1, const float sR[9], const float st[3], const orbt_mappoints *M, float th,
+                     orc_frame_grid *g, int *cand, int *vnMatch) {
+    const int TH_HIGH = 100;
+    float T[12];
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) T[4 * r + c] = sR[3 * r + c];
+        T[4 * r + 3] = st[r];
+    }
+    for (int i = 0; i < src->n; i++) {
+        vnMatch[i] = -1;
+        const int m = mp_src[i];
+        if (m < 0 || already[i]) continue;                                     /* :1535 */
+        if (M->flags[m] & ORBT_MP_BAD) continue;
+        const float *P = M->Xw + 3 * (size_t)m;
+        float pc1[3], pc2[3];
+        mat_rx_t(src->Tcw, P, pc1);                                              /* :1544 */
+        mat_rx_t(T, pc1, pc2);                                                   /* :1546 */
+        if (pc2[2] < 0.0f) continue;
+        const float invz = (float)(1.0 / (double)pc2[2]);
+        const float x = pc2[0] * invz, y = pc2[1] * invz;
+        const float u = k1->fx * x + k1->cx, v = k1->fy * y + k1->cy;
+        if (!(u >= dst->min_x && u < dst->max_x && v >= dst->min_y && v < dst->max_y)) continue;
+        const float maxDistance = 1.2f * M->max_dist[m], minDistance = 0.8f * M->min_dist[m];
+        double ss = 0;
+        for (int k = 0; k < 3; k++) { const double t = pc2[k]; ss += t * t; }
+        const float dist3D = (float)sqrt(ss);                                    /* cv::norm(p3Dc2) */
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        int lvl = (int)ceilf(orc_logf(M->max_dist[m] / dist3D) / dst->log_scale_factor);
+        if (lvl < 0) lvl = 0;
+        else if (lvl >= dst->nlevels) lvl = dst->nlevels - 1;
+        const float radius = th * dst->scale_factors[lvl];
+        const int nc = orc_features_in_area(g, u, v, radius, -1, -1, cand, dst->n + 1);
+        const uint8_t *dMP = M->desc + 32 * (size_t)m;
+        int bestDist = INT_MAX, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int idx = cand[c];
+            const int o = dst->keys_un[idx].octave;
+            if (o < lvl - 1 || o > lvl) continue;
+            const int d = orc_descriptor_distance(dMP, dst->desc + 32 * (size_t)idx);
+            if (d < bestDist) { bestDist = d; bestIdx = idx; }
+        }
+        if (bestDist <= TH_HIGH) vnMatch[i] = bestIdx;
+    }
+    return 0;
+}
+
+void orc_sim3_relative(float s12, const float R12[9], const float t12[3], float sR12[9], float sR21[9], float t21[3]) {
+    for (int k = 0; k < 9; k++) sR12[k] = R12[k] * s12 + 0.0f;
+    const float a = (float)(1.0 / (double)s12);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) sR21[3 * i + j] = R12[3 * j + i] * a + 0.0f;
+    for (int i = 0; i < 3; i++) {
+        float t = sR21[3 * i] * t12[0];
+        t = t + sR21[3 * i + 1] * t12[1];
+        t = t + sR21[3 * i + 2] * t12[2];
+        t21[i] = -t;
+    }
+}
+
+int orc_search_by_sim3(const orbt_frame *kf1, const int32_t *mp1, const orbt_frame *kf2, const int32_t *mp2,
+                       const orbt_mappoints *M, float s12, const float R12[9], const float t12[3], float th,
+                       int32_t *matches12) {
+    const int N1 = kf1->n, N2 = kf2->n;
+    float sR12[9], sR21[9], t21[3];
+    orc_sim3_relative(s12, R12, t12, sR12, sR21, t21);
+    uint8_t *am1 = (uint8_t *)calloc((size_t)N1 + 1, 1), *am2 = (uint8_t *)calloc((size_t)N2 + 1, 1);
+    for (int i = 0; i < N1; i++) {
+        const int m = matches12[i];
+        if (m < 0) continue;
+        am1[i] = 1;
+        for (int j = 0; j < N2; j++)   /* pMP->GetIndexInKeyFrame(pKF2) */
+            if (mp2[j] == m) { am2[j] = 1; break; }
+    }
+    int *v1 = (int *)malloc(sizeof(int) * ((size_t)N1 + 1)), *v2 = (int *)malloc(sizeof(int) * ((size_t)N2 + 1));
+    int *cand = (int *)malloc(sizeof(int) * ((size_t)(N1 > N2 ? N1 : N2) + 1));
+    orc_frame_grid g1, g2;
+    frame_grid(kf1, &g1);
+    frame_grid(kf2, &g2);
+    sim3_pass(kf1, mp1, am1, kf2, kf1, sR21, t21, M, th, &g2, cand, v1);
+    sim3_pass(kf2, mp2, am2, kf1, kf1, sR12, t12, M, th, &g1, cand, v2);
+    int nFound = 0;
+    for (int i1 = 0; i1 < N1; i1++) {                                            /* :1706-1720 */
+        const int idx2 = v1[i1];
+        if (idx2 >= 0 && v2[idx2] == i1) {
+            matches12[i1] = mp2[idx2];
+            nFound++;
+        }
+    }
+    orc_grid_free(&g1); orc_grid_free(&g2);
+    free(am1); free(am2); free(v1); free(v2); free(cand);
+    return nFound;
 }
 
 /* ==========================================================================================

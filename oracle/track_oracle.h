@@ -25,6 +25,12 @@ int orc_search_by_bow(const orbb_keyframe *kf, const orbb_keyframe *F, float nnr
 void orc_sim3_unscale(const float Scw[16], float Tcw[12], float Ow[3]);
 int orc_search_by_projection_sim3(const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M, int th,
                                   int32_t *matched);
+void orc_fuse_sim3_candidates(const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M, float th,
+                              int32_t *best_idx, int32_t *best_dist);
+void orc_sim3_relative(float s12, const float R12[9], const float t12[3], float sR12[9], float sR21[9], float t21[3]);
+int orc_search_by_sim3(const orbt_frame *kf1, const int32_t *mp1, const orbt_frame *kf2, const int32_t *mp2,
+                       const orbt_mappoints *M, float s12, const float R12[9], const float t12[3], float th,
+                       int32_t *matches12);
 int orc_search_by_bow_kf(const orbb_keyframe *k1, const orbb_keyframe *k2, float nnratio, int checkOri,
                          int32_t *matches12);
 int orc_search_for_triangulation(const orbb_keyframe *kf1, const orbb_keyframe *kf2, const float F12[9],

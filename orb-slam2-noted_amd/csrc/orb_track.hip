@@ -6,6 +6,8 @@
 //   ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
 //                                             ORBmatcher.cc:1922-2066 (relocalisation; the
 //                                             keyframe takes the last frame's slot)
+//   ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint), search half  ORBmatcher.cc:1321-1437
+//   ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)  ORBmatcher.cc:1472-1723
 //   ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
 //                                             ORBmatcher.cc:431-560 (loop closing: the
 //                                             keyframe takes the frame's slot, Sim3 pose
@@ -65,7 +67,9 @@ struct FrameDev {
     float log_scale;
     float scale[16];
     float inv_s2[16];  // mvInvLevelSigma2 (Fuse)
-    float lTcw[12];   // last frame pose (frame-to-frame matcher)
+    float lTcw[12];   // last frame pose (frame-to-frame matcher); source keyframe pose (SearchBySim3)
+    float sT[12];     // SearchBySim3: [sR | t] from the source camera into this (target) keyframe's camera
+    float pfx, pfy, pcx, pcy;   // SearchBySim3: pKF1's intrinsics project in both directions
 };
 
 // per-slot device arrays (slot stride = cap)
@@ -747,12 +751,14 @@ __global__ __launch_bounds__(64) void track_frame_resolve_kernel(Slots S, float 
 
 // ---- ORBmatcher::Fuse(pKF, vpMapPoints, th) search half (ORBmatcher.cc:1139-1240): one thread
 // per (slot, map point); no claims -- every point's best keypoint is independent
-__global__ __launch_bounds__(256) void track_fuse_kernel(Slots S, float th, int *best_idx, int *best_dist) {
+// sim3 != 0: LoopClosing's Fuse(pKF, Scw, ...) (ORBmatcher.cc:1347-1433): Sim3-derived pose in the
+// slot, invz = 1.0 / z in double, no chi2 gate, bestDist starting at INT_MAX
+__global__ __launch_bounds__(256) void track_fuse_kernel(Slots S, float th, int sim3, int *best_idx, int *best_dist) {
     const int m = blockIdx.x * 256 + threadIdx.x, s = blockIdx.y;
     const FrameDev &f = S.fr[s];
     if (m >= f.n_mp) return;
     const long long mb = (long long)s * S.cap_mp + m;
-    int bestIdx = -1, bestDist = 256;
+    int bestIdx = -1, bestDist = sim3 ? INT_MAX : 256;
     if (!(S.mflags[mb] & (ORBT_MP_BAD | ORBT_MP_IN_FRAME))) {   // isBad() || IsInKeyFrame(pKF)
         const float *P = S.Xw + mb * 3;
         float p3Dc[3];
@@ -761,7 +767,7 @@ __global__ __launch_bounds__(256) void track_fuse_kernel(Slots S, float th, int 
         float u = 0, v = 0, ur = 0;
         int lvl = 0;
         if (ok) {
-            const float invz = 1 / p3Dc[2];
+            const float invz = sim3 ? (float)(1.0 / (double)p3Dc[2]) : 1 / p3Dc[2];
             const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
             u = f.fx * x + f.cx;
             v = f.fy * y + f.cy;
@@ -805,7 +811,8 @@ __global__ __launch_bounds__(256) void track_fuse_kernel(Slots S, float th, int 
                     const int idx = (int)(pk & 0xFFFFu), kpLevel = (int)((pk >> 16) & 0xFF);
                     if (kpLevel < lvl - 1 || kpLevel > lvl) continue;
                     const float ex = u - g.x, ey = v - g.y;
-                    if (g.z >= 0) {
+                    if (sim3) {
+                    } else if (g.z >= 0) {
                         const float er = ur - g.z;
                         const float e2 = ex * ex + ey * ey + er * er;
                         if ((double)(e2 * f.inv_s2[kpLevel]) > 7.8) continue;
@@ -821,6 +828,71 @@ __global__ __launch_bounds__(256) void track_fuse_kernel(Slots S, float th, int 
     }
     best_idx[mb] = bestIdx;
     best_dist[mb] = bestDist;
+}
+
+// ---- ORBmatcher::SearchBySim3, one direction (ORBmatcher.cc:1530-1618 / 1623-1700): thread per
+// (slot, source keypoint i); the slot's frame is the target keyframe, `last` the source keyframe
+// with its map points and vbAlreadyMatched (last_out). out[i] = vnMatch[i] (-1 = none).
+__global__ __launch_bounds__(256) void track_sim3_match_kernel(Slots S, float th, int *out) {
+    const int i = blockIdx.x * 256 + threadIdx.x, s = blockIdx.y;
+    const FrameDev &f = S.fr[s];
+    if (i >= f.n_last) return;
+    const long long lb = (long long)s * S.cap_kp + i;
+    const int m = S.last_mp[lb];
+    int vn = -1;
+    if (m >= 0 && !S.last_out[lb]) {
+        const long long mb = (long long)s * S.cap_mp + m;
+        if (!(S.mflags[mb] & ORBT_MP_BAD)) {
+            const float *P = S.Xw + mb * 3;
+            float pc1[3], pc2[3];
+            mat_rx_t(f.lTcw, P, pc1);
+            mat_rx_t(f.sT, pc1, pc2);
+            bool ok = !(pc2[2] < 0.0f);
+            float u = 0, v = 0, dist3D = 0;
+            if (ok) {
+                const float invz = (float)(1.0 / (double)pc2[2]);
+                const float x = pc2[0] * invz, y = pc2[1] * invz;
+                u = f.pfx * x + f.pcx;
+                v = f.pfy * y + f.pcy;
+                ok = u >= f.min_x && u < f.max_x && v >= f.min_y && v < f.max_y;   // KeyFrame::IsInImage
+            }
+            if (ok) {
+                double ss = 0;
+                for (int k = 0; k < 3; k++) { const double t = pc2[k]; ss = ss + t * t; }
+                dist3D = (float)sqrt(ss);                                          // cv::norm(p3Dc2)
+                ok = !(dist3D < 0.8f * S.mind[mb] || dist3D > 1.2f * S.maxd[mb]);
+            }
+            int cx0, cx1, cy0, cy1;
+            int lvl = 0;
+            if (ok) {
+                lvl = (int)ceilf(glibc_logf(S.maxd[mb] / dist3D) / f.log_scale);   // PredictScale(dist3D, target)
+                if (lvl < 0) lvl = 0;
+                else if (lvl >= f.nlevels) lvl = f.nlevels - 1;
+            }
+            const float radius = th * f.scale[lvl];
+            if (ok && grid_window(f, u, v, radius, cx0, cx1, cy0, cy1)) {
+                const float4 *rec = S.grec + (long long)s * S.sort_cap;
+                const int *cs = S.cell_start + (long long)s * (NCELL + 1);
+                const long long kb = (long long)s * S.cap_kp;
+                const uint8_t *dMP = S.mdesc + mb * 32;
+                int bestDist = INT_MAX, bestIdx = -1;
+                for (int ix = cx0; ix <= cx1; ix++) {
+                    const int a = cs[ix * GRID_ROWS + cy0], b = cs[ix * GRID_ROWS + cy1 + 1];
+                    for (int t = a; t < b; t++) {
+                        const float4 g = rec[t];
+                        if (!(fabsf(g.x - u) < radius && fabsf(g.y - v) < radius)) continue;
+                        const uint32_t pk = __float_as_uint(g.w);
+                        const int idx = (int)(pk & 0xFFFFu), o = (int)((pk >> 16) & 0xFF);
+                        if (o < lvl - 1 || o > lvl) continue;
+                        const int d = hamming32(dMP, S.desc + (kb + idx) * 32);
+                        if (d < bestDist) { bestDist = d; bestIdx = idx; }
+                    }
+                }
+                if (bestDist <= TH_HIGH) vn = bestIdx;
+            }
+        }
+    }
+    out[lb] = vn;
 }
 
 }  // namespace orbtrack
@@ -1185,13 +1257,141 @@ int orbt_search_by_projection_sim3(orbt_engine *e, const orbt_frame *kf, const f
     return ORBX_OK;
 }
 
+int orbt_stage_fuse_sim3(orbt_engine *e, int slot, const orbt_frame *kf, const float Scw[16],
+                         const orbt_mappoints *M) {
+    if (!e || !kf || !Scw || !M) return ORBX_EINVAL;
+    orbt_frame K = *kf;
+    sim3_unscale(Scw, K.Tcw, K.Ow);
+    return orbt_stage(e, slot, &K, M, nullptr, nullptr, nullptr, nullptr);
+}
+
+int orbt_run_fuse_sim3_batch(orbt_engine *e, int n_slots, float th, void *stream) {
+    if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    hipStream_t st = pick(e, stream);
+    if (grid(e, n_slots, st)) return ORBX_EDEVICE;
+    const int mm = std::max(1, max_n(e, 0, n_slots));
+    track_fuse_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, 1, e->fuse_idx.as<int>(),
+                                                                       e->fuse_dist.as<int>());
+    TR_CHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbt_fuse_sim3_candidates(orbt_engine *e, const orbt_frame *kf, const float Scw[16], const orbt_mappoints *M,
+                              float th, int32_t *best_idx, int32_t *best_dist) {
+    if (!e || !kf || !Scw || !M || !best_idx || !best_dist) return ORBX_EINVAL;
+    if (e->nslots < 1 || e->cap_kp < kf->n || e->cap_mp < M->n) {
+        const int rc = orbt_reserve(e, std::max(1, e->nslots), std::max(e->cap_kp, kf->n), std::max(e->cap_mp, M->n));
+        if (rc) return rc;
+    }
+    int rc = orbt_stage_fuse_sim3(e, 0, kf, Scw, M);
+    if (rc) return rc;
+    rc = orbt_run_fuse_sim3_batch(e, 1, th, nullptr);
+    if (rc) return rc;
+    return orbt_fetch_fuse(e, 0, best_idx, best_dist);
+}
+
+// SearchBySim3 pair k -> slots 2k (target pKF2, source pKF1) and 2k+1 (target pKF1, source pKF2)
+int orbt_stage_search_by_sim3(orbt_engine *e, int pair, const orbt_frame *kf1, const int32_t *kf1_mp,
+                              const orbt_frame *kf2, const int32_t *kf2_mp, const orbt_mappoints *M, float s12,
+                              const float R12[9], const float t12[3], const int32_t *matches12) {
+    if (!e || !kf1 || !kf1_mp || !kf2 || !kf2_mp || !M || !R12 || !t12 || !matches12) return ORBX_EINVAL;
+    if (pair < 0 || 2 * pair + 1 >= e->nslots) return ORBX_EINVAL;
+    float sR12[9], sR21[9], t21[3];
+    for (int k = 0; k < 9; k++) sR12[k] = R12[k] * s12 + 0.0f;             // s12 * R12 (convertTo)
+    const float a = (float)(1.0 / (double)s12);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) sR21[3 * i + j] = R12[3 * j + i] * a + 0.0f;   // (1.0 / s12) * R12.t()
+    for (int i = 0; i < 3; i++) {                                           // t21 = -sR21 * t12
+        float t = sR21[3 * i] * t12[0];
+        t = t + sR21[3 * i + 1] * t12[1];
+        t = t + sR21[3 * i + 2] * t12[2];
+        t21[i] = -t;
+    }
+    // vbAlreadyMatched1 / 2 (ORBmatcher.cc:1509-1522; GetIndexInKeyFrame = the kf2 keypoint holding it)
+    std::vector<uint8_t> am1((size_t)kf1->n + 1, 0), am2((size_t)kf2->n + 1, 0);
+    for (int i = 0; i < kf1->n; i++) {
+        const int m = matches12[i];
+        if (m < 0) continue;
+        if (m >= M->n) return ORBX_EINVAL;
+        am1[i] = 1;
+        for (int j = 0; j < kf2->n; j++)
+            if (kf2_mp[j] == m) { am2[j] = 1; break; }
+    }
+    const orbt_frame *tgt[2] = {kf2, kf1}, *src[2] = {kf1, kf2};
+    const int32_t *mps[2] = {kf1_mp, kf2_mp};
+    const uint8_t *ams[2] = {am1.data(), am2.data()};
+    const float *sRs[2] = {sR21, sR12}, *sts[2] = {t21, t12};
+    for (int d = 0; d < 2; d++) {
+        const int slot = 2 * pair + d;
+        int rc = orbt_stage(e, slot, tgt[d], M, src[d], mps[d], ams[d], nullptr);
+        if (rc) return rc;
+        FrameDev &fd = e->hfr[slot];
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) fd.sT[4 * r + c] = sRs[d][3 * r + c];
+            fd.sT[4 * r + 3] = sts[d][r];
+        }
+        fd.pfx = kf1->fx; fd.pfy = kf1->fy; fd.pcx = kf1->cx; fd.pcy = kf1->cy;
+        TR_CHK(hipMemcpy((char *)e->fr.p + sizeof(FrameDev) * (size_t)slot, &fd, sizeof(FrameDev), hipMemcpyHostToDevice));
+    }
+    return ORBX_OK;
+}
+
+int orbt_run_sim3_match_batch(orbt_engine *e, int n_pairs, float th, void *stream) {
+    if (!e || n_pairs <= 0 || 2 * n_pairs > e->nslots) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    hipStream_t st = pick(e, stream);
+    const int ns = 2 * n_pairs;
+    if (grid(e, ns, st)) return ORBX_EDEVICE;
+    const int nl = std::max(1, max_n(e, 1, ns));
+    track_sim3_match_kernel<<<dim3((nl + 255) / 256, ns), 256, 0, st>>>(make_slots(e), th, e->owner.as<int>());
+    TR_CHK(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbt_fetch_search_by_sim3(orbt_engine *e, int pair, const int32_t *kf2_mp, int32_t *matches12, int32_t *nfound) {
+    if (!e || pair < 0 || 2 * pair + 1 >= e->nslots || !kf2_mp || !matches12 || !nfound) return ORBX_EINVAL;
+    TR_CHK(hipSetDevice(e->device));
+    TR_CHK(hipDeviceSynchronize());
+    const size_t K = (size_t)e->cap_kp;
+    const int N1 = e->hfr[2 * pair].n_last, N2 = e->hfr[2 * pair + 1].n_last;
+    std::vector<int32_t> v1((size_t)N1 + 1), v2((size_t)N2 + 1);
+    if (N1) TR_CHK(hipMemcpy(v1.data(), (char *)e->owner.p + 4 * K * (size_t)(2 * pair), 4 * (size_t)N1, hipMemcpyDeviceToHost));
+    if (N2) TR_CHK(hipMemcpy(v2.data(), (char *)e->owner.p + 4 * K * (size_t)(2 * pair + 1), 4 * (size_t)N2, hipMemcpyDeviceToHost));
+    int nf = 0;
+    for (int i1 = 0; i1 < N1; i1++) {   // agreement check (ORBmatcher.cc:1706-1720)
+        const int idx2 = v1[i1];
+        if (idx2 >= 0 && idx2 < N2 && v2[idx2] == i1) {
+            matches12[i1] = kf2_mp[idx2];
+            nf++;
+        }
+    }
+    *nfound = nf;
+    return ORBX_OK;
+}
+
+int orbt_search_by_sim3(orbt_engine *e, const orbt_frame *kf1, const int32_t *kf1_mp, const orbt_frame *kf2,
+                        const int32_t *kf2_mp, const orbt_mappoints *M, float s12, const float R12[9],
+                        const float t12[3], float th, int32_t *matches12, int32_t *nfound) {
+    if (!e || !kf1 || !kf2 || !M) return ORBX_EINVAL;
+    const int need = std::max(kf1->n, kf2->n);
+    if (e->nslots < 2 || e->cap_kp < need || e->cap_mp < M->n) {
+        const int rc = orbt_reserve(e, std::max(2, e->nslots), std::max(e->cap_kp, need), std::max(e->cap_mp, M->n));
+        if (rc) return rc;
+    }
+    int rc = orbt_stage_search_by_sim3(e, 0, kf1, kf1_mp, kf2, kf2_mp, M, s12, R12, t12, matches12);
+    if (!rc) rc = orbt_run_sim3_match_batch(e, 1, th, nullptr);
+    if (!rc) rc = orbt_fetch_search_by_sim3(e, 0, kf2_mp, matches12, nfound);
+    return rc;
+}
+
 int orbt_run_fuse_batch(orbt_engine *e, int n_slots, float th, void *stream) {
     if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = pick(e, stream);
     if (grid(e, n_slots, st)) return ORBX_EDEVICE;
     const int mm = std::max(1, max_n(e, 0, n_slots));
-    track_fuse_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, e->fuse_idx.as<int>(),
+    track_fuse_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, 0, e->fuse_idx.as<int>(),
                                                                        e->fuse_dist.as<int>());
     TR_CHK(hipGetLastError());
     return ORBX_OK;

@@ -93,6 +93,13 @@ SIGNATURES = [
     ("orbt_search_by_projection_sim3", _I, [_P, _P, _P, _P, _I, _P, _P]),
     ("orbt_stage_sim3", _I, [_P, _I, _P, _P, _P, _P]),
     ("orbt_run_sim3_batch", _I, [_P, _I, _I, _P]),
+    ("orbt_fuse_sim3_candidates", _I, [_P, _P, _P, _P, _F, _P, _P]),
+    ("orbt_stage_fuse_sim3", _I, [_P, _I, _P, _P, _P]),
+    ("orbt_run_fuse_sim3_batch", _I, [_P, _I, _F, _P]),
+    ("orbt_search_by_sim3", _I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _F, _P, _P]),
+    ("orbt_stage_search_by_sim3", _I, [_P, _I, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
+    ("orbt_run_sim3_match_batch", _I, [_P, _I, _F, _P]),
+    ("orbt_fetch_search_by_sim3", _I, [_P, _I, _P, _P, _P]),
     ("orbp_create", _I, [C.POINTER(C.c_void_p)]),
     ("orbp_destroy", None, [_P]),
     ("orbp_pose_optimization", _I, [_P, _P, _P]),
@@ -609,6 +616,56 @@ class Tracker:
         matched = np.array(prob["matched"], np.int32, copy=True)[:n]
         matched[owner >= 0] = owner[owner >= 0]
         return nm, matched
+
+    def fuse_sim3_candidates(self, prob: dict, th=4.0):
+        """LoopClosing's Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) search half -> (best_idx, best_dist)."""
+        F, k1 = _orbt_frame(prob["frame"])
+        M, k2 = _orbt_map(prob["map"])
+        Scw = np.ascontiguousarray(prob["Scw"], np.float32).reshape(16)
+        bi = np.zeros(max(M.n, 1), np.int32)
+        bd = np.zeros(max(M.n, 1), np.int32)
+        _check(lib().orbt_fuse_sim3_candidates(self._h, C.byref(F), Scw.ctypes.data, C.byref(M), th, bi.ctypes.data,
+                                               bd.ctypes.data), "orbt_fuse_sim3_candidates")
+        return bi[: M.n], bd[: M.n]
+
+    @staticmethod
+    def _sim3_args(prob):
+        F1, k1 = _orbt_frame(prob["kf1"])
+        F2, k2 = _orbt_frame(prob["kf2"])
+        M, k3 = _orbt_map(prob["map"])
+        keep = {"mp1": np.ascontiguousarray(prob["kf1_mp"], np.int32), "mp2": np.ascontiguousarray(prob["kf2_mp"], np.int32),
+                "R12": np.ascontiguousarray(prob["R12"], np.float32).reshape(9),
+                "t12": np.ascontiguousarray(prob["t12"], np.float32).reshape(3), "k": (k1, k2, k3)}
+        return F1, F2, M, keep
+
+    def search_by_sim3(self, prob: dict, th=7.5):
+        """ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) -> (nFound, matches12 out)."""
+        F1, F2, M, kp = self._sim3_args(prob)
+        m12 = np.array(prob["matches12"], np.int32, copy=True)
+        nf = C.c_int32()
+        _check(lib().orbt_search_by_sim3(self._h, C.byref(F1), kp["mp1"].ctypes.data, C.byref(F2), kp["mp2"].ctypes.data,
+                                         C.byref(M), float(prob["s12"]), kp["R12"].ctypes.data, kp["t12"].ctypes.data, th,
+                                         m12.ctypes.data, C.byref(nf)), "orbt_search_by_sim3")
+        return nf.value, m12[: F1.n]
+
+    def stage_search_by_sim3(self, pair: int, prob: dict):
+        F1, F2, M, kp = self._sim3_args(prob)
+        m12 = np.ascontiguousarray(prob["matches12"], np.int32)
+        _check(lib().orbt_stage_search_by_sim3(self._h, pair, C.byref(F1), kp["mp1"].ctypes.data, C.byref(F2),
+                                               kp["mp2"].ctypes.data, C.byref(M), float(prob["s12"]),
+                                               kp["R12"].ctypes.data, kp["t12"].ctypes.data, m12.ctypes.data),
+               "orbt_stage_search_by_sim3")
+
+    def run_sim3_match_batch(self, n_pairs: int, th=7.5, stream=None):
+        _check(lib().orbt_run_sim3_match_batch(self._h, n_pairs, th, stream), "orbt_run_sim3_match_batch")
+
+    def fetch_search_by_sim3(self, pair: int, prob: dict):
+        mp2 = np.ascontiguousarray(prob["kf2_mp"], np.int32)
+        m12 = np.array(prob["matches12"], np.int32, copy=True)
+        nf = C.c_int32()
+        _check(lib().orbt_fetch_search_by_sim3(self._h, pair, mp2.ctypes.data, m12.ctypes.data, C.byref(nf)),
+               "orbt_fetch_search_by_sim3")
+        return nf.value, m12
 
     def fuse_candidates(self, prob: dict, th=3.0):
         """ORBmatcher::Fuse(pKF, vpMapPoints, th) search half; prob["frame"] is the KeyFrame."""

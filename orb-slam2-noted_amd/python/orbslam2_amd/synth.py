@@ -679,3 +679,84 @@ def newpoints_problem(seed: int = 21, n: int = 1500, n_points: int = 1400, stere
             pairs.append((i1, where2[p] if rng.random() >= wrong_frac else int(rng.integers(0, n))))
     return {"kf1": k1, "kf2": k2, "pairs": np.array(pairs, np.int32).reshape(-1, 2),
             "ratio_factor": np.float32(1.5) * np.float32(1.2)}
+
+
+# ---------------------------------------------------------------------------------------
+# Loop closing (SearchBySim3): two keyframes of a KITTI-like camera 1.5 m apart observing a
+# shared cloud, each keypoint of an observed point carries the point (GetMapPointMatches) with
+# probability 0.9, descriptors = the point's with 0..40 flipped bits, distractors fill to n;
+# (s12, R12, t12) = the relative pose of camera 2 in camera 1 (s12 = 1 unless given);
+# matches12 = ~10 % of the shared points already matched (SearchByBoW's output).
+# ---------------------------------------------------------------------------------------
+def sim3_pair_problem(seed: int = 80, n: int = 1500, n_points: int = 1300, s12: float = 1.0, W: int = 1241,
+                      H: int = 376, pre_frac: float = 0.1):
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = (np.float32(v) for v in KITTI_CAM)
+    mb = np.float32(bf / fx)
+    nl = 8
+    sf = np.ones(nl, np.float32)
+    for i in range(1, nl):
+        sf[i] = np.float32(sf[i - 1] * np.float32(1.2))
+    feat = np.array([434, 362, 302, 251, 209, 175, 145, 122], np.float64)
+    oct_p = feat / feat.sum()
+    R1 = _small_rot(rng, 2.0)
+    t1 = rng.normal(0, 0.3, 3)
+    C1 = -R1.T @ t1
+    C2 = C1 + R1.T @ np.array([rng.normal(0, 0.3), rng.normal(0, 0.05), 1.5])
+    R2 = R1 @ _small_rot(rng, 4.0)
+    t2 = -R2 @ C2
+    z = rng.uniform(3, 40, n_points)
+    u = rng.uniform(-20, W + 20, n_points)
+    v = rng.uniform(-20, H + 20, n_points)
+    Pw = (np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1) - t1) @ R1
+    octv = rng.choice(nl, size=n_points, p=oct_p)
+    dist = np.linalg.norm(Pw - C1, axis=1)
+    maxd = (dist * (1.2 ** octv) * rng.uniform(0.9, 1.12, n_points)).astype(np.float32)
+    mind = (maxd / sf[nl - 1]).astype(np.float32)
+    nrm = (Pw - C1) / dist[:, None]
+    mdesc = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    flags = np.where(rng.random(n_points) < 0.03, MP_BAD, 0).astype(np.uint8)
+
+    def keyframe(R, t):
+        Pc = Pw @ R.T + t
+        rows = []
+        for p in range(n_points):
+            if Pc[p, 2] <= 0.5 or rng.random() < 0.15:
+                continue
+            o = int(np.clip(octv[p] + rng.integers(-1, 2), 0, nl - 1))
+            s = float(sf[o])
+            x = fx * Pc[p, 0] / Pc[p, 2] + cx + rng.normal(0, 0.7 * s)
+            y = fy * Pc[p, 1] / Pc[p, 2] + cy + rng.normal(0, 0.7 * s)
+            if not (0 <= x < W and 0 <= y < H):
+                continue
+            rows.append((x, y, o, _flip_bits(rng, mdesc[p], int(rng.integers(0, 40))), p if rng.random() < 0.9 else -1))
+        while len(rows) < n:
+            o = int(rng.choice(nl, p=oct_p))
+            rows.append((rng.uniform(0, W), rng.uniform(0, H), o, rng.integers(0, 256, 32, dtype=np.uint8), -1))
+        perm = rng.permutation(len(rows))[:n]
+        keys = np.zeros(n, TRACK_KP_DTYPE)
+        for i, j in enumerate(perm):
+            x, y, o, _, _ = rows[j]
+            keys[i] = (x, y, 31 * float(sf[o]), rng.uniform(0, 360), 0, o, -1)
+        T, Ow = _pose_dict(R, t)
+        fr = {"keys_un": keys, "u_right": np.full(n, -1, np.float32),
+              "desc": np.stack([rows[j][3] for j in perm]).astype(np.uint8), "Tcw": T, "Ow": Ow, "fx": fx, "fy": fy,
+              "cx": cx, "cy": cy, "mbf": bf, "mb": mb, "min_x": 0.0, "max_x": float(W), "min_y": 0.0,
+              "max_y": float(H), "nlevels": nl, "log_scale_factor": np.float32(np.log(np.float32(1.2))),
+              "scale_factors": sf, "inv_level_sigma2": (np.float32(1) / (sf * sf)).astype(np.float32)}
+        return fr, np.array([rows[j][4] for j in perm], np.int32)
+
+    k1, mp1 = keyframe(R1, t1)
+    k2, mp2 = keyframe(R2, t2)
+    R1f, t1f, R2f, t2f = (a.astype(np.float32) for a in (R1, t1, R2, t2))
+    R12 = (R1f @ R2f.T).astype(np.float32)
+    t12 = (-R12 @ t2f + t1f).astype(np.float32)
+    in2 = set(int(p) for p in mp2 if p >= 0)
+    m12 = np.full(n, -1, np.int32)
+    for i in range(n):
+        if mp1[i] >= 0 and int(mp1[i]) in in2 and rng.random() < pre_frac:
+            m12[i] = mp1[i]
+    mp = {"Xw": Pw.astype(np.float32), "normal": nrm.astype(np.float32), "min_dist": mind, "max_dist": maxd,
+          "desc": mdesc, "flags": flags}
+    return {"kf1": k1, "kf1_mp": mp1, "kf2": k2, "kf2_mp": mp2, "map": mp, "s12": np.float32(s12), "R12": R12,
+            "t12": t12, "matches12": m12}

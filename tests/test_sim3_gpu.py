@@ -49,3 +49,39 @@ def test_sim3_batched(amd, oracle_mod):
         nm_r, m_r = oracle_mod.search_by_projection_sim3(p, 10)
         assert nm == nm_r
         np.testing.assert_array_equal(m, m_r)
+
+
+@pytest.mark.parametrize("seed,th", [(90, 4.0), (91, 4.0), (92, 8.0)])
+def test_fuse_sim3_candidates(amd, oracle_mod, seed, th):
+    """LoopClosing's Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) search half (ORBmatcher.cc:1321-1437)."""
+    prob = sim3_problem(seed, scale=1.21)
+    bi_r, bd_r = oracle_mod.fuse_sim3_candidates(prob, th)
+    bi_g, bd_g = amd.Tracker().fuse_sim3_candidates(prob, th)
+    assert (bd_r <= 50).sum() > 20
+    np.testing.assert_array_equal(bi_g, bi_r)
+    np.testing.assert_array_equal(bd_g, bd_r)
+
+
+@pytest.mark.parametrize("seed,s12,th", [(80, 1.0, 7.5), (81, 1.0, 10.0), (82, 1.03, 7.5), (83, 1.0, 4.0)])
+def test_search_by_sim3(amd, oracle_mod, seed, s12, th):
+    """ORBmatcher::SearchBySim3 (ORBmatcher.cc:1472-1723): both projections + mutual agreement."""
+    prob = synth.sim3_pair_problem(seed, s12=s12)
+    nf_r, m_r = oracle_mod.search_by_sim3(prob, th)
+    nf_g, m_g = amd.Tracker().search_by_sim3(prob, th)
+    assert nf_r > 20
+    assert nf_g == nf_r
+    np.testing.assert_array_equal(m_g, m_r)
+
+
+def test_search_by_sim3_batched(amd, oracle_mod):
+    probs = [synth.sim3_pair_problem(84 + s, n=900 + 200 * s, n_points=800 + 150 * s) for s in range(3)]
+    t = amd.Tracker()
+    t.reserve(2 * len(probs), 1500, 1200)
+    for k, p in enumerate(probs):
+        t.stage_search_by_sim3(k, p)
+    t.run_sim3_match_batch(len(probs), 7.5)
+    for k, p in enumerate(probs):
+        nf, m = t.fetch_search_by_sim3(k, p)
+        nf_r, m_r = oracle_mod.search_by_sim3(p, 7.5)
+        assert nf == nf_r
+        np.testing.assert_array_equal(m, m_r)
