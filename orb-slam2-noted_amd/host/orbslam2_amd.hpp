@@ -146,10 +146,66 @@ public:
               "orbt_search_by_projection_frame");
         return nm;
     }
+    // SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (Tracking::Relocalization):
+    // kfMp = pKF->GetMapPointMatches() as indices into M, M.flags ORBT_MP_FOUND = sAlreadyFound
+    int SearchByProjection(const orbt_frame &cur, const orbt_frame &kf, const int32_t *kfMp, const orbt_mappoints &M,
+                           float th, int ORBdist, const uint8_t *blocked, std::vector<int32_t> &owner) {
+        owner.assign(cur.n, -1);
+        int32_t nm = 0;
+        check(orbt_search_by_projection_keyframe(track(), &cur, &kf, kfMp, &M, th, ORBdist, mbCheckOrientation ? 1 : 0,
+                                                 blocked, owner.data(), &nm),
+              "orbt_search_by_projection_keyframe");
+        return nm;
+    }
+    // SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (LoopClosing): vpMatched in/out as indices
+    int SearchByProjection(const orbt_frame &kf, const float Scw[16], const orbt_mappoints &vpPoints,
+                           std::vector<int32_t> &vpMatched, int th) {
+        vpMatched.resize(kf.n, -1);
+        int32_t nm = 0;
+        check(orbt_search_by_projection_sim3(track(), &kf, Scw, &vpPoints, th, vpMatched.data(), &nm),
+              "orbt_search_by_projection_sim3");
+        return nm;
+    }
+    // SearchByBoW(pKF1, pKF2, vpMatches12) (LoopClosing::ComputeSim3)
+    int SearchByBoW(const orbb_keyframe &kf1, const orbb_keyframe &kf2, std::vector<int32_t> &vpMatches12) {
+        vpMatches12.assign(kf1.n, -1);
+        int32_t nm = 0;
+        check(orbb_search_by_bow_kf(bow(), &kf1, &kf2, mfNNratio, mbCheckOrientation ? 1 : 0, vpMatches12.data(), &nm),
+              "orbb_search_by_bow_kf");
+        return nm;
+    }
+    // SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th): vpMatches12 in/out as indices
+    int SearchBySim3(const orbt_frame &kf1, const int32_t *kf1Mp, const orbt_frame &kf2, const int32_t *kf2Mp,
+                     const orbt_mappoints &M, std::vector<int32_t> &vpMatches12, float s12, const float R12[9],
+                     const float t12[3], float th) {
+        vpMatches12.resize(kf1.n, -1);
+        int32_t nf = 0;
+        check(orbt_search_by_sim3(track(), &kf1, kf1Mp, &kf2, kf2Mp, &M, s12, R12, t12, th, vpMatches12.data(), &nf),
+              "orbt_search_by_sim3");
+        return nf;
+    }
+    // Fuse(pKF, Scw, vpPoints, th, vpReplacePoint), search half: the caller applies the updates in
+    // point order for bestDist <= TH_LOW (ORBmatcher.cc:1437-1453)
+    void FuseCandidates(const orbt_frame &kf, const float Scw[16], const orbt_mappoints &vpPoints, float th,
+                        std::vector<int32_t> &bestIdx, std::vector<int32_t> &bestDist) {
+        bestIdx.resize(vpPoints.n);
+        bestDist.resize(vpPoints.n);
+        check(orbt_fuse_sim3_candidates(track(), &kf, Scw, &vpPoints, th, bestIdx.data(), bestDist.data()),
+              "orbt_fuse_sim3_candidates");
+    }
     float mfNNratio;
     bool mbCheckOrientation;
 
 private:
+    static orbb_engine *bow() {
+        struct H {
+            orbb_engine *h = nullptr;
+            H() { check(orbb_create(&h), "orbb_create"); }
+            ~H() { orbb_destroy(h); }
+        };
+        static thread_local H h;
+        return h.h;
+    }
     static orbt_engine *track() {
         struct H {
             orbt_engine *h = nullptr;
