@@ -79,7 +79,7 @@ struct orbx_engine {
     orbamd::DevBuf d_mmap, d_cells, d_rz, d_rzr, d_pattern, d_in, d_pyr, d_blur, d_cell_cnt, d_cell_keys,
         d_qt, d_qt_nodes, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt;
     // stereo
-    orbamd::DevBuf d_st_sorted, d_st_res, d_st_u, d_st_depth, d_st_dist;
+    orbamd::DevBuf d_st_sorted, d_st_res, d_st_u, d_st_depth, d_st_dist, d_st_rows;
     // last extraction (device pointers of level-0 input)
     const uint8_t *last_in = nullptr;
     int last_pitch = 0;

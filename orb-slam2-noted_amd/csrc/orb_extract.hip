@@ -1669,7 +1669,7 @@ void orbx_destroy(orbx_engine *e) {
     orbamd::DevBuf *bufs[] = {&e->d_mmap, &e->d_cells, &e->d_rz, &e->d_rzr, &e->d_pattern, &e->d_in, &e->d_pyr, &e->d_blur,
                               &e->d_cell_cnt, &e->d_cell_keys, &e->d_qt, &e->d_qt_nodes, &e->d_sel,
                               &e->d_sel_cnt, &e->d_kps, &e->d_desc, &e->d_cnt, &e->d_st_sorted,
-                              &e->d_st_res, &e->d_st_u, &e->d_st_depth, &e->d_st_dist};
+                              &e->d_st_res, &e->d_st_u, &e->d_st_depth, &e->d_st_dist, &e->d_st_rows};
     for (auto *b : bufs) b->release();
     for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);

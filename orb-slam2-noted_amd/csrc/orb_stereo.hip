@@ -51,6 +51,8 @@ struct StereoArgs {
     int sort_cap;            // pow2 >= cap
     float mbf, mb;
     float rmax;              // 2 * max scale factor (row-band half-width bound)
+    int nrows;               // row table entries per pair (image height + 2)
+    int *rowtab;             // [pair][nrows]: first sorted right keypoint with y >= row
 };
 
 __device__ __forceinline__ const uint8_t *side_level(const ExtractGeom &g, const StereoSide &s, int img,
@@ -92,6 +94,15 @@ __global__ __launch_bounds__(256) void stereo_sort_right(StereoArgs a, unsigned 
         }
     }
     for (int i = threadIdx.x; i < n; i += 256) sorted[(long long)p * n + i] = sbuf[i];
+    // row table: the left-keypoint scan starts at rowtab[floor(y_lo)] instead of a binary search
+    for (int r = threadIdx.x; r < a.nrows; r += 256) {
+        int lo = 0, hi = nR;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (__uint_as_float((unsigned)(sbuf[mid] >> 32)) < (float)r) lo = mid + 1; else hi = mid;
+        }
+        a.rowtab[(long long)p * a.nrows + r] = lo;
+    }
 }
 
 // ---- S2: per left keypoint
@@ -122,11 +133,9 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
         // candidates: right keypoints whose band [floor(y-r), ceil(y+r)] contains `row`
         const unsigned long long *srt = sorted + (long long)p * a.sort_cap;
         const float ylo = (float)row - a.rmax - 2.0f;
-        int lo = 0, hi = nR;  // first entry with y >= ylo (uniform: scalar loads)
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (__uint_as_float((unsigned)(srt[mid] >> 32)) < ylo) lo = mid + 1; else hi = mid;
-        }
+        // first entry with y >= floor(ylo): entries below ylo fail the band test anyway
+        // (y + r < row - 2), so starting there is exact
+        const int lo = a.rowtab[(long long)p * a.nrows + min(max((int)floorf(ylo), 0), a.nrows - 1)];
         const float yhi = (float)row + a.rmax + 2.0f;
         const uint8_t *dL = a.L.desc + ((long long)imgL * a.cap + iL) * 32;
         const uint8_t *dR = a.R.desc + (long long)imgR * a.cap * 32;
@@ -293,6 +302,9 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
     for (int l = 0; l < g.nlevels; l++) smax = std::max(smax, g.scale[l]);
     a.rmax = 2.0f * smax;
     const size_t slots = (size_t)n_pairs * a.cap;
+    a.nrows = g.H + 2;
+    if (store->d_st_rows.ensure(4 * (size_t)n_pairs * a.nrows)) return ORBX_EDEVICE;
+    a.rowtab = store->d_st_rows.as<int>();
     if (store->d_st_sorted.ensure(8 * (size_t)n_pairs * sc) || store->d_st_u.ensure(4 * slots) ||
         store->d_st_depth.ensure(4 * slots) || store->d_st_dist.ensure(4 * slots))
         return ORBX_EDEVICE;
