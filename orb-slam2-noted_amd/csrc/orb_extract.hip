@@ -3,6 +3,7 @@
 // many images per launch. Behaviour follows ORBextractor::operator() of ORB-SLAM2-noted
 // (ORBextractor.cc:1543-1658) bit-for-bit; the OpenCV primitives follow SURVEY.md
 // Appendix A. See DESIGN.md for layout and rooflines.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1480,13 +1481,19 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         g.node_pow2 = np2;
         if (g.node_cap > 32767 || maxM_total >= (1 << 24)) return ORBX_EINVAL;  // int16 node ids, 24-bit positions
         const size_t node_bytes = (2 * sizeof(QNode) + sizeof(QTmp)) * g.node_cap + 16 * (size_t)np2;
-        g.qt_nodes_in_lds = node_bytes <= 48 * 1024 ? 1 : 0;
+        // Node arrays live in global scratch (L2-resident, per-workgroup slice) and the keys
+        // (2 x u32) + node index (2 x int16) per candidate take at most 28 KB of LDS with the
+        // static QShared, so five workgroups share a CU; levels with more candidates run on the
+        // global scratch. Measured at 256 KITTI pairs (tools/env_sweep.sh): nodes in LDS + 80 KB
+        // (2 per CU) 0.64 ms, nodes in LDS + keys 256 (3 per CU) 0.60 ms, nodes global + 28 KB
+        // (5 per CU) 0.52 ms, 32 KB (4 per CU) 0.57 ms, 16 KB 0.59 ms. ORBX_QT_NODES_LDS=1 /
+        // ORBX_QT_LDS_KB=<k> are tuning knobs.
+        g.qt_nodes_in_lds = 0;
+        if (const char *ev = std::getenv("ORBX_QT_NODES_LDS")) g.qt_nodes_in_lds = std::atoi(ev) != 0 && node_bytes <= 48 * 1024;
         g.qt_node_stride = (long long)((node_bytes + 15) / 16) * 4;
-        // keys (2 x u32) + node index (2 x int16) per candidate in LDS: dynamic + static
-        // (QShared) LDS stays within half of the CU's 160 KB so two workgroups share a CU (at
-        // 78 KB + QShared only one fit, and the 8 x batch workgroups ran in 8 serial waves);
-        // larger levels run on the global scratch
-        const long long kl_bytes = 80 * 1024 - (long long)sizeof(QShared) - 256 -
+        long long qt_lds = 28 * 1024;
+        if (const char *ev = std::getenv("ORBX_QT_LDS_KB")) qt_lds = std::max(16, std::min(160, std::atoi(ev))) * 1024LL;
+        const long long kl_bytes = qt_lds - (long long)sizeof(QShared) - 256 -
                                    (g.qt_nodes_in_lds ? (long long)node_bytes : 0);
         g.qt_kl = (int)std::max<long long>(256, (kl_bytes / 12) & ~63LL);
         g.ini_th = e->p.ini_th_fast;
