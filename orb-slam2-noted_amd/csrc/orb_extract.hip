@@ -1168,14 +1168,15 @@ __device__ __forceinline__ DescSlot desc_slot(const ExtractGeom &g, const uint32
 }
 
 // K5: IC_Angle (:94-141) + computeOrbDescriptor (:153-204) + keypoint assembly
-// (:1603-1657) for DESC_R consecutive output slots per wavefront, in three phases:
+// (:1603-1657) for DESC_R consecutive output slots per wavefront (3 by default: 17.9 KB of
+// LDS per workgroup keeps eight workgroups on a CU), in three phases:
 //  1. per slot: IC_Angle moments (v_dot4 over the lane's 4 row dwords, DPP wave sums) and the
 //     37 x 40 steered-BRIEF patch of the blurred level staged into the slot's LDS buffer --
 //     all global reads of the wavefront are issued before any result is needed;
 //  2. lanes 0..DESC_R-1 evaluate fastAtan2 and glibc sincosf for their slot in one pass;
 //  3. per slot: the 256 tests from LDS (pattern coordinates pre-converted to float once per
 //     wavefront), ballot bit-packing, output rows.
-#define DESC_R 4
+template <int DESC_R>
 __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint8_t *in,
                                                        const uint8_t *pyr, const uint8_t *blur,
                                                        const uint32_t *sel, const int *sel_cnt,
@@ -1607,10 +1608,20 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     prof_end(e, s, ph, "quadtree_kernel");
     const int cap = g.out_base[L];
     ph = prof_begin(e, s);
-    describe_kernel<<<dim3((cap + 4 * DESC_R - 1) / (4 * DESC_R), n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
-                                                          e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>(),
-                                                          e->d_kps.as<orbx_kp>(), e->d_desc.as<uint8_t>(),
-                                                          e->d_cnt.as<int>());
+    static const int desc_r = [] { const char *ev = std::getenv("ORBX_DESC_R"); return ev ? std::atoi(ev) : 3; }();  // tuning knob: 2 0.92 ms, 3 0.88, 4 0.97, 6 1.18 per 256 pairs
+    const dim3 dg4((cap + 15) / 16, n), dg3((cap + 11) / 12, n), dg2((cap + 7) / 8, n), dg6((cap + 23) / 24, n);
+    uint8_t *d_blur = e->d_blur.as<uint8_t>();
+    const uint32_t *d_sel = e->d_sel.as<uint32_t>();
+    const int *d_sel_cnt = e->d_sel_cnt.as<int>();
+    orbx_kp *d_kps = e->d_kps.as<orbx_kp>();
+    uint8_t *d_desc = e->d_desc.as<uint8_t>();
+    int *d_cnt = e->d_cnt.as<int>();
+    switch (desc_r) {
+    case 2: describe_kernel<2><<<dg2, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+    default: describe_kernel<3><<<dg3, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+    case 6: describe_kernel<6><<<dg6, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+    case 4: describe_kernel<4><<<dg4, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+    }
     prof_end(e, s, ph, "describe_kernel");
     HIPCHK(hipGetLastError());
     e->last_in = d_imgs;
