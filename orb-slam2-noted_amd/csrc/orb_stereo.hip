@@ -70,7 +70,10 @@ __device__ __forceinline__ int hamming32(const uint8_t *a, const uint8_t *b) {
 }
 
 // ---- S1: sort right keypoints of each pair by y (key = float bits, positive floats)
-__global__ __launch_bounds__(256) void stereo_sort_right(StereoArgs a, unsigned long long *sorted) {
+// The scan of S2 reads one 16-byte record per right keypoint in y order: {y, x (float bits),
+// minr | maxr << 16 (the row band of Frame.cc:869-888, int16 each), iR | octave << 16}, so the
+// band / octave / disparity filter needs no dependent gather of the keypoint itself.
+__global__ __launch_bounds__(256) void stereo_sort_right(ExtractGeom g, StereoArgs a, uint4 *sorted) {
     extern __shared__ unsigned long long sbuf[];
     const int p = blockIdx.x;
     const int imgR = a.R.img_base + a.R.img_step * p;
@@ -93,7 +96,15 @@ __global__ __launch_bounds__(256) void stereo_sort_right(StereoArgs a, unsigned 
             __syncthreads();
         }
     }
-    for (int i = threadIdx.x; i < n; i += 256) sorted[(long long)p * n + i] = sbuf[i];
+    for (int i = threadIdx.x; i < nR; i += 256) {
+        const int iR = (int)(sbuf[i] & 0xFFFFFFFFu);
+        const orbx_kp kp = kR[iR];
+        const float r = 2.0f * g.scale[kp.octave];
+        const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
+        sorted[(long long)p * n + i] = make_uint4(__float_as_uint(kp.y), __float_as_uint(kp.x),
+                                                  (uint32_t)(minr & 0xFFFF) | (uint32_t)maxr << 16,
+                                                  (uint32_t)iR | (uint32_t)kp.octave << 16);
+    }
     // row table: the left-keypoint scan starts at rowtab[floor(y_lo)] instead of a binary search
     for (int r = threadIdx.x; r < a.nrows; r += 256) {
         int lo = 0, hi = nR;
@@ -107,7 +118,7 @@ __global__ __launch_bounds__(256) void stereo_sort_right(StereoArgs a, unsigned 
 
 // ---- S2: per left keypoint
 __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoArgs a,
-                                                         const unsigned long long *sorted,
+                                                         const uint4 *sorted,
                                                          float *u_right, float *depth, int *sad) {
     const int lane = threadIdx.x & 63, wv = wave_id();
     int bxr, p;
@@ -131,7 +142,7 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
     int bestIdxR = 0;
     if (maxU >= 0) {
         // candidates: right keypoints whose band [floor(y-r), ceil(y+r)] contains `row`
-        const unsigned long long *srt = sorted + (long long)p * a.sort_cap;
+        const uint4 *srt = sorted + (long long)p * a.sort_cap;
         const float ylo = (float)row - a.rmax - 2.0f;
         // first entry with y >= floor(ylo): entries below ylo fail the band test anyway
         // (y + r < row - 2), so starting there is exact
@@ -144,16 +155,15 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
             const int c = base + lane;
             bool stop = false;
             if (c < nR) {
-                const unsigned long long e = srt[c];
-                const float ky = __uint_as_float((unsigned)(e >> 32));
+                const uint4 e = srt[c];
+                const float ky = __uint_as_float(e.x);
                 if (ky > yhi) stop = true;
                 else {
-                    const int iR = (int)(e & 0xFFFFFFFFu);
-                    const orbx_kp kp = kR[iR];
-                    const float r = 2.0f * g.scale[kp.octave];
-                    const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
-                    if (row >= minr && row <= maxr && kp.octave >= levelL - 1 && kp.octave <= levelL + 1 &&
-                        kp.x >= minU && kp.x <= maxU) {
+                    const int iR = (int)(e.w & 0xFFFFu), oct = (int)(e.w >> 16);
+                    const float kx = __uint_as_float(e.y);
+                    const int minr = (int)(int16_t)(e.z & 0xFFFFu), maxr = (int)(int16_t)(e.z >> 16);
+                    if (row >= minr && row <= maxr && oct >= levelL - 1 && oct <= levelL + 1 &&
+                        kx >= minU && kx <= maxU) {
                         const int dist = hamming32(dL, dR + (long long)iR * 32);
                         const unsigned key = ((unsigned)dist << 16) | (unsigned)iR;
                         best = min(best, key);
@@ -305,18 +315,18 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
     a.nrows = g.H + 2;
     if (store->d_st_rows.ensure(4 * (size_t)n_pairs * a.nrows)) return ORBX_EDEVICE;
     a.rowtab = store->d_st_rows.as<int>();
-    if (store->d_st_sorted.ensure(8 * (size_t)n_pairs * sc) || store->d_st_u.ensure(4 * slots) ||
+    if (store->d_st_sorted.ensure(16 * (size_t)n_pairs * sc) || store->d_st_u.ensure(4 * slots) ||
         store->d_st_depth.ensure(4 * slots) || store->d_st_dist.ensure(4 * slots))
         return ORBX_EDEVICE;
     float *u = store->d_st_u.as<float>(), *d = store->d_st_depth.as<float>();
     int *sad = store->d_st_dist.as<int>();
     if (sc * 8 > 64 * 1024) return ORBX_EINVAL;
     int ph = prof_begin(store, s);
-    stereo_sort_right<<<n_pairs, 256, 8 * sc, s>>>(a, store->d_st_sorted.as<unsigned long long>());
+    stereo_sort_right<<<n_pairs, 256, 8 * sc, s>>>(g, a, store->d_st_sorted.as<uint4>());
     prof_end(store, s, ph, "stereo_sort_right");
     ph = prof_begin(store, s);
     stereo_match_left<<<dim3((a.cap + 3) / 4, n_pairs), 256, 0, s>>>(
-        g, a, store->d_st_sorted.as<unsigned long long>(), u, d, sad);
+        g, a, store->d_st_sorted.as<uint4>(), u, d, sad);
     prof_end(store, s, ph, "stereo_match_left");
     ph = prof_begin(store, s);
     stereo_median_cut<<<n_pairs, 256, 4 * sc, s>>>(a, u, d, sad);
