@@ -48,7 +48,7 @@ struct ExtractGeom {
     int ini_th, min_th, resize_mode;
     int rz_col_off[ORBX_MAXL], rz_row_off[ORBX_MAXL], rz_simd_end[ORBX_MAXL];
     int blur_tiles_x[ORBX_MAXL], blur_tiles_y[ORBX_MAXL], blur_tile_base[ORBX_MAXL + 1];
-    int nms_sm_words, nms_wave_words;  // per-wavefront LDS of the cell NMS kernel (u32 words)
+    int nms_sm_words, nms_wave_words, nms_mask_off;  // per-wavefront LDS of the cell NMS kernel (u32 words)
 };
 
 struct DevBuf {

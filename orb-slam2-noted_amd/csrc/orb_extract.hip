@@ -554,13 +554,20 @@ __global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const Cell
                v > thr_score(s[-NMS_P], th) && v > thr_score(s[-NMS_P + 1], th) && v > thr_score(s[NMS_P - 1], th) &&
                v > thr_score(s[NMS_P], th) && v > thr_score(s[NMS_P + 1], th);
     };
+    // pass 1 at iniThFAST keeps its ballots; pass 2 reuses them unless the cell retries at
+    // minThFAST (:1128-1135)
+    uint32_t *kmask = sm32 + g.nms_mask_off;
     int total = 0;
     for (int b0 = 0; b0 < nl; b0 += 64) {
         int v;
         const bool k = b0 + lane < nl && keep_at(lst[b0 + lane], th_a, &v);
-        total += __popcll(__ballot(k));
+        const unsigned long long m = __ballot(k);
+        if (lane == 0) { kmask[b0 >> 5] = (uint32_t)m; kmask[(b0 >> 5) + 1] = (uint32_t)(m >> 32); }
+        total += __popcll(m);
     }
-    const int th = total > 0 ? th_a : th_b;
+    wave_lds_sync();
+    const bool retry = total == 0;
+    const int th = retry ? th_b : th_a;
     uint32_t *out = cell_keys + ((long long)b * g.ncell_total + c) * g.cell_cap;
     int written = 0;
     for (int b0 = 0; b0 < nl; b0 += 64) {
@@ -568,7 +575,12 @@ __global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const Cell
         bool k = false;
         if (b0 + lane < nl) {
             idx = lst[b0 + lane];
-            k = keep_at(idx, th, &v);
+            if (retry) {
+                k = keep_at(idx, th, &v);
+            } else {
+                k = (kmask[(b0 >> 5) + (lane >> 5)] >> (lane & 31)) & 1u;
+                v = thr_score(sm[((idx >> 8) + 1) * NMS_P + (idx & 0xFF) + 1], th);
+            }
         }
         const unsigned long long m = __ballot(k);
         const int rank = (int)lane_rank(m);
@@ -1464,7 +1476,8 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             max_det = std::max(max_det, std::max(cd.rh - 6, 0) * std::max(cd.rw - 6, 0));
         }
         g.nms_sm_words = std::max(max_rh - 4, 1) * (NMS_P / 4);
-        g.nms_wave_words = (g.nms_sm_words + (max_det + 1) / 2 + 3) & ~3;
+        g.nms_mask_off = g.nms_sm_words + (max_det + 1) / 2;   // iniThFAST keep masks, 2 words per 64 candidates
+        g.nms_wave_words = (g.nms_mask_off + 2 * ((max_det + 63) / 64) + 3) & ~3;
         g.ncell_total = g.cell_base[L];
         g.cell_cap = cell_cap;
         g.out_base[0] = 0;
