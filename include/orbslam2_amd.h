@@ -79,6 +79,12 @@ int orbx_reserve(orbx_engine *e, int w, int h, int max_images);
  * (hipStream_t; NULL = the engine's stream). Results stay on the device. */
 int orbx_extract_batch_device(orbx_engine *e, const uint8_t *d_imgs, int n_images, int w,
                               int h, int pitch, size_t image_stride, void *stream);
+/* The same in two halves on one stream, so that two engines can interleave their batches:
+ * phase 1 = pyramid + FAST strength map + blur (the VALU-bound half), phase 2 = cell NMS,
+ * quadtree, orientation + descriptors (latency-bound); phase 2 must follow phase 1 of the same
+ * d_imgs / n_images; phase 3 = both (= orbx_extract_batch_device). */
+int orbx_extract_batch_device_phase(orbx_engine *e, const uint8_t *d_imgs, int n_images, int w,
+                                    int h, int pitch, size_t image_stride, void *stream, int phase);
 /* Device pointers of the last batch: counts[n_images], kps[n_images][cap],
  * desc[n_images][cap][32]. */
 int orbx_batch_results(orbx_engine *e, const int **d_counts, const orbx_kp **d_kps,
@@ -100,6 +106,30 @@ int orbm_stereo_match(orbx_engine *left, orbx_engine *right, float mbf, float mb
 /* Batched stereo over the engine's last device batch: image 2p = left, 2p+1 = right of
  * pair p. Results stay on device: u_right / depth [n_pairs][cap]. */
 int orbm_stereo_match_batch_device(orbx_engine *e, int n_pairs, float mbf, float mb, void *stream);
+
+/* -------- stereo batch pipeline (Frame::Frame stereo constructor, Frame.cc:144-160, over a batch
+ * of pairs) -------- */
+typedef struct orbx_pipeline orbx_pipeline;
+/* n_engines extractors (<= 0: 3), one HIP stream each. A batch is split into n_engines chunks of
+ * consecutive pairs; each chunk runs extraction phase 1, phase 2 and ComputeStereoMatches on its
+ * engine, and the chunks' phase 1 run in turn so one chunk's VALU-bound pyramid / FAST / blur
+ * overlaps the other chunks' latency-bound NMS / quadtree / descriptors / stereo. Results equal
+ * one engine over the whole batch. */
+int orbx_pipeline_create(const orbx_params *p, int n_engines, orbx_pipeline **out);
+void orbx_pipeline_destroy(orbx_pipeline *pl);
+int orbx_pipeline_engines(orbx_pipeline *pl);
+int orbx_pipeline_reserve(orbx_pipeline *pl, int w, int h, int max_pairs);
+/* d_imgs: 2 * n_pairs device images, left / right interleaved (image i at d_imgs + i * image_stride).
+ * Starts after the work queued on `stream` (hipStream_t, NULL = legacy default stream) and returns
+ * without making `stream` wait for it, so consecutive batches overlap; order consumers (or reuse
+ * of d_imgs) with orbx_pipeline_join or a device synchronisation. */
+int orbx_pipeline_stereo_batch(orbx_pipeline *pl, const uint8_t *d_imgs, int n_pairs, int w, int h,
+                               int pitch, size_t image_stride, float mbf, float mb, void *stream);
+/* Engine i and its chunk [first_pair, first_pair + n_pairs) of the last batch: its results are
+ * read with orbx_batch_* (images 2p, 2p + 1 of the chunk) and orbm_stereo_*. */
+int orbx_pipeline_chunk(orbx_pipeline *pl, int i, orbx_engine **e, int *first_pair, int *n_pairs);
+/* Make `stream` wait for every chunk of the last batch. */
+int orbx_pipeline_join(orbx_pipeline *pl, void *stream);
 int orbm_stereo_results(orbx_engine *e, const float **d_u_right, const float **d_depth);
 int orbm_stereo_fetch(orbx_engine *e, int pair, float *u_right, float *depth, int cap);
 

@@ -82,6 +82,8 @@ struct orbx_engine {
     orbamd::DevBuf d_st_sorted, d_st_res, d_st_u, d_st_depth, d_st_dist, d_st_rows;
     // last extraction (device pointers of level-0 input)
     const uint8_t *last_in = nullptr;
+    const uint8_t *pending_in = nullptr;   // phase-1 batch awaiting phase 2
+    int pending_n = 0;
     int last_pitch = 0;
     long long last_stride = 0;
     int last_n = 0;
@@ -101,5 +103,5 @@ int prof_begin(orbx_engine *e, hipStream_t s);
 void prof_end(orbx_engine *e, hipStream_t s, int h, const char *name);
 int engine_reserve(orbx_engine *e, int w, int h, int max_images);
 int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitch,
-                          long long stride, hipStream_t s);
+                          long long stride, hipStream_t s, int phase);
 }  // namespace orbamd

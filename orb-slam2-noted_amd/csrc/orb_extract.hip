@@ -1584,13 +1584,15 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
 }
 
 int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitch,
-                          long long stride, hipStream_t s) {
+                          long long stride, hipStream_t s, int phase) {
     ExtractGeom g = e->g;
     g.nimg = n;
     g.in_pitch = pitch;
     g.in_stride = stride;
     const int L = g.nlevels;
     uint8_t *pyr = e->d_pyr.as<uint8_t>();
+    const int cap = g.out_base[L];
+    if (phase & 1) {
     int ph = prof_begin(e, s);
     for (int l = 1; l < L; l++) {
         const int tiles_x = (g.lw[l] + RZ_TW - 1) / RZ_TW, tiles_y = (g.lh[l] + RZ_TH - 1) / RZ_TH;
@@ -1608,7 +1610,9 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     fast_blur_kernel<<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
                                                                    e->d_mmap.as<uint8_t>());
     prof_end(e, s, ph, "fast_blur_kernel");
-    ph = prof_begin(e, s);
+    }
+    if (phase & 2) {
+    int ph = prof_begin(e, s);
     fast_nms_kernel<<<dim3((g.ncell_total + 3) / 4, n), 256, 16 * (size_t)g.nms_wave_words, s>>>(g, e->d_cells.as<CellDesc>(), e->d_mmap.as<uint8_t>(),
                                                         e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
     prof_end(e, s, ph, "fast_nms_kernel");
@@ -1619,7 +1623,6 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
         g, e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>(), e->d_qt.as<uint32_t>(),
         e->d_qt_nodes.as<unsigned char>(), e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>());
     prof_end(e, s, ph, "quadtree_kernel");
-    const int cap = g.out_base[L];
     ph = prof_begin(e, s);
     static const int desc_r = [] { const char *ev = std::getenv("ORBX_DESC_R"); return ev ? std::atoi(ev) : 3; }();  // tuning knob: 2 0.92 ms, 3 0.88, 4 0.97, 6 1.18 per 256 pairs
     const dim3 dg4((cap + 15) / 16, n), dg3((cap + 11) / 12, n), dg2((cap + 7) / 8, n), dg6((cap + 23) / 24, n);
@@ -1636,6 +1639,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     case 4: describe_kernel<4><<<dg4, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
     }
     prof_end(e, s, ph, "describe_kernel");
+    }
     HIPCHK(hipGetLastError());
     e->last_in = d_imgs;
     e->last_pitch = pitch;
@@ -1773,11 +1777,20 @@ int orbx_reserve(orbx_engine *e, int w, int h, int max_images) {
 
 int orbx_extract_batch_device(orbx_engine *e, const uint8_t *d_imgs, int n_images, int w, int h,
                               int pitch, size_t image_stride, void *stream) {
-    if (!e || !d_imgs || n_images <= 0 || pitch < w) return ORBX_EINVAL;
+    return orbx_extract_batch_device_phase(e, d_imgs, n_images, w, h, pitch, image_stride, stream, 3);
+}
+
+int orbx_extract_batch_device_phase(orbx_engine *e, const uint8_t *d_imgs, int n_images, int w, int h,
+                                    int pitch, size_t image_stride, void *stream, int phase) {
+    if (!e || !d_imgs || n_images <= 0 || pitch < w || phase < 1 || phase > 3) return ORBX_EINVAL;
+    if (phase == 2 && (e->pending_in != d_imgs || e->pending_n != n_images)) return ORBX_ESTATE;
     int rc = orbamd::engine_reserve(e, w, h, std::max(n_images, e->max_images));
     if (rc) return rc;
-    return orbamd::engine_extract_device(e, d_imgs, n_images, pitch, (long long)image_stride,
-                                         stream ? (hipStream_t)stream : e->stream);
+    rc = orbamd::engine_extract_device(e, d_imgs, n_images, pitch, (long long)image_stride,
+                                       stream ? (hipStream_t)stream : e->stream, phase);
+    e->pending_in = phase == 1 ? d_imgs : nullptr;
+    e->pending_n = phase == 1 ? n_images : 0;
+    return rc;
 }
 
 int orbx_batch_results(orbx_engine *e, const int **d_counts, const orbx_kp **d_kps,
@@ -1819,7 +1832,7 @@ int orbx_extract(orbx_engine *e, const uint8_t *img, int w, int h, int stride, o
     if (rc) return rc;
     if (e->d_in.ensure((size_t)w * h)) return ORBX_EDEVICE;
     HIPCHK(hipMemcpy2DAsync(e->d_in.p, w, img, stride, w, h, hipMemcpyHostToDevice, e->stream));
-    rc = orbamd::engine_extract_device(e, e->d_in.as<uint8_t>(), 1, w, (long long)w * h, e->stream);
+    rc = orbamd::engine_extract_device(e, e->d_in.as<uint8_t>(), 1, w, (long long)w * h, e->stream, 3);
     if (rc) return rc;
     return orbx_batch_fetch(e, 0, kps, desc, cap, n);
 }

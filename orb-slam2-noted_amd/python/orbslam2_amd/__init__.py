@@ -54,6 +54,14 @@ SIGNATURES = [
     ("orbx_pyramid_level", _I, [_P, _I, _I, _P, _P, _P]),
     ("orbx_reserve", _I, [_P, _I, _I, _I]),
     ("orbx_extract_batch_device", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _P]),
+    ("orbx_extract_batch_device_phase", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _P, _I]),
+    ("orbx_pipeline_create", _I, [_P, _I, _P]),
+    ("orbx_pipeline_destroy", None, [_P]),
+    ("orbx_pipeline_engines", _I, [_P]),
+    ("orbx_pipeline_reserve", _I, [_P, _I, _I, _I]),
+    ("orbx_pipeline_stereo_batch", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _F, _F, _P]),
+    ("orbx_pipeline_chunk", _I, [_P, _I, _P, _P, _P]),
+    ("orbx_pipeline_join", _I, [_P, _P]),
     ("orbx_batch_results", _I, [_P, _P, _P, _P, _P]),
     ("orbx_batch_fetch", _I, [_P, _I, _P, _P, _I, _P]),
     ("orbx_stream", _P, [_P]),
@@ -204,6 +212,8 @@ class ORBextractor:
         self.nlevels = nlevels
 
     def close(self):
+        if getattr(self, "_view", False):   # engine owned by a StereoPipeline
+            return
         if getattr(self, "_h", None) and self._h.value:
             lib().orbx_destroy(self._h)
             self._h = C.c_void_p()
@@ -276,6 +286,13 @@ class BatchExtractor(ORBextractor):
         _check(lib().orbx_extract_batch_device(self._h, C.c_void_p(d_ptr), n_images, w, h, pitch,
                                                image_stride, C.c_void_p(stream or 0)),
                "orbx_extract_batch_device")
+
+    def extract_device_phase(self, d_ptr: int, n_images: int, w: int, h: int, pitch: int,
+                             image_stride: int, phase: int, stream: int | None = None):
+        """Phase 1 (pyramid + FAST map + blur) or 2 (NMS, quadtree, descriptors) of extract_device."""
+        _check(lib().orbx_extract_batch_device_phase(self._h, C.c_void_p(d_ptr), n_images, w, h, pitch,
+                                                     image_stride, C.c_void_p(stream or 0), phase),
+               "orbx_extract_batch_device_phase")
 
     def stream(self) -> int:
         return lib().orbx_stream(self._h) or 0
@@ -352,6 +369,84 @@ class BatchExtractor(ORBextractor):
         return u, d
 
 
+class StereoPipeline:
+    """Batched stereo Frame construction (extract L + R, ComputeStereoMatches) over k engines on
+    k HIP streams, their pyramid / FAST / blur phases in turn (orbx_pipeline_*, orb_pipeline.hip).
+    Pair p of the last batch lives on engine chunk_of(p)."""
+
+    def __init__(self, nfeatures: int = 2000, scaleFactor: float = 1.2, nlevels: int = 8,
+                 iniThFAST: int = 20, minThFAST: int = 7, n_engines: int = 3, resize_mode: int = 0):
+        self._h = C.c_void_p()
+        p = OrbxParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_mode)
+        _check(lib().orbx_pipeline_create(C.byref(p), n_engines, C.byref(self._h)), "orbx_pipeline_create")
+        self.nfeatures, self.nlevels = nfeatures, nlevels
+        self.engines = []
+        for i in range(lib().orbx_pipeline_engines(self._h)):
+            e = C.c_void_p()
+            _check(lib().orbx_pipeline_chunk(self._h, i, C.byref(e), None, None), "orbx_pipeline_chunk")
+            v = BatchExtractor.__new__(BatchExtractor)
+            v._h, v._view, v.nfeatures, v.nlevels = e, True, nfeatures, nlevels
+            self.engines.append(v)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().orbx_pipeline_destroy(self._h)
+            self._h = C.c_void_p()
+            self.engines = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, w: int, h: int, max_pairs: int):
+        _check(lib().orbx_pipeline_reserve(self._h, w, h, max_pairs), "orbx_pipeline_reserve")
+
+    def stereo_batch(self, d_ptr: int, n_pairs: int, w: int, h: int, pitch: int, image_stride: int,
+                     mbf: float, mb: float, stream: int | None = None):
+        _check(lib().orbx_pipeline_stereo_batch(self._h, C.c_void_p(d_ptr), n_pairs, w, h, pitch, image_stride,
+                                                mbf, mb, C.c_void_p(stream or 0)), "orbx_pipeline_stereo_batch")
+
+    def join(self, stream: int | None = None):
+        """Make `stream` (default: the legacy default stream) wait for the last batch."""
+        _check(lib().orbx_pipeline_join(self._h, C.c_void_p(stream or 0)), "orbx_pipeline_join")
+
+    def chunk(self, i: int):
+        first, n = C.c_int(), C.c_int()
+        _check(lib().orbx_pipeline_chunk(self._h, i, None, C.byref(first), C.byref(n)), "orbx_pipeline_chunk")
+        return self.engines[i], first.value, n.value
+
+    def chunk_of(self, pair: int):
+        for i in range(len(self.engines)):
+            ex, first, n = self.chunk(i)
+            if first <= pair < first + n:
+                return ex, pair - first
+        raise IndexError(pair)
+
+    def fetch(self, pair: int):
+        """(left keypoints, left descriptors, right keypoints, right descriptors) of a pair."""
+        ex, p = self.chunk_of(pair)
+        return (*ex.fetch(2 * p), *ex.fetch(2 * p + 1))
+
+    def stereo_fetch(self, pair: int):
+        ex, p = self.chunk_of(pair)
+        return ex.stereo_fetch(p)
+
+    def profile(self, enable: bool):
+        for ex in self.engines:
+            ex.profile(enable)
+
+    def profile_read(self) -> dict:
+        """{kernel name: (total ms, launches)} summed over the engines."""
+        out = {}
+        for ex in self.engines:
+            for k, (ms, n) in ex.profile_read().items():
+                a, b = out.get(k, (0.0, 0))
+                out[k] = (a + ms, b + n)
+        return out
+
+
 def compute_stereo_from_rgbd(ex: ORBextractor, n: int, depth: np.ndarray, K, dist, mbf: float):
     """UndistortKeyPoints + ComputeStereoFromRGBD for the extractor's last image ->
     (mvKeysUn, mvuRight, mvDepth)."""
@@ -426,6 +521,8 @@ class LocalBundleAdjustment:
         _check(lib().lba_create(C.byref(self._h)), "lba_create")
 
     def close(self):
+        if getattr(self, "_view", False):   # engine owned by a StereoPipeline
+            return
         if getattr(self, "_h", None) and self._h.value:
             lib().lba_destroy(self._h)
             self._h = C.c_void_p()

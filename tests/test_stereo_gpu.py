@@ -67,3 +67,33 @@ def test_hamming_best2(amd, oracle_mod):
     np.testing.assert_array_equal(bi, ri)
     np.testing.assert_array_equal(bd, rd)
     np.testing.assert_array_equal(sd, rs)
+
+
+@pytest.mark.parametrize("P,k", [(5, 3), (2, 3), (4, 2)])
+def test_stereo_pipeline(amd, oracle_mod, P, k):
+    """orbx_pipeline_*: k engines on k streams, chunks of consecutive pairs (uneven and empty
+    chunks included), two batches back to back (the second's phase 1 waits on the first's),
+    every pair bit-exact with the oracle's extraction + ComputeStereoMatches."""
+    import torch
+    h, w = 376, 1241
+    pairs = [synth.stereo_pair(h, w, 20 + p) for p in range(P)]
+    imgs = np.stack([im for pr in pairs for im in pr])
+    dev = torch.from_numpy(imgs).cuda()
+    dev2 = torch.flip(dev, dims=[0]).contiguous()   # second batch: pairs reversed, L / R swapped
+    pl = amd.StereoPipeline(2000, n_engines=k)
+    pl.reserve(w, h, P)
+    mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    torch.cuda.synchronize()
+    pl.stereo_batch(dev2.data_ptr(), P, w, h, w, h * w, KITTI_BF, mb)
+    pl.stereo_batch(dev.data_ptr(), P, w, h, w, h * w, KITTI_BF, mb)
+    torch.cuda.synchronize()
+    assert sum(pl.chunk(i)[2] for i in range(k)) == P
+    for p in range(P):
+        kL, u_ref, d_ref, _ = _stereo_ref(oracle_mod, *pairs[p], 2000)
+        gkL, gdL, gkR, gdR = pl.fetch(p)
+        assert gkL.tobytes() == kL.tobytes()
+        u, d = pl.stereo_fetch(p)
+        n = len(kL)
+        np.testing.assert_array_equal(u[:n].view(np.uint32), u_ref.view(np.uint32))
+        np.testing.assert_array_equal(d[:n].view(np.uint32), d_ref.view(np.uint32))
+    pl.close()
