@@ -128,6 +128,18 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
             d[k] = c[k].y >> 16;              // sx1 - sx (0 at the right border)
             coef[k] = (uint32_t)(c[k].x >> 16) | (uint32_t)(c[k].y & 0xFFFF) << 16;
         }
+        // the lane's 4 outputs read source bytes sxa + o .. sxa + o + d; when they all fall in
+        // an 8-byte window (scale <= ~1.75, every lane at 1.2), two v_alignbyte per source row
+        // build the window and each output is one v_perm with a lane-constant selector + one
+        // v_dot2 (else the per-row selector path below)
+        uint32_t sel[4];
+        int span = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            sel[k] = 0x0c000c00u | (uint32_t)(o[k] + d[k]) << 16 | (uint32_t)o[k];
+            span = max(span, o[k] + d[k]);
+        }
+        const bool win8 = span <= 7;
         // all loads of a thread's source rows are issued before any use (6 rows x 3 dwords
         // in flight; the level-1 pass streams the input image from HBM)
         for (int jb = threadIdx.x >> 5; jb < nsr; jb += 8 * RZ_HJ) {
@@ -148,6 +160,14 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
                 const int j = jb + 8 * u;
                 if (j >= nsr) break;
                 uint32_t hv[4];
+                if (win8) {
+                    const uint32_t W0 = __builtin_amdgcn_alignbyte(D[u][1], D[u][0], (uint32_t)mis[u]);
+                    const uint32_t W1 = __builtin_amdgcn_alignbyte(D[u][2], D[u][1], (uint32_t)mis[u]);
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        hv[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(W1, W0, sel[k])),
+                                                       __builtin_bit_cast(u16x2, coef[k]), 0u, false);
+                } else
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const int q = o[k] + mis[u];   // byte offset of p[sx] in D0..D2 (<= 10)
