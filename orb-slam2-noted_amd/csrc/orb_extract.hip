@@ -193,7 +193,8 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
         uint32_t out = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            uint32_t v = min((S0[k] * (uint32_t)ry.z + S1[k] * (uint32_t)ry.w + (1u << 21)) >> 22, 255u);
+            // S < 2^20 (Q11 sums of bytes), weights <= 2^11: full-rate 24-bit multiplies
+            uint32_t v = min((__umul24(S0[k], (uint32_t)ry.z) + __umul24(S1[k], (uint32_t)ry.w) + (1u << 21)) >> 22, 255u);
             if (SIMD && dx0 + k < g.rz_simd_end[l]) v = resize_px_simd((int)S0[k], (int)S1[k], ry);
             out |= v << (8 * k);
         }
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const Cell
         const int rpi = 64 / qw, ro = lane / qw, jq = lane - ro * qw;
         if (ro < rpi && ndet > 0)
             for (int rr = ro; rr < dh + 2; rr += rpi)
-                sm32[rr * (NMS_P / 4) + jq] = load_u32_unaligned(base + (long long)rr * bp + 4 * jq);
+                sm32[rr * (NMS_P / 4) + jq] = load_u32_unaligned(base + __mul24(rr, bp) + 4 * jq);   // rr < 256: 24-bit multiply
     }
     wave_lds_sync();
     // zero the one-pixel frame: neighbours outside the detection region score 0
@@ -1246,7 +1247,7 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
             if (j < 31 * 8) {
                 const int v = (j >> 3) - 15, w = j & 7;
                 const uint2 wt = c_icw[(v < 0 ? -v : v) * 8 + w];
-                const uint32_t P = load_u32_unaligned(rowc + v * pitch + 4 * w);
+                const uint32_t P = load_u32_unaligned(rowc + __mul24(v, pitch) + 4 * w);   // |v| <= 15: 24-bit multiply
                 const int su = (int)__builtin_amdgcn_udot4(P, wt.x, 0u, false);
                 const int sm = (int)__builtin_amdgcn_udot4(P, wt.y, 0u, false);
                 m10 += su - 16 * sm;
@@ -1272,7 +1273,7 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
                 const int idx = lane + 64 * k;
                 if (idx < 370) {
                     const int rr = idx / 10, q = idx - rr * 10;
-                    pt[idx] = src[rr * bw4 + q];
+                    pt[idx] = src[__mul24(rr, bw4) + q];
                 }
             }
         } else {
@@ -1323,8 +1324,9 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
         unsigned long long words[4];
 #pragma unroll
         for (int w = 0; w < 4; w++) {
-            const int t0 = pc[cv_round_f(PX0[w] * bs + PY0[w] * a) * 40 + cv_round_f(PX0[w] * a - PY0[w] * bs)];
-            const int t1 = pc[cv_round_f(PX1[w] * bs + PY1[w] * a) * 40 + cv_round_f(PX1[w] * a - PY1[w] * bs)];
+            // rotated offsets are within +-18: full-rate 24-bit multiplies for the row stride
+            const int t0 = pc[__mul24(cv_round_f(PX0[w] * bs + PY0[w] * a), 40) + cv_round_f(PX0[w] * a - PY0[w] * bs)];
+            const int t1 = pc[__mul24(cv_round_f(PX1[w] * bs + PY1[w] * a), 40) + cv_round_f(PX1[w] * a - PY1[w] * bs)];
             words[w] = __ballot(t0 < t1);
         }
         if (lane == 0) {
