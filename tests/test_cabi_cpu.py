@@ -35,3 +35,20 @@ def test_python_binding_covers_abi():
     import orbslam2_amd
     bound = {name for name, _, _ in orbslam2_amd.SIGNATURES}
     assert set(declared_symbols()) <= bound, set(declared_symbols()) - bound
+
+
+def test_pipeline_argument_errors_without_gpu():
+    """orbx_pipeline_* reject bad arguments before touching the device (ORBX_EINVAL)."""
+    import orbslam2_amd as amd
+    lib = amd.lib()
+    einval = lib.orbx_pipeline_create(None, 3, None)
+    assert einval != 0
+    p = amd.OrbxParams(2000, 1.2, 8, 20, 7, 0)
+    out = ctypes.c_void_p()
+    assert lib.orbx_pipeline_create(ctypes.byref(p), 17, ctypes.byref(out)) == einval and not out.value
+    assert lib.orbx_pipeline_stereo_batch(None, None, 1, 1241, 376, 1241, 1241 * 376, 386.1448, 0.537, None) == einval
+    assert lib.orbx_pipeline_reserve(None, 1241, 376, 8) == einval
+    assert lib.orbx_pipeline_join(None, None) == einval
+    assert lib.orbx_pipeline_chunk(None, 0, None, None, None) == einval
+    assert lib.orbx_pipeline_engines(None) == 0
+    assert lib.orbx_extract_batch_device_phase(None, None, 2, 1241, 376, 1241, 1241 * 376, None, 1) == einval
