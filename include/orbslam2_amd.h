@@ -59,7 +59,9 @@ int orbx_levels(const orbx_engine *e, int *nlevels, float *scale, float *inv_sca
                 float *sigma2, float *inv_sigma2, int *features_per_level);
 
 /* ORBextractor::operator()(image, mask, keypoints, descriptors) (ORBextractor.h:107,
- * ORBextractor.cc:1543-1658) on a host u8 image (row pitch `stride` bytes). Writes up to
+ * ORBextractor.cc:1543-1658) on a host u8 image (row pitch `stride` bytes). Thread-safe across
+ * engines: each engine uploads, runs and downloads on its own stream and waits for nothing
+ * else, so the left / right extractors of Frame.cc:144-153 run concurrently from two threads. Writes up to
  * `cap` keypoints (level-major, quadtree list order) and N x 32 descriptor bytes; *n gets
  * the count. Empty image (w or h == 0) -> *n = 0 (reference returns untouched). The mask is
  * ignored, as in the reference. The pyramid stays resident on the device for
@@ -75,8 +77,12 @@ int orbx_pyramid_level(orbx_engine *e, int image, int level, uint8_t *dst, int *
 /* Size device buffers for up to max_images images of w x h. */
 int orbx_reserve(orbx_engine *e, int w, int h, int max_images);
 /* Extract n_images frames already resident in device memory (u8, image i at
- * d_imgs + i * image_stride, rows `pitch` bytes apart). Asynchronous on `stream`
- * (hipStream_t; NULL = the engine's stream). Results stay on the device. */
+ * d_imgs + i * image_stride, rows `pitch` bytes apart; image_stride >= pitch*(h-1)+w when
+ * n_images > 1). Input tail: the 16 bytes after the last pixel of the last image must be
+ * readable device memory (the level-0 staging and level-1 resize read aligned dwords; the
+ * extra bytes never reach a result). Asynchronous on `stream` (hipStream_t; NULL = the
+ * engine's stream), ordered after the engine's previous work; results stay on the device and
+ * orbx_batch_fetch waits for this engine's work only. */
 int orbx_extract_batch_device(orbx_engine *e, const uint8_t *d_imgs, int n_images, int w,
                               int h, int pitch, size_t image_stride, void *stream);
 /* The same in two halves on one stream, so that two engines can interleave their batches:
@@ -89,7 +95,8 @@ int orbx_extract_batch_device_phase(orbx_engine *e, const uint8_t *d_imgs, int n
  * desc[n_images][cap][32]. */
 int orbx_batch_results(orbx_engine *e, const int **d_counts, const orbx_kp **d_kps,
                        const uint8_t **d_desc, int *cap);
-/* Copy one image's results of the last batch to host. */
+/* Copy one image's results of the last batch to host. Waits for this engine's last launch
+ * (an event), never for the device: engines on other threads keep running. */
 int orbx_batch_fetch(orbx_engine *e, int image, orbx_kp *kps, uint8_t *desc, int cap, int *n);
 /* The engine's HIP stream (hipStream_t). */
 void *orbx_stream(orbx_engine *e);
@@ -139,6 +146,53 @@ int orbm_stereo_fetch(orbx_engine *e, int pair, float *u_right, float *depth, in
  * matchers). Host pointers. */
 int orbm_hamming_best2(const uint8_t *q, int nq, const uint8_t *db, int ndb, int *best_idx,
                        int *best_d, int *second_d);
+
+/* -------- ORBmatcher instance: ORBmatcher(float nnratio = 0.6, bool checkOri = true)
+ * (include/ORBmatcher.h:57, ORBmatcher.cc:61). Holds mfNNratio / mbCheckOrientation, a private
+ * HIP stream and grow-only device buffers; any number of matchers may be used from different
+ * host threads concurrently (each waits only for its own work). -------- */
+typedef struct orbm_matcher orbm_matcher;
+int orbm_create(float nnratio, int check_ori, orbm_matcher **out);
+void orbm_destroy(orbm_matcher *m);
+
+/* The scan core of every ORBmatcher search (ORBmatcher.cc:639-668 and the same loop in the
+ * SearchByProjection / SearchByBoW overloads) over caller-built candidate lists: query i's
+ * candidates are cand_idx[cand_off[i] .. cand_off[i+1]) into db (CSR, cand_off[0] == 0, indices in
+ * [0, ndb)). best_idx = the candidate (db index) of the FIRST minimum distance in list order,
+ * best_d its distance, second_d the minimum over the other candidates (INT_MAX when there are
+ * none; best_idx -1 / best_d INT_MAX for an empty list). cand_off == NULL scans all of db in index
+ * order (= orbm_hamming_best2). Host pointers. SURVEY.md §8b orbm_hamming_best2. */
+int orbm_hamming_best2_cand(orbm_matcher *m, const uint8_t *q, int nq, const uint8_t *db, int ndb,
+                            const int32_t *cand_off, const int32_t *cand_idx, int32_t *best_idx,
+                            int32_t *best_d, int32_t *second_d);
+/* Device-pointer form, enqueued on `stream` (NULL = the matcher's stream); outputs stay on device. */
+int orbm_hamming_best2_cand_device(orbm_matcher *m, const uint8_t *d_q, int nq, const uint8_t *d_db,
+                                   int ndb, const int32_t *d_cand_off, const int32_t *d_cand_idx,
+                                   int32_t *d_best_idx, int32_t *d_best_d, int32_t *d_second_d,
+                                   void *stream);
+
+/* The Frame members SearchForInitialization reads (include/Frame.h): N, mvKeysUn, mDescriptors
+ * and the image bounds of the grid (static mnMinX / mnMaxX / mnMinY / mnMaxY, computed once by
+ * Frame::ComputeImageBounds, Frame.cc:780-830; the grid cell inverses follow from them as in
+ * Frame.cc:183-184). Host pointers. */
+typedef struct {
+    int32_t n;
+    const orbx_kp *keys_un;   /* n undistorted keypoints, extractor order */
+    const uint8_t *desc;      /* n x 32 */
+    float min_x, max_x, min_y, max_y;
+} orbm_frame;
+
+/* ORBmatcher::SearchForInitialization(Frame &F1, Frame &F2, vector<cv::Point2f> &vbPrevMatched,
+ * vector<int> &vnMatches12, int windowSize) (ORBmatcher.h:169, ORBmatcher.cc:580-748) with the
+ * matcher's nnratio / checkOri, on two independently built host frames.
+ * prev_matched: F1->n (x, y) pairs, in/out -- read as the search-window centre of each octave-0
+ * F1 keypoint (:627) and overwritten with the matched F2 keypoint position (:742-745), so the
+ * caller carries it from call to call as Tracking::MonocularInitialization does
+ * (Tracking.cc:893-897, 929-933). matches12: F1->n entries (vnMatches12, -1 = none). *nmatches =
+ * the return value of the reference. F1->n, F2->n <= 4096. Greedy order kept exactly. */
+int orbm_search_for_initialization(orbm_matcher *m, const orbm_frame *F1, const orbm_frame *F2,
+                                   float *prev_matched, int32_t *matches12, int window,
+                                   int32_t *nmatches);
 
 /* -------- RGB-D frame + frame-to-frame matching (C3) -------- */
 

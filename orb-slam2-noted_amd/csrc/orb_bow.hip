@@ -218,6 +218,8 @@ using namespace orbbow;
 struct orbv_vocab {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;          // end of the last run (fetch waits on it only)
+    hipStream_t done_stream = nullptr;
     int k = 0, L = 0, scoring = 0, weighting = 0, n_nodes = 0, n_words = 0;
     DevBuf child_start, child_node, child_desc, word_id, weight;
     // batch buffers
@@ -251,6 +253,7 @@ int ensure_batch(orbv_vocab *v, int frames, int cap) {
 
 int launch(orbv_vocab *v, const uint8_t *d_desc, const int32_t *d_counts, int n_frames, int cap, size_t stride,
            int levelsup, hipStream_t st) {
+    if (order_after_done(v, st) != hipSuccess) return -1;
     int sc = 256;
     while (sc < cap) sc <<= 1;
     bow_descend_kernel<<<dim3((cap + 255) / 256, n_frames), 256, 0, st>>>(vdev(v), d_desc, d_counts, cap, (long long)stride,
@@ -263,7 +266,8 @@ int launch(orbv_vocab *v, const uint8_t *d_desc, const int32_t *d_counts, int n_
     bow_aggregate_kernel<<<n_frames, 256, (8 + 8 + 4) * (size_t)sc, st>>>(vdev(v), d_counts, cap, sc, v->cap,
                                                                                  v->word.as<int>(), v->wt.as<double>(),
                                                                                  v->nid.as<int>(), O);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    if (hipGetLastError() != hipSuccess) return -1;
+    return mark_done(v, st) == hipSuccess ? 0 : -1;
 }
 
 }  // namespace
@@ -295,7 +299,8 @@ int orbv_create(int k, int L, int scoring, int weighting, int n_nodes, const int
         w[i] = i == 0 ? 0.0 : weight[i];
     }
     orbv_vocab *v = new orbv_vocab();
-    if (hipGetDevice(&v->device) != hipSuccess || hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipGetDevice(&v->device) != hipSuccess || hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess ||
+        !(v->done = make_done_event())) {
         delete v;
         return ORBX_EDEVICE;
     }
@@ -346,6 +351,7 @@ void orbv_destroy(orbv_vocab *v) {
     if (!v) return;
     (void)hipSetDevice(v->device);
     if (v->stream) { (void)hipStreamSynchronize(v->stream); (void)hipStreamDestroy(v->stream); }
+    if (v->done) { (void)hipEventSynchronize(v->done); (void)hipEventDestroy(v->done); }
     DevBuf *bufs[] = {&v->child_start, &v->child_node, &v->child_desc, &v->word_id, &v->weight, &v->in_desc,
                       &v->in_counts, &v->word, &v->wt, &v->nid, &v->o_words, &v->o_values, &v->o_nw, &v->o_fvn,
                       &v->o_fvs, &v->o_fvf, &v->o_nfv};
@@ -377,17 +383,17 @@ int orbv_batch_fetch(orbv_vocab *v, int frame, uint32_t *words, double *values, 
                      int32_t *fv_start, int32_t *fv_features, int32_t *n_fv) {
     if (!v || frame < 0 || frame >= v->frames || !n_words || !n_fv) return ORBX_EINVAL;
     BW_CHK(hipSetDevice(v->device));
-    BW_CHK(hipDeviceSynchronize());
+    BW_CHK(hipStreamWaitEvent(v->stream, v->done, 0));
     const size_t C = (size_t)v->cap, f = (size_t)frame;
-    BW_CHK(hipMemcpy(n_words, (char *)v->o_nw.p + 4 * f, 4, hipMemcpyDeviceToHost));
-    BW_CHK(hipMemcpy(n_fv, (char *)v->o_nfv.p + 4 * f, 4, hipMemcpyDeviceToHost));
+    BW_CHK(d2h_sync(n_words, (char *)v->o_nw.p + 4 * f, 4, v->stream));
+    BW_CHK(d2h_sync(n_fv, (char *)v->o_nfv.p + 4 * f, 4, v->stream));
     int32_t m = 0;
-    BW_CHK(hipMemcpy(&m, (char *)v->o_fvs.p + 4 * (f * (C + 1) + (size_t)*n_fv), 4, hipMemcpyDeviceToHost));
-    if (words && *n_words) BW_CHK(hipMemcpy(words, (char *)v->o_words.p + 4 * f * C, 4 * (size_t)*n_words, hipMemcpyDeviceToHost));
-    if (values && *n_words) BW_CHK(hipMemcpy(values, (char *)v->o_values.p + 8 * f * C, 8 * (size_t)*n_words, hipMemcpyDeviceToHost));
-    if (fv_nodes && *n_fv) BW_CHK(hipMemcpy(fv_nodes, (char *)v->o_fvn.p + 4 * f * C, 4 * (size_t)*n_fv, hipMemcpyDeviceToHost));
-    if (fv_start) BW_CHK(hipMemcpy(fv_start, (char *)v->o_fvs.p + 4 * f * (C + 1), 4 * ((size_t)*n_fv + 1), hipMemcpyDeviceToHost));
-    if (fv_features && m) BW_CHK(hipMemcpy(fv_features, (char *)v->o_fvf.p + 4 * f * C, 4 * (size_t)m, hipMemcpyDeviceToHost));
+    BW_CHK(d2h_sync(&m, (char *)v->o_fvs.p + 4 * (f * (C + 1) + (size_t)*n_fv), 4, v->stream));
+    if (words && *n_words) BW_CHK(d2h_sync(words, (char *)v->o_words.p + 4 * f * C, 4 * (size_t)*n_words, v->stream));
+    if (values && *n_words) BW_CHK(d2h_sync(values, (char *)v->o_values.p + 8 * f * C, 8 * (size_t)*n_words, v->stream));
+    if (fv_nodes && *n_fv) BW_CHK(d2h_sync(fv_nodes, (char *)v->o_fvn.p + 4 * f * C, 4 * (size_t)*n_fv, v->stream));
+    if (fv_start) BW_CHK(d2h_sync(fv_start, (char *)v->o_fvs.p + 4 * f * (C + 1), 4 * ((size_t)*n_fv + 1), v->stream));
+    if (fv_features && m) BW_CHK(d2h_sync(fv_features, (char *)v->o_fvf.p + 4 * f * C, 4 * (size_t)m, v->stream));
     return ORBX_OK;
 }
 

@@ -292,6 +292,8 @@ using namespace orbbm;
 struct orbb_engine {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;          // end of the last run (fetch waits on it only)
+    hipStream_t done_stream = nullptr;
     int nslots = 0, cap = 0;
     DevBuf hdr, kA, kB, uA, uB, dA, dB, mpA, mpB, badA, badB, fA, fB, nodes;
     DevBuf out, hidx, hbin, hn, counts, nmatch, pairs;
@@ -342,7 +344,8 @@ int orbb_create(orbb_engine **out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORBX_EDEVICE;
     orbb_engine *e = new orbb_engine();
-    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        !(e->done = make_done_event())) {
         delete e;
         return ORBX_EDEVICE;
     }
@@ -354,6 +357,7 @@ void orbb_destroy(orbb_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
+    if (e->done) { (void)hipEventSynchronize(e->done); (void)hipEventDestroy(e->done); }
     DevBuf *bufs[] = {&e->hdr, &e->kA, &e->kB, &e->uA, &e->uB, &e->dA, &e->dB, &e->mpA, &e->mpB, &e->badA, &e->badB, &e->fA,
                       &e->fB, &e->nodes, &e->out, &e->hidx, &e->hbin, &e->hn, &e->counts, &e->nmatch, &e->pairs};
     for (DevBuf *b : bufs) b->release();
@@ -405,6 +409,7 @@ int orbb_stage(orbb_engine *e, int slot, const orbb_keyframe *a, const orbb_keyf
     h.n_nodes = (int)nodes.size();
     const size_t C = (size_t)e->cap, s = (size_t)slot;
     hipStream_t st = e->stream;
+    BM_CHK(order_after_done(e, st));
     auto up = [&](DevBuf &bf, size_t off, const void *src, size_t bytes) -> bool {
         return bytes == 0 || !src || hipMemcpyAsync((char *)bf.p + off, src, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
     };
@@ -433,6 +438,7 @@ static int run(orbb_engine *e, int n_slots, int mode, float nnratio, int only_st
     if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
     BM_CHK(hipSetDevice(e->device));
     hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+    BM_CHK(order_after_done(e, st));
     int maxn = 1, maxnodes = 1;
     for (int s = 0; s < n_slots; s++) {
         maxn = std::max(maxn, std::max(e->h[s].nA, e->h[s].nB));
@@ -447,6 +453,7 @@ static int run(orbb_engine *e, int n_slots, int mode, float nnratio, int only_st
     else bm_node_kernel<BM_BOW><<<grid, 64, e->cap, st>>>(S, nnratio, only_stereo, check_ori, W);
     bm_finish_kernel<<<n_slots, 256, 0, st>>>(S, mode, check_ori, W);
     BM_CHK(hipGetLastError());
+    BM_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
@@ -465,14 +472,14 @@ int orbb_run_bowkf_batch(orbb_engine *e, int n_slots, float nnratio, int check_o
 int orbb_fetch(orbb_engine *e, int slot, int tri, int32_t *out, int32_t *n) {
     if (!e || slot < 0 || slot >= e->nslots || !out || !n) return ORBX_EINVAL;
     BM_CHK(hipSetDevice(e->device));
-    BM_CHK(hipDeviceSynchronize());
+    BM_CHK(hipStreamWaitEvent(e->stream, e->done, 0));
     const size_t C = (size_t)e->cap, s = (size_t)slot;
-    BM_CHK(hipMemcpy(n, (char *)e->nmatch.p + 4 * s, 4, hipMemcpyDeviceToHost));
+    BM_CHK(d2h_sync(n, (char *)e->nmatch.p + 4 * s, 4, e->stream));
     if (tri == 0 || tri == 2) {   // matches[b.n] (SearchByBoW(KF, F)) / matches12[a.n] (SearchByBoW(KF1, KF2))
         const size_t m = (size_t)(tri == 0 ? e->h[slot].nB : e->h[slot].nA);
-        if (m) BM_CHK(hipMemcpy(out, (char *)e->out.p + 4 * s * C, 4 * m, hipMemcpyDeviceToHost));
+        if (m) BM_CHK(d2h_sync(out, (char *)e->out.p + 4 * s * C, 4 * m, e->stream));
     } else if (*n > 0) {
-        BM_CHK(hipMemcpy(out, (char *)e->pairs.p + 8 * s * C, 8 * (size_t)*n, hipMemcpyDeviceToHost));
+        BM_CHK(d2h_sync(out, (char *)e->pairs.p + 8 * s * C, 8 * (size_t)*n, e->stream));
     }
     return ORBX_OK;
 }

@@ -59,7 +59,47 @@ struct DevBuf {
     template <class T> T *as() const { return (T *)p; }
 };
 
+// Completion tracking of the single-call and fetch paths. Every producer records the
+// engine's `done` event on the stream it launched on; a fetch makes the engine's own stream
+// wait for that event and copies on that stream, then waits for that stream only. Nothing
+// here touches the legacy null stream or synchronises the device, so engines driven from
+// different host threads -- the left / right extractor threads of Frame.cc:144-153, the
+// LocalMapping thread running LocalBA (LocalMapping.cc:116-118) -- never wait for each other.
+struct HostCopy {
+    hipStream_t st;
+    hipError_t err = hipSuccess;
+    HostCopy(hipStream_t s, hipEvent_t producer) : st(s) {
+        if (producer) err = hipStreamWaitEvent(st, producer, 0);
+    }
+    void d2h(void *dst, const void *src, size_t bytes) {
+        if (err == hipSuccess && dst && src && bytes) err = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    }
+    void h2d(void *dst, const void *src, size_t bytes) {
+        if (err == hipSuccess && dst && src && bytes) err = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+    }
+    // waits for the copies (and the producer) on this stream only
+    int finish() {
+        if (err == hipSuccess) err = hipStreamSynchronize(st);
+        return err == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+    }
+};
+
+// one device -> host copy on `st`, complete on return (fetch paths; `st` is the engine's own
+// stream, already ordered after the producer)
+inline hipError_t d2h_sync(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    const hipError_t r = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    return r == hipSuccess ? hipStreamSynchronize(st) : r;
+}
+
+inline hipEvent_t make_done_event() {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return ev;
+}
+
 }  // namespace orbamd
+
+struct orbf_state;   // per-engine Frame buffers (orb_frame.hip)
 
 struct orbx_engine {
     orbx_params p{};
@@ -87,6 +127,13 @@ struct orbx_engine {
     int last_pitch = 0;
     long long last_stride = 0;
     int last_n = 0;
+    long long gen = 0;            // extraction generation (bumped by every phase-2 launch)
+    int pending_w = 0, pending_h = 0, pending_pitch = 0;
+    long long pending_stride = 0;
+    int st_pairs = 0;             // pairs of the last stereo run (orbm_stereo_fetch bound)
+    hipEvent_t done = nullptr;    // recorded after the last launch of every producer
+    hipStream_t done_stream = nullptr;   // stream `done` was last recorded on
+    orbf_state *fs = nullptr;     // Frame / SearchForInitialization buffers, owned
     std::string err;
     // per-kernel hipEvent profiling (bench.py roofline), recorded on the launch stream
     bool prof = false;
@@ -94,6 +141,19 @@ struct orbx_engine {
     std::vector<ProfRec> prof_recs;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
+};
+
+// ORBmatcher(float nnratio, bool checkOri) (ORBmatcher.h:57): the two members plus a private
+// stream and grow-only device buffers for the host-pointer matcher entries.
+struct orbm_matcher {
+    float nnratio = 0.6f;
+    int check_ori = 1;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    hipStream_t done_stream = nullptr;
+    orbamd::DevBuf q, db, off, idx, out;                                    // Hamming scans
+    orbamd::DevBuf kun, desc, cnt, keys, nkeys, prev, m12, nmatch, list, lcnt;   // SearchForInitialization
 };
 
 namespace orbamd {
@@ -104,4 +164,17 @@ void prof_end(orbx_engine *e, hipStream_t s, int h, const char *name);
 int engine_reserve(orbx_engine *e, int w, int h, int max_images);
 int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitch,
                           long long stride, hipStream_t s, int phase);
+void frame_state_free(orbx_engine *e);   // orb_frame.hip
+
+// A producer launching on `s` first orders itself after the engine's previous producer when
+// that one ran on another stream (buffers are reused across calls), and records `done` after
+// its own last launch. E: any engine with `done` / `done_stream` members.
+template <class E> inline hipError_t order_after_done(E *e, hipStream_t s) {
+    if (e->done_stream && e->done_stream != s) return hipStreamWaitEvent(s, e->done, 0);
+    return hipSuccess;
+}
+template <class E> inline hipError_t mark_done(E *e, hipStream_t s) {
+    e->done_stream = s;
+    return hipEventRecord(e->done, s);
+}
 }  // namespace orbamd

@@ -1426,9 +1426,13 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
     HIPCHK(hipSetDevice(e->device));
     const bool same = (W == e->W && H == e->H);
     if (same && max_images <= e->max_images) return ORBX_OK;
-    ExtractGeom &g = e->g;
+    // A new size is built into locals and committed only after every check and upload has
+    // passed, so a rejected size leaves the engine's current geometry intact.
+    ExtractGeom gnew{};
+    std::vector<CellDesc> cells;
+    int rz_rows[ORBX_MAXL] = {};
+    ExtractGeom &g = same ? e->g : gnew;
     if (!same) {
-        g = ExtractGeom{};
         const int L = e->p.nlevels;
         g.nlevels = L; g.W = W; g.H = H;
         long long pyr = 0, blur = 0;
@@ -1447,8 +1451,7 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         g.pyr_stride = std::max(pyr, 64LL);
         g.blur_stride = blur;
         // FAST cell grid (:1046-1153)
-        e->cells.clear();
-        int cell_cap = 0, maxM_total = 0;
+                int cell_cap = 0, maxM_total = 0;
         long long qt = 0;
         int node_cap = 0;
         for (int l = 0; l < L; l++) {
@@ -1460,7 +1463,7 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
             if (wCell + 6 > ORBX_TMAX || hCell + 6 > ORBX_TMAX) return ORBX_EINVAL;
             cell_cap = std::max(cell_cap, ((wCell + 1) / 2) * ((hCell + 1) / 2));
-            g.cell_base[l] = (int)e->cells.size();
+            g.cell_base[l] = (int)cells.size();
             for (int i = 0; i < nRows; i++) {
                 const float iniY = (float)(minB + i * hCell);
                 float maxY = iniY + hCell + 6;
@@ -1477,10 +1480,10 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
                     cd.rh = (int16_t)((int)maxY - (int)iniY); cd.rw = (int16_t)((int)maxX - (int)iniX);
                     cd.offx = (int16_t)(j * wCell); cd.offy = (int16_t)(i * hCell);
                     cd.pad = 0;
-                    e->cells.push_back(cd);
+                    cells.push_back(cd);
                 }
             }
-            const int ncl = (int)e->cells.size() - g.cell_base[l];
+            const int ncl = (int)cells.size() - g.cell_base[l];
             // quadtree parameters (:700-705)
             g.N[l] = e->nfeat[l];
             const int nIni = (int)std::round((float)(maxBX - minB) / (maxBY - minB));
@@ -1491,9 +1494,9 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             node_cap = std::max(node_cap, g.out_cap[l] + 4);
             (void)ncl;
         }
-        g.cell_base[L] = (int)e->cells.size();
+        g.cell_base[L] = (int)cells.size();
         int max_rh = 0, max_det = 0;
-        for (const CellDesc &cd : e->cells) {
+        for (const CellDesc &cd : cells) {
             max_rh = std::max(max_rh, (int)cd.rh);
             max_det = std::max(max_det, std::max(cd.rh - 6, 0) * std::max(cd.rw - 6, 0));
         }
@@ -1570,7 +1573,7 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
                 rows = std::max(rows, rzr[g.rz_row_off[l] + y1].y - rzr[g.rz_row_off[l] + y0].x + 1);
             }
             if (rows * 32 * (int)sizeof(uint4) > 64 * 1024) return ORBX_EINVAL;
-            e->rz_rows[l] = rows;
+            rz_rows[l] = rows;
         }
         if (rzc.empty()) rzc.push_back(make_int2(0, 0));
         if (rzr.empty()) rzr.push_back(make_int4(0, 0, 0, 0));
@@ -1581,25 +1584,38 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             g.blur_tiles_y[l] = (g.lh[l] + FB_TH - 1) / FB_TH;
             g.blur_tile_base[l + 1] = g.blur_tile_base[l] + g.blur_tiles_x[l] * g.blur_tiles_y[l];
         }
-        if (e->d_cells.ensure(sizeof(CellDesc) * e->cells.size())) return ORBX_EDEVICE;
-        HIPCHK(hipMemcpy(e->d_cells.p, e->cells.data(), sizeof(CellDesc) * e->cells.size(), hipMemcpyHostToDevice));
+        // From here on the engine's tables change: drop the old size first, so a failure
+        // below leaves an engine that rebuilds on the next call instead of one that runs the
+        // new tables against the old geometry.
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if (e->done) HIPCHK(hipEventSynchronize(e->done));   // last launches may still read the tables
+        e->W = e->H = 0;
+        e->max_images = 0;
+        e->last_n = 0;
+        e->st_pairs = 0;
+        e->pending_in = nullptr;
+        if (e->d_cells.ensure(sizeof(CellDesc) * cells.size())) return ORBX_EDEVICE;
         if (e->d_rz.ensure(sizeof(int2) * rzc.size()) || e->d_rzr.ensure(sizeof(int4) * rzr.size())) return ORBX_EDEVICE;
+        HIPCHK(hipMemcpy(e->d_cells.p, cells.data(), sizeof(CellDesc) * cells.size(), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->d_rz.p, rzc.data(), sizeof(int2) * rzc.size(), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->d_rzr.p, rzr.data(), sizeof(int4) * rzr.size(), hipMemcpyHostToDevice));
+        e->g = gnew;
+        e->cells.swap(cells);
+        for (int l = 0; l < ORBX_MAXL; l++) e->rz_rows[l] = rz_rows[l];
         e->W = W; e->H = H;
-        e->max_images = 0;
     }
+    ExtractGeom &gc = e->g;
     const long long B = max_images;
-    if (e->d_pyr.ensure(B * g.pyr_stride) || e->d_blur.ensure(B * g.blur_stride) ||
-        e->d_mmap.ensure(B * g.blur_stride) ||
-        e->d_cell_cnt.ensure(sizeof(int) * B * g.ncell_total) ||
-        e->d_cell_keys.ensure(sizeof(uint32_t) * B * g.ncell_total * g.cell_cap) ||
-        e->d_qt.ensure(sizeof(uint32_t) * B * g.qt_off[g.nlevels]) ||
-        e->d_qt_nodes.ensure(g.qt_nodes_in_lds ? 16 : (size_t)4 * B * g.nlevels * g.qt_node_stride) ||
-        e->d_sel.ensure(sizeof(uint32_t) * B * g.out_base[g.nlevels]) ||
-        e->d_sel_cnt.ensure(sizeof(int) * B * g.nlevels) ||
-        e->d_kps.ensure(sizeof(orbx_kp) * B * g.out_base[g.nlevels]) ||
-        e->d_desc.ensure((size_t)32 * B * g.out_base[g.nlevels]) || e->d_cnt.ensure(sizeof(int) * B))
+    if (e->d_pyr.ensure(B * gc.pyr_stride) || e->d_blur.ensure(B * gc.blur_stride) ||
+        e->d_mmap.ensure(B * gc.blur_stride) ||
+        e->d_cell_cnt.ensure(sizeof(int) * B * gc.ncell_total) ||
+        e->d_cell_keys.ensure(sizeof(uint32_t) * B * gc.ncell_total * gc.cell_cap) ||
+        e->d_qt.ensure(sizeof(uint32_t) * B * gc.qt_off[gc.nlevels]) ||
+        e->d_qt_nodes.ensure(gc.qt_nodes_in_lds ? 16 : (size_t)4 * B * gc.nlevels * gc.qt_node_stride) ||
+        e->d_sel.ensure(sizeof(uint32_t) * B * gc.out_base[gc.nlevels]) ||
+        e->d_sel_cnt.ensure(sizeof(int) * B * gc.nlevels) ||
+        e->d_kps.ensure(sizeof(orbx_kp) * B * gc.out_base[gc.nlevels]) ||
+        e->d_desc.ensure((size_t)32 * B * gc.out_base[gc.nlevels]) || e->d_cnt.ensure(sizeof(int) * B))
         return ORBX_EDEVICE;
     e->max_images = max_images;
     return ORBX_OK;
@@ -1614,6 +1630,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     const int L = g.nlevels;
     uint8_t *pyr = e->d_pyr.as<uint8_t>();
     const int cap = g.out_base[L];
+    HIPCHK(order_after_done(e, s));
     if (phase & 1) {
     int ph = prof_begin(e, s);
     for (int l = 1; l < L; l++) {
@@ -1663,10 +1680,12 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     prof_end(e, s, ph, "describe_kernel");
     }
     HIPCHK(hipGetLastError());
+    HIPCHK(mark_done(e, s));
     e->last_in = d_imgs;
     e->last_pitch = pitch;
     e->last_stride = stride;
     e->last_n = n;
+    if (phase & 2) e->gen++;
     return ORBX_OK;
 }
 
@@ -1697,6 +1716,8 @@ int orbx_create(const orbx_params *p, orbx_engine **out) {
     if (hipGetDevice(&e->device) != hipSuccess) { delete e; return ORBX_EDEVICE; }
     compute_tables(e);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return ORBX_EDEVICE; }
+    e->done = orbamd::make_done_event();
+    if (!e->done) { (void)hipStreamDestroy(e->stream); delete e; return ORBX_EDEVICE; }
     uint2 icw[16 * 8];
     for (int av = 0; av < 16; av++) {
         for (int w = 0; w < 8; w++) {
@@ -1711,6 +1732,7 @@ int orbx_create(const orbx_params *p, orbx_engine **out) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), e->pattern, 1024) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(c_umax), e->umax, sizeof(e->umax)) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(c_icw), icw, sizeof(icw)) != hipSuccess) {
+        (void)hipEventDestroy(e->done);
         (void)hipStreamDestroy(e->stream);
         delete e;
         return ORBX_EDEVICE;
@@ -1723,12 +1745,15 @@ void orbx_destroy(orbx_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->done) (void)hipEventSynchronize(e->done);
+    orbamd::frame_state_free(e);
     orbamd::DevBuf *bufs[] = {&e->d_mmap, &e->d_cells, &e->d_rz, &e->d_rzr, &e->d_pattern, &e->d_in, &e->d_pyr, &e->d_blur,
                               &e->d_cell_cnt, &e->d_cell_keys, &e->d_qt, &e->d_qt_nodes, &e->d_sel,
                               &e->d_sel_cnt, &e->d_kps, &e->d_desc, &e->d_cnt, &e->d_st_sorted,
                               &e->d_st_res, &e->d_st_u, &e->d_st_depth, &e->d_st_dist, &e->d_st_rows};
     for (auto *b : bufs) b->release();
     for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+    if (e->done) (void)hipEventDestroy(e->done);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -1760,7 +1785,7 @@ int orbslam2_amd_device_sync(void) {
 
 int orbx_profile(orbx_engine *e, int enable) {
     if (!e) return ORBX_EINVAL;
-    if (e->prof) (void)hipDeviceSynchronize();
+    for (auto &r : e->prof_recs) (void)hipEventSynchronize(r.b);   // events are reused after the reset
     e->prof = enable != 0;
     e->prof_recs.clear();
     e->ev_used = 0;
@@ -1770,7 +1795,7 @@ int orbx_profile(orbx_engine *e, int enable) {
 int orbx_profile_read(orbx_engine *e, int idx, char *name, int name_cap, double *total_ms,
                       int *launches) {
     if (!e || idx < 0) return ORBX_EINVAL;
-    HIPCHK(hipDeviceSynchronize());
+    for (auto &r : e->prof_recs) HIPCHK(hipEventSynchronize(r.b));
     std::vector<std::string> names;
     for (auto &r : e->prof_recs)
         if (std::find(names.begin(), names.end(), std::string(r.name)) == names.end()) names.push_back(r.name);
@@ -1804,14 +1829,22 @@ int orbx_extract_batch_device(orbx_engine *e, const uint8_t *d_imgs, int n_image
 
 int orbx_extract_batch_device_phase(orbx_engine *e, const uint8_t *d_imgs, int n_images, int w, int h,
                                     int pitch, size_t image_stride, void *stream, int phase) {
-    if (!e || !d_imgs || n_images <= 0 || pitch < w || phase < 1 || phase > 3) return ORBX_EINVAL;
-    if (phase == 2 && (e->pending_in != d_imgs || e->pending_n != n_images)) return ORBX_ESTATE;
+    if (!e || !d_imgs || n_images <= 0 || w <= 0 || h <= 0 || pitch < w || phase < 1 || phase > 3) return ORBX_EINVAL;
+    if (n_images > 1 && image_stride < (size_t)pitch * (size_t)(h - 1) + (size_t)w) return ORBX_EINVAL;  // images overlap
+    if (phase == 2 && (e->pending_in != d_imgs || e->pending_n != n_images || e->pending_w != w ||
+                       e->pending_h != h || e->pending_pitch != pitch || e->pending_stride != (long long)image_stride))
+        return ORBX_ESTATE;   // phase 2 must continue exactly the phase-1 batch
     int rc = orbamd::engine_reserve(e, w, h, std::max(n_images, e->max_images));
     if (rc) return rc;
     rc = orbamd::engine_extract_device(e, d_imgs, n_images, pitch, (long long)image_stride,
                                        stream ? (hipStream_t)stream : e->stream, phase);
-    e->pending_in = phase == 1 ? d_imgs : nullptr;
-    e->pending_n = phase == 1 ? n_images : 0;
+    const bool p1 = phase == 1 && rc == ORBX_OK;
+    e->pending_in = p1 ? d_imgs : nullptr;
+    e->pending_n = p1 ? n_images : 0;
+    e->pending_w = p1 ? w : 0;
+    e->pending_h = p1 ? h : 0;
+    e->pending_pitch = p1 ? pitch : 0;
+    e->pending_stride = p1 ? (long long)image_stride : 0;
     return rc;
 }
 
@@ -1829,16 +1862,20 @@ int orbx_batch_fetch(orbx_engine *e, int image, orbx_kp *kps, uint8_t *desc, int
     if (!e || !n) return ORBX_EINVAL;
     if (e->last_n == 0 || image < 0 || image >= e->last_n) return ORBX_ESTATE;
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    HIPCHK(hipDeviceSynchronize());
     int cnt = 0;
-    HIPCHK(hipMemcpy(&cnt, e->d_cnt.as<int>() + image, sizeof(int), hipMemcpyDeviceToHost));
+    {
+        orbamd::HostCopy hc(e->stream, e->done);
+        hc.d2h(&cnt, e->d_cnt.as<int>() + image, sizeof(int));
+        if (hc.finish()) return ORBX_EDEVICE;
+    }
     *n = cnt;
     if (cnt > cap) return ORBX_ECAP;
     const long long kc = e->g.out_base[e->g.nlevels];
     if (cnt > 0) {
-        if (kps) HIPCHK(hipMemcpy(kps, e->d_kps.as<orbx_kp>() + image * kc, sizeof(orbx_kp) * cnt, hipMemcpyDeviceToHost));
-        if (desc) HIPCHK(hipMemcpy(desc, e->d_desc.as<uint8_t>() + image * kc * 32, 32 * (size_t)cnt, hipMemcpyDeviceToHost));
+        orbamd::HostCopy hc(e->stream, nullptr);
+        hc.d2h(kps, e->d_kps.as<orbx_kp>() + image * kc, sizeof(orbx_kp) * cnt);
+        hc.d2h(desc, e->d_desc.as<uint8_t>() + image * kc * 32, 32 * (size_t)cnt);
+        if (hc.finish()) return ORBX_EDEVICE;
     }
     return ORBX_OK;
 }
@@ -1852,7 +1889,9 @@ int orbx_extract(orbx_engine *e, const uint8_t *img, int w, int h, int stride, o
     HIPCHK(hipSetDevice(e->device));
     int rc = orbamd::engine_reserve(e, w, h, std::max(1, e->max_images));
     if (rc) return rc;
-    if (e->d_in.ensure((size_t)w * h)) return ORBX_EDEVICE;
+    // +16: the aligned dword loads of the level-0 staging / level-1 resize may read up to
+    // 11 bytes past the last pixel of the last row (include/orbslam2_amd.h, input tail)
+    if (e->d_in.ensure((size_t)w * h + 16)) return ORBX_EDEVICE;
     HIPCHK(hipMemcpy2DAsync(e->d_in.p, w, img, stride, w, h, hipMemcpyHostToDevice, e->stream));
     rc = orbamd::engine_extract_device(e, e->d_in.as<uint8_t>(), 1, w, (long long)w * h, e->stream, 3);
     if (rc) return rc;
@@ -1867,13 +1906,15 @@ int orbx_pyramid_level(orbx_engine *e, int image, int level, uint8_t *dst, int *
     if (h) *h = lh;
     if (!dst) return ORBX_OK;
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipStreamWaitEvent(e->stream, e->done, 0));
     if (level == 0) {
-        HIPCHK(hipMemcpy2D(dst, lw, e->last_in + image * e->last_stride, e->last_pitch, lw, lh, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy2DAsync(dst, lw, e->last_in + image * e->last_stride, e->last_pitch, lw, lh, hipMemcpyDeviceToHost,
+                                e->stream));
     } else {
-        HIPCHK(hipMemcpy2D(dst, lw, e->d_pyr.as<uint8_t>() + image * e->g.pyr_stride + e->g.pyr_off[level],
-                           e->g.bp[level], lw, lh, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy2DAsync(dst, lw, e->d_pyr.as<uint8_t>() + image * e->g.pyr_stride + e->g.pyr_off[level],
+                                e->g.bp[level], lw, lh, hipMemcpyDeviceToHost, e->stream));
     }
+    HIPCHK(hipStreamSynchronize(e->stream));
     return ORBX_OK;
 }
 

@@ -436,17 +436,31 @@ static GridParams make_grid(const Camera &c, int cols, int rows) {
 
 using namespace orbframe;
 
+// Per-engine Frame buffers, owned by the engine (freed by orbx_destroy). kun / uR / dep are
+// valid for the extraction generation `kun_gen` (n images x `kun_cap` keypoints); m12 / prev
+// for `si_pairs` pairs of the SearchForInitialization run that followed.
 struct orbf_state {
     DevBuf kun, uR, dep, keys, nkeys, prev, m12, nmatch, depth_in, list, lcnt;
+    long long kun_gen = -1;
+    int kun_n = 0, kun_cap = 0, si_pairs = 0;
 };
 
 static orbf_state &fstate(orbx_engine *e) {
-    // per-engine frame buffers live in a side table keyed by engine pointer
-    static std::vector<std::pair<orbx_engine *, orbf_state *>> tab;
-    for (auto &t : tab) if (t.first == e) return *t.second;
-    tab.push_back({e, new orbf_state()});
-    return *tab.back().second;
+    if (!e->fs) e->fs = new orbf_state();
+    return *e->fs;
 }
+
+namespace orbamd {
+void frame_state_free(orbx_engine *e) {
+    if (!e->fs) return;
+    orbf_state *S = e->fs;
+    DevBuf *bufs[] = {&S->kun, &S->uR, &S->dep, &S->keys, &S->nkeys, &S->prev, &S->m12, &S->nmatch,
+                      &S->depth_in, &S->list, &S->lcnt};
+    for (DevBuf *b : bufs) b->release();
+    delete S;
+    e->fs = nullptr;
+}
+}  // namespace orbamd
 
 extern "C" {
 
@@ -460,12 +474,18 @@ int orbf_rgbd_batch_device(orbx_engine *e, const float *d_depth, size_t depth_st
         return ORBX_EDEVICE;
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
     const Camera cam = make_camera(K, dist, mbf);
+    FR_CHK(order_after_done(e, s));
     int ph = prof_begin(e, s);
     rgbd_kernel<<<dim3((cap + 255) / 256, n), 256, 0, s>>>(cam, e->d_kps.as<orbx_kp>(), e->d_cnt.as<int>(), cap, d_depth,
                                                            (long long)depth_stride, dpitch, S.kun.as<orbx_kp>(),
                                                            S.uR.as<float>(), S.dep.as<float>());
     prof_end(e, s, ph, "rgbd_kernel");
     FR_CHK(hipGetLastError());
+    FR_CHK(mark_done(e, s));
+    S.kun_gen = e->gen;
+    S.kun_n = n;
+    S.kun_cap = cap;
+    S.si_pairs = 0;
     return ORBX_OK;
 }
 
@@ -473,19 +493,27 @@ int orbf_rgbd(orbx_engine *e, const float *depth, int dpitch, const float K[4], 
               orbx_kp *keys_un, float *u_right, float *depth_out, int n) {
     if (!e || !depth || n < 0) return ORBX_EINVAL;
     if (e->last_n < 1) return ORBX_ESTATE;
+    if (dpitch < e->W) return ORBX_EINVAL;
     orbf_state &S = fstate(e);
     if (S.depth_in.ensure(sizeof(float) * (size_t)dpitch * e->H)) return ORBX_EDEVICE;
+    // the previous launch on this stream may still read depth_in: stream order covers it
+    FR_CHK(hipStreamWaitEvent(e->stream, e->done, 0));
     FR_CHK(hipMemcpyAsync(S.depth_in.p, depth, sizeof(float) * (size_t)dpitch * e->H, hipMemcpyHostToDevice, e->stream));
     int rc = orbf_rgbd_batch_device(e, S.depth_in.as<float>(), 0, dpitch, K, dist, mbf, e->stream);
     if (rc) return rc;
-    FR_CHK(hipStreamSynchronize(e->stream));
     int cnt = 0;
-    FR_CHK(hipMemcpy(&cnt, e->d_cnt.p, sizeof(int), hipMemcpyDeviceToHost));
+    {
+        HostCopy hc(e->stream, nullptr);
+        hc.d2h(&cnt, e->d_cnt.p, sizeof(int));
+        if (hc.finish()) return ORBX_EDEVICE;
+    }
     if (cnt != n) return ORBX_EINVAL;
     if (n > 0) {
-        if (keys_un) FR_CHK(hipMemcpy(keys_un, S.kun.p, sizeof(orbx_kp) * n, hipMemcpyDeviceToHost));
-        if (u_right) FR_CHK(hipMemcpy(u_right, S.uR.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
-        if (depth_out) FR_CHK(hipMemcpy(depth_out, S.dep.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        HostCopy hc(e->stream, nullptr);
+        hc.d2h(keys_un, S.kun.p, sizeof(orbx_kp) * n);
+        hc.d2h(u_right, S.uR.p, 4 * (size_t)n);
+        hc.d2h(depth_out, S.dep.p, 4 * (size_t)n);
+        if (hc.finish()) return ORBX_EDEVICE;
     }
     return ORBX_OK;
 }
@@ -495,14 +523,17 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
                                   void *stream) {
     if (!e || n_pairs <= 0 || !K || !dist) return ORBX_EINVAL;
     orbf_state &S = fstate(e);
-    if (!S.kun.p) return ORBX_ESTATE;  // needs orbf_rgbd*: undistorted keypoints
     const int n = e->last_n, cap = e->g.out_base[e->g.nlevels];
-    if (f1_base + f1_step * (n_pairs - 1) >= n || f2_base + f2_step * (n_pairs - 1) >= n) return ORBX_EINVAL;
+    // needs the undistorted keypoints (orbf_rgbd*) of the engine's current extraction
+    if (!S.kun.p || S.kun_gen != e->gen || S.kun_n != n || S.kun_cap != cap) return ORBX_ESTATE;
+    if (f1_base < 0 || f2_base < 0 || f1_step < 0 || f2_step < 0 ||
+        f1_base + f1_step * (n_pairs - 1) >= n || f2_base + f2_step * (n_pairs - 1) >= n) return ORBX_EINVAL;
     int sort_cap = 1;
     while (sort_cap < cap) sort_cap <<= 1;
     if (cap > 4096 || sort_cap > 4096 || cap > 32767) return ORBX_EINVAL;
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
     const Camera cam = make_camera(K, dist, 0.f);
+    FR_CHK(order_after_done(e, s));
     const GridParams gp = make_grid(cam, e->W, e->H);
     if (S.keys.ensure(4 * (size_t)n * sort_cap) || S.nkeys.ensure(4 * (size_t)n) ||
         S.prev.ensure(8 * (size_t)n_pairs * cap) || S.m12.ensure(4 * (size_t)n_pairs * cap) ||
@@ -542,33 +573,115 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
     search_init_resolve_kernel<<<n_pairs, 256, lds, s>>>(a, S.prev.as<float>(), S.m12.as<int>(), S.nmatch.as<int>());
     prof_end(e, s, ph, "search_init_kernel");
     FR_CHK(hipGetLastError());
+    FR_CHK(mark_done(e, s));
+    S.si_pairs = n_pairs;
     return ORBX_OK;
 }
 
 int orbm_search_init_fetch(orbx_engine *e, int pair, int *matches12, float *prev_xy, int cap, int *nmatches) {
     if (!e) return ORBX_EINVAL;
     orbf_state &S = fstate(e);
-    if (!S.m12.p) return ORBX_ESTATE;
+    if (!S.m12.p || S.si_pairs == 0 || S.kun_gen != e->gen) return ORBX_ESTATE;
+    if (pair < 0 || pair >= S.si_pairs) return ORBX_EINVAL;
     const int kc = e->g.out_base[e->g.nlevels];
     if (cap < kc) return ORBX_ECAP;
-    FR_CHK(hipDeviceSynchronize());
-    if (matches12) FR_CHK(hipMemcpy(matches12, S.m12.as<int>() + (size_t)pair * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
-    if (prev_xy) FR_CHK(hipMemcpy(prev_xy, S.prev.as<float>() + (size_t)pair * kc * 2, 8 * (size_t)kc, hipMemcpyDeviceToHost));
-    if (nmatches) FR_CHK(hipMemcpy(nmatches, S.nmatch.as<int>() + pair, 4, hipMemcpyDeviceToHost));
-    return ORBX_OK;
+    FR_CHK(hipSetDevice(e->device));
+    HostCopy hc(e->stream, e->done);
+    hc.d2h(matches12, S.m12.as<int>() + (size_t)pair * kc, 4 * (size_t)kc);
+    hc.d2h(prev_xy, S.prev.as<float>() + (size_t)pair * kc * 2, 8 * (size_t)kc);
+    hc.d2h(nmatches, S.nmatch.as<int>() + pair, 4);
+    return hc.finish();
 }
 
 int orbf_rgbd_fetch(orbx_engine *e, int image, orbx_kp *keys_un, float *u_right, float *depth_out, int cap) {
     if (!e) return ORBX_EINVAL;
     orbf_state &S = fstate(e);
-    if (!S.kun.p) return ORBX_ESTATE;
+    if (!S.kun.p || S.kun_gen != e->gen) return ORBX_ESTATE;
+    if (image < 0 || image >= S.kun_n) return ORBX_EINVAL;
     const int kc = e->g.out_base[e->g.nlevels];
     if (cap < kc) return ORBX_ECAP;
-    FR_CHK(hipDeviceSynchronize());
-    if (keys_un) FR_CHK(hipMemcpy(keys_un, S.kun.as<orbx_kp>() + (size_t)image * kc, sizeof(orbx_kp) * kc, hipMemcpyDeviceToHost));
-    if (u_right) FR_CHK(hipMemcpy(u_right, S.uR.as<float>() + (size_t)image * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
-    if (depth_out) FR_CHK(hipMemcpy(depth_out, S.dep.as<float>() + (size_t)image * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
-    return ORBX_OK;
+    FR_CHK(hipSetDevice(e->device));
+    HostCopy hc(e->stream, e->done);
+    hc.d2h(keys_un, S.kun.as<orbx_kp>() + (size_t)image * kc, sizeof(orbx_kp) * kc);
+    hc.d2h(u_right, S.uR.as<float>() + (size_t)image * kc, 4 * (size_t)kc);
+    hc.d2h(depth_out, S.dep.as<float>() + (size_t)image * kc, 4 * (size_t)kc);
+    return hc.finish();
+}
+
+// ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) on two
+// host Frames (ORBmatcher.h:169, ORBmatcher.cc:580-748), as Tracking::MonocularInitialization
+// calls it frame after frame against a fixed initial frame (Tracking.cc:893-897, 929-933):
+// vbPrevMatched is the window centre per F1 keypoint on input (:627) and is rewritten with the
+// matched F2 positions on output (:742-745), so consecutive calls chain exactly as in the
+// reference. Same two-phase kernels as the batched form, F1 / F2 = images 0 / 1 of the matcher's
+// buffers.
+int orbm_search_for_initialization(orbm_matcher *m, const orbm_frame *F1, const orbm_frame *F2, float *prev_matched,
+                                   int32_t *matches12, int window, int32_t *nmatches) {
+    if (!m || !F1 || !F2 || !nmatches) return ORBX_EINVAL;
+    *nmatches = 0;
+    if (F1->n < 0 || F2->n < 0) return ORBX_EINVAL;
+    if (F1->n == 0) return ORBX_OK;   // vnMatches12 = vector<int>(0)
+    if (!prev_matched || !matches12 || !F1->keys_un || !F1->desc) return ORBX_EINVAL;
+    if (F2->n > 0 && (!F2->keys_un || !F2->desc)) return ORBX_EINVAL;
+    if (!(F2->max_x > F2->min_x) || !(F2->max_y > F2->min_y) || window < 0) return ORBX_EINVAL;
+    const int cap = std::max(std::max(F1->n, F2->n), 1);
+    int sort_cap = 1;
+    while (sort_cap < cap) sort_cap <<= 1;
+    if (sort_cap > 4096) return ORBX_EINVAL;   // one workgroup's LDS sort of F2's grid keys
+    const int cap0 = cap;                     // every F1 keypoint may be of octave 0
+    const size_t fixed = 4 * ((size_t)cap0 + 1) + 7 * (size_t)cap + 16;
+    if (fixed >= 60 * 1024) return ORBX_EINVAL;
+    SearchArgs a;
+    a.stage_cap = (int)std::min<size_t>(16384, (60 * 1024 - fixed) / 4);
+    if (a.stage_cap < cap0) return ORBX_EINVAL;
+    FR_CHK(hipSetDevice(m->device));
+    const hipStream_t s = m->stream;
+    FR_CHK(order_after_done(m, s));
+    FR_CHK(hipStreamWaitEvent(s, m->done, 0));
+    if (m->kun.ensure(sizeof(orbx_kp) * 2 * (size_t)cap) || m->desc.ensure(64 * (size_t)cap) || m->cnt.ensure(8) ||
+        m->keys.ensure(8 * (size_t)sort_cap) || m->nkeys.ensure(8) || m->prev.ensure(8 * (size_t)cap) ||
+        m->m12.ensure(4 * (size_t)cap) || m->nmatch.ensure(4) || m->list.ensure(4 * (size_t)cap0 * cap0) ||
+        m->lcnt.ensure(4 * (size_t)cap0))
+        return ORBX_EDEVICE;
+    const int counts[2] = {F1->n, F2->n};
+    HostCopy up(s, nullptr);
+    up.h2d(m->kun.p, F1->keys_un, sizeof(orbx_kp) * (size_t)F1->n);
+    up.h2d((char *)m->kun.p + sizeof(orbx_kp) * (size_t)cap, F2->keys_un, sizeof(orbx_kp) * (size_t)F2->n);
+    up.h2d(m->desc.p, F1->desc, 32 * (size_t)F1->n);
+    up.h2d((char *)m->desc.p + 32 * (size_t)cap, F2->desc, 32 * (size_t)F2->n);
+    up.h2d(m->cnt.p, counts, sizeof counts);
+    up.h2d(m->prev.p, prev_matched, 8 * (size_t)F1->n);
+    if (up.finish()) return ORBX_EDEVICE;   // host arrays (counts) go out of scope
+    GridParams gp;
+    gp.minX = F2->min_x; gp.maxX = F2->max_x; gp.minY = F2->min_y; gp.maxY = F2->max_y;
+    gp.invW = (float)GRID_COLS / (gp.maxX - gp.minX);   // Frame.cc:183-184
+    gp.invH = (float)GRID_ROWS / (gp.maxY - gp.minY);
+    a.f1_base = 0; a.f1_step = 0; a.f2_base = 1; a.f2_step = 0;
+    a.kun = m->kun.as<orbx_kp>();
+    a.desc = m->desc.as<uint8_t>();
+    a.cnt = m->cnt.as<int>();
+    a.cap = cap;
+    a.sort_cap = sort_cap;
+    a.cap0 = cap0;
+    a.keys = m->keys.as<uint32_t>();
+    a.nkeys = m->nkeys.as<int>();
+    a.gp = gp;
+    a.r = (float)window;
+    a.nnratio = m->nnratio;
+    a.check_ori = m->check_ori;
+    a.list = m->list.as<uint32_t>();
+    a.lcnt = m->lcnt.as<int>();
+    grid_sort_kernel<<<2, 256, 4 * sort_cap, s>>>(gp, a.kun, a.cnt, cap, sort_cap, m->keys.as<uint32_t>(), m->nkeys.as<int>());
+    search_init_cand_kernel<<<dim3((cap0 + 3) / 4, 1), 256, 0, s>>>(a, m->prev.as<float>());
+    search_init_resolve_kernel<<<1, 256, 4 * (size_t)a.stage_cap + fixed, s>>>(a, m->prev.as<float>(), m->m12.as<int>(),
+                                                                              m->nmatch.as<int>());
+    FR_CHK(hipGetLastError());
+    FR_CHK(mark_done(m, s));
+    HostCopy dn(s, nullptr);
+    dn.d2h(matches12, m->m12.p, 4 * (size_t)F1->n);
+    dn.d2h(prev_matched, m->prev.p, 8 * (size_t)F1->n);
+    dn.d2h(nmatches, m->nmatch.p, 4);
+    return dn.finish();
 }
 
 }  // extern "C"

@@ -313,6 +313,8 @@ using namespace orbnp;
 struct orbn_engine {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;          // end of the last run (fetch waits on it only)
+    hipStream_t done_stream = nullptr;
     int nslots = 0, cap = 0, cap_pairs = 0;
     std::vector<SlotHdr> h;
     DevBuf hdr, kp[2], oct[2], ud[2], pairs, x3d, ok, nnew;
@@ -352,7 +354,8 @@ int orbn_create(orbn_engine **out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORBX_EDEVICE;
     orbn_engine *e = new orbn_engine();
-    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        !(e->done = make_done_event())) {
         delete e;
         return ORBX_EDEVICE;
     }
@@ -364,6 +367,7 @@ void orbn_destroy(orbn_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
+    if (e->done) { (void)hipEventSynchronize(e->done); (void)hipEventDestroy(e->done); }
     DevBuf *bufs[] = {&e->hdr, &e->kp[0], &e->kp[1], &e->oct[0], &e->oct[1], &e->ud[0], &e->ud[1],
                       &e->pairs, &e->x3d, &e->ok, &e->nnew};
     for (DevBuf *b : bufs) b->release();
@@ -407,6 +411,7 @@ int orbn_stage(orbn_engine *e, int slot, const orbn_keyframe *kf1, const orbn_ke
     h.ratio_factor = ratio_factor;
     const size_t C = (size_t)e->cap, s = (size_t)slot;
     hipStream_t st = e->stream;
+    NP_CHK(order_after_done(e, st));
     for (int i = 0; i < 2; i++) {
         KFHdr &d = h.k[i];
         const orbn_keyframe *k = K[i];
@@ -445,21 +450,23 @@ int orbn_run_batch(orbn_engine *e, int n_slots, void *stream) {
     hipStream_t st = stream ? (hipStream_t)stream : e->stream;
     int maxp = 1;
     for (int s = 0; s < n_slots; s++) maxp = std::max(maxp, e->h[s].npairs);
+    NP_CHK(order_after_done(e, st));
     NP_CHK(hipMemsetAsync(e->nnew.p, 0, 4 * (size_t)n_slots, st));
     triangulate_kernel<<<dim3((maxp + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e));
     NP_CHK(hipGetLastError());
+    NP_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
 int orbn_fetch(orbn_engine *e, int slot, float *x3d, uint8_t *ok, int32_t *nnew) {
     if (!e || slot < 0 || slot >= e->nslots) return ORBX_EINVAL;
     NP_CHK(hipSetDevice(e->device));
-    NP_CHK(hipDeviceSynchronize());
+    NP_CHK(hipStreamWaitEvent(e->stream, e->done, 0));
     const size_t s = (size_t)slot, P = (size_t)e->cap_pairs, n = (size_t)e->h[slot].npairs;
-    if (nnew) NP_CHK(hipMemcpy(nnew, (char *)e->nnew.p + 4 * s, 4, hipMemcpyDeviceToHost));
+    if (nnew) NP_CHK(d2h_sync(nnew, (char *)e->nnew.p + 4 * s, 4, e->stream));
     if (n) {
-        if (x3d) NP_CHK(hipMemcpy(x3d, (char *)e->x3d.p + 12 * s * P, 12 * n, hipMemcpyDeviceToHost));
-        if (ok) NP_CHK(hipMemcpy(ok, (char *)e->ok.p + s * P, n, hipMemcpyDeviceToHost));
+        if (x3d) NP_CHK(d2h_sync(x3d, (char *)e->x3d.p + 12 * s * P, 12 * n, e->stream));
+        if (ok) NP_CHK(d2h_sync(ok, (char *)e->ok.p + s * P, n, e->stream));
     }
     return ORBX_OK;
 }

@@ -442,6 +442,8 @@ using namespace orbpose;
 struct orbp_engine {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;          // end of the last run (fetch waits on it only)
+    hipStream_t done_stream = nullptr;
     int nslots = 0, cap = 0;
     DevBuf hdr, xw, ob, err, outlier, Tout, nin, iters;
     std::vector<int> n;
@@ -454,7 +456,8 @@ int orbp_create(orbp_engine **out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORBX_EDEVICE;
     orbp_engine *e = new orbp_engine();
-    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        !(e->done = make_done_event())) {
         delete e;
         return ORBX_EDEVICE;
     }
@@ -466,6 +469,7 @@ void orbp_destroy(orbp_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
+    if (e->done) { (void)hipEventSynchronize(e->done); (void)hipEventDestroy(e->done); }
     DevBuf *bufs[] = {&e->hdr, &e->xw, &e->ob, &e->err, &e->outlier, &e->Tout, &e->nin, &e->iters};
     for (DevBuf *b : bufs) b->release();
     delete e;
@@ -502,6 +506,7 @@ int orbp_stage(orbp_engine *e, int slot, const orbp_frame *f) {
     }
     const size_t s = (size_t)slot, C = (size_t)e->cap;
     hipStream_t st = e->stream;
+    PO_CHK(order_after_done(e, st));
     PO_CHK(hipMemcpyAsync((char *)e->hdr.p + sizeof(FrameHdr) * s, &h, sizeof h, hipMemcpyHostToDevice, st));
     if (f->n) {
         PO_CHK(hipMemcpyAsync((char *)e->xw.p + 16 * s * C, xw.data(), 16 * (size_t)f->n, hipMemcpyHostToDevice, st));
@@ -519,15 +524,18 @@ int orbp_run_batch(orbp_engine *e, int n_slots, void *stream) {
     P.hdr = e->hdr.as<FrameHdr>(); P.xw = e->xw.as<float4>(); P.ob = e->ob.as<float4>();
     P.err = e->err.as<double>(); P.outlier = e->outlier.as<uint8_t>(); P.Tout = e->Tout.as<float>();
     P.nin = e->nin.as<int>(); P.iters = e->iters.as<int>(); P.cap = e->cap;
-    pose_opt_kernel<<<n_slots, kThreads, 0, stream ? (hipStream_t)stream : e->stream>>>(P);
+    const hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+    PO_CHK(order_after_done(e, st));
+    pose_opt_kernel<<<n_slots, kThreads, 0, st>>>(P);
     PO_CHK(hipGetLastError());
+    PO_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
 int orbp_fetch(orbp_engine *e, int slot, orbp_result *r) {
     if (!e || !r || slot < 0 || slot >= e->nslots) return ORBX_EINVAL;
     PO_CHK(hipSetDevice(e->device));
-    PO_CHK(hipDeviceSynchronize());
+    PO_CHK(hipStreamWaitEvent(e->stream, e->done, 0));
     hipStream_t st = e->stream;
     const size_t s = (size_t)slot, C = (size_t)e->cap;
     PO_CHK(hipMemcpyAsync(r->Tcw, (char *)e->Tout.p + 64 * s, 64, hipMemcpyDeviceToHost, st));

@@ -313,6 +313,7 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
     a.rmax = 2.0f * smax;
     const size_t slots = (size_t)n_pairs * a.cap;
     a.nrows = g.H + 2;
+    HIPCHK(order_after_done(store, s));
     if (store->d_st_rows.ensure(4 * (size_t)n_pairs * a.nrows)) return ORBX_EDEVICE;
     a.rowtab = store->d_st_rows.as<int>();
     if (store->d_st_sorted.ensure(16 * (size_t)n_pairs * sc) || store->d_st_u.ensure(4 * slots) ||
@@ -332,6 +333,8 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
     stereo_median_cut<<<n_pairs, 256, 4 * sc, s>>>(a, u, d, sad);
     prof_end(store, s, ph, "stereo_median_cut");
     HIPCHK(hipGetLastError());
+    HIPCHK(mark_done(store, s));
+    store->st_pairs = n_pairs;
     return ORBX_OK;
 }
 
@@ -349,20 +352,31 @@ static StereoSide side_of(orbx_engine *e, int base, int step) {
     return s;
 }
 
-// ---- brute-force Hamming best / second best (ORBmatcher scan core)
-__global__ __launch_bounds__(256) void hamming_best2_kernel(const uint8_t *q, int nq, const uint8_t *db,
-                                                            int ndb, int *best_idx, int *best_d,
-                                                            int *second_d) {
+// ---- Hamming best / second best (the scan core every ORBmatcher search shares)
+// One wavefront per query. The reference loops over its candidates in order with
+//   if (dist < bestDist) { bestDist2 = bestDist; bestDist = dist; bestIdx = idx; }
+//   else if (dist < bestDist2) bestDist2 = dist;
+// (e.g. ORBmatcher.cc:639-668), i.e. best = the FIRST minimum in candidate order and second =
+// the minimum over the remaining candidates. Each lane keeps (dist << 20 | position) over its
+// strided subset, then a butterfly merge keeps the lexicographic minimum as best and folds the
+// other key into the second distance. CAND: candidates cand_idx[off[i] .. off[i+1]) (list
+// order = position order); otherwise the whole database in index order.
+template <bool CAND>
+__global__ __launch_bounds__(256) void hamming_best2_kernel(const uint8_t *q, int nq, const uint8_t *db, int ndb,
+                                                            const int *cand_off, const int *cand_idx, int *best_idx,
+                                                            int *best_d, int *second_d) {
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + wave_id();
     if (i >= nq) return;
     const uint8_t *qi = q + (long long)i * 32;
-    // per-lane (best, second) over its strided subset in ascending index order, then a
-    // merge that keeps the (dist, index) lexicographic minimum as best.
-    unsigned b1 = 0xFFFFFFFFu;   // (dist << 20) | idx
+    int c0 = 0, n = ndb;
+    if (CAND) { c0 = cand_off[i]; n = cand_off[i + 1] - c0; }
+    unsigned b1 = 0xFFFFFFFFu;   // (dist << 20) | position
     int d2 = INT_MAX;
-    for (int j = lane; j < ndb; j += 64) {
-        const int d = hamming32(qi, db + (long long)j * 32);
+    for (int j = lane; j < n; j += 64) {
+        const int idx = CAND ? cand_idx[c0 + j] : j;
+        const int d = (unsigned)idx < (unsigned)ndb ? hamming32(qi, db + (long long)idx * 32) : 256 + 1;
+        if (d > 256) continue;   // out-of-range candidate index: skipped (the host checks them)
         const unsigned key = ((unsigned)d << 20) | (unsigned)j;
         if (key < b1) {
             if (b1 != 0xFFFFFFFFu) d2 = min(d2, (int)(b1 >> 20));
@@ -382,7 +396,8 @@ __global__ __launch_bounds__(256) void hamming_best2_kernel(const uint8_t *q, in
         d2 = s2;
     }
     if (lane == 0) {
-        best_idx[i] = b1 == 0xFFFFFFFFu ? -1 : (int)(b1 & 0xFFFFF);
+        const int pos = (int)(b1 & 0xFFFFF);
+        best_idx[i] = b1 == 0xFFFFFFFFu ? -1 : (CAND ? cand_idx[c0 + pos] : pos);
         best_d[i] = b1 == 0xFFFFFFFFu ? INT_MAX : (int)(b1 >> 20);
         second_d[i] = d2;
     }
@@ -398,7 +413,10 @@ int orbm_stereo_match(orbx_engine *left, orbx_engine *right, float mbf, float mb
     if (left->last_n < 1 || right->last_n < 1) return ORBX_ESTATE;
     if (left->W != right->W || left->H != right->H || left->p.nlevels != right->p.nlevels) return ORBX_EINVAL;
     HIPCHK(hipSetDevice(left->device));
-    HIPCHK(hipStreamSynchronize(right->stream));
+    // the right extractor ran on its own stream / thread (Frame.cc:144-153): order after it
+    // and after the left one's last launch, on the left stream only
+    HIPCHK(hipStreamWaitEvent(left->stream, right->done, 0));
+    HIPCHK(hipStreamWaitEvent(left->stream, left->done, 0));
     StereoArgs a{};
     a.L = side_of(left, 0, 1);
     a.R = side_of(right, 0, 1);
@@ -408,13 +426,19 @@ int orbm_stereo_match(orbx_engine *left, orbx_engine *right, float mbf, float mb
     a.mb = mb;
     int rc = run_stereo(left->g, a, 1, left, left->stream);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(left->stream));
     int cnt = 0;
-    HIPCHK(hipMemcpy(&cnt, left->d_cnt.as<int>(), sizeof(int), hipMemcpyDeviceToHost));
+    {
+        HostCopy hc(left->stream, nullptr);   // same stream as the launches
+        hc.d2h(&cnt, left->d_cnt.as<int>(), sizeof(int));
+        if (hc.finish()) return ORBX_EDEVICE;
+    }
     if (n != cnt) return ORBX_EINVAL;
     if (n > 0) {
-        HIPCHK(hipMemcpy(u_right, left->d_st_u.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(depth, left->d_st_depth.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        if (!u_right || !depth) return ORBX_EINVAL;
+        HostCopy hc(left->stream, nullptr);
+        hc.d2h(u_right, left->d_st_u.p, 4 * (size_t)n);
+        hc.d2h(depth, left->d_st_depth.p, 4 * (size_t)n);
+        if (hc.finish()) return ORBX_EDEVICE;
     }
     return ORBX_OK;
 }
@@ -439,37 +463,127 @@ int orbm_stereo_results(orbx_engine *e, const float **d_u_right, const float **d
 }
 
 int orbm_stereo_fetch(orbx_engine *e, int pair, float *u_right, float *depth, int cap) {
-    if (!e || !e->d_st_u.p) return ORBX_ESTATE;
+    if (!e) return ORBX_EINVAL;
+    if (!e->d_st_u.p || e->st_pairs == 0) return ORBX_ESTATE;
+    if (pair < 0 || pair >= e->st_pairs) return ORBX_EINVAL;
     const int kc = e->g.out_base[e->g.nlevels];
     if (cap < kc) return ORBX_ECAP;
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(u_right, e->d_st_u.as<float>() + (size_t)pair * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(depth, e->d_st_depth.as<float>() + (size_t)pair * kc, 4 * (size_t)kc, hipMemcpyDeviceToHost));
+    HostCopy hc(e->stream, e->done);
+    hc.d2h(u_right, e->d_st_u.as<float>() + (size_t)pair * kc, 4 * (size_t)kc);
+    hc.d2h(depth, e->d_st_depth.as<float>() + (size_t)pair * kc, 4 * (size_t)kc);
+    return hc.finish();
+}
+
+int orbm_create(float nnratio, int check_ori, orbm_matcher **out) {
+    if (!out) return ORBX_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ORBX_EDEVICE;
+    orbm_matcher *m = new orbm_matcher();
+    m->nnratio = nnratio;
+    m->check_ori = check_ori != 0;
+    if (hipGetDevice(&m->device) != hipSuccess || hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
+        !(m->done = make_done_event())) {
+        if (m->stream) (void)hipStreamDestroy(m->stream);
+        delete m;
+        return ORBX_EDEVICE;
+    }
+    *out = m;
     return ORBX_OK;
 }
 
-int orbm_hamming_best2(const uint8_t *q, int nq, const uint8_t *db, int ndb, int *best_idx, int *best_d,
-                       int *second_d) {
-    if (nq < 0 || ndb < 0 || ndb >= (1 << 20)) return ORBX_EINVAL;
+void orbm_destroy(orbm_matcher *m) {
+    if (!m) return;
+    (void)hipSetDevice(m->device);
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    if (m->done) { (void)hipEventSynchronize(m->done); (void)hipEventDestroy(m->done); }
+    DevBuf *bufs[] = {&m->q, &m->db, &m->off, &m->idx, &m->out, &m->kun, &m->desc, &m->cnt, &m->keys,
+                      &m->nkeys, &m->prev, &m->m12, &m->nmatch, &m->list, &m->lcnt};
+    for (DevBuf *b : bufs) b->release();
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+}
+
+int orbm_hamming_best2_cand_device(orbm_matcher *m, const uint8_t *d_q, int nq, const uint8_t *d_db, int ndb,
+                                   const int32_t *d_cand_off, const int32_t *d_cand_idx, int32_t *d_best_idx,
+                                   int32_t *d_best_d, int32_t *d_second_d, void *stream) {
+    if (!m || nq < 0 || ndb < 0 || ndb >= (1 << 20)) return ORBX_EINVAL;
+    if (nq == 0) return ORBX_OK;
+    if (!d_q || (ndb > 0 && !d_db) || !d_best_idx || !d_best_d || !d_second_d) return ORBX_EINVAL;
+    HIPCHK(hipSetDevice(m->device));
+    const hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+    HIPCHK(order_after_done(m, s));
+    if (d_cand_off) {
+        if (!d_cand_idx) return ORBX_EINVAL;
+        hamming_best2_kernel<true><<<(nq + 3) / 4, 256, 0, s>>>(d_q, nq, d_db, ndb, d_cand_off, d_cand_idx, d_best_idx,
+                                                                 d_best_d, d_second_d);
+    } else {
+        hamming_best2_kernel<false><<<(nq + 3) / 4, 256, 0, s>>>(d_q, nq, d_db, ndb, nullptr, nullptr, d_best_idx,
+                                                                  d_best_d, d_second_d);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(mark_done(m, s));
+    return ORBX_OK;
+}
+
+int orbm_hamming_best2_cand(orbm_matcher *m, const uint8_t *q, int nq, const uint8_t *db, int ndb,
+                            const int32_t *cand_off, const int32_t *cand_idx, int32_t *best_idx, int32_t *best_d,
+                            int32_t *second_d) {
+    if (!m || nq < 0 || ndb < 0 || ndb >= (1 << 20)) return ORBX_EINVAL;
     if (nq == 0) return ORBX_OK;
     if (!q || !best_idx || !best_d || !second_d || (ndb > 0 && !db)) return ORBX_EINVAL;
-    uint8_t *dq = nullptr, *ddb = nullptr;
-    int *dout = nullptr;
-    HIPCHK(hipMalloc(&dq, 32 * (size_t)nq));
-    HIPCHK(hipMalloc(&ddb, 32 * (size_t)std::max(ndb, 1)));
-    HIPCHK(hipMalloc(&dout, 12 * (size_t)nq));
-    HIPCHK(hipMemcpy(dq, q, 32 * (size_t)nq, hipMemcpyHostToDevice));
-    if (ndb > 0) HIPCHK(hipMemcpy(ddb, db, 32 * (size_t)ndb, hipMemcpyHostToDevice));
-    hamming_best2_kernel<<<(nq + 3) / 4, 256>>>(dq, nq, ddb, ndb, dout, dout + nq, dout + 2 * nq);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(best_idx, dout, 4 * (size_t)nq, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(best_d, dout + nq, 4 * (size_t)nq, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(second_d, dout + 2 * nq, 4 * (size_t)nq, hipMemcpyDeviceToHost));
-    (void)hipFree(dq);
-    (void)hipFree(ddb);
-    (void)hipFree(dout);
-    return ORBX_OK;
+    size_t nc = 0;
+    if (cand_off) {   // CSR candidate lists: monotone offsets, indices inside db
+        if (!cand_idx && cand_off[nq] > cand_off[0]) return ORBX_EINVAL;
+        if (cand_off[0] != 0) return ORBX_EINVAL;
+        for (int i = 0; i < nq; i++)
+            if (cand_off[i + 1] < cand_off[i] || cand_off[i + 1] - cand_off[i] >= (1 << 20)) return ORBX_EINVAL;
+        nc = (size_t)cand_off[nq];
+        for (size_t c = 0; c < nc; c++)
+            if (cand_idx[c] < 0 || cand_idx[c] >= ndb) return ORBX_EINVAL;
+    }
+    HIPCHK(hipSetDevice(m->device));
+    HIPCHK(hipStreamWaitEvent(m->stream, m->done, 0));
+    if (m->q.ensure(32 * (size_t)nq) || m->db.ensure(32 * (size_t)std::max(ndb, 1)) || m->out.ensure(12 * (size_t)nq) ||
+        m->off.ensure(4 * ((size_t)nq + 1)) || m->idx.ensure(4 * std::max<size_t>(nc, 1)))
+        return ORBX_EDEVICE;
+    HostCopy up(m->stream, nullptr);
+    up.h2d(m->q.p, q, 32 * (size_t)nq);
+    up.h2d(m->db.p, db, 32 * (size_t)ndb);
+    if (cand_off) {
+        up.h2d(m->off.p, cand_off, 4 * ((size_t)nq + 1));
+        up.h2d(m->idx.p, cand_idx, 4 * nc);
+    }
+    if (up.err != hipSuccess) return ORBX_EDEVICE;
+    int *o = m->out.as<int>();
+    const int rc = orbm_hamming_best2_cand_device(m, m->q.as<uint8_t>(), nq, m->db.as<uint8_t>(), ndb,
+                                                  cand_off ? m->off.as<int>() : nullptr, cand_off ? m->idx.as<int>() : nullptr,
+                                                  o, o + nq, o + 2 * nq, m->stream);
+    if (rc) return rc;
+    HostCopy dn(m->stream, nullptr);
+    dn.d2h(best_idx, o, 4 * (size_t)nq);
+    dn.d2h(best_d, o + nq, 4 * (size_t)nq);
+    dn.d2h(second_d, o + 2 * nq, 4 * (size_t)nq);
+    return dn.finish();
+}
+
+// The brute-force form without a matcher handle: one matcher per calling thread (its own stream
+// and buffers), so concurrent callers never share state or wait for each other.
+int orbm_hamming_best2(const uint8_t *q, int nq, const uint8_t *db, int ndb, int *best_idx, int *best_d,
+                       int *second_d) {
+    struct Tls {
+        orbm_matcher *m = nullptr;
+        ~Tls() { orbm_destroy(m); }
+    };
+    static thread_local Tls tls;
+    if (nq < 0 || ndb < 0 || ndb >= (1 << 20)) return ORBX_EINVAL;
+    if (nq == 0) return ORBX_OK;
+    if (!tls.m) {
+        const int rc = orbm_create(0.6f, 1, &tls.m);
+        if (rc) return rc;
+    }
+    return orbm_hamming_best2_cand(tls.m, q, nq, db, ndb, nullptr, nullptr, best_idx, best_d, second_d);
 }
 
 }  // extern "C"

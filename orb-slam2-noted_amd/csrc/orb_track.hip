@@ -902,6 +902,8 @@ using namespace orbtrack;
 struct orbt_engine {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;          // end of the last run (fetch waits on it only)
+    hipStream_t done_stream = nullptr;
     int nslots = 0, cap_kp = 0, cap_mp = 0, sort_cap = 0;
     DevBuf fr, kun, uR, desc, blocked, keys, cell_start, lkun, last_mp, last_out;
     DevBuf Xw, nrm, mind, maxd, mdesc, mflags;
@@ -988,7 +990,8 @@ int orbt_create(orbt_engine **out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORBX_EDEVICE;
     orbt_engine *e = new orbt_engine();
-    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        !(e->done = make_done_event())) {
         delete e;
         return ORBX_EDEVICE;
     }
@@ -1000,6 +1003,7 @@ void orbt_destroy(orbt_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
+    if (e->done) { (void)hipEventSynchronize(e->done); (void)hipEventDestroy(e->done); }
     DevBuf *bufs[] = {&e->fr, &e->kun, &e->uR, &e->desc, &e->blocked, &e->keys, &e->cell_start, &e->lkun, &e->last_mp,
                       &e->last_out, &e->Xw, &e->nrm, &e->mind, &e->maxd, &e->mdesc, &e->mflags, &e->in_view, &e->px,
                       &e->py, &e->pxr, &e->vcos, &e->level, &e->cand, &e->ncand, &e->owner, &e->nmatch, &e->hist_idx,
@@ -1043,6 +1047,7 @@ int orbt_stage(orbt_engine *e, int slot, const orbt_frame *F, const orbt_mappoin
     if (F->nlevels < 1 || F->nlevels > 16) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
+    TR_CHK(order_after_done(e, st));   // a run on another stream may still read the slot
     FrameDev &d = e->hfr[slot];
     d = FrameDev{};
     fill_frame(d, F);
@@ -1091,6 +1096,7 @@ int orbt_run_local_batch(orbt_engine *e, int n_slots, float view_cos_limit, floa
     if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = pick(e, stream);
+    TR_CHK(order_after_done(e, st));
     if (grid(e, n_slots, st)) return ORBX_EDEVICE;
     const int mm = std::max(1, max_n(e, 0, n_slots));
     track_local_cand_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), view_cos_limit, th,
@@ -1100,6 +1106,7 @@ int orbt_run_local_batch(orbt_engine *e, int n_slots, float view_cos_limit, floa
                                                                 e->cand.as<Cand>(), e->ncand.as<int>(),
                                                                 e->owner.as<int>(), e->nmatch.as<int>());
     TR_CHK(hipGetLastError());
+    TR_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
@@ -1107,6 +1114,7 @@ int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int ch
     if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = pick(e, stream);
+    TR_CHK(order_after_done(e, st));
     if (grid(e, n_slots, st)) return ORBX_EDEVICE;
     const int nl = std::max(1, max_n(e, 1, n_slots));
     track_frame_cand_kernel<<<dim3((nl + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, mono, kModeMotion,
@@ -1117,6 +1125,7 @@ int orbt_run_frame_batch(orbt_engine *e, int n_slots, float th, int mono, int ch
                                                                 e->nmatch.as<int>(), e->hist_idx.as<int>(),
                                                                 e->hist_bin.as<int8_t>());
     TR_CHK(hipGetLastError());
+    TR_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
@@ -1124,6 +1133,7 @@ int orbt_run_reloc_batch(orbt_engine *e, int n_slots, float th, int orb_dist, in
     if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = pick(e, stream);
+    TR_CHK(order_after_done(e, st));
     if (grid(e, n_slots, st)) return ORBX_EDEVICE;
     const int nl = std::max(1, max_n(e, 1, n_slots));
     track_frame_cand_kernel<<<dim3((nl + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, 0, kModeReloc,
@@ -1133,6 +1143,7 @@ int orbt_run_reloc_batch(orbt_engine *e, int n_slots, float th, int orb_dist, in
                                                                 e->owner.as<int>(), e->nmatch.as<int>(),
                                                                 e->hist_idx.as<int>(), e->hist_bin.as<int8_t>());
     TR_CHK(hipGetLastError());
+    TR_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
@@ -1140,7 +1151,7 @@ int orbt_fetch(orbt_engine *e, int slot, orbt_view *view, int32_t *owner, int32_
     if (!e || slot < 0 || slot >= e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
-    TR_CHK(hipDeviceSynchronize());
+    TR_CHK(hipStreamWaitEvent(e->stream, e->done, 0));
     const FrameDev &d = e->hfr[slot];
     const size_t K = (size_t)e->cap_kp, M = (size_t)e->cap_mp, s = (size_t)slot, m = (size_t)d.n_mp;
     auto dn = [&](void *dst, const DevBuf &b, size_t off, size_t bytes) -> bool {
@@ -1225,6 +1236,7 @@ int orbt_run_sim3_batch(orbt_engine *e, int n_slots, int th, void *stream) {
     if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = pick(e, stream);
+    TR_CHK(order_after_done(e, st));
     if (grid(e, n_slots, st)) return ORBX_EDEVICE;
     const int mm = std::max(1, max_n(e, 0, n_slots));
     const float thf = (float)th;
@@ -1235,6 +1247,7 @@ int orbt_run_sim3_batch(orbt_engine *e, int n_slots, int th, void *stream) {
                                                                 e->owner.as<int>(), e->nmatch.as<int>(),
                                                                 e->hist_idx.as<int>(), e->hist_bin.as<int8_t>());
     TR_CHK(hipGetLastError());
+    TR_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
@@ -1269,11 +1282,13 @@ int orbt_run_fuse_sim3_batch(orbt_engine *e, int n_slots, float th, void *stream
     if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = pick(e, stream);
+    TR_CHK(order_after_done(e, st));
     if (grid(e, n_slots, st)) return ORBX_EDEVICE;
     const int mm = std::max(1, max_n(e, 0, n_slots));
     track_fuse_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, 1, e->fuse_idx.as<int>(),
                                                                        e->fuse_dist.as<int>());
     TR_CHK(hipGetLastError());
+    TR_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
@@ -1332,7 +1347,9 @@ int orbt_stage_search_by_sim3(orbt_engine *e, int pair, const orbt_frame *kf1, c
             fd.sT[4 * r + 3] = sts[d][r];
         }
         fd.pfx = kf1->fx; fd.pfy = kf1->fy; fd.pcx = kf1->cx; fd.pcy = kf1->cy;
-        TR_CHK(hipMemcpy((char *)e->fr.p + sizeof(FrameDev) * (size_t)slot, &fd, sizeof(FrameDev), hipMemcpyHostToDevice));
+        TR_CHK(hipMemcpyAsync((char *)e->fr.p + sizeof(FrameDev) * (size_t)slot, &fd, sizeof(FrameDev), hipMemcpyHostToDevice,
+                              e->stream));
+        TR_CHK(hipStreamSynchronize(e->stream));
     }
     return ORBX_OK;
 }
@@ -1341,23 +1358,25 @@ int orbt_run_sim3_match_batch(orbt_engine *e, int n_pairs, float th, void *strea
     if (!e || n_pairs <= 0 || 2 * n_pairs > e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = pick(e, stream);
+    TR_CHK(order_after_done(e, st));
     const int ns = 2 * n_pairs;
     if (grid(e, ns, st)) return ORBX_EDEVICE;
     const int nl = std::max(1, max_n(e, 1, ns));
     track_sim3_match_kernel<<<dim3((nl + 255) / 256, ns), 256, 0, st>>>(make_slots(e), th, e->owner.as<int>());
     TR_CHK(hipGetLastError());
+    TR_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
 int orbt_fetch_search_by_sim3(orbt_engine *e, int pair, const int32_t *kf2_mp, int32_t *matches12, int32_t *nfound) {
     if (!e || pair < 0 || 2 * pair + 1 >= e->nslots || !kf2_mp || !matches12 || !nfound) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
-    TR_CHK(hipDeviceSynchronize());
+    TR_CHK(hipStreamWaitEvent(e->stream, e->done, 0));
     const size_t K = (size_t)e->cap_kp;
     const int N1 = e->hfr[2 * pair].n_last, N2 = e->hfr[2 * pair + 1].n_last;
     std::vector<int32_t> v1((size_t)N1 + 1), v2((size_t)N2 + 1);
-    if (N1) TR_CHK(hipMemcpy(v1.data(), (char *)e->owner.p + 4 * K * (size_t)(2 * pair), 4 * (size_t)N1, hipMemcpyDeviceToHost));
-    if (N2) TR_CHK(hipMemcpy(v2.data(), (char *)e->owner.p + 4 * K * (size_t)(2 * pair + 1), 4 * (size_t)N2, hipMemcpyDeviceToHost));
+    if (N1) TR_CHK(d2h_sync(v1.data(), (char *)e->owner.p + 4 * K * (size_t)(2 * pair), 4 * (size_t)N1, e->stream));
+    if (N2) TR_CHK(d2h_sync(v2.data(), (char *)e->owner.p + 4 * K * (size_t)(2 * pair + 1), 4 * (size_t)N2, e->stream));
     int nf = 0;
     for (int i1 = 0; i1 < N1; i1++) {   // agreement check (ORBmatcher.cc:1706-1720)
         const int idx2 = v1[i1];
@@ -1389,21 +1408,23 @@ int orbt_run_fuse_batch(orbt_engine *e, int n_slots, float th, void *stream) {
     if (!e || n_slots <= 0 || n_slots > e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
     hipStream_t st = pick(e, stream);
+    TR_CHK(order_after_done(e, st));
     if (grid(e, n_slots, st)) return ORBX_EDEVICE;
     const int mm = std::max(1, max_n(e, 0, n_slots));
     track_fuse_kernel<<<dim3((mm + 255) / 256, n_slots), 256, 0, st>>>(make_slots(e), th, 0, e->fuse_idx.as<int>(),
                                                                        e->fuse_dist.as<int>());
     TR_CHK(hipGetLastError());
+    TR_CHK(mark_done(e, st));
     return ORBX_OK;
 }
 
 int orbt_fetch_fuse(orbt_engine *e, int slot, int32_t *best_idx, int32_t *best_dist) {
     if (!e || slot < 0 || slot >= e->nslots) return ORBX_EINVAL;
     TR_CHK(hipSetDevice(e->device));
-    TR_CHK(hipDeviceSynchronize());
+    TR_CHK(hipStreamWaitEvent(e->stream, e->done, 0));
     const size_t M = (size_t)e->cap_mp, s = (size_t)slot, m = (size_t)e->hfr[slot].n_mp;
-    if (m && best_idx) TR_CHK(hipMemcpy(best_idx, (char *)e->fuse_idx.p + 4 * s * M, 4 * m, hipMemcpyDeviceToHost));
-    if (m && best_dist) TR_CHK(hipMemcpy(best_dist, (char *)e->fuse_dist.p + 4 * s * M, 4 * m, hipMemcpyDeviceToHost));
+    if (m && best_idx) TR_CHK(d2h_sync(best_idx, (char *)e->fuse_idx.p + 4 * s * M, 4 * m, e->stream));
+    if (m && best_dist) TR_CHK(d2h_sync(best_dist, (char *)e->fuse_dist.p + 4 * s * M, 4 * m, e->stream));
     return ORBX_OK;
 }
 

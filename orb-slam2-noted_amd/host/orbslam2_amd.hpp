@@ -4,7 +4,7 @@
 // these into the reference tree unchanged for Tracking.cc / LocalMapping.cc.
 //
 //   orbslam2_amd::ORBextractor   <- ORB_SLAM2::ORBextractor (include/ORBextractor.h:80-216)
-//   orbslam2_amd::ORBmatcher     <- ORB_SLAM2::ORBmatcher   (include/ORBmatcher.h:57-65)
+//   orbslam2_amd::ORBmatcher     <- ORB_SLAM2::ORBmatcher   (include/ORBmatcher.h:57-65, 169)
 //   orbslam2_amd::ComputeStereoMatches <- Frame::ComputeStereoMatches (Frame.cc:831-1128)
 //   orbslam2_amd::Optimizer::LocalBundleAdjustment <- Optimizer.h:112 (graph supplied flat)
 //   orbslam2_amd::Optimizer::PoseOptimization     <- Optimizer.h:105 (edges supplied flat)
@@ -102,10 +102,25 @@ inline void ComputeStereoMatches(ORBextractor &left, ORBextractor &right, int N,
           "orbm_stereo_match");
 }
 
+// The Frame members SearchForInitialization reads (Frame.h): mvKeysUn, mDescriptors (N x 32)
+// and the static image bounds mnMinX / mnMaxX / mnMinY / mnMaxY.
+struct InitFrame {
+    std::vector<KeyPoint> mvKeysUn;
+    std::vector<uint8_t> mDescriptors;
+    float mnMinX = 0, mnMaxX = 0, mnMinY = 0, mnMaxY = 0;
+};
+
+struct Point2f {   // cv::Point2f
+    float x, y;
+};
+
 class ORBmatcher {
 public:
     static const int TH_LOW = 50, TH_HIGH = 100, HISTO_LENGTH = 30;
     explicit ORBmatcher(float nnratio = 0.6f, bool checkOri = true) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
+    ~ORBmatcher() { orbm_destroy(m_); }
+    ORBmatcher(const ORBmatcher &) = delete;
+    ORBmatcher &operator=(const ORBmatcher &) = delete;
     // DescriptorDistance (ORBmatcher.cc:2123-2143)
     static int DescriptorDistance(const uint8_t *a, const uint8_t *b) {
         int d = 0;
@@ -119,6 +134,37 @@ public:
         best.resize(nq); bestDist.resize(nq); secondDist.resize(nq);
         check(orbm_hamming_best2(q.data(), nq, db.data(), ndb, best.data(), bestDist.data(), secondDist.data()),
               "orbm_hamming_best2");
+    }
+    // best / second over caller-built candidate lists (CSR: query i's candidates are
+    // candIdx[candOff[i] .. candOff[i+1]) into db), first minimum in list order
+    void HammingBest2(const std::vector<uint8_t> &q, const std::vector<uint8_t> &db, const std::vector<int32_t> &candOff,
+                      const std::vector<int32_t> &candIdx, std::vector<int32_t> &best, std::vector<int32_t> &bestDist,
+                      std::vector<int32_t> &secondDist) {
+        const int nq = (int)(q.size() / 32), ndb = (int)(db.size() / 32);
+        if ((int)candOff.size() != nq + 1) throw std::invalid_argument("candOff needs nq + 1 entries");
+        best.resize(nq); bestDist.resize(nq); secondDist.resize(nq);
+        check(orbm_hamming_best2_cand(handle(), q.data(), nq, db.data(), ndb, candOff.data(), candIdx.data(), best.data(),
+                                      bestDist.data(), secondDist.data()),
+              "orbm_hamming_best2_cand");
+    }
+    // SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) (ORBmatcher.cc:580-748):
+    // vbPrevMatched is read as the window centres and updated with the matched F2 positions.
+    int SearchForInitialization(const InitFrame &F1, const InitFrame &F2, std::vector<Point2f> &vbPrevMatched,
+                                std::vector<int> &vnMatches12, int windowSize = 10) {
+        static_assert(sizeof(Point2f) == 8 && sizeof(int) == 4, "Point2f / int layout");
+        const int n1 = (int)F1.mvKeysUn.size();
+        vnMatches12.assign(n1, -1);
+        if (vbPrevMatched.size() < (size_t)n1) throw std::invalid_argument("vbPrevMatched shorter than F1");
+        if (F1.mDescriptors.size() < (size_t)n1 * 32 || F2.mDescriptors.size() < F2.mvKeysUn.size() * 32)
+            throw std::invalid_argument("descriptors shorter than keypoints");
+        const orbm_frame f1{n1, F1.mvKeysUn.data(), F1.mDescriptors.data(), F1.mnMinX, F1.mnMaxX, F1.mnMinY, F1.mnMaxY};
+        const orbm_frame f2{(int32_t)F2.mvKeysUn.size(), F2.mvKeysUn.data(), F2.mDescriptors.data(), F2.mnMinX, F2.mnMaxX,
+                            F2.mnMinY, F2.mnMaxY};
+        int32_t nmatches = 0;
+        check(orbm_search_for_initialization(handle(), &f1, &f2, reinterpret_cast<float *>(vbPrevMatched.data()),
+                                             vnMatches12.data(), windowSize, &nmatches),
+              "orbm_search_for_initialization");
+        return nmatches;
     }
     // SearchByProjection(Frame&, const vector<MapPoint*>&, th) with the in-view selection of
     // Tracking::SearchLocalPoints (isInFrustum(pMP, 0.5)); owner[i] = index into M assigned to
@@ -197,6 +243,11 @@ public:
     bool mbCheckOrientation;
 
 private:
+    orbm_matcher *handle() {   // created on first use: matchers are cheap stack objects in the reference
+        if (!m_) check(orbm_create(mfNNratio, mbCheckOrientation ? 1 : 0, &m_), "orbm_create");
+        return m_;
+    }
+    orbm_matcher *m_ = nullptr;
     static orbb_engine *bow() {
         struct H {
             orbb_engine *h = nullptr;

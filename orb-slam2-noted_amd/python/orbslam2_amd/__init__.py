@@ -70,6 +70,11 @@ SIGNATURES = [
     ("orbm_stereo_results", _I, [_P, _P, _P]),
     ("orbm_stereo_fetch", _I, [_P, _I, _P, _P, _I]),
     ("orbm_hamming_best2", _I, [_P, _I, _P, _I, _P, _P, _P]),
+    ("orbm_create", _I, [_F, _I, _P]),
+    ("orbm_destroy", None, [_P]),
+    ("orbm_hamming_best2_cand", _I, [_P, _P, _I, _P, _I, _P, _P, _P, _P, _P]),
+    ("orbm_hamming_best2_cand_device", _I, [_P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
+    ("orbm_search_for_initialization", _I, [_P, _P, _P, _P, _P, _I, _P]),
     ("orbslam2_amd_version", C.c_char_p, []),
     ("orbslam2_amd_device_count", _I, []),
     ("orbslam2_amd_device_sync", _I, []),
@@ -468,17 +473,38 @@ def compute_stereo_matches(left: ORBextractor, right: ORBextractor, n_left: int,
     return u[:n_left], d[:n_left]
 
 
+class OrbmFrame(C.Structure):
+    """orbm_frame: the Frame members SearchForInitialization reads (include/Frame.h)."""
+    _fields_ = [("n", C.c_int32), ("keys_un", C.c_void_p), ("desc", C.c_void_p), ("min_x", C.c_float),
+                ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float)]
+
+
 class ORBmatcher:
-    """ORBmatcher Hamming core (ORBmatcher.h:57-65)."""
+    """ORBmatcher(nnratio=0.6, checkOri=True) (ORBmatcher.h:57): a matcher handle with its own HIP
+    stream (orbm_create), DescriptorDistance scans and SearchForInitialization on host frames."""
 
     TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
 
     def __init__(self, nnratio: float = 0.6, checkOri: bool = True):
         self.mfNNratio = nnratio
         self.mbCheckOrientation = checkOri
+        self._h = C.c_void_p()
+        _check(lib().orbm_create(nnratio, 1 if checkOri else 0, C.byref(self._h)), "orbm_create")
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().orbm_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     @staticmethod
     def hamming_best2(q: np.ndarray, db: np.ndarray):
+        """Brute force over db (orbm_hamming_best2, per-thread matcher)."""
         q = np.ascontiguousarray(q, np.uint8)
         db = np.ascontiguousarray(db, np.uint8)
         n = len(q)
@@ -487,6 +513,45 @@ class ORBmatcher:
         sd = np.zeros(max(n, 1), np.int32)
         _check(lib().orbm_hamming_best2(_p(q), n, _p(db), len(db), _p(bi), _p(bd), _p(sd)), "orbm_hamming_best2")
         return bi[:n], bd[:n], sd[:n]
+
+    def hamming_best2_cand(self, q: np.ndarray, db: np.ndarray, cand_off=None, cand_idx=None):
+        """Best / second over CSR candidate lists cand_idx[cand_off[i]:cand_off[i+1]] (None: all of db)."""
+        q = np.ascontiguousarray(q, np.uint8)
+        db = np.ascontiguousarray(db, np.uint8)
+        n = len(q)
+        bi = np.zeros(max(n, 1), np.int32)
+        bd = np.zeros(max(n, 1), np.int32)
+        sd = np.zeros(max(n, 1), np.int32)
+        off = idx = None
+        if cand_off is not None:
+            off = np.ascontiguousarray(cand_off, np.int32)
+            idx = np.ascontiguousarray(cand_idx if cand_idx is not None else np.zeros(0), np.int32)
+            if len(idx) == 0:
+                idx = np.zeros(1, np.int32)
+        _check(lib().orbm_hamming_best2_cand(self._h, _p(q), n, _p(db), len(db), _p(off) if off is not None else None,
+                                             _p(idx) if idx is not None else None, _p(bi), _p(bd), _p(sd)),
+               "orbm_hamming_best2_cand")
+        return bi[:n], bd[:n], sd[:n]
+
+    def SearchForInitialization(self, F1, F2, vbPrevMatched: np.ndarray, windowSize: int = 10):
+        """SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) on host frames.
+        F = (keys_un KP_DTYPE array, desc n x 32, (minX, maxX, minY, maxY)). vbPrevMatched (n1 x 2
+        float32) is updated in place, as the reference's reference argument. -> (nmatches, vnMatches12)."""
+        def frame(F):
+            ku, de, b = F
+            ku = np.ascontiguousarray(ku, KP_DTYPE)
+            de = np.ascontiguousarray(de, np.uint8)
+            return OrbmFrame(len(ku), ku.ctypes.data if len(ku) else None, de.ctypes.data if len(ku) else None,
+                             *[float(v) for v in b]), (ku, de)
+        f1, keep1 = frame(F1)
+        f2, keep2 = frame(F2)
+        if vbPrevMatched.dtype != np.float32 or not vbPrevMatched.flags.c_contiguous:
+            raise ValueError("vbPrevMatched must be a C-contiguous float32 (n1, 2) array (updated in place)")
+        m12 = np.full(max(f1.n, 1), -1, np.int32)
+        n = C.c_int32()
+        _check(lib().orbm_search_for_initialization(self._h, C.byref(f1), C.byref(f2), _p(vbPrevMatched), _p(m12),
+                                                    int(windowSize), C.byref(n)), "orbm_search_for_initialization")
+        return n.value, m12[: f1.n]
 
 
 class LbaProblem(C.Structure):

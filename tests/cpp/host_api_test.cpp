@@ -7,7 +7,15 @@
 //   host_api_test pose <edges.bin> <out.bin>
 //   host_api_test bow <vocab.txt> <desc.u8> <n> <levelsup> <out.bin>
 //   host_api_test newpts <problem.bin> <out.bin>
+//   host_api_test concurrent <left.u8> <right.u8> <w> <h> <nfeat> <mbf> <mb> <problem.bin> <rounds> <out.bin>
+//     Frame.cc:144-153 + LocalMapping.cc:116-118 concurrency: every round runs the left and right
+//     ORBextractor on two std::threads while a third thread keeps running
+//     Optimizer::LocalBundleAdjustment; each round's keypoints / descriptors / stereo must equal the
+//     serial run's bytes, every LocalBA result is written out for the tolerance check.
+#include <atomic>
+#include <chrono>
 #include <cstdio>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -29,8 +37,90 @@ template <class T> static void put(std::ofstream &o, const std::vector<T> &v) {
     o.write((const char *)v.data(), sizeof(T) * v.size());
 }
 
+static lba_problem read_lba(const std::vector<uint8_t> &b) {
+    const int32_t *hdr = (const int32_t *)b.data();
+    const int np = hdr[0], nq = hdr[1], ne = hdr[2];
+    const uint8_t *p = b.data() + 12;
+    lba_problem g{};
+    g.n_poses = np; g.n_points = nq; g.n_edges = ne;
+    g.pose_id = (const int32_t *)p; p += 4 * np;
+    g.pose_fixed = p; p += np; p += (4 - (np % 4)) % 4;
+    g.pose_Tcw = (const float *)p; p += 4 * 16 * np;
+    g.pose_cam = (const float *)p; p += 4 * 5 * np;
+    g.point_id = (const int32_t *)p; p += 4 * nq;
+    g.point_Xw = (const float *)p; p += 4 * 3 * nq;
+    g.edge_point = (const int32_t *)p; p += 4 * ne;
+    g.edge_pose = (const int32_t *)p; p += 4 * ne;
+    g.edge_obs = (const float *)p; p += 4 * 3 * ne;
+    g.edge_inv_sigma2 = (const float *)p;
+    return g;
+}
+
+static int run_concurrent(char **argv) {
+    auto L = read_file(argv[2]), R = read_file(argv[3]);
+    const int w = atoi(argv[4]), h = atoi(argv[5]), nf = atoi(argv[6]);
+    const float mbf = (float)atof(argv[7]), mb = (float)atof(argv[8]);
+    auto pb = read_file(argv[9]);
+    const lba_problem g = read_lba(pb);
+    const int rounds = atoi(argv[10]);
+    ORBextractor exL(nf, 1.2f, 8, 20, 7), exR(nf, 1.2f, 8, 20, 7);
+    // serial reference run
+    std::vector<KeyPoint> kL0, kR0;
+    std::vector<uint8_t> dL0, dR0;
+    exL(ImageU8{L.data(), w, h, w}, kL0, dL0);
+    exR(ImageU8{R.data(), w, h, w}, kR0, dR0);
+    std::vector<float> u0, z0;
+    ComputeStereoMatches(exL, exR, (int)kL0.size(), mbf, mb, u0, z0);
+    // LocalMapping thread: LocalBA back to back until the tracking rounds are done
+    std::atomic<bool> tracking_done{false};
+    std::vector<std::vector<float>> lbaT, lbaX;
+    std::vector<std::vector<uint8_t>> lbaE;
+    std::string lba_err;
+    std::thread mapping([&] {
+        try {
+            do {
+                bool stop = false;
+                std::vector<float> T, X;
+                std::vector<uint8_t> er;
+                Optimizer::LocalBundleAdjustment(g, &stop, T, X, er);
+                lbaT.push_back(T); lbaX.push_back(X); lbaE.push_back(er);
+            } while (!tracking_done.load() || lbaT.size() < 2);
+        } catch (const std::exception &e) { lba_err = e.what(); }
+    });
+    int mismatches = 0;
+    double t_total = 0;
+    for (int r = 0; r < rounds; r++) {
+        std::vector<KeyPoint> kL, kR;
+        std::vector<uint8_t> dL, dR;
+        std::string errL, errR;
+        const auto t0 = std::chrono::steady_clock::now();
+        std::thread tl([&] { try { exL(ImageU8{L.data(), w, h, w}, kL, dL); } catch (const std::exception &e) { errL = e.what(); } });
+        std::thread tr([&] { try { exR(ImageU8{R.data(), w, h, w}, kR, dR); } catch (const std::exception &e) { errR = e.what(); } });
+        tl.join();
+        tr.join();
+        if (!errL.empty() || !errR.empty()) throw std::runtime_error("extract thread: " + errL + errR);
+        std::vector<float> u, z;
+        ComputeStereoMatches(exL, exR, (int)kL.size(), mbf, mb, u, z);
+        t_total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        const bool same = kL.size() == kL0.size() && kR.size() == kR0.size() &&
+                          !std::memcmp(kL.data(), kL0.data(), sizeof(KeyPoint) * kL.size()) &&
+                          !std::memcmp(kR.data(), kR0.data(), sizeof(KeyPoint) * kR.size()) && dL == dL0 && dR == dR0 &&
+                          !std::memcmp(u.data(), u0.data(), 4 * u.size()) && !std::memcmp(z.data(), z0.data(), 4 * z.size());
+        mismatches += !same;
+    }
+    tracking_done = true;
+    mapping.join();
+    if (!lba_err.empty()) throw std::runtime_error("LocalBA thread: " + lba_err);
+    std::ofstream o(argv[11], std::ios::binary);
+    put(o, std::vector<int32_t>{mismatches, rounds, (int32_t)lbaT.size()});
+    put(o, std::vector<double>{t_total / rounds});
+    for (size_t i = 0; i < lbaT.size(); i++) { put(o, lbaT[i]); put(o, lbaX[i]); put(o, lbaE[i]); }
+    return 0;
+}
+
 int main(int argc, char **argv) {
     try {
+        if (argc >= 12 && !strcmp(argv[1], "concurrent")) return run_concurrent(argv);
         if (argc >= 4 && !strcmp(argv[1], "newpts")) {
             // problem.bin: int32 n1, n2, npairs; float ratio; per keyframe: keys[n], keys_un[n]
             // (28 B), u_right[n], depth[n], 23 floats (Tcw, Ow, fx fy cx cy invfx invfy mb mbf),
@@ -107,21 +197,7 @@ int main(int argc, char **argv) {
         }
         if (argc >= 4 && !strcmp(argv[1], "lba")) {
             auto b = read_file(argv[2]);
-            const int32_t *hdr = (const int32_t *)b.data();
-            const int np = hdr[0], nq = hdr[1], ne = hdr[2];
-            const uint8_t *p = b.data() + 12;
-            lba_problem g{};
-            g.n_poses = np; g.n_points = nq; g.n_edges = ne;
-            g.pose_id = (const int32_t *)p; p += 4 * np;
-            g.pose_fixed = p; p += np; p += (4 - (np % 4)) % 4;
-            g.pose_Tcw = (const float *)p; p += 4 * 16 * np;
-            g.pose_cam = (const float *)p; p += 4 * 5 * np;
-            g.point_id = (const int32_t *)p; p += 4 * nq;
-            g.point_Xw = (const float *)p; p += 4 * 3 * nq;
-            g.edge_point = (const int32_t *)p; p += 4 * ne;
-            g.edge_pose = (const int32_t *)p; p += 4 * ne;
-            g.edge_obs = (const float *)p; p += 4 * 3 * ne;
-            g.edge_inv_sigma2 = (const float *)p;
+            const lba_problem g = read_lba(b);
             bool stop = false;
             std::vector<float> T, X;
             std::vector<uint8_t> erase;

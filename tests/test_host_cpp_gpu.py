@@ -62,6 +62,65 @@ def test_cpp_stereo(tmp_path, oracle_mod):
     assert u.tobytes() == ru.tobytes() and d.tobytes() == rd.tobytes()
 
 
+def _lba_blob(prob):
+    np_, nq, ne = len(prob["pose_id"]), len(prob["point_id"]), len(prob["edge_point"])
+    parts = [np.array([np_, nq, ne], np.int32).tobytes(), prob["pose_id"].astype(np.int32).tobytes(),
+             prob["pose_fixed"].astype(np.uint8).tobytes(), b"\0" * ((4 - np_ % 4) % 4),
+             prob["pose_Tcw"].astype(np.float32).tobytes(), prob["pose_cam"].astype(np.float32).tobytes(),
+             prob["point_id"].astype(np.int32).tobytes(), prob["point_Xw"].astype(np.float32).tobytes(),
+             prob["edge_point"].astype(np.int32).tobytes(), prob["edge_pose"].astype(np.int32).tobytes(),
+             prob["edge_obs"].astype(np.float32).tobytes(), prob["edge_inv_sigma2"].astype(np.float32).tobytes()]
+    return b"".join(parts)
+
+
+def test_cpp_concurrent_frame_threads_and_localba(tmp_path, oracle_mod):
+    """Frame.cc:144-153 runs the left / right ORBextractor on two std::threads while the
+    LocalMapping thread runs LocalBundleAdjustment (LocalMapping.cc:116-118). 12 rounds of L || R
+    extraction + ComputeStereoMatches with LocalBA running back to back on a third thread: every
+    round bit-exact with the serial run and with the oracle, every LocalBA within 1e-4 of the
+    oracle with the same erase set."""
+    L, R = synth.stereo_pair(376, 1241, 6)
+    (tmp_path / "l.u8").write_bytes(L.tobytes())
+    (tmp_path / "r.u8").write_bytes(R.tobytes())
+    prob = synth.localba_problem(seed=9, n_kf=10, n_points=600)
+    (tmp_path / "p.bin").write_bytes(_lba_blob(prob))
+    mb = float(np.float32(386.1448) / np.float32(718.856))
+    rounds = 12
+    _run("concurrent", tmp_path / "l.u8", tmp_path / "r.u8", 1241, 376, 2000, repr(386.1448), repr(mb),
+         tmp_path / "p.bin", rounds, tmp_path / "o.bin")
+    buf = (tmp_path / "o.bin").read_bytes()
+    hdr, ms = _read_prefix(buf, [np.int32, np.float64])
+    mism, nr, nlba = (int(v) for v in hdr)
+    assert nr == rounds and mism == 0, f"{mism} of {rounds} concurrent rounds differ from the serial run"
+    assert nlba >= 2
+    # serial run vs oracle (extraction + stereo), once
+    exL, exR = oracle_mod.Extractor(2000), oracle_mod.Extractor(2000)
+    kL, dL = exL.extract(L)
+    kR, dR = exR.extract(R)
+    _run("stereo", tmp_path / "l.u8", tmp_path / "r.u8", 1241, 376, 2000, repr(386.1448), repr(mb), tmp_path / "s.bin")
+    u, d = _read(tmp_path / "s.bin", [np.float32, np.float32])
+    ru, rd = oracle_mod.stereo_matches(exL, exR, kL, dL, kR, dR, np.float32(386.1448), np.float32(mb))
+    assert u.tobytes() == ru.tobytes() and d.tobytes() == rd.tobytes()
+    ref = oracle_mod.lba_solve(prob)
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    arrs = _read(tmp_path / "o.bin", [np.int32, np.float64] + [np.float32, np.float32, np.uint8] * nlba)[2:]
+    for i in range(nlba):
+        T, X, er = arrs[3 * i: 3 * i + 3]
+        assert rel(T.reshape(-1, 16).astype(np.float64), ref["pose_Tcw"]) < 1e-4
+        assert rel(X.reshape(-1, 3).astype(np.float64), ref["point_Xw"]) < 1e-4
+        assert np.array_equal(er, ref["edge_erase"])
+
+
+def _read_prefix(buf, dtypes):
+    out, off = [], 0
+    for dt in dtypes:
+        n = int(np.frombuffer(buf, np.int64, 1, off)[0])
+        off += 8
+        out.append(np.frombuffer(buf, dt, n, off).copy())
+        off += n * np.dtype(dt).itemsize
+    return out
+
+
 def test_cpp_localba(tmp_path, oracle_mod):
     prob = synth.localba_problem(seed=9, n_kf=10, n_points=600)
     np_, nq, ne = len(prob["pose_id"]), len(prob["point_id"]), len(prob["edge_point"])
