@@ -97,6 +97,117 @@ def cpu_baseline(pool, n_frames: int):
                               "sample": f"{n_frames} frames one after another, {dt1:.1f} s"}}
 
 
+def cpu_latency(pool, warmup: int, frames: int):
+    """The oracle in SURVEY §8d's latency mode: per stereo frame the left and right extraction on
+    two threads (Frame.cc:144-153 starts two std::threads per frame), then ComputeStereoMatches;
+    median / mean wall time per frame. The oracle's C calls release the GIL."""
+    import threading
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    oracle.build()
+    mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    exL, exR = oracle.Extractor(NFEAT), oracle.Extractor(NFEAT)
+    ms = []
+    for t in range(warmup + frames):
+        L, R = pool[t % len(pool)]
+        res = {}
+        t0 = time.perf_counter()
+        tl = threading.Thread(target=lambda: res.__setitem__("L", exL.extract(L)))
+        tr = threading.Thread(target=lambda: res.__setitem__("R", exR.extract(R)))
+        tl.start(); tr.start(); tl.join(); tr.join()
+        (kL, dL), (kR, dR) = res["L"], res["R"]
+        oracle.stereo_matches(exL, exR, kL, dL, kR, dR, KITTI_BF, mb)
+        if t >= warmup:
+            ms.append(1000 * (time.perf_counter() - t0))
+    a = np.array(ms)
+    return {"median_ms": round(float(np.median(a)), 3), "mean_ms": round(float(a.mean()), 3),
+            "frames": frames, "warmup": warmup, "cores": 2, "kind": "port",
+            "sample": f"{frames} synthetic 1241x376 stereo frames ({len(pool)} distinct), oracle, L and R on two "
+                      f"threads per frame + ComputeStereoMatches, {a.sum() / 1000:.1f} s"}
+
+
+def bench_latency(amd, args, pool, with_cpu):
+    """Drop-in latency (SURVEY §8d latency mode): the C++ host layer's
+    ORBextractor L and R on two std::threads per frame + ComputeStereoMatches, host image in and
+    host keypoints / descriptors / mvuRight / mvDepth out (tools/stereo_latency.cpp), 16 warm-up
+    and 512 timed frames; `serial` runs L then R on one thread for comparison."""
+    import subprocess
+    import tempfile
+    exe = ROOT / "orb-slam2-noted_amd" / "build" / "stereo_latency"
+    mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    with tempfile.NamedTemporaryFile(suffix=".u8", delete=False) as f:
+        for L, R in pool:
+            f.write(np.ascontiguousarray(L).tobytes())
+            f.write(np.ascontiguousarray(R).tobytes())
+        path = f.name
+    out = {}
+    try:
+        for mode, frames in (("threads", args.latency_frames), ("serial", max(64, args.latency_frames // 4))):
+            r = subprocess.run([str(exe), path, str(len(pool)), str(W), str(H), str(NFEAT), repr(KITTI_BF), repr(mb),
+                                str(args.latency_warmup), str(frames), mode], capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                raise RuntimeError(f"stereo_latency {mode} failed: {r.stderr.strip()}")
+            out[mode] = json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        os.unlink(path)
+    t = out["threads"]
+    res = {"latency": {"workload": "C2 single stereo frame through the drop-in boundary: host 1241x376 L/R in, "
+                                   "ORBextractor(2000) L || R on two std::threads (Frame.cc:144-153) + "
+                                   "ComputeStereoMatches, host outputs",
+                       "median_ms": t["median_ms"], "mean_ms": t["mean_ms"], "p90_ms": t["p90_ms"],
+                       "frames": t["frames"], "warmup": t["warmup"],
+                       "frames_per_s": round(1000.0 / t["mean_ms"], 2),
+                       "serial_median_ms": out["serial"]["median_ms"], "serial_mean_ms": out["serial"]["mean_ms"]}}
+    if with_cpu:
+        res["latency"]["cpu_baseline"] = cpu_latency(pool, args.latency_warmup, args.cpu_latency_frames)
+    return res
+
+
+def bench_e2e(amd, args, pool, bf, mb):
+    """C2 with host I/O: the same 384-pair batches from page-locked host
+    memory through orbx_pipeline_stereo_batch_host -- H2D of batch k+1 on a copy stream overlapped
+    with batch k's kernels, every engine's keypoints / descriptors / mvuRight / mvDepth copied back
+    to page-locked host memory -- timed to the last output byte in host memory."""
+    B = args.batch
+    ins, outs = [], []
+    for k in range(2):
+        a = amd.host_empty((2 * B, H, W), np.uint8)
+        for i in range(B):
+            L, R = pool[(i + 3 * k) % len(pool)]
+            if k:
+                L, R = np.roll(L, 7 * k, axis=1), np.roll(R, 7 * k, axis=1)
+            a[2 * i], a[2 * i + 1] = L, R
+        ins.append(a)
+    pl = amd.StereoPipeline(NFEAT, n_engines=args.engines)
+    pl.reserve(W, H, B)
+    cap = pl.capacity()
+    outs = [amd.StereoHostBatch(B, cap) for _ in range(2)]
+
+    def step(k):
+        pl.stereo_batch_host(ins[k % 2], B, W, H, W, W * H, float(bf), mb, outs[k % 2])
+
+    for k in range(args.warmup):
+        step(k)
+    pl.wait()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    pl.wait()
+    dt = time.perf_counter() - t0
+    kL = outs[(args.steps - 1) % 2].pair(0)
+    if len(kL[0]) < 100 or int((kL[4] >= 0).sum()) < 10:
+        raise RuntimeError("implausible host-mode output")
+    h2d = 2 * B * W * H
+    d2h = 2 * B * cap * (28 + 32 + 4) + 2 * B * cap * 4
+    pl.close()
+    return {"value_e2e": round(B * args.steps / dt, 2),
+            "e2e": {"ms_per_step": round(1000 * dt / args.steps, 4), "stereo_frames_per_step": B,
+                    "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
+                    "pcie_gbs": round((h2d + d2h) * args.steps / dt / 1e9, 2),
+                    "note": "page-locked host images in, host keypoints / descriptors / mvuRight / mvDepth out; "
+                            "PCIe-inclusive rate (value is the HBM-resident rate)"}}
+
+
 def bench_localba(amd, args, dist, world, with_cpu):
     """C4: LocalBundleAdjustment on the synthetic 20 KF x 3000 MP graph; one LocalBA call per
     inserted keyframe (LocalMapping.cc:116-118) -> keyframes/s = calls/s, summed over ranks."""
@@ -478,6 +589,11 @@ def main():
     ap.add_argument("--newpts-batch", type=int, default=256)
     ap.add_argument("--newpts-steps", type=int, default=10)
     ap.add_argument("--no-newpts", action="store_true")
+    ap.add_argument("--latency-frames", type=int, default=512)
+    ap.add_argument("--latency-warmup", type=int, default=16)
+    ap.add_argument("--cpu-latency-frames", type=int, default=512)
+    ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -598,6 +714,11 @@ def main():
             out["roofline"]["valu_insts_per_launch"] = valu
         # summed over the engines' launches, which overlap in time (so the sum exceeds ms_per_step)
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
+    del bufs   # the resident batches are not needed by the legs below
+    if not args.no_e2e:
+        out.update(bench_e2e(amd, args, pool, bf, mb))
+    if not args.no_latency and rank == 0:
+        out.update(bench_latency(amd, args, pool, world == 1 and not args.no_cpu_baseline))
     if not args.no_rgbd:
         out.update(bench_rgbd(amd, args, dist, world))
     if not args.no_track:

@@ -95,6 +95,9 @@ int orbx_extract_batch_device_phase(orbx_engine *e, const uint8_t *d_imgs, int n
  * desc[n_images][cap][32]. */
 int orbx_batch_results(orbx_engine *e, const int **d_counts, const orbx_kp **d_kps,
                        const uint8_t **d_desc, int *cap);
+/* Keypoint capacity per image (the row count of the kps / desc result arrays) for the reserved
+ * image size; ORBX_ESTATE before the first reserve / extraction. */
+int orbx_capacity(const orbx_engine *e, int *cap);
 /* Copy one image's results of the last batch to host. Waits for this engine's last launch
  * (an event), never for the device: engines on other threads keep running. */
 int orbx_batch_fetch(orbx_engine *e, int image, orbx_kp *kps, uint8_t *desc, int cap, int *n);
@@ -137,6 +140,31 @@ int orbx_pipeline_stereo_batch(orbx_pipeline *pl, const uint8_t *d_imgs, int n_p
 int orbx_pipeline_chunk(orbx_pipeline *pl, int i, orbx_engine **e, int *first_pair, int *n_pairs);
 /* Make `stream` wait for every chunk of the last batch. */
 int orbx_pipeline_join(orbx_pipeline *pl, void *stream);
+/* Host-memory outputs of a stereo batch (the Frame members the boundary returns: mvKeys,
+ * mDescriptors of both images, mvuRight, mvDepth). cap = orbx_pipeline_capacity. */
+typedef struct {
+    int32_t *counts;    /* [2 n_pairs] keypoints of image 2p (left) / 2p+1 (right) */
+    orbx_kp *kps;       /* [2 n_pairs][cap] */
+    uint8_t *desc;      /* [2 n_pairs][cap][32] */
+    float *u_right;     /* [n_pairs][cap] mvuRight of the left image (-1 = none) */
+    float *depth;       /* [n_pairs][cap] mvDepth */
+} orbx_stereo_host_out;
+/* Keypoint capacity per image of the pipeline's engines (after orbx_pipeline_reserve). */
+int orbx_pipeline_capacity(orbx_pipeline *pl, int *cap);
+/* The stereo batch with HOST images in and host outputs (ORBextractor::operator() takes a host
+ * cv::InputArray, ORBextractor.h:107): the batch is uploaded chunk by chunk on the pipeline's H2D
+ * stream into one of two device slots (batch k+1's upload overlaps batch k's kernels), each
+ * engine starts when its chunk has landed, and its results are copied out on a D2H stream right
+ * after its stereo pass. Returns once enqueued; orbx_pipeline_wait blocks until the outputs are
+ * in host memory. h_imgs and the outputs should be pinned (orbx_host_alloc) and stay valid until
+ * the wait; results equal orbx_pipeline_stereo_batch's. */
+int orbx_pipeline_stereo_batch_host(orbx_pipeline *pl, const uint8_t *h_imgs, int n_pairs, int w,
+                                    int h, int pitch, size_t image_stride, float mbf, float mb,
+                                    const orbx_stereo_host_out *out);
+int orbx_pipeline_wait(orbx_pipeline *pl);
+/* Page-locked host memory (hipHostMalloc) for the host-mode buffers. */
+int orbx_host_alloc(size_t bytes, void **p);
+int orbx_host_free(void *p);
 int orbm_stereo_results(orbx_engine *e, const float **d_u_right, const float **d_depth);
 int orbm_stereo_fetch(orbx_engine *e, int pair, float *u_right, float *depth, int cap);
 

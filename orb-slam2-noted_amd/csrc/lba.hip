@@ -1285,7 +1285,10 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     ActiveSet A;
     build_active(h, A);
     if (setup(A)) return ORBX_EDEVICE;
+    // lba_optimize: >= 0 iterations, -1 = the pre-LM error evaluation failed (g2o's optimize()
+    // returning -1, a valid outcome), -3 = HIP runtime error
     r->iterations[0] = lba_optimize(e, g, A, 5, np, nq, stop, &r->chi2[0]);
+    if (r->iterations[0] == -3) return ORBX_EDEVICE;
     if (r->iterations[0] < -1) return ORBX_EINVAL;
     const bool bDoMore = !(stop && *stop);
     std::vector<uint8_t> flag(std::max(ne, 1));
@@ -1302,6 +1305,8 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         build_active(h, A);
         if (setup(A)) return ORBX_EDEVICE;
         r->iterations[1] = lba_optimize(e, g, A, 10, np, nq, stop, &r->chi2[1]);
+        if (r->iterations[1] == -3) return ORBX_EDEVICE;
+        if (r->iterations[1] < -1) return ORBX_EINVAL;
     } else {
         r->stopped = 1;
     }

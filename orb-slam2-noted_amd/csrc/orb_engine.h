@@ -91,6 +91,26 @@ inline hipError_t d2h_sync(void *dst, const void *src, size_t bytes, hipStream_t
     return r == hipSuccess ? hipStreamSynchronize(st) : r;
 }
 
+// Grow-only page-locked host buffer: the single-frame paths stage host images and results
+// through it so every transfer is one DMA (pageable 2-D copies split into a copy per row).
+struct PinnedBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    int ensure(size_t n) {
+        if (n <= bytes && p) return 0;
+        release();
+        if (hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault) != hipSuccess) { p = nullptr; return ORBX_EDEVICE; }
+        bytes = n ? n : 16;
+        return 0;
+    }
+    template <class T> T *as(size_t byte_off = 0) const { return (T *)((char *)p + byte_off); }
+};
+
 inline hipEvent_t make_done_event() {
     hipEvent_t ev = nullptr;
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return nullptr;
@@ -133,6 +153,7 @@ struct orbx_engine {
     int st_pairs = 0;             // pairs of the last stereo run (orbm_stereo_fetch bound)
     hipEvent_t done = nullptr;    // recorded after the last launch of every producer
     hipStream_t done_stream = nullptr;   // stream `done` was last recorded on
+    orbamd::PinnedBuf h_stage;    // single-frame host staging (input image, results)
     orbf_state *fs = nullptr;     // Frame / SearchForInitialization buffers, owned
     std::string err;
     // per-kernel hipEvent profiling (bench.py roofline), recorded on the launch stream

@@ -1752,6 +1752,7 @@ void orbx_destroy(orbx_engine *e) {
                               &e->d_sel_cnt, &e->d_kps, &e->d_desc, &e->d_cnt, &e->d_st_sorted,
                               &e->d_st_res, &e->d_st_u, &e->d_st_depth, &e->d_st_dist, &e->d_st_rows};
     for (auto *b : bufs) b->release();
+    e->h_stage.release();
     for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->done) (void)hipEventDestroy(e->done);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1848,6 +1849,13 @@ int orbx_extract_batch_device_phase(orbx_engine *e, const uint8_t *d_imgs, int n
     return rc;
 }
 
+int orbx_capacity(const orbx_engine *e, int *cap) {
+    if (!e || !cap) return ORBX_EINVAL;
+    if (e->W == 0) return ORBX_ESTATE;   // no size reserved yet
+    *cap = e->g.out_base[e->g.nlevels];
+    return ORBX_OK;
+}
+
 int orbx_batch_results(orbx_engine *e, const int **d_counts, const orbx_kp **d_kps,
                        const uint8_t **d_desc, int *cap) {
     if (!e || e->last_n == 0) return ORBX_ESTATE;
@@ -1858,26 +1866,33 @@ int orbx_batch_results(orbx_engine *e, const int **d_counts, const orbx_kp **d_k
     return ORBX_OK;
 }
 
+// One image's results through the engine's pinned staging buffer: count, keypoints and
+// descriptors (all `cap` rows) in one round trip on the engine's own stream, then the first
+// `count` rows copied into the caller's arrays.
+static int fetch_staged(orbx_engine *e, int image, orbx_kp *kps, uint8_t *desc, int cap, int *n, hipEvent_t producer) {
+    const size_t kc = (size_t)e->g.out_base[e->g.nlevels];
+    const size_t o_kps = 64, o_desc = o_kps + sizeof(orbx_kp) * kc;
+    if (e->h_stage.ensure(o_desc + 32 * kc)) return ORBX_EDEVICE;
+    orbamd::HostCopy hc(e->stream, producer);
+    hc.d2h(e->h_stage.p, e->d_cnt.as<int>() + image, sizeof(int));
+    hc.d2h(e->h_stage.as<void>(o_kps), e->d_kps.as<orbx_kp>() + image * kc, sizeof(orbx_kp) * kc);
+    hc.d2h(e->h_stage.as<void>(o_desc), e->d_desc.as<uint8_t>() + image * kc * 32, 32 * kc);
+    if (hc.finish()) return ORBX_EDEVICE;
+    const int cnt = *e->h_stage.as<int>();
+    *n = cnt;
+    if (cnt > cap) return ORBX_ECAP;
+    if (cnt > 0) {
+        if (kps) std::memcpy(kps, e->h_stage.as<void>(o_kps), sizeof(orbx_kp) * cnt);
+        if (desc) std::memcpy(desc, e->h_stage.as<void>(o_desc), 32 * (size_t)cnt);
+    }
+    return ORBX_OK;
+}
+
 int orbx_batch_fetch(orbx_engine *e, int image, orbx_kp *kps, uint8_t *desc, int cap, int *n) {
     if (!e || !n) return ORBX_EINVAL;
     if (e->last_n == 0 || image < 0 || image >= e->last_n) return ORBX_ESTATE;
     HIPCHK(hipSetDevice(e->device));
-    int cnt = 0;
-    {
-        orbamd::HostCopy hc(e->stream, e->done);
-        hc.d2h(&cnt, e->d_cnt.as<int>() + image, sizeof(int));
-        if (hc.finish()) return ORBX_EDEVICE;
-    }
-    *n = cnt;
-    if (cnt > cap) return ORBX_ECAP;
-    const long long kc = e->g.out_base[e->g.nlevels];
-    if (cnt > 0) {
-        orbamd::HostCopy hc(e->stream, nullptr);
-        hc.d2h(kps, e->d_kps.as<orbx_kp>() + image * kc, sizeof(orbx_kp) * cnt);
-        hc.d2h(desc, e->d_desc.as<uint8_t>() + image * kc * 32, 32 * (size_t)cnt);
-        if (hc.finish()) return ORBX_EDEVICE;
-    }
-    return ORBX_OK;
+    return fetch_staged(e, image, kps, desc, cap, n, e->done);
 }
 
 int orbx_extract(orbx_engine *e, const uint8_t *img, int w, int h, int stride, orbx_kp *kps,
@@ -1891,11 +1906,23 @@ int orbx_extract(orbx_engine *e, const uint8_t *img, int w, int h, int stride, o
     if (rc) return rc;
     // +16: the aligned dword loads of the level-0 staging / level-1 resize may read up to
     // 11 bytes past the last pixel of the last row (include/orbslam2_amd.h, input tail)
-    if (e->d_in.ensure((size_t)w * h + 16)) return ORBX_EDEVICE;
-    HIPCHK(hipMemcpy2DAsync(e->d_in.p, w, img, stride, w, h, hipMemcpyHostToDevice, e->stream));
+    const size_t img_bytes = (size_t)w * h;
+    if (e->d_in.ensure(img_bytes + 16)) return ORBX_EDEVICE;
+    // the host image is packed into the pinned staging buffer (the previous call's transfers on
+    // this stream have completed: every call ends with a stream synchronisation) and goes up in
+    // one DMA
+    if (e->h_stage.ensure(std::max<size_t>(img_bytes, 64))) return ORBX_EDEVICE;
+    HIPCHK(hipStreamWaitEvent(e->stream, e->done, 0));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (stride == w) {
+        std::memcpy(e->h_stage.p, img, img_bytes);
+    } else {
+        for (int r = 0; r < h; r++) std::memcpy(e->h_stage.as<uint8_t>((size_t)r * w), img + (size_t)r * stride, (size_t)w);
+    }
+    HIPCHK(hipMemcpyAsync(e->d_in.p, e->h_stage.p, img_bytes, hipMemcpyHostToDevice, e->stream));
     rc = orbamd::engine_extract_device(e, e->d_in.as<uint8_t>(), 1, w, (long long)w * h, e->stream, 3);
     if (rc) return rc;
-    return orbx_batch_fetch(e, 0, kps, desc, cap, n);
+    return fetch_staged(e, 0, kps, desc, cap, n, nullptr);   // same stream: no event wait
 }
 
 int orbx_pyramid_level(orbx_engine *e, int image, int level, uint8_t *dst, int *w, int *h) {

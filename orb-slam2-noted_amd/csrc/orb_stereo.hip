@@ -12,6 +12,8 @@
 //                         1.5*1.4*median rejection (:1112-1127)
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include <algorithm>
 #include <climits>
 #include <cstdio>
@@ -69,50 +71,78 @@ __device__ __forceinline__ int hamming32(const uint8_t *a, const uint8_t *b) {
            __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
 }
 
-// ---- S1: sort right keypoints of each pair by y (key = float bits, positive floats)
+// ---- S1: right keypoints of each pair in (y, index) order, as 16-byte records
 // The scan of S2 reads one 16-byte record per right keypoint in y order: {y, x (float bits),
 // minr | maxr << 16 (the row band of Frame.cc:869-888, int16 each), iR | octave << 16}, so the
 // band / octave / disparity filter needs no dependent gather of the keypoint itself.
-__global__ __launch_bounds__(256) void stereo_sort_right(ExtractGeom g, StereoArgs a, uint4 *sorted) {
-    extern __shared__ unsigned long long sbuf[];
-    const int p = blockIdx.x;
+// Counting sort on the image row floor(y) (y >= 0): row histogram, block scan -- whose exclusive
+// prefix IS the row table of S2 (first record with y >= r) -- scatter into row buckets, then each
+// keypoint's final slot = bucket start + its rank among the bucket's few members by (y, index).
+// Replaces a 4096-key bitonic sort in LDS (86 -> ~10 us for one pair: the single-frame latency).
+#define ST_THREADS 512
+__global__ __launch_bounds__(ST_THREADS) void stereo_sort_right(ExtractGeom g, StereoArgs a, uint4 *sorted) {
+    extern __shared__ int st_lds[];
+    int *cnt = st_lds;                       // [nrows] bucket sizes, then fill counters
+    int *start = cnt + a.nrows;              // [nrows] exclusive prefix = row table
+    int *mem = start + a.nrows;              // [cap] bucket members (keypoint index)
+    float *yk = (float *)(mem + a.cap);      // [cap] y of keypoint i
+    __shared__ int wsum[ST_THREADS / 64];
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = wave_id();
     const int imgR = a.R.img_base + a.R.img_step * p;
     const int nR = min(a.R.cnt[imgR], a.cap);
     const orbx_kp *kR = a.R.kps + (long long)imgR * a.cap;
-    const int n = a.sort_cap;
-    for (int i = threadIdx.x; i < n; i += 256)
-        sbuf[i] = i < nR ? (((unsigned long long)__float_as_uint(kR[i].y) << 32) | (unsigned)i) : ~0ull;
+    const int nrows = a.nrows;
+    for (int r = tid; r < nrows; r += ST_THREADS) cnt[r] = 0;
     __syncthreads();
-    for (int k = 2; k <= n; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < n; i += 256) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long x = sbuf[i], y = sbuf[ixj];
-                    const bool asc = (i & k) == 0;
-                    if (asc ? (x > y) : (x < y)) { sbuf[i] = y; sbuf[ixj] = x; }
-                }
-            }
-            __syncthreads();
-        }
+    for (int i = tid; i < nR; i += ST_THREADS) {
+        const float y = kR[i].y;
+        yk[i] = y;
+        atomicAdd(&cnt[min(max((int)y, 0), nrows - 1)], 1);
     }
-    for (int i = threadIdx.x; i < nR; i += 256) {
-        const int iR = (int)(sbuf[i] & 0xFFFFFFFFu);
-        const orbx_kp kp = kR[iR];
+    __syncthreads();
+    // block exclusive scan of cnt: thread t owns rows [t*per, (t+1)*per)
+    const int per = (nrows + ST_THREADS - 1) / ST_THREADS;
+    const int r0 = tid * per, r1 = min(r0 + per, nrows);
+    int local = 0;
+    for (int r = r0; r < r1; r++) local += cnt[r];
+    int incl = local;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int run = incl - local;
+    for (int w = 0; w < wv; w++) run += wsum[w];
+    for (int r = r0; r < r1; r++) {
+        const int c = cnt[r];
+        start[r] = run;
+        a.rowtab[(long long)p * nrows + r] = run;
+        run += c;
+    }
+    __syncthreads();
+    for (int r = tid; r < nrows; r += ST_THREADS) cnt[r] = 0;
+    __syncthreads();
+    for (int i = tid; i < nR; i += ST_THREADS) {
+        const int b = min(max((int)yk[i], 0), nrows - 1);
+        mem[start[b] + atomicAdd(&cnt[b], 1)] = i;
+    }
+    __syncthreads();
+    for (int i = tid; i < nR; i += ST_THREADS) {
+        const float y = yk[i];
+        const int b = min(max((int)y, 0), nrows - 1), s0 = start[b], nb = cnt[b];
+        int rank = 0;
+        for (int q = 0; q < nb; q++) {
+            const int j = mem[s0 + q];
+            const float yj = yk[j];
+            rank += (yj < y) || (yj == y && j < i);
+        }
+        const orbx_kp kp = kR[i];
         const float r = 2.0f * g.scale[kp.octave];
         const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
-        sorted[(long long)p * n + i] = make_uint4(__float_as_uint(kp.y), __float_as_uint(kp.x),
-                                                  (uint32_t)(minr & 0xFFFF) | (uint32_t)maxr << 16,
-                                                  (uint32_t)iR | (uint32_t)kp.octave << 16);
-    }
-    // row table: the left-keypoint scan starts at rowtab[floor(y_lo)] instead of a binary search
-    for (int r = threadIdx.x; r < a.nrows; r += 256) {
-        int lo = 0, hi = nR;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (__uint_as_float((unsigned)(sbuf[mid] >> 32)) < (float)r) lo = mid + 1; else hi = mid;
-        }
-        a.rowtab[(long long)p * a.nrows + r] = lo;
+        sorted[(long long)p * a.sort_cap + s0 + rank] =
+            make_uint4(__float_as_uint(kp.y), __float_as_uint(kp.x), (uint32_t)(minr & 0xFFFF) | (uint32_t)maxr << 16,
+                       (uint32_t)i | (uint32_t)kp.octave << 16);
     }
 }
 
@@ -261,43 +291,58 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
     }
 }
 
-// ---- S3: median of SAD distances and outlier cut
-__global__ __launch_bounds__(256) void stereo_median_cut(StereoArgs a, float *u_right, float *depth,
-                                                         const int *sad) {
-    extern __shared__ int ibuf[];
-    __shared__ int nd;
-    const int p = blockIdx.x;
+// ---- S3: median of SAD distances and outlier cut (Frame.cc:1112-1127)
+// The reference sorts (SAD, iL) pairs and takes element nd/2; only that order statistic is
+// needed: a two-pass radix select on the SAD value (< 121 * 510 < 2^16) with LDS histograms of
+// its high and low byte. Replaces a 4096-key bitonic sort (74 -> a few us for one pair).
+__global__ __launch_bounds__(ST_THREADS) void stereo_median_cut(StereoArgs a, float *u_right, float *depth,
+                                                               const int *sad) {
+    __shared__ int hist[256];
+    __shared__ int nd, sel, rem;
+    const int p = blockIdx.x, tid = threadIdx.x;
     const int imgL = a.L.img_base + a.L.img_step * p;
     const int nL = min(a.L.cnt[imgL], a.cap);
-    const int n = a.sort_cap;
     const int *s = sad + (long long)p * a.cap;
-    if (threadIdx.x == 0) nd = 0;
-    for (int i = threadIdx.x; i < n; i += 256) ibuf[i] = INT_MAX;
+    if (tid < 256) hist[tid] = 0;
+    if (tid == 0) nd = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < nL; i += 256) {
+    int mine = 0;
+    for (int i = tid; i < nL; i += ST_THREADS) {
         const int v = s[i];
-        if (v >= 0) ibuf[atomicAdd(&nd, 1)] = v;
+        if (v >= 0) { atomicAdd(&hist[min(v >> 8, 255)], 1); mine++; }
+    }
+    if (mine) atomicAdd(&nd, mine);
+    __syncthreads();
+    const int n = nd;
+    if (n == 0) return;   // no match: nothing to cut (the reference would index an empty vector)
+    const int k = n / 2;  // vDistIdx[vDistIdx.size() / 2] of the sorted SADs
+    if (tid == 0) {
+        int c = 0, b = 0;
+        while (c + hist[b] <= k) c += hist[b++];
+        sel = b;
+        rem = k - c;
     }
     __syncthreads();
-    for (int k = 2; k <= n; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < n; i += 256) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const int x = ibuf[i], y = ibuf[ixj];
-                    const bool asc = (i & k) == 0;
-                    if (asc ? (x > y) : (x < y)) { ibuf[i] = y; ibuf[ixj] = x; }
-                }
-            }
-            __syncthreads();
-        }
+    const int hi = sel, r_lo = rem;
+    __syncthreads();
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < nL; i += ST_THREADS) {
+        const int v = s[i];
+        if (v >= 0 && min(v >> 8, 255) == hi) atomicAdd(&hist[v & 255], 1);
     }
-    if (nd == 0) return;
-    const float median = (float)ibuf[nd / 2];
+    __syncthreads();
+    if (tid == 0) {
+        int c = 0, b = 0;
+        while (c + hist[b] <= r_lo) c += hist[b++];
+        sel = (hi << 8) | b;
+    }
+    __syncthreads();
+    const float median = (float)sel;
     const float thDist = 1.5f * 1.4f * median;
     float *u = u_right + (long long)p * a.cap;
     float *d = depth + (long long)p * a.cap;
-    for (int i = threadIdx.x; i < nL; i += 256) {
+    for (int i = tid; i < nL; i += ST_THREADS) {
         const int v = s[i];
         if (v >= 0 && !((float)v < thDist)) { u[i] = -1; d[i] = -1; }
     }
@@ -321,16 +366,17 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
         return ORBX_EDEVICE;
     float *u = store->d_st_u.as<float>(), *d = store->d_st_depth.as<float>();
     int *sad = store->d_st_dist.as<int>();
-    if (sc * 8 > 64 * 1024) return ORBX_EINVAL;
+    const size_t sort_lds = 4 * (2 * (size_t)a.nrows + 2 * (size_t)a.cap);
+    if (sort_lds > 64 * 1024) return ORBX_EINVAL;
     int ph = prof_begin(store, s);
-    stereo_sort_right<<<n_pairs, 256, 8 * sc, s>>>(g, a, store->d_st_sorted.as<uint4>());
+    stereo_sort_right<<<n_pairs, ST_THREADS, sort_lds, s>>>(g, a, store->d_st_sorted.as<uint4>());
     prof_end(store, s, ph, "stereo_sort_right");
     ph = prof_begin(store, s);
     stereo_match_left<<<dim3((a.cap + 3) / 4, n_pairs), 256, 0, s>>>(
         g, a, store->d_st_sorted.as<uint4>(), u, d, sad);
     prof_end(store, s, ph, "stereo_match_left");
     ph = prof_begin(store, s);
-    stereo_median_cut<<<n_pairs, 256, 4 * sc, s>>>(a, u, d, sad);
+    stereo_median_cut<<<n_pairs, ST_THREADS, 0, s>>>(a, u, d, sad);
     prof_end(store, s, ph, "stereo_median_cut");
     HIPCHK(hipGetLastError());
     HIPCHK(mark_done(store, s));
@@ -426,19 +472,19 @@ int orbm_stereo_match(orbx_engine *left, orbx_engine *right, float mbf, float mb
     a.mb = mb;
     int rc = run_stereo(left->g, a, 1, left, left->stream);
     if (rc) return rc;
-    int cnt = 0;
-    {
-        HostCopy hc(left->stream, nullptr);   // same stream as the launches
-        hc.d2h(&cnt, left->d_cnt.as<int>(), sizeof(int));
-        if (hc.finish()) return ORBX_EDEVICE;
-    }
-    if (n != cnt) return ORBX_EINVAL;
+    // count, mvuRight, mvDepth in one round trip through the left engine's pinned staging
+    const size_t cap = (size_t)a.cap;
+    if (left->h_stage.ensure(64 + 8 * cap)) return ORBX_EDEVICE;
+    HostCopy hc(left->stream, nullptr);   // same stream as the launches
+    hc.d2h(left->h_stage.p, left->d_cnt.as<int>(), sizeof(int));
+    hc.d2h(left->h_stage.as<void>(64), left->d_st_u.p, 4 * cap);
+    hc.d2h(left->h_stage.as<void>(64 + 4 * cap), left->d_st_depth.p, 4 * cap);
+    if (hc.finish()) return ORBX_EDEVICE;
+    if (n != *left->h_stage.as<int>()) return ORBX_EINVAL;
     if (n > 0) {
         if (!u_right || !depth) return ORBX_EINVAL;
-        HostCopy hc(left->stream, nullptr);
-        hc.d2h(u_right, left->d_st_u.p, 4 * (size_t)n);
-        hc.d2h(depth, left->d_st_depth.p, 4 * (size_t)n);
-        if (hc.finish()) return ORBX_EDEVICE;
+        std::memcpy(u_right, left->h_stage.as<void>(64), 4 * (size_t)n);
+        std::memcpy(depth, left->h_stage.as<void>(64 + 4 * cap), 4 * (size_t)n);
     }
     return ORBX_OK;
 }

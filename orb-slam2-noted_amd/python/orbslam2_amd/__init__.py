@@ -61,6 +61,11 @@ SIGNATURES = [
     ("orbx_pipeline_reserve", _I, [_P, _I, _I, _I]),
     ("orbx_pipeline_stereo_batch", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _F, _F, _P]),
     ("orbx_pipeline_chunk", _I, [_P, _I, _P, _P, _P]),
+    ("orbx_pipeline_capacity", _I, [_P, _P]),
+    ("orbx_pipeline_stereo_batch_host", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _F, _F, _P]),
+    ("orbx_pipeline_wait", _I, [_P]),
+    ("orbx_host_alloc", _I, [C.c_size_t, _P]),
+    ("orbx_host_free", _I, [_P]),
     ("orbx_pipeline_join", _I, [_P, _P]),
     ("orbx_batch_results", _I, [_P, _P, _P, _P, _P]),
     ("orbx_batch_fetch", _I, [_P, _I, _P, _P, _I, _P]),
@@ -374,6 +379,58 @@ class BatchExtractor(ORBextractor):
         return u, d
 
 
+class StereoHostOut(C.Structure):
+    """orbx_stereo_host_out (include/orbslam2_amd.h)."""
+    _fields_ = [("counts", C.c_void_p), ("kps", C.c_void_p), ("desc", C.c_void_p), ("u_right", C.c_void_p),
+                ("depth", C.c_void_p)]
+
+
+class _HostBlock:
+    """Owner of one orbx_host_alloc block; numpy views keep it alive via .base chains."""
+
+    def __init__(self, nbytes: int):
+        self.p = C.c_void_p()
+        self.nbytes = max(int(nbytes), 1)
+        _check(lib().orbx_host_alloc(self.nbytes, C.byref(self.p)), "orbx_host_alloc")
+
+    def __del__(self):
+        try:
+            if self.p.value:
+                lib().orbx_host_free(self.p)
+        except Exception:
+            pass
+
+
+def host_empty(shape, dtype) -> np.ndarray:
+    """numpy array over page-locked host memory (orbx_host_alloc), for the host-mode pipeline."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    blk = _HostBlock(n)
+    buf = (C.c_char * blk.nbytes).from_address(blk.p.value)
+    buf.owner = blk   # the array's base chain ends at buf, which keeps the block alive
+    return np.frombuffer(buf, np.uint8, n).view(dt).reshape(shape)
+
+
+class StereoHostBatch:
+    """Page-locked host outputs of one stereo batch (orbx_stereo_host_out)."""
+
+    def __init__(self, n_pairs: int, cap: int):
+        self.n_pairs, self.cap = n_pairs, cap
+        self.counts = host_empty((2 * n_pairs,), np.int32)
+        self.kps = host_empty((2 * n_pairs, cap), KP_DTYPE)
+        self.desc = host_empty((2 * n_pairs, cap, 32), np.uint8)
+        self.u_right = host_empty((n_pairs, cap), np.float32)
+        self.depth = host_empty((n_pairs, cap), np.float32)
+        self.c = StereoHostOut(self.counts.ctypes.data, self.kps.ctypes.data, self.desc.ctypes.data,
+                               self.u_right.ctypes.data, self.depth.ctypes.data)
+
+    def pair(self, p: int):
+        """(kL, dL, kR, dR, mvuRight, mvDepth) of pair p, trimmed to the keypoint counts."""
+        nL, nR = int(self.counts[2 * p]), int(self.counts[2 * p + 1])
+        return (self.kps[2 * p, :nL], self.desc[2 * p, :nL], self.kps[2 * p + 1, :nR], self.desc[2 * p + 1, :nR],
+                self.u_right[p, :nL], self.depth[p, :nL])
+
+
 class StereoPipeline:
     """Batched stereo Frame construction (extract L + R, ComputeStereoMatches) over k engines on
     k HIP streams, their pyramid / FAST / blur phases in turn (orbx_pipeline_*, orb_pipeline.hip).
@@ -412,6 +469,23 @@ class StereoPipeline:
                      mbf: float, mb: float, stream: int | None = None):
         _check(lib().orbx_pipeline_stereo_batch(self._h, C.c_void_p(d_ptr), n_pairs, w, h, pitch, image_stride,
                                                 mbf, mb, C.c_void_p(stream or 0)), "orbx_pipeline_stereo_batch")
+
+    def capacity(self) -> int:
+        cap = C.c_int()
+        _check(lib().orbx_pipeline_capacity(self._h, C.byref(cap)), "orbx_pipeline_capacity")
+        return cap.value
+
+    def stereo_batch_host(self, h_imgs: np.ndarray, n_pairs: int, w: int, h: int, pitch: int, image_stride: int,
+                          mbf: float, mb: float, out: "StereoHostBatch"):
+        """Host images in (ideally host_empty memory), host outputs into `out`; asynchronous until wait()."""
+        if not h_imgs.flags.c_contiguous or h_imgs.nbytes < 2 * n_pairs * image_stride:
+            raise ValueError("h_imgs must be a contiguous buffer of 2 * n_pairs images")
+        _check(lib().orbx_pipeline_stereo_batch_host(self._h, C.c_void_p(h_imgs.ctypes.data), n_pairs, w, h, pitch,
+                                                     image_stride, mbf, mb, C.byref(out.c)),
+               "orbx_pipeline_stereo_batch_host")
+
+    def wait(self):
+        _check(lib().orbx_pipeline_wait(self._h), "orbx_pipeline_wait")
 
     def join(self, stream: int | None = None):
         """Make `stream` (default: the legacy default stream) wait for the last batch."""

@@ -97,3 +97,55 @@ def test_stereo_pipeline(amd, oracle_mod, P, k):
         np.testing.assert_array_equal(u[:n].view(np.uint32), u_ref.view(np.uint32))
         np.testing.assert_array_equal(d[:n].view(np.uint32), d_ref.view(np.uint32))
     pl.close()
+
+
+def test_stereo_pipeline_host_mode(amd, oracle_mod):
+    """orbx_pipeline_stereo_batch_host: host (pinned) images in, host outputs out, the H2D of the
+    next batch overlapping the current one, three batches back to back into two output buffers
+    (two device input slots): every pair bit-exact with the oracle."""
+    h, w, P, k = 376, 1241, 7, 3
+    pairs = [synth.stereo_pair(h, w, 40 + p) for p in range(P)]
+    ins = []
+    for b in range(3):
+        a = amd.host_empty((2 * P, h, w), np.uint8)
+        for p in range(P):
+            L, R = pairs[(p + b) % P]
+            a[2 * p], a[2 * p + 1] = L, R
+        ins.append(a)
+    pl = amd.StereoPipeline(2000, n_engines=k)
+    pl.reserve(w, h, P)
+    cap = pl.capacity()
+    outs = [amd.StereoHostBatch(P, cap), amd.StereoHostBatch(P, cap)]
+    mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    refs = [_stereo_ref_full(oracle_mod, *pairs[p]) for p in range(P)]
+    pl.stereo_batch_host(ins[0], P, w, h, w, w * h, KITTI_BF, mb, outs[0])
+    pl.stereo_batch_host(ins[1], P, w, h, w, w * h, KITTI_BF, mb, outs[1])
+    pl.wait()
+    got1 = [outs[1].pair(p) for p in range(P)]
+    got1 = [tuple(np.array(x) for x in g) for g in got1]
+    for b, out in ((0, outs[0]),):
+        for p in range(P):
+            _check_pair(out.pair(p), refs[(p + b) % P], f"batch {b} pair {p}")
+    pl.stereo_batch_host(ins[2], P, w, h, w, w * h, KITTI_BF, mb, outs[0])
+    pl.wait()
+    for p in range(P):
+        _check_pair(got1[p], refs[(p + 1) % P], f"batch 1 pair {p}")
+        _check_pair(outs[0].pair(p), refs[(p + 2) % P], f"batch 2 pair {p}")
+    pl.close()
+
+
+def _stereo_ref_full(oracle_mod, L, R):
+    exL, exR = oracle_mod.Extractor(2000), oracle_mod.Extractor(2000)
+    kL, dL = exL.extract(L)
+    kR, dR = exR.extract(R)
+    mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    u, d = oracle_mod.stereo_matches(exL, exR, kL, dL, kR, dR, KITTI_BF, mb)
+    return kL, dL, kR, dR, u, d
+
+
+def _check_pair(got, ref, what):
+    gkL, gdL, gkR, gdR, gu, gd = got
+    kL, dL, kR, dR, u, d = ref
+    assert gkL.tobytes() == kL.tobytes() and np.array_equal(gdL, dL), what + " left"
+    assert gkR.tobytes() == kR.tobytes() and np.array_equal(gdR, dR), what + " right"
+    assert gu.tobytes() == u.tobytes() and gd.tobytes() == d.tobytes(), what + " stereo"
