@@ -62,6 +62,7 @@ SIGNATURES = [
     ("orbx_pipeline_stereo_batch", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _F, _F, _P]),
     ("orbx_pipeline_chunk", _I, [_P, _I, _P, _P, _P]),
     ("orbx_pipeline_capacity", _I, [_P, _P]),
+    ("orbx_capacity", _I, [_P, _P]),
     ("orbx_pipeline_stereo_batch_host", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _F, _F, _P]),
     ("orbx_pipeline_wait", _I, [_P]),
     ("orbx_host_alloc", _I, [C.c_size_t, _P]),
