@@ -350,6 +350,18 @@ static void restore_diagonal(sys_t *S) {
 }
 
 /* BlockSolver::solve with the Schur complement; dense Cholesky on Hschur */
+/* Exposure of the linear-solver pin: the dense Cholesky rejects a trial on any
+ * pivot <= 0, Eigen's SimplicialLDLT (linear_solver_eigen.h:105) only on a zero pivot, so results
+ * can differ only in trials with a non-positive pivot. Counters of the calling thread: [0] Schur
+ * solves, [1] solves with a pivot <= 0; and the smallest pivot / diagonal ratio seen. */
+static _Thread_local long g_chol_stats[2];
+static _Thread_local double g_chol_min_ratio = 1e300;
+void lba_oracle_chol_stats(long out[2], double *min_ratio, int reset) {
+    if (out) { out[0] = g_chol_stats[0]; out[1] = g_chol_stats[1]; }
+    if (min_ratio) *min_ratio = g_chol_min_ratio;
+    if (reset) { g_chol_stats[0] = g_chol_stats[1] = 0; g_chol_min_ratio = 1e300; }
+}
+
 static int schur_solve(const graph_t *g, sys_t *S) {
     const int n6 = 6 * S->P;
     double *Hs = (double *)malloc(sizeof(double) * (n6 * n6 + 1));
@@ -405,10 +417,13 @@ static int schur_solve(const graph_t *g, sys_t *S) {
     for (int i = 0; i < n6; i++) bs[i] = S->b[i] - coef[i];
     /* dense Cholesky Hs = L L^T */
     int ok = 1;
+    g_chol_stats[0]++;
     for (int j = 0; j < n6 && ok; j++) {
         double d = Hs[(size_t)j * n6 + j];
+        const double diag = d;
         for (int k = 0; k < j; k++) d -= Hs[(size_t)j * n6 + k] * Hs[(size_t)j * n6 + k];
-        if (!(d > 0)) { ok = 0; break; }
+        if (diag > 0 && d / diag < g_chol_min_ratio) g_chol_min_ratio = d / diag;
+        if (!(d > 0)) { ok = 0; g_chol_stats[1]++; break; }
         const double ljj = sqrt(d);
         Hs[(size_t)j * n6 + j] = ljj;
         for (int i = j + 1; i < n6; i++) {

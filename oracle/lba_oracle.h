@@ -12,6 +12,7 @@ extern "C" {
 int lba_oracle_solve(const lba_problem *p, lba_result *r, const volatile uint8_t *stop);
 /* Optimizer::PoseOptimization (Optimizer.cc:375-622) */
 int pose_oracle_optimize(const orbp_frame *f, orbp_result *r);
+void lba_oracle_chol_stats(long out[2], double *min_ratio, int reset);
 int orc_ldlt_solve6(const double H[36], const double b[6], double x[6]);
 #ifdef __cplusplus
 }

@@ -83,12 +83,35 @@ def lib() -> C.CDLL:
         L.orc_undistort_points.argtypes = [P, P, C.c_int, P, P]
         L.orc_stereo_from_rgbd.argtypes = [P, P, C.c_int, P, C.c_int, C.c_float, P, P]
         L.orc_hamming_best2.argtypes = [P, C.c_int, P, C.c_int, P, P, P]
+        L.orc_qt_tie_stats.argtypes = [P, C.c_int]
+        L.orc_qt_tie_stats.restype = None
+        L.orc_set_blur_mode.argtypes = [C.c_int]
+        L.orc_set_blur_mode.restype = None
+        L.orc_set_tie_mode.argtypes = [C.c_int]
+        L.orc_set_tie_mode.restype = None
         _lib = L
     return _lib
 
 
 def _p(a: np.ndarray) -> C.c_void_p:
     return C.c_void_p(a.ctypes.data)
+
+
+def qt_tie_stats(reset: bool = False) -> dict:
+    """Quadtree tie-pin exposure counters of the calling thread (orc_qt_tie_stats)."""
+    a = np.zeros(4, np.int64)
+    lib().orc_qt_tie_stats(_p(a), 1 if reset else 0)
+    return {"calls": int(a[0]), "final_phase": int(a[1]), "order_exposed": int(a[2]), "set_exposed": int(a[3])}
+
+
+def set_tie_mode(mode: int):
+    """Quadtree final-phase tie key: 0 = creation sequence (pin), 1 = reversed, 2 = hashed."""
+    lib().orc_set_tie_mode(int(mode))
+
+
+def set_blur_mode(mode: int):
+    """0 = pinned blur (OpenCV >= 3.4 / scalar rounding), 1 = OpenCV 3.2 SSE2 half-even prefix."""
+    lib().orc_set_blur_mode(int(mode))
 
 
 class Extractor:
@@ -317,6 +340,17 @@ def make_lba_result(prob: dict):
            "edge_erase": np.zeros(len(prob["edge_point"]), np.uint8)}
     R = LbaResult(out["pose_Tcw"].ctypes.data, out["point_Xw"].ctypes.data, out["edge_erase"].ctypes.data)
     return R, out
+
+
+def lba_chol_stats(reset: bool = False) -> dict:
+    """Dense-Cholesky pin exposure counters of the calling thread (lba_oracle_chol_stats)."""
+    L = lib()
+    L.lba_oracle_chol_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    L.lba_oracle_chol_stats.restype = None
+    a = np.zeros(2, np.int64)
+    r = C.c_double()
+    L.lba_oracle_chol_stats(_p(a), C.byref(r), 1 if reset else 0)
+    return {"schur_solves": int(a[0]), "nonpositive_pivot": int(a[1]), "min_pivot_ratio": r.value}
 
 
 def lba_solve(prob: dict, stop: bool = False):

@@ -522,14 +522,46 @@ static onode *push_child(olist *L, otmp *t) {
     return nd;
 }
 typedef struct { int size; long seq; onode *node; } sizeptr;
+/* tie key of equal-size nodes: 0 = creation sequence (the pin: later-created nodes are split
+ * first), 1 = reversed, 2 = a hash of the sequence (stands in for the heap addresses the reference
+ * compares, which glibc's reuse of freed nodes makes non-monotone); 1 and 2 exist only to measure
+ * how much the pin decides (tools/parity_exposure.py) */
+static int g_tie_mode;
+void orc_set_tie_mode(int mode) { g_tie_mode = mode; }
+static unsigned long tie_key(long seq) {
+    if (g_tie_mode == 1) return (unsigned long)(-seq);
+    if (g_tie_mode == 2) {
+        unsigned long z = (unsigned long)seq * 0x9E3779B97F4A7C15ul;
+        z ^= z >> 29;
+        return z * 0xBF58476D1CE4E5B9ul;
+    }
+    return (unsigned long)seq;
+}
 static int cmp_sizeptr(const void *a, const void *b) {
     const sizeptr *x = (const sizeptr *)a, *y = (const sizeptr *)b;
     if (x->size != y->size) return x->size < y->size ? -1 : 1;
-    return x->seq < y->seq ? -1 : (x->seq > y->seq ? 1 : 0);
+    const unsigned long kx = tie_key(x->seq), ky = tie_key(y->seq);
+    return kx < ky ? -1 : (kx > ky ? 1 : 0);
+}
+
+/* Exposure of the tie pin: per DistributeOctTree call that reaches the final
+ * phase, whether two processed nodes of equal size were split (their order -- creation sequence
+ * here, heap address in the reference -- decides the order of their children in lNodes, so the
+ * keypoint ORDER of the level may differ from the reference) and whether the cut `lNodes.size()
+ * >= N` fell inside a run of equal sizes (then the keypoint SET may differ). Counters:
+ * [0] calls, [1] calls reaching the final phase, [2] order-exposed calls, [3] set-exposed calls. */
+static _Thread_local long g_qt_stats[4];
+void orc_qt_tie_stats(long out[4], int reset) {
+    for (int i = 0; i < 4; i++) {
+        if (out) out[i] = g_qt_stats[i];
+        if (reset) g_qt_stats[i] = 0;
+    }
 }
 
 int orc_distribute_octtree(const orc_kp *keys, int nkeys, int minX, int maxX, int minY,
                            int maxY, int N, orc_kp *out, int cap) {
+    int st_final = 0, st_order = 0, st_set = 0;
+    g_qt_stats[0]++;
     const int nIni = (int)roundf((float)(maxX - minX) / (maxY - minY));
     if (nIni <= 0) return -1;            /* reference divides by zero here */
     const float hX = (float)(maxX - minX) / nIni;
@@ -583,6 +615,8 @@ int orc_distribute_octtree(const orc_kp *keys, int nkeys, int minX, int maxX, in
                 memcpy(vprev, vsp, sizeof(sizeptr) * pn);
                 vn = 0;
                 qsort(vprev, pn, sizeof(sizeptr), cmp_sizeptr);
+                st_final = 1;
+                int j_stop = -1;
                 for (int j = pn - 1; j >= 0; j--) {
                     otmp c[4];
                     divide_node(vprev[j].node, c);
@@ -594,8 +628,10 @@ int orc_distribute_octtree(const orc_kp *keys, int nkeys, int minX, int maxX, in
                         free(c[k].keys);
                     }
                     olist_erase(&L, vprev[j].node);
-                    if (L.size >= N) break;
+                    if (j < pn - 1 && vprev[j].size == vprev[j + 1].size) st_order = 1;
+                    if (L.size >= N) { j_stop = j; break; }
                 }
+                if (j_stop > 0 && vprev[j_stop - 1].size == vprev[j_stop].size) st_set = 1;
                 free(vprev);
                 if (L.size >= N || L.size == prevSize) bFinish = 1;
             }
@@ -603,6 +639,9 @@ int orc_distribute_octtree(const orc_kp *keys, int nkeys, int minX, int maxX, in
     }
 #undef VPUSH
     free(vsp);
+    g_qt_stats[1] += st_final;
+    g_qt_stats[2] += st_order;
+    g_qt_stats[3] += st_set;
     int n = 0;
     for (onode *it = L.head; it; it = it->next) {
         const orc_kp *best = &it->keys[0];
@@ -646,7 +685,24 @@ static inline int refl101(int i, int n) {
     while (i < 0 || i >= n) { if (i < 0) i = -i; if (i >= n) i = 2 * n - 2 - i; }
     return i;
 }
+/* OpenCV 3.2 (README.md:9) runs this blur through createSeparableLinearFilter's 8U smooth-kernel
+ * branch: the same integer taps (cvRound(256 * getGaussianKernel(9, 2, CV_32F))), exact integer
+ * row sums, and a column pass whose SSE2 part (SymmColumnVec_32s8u) accumulates in float -- exact
+ * here, every partial sum is a multiple of 2^-16 below 256 -- and rounds half to EVEN
+ * (_mm_cvtps_epi32), while its scalar tail (FixedPtCastEx) and OpenCV >= 3.4 round half UP. The
+ * two differ by one level exactly when acc = 2^16 (2k) + 2^15. Mode 1 restates that variant for
+ * the vectorised prefix of each row (16 then 4 columns at a time, as resize's mode 1) so its
+ * parity exposure can be counted (tools/parity_exposure.py); mode 0 (default) is the pin. */
+static int g_blur_mode;
+void orc_set_blur_mode(int mode) { g_blur_mode = mode; }
+static int simd_end16_4(int width) {
+    int x = 0;
+    for (; x <= width - 16; x += 16) {}
+    for (; x <= width - 4; x += 4) {}
+    return x;
+}
 void orc_gaussian_blur9(const uint8_t *src, int w, int h, uint8_t *dst) {
+    const int simd_end = g_blur_mode == 1 ? simd_end16_4(w) : 0;
     int *rows = (int *)malloc(sizeof(int) * (size_t)w * h);
     for (int y = 0; y < h; y++) {
         const uint8_t *s = src + (size_t)y * w;
@@ -660,7 +716,9 @@ void orc_gaussian_blur9(const uint8_t *src, int w, int h, uint8_t *dst) {
         for (int x = 0; x < w; x++) {
             uint32_t acc = 0;
             for (int k = 0; k < 9; k++) acc += (uint32_t)gk9[k] * (uint32_t)rows[(size_t)refl101(y + k - 4, h) * w + x];
-            dst[(size_t)y * w + x] = sat_u8((int)((acc + 32768u) >> 16));
+            int v = (int)((acc + 32768u) >> 16);
+            if (x < simd_end && (acc & 0x1FFFFu) == 0x8000u) v--;   /* half-even on an exact tie */
+            dst[(size_t)y * w + x] = sat_u8(v);
         }
     free(rows);
 }

@@ -116,6 +116,15 @@ void orc_undistort_points(const float *xy_in, float *xy_out, int n, const float 
 void orc_stereo_from_rgbd(const orc_kp *keys, const orc_kp *keysUn, int N, const float *depth,
                           int dstride, float mbf, float *uRight, float *depthOut);
 
+/* parity-exposure instruments (test infrastructure): quadtree tie counters of the calling
+ * thread ([0] calls, [1] final phase reached, [2] equal-size nodes split (order exposed),
+ * [3] cut inside an equal-size run (set exposed)); blur variant (0 = pin, 1 = OpenCV 3.2 SSE2
+ * half-even column rounding on the vectorised prefix). */
+void orc_qt_tie_stats(long out[4], int reset);
+void orc_set_blur_mode(int mode);
+/* tie key of the final-phase sort: 0 = creation sequence (pin), 1 = reversed, 2 = hashed */
+void orc_set_tie_mode(int mode);
+
 /* batched Hamming best/second-best (the ORBmatcher scan core) */
 void orc_hamming_best2(const uint8_t *q, int nq, const uint8_t *db, int ndb,
                        int *best_idx, int *best_d, int *second_d);
