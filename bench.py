@@ -208,6 +208,35 @@ def bench_e2e(amd, args, pool, bf, mb):
                             "PCIe-inclusive rate (value is the HBM-resident rate)"}}
 
 
+FP64_MFMA_PEAK_TFS = 75.08   # measured, tools/microbench/mfma_f64_peak.hip (profiles/r02_mfma_f64_peak.json)
+
+
+def lba_flops(prob: dict) -> dict:
+    """SURVEY §8d algorithmic FP64 flops of one LM trial: E * 450 (residual, Jacobians, quadratic
+    form) + sum over points of k(k+1)/2 * 324 + k * 90 + 60 (Schur pair products, k = free-pose
+    observations of the point) + (6P)^3 / 3 (Cholesky)."""
+    fixed = np.asarray(prob["pose_fixed"]).astype(bool)
+    ep = np.asarray(prob["edge_pose"])
+    free = ~fixed[ep]
+    k = np.bincount(np.asarray(prob["edge_point"])[free], minlength=len(prob["point_id"])).astype(np.float64)
+    P = int((~fixed).sum())
+    lin = 450.0 * len(ep)
+    schur = float((k * (k + 1) / 2 * 324 + k * 90 + 60).sum())
+    chol = (6.0 * P) ** 3 / 3
+    return {"linearize": lin, "schur": schur, "cholesky": chol, "per_trial": lin + schur + chol}
+
+
+def load_lba_pmc():
+    """MFMA PMC pass of the LocalBA kernels (profiles/r02_lba_pmc.json), if committed."""
+    f = ROOT / "profiles" / "r02_lba_pmc.json"
+    if not f.exists():
+        return None
+    try:
+        return json.loads(f.read_text()).get("kernels")
+    except ValueError:
+        return None
+
+
 def bench_localba(amd, args, dist, world, with_cpu):
     """C4: LocalBundleAdjustment on the synthetic 20 KF x 3000 MP graph; one LocalBA call per
     inserted keyframe (LocalMapping.cc:116-118) -> keyframes/s = calls/s, summed over ranks."""
@@ -232,9 +261,39 @@ def bench_localba(amd, args, dist, world, with_cpu):
     res = {"localba_kf_per_s": round(world * args.lba_steps / dt, 3),
            "localba": {"ms_per_call": round(1000 * dt / args.lba_steps, 3), "edges": int(len(prob["edge_point"])),
                        "keyframes": 20, "map_points": 3000, "lm_iterations": list(r["iterations"]),
-                       "dtype": "f64", "lm_control": "device-resident LM state (lba_decide), one host readback per chunk of trials",
+                       "lm_trials": list(r["trials"]),
+                       "dtype": "f64", "lm_control": "device-resident LM state, decided in lba_errors' last block; "
+                                                     "one host readback per chunk of trials",
                        "map_snapshot_bytes": map_bytes,
                        "map_source": "rank 0, RCCL broadcast" if dist is not None else "local"}}
+    # roofline: algorithmic FP64 flops per LM trial over the measured device time of
+    # one trial, against the FP64 matrix peak; the Schur SYRK alone against the same peak
+    ncall = 5
+    lba.profile(True)
+    for _ in range(ncall):
+        r = lba.solve(prob)
+    prof = lba.profile_read()
+    lba.profile(False)
+    trials = sum(r["trials"])
+    fl = lba_flops(prob)
+    gpu_ms_call = sum(v[0] for v in prof.values()) / ncall
+    syrk_ms, syrk_n = prof.get("lba_syrk_mfma", (0.0, 1))
+    syrk_avg_s = syrk_ms / max(syrk_n, 1) / 1e3
+    trial_s = gpu_ms_call / 1e3 / max(trials, 1)
+    achieved = fl["per_trial"] / trial_s / 1e12
+    pmc = load_lba_pmc()
+    res["localba"]["roofline"] = {
+        "bound": "mfma", "kernel": "LM trial (linearize .. decide)", "achieved": round(achieved, 5),
+        "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP64_MFMA_PEAK_TFS, 7), "traffic": None,
+        "algorithmic_flops_per_trial": fl["per_trial"], "flops_split": fl, "trial_ms": round(trial_s * 1e3, 4),
+        "syrk": {"avg_launch_ms": round(syrk_avg_s * 1e3, 4),
+                 "achieved": round(fl["schur"] / syrk_avg_s / 1e12, 4) if syrk_avg_s > 0 else None,
+                 "frac": round(fl["schur"] / syrk_avg_s / 1e12 / FP64_MFMA_PEAK_TFS, 5) if syrk_avg_s > 0 else None},
+        "peak_source": "v_mfma_f64_16x16x4_f64 measured on this MI355X (tools/microbench/mfma_f64_peak.hip; AMD spec 78.6)",
+        "pmc": pmc}
+    res["localba"]["gpu_ms_per_call"] = round(gpu_ms_call, 4)
+    res["localba"]["host_ms_per_call"] = round(1000 * dt / args.lba_steps - gpu_ms_call, 4)
+    res["localba"]["kernel_ms_per_call"] = {k: round(v[0] / ncall, 4) for k, v in sorted(prof.items())}
     if with_cpu:
         sys.path.insert(0, str(ROOT / "oracle"))
         import oracle

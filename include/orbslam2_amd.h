@@ -609,6 +609,7 @@ typedef struct {
     int32_t stopped;             /* 2 = *stop set before optimising: early return, outputs =
                                     inputs, nothing to write back (Optimizer.cc:902-904);
                                     1 = set after phase 1: phase 2 skipped (:913-917) */
+    int32_t trials[2];           /* LM trials (solve + update + chi2 evaluations) per phase */
 } lba_result;
 
 typedef struct lba_engine lba_engine;
@@ -622,6 +623,10 @@ typedef struct lba_engine lba_engine;
 int lba_create(lba_engine **out);
 void lba_destroy(lba_engine *e);
 int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile uint8_t *stop);
+/* Per-kernel hipEvent timing of lba_solve's trial chain on the engine stream (bench.py localba
+ * roofline); same semantics as orbx_profile / orbx_profile_read. */
+int lba_profile(lba_engine *e, int enable);
+int lba_profile_read(lba_engine *e, int idx, char *name, int name_cap, double *total_ms, int *launches);
 
 /* -------- library / measurement -------- */
 const char *orbslam2_amd_version(void);

@@ -625,6 +625,7 @@ int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint
     res->iterations[0] = res->iterations[1] = 0;
     res->chi2[0] = res->chi2[1] = 0;
     res->stopped = 0;
+    res->trials[0] = res->trials[1] = 0;   /* not counted by the oracle */
     int rc = 0;
     if (stop && *stop) {                  /* Optimizer.cc:902-904: return before optimising */
         res->stopped = 2;

@@ -317,7 +317,8 @@ class LbaProblem(C.Structure):
 
 class LbaResult(C.Structure):
     _fields_ = [("pose_Tcw", C.c_void_p), ("point_Xw", C.c_void_p), ("edge_erase", C.c_void_p),
-                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2), ("stopped", C.c_int32)]
+                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2), ("stopped", C.c_int32),
+                ("trials", C.c_int32 * 2)]
 
 
 def make_lba_structs(prob: dict):

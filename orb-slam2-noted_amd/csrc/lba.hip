@@ -39,6 +39,7 @@
 #include <cstdio>
 #include <cstring>
 #include <numeric>
+#include <string>
 #include <vector>
 
 #include "orb_engine.h"
@@ -66,7 +67,8 @@ constexpr int kRedBlocks = 16384;    // partial-sum region stride (blocks) for s
 // device-resident LM control (optimization_algorithm_levenberg.cpp:61-164 state)
 struct LMState {
     double lambda, ni, currentChi, iniChi, rho, final_chi;
-    int qmax, nBad, it, iterations, done, newiter, accepted, pad;
+    int qmax, nBad, it, iterations, done, newiter, accepted, trials;   // trials: LM trials decided
+    int cur, pad;   // estimate buffers: cur = 0 -> (T, X) current, (T2, X2) trial; 1 -> swapped
 };
 
 struct EdgeDev {
@@ -108,6 +110,7 @@ struct Graph {
     double *partial;       // [4][kRedBlocks]
     double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok, lambda
     LMState *lm;
+    unsigned *arrive;      // lba_errors block-arrival counter (the last block runs the LM decision)
     int Kpad, S;
     int NP;                // Schur dimension 6P padded to a multiple of kCB
     int NPW, wrow;         // slab leading dimension; Y row holding w (16 * ceil(6P / 16))
@@ -165,16 +168,19 @@ __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
         const int k = g.act[s];
         const EdgeDev e = g.E[k];
         double err[3];
-        edge_error(g, e, g.T, g.X, err);
+        const bool cur = g.lm->cur;
+        const Pose *Tc = cur ? g.T2 : g.T;
+        const double *Xc = cur ? g.X2 : g.X;
+        edge_error(g, e, Tc, Xc, err);
         g.err[3 * k] = err[0]; g.err[3 * k + 1] = err[1]; g.err[3 * k + 2] = err[2];
         const double chi = edge_chi2(e, err);
         double r0 = chi, r1 = 1.0;
         if (e.robust) huber(e, chi, r0, r1);
         rchi = r0;
         // Jacobians (types_six_dof_expmap.cpp:103-139, 188-234)
-        const Pose T = g.T[e.pose];
+        const Pose T = Tc[e.pose];
         double p[3], R[9];
-        pose_map(T, g.X + 3 * e.point, p);
+        pose_map(T, Xc + 3 * e.point, p);
         quat_to_R(T.q, R);
         const double x = p[0], y = p[1], z = p[2], z2 = z * z, fx = e.fx, fy = e.fy, bf = e.bf;
         double Jp[9], Jt[18];
@@ -504,6 +510,13 @@ template <int C> __device__ __forceinline__ double row_bcast(double v) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+#ifndef LBA_RSQ_NEWTON
+#define LBA_RSQ_NEWTON 2   // Newton steps after v_rsq_f64 on the pivot (the diagonal chain's latency)
+#endif
+#ifndef LBA_DIAG_PRIO
+#define LBA_DIAG_PRIO 0    // s_setprio of wave 0 while it factors a diagonal tile (critical path)
+#endif
+
 template <int J, int C> __device__ __forceinline__ void chol16_update(double (&row)[16], double (&li)[16]) {
     if constexpr (C < 16) {
         const double l = row_bcast<C>(row[J]);   // L[C][J]
@@ -526,7 +539,9 @@ template <int J> __device__ __forceinline__ void chol16_factor(double (&row)[16]
         const double h = 0.5 * d;
         double y = __builtin_amdgcn_rsq(d);
         y = __builtin_fma(y, __builtin_fma(-(h * y), y, 0.5), y);
+#if LBA_RSQ_NEWTON > 1
         y = __builtin_fma(y, __builtin_fma(-(h * y), y, 0.5), y);
+#endif
         row[J] = i == J ? d * y : row[J] * y;
         li[J] = (i == J ? 1.0 + li[J] : li[J]) * y;   // li[J] held -sum L[J][k] li[k]
         chol16_update<J, J + 1>(row, li);
@@ -540,7 +555,11 @@ __host__ __device__ constexpr size_t chol_tiled_lds(int n) {
                              2 * (size_t)chol_tiled_dim(n));
 }
 
-__global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
+#ifndef LBA_CHOL_THREADS
+#define LBA_CHOL_THREADS 1024   // 512: 87k cycles per 120 x 120 solve, 1024: 84k (faster load phase)
+#endif
+constexpr int kCT = LBA_CHOL_THREADS, kCW = kCT / 64;   // threads, waves of lba_chol_tiled
+__global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
     extern __shared__ double A[];   // N2 x LDA, then Linv[NT][16][17], y[N2], x[N2]
     __shared__ int fail;
     if (g.lm->done) return;
@@ -554,15 +573,16 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
 #define LBA_T(acc) do {} while (0)
 #endif
     const long long NP = g.NP;
-    // load: lower triangle of Hs, bs as row n, identity padding; 128 rows per pass (16 per
-    // wave, lanes along the row; N2 <= kSmallNP = 128), 32 loads in flight per thread
+    // load: lower triangle of Hs, bs as row n, identity padding; 128 rows per pass (128 / kCW
+    // per wave, lanes along the row; N2 <= kSmallNP = 128), all loads of a pass in flight
+    constexpr int RU = 128 / kCW;
     for (int rb = 0; rb < N2; rb += 128) {
-        double v[16][2];
+        double v[RU][2];
 #pragma unroll
-        for (int u = 0; u < 16; u++)
+        for (int u = 0; u < RU; u++)
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-                const int r = rb + wv + 8 * u, c = lane + 64 * h;
+                const int r = rb + wv + kCW * u, c = lane + 64 * h;
                 v[u][h] = 0.0;
                 if (r < N2 && c <= r) {
                     if (r < n) v[u][h] = g.Hs[r * NP + c];
@@ -571,10 +591,10 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
                 }
             }
 #pragma unroll
-        for (int u = 0; u < 16; u++)
+        for (int u = 0; u < RU; u++)
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-                const int r = rb + wv + 8 * u, c = lane + 64 * h;
+                const int r = rb + wv + kCW * u, c = lane + 64 * h;
                 if (r < N2 && c <= r) A[r * LDA + c] = v[u][h];
             }
     }
@@ -586,6 +606,7 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
 #endif
     // wave 0: factor + invert diagonal tile K (lane i of each 16-lane row = row i)
     auto diag = [&](int K) {
+        if (LBA_DIAG_PRIO) __builtin_amdgcn_s_setprio(LBA_DIAG_PRIO);
         const int k0 = 16 * K, i = lane & 15;
         double *LK = Linv + K * 16 * 17;
         double row[16], li[16];   // li: column i of L_kk^-1
@@ -603,6 +624,7 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
 #pragma unroll
         for (int r = 0; r < 16; r++) LK[r * 17 + i] = li[r];
         if (lane == 0 && bad) fail = 1;
+        if (LBA_DIAG_PRIO) __builtin_amdgcn_s_setprio(0);
     };
     if (wv == 0) diag(0);
     __syncthreads();
@@ -616,7 +638,7 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
         }
         const int k0 = 16 * K, r0 = k0 + 16, m = NT - K - 1;
         const double *LK = Linv + K * 16 * 17;
-        for (int I = wv; I < m; I += 8) {   // panel: L_ik = A_ik L_kk^-T
+        for (int I = wv; I < m; I += kCW) {   // panel: L_ik = A_ik L_kk^-T
             const int ri = r0 + 16 * I;
             double4_t acc = {0, 0, 0, 0};
 #pragma unroll
@@ -632,8 +654,8 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
         LBA_T(t_trsm);
         if (m == 0) break;
         const int ntile = m * (m + 1) / 2;
-        // trailing lower tiles; tile 0 = diagonal tile K + 1 -> wave 0, the rest -> waves 1-7
-        for (int t = wv == 0 ? 0 : wv; t < ntile; t += wv == 0 ? ntile : 7) {
+        // trailing lower tiles; tile 0 = diagonal tile K + 1 -> wave 0, the rest -> the other waves
+        for (int t = wv == 0 ? 0 : wv; t < ntile; t += wv == 0 ? ntile : kCW - 1) {
             int I = 0, u = t;
             while (u > I) { u -= I + 1; I++; }
             const int J = u;
@@ -662,7 +684,7 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
 #endif
     // back substitution L^T x = y, y = row n of the factor, zero past n: the padded rows of
     // the last block then contribute exactly 0 and every block runs fixed 16-term sums
-    for (int j = tid; j < N2; j += 512) yv[j] = j < n ? A[n * LDA + j] : 0.0;
+    for (int j = tid; j < N2; j += kCT) yv[j] = j < n ? A[n * LDA + j] : 0.0;
     __syncthreads();
     for (int K = (n - 1) / 16; K >= 0; K--) {
         const int k0 = 16 * K;
@@ -674,7 +696,7 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
             xv[k0 + tid] = s;
         }
         __syncthreads();
-        for (int j = tid; j < k0; j += 512) {
+        for (int j = tid; j < k0; j += kCT) {
             double s = yv[j];
 #pragma unroll
             for (int k = 0; k < 16; k++) s -= A[(k0 + k) * LDA + j] * xv[k0 + k];
@@ -682,7 +704,7 @@ __global__ __launch_bounds__(512) void lba_chol_tiled(Graph g) {
         }
         __syncthreads();
     }
-    for (int j = tid; j < n; j += 512) g.x[j] = xv[j];
+    for (int j = tid; j < n; j += kCT) g.x[j] = xv[j];
     if (tid == 0) g.scalars[4] = 1;
 #ifdef LBA_PROFILE
     if (tid == 0)
@@ -835,11 +857,16 @@ __global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
     if (g.lm->done) return;
     const int t = blockIdx.x * 256 + threadIdx.x;
     const double lambda = g.scalars[5];
+    const bool cur = g.lm->cur;   // current estimate -> trial buffer
+    const Pose *Tc = cur ? g.T2 : g.T;
+    Pose *Tt = cur ? g.T : g.T2;
+    const double *Xc = cur ? g.X2 : g.X;
+    double *Xt = cur ? g.X : g.X2;
     double sc = 0;
     if (t < g.P) {
         const int v = g.hpose[t];
         const double *xp = g.x + 6 * t;
-        g.T2[v] = pose_oplus(g.T[v], xp);
+        Tt[v] = pose_oplus(Tc[v], xp);
         for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + g.bp[6 * t + k]);
     } else if (t < g.P + g.Lm) {
         const int l = t - g.P, v = g.hpoint[l];
@@ -868,13 +895,18 @@ __global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
         for (int a = 0; a < 3; a++) {
             const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
             xl[a] = xa;
-            g.X2[3 * v + a] = g.X[3 * v + a] + xa;
+            Xt[3 * v + a] = Xc[3 * v + a] + xa;
             sc += xa * (lambda * xa + g.bl[3 * l + a]);
         }
     }
     block_sum_to(sc, part + blockIdx.x);
 }
-__global__ __launch_bounds__(256) void lba_errors(Graph g, double *part) {
+__device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthreads);
+
+// Trial chi2 of the active edges (block sums -> part[]) fused with the LM decision: the last
+// block to arrive (agent-scope release by every wave, one counter; the arriving block acquires,
+// cdna_hip_programming.md G16) sums the partials and runs lm_decide -- one launch fewer per trial.
+__global__ __launch_bounds__(256) void lba_errors(Graph g, double *part, int nbu, int nbe, int np, int nq) {
     if (g.lm->done) return;
     const int s = blockIdx.x * 256 + threadIdx.x;
     double r0 = 0;
@@ -882,7 +914,8 @@ __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part) {
         const int k = g.act[s];
         const EdgeDev e = g.E[k];
         double err[3];
-        edge_error(g, e, g.T2, g.X2, err);
+        const bool cur = g.lm->cur;
+        edge_error(g, e, cur ? g.T : g.T2, cur ? g.X : g.X2, err);
         g.err[3 * k] = err[0]; g.err[3 * k + 1] = err[1]; g.err[3 * k + 2] = err[2];
         const double chi = edge_chi2(e, err);
         double r1 = 1;
@@ -890,11 +923,24 @@ __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part) {
         if (e.robust) huber(e, chi, r0, r1);
     }
     block_sum_to(r0, part + blockIdx.x);
+    __shared__ int last;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this wave's stores (err, part) reach L2 / memory
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(g.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == gridDim.x - 1;
+        if (last) __hip_atomic_store(g.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next trial
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other blocks' partials
+    lm_decide(g, nbu, nbe, np, nq, 256);
 }
 
 // SparseOptimizer::optimize(iterations) start: lambda / nu / nBad reset (levenberg.cpp:66-72)
 __global__ void lba_lm_init(Graph g, int iterations) {
     LMState s{};
+    s.cur = g.lm->cur;   // which buffer holds the estimate carries over between optimize() calls
     s.ni = 2;
     s.iterations = iterations;
     s.newiter = 1;
@@ -906,9 +952,15 @@ __global__ void lba_lm_init(Graph g, int iterations) {
 // :155-161): thread 0 sums the update's computeScale block sums and the trial chi2 block sums
 // in block order, decides, and advances the state; an accepted trial becomes the current
 // estimate (copy T2 -> T, X2 -> X by the whole workgroup).
-__global__ __launch_bounds__(1024) void lba_decide(Graph g, int nbu, int nbe, int np, int nq) {
-    __shared__ int acc;
-    if (g.lm->done) return;
+__device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthreads) {
+    // the block partials come into LDS with one load per thread (a dependent chain of global
+    // loads on thread 0 cost ~10 us); thread 0 then sums them in block order as before
+    __shared__ double part_s[1024];
+    const int npart = nbu + nbe;
+    const bool staged = npart <= 1024;
+    if (staged)
+        for (int b = threadIdx.x; b < npart; b += nthreads) part_s[b] = g.scalars[8 + b];
+    __syncthreads();
     if (threadIdx.x == 0) {
         LMState s = *g.lm;
         const double *sc = g.scalars;
@@ -916,9 +968,10 @@ __global__ __launch_bounds__(1024) void lba_decide(Graph g, int nbu, int nbe, in
             s.currentChi = s.iniChi = sc[0];
             if (s.it == 0) s.lambda = sc[5];   // tau * maxDiagonal, formed by lba_prep_slots
         }
+        const double *pp = staged ? part_s : sc + 8;
         double sc_sum = 0, chi_sum = 0;
-        for (int b = 0; b < nbu; b++) sc_sum += sc[8 + b];
-        for (int b = 0; b < nbe; b++) chi_sum += sc[8 + nbu + b];
+        for (int b = 0; b < nbu; b++) sc_sum += pp[b];
+        for (int b = 0; b < nbe; b++) chi_sum += pp[nbu + b];
         const double tempChi = sc[4] != 0 ? chi_sum : DBL_MAX;
         double rho = s.currentChi - tempChi;
         const double scale = sc_sum + 1e-3;
@@ -936,6 +989,7 @@ __global__ __launch_bounds__(1024) void lba_decide(Graph g, int nbu, int nbe, in
             s.ni *= 2;
         }
         s.qmax++;
+        s.trials++;
         s.rho = rho;
         s.accepted = a;
         if (rho < 0 && s.qmax < 10) {
@@ -953,14 +1007,27 @@ __global__ __launch_bounds__(1024) void lba_decide(Graph g, int nbu, int nbe, in
             s.qmax = 0;
             if (!ok || s.it >= s.iterations) s.done = 1;
         }
+        if (a) s.cur ^= 1;   // the trial buffers become the current estimate (no copy)
         *g.lm = s;
-        acc = a;
     }
-    __syncthreads();
-    if (acc) {
-        for (int i = threadIdx.x; i < np; i += 1024) g.T[i] = g.T2[i];
-        for (int i = threadIdx.x; i < 3 * nq; i += 1024) g.X[i] = g.X2[i];
-    }
+    (void)np; (void)nq; (void)nthreads;
+}
+
+// End of one LM trial (optimization_algorithm_levenberg.cpp:96-164 + the ORB-SLAM2 stop rule
+// :155-161): thread 0 sums the update's computeScale block sums and the trial chi2 block sums
+// in block order, decides, and advances the state; an accepted trial becomes the current
+// estimate by swapping the roles of the two estimate buffers (LMState::cur). Standalone form (unused by
+// lba_optimize, which runs the decision in lba_errors' last block).
+__global__ __launch_bounds__(1024) void lba_decide(Graph g, int nbu, int nbe, int np, int nq) {
+    if (g.lm->done) return;
+    lm_decide(g, nbu, nbe, np, nq, 1024);
+}
+
+// Optimizer.cc:925-962: after optimize(5) every edge drops its robust kernel; outliers (flag)
+// go to level 1. In place on the device edges (was a 1.7 MB re-upload of the edge array).
+__global__ __launch_bounds__(256) void lba_drop_robust(EdgeDev *E, int ne) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k < ne) E[k].robust = 0;
 }
 
 // outlier test of Optimizer.cc:925-962 / 977-1008: chi2 (stale _error) + depth sign
@@ -1004,10 +1071,37 @@ struct lba_engine {
     hipStream_t stream = nullptr;
     DBuf T, T2, X, X2, E, err, act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items,
         ps_start, ps_items, slot_pt, slot_ph, con, hpl, Hll, bl, Hpp, bp, Dinv, Lc, Y, slab, Hs, bs, x, partial,
-        scalars, flags, lm;
+        scalars, flags, lm, arrive, arenaA, arenaB;
     double *h_scalars = nullptr;  // pinned
     LMState *h_lm = nullptr;      // pinned
+    void *h_stage = nullptr;      // pinned upload staging (grow-only)
+    size_t h_stage_bytes = 0;
+    // per-kernel hipEvent timing on the engine stream (lba_profile; bench.py localba roofline)
+    bool prof = false;
+    struct ProfRec { const char *name; hipEvent_t a, b; };
+    std::vector<ProfRec> recs;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
 };
+
+static int lprof_begin(lba_engine *e) {
+    if (!e->prof) return -1;
+    if (e->used + 2 > e->pool.size())
+        for (int k = 0; k < 256; k++) {
+            hipEvent_t ev;
+            if (hipEventCreate(&ev) != hipSuccess) return -1;
+            e->pool.push_back(ev);
+        }
+    const int h = (int)e->used;
+    e->used += 2;
+    (void)hipEventRecord(e->pool[h], e->stream);
+    return h;
+}
+static void lprof_end(lba_engine *e, int h, const char *name) {
+    if (h < 0) return;
+    (void)hipEventRecord(e->pool[h + 1], e->stream);
+    e->recs.push_back({name, e->pool[h], e->pool[h + 1]});
+}
 
 namespace {
 
@@ -1066,11 +1160,37 @@ void build_active(const HostGraph &h, ActiveSet &A) {
     }
 }
 
-template <class T> int upload(DBuf &b, const std::vector<T> &v, hipStream_t s) {
-    if (b.ensure(sizeof(T) * std::max<size_t>(1, v.size()))) return -1;
-    if (!v.empty() && hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s) != hipSuccess) return -1;
-    return 0;
+// The host arrays of one upload step packed into the engine's page-locked staging buffer and
+// sent to one device arena in ONE DMA (one pageable copy per array before: ~40 staged copies per
+// LocalBA call). add() returns the array's byte offset inside the arena.
+struct UploadSet {
+    struct Item { const void *src; size_t bytes, off; };
+    std::vector<Item> items;
+    size_t total = 0;
+    template <class T> size_t add(const std::vector<T> &v) { return add(v.data(), sizeof(T) * v.size()); }
+    size_t add(const void *src, size_t bytes) {
+        const size_t off = total;
+        items.push_back({src, bytes, off});
+        total += (std::max<size_t>(bytes, 1) + 255) & ~(size_t)255;
+        return off;
+    }
+};
+int upload_set(lba_engine *e, DBuf &arena, const UploadSet &u, hipStream_t s) {
+    // the staging buffer is reused: the previous upload from it must have landed
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+    if (u.total > e->h_stage_bytes) {
+        if (e->h_stage) (void)hipHostFree(e->h_stage);
+        e->h_stage = nullptr;
+        e->h_stage_bytes = 0;
+        if (hipHostMalloc(&e->h_stage, u.total, hipHostMallocDefault) != hipSuccess) return -1;
+        e->h_stage_bytes = u.total;
+    }
+    for (const auto &it : u.items)
+        if (it.bytes) std::memcpy((char *)e->h_stage + it.off, it.src, it.bytes);
+    if (arena.ensure(u.total)) return -1;
+    return hipMemcpyAsync(arena.p, e->h_stage, u.total, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : -1;
 }
+template <class T> T *at(DBuf &arena, size_t off) { return (T *)((char *)arena.p + off); }
 
 int nblk(int n) { return std::max(1, (n + 255) / 256); }
 
@@ -1081,7 +1201,7 @@ int nblk(int n) { return std::max(1, (n + 255) / 256); }
 // in chunks without host synchronisation; the device LM state turns the slots after the
 // last trial into no-ops. One state readback per chunk (the stop flag is polled there).
 static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterations, int np, int nq,
-                        const volatile uint8_t *stop, double *final_chi) {
+                        const volatile uint8_t *stop, double *final_chi, int *trials, int *cur) {
     hipStream_t s = e->stream;
     auto term = [&]() { return stop && *stop; };
     if (A.P + A.Lm == 0) return -1;
@@ -1092,16 +1212,26 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
     const int npair = ntile1 * (ntile1 + 1) / 2 - 1;           // without (w, w)
     const int nbu = nblk(A.P + A.Lm), nbe = nblk(nact);
     auto slot = [&]() {
+        int ph = lprof_begin(e);
         lba_linearize<<<nblk(nact), 256, 0, s>>>(g);
+        lprof_end(e, ph, "lba_linearize");
+        ph = lprof_begin(e);
         lba_reduce_points<<<nblk(A.Lm), 256, 0, s>>>(g);
         if (A.P > 0) lba_reduce_poses<<<A.P, 1024, 0, s>>>(g);
         lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nblk(nact), nblk(A.Lm), A.P);
+        lprof_end(e, ph, "lba_reduce_prep");
         if (A.P > 0) {
             const int kchunk = (((g.Kpad + g.S - 1) / g.S + 3) / 4) * 4;  // S * kchunk >= Kpad
+            ph = lprof_begin(e);
             lba_syrk_mfma<<<dim3(npair, g.S), 256, 0, s>>>(g, ntile1, kchunk);
+            lprof_end(e, ph, "lba_syrk_mfma");
+            ph = lprof_begin(e);
             lba_schur_reduce<<<n6, 256, 0, s>>>(g);   // slab sums: spread over n6 workgroups
+            lprof_end(e, ph, "lba_schur_reduce");
+            ph = lprof_begin(e);
             if (n6 <= kSmallNP) {
-                lba_chol_tiled<<<1, 512, chol_tiled_lds(n6), s>>>(g);
+                lba_chol_tiled<<<1, kCT, chol_tiled_lds(n6), s>>>(g);
+                lprof_end(e, ph, "lba_chol_tiled");
             } else {
                 lba_set_ok<<<1, 1, 0, s>>>(g);
                 for (int kb = 0; kb < n6; kb += kCB) {
@@ -1113,18 +1243,21 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
                     }
                 }
                 lba_chol_solve_blocked<<<1, 1024, sizeof(double) * n6, s>>>(g);
+                lprof_end(e, ph, "lba_chol_blocked");
             }
         } else {
             lba_set_ok<<<1, 1, 0, s>>>(g);
         }
         // scalars[8..): the update's computeScale block sums, then the trial chi2 block sums
+        ph = lprof_begin(e);
         lba_update<<<nbu, 256, 0, s>>>(g, g.scalars + 8);
-        lba_errors<<<nbe, 256, 0, s>>>(g, g.scalars + 8 + nbu);
-        lba_decide<<<1, 1024, 0, s>>>(g, nbu, nbe, np, nq);
+        lba_errors<<<nbe, 256, 0, s>>>(g, g.scalars + 8 + nbu, nbu, nbe, np, nq);   // + the LM decision
+        lprof_end(e, ph, "lba_update_errors_decide");
     };
     lba_lm_init<<<1, 1, 0, s>>>(g, iterations);
-    // first chunk: one trial per iteration plus one retry; then two slots per chunk
-    int chunk = iterations + 1, slots = 0;
+    // first chunk: one trial per iteration (the common case: every first trial accepted); then
+    // two slots per chunk while retries remain
+    int chunk = iterations, slots = 0;
     LMState st{};
     while (true) {
         for (int k = 0; k < chunk; k++) slot();
@@ -1142,6 +1275,8 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
         chunk = 2;
     }
     *final_chi = st.final_chi;
+    *trials = st.trials;
+    *cur = st.cur;
     return st.it;
 }
 
@@ -1168,6 +1303,8 @@ void lba_destroy(lba_engine *e) {
     if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
     if (e->h_scalars) (void)hipHostFree(e->h_scalars);
     if (e->h_lm) (void)hipHostFree(e->h_lm);
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    for (hipEvent_t ev : e->pool) (void)hipEventDestroy(ev);
     delete e;
 }
 
@@ -1177,6 +1314,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     hipStream_t s = e->stream;
     const int np = p->n_poses, nq = p->n_points, ne = p->n_edges;
     r->iterations[0] = r->iterations[1] = 0;
+    r->trials[0] = r->trials[1] = 0;
     r->chi2[0] = r->chi2[1] = 0;
     r->stopped = 0;
     if (stop && *stop) {  // Optimizer.cc:902-904: return before optimising, nothing written back
@@ -1221,34 +1359,44 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         const float *cam = p->pose_cam + 5 * d.pose;
         d.fx = cam[0]; d.fy = cam[1]; d.cx = cam[2]; d.cy = cam[3]; d.bf = cam[4];
     }
-    if (upload(e->T, T, s) || upload(e->T2, T, s) || upload(e->X, X, s) || upload(e->X2, X, s) ||
-        upload(e->E, E, s) || e->err.ensure(sizeof(double) * 3 * std::max(ne, 1)) ||
+    UploadSet ua;
+    const size_t oT = ua.add(T), oT2 = ua.add(T), oX = ua.add(X), oX2 = ua.add(X), oE = ua.add(E);
+    if (upload_set(e, e->arenaA, ua, s) || e->err.ensure(sizeof(double) * 3 * std::max(ne, 1)) ||
         e->flags.ensure(std::max(ne, 1)) || e->scalars.ensure((8 + 2 * kRedBlocks) * sizeof(double)) ||
-        e->partial.ensure(sizeof(double) * 4 * kRedBlocks) || e->lm.ensure(sizeof(LMState)))
+        e->partial.ensure(sizeof(double) * 4 * kRedBlocks) || e->lm.ensure(sizeof(LMState)) || e->arrive.ensure(64))
         return ORBX_EDEVICE;
     LBA_CHK(hipMemsetAsync(e->err.p, 0, sizeof(double) * 3 * std::max(ne, 1), s));
+    LBA_CHK(hipMemsetAsync(e->arrive.p, 0, 64, s));
+    LBA_CHK(hipMemsetAsync(e->lm.p, 0, sizeof(LMState), s));   // cur = 0: (T, X) hold the estimate
+    int cur = 0;
     Graph g{};
-    g.T = e->T.as<Pose>(); g.T2 = e->T2.as<Pose>();
-    g.X = e->X.as<double>(); g.X2 = e->X2.as<double>();
-    g.E = e->E.as<EdgeDev>();
+    g.T = at<Pose>(e->arenaA, oT); g.T2 = at<Pose>(e->arenaA, oT2);
+    g.X = at<double>(e->arenaA, oX); g.X2 = at<double>(e->arenaA, oX2);
+    g.E = at<EdgeDev>(e->arenaA, oE);
+    g.arrive = e->arrive.as<unsigned>();
     g.err = e->err.as<double>();
     g.scalars = e->scalars.as<double>();
     g.partial = e->partial.as<double>();
     g.lm = e->lm.as<LMState>();
-    auto setup = [&](ActiveSet &A) -> int {
-        if (upload(e->act, A.act, s) || upload(e->pose_hidx, A.pose_hidx, s) || upload(e->point_hidx, A.point_hidx, s) ||
-            upload(e->hpose, A.hpose, s) || upload(e->hpoint, A.hpoint, s) || upload(e->pt_start, A.pt_start, s) ||
-            upload(e->pt_items, A.pt_items, s) || upload(e->ps_start, A.ps_start, s) || upload(e->ps_items, A.ps_items, s) ||
-            upload(e->slot_pt, A.slot_pt, s) || upload(e->slot_ph, A.slot_ph, s))
-            return -1;
+    // per optimize(): the active-set index arrays (and, for the second phase, the edges with their
+    // robust kernels removed) in one upload
+    auto setup = [&](ActiveSet &A, const std::vector<EdgeDev> *edges) -> int {
+        UploadSet ub;
+        const size_t o_act = ub.add(A.act), o_pose_hidx = ub.add(A.pose_hidx), o_point_hidx = ub.add(A.point_hidx),
+                     o_hpose = ub.add(A.hpose), o_hpoint = ub.add(A.hpoint), o_pt_start = ub.add(A.pt_start),
+                     o_pt_items = ub.add(A.pt_items), o_ps_start = ub.add(A.ps_start), o_ps_items = ub.add(A.ps_items),
+                     o_slot_pt = ub.add(A.slot_pt), o_slot_ph = ub.add(A.slot_ph);
+        const size_t o_E = edges ? ub.add(*edges) : 0;
+        if (upload_set(e, e->arenaB, ub, s)) return -1;
         const int nact = (int)A.act.size();
-        g.act = e->act.as<int>(); g.nact = nact;
-        g.pose_hidx = e->pose_hidx.as<int>(); g.point_hidx = e->point_hidx.as<int>();
-        g.hpose = e->hpose.as<int>(); g.hpoint = e->hpoint.as<int>();
+        g.act = at<int>(e->arenaB, o_act); g.nact = nact;
+        g.pose_hidx = at<int>(e->arenaB, o_pose_hidx); g.point_hidx = at<int>(e->arenaB, o_point_hidx);
+        g.hpose = at<int>(e->arenaB, o_hpose); g.hpoint = at<int>(e->arenaB, o_hpoint);
         g.P = A.P; g.Lm = A.Lm;
-        g.pt_start = e->pt_start.as<int>(); g.pt_items = e->pt_items.as<int>();
-        g.ps_start = e->ps_start.as<int>(); g.ps_items = e->ps_items.as<int>();
-        g.slot_pt = e->slot_pt.as<int>(); g.slot_ph = e->slot_ph.as<int>();
+        g.pt_start = at<int>(e->arenaB, o_pt_start); g.pt_items = at<int>(e->arenaB, o_pt_items);
+        g.ps_start = at<int>(e->arenaB, o_ps_start); g.ps_items = at<int>(e->arenaB, o_ps_items);
+        g.slot_pt = at<int>(e->arenaB, o_slot_pt); g.slot_ph = at<int>(e->arenaB, o_slot_ph);
+        if (edges) g.E = at<EdgeDev>(e->arenaB, o_E);
         g.Kpad = std::max(4, ((3 * A.Lm + 3) / 4) * 4);
         g.NP = std::max(kCB, ((6 * A.P + kCB - 1) / kCB) * kCB);
         const size_t NP = (size_t)g.NP, NPW = NP + 16;
@@ -1277,44 +1425,42 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
             hipMemsetAsync(g.x, 0, sizeof(double) * (6 * A.P + 3 * A.Lm + 8), s) != hipSuccess)
             return -1;
         // trial buffers start equal to the current estimate (inactive vertices never change)
-        if (hipMemcpyAsync(g.T2, g.T, sizeof(Pose) * std::max(np, 1), hipMemcpyDeviceToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(g.X2, g.X, sizeof(double) * 3 * std::max(nq, 1), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        if (hipMemcpyAsync(cur ? g.T : g.T2, cur ? g.T2 : g.T, sizeof(Pose) * std::max(np, 1), hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(cur ? g.X : g.X2, cur ? g.X2 : g.X, sizeof(double) * 3 * std::max(nq, 1), hipMemcpyDeviceToDevice, s) != hipSuccess)
             return -1;
         return 0;
     };
     ActiveSet A;
     build_active(h, A);
-    if (setup(A)) return ORBX_EDEVICE;
+    if (setup(A, nullptr)) return ORBX_EDEVICE;
     // lba_optimize: >= 0 iterations, -1 = the pre-LM error evaluation failed (g2o's optimize()
     // returning -1, a valid outcome), -3 = HIP runtime error
-    r->iterations[0] = lba_optimize(e, g, A, 5, np, nq, stop, &r->chi2[0]);
+    r->iterations[0] = lba_optimize(e, g, A, 5, np, nq, stop, &r->chi2[0], &r->trials[0], &cur);
     if (r->iterations[0] == -3) return ORBX_EDEVICE;
     if (r->iterations[0] < -1) return ORBX_EINVAL;
     const bool bDoMore = !(stop && *stop);
     std::vector<uint8_t> flag(std::max(ne, 1));
     if (bDoMore) {
-        lba_outliers<<<nblk(ne), 256, 0, s>>>(g.E, g.err, g.T, g.X, ne, e->flags.as<uint8_t>());
+        lba_outliers<<<nblk(ne), 256, 0, s>>>(g.E, g.err, cur ? g.T2 : g.T, cur ? g.X2 : g.X, ne, e->flags.as<uint8_t>());
         LBA_CHK(hipMemcpyAsync(flag.data(), e->flags.p, ne, hipMemcpyDeviceToHost, s));
         LBA_CHK(hipStreamSynchronize(s));
-        for (int k = 0; k < ne; k++) {
+        for (int k = 0; k < ne; k++)
             if (flag[k]) h.level[k] = 1;
-            E[k].robust = 0;
-        }
-        if (upload(e->E, E, s)) return ORBX_EDEVICE;
-        g.E = e->E.as<EdgeDev>();
+        lba_drop_robust<<<nblk(ne), 256, 0, s>>>(const_cast<EdgeDev *>(g.E), ne);
+        LBA_CHK(hipGetLastError());
         build_active(h, A);
-        if (setup(A)) return ORBX_EDEVICE;
-        r->iterations[1] = lba_optimize(e, g, A, 10, np, nq, stop, &r->chi2[1]);
+        if (setup(A, nullptr)) return ORBX_EDEVICE;
+        r->iterations[1] = lba_optimize(e, g, A, 10, np, nq, stop, &r->chi2[1], &r->trials[1], &cur);
         if (r->iterations[1] == -3) return ORBX_EDEVICE;
         if (r->iterations[1] < -1) return ORBX_EINVAL;
     } else {
         r->stopped = 1;
     }
-    lba_outliers<<<nblk(ne), 256, 0, s>>>(g.E, g.err, g.T, g.X, ne, e->flags.as<uint8_t>());
+    lba_outliers<<<nblk(ne), 256, 0, s>>>(g.E, g.err, cur ? g.T2 : g.T, cur ? g.X2 : g.X, ne, e->flags.as<uint8_t>());
     LBA_CHK(hipGetLastError());
     LBA_CHK(hipMemcpyAsync(r->edge_erase, e->flags.p, ne, hipMemcpyDeviceToHost, s));
-    LBA_CHK(hipMemcpyAsync(T.data(), g.T, sizeof(Pose) * np, hipMemcpyDeviceToHost, s));
-    LBA_CHK(hipMemcpyAsync(X.data(), g.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, s));
+    LBA_CHK(hipMemcpyAsync(T.data(), cur ? g.T2 : g.T, sizeof(Pose) * np, hipMemcpyDeviceToHost, s));
+    LBA_CHK(hipMemcpyAsync(X.data(), cur ? g.X2 : g.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, s));
     LBA_CHK(hipStreamSynchronize(s));
     for (int i = 0; i < np; i++) {  // Converter::toCvMat(SE3Quat)
         double R[9];
@@ -1327,6 +1473,38 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         o[12] = 0; o[13] = 0; o[14] = 0; o[15] = 1;
     }
     for (int i = 0; i < 3 * nq; i++) r->point_Xw[i] = (float)X[i];
+    return ORBX_OK;
+}
+
+int lba_profile(lba_engine *e, int enable) {
+    if (!e) return ORBX_EINVAL;
+    for (auto &r : e->recs) (void)hipEventSynchronize(r.b);
+    e->prof = enable != 0;
+    e->recs.clear();
+    e->used = 0;
+    return ORBX_OK;
+}
+
+int lba_profile_read(lba_engine *e, int idx, char *name, int name_cap, double *total_ms, int *launches) {
+    if (!e || idx < 0) return ORBX_EINVAL;
+    std::vector<std::string> names;
+    for (auto &r : e->recs) {
+        LBA_CHK(hipEventSynchronize(r.b));
+        if (std::find(names.begin(), names.end(), std::string(r.name)) == names.end()) names.push_back(r.name);
+    }
+    if (idx >= (int)names.size()) return ORBX_ESTATE;
+    double tot = 0;
+    int cnt = 0;
+    for (auto &r : e->recs) {
+        if (names[idx] != r.name) continue;
+        float ms = 0;
+        LBA_CHK(hipEventElapsedTime(&ms, r.a, r.b));
+        tot += ms;
+        cnt++;
+    }
+    if (name && name_cap > 0) std::snprintf(name, (size_t)name_cap, "%s", names[idx].c_str());
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = cnt;
     return ORBX_OK;
 }
 

@@ -23,7 +23,8 @@ from pathlib import Path
 import numpy as np
 
 PKG_ROOT = Path(__file__).resolve().parents[2]          # orb-slam2-noted_amd/
-LIB_PATH = PKG_ROOT / "liborbslam2_amd.so"
+# ORBSLAM_AMD_LIB: an instrumented build of the same sources (tools/*: profiling variants)
+LIB_PATH = Path(os.environ["ORBSLAM_AMD_LIB"]) if os.environ.get("ORBSLAM_AMD_LIB") else PKG_ROOT / "liborbslam2_amd.so"
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -86,6 +87,8 @@ SIGNATURES = [
     ("orbslam2_amd_device_sync", _I, []),
     ("orbslam2_amd_set_device", _I, [_I]),
     ("orbx_profile", _I, [_P, _I]),
+    ("lba_profile", _I, [_P, _I]),
+    ("lba_profile_read", _I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     ("orbf_rgbd", _I, [_P, _P, _I, _P, _P, _F, _P, _P, _P, _I]),
     ("orbf_rgbd_batch_device", _I, [_P, _P, C.c_size_t, _I, _P, _P, _F, _P]),
     ("orbf_rgbd_fetch", _I, [_P, _I, _P, _P, _P, _I]),
@@ -640,7 +643,8 @@ class LbaProblem(C.Structure):
 
 class LbaResult(C.Structure):
     _fields_ = [("pose_Tcw", C.c_void_p), ("point_Xw", C.c_void_p), ("edge_erase", C.c_void_p),
-                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2), ("stopped", C.c_int32)]
+                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2), ("stopped", C.c_int32),
+                ("trials", C.c_int32 * 2)]
 
 
 _LBA_FIELDS = ("pose_id", "pose_fixed", "pose_Tcw", "pose_cam", "point_id", "point_Xw", "edge_point",
@@ -689,6 +693,24 @@ class LocalBundleAdjustment:
         out["iterations"] = tuple(R.iterations)
         out["chi2"] = tuple(R.chi2)
         out["stopped"] = R.stopped
+        out["trials"] = tuple(R.trials)
+        return out
+
+    def profile(self, enable: bool):
+        _check(lib().lba_profile(self._h, 1 if enable else 0), "lba_profile")
+
+    def profile_read(self) -> dict:
+        """{kernel group: (total ms, launches)} since profile(True)."""
+        out, i = {}, 0
+        buf = C.create_string_buffer(64)
+        while True:
+            ms, n = C.c_double(), C.c_int()
+            rc = lib().lba_profile_read(self._h, i, buf, 64, C.byref(ms), C.byref(n))
+            if rc == ORBX_ESTATE:
+                break
+            _check(rc, "lba_profile_read")
+            out[buf.value.decode()] = (ms.value, n.value)
+            i += 1
         return out
 
 
