@@ -48,7 +48,10 @@ struct ExtractGeom {
     int ini_th, min_th, resize_mode;
     int rz_col_off[ORBX_MAXL], rz_row_off[ORBX_MAXL], rz_simd_end[ORBX_MAXL];
     int blur_tiles_x[ORBX_MAXL], blur_tiles_y[ORBX_MAXL], blur_tile_base[ORBX_MAXL + 1];
-    int nms_sm_words, nms_wave_words, nms_mask_off;  // per-wavefront LDS of the cell NMS kernel (u32 words)
+    // FAST cell grid per level (ORBextractor.cc:1084-1118): cell sides, the cells kept by the
+    // row / column bounds, and ceil(2^20 / side) for the pixel -> cell division
+    int hcell[ORBX_MAXL], wcell[ORBX_MAXL], ncell_rows[ORBX_MAXL], ncell_cols[ORBX_MAXL];
+    int hcell_mag[ORBX_MAXL], wcell_mag[ORBX_MAXL];
 };
 
 struct DevBuf {
@@ -136,7 +139,7 @@ struct orbx_engine {
     orbamd::ExtractGeom g{};
     std::vector<orbamd::CellDesc> cells;
     // device buffers
-    orbamd::DevBuf d_mmap, d_cells, d_rz, d_rzr, d_pattern, d_in, d_pyr, d_blur, d_cell_cnt, d_cell_keys,
+    orbamd::DevBuf d_rz, d_rzr, d_pattern, d_in, d_pyr, d_blur, d_cell_cnt, d_cell_keys,
         d_qt, d_qt_nodes, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt;
     // stereo
     orbamd::DevBuf d_st_sorted, d_st_res, d_st_u, d_st_depth, d_st_dist, d_st_rows;

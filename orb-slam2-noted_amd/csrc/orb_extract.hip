@@ -208,36 +208,55 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 }
 
 // ------------------------------------------------------------------------------------
-// K2: fused FAST strength map + GaussianBlur over 128x16 tiles of every level.
+// K2: FAST + per-cell non-maximum suppression + GaussianBlur over 128x16 tiles of every
+// level, one 256-thread workgroup per tile (ComputeKeyPointsOctTree's cell loop,
+// ORBextractor.cc:1084-1153, and the blur of :1617-1625).
 //
 // cornerScore<16> (OpenCV fast_score.cpp) returns max(th, M) - 1 where
 //   M = max over the 16 circular 9-arcs of max(min_arc(v - ring), min_arc(ring - v)),
 // and the FAST-9 test at threshold th is exactly M > th (the pre-tests of
-// FAST_t are necessary conditions of the 9-arc test). M is therefore pixel-intrinsic: one
-// pass computes it once per pixel for both thresholds of the per-cell retry
-// (ORBextractor.cc:1122-1135), and the cell kernel (K2b) applies threshold, NMS and order.
+// FAST_t are necessary conditions of the 9-arc test). M is pixel-intrinsic, and the cells
+// of the grid partition the detection region: cell (i, j) detects in rows
+// [19 + i*hCell, min(19 + (i+1)*hCell, maxBorderY - 3)) and the matching columns, its ROI
+// being the detection rectangle plus cv::FAST's 3-pixel ring margin. cv::FAST's 3x3 NMS on
+// the ROI scores neighbours outside the detection rectangle 0, so a pixel's NMS only reads
+// the M of its 8 neighbours that share its cell. With s_th(q) = M_q > th ? M_q - 1 : 0 the
+// survivors at a threshold th >= tlo = min(iniThFAST, minThFAST) are exactly the
+// survivors at tlo with M > th (every neighbour keeps its order with M_p - 1), so one NMS
+// at tlo serves both passes of the per-cell retry: the workgroup emits every survivor at
+// tlo into its cell's slot list (score M - 1), and the quadtree kernel keeps a cell's
+// entries with score >= iniThFAST when there is one, else those >= minThFAST (:1119-1135).
+// The order inside a cell's list is free (global atomics): the only order the quadtree
+// depends on -- the first key of maximal response in a node (:1028-1034) -- is restated
+// there as the reference list position (cell row-major, then row-major in the cell).
 //
-// One 256-thread workgroup per tile, one 24x136 LDS halo tile (reflect-101) feeding both:
+// The LDS halo tile (24x136 bytes, reflect-101 at the level edges) feeds:
 //  1. staging: aligned dword loads + v_alignbyte (per-byte reflection only at edges);
-//  2. FAST pre-filter: every 9-arc holds two adjacent compass pixels (ring 0/4/8/12), so
-//     max over adjacent compass pairs of min(d) (darker) / min(-d) (brighter) bounds M
-//     from above; packed int16 pairs, 8 pixels per thread. Pixels whose bound exceeds
-//     the lower threshold join a per-wavefront candidate list (~12 % of the pixels of
-//     textured imagery; ~1.4 % are corners);
-//  3. exact M for the candidates only (v_min3/v_max3 9-arc windows) into an LDS strength
-//     tile; every other pixel stores 0 -- thr_score(0, th) == thr_score(M, th) for every
-//     M <= min(thresholds), so K2b sees the scores of the dense map;
-//  4. cv::GaussianBlur(9x9, sigma 2) of ORBextractor.cc:1617-1625 (bit-exact fixed-point
-//     path, SURVEY.md A.3 -- exact integer row sums, Q16 column sums, (acc + 2^15) >> 16):
-//     row pass with v_dot4_u32_u8 on byte quads, stored vertically pair-interleaved (rows
-//     2p, 2p+1 in one dword) so the column pass runs on v_dot2_u32_u16.
-// Blurred level and strength map use the row pitch g.bp[l] (16-byte aligned) so both are
-// written with dword / dwordx2 stores.
+//  2. FAST pre-filter over the tile plus its one-pixel ring (the NMS neighbours): every
+//     9-arc holds two adjacent compass pixels (ring 0/4/8/12), so a pixel is a darker
+//     (brighter) candidate only if the sign-bit test below passes for an adjacent compass
+//     pair; packed int16 pairs, 4-pixel groups. Candidates (~12 % of the pixels of textured
+//     imagery, ~1.4 % are corners) join a per-wavefront list with their polarity flags;
+//  3. exact M per candidate: one 9-arc score (v_mad_i32_i24 signs the differences, so the
+//     darker and brighter scores run the same instructions; the ~0.4 % candidates of
+//     both polarities run it twice) into an LDS score tile (0 elsewhere: every M <= tlo
+//     behaves as 0). Tile pixels with M > tlo go to a hot list written into the
+//     wavefront's already consumed candidate slots;
+//  4. GaussianBlur 9x9 sigma 2 (bit-exact fixed-point path, SURVEY.md A.3 -- exact integer
+//     row sums, Q16 column sums, (acc + 2^15) >> 16): row pass with v_dot4_u32_u8 on byte
+//     quads, stored vertically pair-interleaved (rows 2p, 2p+1 in one dword) so the column
+//     pass runs on v_dot2_u32_u16; written with dword stores at the row pitch g.bp[l];
+//  5. NMS of the hot pixels against their in-cell neighbours and the atomic emission of
+//     the survivors' keys (pack_key: x, y relative to minBorder, score M - 1).
+// No strength map leaves the workgroup.
 // ------------------------------------------------------------------------------------
 #define FB_TW 128
 #define FB_TH 16
-#define FB_LW (FB_TW + 8)   // LDS tile row bytes
+#define FB_LW (FB_TW + 8)   // LDS tile row bytes (cols x0-4 .. x0+131)
 #define FB_LD (FB_LW / 4)   // LDS tile row dwords
+#define FB_MR (FB_TH + 2)   // score rows y0-1 .. y0+16 (tile + NMS ring)
+#define FB_NG (FB_MR * FB_LD)   // score tile dwords
+#define FB_CCAP (FB_MR * (FB_TW + 2) + 64)   // candidate slots: every score pixel + one chunk of hot-list slack
 
 __device__ __forceinline__ int refl101(int i, int n) {
     if (n == 1) return 0;
@@ -248,8 +267,6 @@ __device__ __forceinline__ int refl101(int i, int n) {
     return i;
 }
 
-
-
 // bytes j, j+1 of the little-endian 16-byte segment w[0..3], zero-extended into int16 lanes
 __device__ __forceinline__ s16x2 byte_pair(const uint32_t *w, int j) {
     const int k = j & 3, d = j >> 2;
@@ -258,18 +275,32 @@ __device__ __forceinline__ s16x2 byte_pair(const uint32_t *w, int j) {
     return __builtin_bit_cast(s16x2, r);
 }
 
-
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
 
+// 9-arc score max(0, max_arc min_k d_k) with d_k = (ring_k ^ xm) + c: darker d = v - ring
+// (xm = -1, c = v + 1), brighter d = ring - v (xm = 0, c = -v) -- one v_xad_u32 per ring pixel
+__device__ __forceinline__ int fast_arc_score(const int *rg, int c, int xm) {
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = (rg[k] ^ xm) + c;
+    int n3[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) n3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+    int A = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) A = max(A, min(min(n3[k], n3[(k + 3) & 15]), n3[(k + 6) & 15]));
+    return A;
+}
+
 __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
-                                                        uint8_t *blur, uint8_t *mmap) {
+                                                        uint8_t *blur, int *cell_cnt, uint32_t *cell_keys) {
     __shared__ uint32_t tin[(FB_TH + 8) * FB_LD];
     __shared__ uint32_t trowp[((FB_TH + 8) / 2) * FB_TW];
-    __shared__ uint32_t mt[FB_TH * FB_TW / 4];
-    __shared__ uint16_t clist[4][512];
-    __shared__ int ccount[4];
+    __shared__ uint32_t mt[FB_NG];   // exact M bytes, (mrow, x - x0 + 4)
+    __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets)
+    __shared__ int ncand_sh, hcount[4];
     const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
     int t = blockIdx.x, l = 0;
     while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
@@ -279,13 +310,6 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     const int x0 = tx * FB_TW, y0 = ty * FB_TH;
     int pitch;
     const uint8_t *src = level_ptr(g, in, pyr, b, l, &pitch);
-#ifdef FB_PROFILE
-    long long fbt[8];
-#define FBP(k) do { fbt[k] = clock64(); } while (0)
-    FBP(0);
-#else
-#define FBP(k) do {} while (0)
-#endif
     // 1. stage rows y0-4 .. y0+19, cols x0-4 .. x0+131 (interior tiles: no reflection tests)
     if (y0 >= 4 && y0 + FB_TH + 4 <= h && x0 >= 4 && x0 + FB_TW + 4 <= w) {
         const uint8_t *s0 = src + (long long)(y0 - 4) * pitch + (x0 - 4);
@@ -308,63 +332,100 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         }
         tin[i] = v;
     }
+    for (int i = threadIdx.x; i < FB_NG; i += 256) mt[i] = 0u;
+    if (threadIdx.x == 0) ncand_sh = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = wave_id();
-    const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;  // pixels (y0 + r, x0 + cb + i)
     const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
     const int tlo = min(th_a, th_b);
-    FBP(1);
-    // 2. FAST pre-filter. Only pixels of the FAST detection region [19, w-19) x [19, h-19)
-    // (cell ROIs start at minBorder 16 and end at maxBorder = size - 16, cv::FAST detects in
-    // [3, roi - 3), ORBextractor.cc:1061-1135) can be keypoints: a wavefront whose 4 rows all
-    // lie outside skips the test, and candidates outside the region are dropped.
-    int ncand = 0;
-    mt[r * (FB_TW / 4) + (cb >> 2)] = 0u;
-    mt[r * (FB_TW / 4) + (cb >> 2) + 1] = 0u;
-    if (y0 + 4 * wv + 3 >= 19 && y0 + 4 * wv < h - 19) {   // wave-uniform
-        uint32_t S[4], C[4], N[4];  // tile cols cb .. cb+15 (image x0+cb-4 .. x0+cb+11)
+    // 2. FAST pre-filter over the score domain rows y0-1 .. y0+16, cols x0-1 .. x0+128 (the
+    // tile and its NMS ring), clipped to the detection region [19, w-19) x [19, h-19) (cell
+    // ROIs start at minBorder 16 and end at maxBorder = size - 16, cv::FAST detects in
+    // [3, roi - 3)). Tile rows: 16 threads x 8 pixels per row; ring rows y0-1 and y0+16:
+    // 17 groups of 8 each on wavefront 2; ring columns x0-1 and x0+128 (32 pixels) go to the
+    // exact score unfiltered on wavefront 3 (the two wavefronts with one blur-row task).
+    {
+        const int dx0 = max(19, x0 - 1), dx1 = min(w - 19, x0 + FB_TW + 1);
+        const int dy0 = max(19, y0 - 1), dy1 = min(h - 19, y0 + FB_TH + 1);
+        // Compass bound on four pixels per dword (SWAR on v_lerp_u8, which adds two bytes and a
+        // rounding bit and halves, per byte): u = lerp(c, ~r, 1) = 128 + floor((c - r) / 2), so
+        // c - r >= T (T = tlo + 1) implies u >= 128 + floor(T / 2) (equivalent for even T), and
+        // lerp(u, ~K, 1) has its top bit set iff u >= K. Darker pass at compass pixel r:
+        // c - r >= T; brighter: r - c >= T. A pixel is a candidate iff (N or S) and (E or W)
+        // pass for one polarity (every 9-arc holds two adjacent compass pixels). The bound is
+        // only ever looser than the exact test, never tighter.
+        const uint32_t ONE = 0x01010101u, HI = 0x80808080u;
+        const uint32_t NK = ~((uint32_t)min(128 + ((tlo + 1) >> 1), 255) * ONE);
+        auto swar4 = [&](uint32_t C, uint32_t Cm, uint32_t Cp, uint32_t N, uint32_t S) {
+            const uint32_t W = __builtin_amdgcn_alignbyte(C, Cm, 1);   // cols -3 .. 0
+            const uint32_t E = __builtin_amdgcn_alignbyte(Cp, C, 3);   // cols +3 .. +6
+            const uint32_t NC = ~C;
+            auto dk = [&](uint32_t r) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(C, ~r, ONE), NK, ONE); };
+            auto bk = [&](uint32_t r) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(r, NC, ONE), NK, ONE); };
+            const uint32_t dark = (dk(N) | dk(S)) & (dk(E) | dk(W));
+            const uint32_t bright = (bk(N) | bk(S)) & (bk(E) | bk(W));
+            return (dark | bright) & HI;
+        };
+        // candidates among the 8 pixels xb .. xb+7 of score row mrow (xb = x0 + 4 d): LDS dwords
+        // d .. d+3 of the centre row (cols xb-4 .. xb+11), d+1 and d+2 of the rows 3 above / below
+        auto prefilter8 = [&](int mrow, int d, bool active) {
+            const int y = y0 - 1 + mrow, xb = x0 + 4 * d;
+            uint32_t cA = 0, cB = 0;   // top bit of byte i: pixel xb+i (cA), xb+4+i (cB)
+            if (active && y >= dy0 && y < dy1 && xb + 7 >= dx0 && xb < dx1) {
+                const uint32_t *row = tin + (mrow + 3) * FB_LD;
+                auto ld = [&](const uint32_t *rw, int i) { return (unsigned)i < (unsigned)FB_LD ? rw[i] : 0u; };
+                const uint32_t C0 = ld(row, d), C1 = ld(row, d + 1), C2 = ld(row, d + 2), C3 = ld(row, d + 3);
+                const uint32_t *rn = row - 3 * FB_LD, *rs = row + 3 * FB_LD;
+                cA = swar4(C1, C0, C2, ld(rn, d + 1), ld(rs, d + 1));
+                cB = swar4(C2, C1, C3, ld(rn, d + 2), ld(rs, d + 2));
+                const int lo = max(dx0 - xb, 0), hi = min(dx1 - xb, 8);   // valid pixels [lo, hi)
+                const unsigned long long vm = hi > lo ? (~0ull << (8 * lo)) & (~0ull >> (64 - 8 * hi)) : 0ull;
+                cA &= (uint32_t)vm;
+                cB &= (uint32_t)(vm >> 32);
+            }
+            // compaction into the pooled list: one LDS atomic per wavefront reserves its slots
+            const int pos0 = mrow * FB_LW + 4 * d + 4;   // score-tile byte of pixel xb
+            unsigned long long bal[8];
+            int tot8 = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            N[k] = tin[(r + 1) * FB_LD + (cb >> 2) + k];
-            C[k] = tin[(r + 4) * FB_LD + (cb >> 2) + k];
-            S[k] = tin[(r + 7) * FB_LD + (cb >> 2) + k];
+            for (int i = 0; i < 8; i++) {
+                bal[i] = __ballot(((i < 4 ? cA : cB) >> (8 * (i & 3) + 7)) & 1u);
+                tot8 += __popcll(bal[i]);
+            }
+            if (tot8 == 0) return;   // wave-uniform
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&ncand_sh, tot8);
+            base = __builtin_amdgcn_readfirstlane(base);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                if (((i < 4 ? cA : cB) >> (8 * (i & 3) + 7)) & 1u) clist[base + lane_rank(bal[i])] = (uint16_t)(pos0 + i);
+                base += __popcll(bal[i]);
+            }
+        };
+        const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;   // pixels (y0 + r, x0 + cb + i)
+#ifndef FB_SKIP_PRE   // instruction-count experiments (make variant VDEFS=-DFB_SKIP_...)
+        if (y0 + 4 * wv + 3 >= dy0 && y0 + 4 * wv < dy1)   // wave-uniform: 4 tile rows per wavefront
+            prefilter8(r + 1, cb >> 2, true);
+        if (wv == 2) {   // ring rows: lanes 0..16 row y0-1, lanes 17..33 row y0+16
+            const int hr = lane >= 17, j = lane - 17 * hr;
+            if ((y0 - 1 >= dy0 && y0 - 1 < dy1) || (y0 + FB_TH >= dy0 && y0 + FB_TH < dy1))
+                prefilter8(hr ? FB_TH + 1 : 0, 2 * j - 1, lane < 34);
         }
-        // Pixel passes the darker bound iff some adjacent compass pair (i, j) has both
-        // e = c - ring - (tlo + 1) >= 0, i.e. the sign bit of (e_i | e_j) is clear; ANDed over
-        // the 4 pairs, (e0|e4)&(e4|e8)&(e8|e12)&(e12|e0) == (e0 & e8) | (e4 & e12): one v_and
-        // + one v_and_or per direction for two pixels (brighter: f = ring - c - (tlo + 1)).
-        const s16x2 th1 = {(short)(tlo + 1), (short)(tlo + 1)};
-        uint32_t cand = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const s16x2 c = byte_pair(C, 4 + 2 * q);
-            const s16x2 cm = c - th1, cp = c + th1;
-            const s16x2 r0 = byte_pair(S, 4 + 2 * q);    // ring 0  (0, +3)
-            const s16x2 r4 = byte_pair(C, 7 + 2 * q);    // ring 4  (+3, 0)
-            const s16x2 r8 = byte_pair(N, 4 + 2 * q);    // ring 8  (0, -3)
-            const s16x2 r12 = byte_pair(C, 1 + 2 * q);   // ring 12 (-3, 0)
-            const uint32_t e0 = __builtin_bit_cast(uint32_t, cm - r0), e4 = __builtin_bit_cast(uint32_t, cm - r4);
-            const uint32_t e8 = __builtin_bit_cast(uint32_t, cm - r8), e12 = __builtin_bit_cast(uint32_t, cm - r12);
-            const uint32_t f0 = __builtin_bit_cast(uint32_t, r0 - cp), f4 = __builtin_bit_cast(uint32_t, r4 - cp);
-            const uint32_t f8 = __builtin_bit_cast(uint32_t, r8 - cp), f12 = __builtin_bit_cast(uint32_t, r12 - cp);
-            const uint32_t u = ((e0 & e8) | (e4 & e12)) & ((f0 & f8) | (f4 & f12));   // sign clear <=> candidate
-            cand |= (((~u >> 15) & 1u) | ((~u >> 30) & 2u)) << (2 * q);
-        }
-        const int y = y0 + r, xb = x0 + cb;
-        if (y < 19 || y >= h - 19) cand = 0;
-        const int lo = max(19 - xb, 0), hi = min(w - 19 - xb, 8);
-        cand &= hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const bool f = (cand >> i) & 1u;
+        if (wv == 3) {   // ring columns: lane -> (row y0 + (lane & 15), column x0-1 or x0+128)
+            const int y = y0 + (lane & 15), x = lane < 16 ? x0 - 1 : x0 + FB_TW;
+            const bool f = lane < 32 && y >= dy0 && y < dy1 && x >= dx0 && x < dx1;
             const unsigned long long bal = __ballot(f);
-            if (f) clist[wv][ncand + lane_rank(bal)] = (uint16_t)((r << 7) | (cb + i));
-            ncand += __popcll(bal);
+            if (bal) {
+                int base = 0;
+                if (lane == 0) base = atomicAdd(&ncand_sh, __popcll(bal));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (f) clist[base + lane_rank(bal)] = (uint16_t)(((lane & 15) + 1) * FB_LW + (x - x0 + 4));
+            }
         }
+#endif
     }
-    if (lane == 0) ccount[wv] = ncand;
-    FBP(2);
     // 4a. blur row pass: tile rows (2p, 2p+1) x output cols 4cg .. 4cg+3
+#ifndef FB_SKIP_BLUR
     {
         const uint32_t K0123 = 7u | 17u << 8 | 32u << 16 | 46u << 24;
         const uint32_t K4567 = 52u | 46u << 8 | 32u << 16 | 17u << 24;
@@ -392,46 +453,54 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             *(uint4 *)&trowp[p * FB_TW + 4 * cg] = v;
         }
     }
-    FBP(3);
+#endif
     __syncthreads();
-    FBP(4);
-    // 3. exact M for this wavefront's candidates
+    // 3. exact M of the pooled candidates: wavefront wv takes chunks wv, wv + 4, ... of 64; its
+    // hot pixels (tile pixels with M > tlo) go into the slots of chunks it has already consumed
+    // (hot entry n -> slot 64 (wv + 4 (n / 64)) + n % 64)
+#ifdef FB_SKIP_EXACT
+    const int tot = 0;
+#else
+    const int tot = ncand_sh;
+#endif
     {
         const uint8_t *t8 = (const uint8_t *)tin;
         uint8_t *m8 = (uint8_t *)mt;
         const int RX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
         const int RY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-        // the four wavefronts' lists pooled: wavefront wv takes pooled chunks wv, wv + 4, ...
-        // (~1 full 64-lane pass each instead of ~1.4 partly filled passes)
-        const int o1 = ccount[0], o2 = o1 + ccount[1], o3 = o2 + ccount[2], tot = o3 + ccount[3];
+        const int t1 = tlo + 1;
+        int nh = 0;
         for (int base = 64 * wv; base < tot; base += 256) {
             const int q = base + lane;
+            bool hot = false;
+            int pos = 0;
             if (q < tot) {
-                const int e = q < o1 ? clist[0][q] : q < o2 ? clist[1][q - o1] : q < o3 ? clist[2][q - o2] : clist[3][q - o3];
-                const int rr = e >> 7, cx = e & 127;
-                const uint8_t *pc = t8 + (rr + 4) * FB_LW + cx + 4;
+                pos = clist[q];
+                const uint8_t *pc = t8 + pos + 3 * FB_LW;   // LDS tile row = score row + 3
                 const int v = pc[0];
-                int d[16];
+                int rg[16];
 #pragma unroll
-                for (int k = 0; k < 16; k++) d[k] = v - (int)pc[RY[k] * FB_LW + RX[k]];
-                int n3[16], x3[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    n3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-                    x3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-                }
-                int A = -256, Bm = 256;
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    A = max(A, min(min(n3[k], n3[(k + 3) & 15]), n3[(k + 6) & 15]));    // darker 9-arc
-                    Bm = min(Bm, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15])); // brighter 9-arc
-                }
-                m8[rr * FB_TW + cx] = (uint8_t)max(max(A, -Bm), 0);
+                for (int k = 0; k < 16; k++) rg[k] = pc[RY[k] * FB_LW + RX[k]];
+                // polarity of the compass bound (step 2); both only for a few candidates
+                const bool pd = v - max(min(rg[0], rg[8]), min(rg[4], rg[12])) >= t1;
+                const bool pb = min(max(rg[0], rg[8]), max(rg[4], rg[12])) - v >= t1;
+                int Mv = fast_arc_score(rg, pd ? v + 1 : -v, pd ? -1 : 0);
+                if (pd && pb) Mv = max(Mv, fast_arc_score(rg, -v, 0));
+                m8[pos] = (uint8_t)Mv;
+                const int mrow = pos / FB_LW, col = pos - mrow * FB_LW;
+                hot = Mv > tlo && mrow >= 1 && mrow <= FB_TH && col >= 4 && col < FB_TW + 4;
             }
+            const unsigned long long bal = __ballot(hot);
+            if (hot) {
+                const int n = nh + (int)lane_rank(bal);
+                clist[64 * (wv + 4 * (n >> 6)) + (n & 63)] = (uint16_t)pos;
+            }
+            nh += __popcll(bal);
         }
+        if (lane == 0) hcount[wv] = nh;
     }
-    FBP(5);
     // 4b. blur column pass: output rows 2rp, 2rp+1 x cols 4cg .. 4cg+3
+#ifndef FB_SKIP_BLUR
     {
         const int rp = threadIdx.x >> 5, cg = threadIdx.x & 31;
         uint4 P[5];
@@ -467,151 +536,46 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             }
         }
     }
-    __syncthreads();
-    FBP(7);
-    // strength map rows (exact M written by any wavefront of the workgroup)
-    {
-        const int y = y0 + r, x = x0 + cb;
-        if (y < h && x < w) {
-            uint8_t *o = mmap + (long long)b * g.blur_stride + g.blur_off[l] + (long long)y * bp + x;
-            const uint32_t m0 = mt[r * (FB_TW / 4) + (cb >> 2)], m1 = mt[r * (FB_TW / 4) + (cb >> 2) + 1];
-            if (x + 7 < w) {
-                *(uint2 *)o = make_uint2(m0, m1);
-            } else {
-                for (int k = 0; k < w - x; k++) o[k] = (uint8_t)((k < 4 ? m0 : m1) >> (8 * (k & 3)));
-            }
-        }
-    }
-#ifdef FB_PROFILE
-    FBP(6);
-    if (threadIdx.x == 0 && blockIdx.y == 0 && (blockIdx.x % 97) == 0)
-        printf("FBPROF blk=%d l=%d stage=%lld pre=%lld rowblur=%lld bar=%lld exactM=%lld colblur=%lld store=%lld\n", blockIdx.x, l,
-               fbt[1] - fbt[0], fbt[2] - fbt[1], fbt[3] - fbt[2], fbt[4] - fbt[3], fbt[5] - fbt[4], fbt[7] - fbt[5], fbt[6] - fbt[7]);
 #endif
-}
-
-// ------------------------------------------------------------------------------------
-// K2b: per-cell threshold + 3x3 NMS + row-major emission on the strength map
-// (ORBextractor.cc:1084-1153 with cv::FAST's per-ROI semantics): score = M > th ? M - 1 : 0
-// inside the cell's detection region [3, rh-3) x [3, rw-3), 0 outside (neighbours in the
-// adjacent cell never suppress), retry at minThFAST when the cell is empty at iniThFAST.
-// One wavefront per cell, four cells per workgroup. The region is staged with dword loads;
-// the few pixels with M > min(thresholds) are compacted in row-major order (ballot ranks),
-// and only those run the 3x3 test at both thresholds.
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ int thr_score(int m, int th) { return m > th ? m - 1 : 0; }
-
-#define NMS_P 68   // LDS row pitch of the staged region (bytes)
-
-__global__ __launch_bounds__(256) void fast_nms_kernel(ExtractGeom g, const CellDesc *cells, const uint8_t *mmap,
-                                                       int *cell_cnt, uint32_t *cell_keys) {
-    extern __shared__ uint32_t nms_lds[];
-    const int lane = threadIdx.x & 63, wv = wave_id();
-    int bxr, b;
-    xcd_remap2(bxr, b);
-    const int c = bxr * 4 + wv;
-    if (c >= g.ncell_total) return;
-    uint32_t *sm32 = nms_lds + wv * g.nms_wave_words;
-    uint8_t *sm = (uint8_t *)sm32;
-    uint16_t *lst = (uint16_t *)(sm32 + g.nms_sm_words);
-    const CellDesc cd = cells[c];
-    const int l = cd.level, bp = g.bp[l];
-    const int dh = cd.rh - 6, dwid = cd.rw - 6;
-    const int ndet = (dh > 0 && dwid > 0) ? dh * dwid : 0;
-    // region rows r0+2 .. r0+rh-3, cols c0+2 .. c0+rw-3 (detection region + 1); sm(0,0) = (r0+2, c0+2)
-    const uint8_t *base = mmap + (long long)b * g.blur_stride + g.blur_off[l] + (long long)(cd.r0 + 2) * bp + cd.c0 + 2;
-    const int qw = (dwid + 2 + 3) >> 2;   // <= NMS_P / 4 = 17 dwords per row
-    {   // lane -> (row offset, dword) once per cell: no per-element integer division
-        const int rpi = 64 / qw, ro = lane / qw, jq = lane - ro * qw;
-        if (ro < rpi && ndet > 0)
-            for (int rr = ro; rr < dh + 2; rr += rpi)
-                sm32[rr * (NMS_P / 4) + jq] = load_u32_unaligned(base + __mul24(rr, bp) + 4 * jq);   // rr < 256: 24-bit multiply
-    }
-    wave_lds_sync();
-    // zero the one-pixel frame: neighbours outside the detection region score 0
-    for (int i = lane; i < 2 * (dwid + 2) + 2 * dh && ndet > 0; i += 64) {
-        int rr, cc;
-        if (i < dwid + 2) { rr = 0; cc = i; }
-        else if (i < 2 * (dwid + 2)) { rr = dh + 1; cc = i - (dwid + 2); }
-        else { const int k = i - 2 * (dwid + 2); rr = 1 + (k >> 1); cc = (k & 1) ? dwid + 1 : 0; }
-        sm[rr * NMS_P + cc] = 0;
-    }
-    const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
-    const int tlo = min(th_a, th_b);
-    wave_lds_sync();
-    // candidates in row-major order as (i << 8 | j): rows of the region map onto the lanes
-    // (64 / dwid rows per step, lane = row offset * dwid + j keeps row-major order)
-    int nl = 0;
-    if (dwid <= 64 && dh < 256) {
-        const int rpi = 64 / max(dwid, 1), ro = lane / max(dwid, 1), j = lane - ro * max(dwid, 1);
-        for (int i0 = 0; i0 < dh && ndet > 0; i0 += rpi) {
-            const int i = i0 + ro;
-            const bool f = ro < rpi && i < dh && sm[(i + 1) * NMS_P + j + 1] > tlo;
-            const unsigned long long bal = __ballot(f);
-            if (f) lst[nl + lane_rank(bal)] = (uint16_t)((i << 8) | j);
-            nl += __popcll(bal);
-        }
-    } else {
-        for (int b0 = 0; b0 < ndet; b0 += 64) {
-            const int idx = b0 + lane;
-            bool f = false;
-            int i = 0, j = 0;
-            if (idx < ndet) {
-                i = idx / dwid; j = idx - i * dwid;
-                f = sm[(i + 1) * NMS_P + j + 1] > tlo;
-            }
-            const unsigned long long bal = __ballot(f);
-            if (f) lst[nl + lane_rank(bal)] = (uint16_t)((i << 8) | j);   // dwid <= 64 above ->
-            nl += __popcll(bal);                                          // here j < NMS_P, i < 256
-        }
-    }
-    wave_lds_sync();
-    auto keep_at = [&](int e, int th, int *score) {
-        const int i = e >> 8, j = e & 0xFF;
-        const uint8_t *s = sm + (i + 1) * NMS_P + j + 1;
-        const int v = thr_score(s[0], th);
-        *score = v;
-        return v > thr_score(s[1], th) && v > thr_score(s[-1], th) && v > thr_score(s[-NMS_P - 1], th) &&
-               v > thr_score(s[-NMS_P], th) && v > thr_score(s[-NMS_P + 1], th) && v > thr_score(s[NMS_P - 1], th) &&
-               v > thr_score(s[NMS_P], th) && v > thr_score(s[NMS_P + 1], th);
-    };
-    // pass 1 at iniThFAST keeps its ballots; pass 2 reuses them unless the cell retries at
-    // minThFAST (:1128-1135)
-    uint32_t *kmask = sm32 + g.nms_mask_off;
-    int total = 0;
-    for (int b0 = 0; b0 < nl; b0 += 64) {
-        int v;
-        const bool k = b0 + lane < nl && keep_at(lst[b0 + lane], th_a, &v);
-        const unsigned long long m = __ballot(k);
-        if (lane == 0) { kmask[b0 >> 5] = (uint32_t)m; kmask[(b0 >> 5) + 1] = (uint32_t)(m >> 32); }
-        total += __popcll(m);
-    }
-    wave_lds_sync();
-    const bool retry = total == 0;
-    const int th = retry ? th_b : th_a;
-    uint32_t *out = cell_keys + ((long long)b * g.ncell_total + c) * g.cell_cap;
-    int written = 0;
-    for (int b0 = 0; b0 < nl; b0 += 64) {
-        int v = 0, idx = 0;
-        bool k = false;
-        if (b0 + lane < nl) {
-            idx = lst[b0 + lane];
-            if (retry) {
-                k = keep_at(idx, th, &v);
-            } else {
-                k = (kmask[(b0 >> 5) + (lane >> 5)] >> (lane & 31)) & 1u;
-                v = thr_score(sm[((idx >> 8) + 1) * NMS_P + (idx & 0xFF) + 1], th);
+    __syncthreads();
+    // 5. 3x3 NMS of the hot pixels at tlo against their in-cell neighbours (others score 0),
+    // survivors appended to their cell's slot list
+    {
+        const int h1 = hcount[0], h2 = h1 + hcount[1], h3 = h2 + hcount[2], htot = h3 + hcount[3];
+        const uint8_t *m8 = (const uint8_t *)mt;
+        const int hC = g.hcell[l], wC = g.wcell[l];
+        const int ry_end = g.maxBY[l] - 3, rx_end = g.maxBX[l] - 3;
+        for (int base = 64 * wv; base < htot; base += 256) {
+            const int q = base + lane;
+            if (q >= htot) continue;
+            const int ow = (int)(q >= h1) + (int)(q >= h2) + (int)(q >= h3);
+            int hb = q >= h1 ? h1 : 0;
+            hb = q >= h2 ? h2 : hb;
+            hb = q >= h3 ? h3 : hb;
+            const int n = q - hb;
+            const int pos = clist[64 * (ow + 4 * (n >> 6)) + (n & 63)];
+            const int mrow = pos / FB_LW, col = pos - mrow * FB_LW;
+            const int y = y0 - 1 + mrow, x = x0 - 4 + col;
+            // cell of (x, y): (v - 19) / cell side by a 20-bit reciprocal (exact for v < 2^20 / side)
+            const int ci = (int)(((unsigned)(y - 19) * (unsigned)g.hcell_mag[l]) >> 20);
+            const int cj = (int)(((unsigned)(x - 19) * (unsigned)g.wcell_mag[l]) >> 20);
+            const int ry0 = 19 + ci * hC, ry1 = min(ry0 + hC, ry_end);
+            const int rx0 = 19 + cj * wC, rx1 = min(rx0 + wC, rx_end);
+            if (ci >= g.ncell_rows[l] || cj >= g.ncell_cols[l] || y >= ry1 || x >= rx1) continue;
+            const bool up = y > ry0, dn = y + 1 < ry1, lf = x > rx0, rt = x + 1 < rx1;
+            const uint8_t *pm = m8 + pos;
+            const int sp = (int)pm[0] - 1;
+            auto sc = [&](int off, bool in) { const int m = pm[off]; return in && m > tlo ? m - 1 : 0; };
+            const int sn = max(max(max(sc(-1, lf), sc(1, rt)), max(sc(-FB_LW - 1, up && lf), sc(-FB_LW, up))),
+                               max(max(sc(-FB_LW + 1, up && rt), sc(FB_LW - 1, dn && lf)), max(sc(FB_LW, dn), sc(FB_LW + 1, dn && rt))));
+            const bool keep = sp > sn;
+            if (keep) {
+                const long long cidx = (long long)b * g.ncell_total + g.cell_base[l] + ci * g.ncell_cols[l] + cj;
+                const int slot = atomicAdd(cell_cnt + cidx, 1);
+                if (slot < g.cell_cap) cell_keys[cidx * g.cell_cap + slot] = pack_key(x - 16, y - 16, sp);
             }
         }
-        const unsigned long long m = __ballot(k);
-        const int rank = (int)lane_rank(m);
-        if (k && written + rank < g.cell_cap) {
-            const int i = idx >> 8, j = idx & 0xFF;
-            out[written + rank] = pack_key(j + 3 + cd.offx, i + 3 + cd.offy, v);
-        }
-        written += __popcll(m);
     }
-    if (lane == 0) cell_cnt[(long long)b * g.ncell_total + c] = min(written, g.cell_cap);
 }
 
 // ------------------------------------------------------------------------------------
@@ -933,13 +897,30 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         Q.nxt = (QNode *)p; p += sizeof(QNode) * NC;
         if (g.qt_nodes_in_lds) lds = p;
     }
-    // ---- 1. gather candidates in cell (row-major) order -> M
+    // ---- 1. gather the cells' keypoints in cell order -> M. A cell's slots hold its FAST
+    //         survivors at min(iniThFAST, minThFAST) with score M - 1; FAST at iniThFAST keeps
+    //         those with score >= iniThFAST, and the cell retries at minThFAST when none does
+    //         (:1119-1135). The order inside a cell is restated in step 5.
     const int *cnt = cell_cnt + (long long)b * g.ncell_total + cb0;
+    const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
+    auto cell_take = [&](int c, int *th) {   // keypoints of cell c, threshold in *th
+        const uint32_t *src = cell_keys + ((long long)b * g.ncell_total + cb0 + c) * g.cell_cap;
+        const int v = min(cnt[c], g.cell_cap);
+        int na = 0, nb = 0;
+        for (int i = 0; i < v; i++) {
+            const int sc = key_score(src[i]);
+            na += sc >= th_a;
+            nb += sc >= th_b;
+        }
+        *th = na > 0 ? th_a : th_b;
+        return na > 0 ? na : nb;
+    };
     int M = 0;
     for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS) {
         const int c = c0 + tid;
+        int th;
         unsigned long long tot;
-        block_scan64(S, c < ncell ? (unsigned)cnt[c] : 0u, &tot, par);
+        block_scan64(S, c < ncell ? (unsigned)cell_take(c, &th) : 0u, &tot, par);
         M += (int)tot;
     }
     Q.M = M;
@@ -960,19 +941,18 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         int base = 0;
         for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS) {
             const int c = c0 + tid;
-            const int v = c < ncell ? cnt[c] : 0;
+            int th = 0;
+            const int v = c < ncell ? cell_take(c, &th) : 0;
             unsigned long long tot;
             const int pre = (int)block_scan64(S, (unsigned)v, &tot, par);
-            if (c < ncell) {   // 4 loads in flight per step
+            if (v > 0) {
                 const uint32_t *src = cell_keys + ((long long)b * g.ncell_total + cb0 + c) * g.cell_cap;
+                const int nv = min(cnt[c], g.cell_cap);
                 uint32_t *dk = Q.K[0] + base + pre;
-                for (int i = 0; i < v; i += 4) {
-                    uint32_t t4[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) t4[u] = i + u < v ? src[i + u] : 0u;
-#pragma unroll
-                    for (int u = 0; u < 4; u++)
-                        if (i + u < v) dk[i + u] = t4[u];
+                int o = 0;
+                for (int i = 0; i < nv; i++) {
+                    const uint32_t k = src[i];
+                    if (key_score(k) >= th) dk[o++] = k;
                 }
             }
             base += (int)tot;
@@ -1115,23 +1095,35 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         }
     }
     QT_MARK(4);
-    // ---- 5. every remaining multi-key node -> its first key of maximal response (:1028)
+    // ---- 5. every remaining multi-key node -> its first key of maximal response (:1028) in
+    //         the reference list order: cells row-major (:1084-1093), then cv::FAST's row-major
+    //         order inside the cell; rank = (cell, row, column in the cell), from the key
     {
         const int na = S.n_act;
         const int R = (M + ORBX_QT_THREADS - 1) / ORBX_QT_THREADS;
         const int i0 = tid * R, i1 = min(i0 + R, M);
-        unsigned *best = (unsigned *)Q.sortbuf;
-        for (int i = tid; i < na; i += ORBX_QT_THREADS) best[i] = 0u;
+        unsigned long long *best = Q.sortbuf;
+        const int hC = g.hcell[l], wC = g.wcell[l];
+        for (int i = tid; i < na; i += ORBX_QT_THREADS) best[i] = 0ull;
         __syncthreads();
         for (int i = i0; i < i1; i++) {
             const int nd = Q.nodes_of(Q.src)[i];
-            if (nd >= 0) atomicMax(&best[nd], ((unsigned)key_score(Q.keys(Q.src)[i]) << 24) | (0xFFFFFFu - (unsigned)i));
+            if (nd >= 0) {
+                const uint32_t key = Q.keys(Q.src)[i];
+                const int ry = key_y(key) - 3, rx = key_x(key) - 3;   // from the first detection row / column
+                const int ci = (int)(((unsigned)ry * (unsigned)g.hcell_mag[l]) >> 20);
+                const int cj = (int)(((unsigned)rx * (unsigned)g.wcell_mag[l]) >> 20);
+                const uint32_t rank = ((uint32_t)(ci * g.ncell_cols[l] + cj) << 12) | ((uint32_t)(ry - ci * hC) << 6) |
+                                      (uint32_t)(rx - cj * wC);
+                atomicMax(&best[nd], ((unsigned long long)key_score(key) << 56) |
+                                         ((unsigned long long)(0xFFFFFFFFu - rank) << 24) | (unsigned)i);
+            }
         }
         __syncthreads();
         for (int t = tid; t < na; t += ORBX_QT_THREADS) {
             const int o = S.n_out + t;
             if (o < NP) {
-                const uint32_t key = Q.keys(Q.src)[0xFFFFFF - (best[t] & 0xFFFFFF)];
+                const uint32_t key = Q.keys(Q.src)[best[t] & 0xFFFFFF];
                 Q.outrec[o] = ((unsigned long long)(uint32_t)(Q.cur[t].id + 0x40000000) << 32) | key;
             }
         }
@@ -1429,7 +1421,6 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
     // A new size is built into locals and committed only after every check and upload has
     // passed, so a rejected size leaves the engine's current geometry intact.
     ExtractGeom gnew{};
-    std::vector<CellDesc> cells;
     int rz_rows[ORBX_MAXL] = {};
     ExtractGeom &g = same ? e->g : gnew;
     if (!same) {
@@ -1450,8 +1441,9 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         }
         g.pyr_stride = std::max(pyr, 64LL);
         g.blur_stride = blur;
-        // FAST cell grid (:1046-1153)
-                int cell_cap = 0, maxM_total = 0;
+        // FAST cell grid (:1046-1153): the cells of a level are the rows i < ncell_rows, columns
+        // j < ncell_cols that pass this fork's skip tests, numbered row-major from cell_base
+        int cell_cap = 0, maxM_total = 0, ncells = 0;
         long long qt = 0;
         int node_cap = 0;
         for (int l = 0; l < L; l++) {
@@ -1463,27 +1455,19 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
             if (wCell + 6 > ORBX_TMAX || hCell + 6 > ORBX_TMAX) return ORBX_EINVAL;
             cell_cap = std::max(cell_cap, ((wCell + 1) / 2) * ((hCell + 1) / 2));
-            g.cell_base[l] = (int)cells.size();
-            for (int i = 0; i < nRows; i++) {
-                const float iniY = (float)(minB + i * hCell);
-                float maxY = iniY + hCell + 6;
-                if (iniY >= maxBY - 3) continue;
-                if (maxY > maxBY) maxY = (float)maxBY;
-                for (int j = 0; j < nCols; j++) {
-                    const float iniX = (float)(minB + j * wCell);
-                    float maxX = iniX + wCell + 6;
-                    if (iniX >= maxBX - 6) continue;  // this fork's bound (:1112)
-                    if (maxX > maxBX) maxX = (float)maxBX;
-                    CellDesc cd;
-                    cd.level = (int16_t)l;
-                    cd.r0 = (int16_t)(int)iniY; cd.c0 = (int16_t)(int)iniX;
-                    cd.rh = (int16_t)((int)maxY - (int)iniY); cd.rw = (int16_t)((int)maxX - (int)iniX);
-                    cd.offx = (int16_t)(j * wCell); cd.offy = (int16_t)(i * hCell);
-                    cd.pad = 0;
-                    cells.push_back(cd);
-                }
-            }
-            const int ncl = (int)cells.size() - g.cell_base[l];
+            g.cell_base[l] = ncells;
+            int rows = 0, cols = 0;
+            for (int i = 0; i < nRows; i++)
+                if ((float)(minB + i * hCell) < maxBY - 3) rows = i + 1;   // :1099 skips iniY >= maxBorderY - 3
+            for (int j = 0; j < nCols; j++)
+                if ((float)(minB + j * wCell) < maxBX - 6) cols = j + 1;   // this fork's bound (:1112)
+            g.hcell[l] = hCell; g.wcell[l] = wCell;
+            g.ncell_rows[l] = rows; g.ncell_cols[l] = cols;
+            // ceil(2^20 / side): floor(v * mag / 2^20) == v / side for v * (mag * side - 2^20) < 2^20,
+            // i.e. every coordinate below 4096 with side <= 60
+            g.hcell_mag[l] = ((1 << 20) + hCell - 1) / hCell;
+            g.wcell_mag[l] = ((1 << 20) + wCell - 1) / wCell;
+            ncells += rows * cols;
             // quadtree parameters (:700-705)
             g.N[l] = e->nfeat[l];
             const int nIni = (int)std::round((float)(maxBX - minB) / (maxBY - minB));
@@ -1492,17 +1476,8 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             g.hX[l] = (float)(maxBX - minB) / nIni;
             g.out_cap[l] = std::max(g.N[l] + 3, 4 * nIni);
             node_cap = std::max(node_cap, g.out_cap[l] + 4);
-            (void)ncl;
         }
-        g.cell_base[L] = (int)cells.size();
-        int max_rh = 0, max_det = 0;
-        for (const CellDesc &cd : cells) {
-            max_rh = std::max(max_rh, (int)cd.rh);
-            max_det = std::max(max_det, std::max(cd.rh - 6, 0) * std::max(cd.rw - 6, 0));
-        }
-        g.nms_sm_words = std::max(max_rh - 4, 1) * (NMS_P / 4);
-        g.nms_mask_off = g.nms_sm_words + (max_det + 1) / 2;   // iniThFAST keep masks, 2 words per 64 candidates
-        g.nms_wave_words = (g.nms_mask_off + 2 * ((max_det + 63) / 64) + 3) & ~3;
+        g.cell_base[L] = ncells;
         g.ncell_total = g.cell_base[L];
         g.cell_cap = cell_cap;
         g.out_base[0] = 0;
@@ -1594,20 +1569,16 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         e->last_n = 0;
         e->st_pairs = 0;
         e->pending_in = nullptr;
-        if (e->d_cells.ensure(sizeof(CellDesc) * cells.size())) return ORBX_EDEVICE;
         if (e->d_rz.ensure(sizeof(int2) * rzc.size()) || e->d_rzr.ensure(sizeof(int4) * rzr.size())) return ORBX_EDEVICE;
-        HIPCHK(hipMemcpy(e->d_cells.p, cells.data(), sizeof(CellDesc) * cells.size(), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->d_rz.p, rzc.data(), sizeof(int2) * rzc.size(), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->d_rzr.p, rzr.data(), sizeof(int4) * rzr.size(), hipMemcpyHostToDevice));
         e->g = gnew;
-        e->cells.swap(cells);
         for (int l = 0; l < ORBX_MAXL; l++) e->rz_rows[l] = rz_rows[l];
         e->W = W; e->H = H;
     }
     ExtractGeom &gc = e->g;
     const long long B = max_images;
     if (e->d_pyr.ensure(B * gc.pyr_stride) || e->d_blur.ensure(B * gc.blur_stride) ||
-        e->d_mmap.ensure(B * gc.blur_stride) ||
         e->d_cell_cnt.ensure(sizeof(int) * B * gc.ncell_total) ||
         e->d_cell_keys.ensure(sizeof(uint32_t) * B * gc.ncell_total * gc.cell_cap) ||
         e->d_qt.ensure(sizeof(uint32_t) * B * gc.qt_off[gc.nlevels]) ||
@@ -1645,17 +1616,14 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
             resize_level_kernel<false><<<grid, 256, lds, s>>>(g, l, tiles_x, cx, ry, d_imgs, pyr);
     }
     prof_end(e, s, ph, "resize_level_kernel");
+    HIPCHK(hipMemsetAsync(e->d_cell_cnt.p, 0, sizeof(int) * (size_t)n * g.ncell_total, s));   // cell slot counters
     ph = prof_begin(e, s);
     fast_blur_kernel<<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
-                                                                   e->d_mmap.as<uint8_t>());
+                                                                   e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
     prof_end(e, s, ph, "fast_blur_kernel");
     }
     if (phase & 2) {
     int ph = prof_begin(e, s);
-    fast_nms_kernel<<<dim3((g.ncell_total + 3) / 4, n), 256, 16 * (size_t)g.nms_wave_words, s>>>(g, e->d_cells.as<CellDesc>(), e->d_mmap.as<uint8_t>(),
-                                                        e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
-    prof_end(e, s, ph, "fast_nms_kernel");
-    ph = prof_begin(e, s);
     size_t lds = 12 * (size_t)g.qt_kl;
     if (g.qt_nodes_in_lds) lds += (2 * sizeof(QNode) + sizeof(QTmp)) * g.node_cap + 16 * (size_t)g.node_pow2;
     quadtree_kernel<<<dim3(L, n), ORBX_QT_THREADS, lds, s>>>(
@@ -1747,7 +1715,7 @@ void orbx_destroy(orbx_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->done) (void)hipEventSynchronize(e->done);
     orbamd::frame_state_free(e);
-    orbamd::DevBuf *bufs[] = {&e->d_mmap, &e->d_cells, &e->d_rz, &e->d_rzr, &e->d_pattern, &e->d_in, &e->d_pyr, &e->d_blur,
+    orbamd::DevBuf *bufs[] = {&e->d_rz, &e->d_rzr, &e->d_pattern, &e->d_in, &e->d_pyr, &e->d_blur,
                               &e->d_cell_cnt, &e->d_cell_keys, &e->d_qt, &e->d_qt_nodes, &e->d_sel,
                               &e->d_sel_cnt, &e->d_kps, &e->d_desc, &e->d_cnt, &e->d_st_sorted,
                               &e->d_st_res, &e->d_st_u, &e->d_st_depth, &e->d_st_dist, &e->d_st_rows};
