@@ -296,10 +296,11 @@ __device__ __forceinline__ int fast_arc_score(const int *rg, int c, int xm) {
 
 __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
                                                         uint8_t *blur, int *cell_cnt, uint32_t *cell_keys) {
-    __shared__ uint32_t tin[(FB_TH + 8) * FB_LD];
+    __shared__ __align__(16) uint32_t tin[(FB_TH + 8) * FB_LD];
     __shared__ uint32_t trowp[((FB_TH + 8) / 2) * FB_TW];
     __shared__ uint32_t mt[FB_NG];   // exact M bytes, (mrow, x - x0 + 4)
     __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets)
+    __shared__ uint16_t bboth[4][128];     // per-wavefront queue of dual-polarity candidates
     __shared__ int ncand_sh, hcount[4];
     const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
     int t = blockIdx.x, l = 0;
@@ -310,27 +311,41 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     const int x0 = tx * FB_TW, y0 = ty * FB_TH;
     int pitch;
     const uint8_t *src = level_ptr(g, in, pyr, b, l, &pitch);
-    // 1. stage rows y0-4 .. y0+19, cols x0-4 .. x0+131 (interior tiles: no reflection tests)
-    if (y0 >= 4 && y0 + FB_TH + 4 <= h && x0 >= 4 && x0 + FB_TW + 4 <= w) {
-        const uint8_t *s0 = src + (long long)(y0 - 4) * pitch + (x0 - 4);
-        for (int i = threadIdx.x; i < (FB_TH + 8) * FB_LD; i += 256) {
-            const int rr = i / FB_LD, j = i - rr * FB_LD;
-            tin[i] = load_u32_unaligned(s0 + rr * pitch + 4 * j);
-        }
-    } else
-    for (int i = threadIdx.x; i < (FB_TH + 8) * FB_LD; i += 256) {
-        const int rr = i / FB_LD, j = i - rr * FB_LD;
-        const uint8_t *rowp = src + (long long)refl101(y0 + rr - 4, h) * pitch;
-        const int xs = x0 - 4 + 4 * j;
-        uint32_t v;
-        if (xs >= 0 && xs + 3 < w) {
-            v = load_u32_unaligned(rowp + xs);
-        } else {
-            v = 0;
+    // 1. stage rows y0-4 .. y0+19, cols x0-4 .. x0+131 as dword pairs: three aligned dword loads
+    // + two v_alignbyte per pair (the last load may read up to 4 bytes past a row's end: inputs
+    // carry a 16-byte readable tail, the pyramid allocation a 64-byte one); reflect-101 of rows
+    // (the 4-row halo never reaches past a level of >= 40 rows) and, per byte, of the few pairs
+    // that cross the left / right edge.
+    {
+        const bool inner_x = x0 >= 4 && x0 + FB_TW + 4 <= w;
+        for (int i = threadIdx.x; i < (FB_TH + 8) * (FB_LD / 2); i += 256) {
+            const int rr = i / (FB_LD / 2), jj = i - rr * (FB_LD / 2);
+            int yy = y0 - 4 + rr;
+            yy = yy < 0 ? -yy : yy;
+            yy = yy >= h ? 2 * h - 2 - yy : yy;
+            const uint8_t *rowp = src + (long long)yy * pitch;
+            const int xs = x0 - 4 + 8 * jj;
+            uint2 v;
+            if (inner_x || (xs >= 0 && xs + 7 < w)) {
+                const uintptr_t a = (uintptr_t)(rowp + xs);
+                const uint32_t *pa = (const uint32_t *)(a & ~(uintptr_t)3);
+                const uint32_t sh = (uint32_t)(a & 3);
+                const uint32_t d0 = pa[0], d1 = pa[1], d2 = pa[2];
+                v.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            } else {
+                v.x = v.y = 0;
 #pragma unroll
-            for (int e = 0; e < 4; e++) v |= (uint32_t)rowp[refl101(xs + e, w)] << (8 * e);
+                for (int e = 0; e < 8; e++) {
+                    int xx = xs + e;
+                    xx = xx < 0 ? -xx : xx;
+                    xx = xx >= w ? 2 * w - 2 - xx : xx;
+                    const uint32_t by = rowp[xx];
+                    if (e < 4) v.x |= by << (8 * e); else v.y |= by << (8 * (e - 4));
+                }
+            }
+            *(uint2 *)&tin[rr * FB_LD + 2 * jj] = v;
         }
-        tin[i] = v;
     }
     for (int i = threadIdx.x; i < FB_NG; i += 256) mt[i] = 0u;
     if (threadIdx.x == 0) ncand_sh = 0;
@@ -469,34 +484,69 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         const int RX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
         const int RY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
         const int t1 = tlo + 1;
-        int nh = 0;
-        for (int base = 64 * wv; base < tot; base += 256) {
-            const int q = base + lane;
-            bool hot = false;
-            int pos = 0;
-            if (q < tot) {
-                pos = clist[q];
-                const uint8_t *pc = t8 + pos + 3 * FB_LW;   // LDS tile row = score row + 3
-                const int v = pc[0];
-                int rg[16];
+        uint16_t *bb = bboth[wv];
+        int nh = 0, nb = 0;   // hot entries, queued dual-polarity candidates (wave-uniform)
+        auto ring = [&](int pos, int *rg) {
+            const uint8_t *pc = t8 + pos + 3 * FB_LW;   // LDS tile row = score row + 3
 #pragma unroll
-                for (int k = 0; k < 16; k++) rg[k] = pc[RY[k] * FB_LW + RX[k]];
-                // polarity of the compass bound (step 2); both only for a few candidates
-                const bool pd = v - max(min(rg[0], rg[8]), min(rg[4], rg[12])) >= t1;
-                const bool pb = min(max(rg[0], rg[8]), max(rg[4], rg[12])) - v >= t1;
-                int Mv = fast_arc_score(rg, pd ? v + 1 : -v, pd ? -1 : 0);
-                if (pd && pb) Mv = max(Mv, fast_arc_score(rg, -v, 0));
-                m8[pos] = (uint8_t)Mv;
-                const int mrow = pos / FB_LW, col = pos - mrow * FB_LW;
-                hot = Mv > tlo && mrow >= 1 && mrow <= FB_TH && col >= 4 && col < FB_TW + 4;
-            }
+            for (int k = 0; k < 16; k++) rg[k] = pc[RY[k] * FB_LW + RX[k]];
+            return (int)pc[0];
+        };
+        auto push_hot = [&](bool hot, int pos) {
             const unsigned long long bal = __ballot(hot);
             if (hot) {
                 const int n = nh + (int)lane_rank(bal);
                 clist[64 * (wv + 4 * (n >> 6)) + (n & 63)] = (uint16_t)pos;
             }
             nh += __popcll(bal);
+        };
+        auto in_tile = [&](int pos) {
+            const int mrow = pos / FB_LW, col = pos - mrow * FB_LW;
+            return mrow >= 1 && mrow <= FB_TH && col >= 4 && col < FB_TW + 4;
+        };
+        // the brighter score of queued candidates whose darker score is already in the tile
+        auto drain = [&](int n) {
+            const bool act = lane < n;
+            const int pos = act ? bb[lane] : 0;
+            bool hot = false;
+            if (act) {
+                int rg[16];
+                const int v = ring(pos, rg);
+                const int Mv = max((int)m8[pos], fast_arc_score(rg, -v, 0));
+                m8[pos] = (uint8_t)Mv;
+                hot = Mv > tlo && in_tile(pos);
+            }
+            push_hot(hot, pos);
+        };
+        for (int base = 64 * wv; base < tot; base += 256) {
+            const int q = base + lane;
+            bool hot = false, both = false;
+            int pos = 0;
+            if (q < tot) {
+                pos = clist[q];
+                int rg[16];
+                const int v = ring(pos, rg);
+                // polarity of the compass bound (step 2); candidates of both polarities (up to
+                // ~18 % on the noisier levels) get their brighter score in a queued pass
+                const bool pd = v - max(min(rg[0], rg[8]), min(rg[4], rg[12])) >= t1;
+                const bool pb = min(max(rg[0], rg[8]), max(rg[4], rg[12])) - v >= t1;
+                const int Mv = fast_arc_score(rg, pd ? v + 1 : -v, pd ? -1 : 0);
+                m8[pos] = (uint8_t)Mv;
+                both = pd && pb;
+                hot = !both && Mv > tlo && in_tile(pos);
+            }
+            push_hot(hot, pos);
+            const unsigned long long bbal = __ballot(both);
+            if (both) bb[nb + lane_rank(bbal)] = (uint16_t)pos;
+            nb += __popcll(bbal);
+            if (nb >= 64) {
+                drain(64);
+                nb -= 64;
+                const int rest = lane < nb ? bb[64 + lane] : 0;
+                if (lane < nb) bb[lane] = (uint16_t)rest;
+            }
         }
+        if (nb > 0) drain(nb);
         if (lane == 0) hcount[wv] = nh;
     }
     // 4b. blur column pass: output rows 2rp, 2rp+1 x cols 4cg .. 4cg+3
@@ -1578,7 +1628,8 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
     }
     ExtractGeom &gc = e->g;
     const long long B = max_images;
-    if (e->d_pyr.ensure(B * gc.pyr_stride) || e->d_blur.ensure(B * gc.blur_stride) ||
+    // the pyramid carries a 64-byte readable tail (fast_blur_kernel's staging loads)
+    if (e->d_pyr.ensure(B * gc.pyr_stride + 64) || e->d_blur.ensure(B * gc.blur_stride) ||
         e->d_cell_cnt.ensure(sizeof(int) * B * gc.ncell_total) ||
         e->d_cell_keys.ensure(sizeof(uint32_t) * B * gc.ncell_total * gc.cell_cap) ||
         e->d_qt.ensure(sizeof(uint32_t) * B * gc.qt_off[gc.nlevels]) ||
