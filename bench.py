@@ -36,6 +36,7 @@ W, H = 1241, 376
 NFEAT = 2000
 BYTES_PER_STEREO_FRAME = 2 * W * H + 2 * NFEAT * (28 + 32) + NFEAT * 8   # 1,189,232 B
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+C3_BYTES_PER_FRAME = 640 * 480 + 1000 * 60 + 1000 * (4 + 8)   # 379,200 B per RGB-D frame
 
 
 def log(*a):
@@ -208,6 +209,108 @@ def bench_e2e(amd, args, pool, bf, mb):
                             "PCIe-inclusive rate (value is the HBM-resident rate)"}}
 
 
+def bench_c2(amd, args, dist, world, params, pool):
+    """C2 headline leg: B resident stereo pairs per step through the 3-engine pipeline."""
+    import torch
+    from orbslam2_amd import dist as odist
+    nf, sf, nl, ith, mth, bf, mb = params
+    B = args.batch
+    bufs = []
+    for k in range(args.bufs):
+        imgs = np.empty((2 * B, H, W), np.uint8)
+        for i in range(B):
+            L, R = pool[(i + 3 * k) % len(pool)]
+            if k:  # make rotating buffers differ (avoid identical cached inputs)
+                L = np.roll(L, 7 * k, axis=1)
+                R = np.roll(R, 7 * k, axis=1)
+            imgs[2 * i], imgs[2 * i + 1] = L, R
+        bufs.append(torch.from_numpy(imgs).cuda())
+    torch.cuda.synchronize()
+
+    ex = amd.StereoPipeline(int(nf), float(sf), int(nl), int(ith), int(mth), n_engines=args.engines)
+    ex.reserve(W, H, B)
+    per_launch = B / len(ex.engines)   # stereo pairs one extraction / stereo launch processes
+
+    def step(k):
+        t = bufs[k % len(bufs)]
+        ex.stereo_batch(t.data_ptr(), B, W, H, W, W * H, float(bf), mb)
+
+    for k in range(args.warmup):
+        step(k)
+    amd.device_sync()
+    if not args.no_profile:
+        ex.profile(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    amd.device_sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    amd.device_sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = ex.profile_read() if not args.no_profile else {}
+    ex.profile(False)
+    elapsed = odist.max_over_ranks(elapsed, COLL_DEV, dist)
+
+    # sanity: the batch produced keypoints and stereo matches
+    k0 = ex.fetch(0)[0]
+    u0, _ = ex.stereo_fetch(0)
+    n_match = int((u0[: len(k0)] >= 0).sum())
+    if len(k0) < 100 or n_match < 10:
+        raise RuntimeError(f"implausible output: {len(k0)} keypoints, {n_match} stereo matches")
+
+    frames = B * args.steps * world
+    value = frames / elapsed
+    out = {
+        "metric": "frames/sec ORB extract+match @1241x376 (1 GPU) + LocalBA keyframes/sec",
+        "value": round(value, 2),
+        "unit": "stereo frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": "C2: KITTI-like synthetic stereo 1241x376, ORBextractor(2000,1.2,8,20,7) L+R "
+                        "+ Frame::ComputeStereoMatches",
+            "stereo_frames_per_step_per_gpu": B,
+            "pipeline_engines": len(ex.engines),
+            "image": f"{W}x{H}",
+            "nfeatures": NFEAT,
+            "parallelism": f"independent sequence per GPU x{world}",
+            "keypoints_img0": int(len(k0)),
+            "stereo_matches_img0": n_match,
+        },
+    }
+    if prof:
+        name, (tot, n) = max(prof.items(), key=lambda kv: kv[1][0])
+        avg_s = tot / n / 1000.0
+        achieved = BYTES_PER_STEREO_FRAME * per_launch / avg_s / 1e9
+        traffic = load_pmc(name, round(per_launch))
+        out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 3),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                           "traffic": traffic, "avg_launch_ms": round(tot / n, 4),
+                           "algorithmic_bytes_per_launch": round(BYTES_PER_STEREO_FRAME * per_launch),
+                           "pairs_per_launch": per_launch}
+        valu = load_pmc(name, round(per_launch), "valu_insts_per_launch")
+        if valu:   # the ceiling this integer kernel actually sits against (DESIGN.md §5)
+            out["roofline"]["valu_issue_frac"] = round(
+                valu * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (tot / n / 1e3), 4)
+            out["roofline"]["valu_insts_per_launch"] = valu
+        # summed over the engines' launches, which overlap in time (so the sum exceeds ms_per_step)
+        out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
+    del bufs   # the resident batches are not needed by the legs below
+    return out
+
+
 FP64_MFMA_PEAK_TFS = 75.08   # measured, tools/microbench/mfma_f64_peak.hip (profiles/r02_mfma_f64_peak.json)
 
 
@@ -338,10 +441,18 @@ def bench_rgbd(amd, args, dist, world):
     amd.device_sync()
     dt = odist.max_over_ranks(time.perf_counter() - t0, COLL_DEV, dist)
     n, m, _ = ex.search_init_fetch(0)
-    return {"c3_rgbd_frames_per_s": round(world * T * args.rgbd_steps / dt, 2),
+    fps = world * T * args.rgbd_steps / dt
+    # SURVEY §8d algorithmic bytes per RGB-D frame: gray in + keypoints / descriptors out +
+    # depth gather and (uR, depth) out; HBM GB/s of that compulsory I/O against the 8 TB/s peak
+    bpf = C3_BYTES_PER_FRAME
+    return {"c3_rgbd_frames_per_s": round(fps, 2),
             "c3": {"frames_per_step": T, "ms_per_step": round(1000 * dt / args.rgbd_steps, 3),
-                   "search_init_matches_pair0": int(n),
-                   "bytes_per_frame": 640 * 480 + 1000 * 60 + 1000 * 12}}
+                   "search_init_matches_pair0": int(n), "bytes_per_frame": bpf,
+                   "hbm_gbs": round(fps / world * bpf / 1e9, 3),
+                   "hbm_frac": round(fps / world * bpf / 1e9 / HBM_PEAK_GBS, 6),
+                   "note": "GB/s per GPU of SURVEY §8d's compulsory bytes (640x480 u8 in, 1000 x 60 B keypoints + "
+                           "descriptors out, 1000 x 12 B depth gather + uR / depth out); the rocprofv3 summary of "
+                           "this leg alone is profiles/r02_kernel_stats_c3.csv (bench.py --no-c2)"}}
 
 
 def bench_track(amd, args, dist, world, with_cpu):
@@ -653,6 +764,7 @@ def main():
     ap.add_argument("--cpu-latency-frames", type=int, default=512)
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-c2", action="store_true", help="skip the headline leg (profiling the other legs)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -681,100 +793,12 @@ def main():
     mb = float(np.float32(bf) / np.float32(fx))
 
     pool = make_pool(args.pool, 2 + 100 * rank)
-    bufs = []
-    for k in range(args.bufs):
-        imgs = np.empty((2 * B, H, W), np.uint8)
-        for i in range(B):
-            L, R = pool[(i + 3 * k) % len(pool)]
-            if k:  # make rotating buffers differ (avoid identical cached inputs)
-                L = np.roll(L, 7 * k, axis=1)
-                R = np.roll(R, 7 * k, axis=1)
-            imgs[2 * i], imgs[2 * i + 1] = L, R
-        bufs.append(torch.from_numpy(imgs).cuda())
-    torch.cuda.synchronize()
-
-    ex = amd.StereoPipeline(int(nf), float(sf), int(nl), int(ith), int(mth), n_engines=args.engines)
-    ex.reserve(W, H, B)
-    per_launch = B / len(ex.engines)   # stereo pairs one extraction / stereo launch processes
-
-    def step(k):
-        t = bufs[k % len(bufs)]
-        ex.stereo_batch(t.data_ptr(), B, W, H, W, W * H, float(bf), mb)
-
-    for k in range(args.warmup):
-        step(k)
-    amd.device_sync()
-    if not args.no_profile:
-        ex.profile(True)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    amd.device_sync()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    amd.device_sync()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    prof = ex.profile_read() if not args.no_profile else {}
-    ex.profile(False)
-    elapsed = odist.max_over_ranks(elapsed, COLL_DEV, dist)
-
-    # sanity: the batch produced keypoints and stereo matches
-    k0 = ex.fetch(0)[0]
-    u0, _ = ex.stereo_fetch(0)
-    n_match = int((u0[: len(k0)] >= 0).sum())
-    if len(k0) < 100 or n_match < 10:
-        raise RuntimeError(f"implausible output: {len(k0)} keypoints, {n_match} stereo matches")
-
-    frames = B * args.steps * world
-    value = frames / elapsed
-    out = {
-        "metric": "frames/sec ORB extract+match @1241x376 (1 GPU) + LocalBA keyframes/sec",
-        "value": round(value, 2),
-        "unit": "stereo frames/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1000 * elapsed / args.steps, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic",
-        "config": {
-            "workload": "C2: KITTI-like synthetic stereo 1241x376, ORBextractor(2000,1.2,8,20,7) L+R "
-                        "+ Frame::ComputeStereoMatches",
-            "stereo_frames_per_step_per_gpu": B,
-            "pipeline_engines": len(ex.engines),
-            "image": f"{W}x{H}",
-            "nfeatures": NFEAT,
-            "parallelism": f"independent sequence per GPU x{world}",
-            "keypoints_img0": int(len(k0)),
-            "stereo_matches_img0": n_match,
-        },
-    }
-    if prof:
-        name, (tot, n) = max(prof.items(), key=lambda kv: kv[1][0])
-        avg_s = tot / n / 1000.0
-        achieved = BYTES_PER_STEREO_FRAME * per_launch / avg_s / 1e9
-        traffic = load_pmc(name, round(per_launch))
-        out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 3),
-                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                           "traffic": traffic, "avg_launch_ms": round(tot / n, 4),
-                           "algorithmic_bytes_per_launch": round(BYTES_PER_STEREO_FRAME * per_launch),
-                           "pairs_per_launch": per_launch}
-        valu = load_pmc(name, round(per_launch), "valu_insts_per_launch")
-        if valu:   # the ceiling this integer kernel actually sits against
-            out["roofline"]["valu_issue_frac"] = round(
-                valu * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (tot / n / 1e3), 4)
-            out["roofline"]["valu_insts_per_launch"] = valu
-        # summed over the engines' launches, which overlap in time (so the sum exceeds ms_per_step)
-        out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
-    del bufs   # the resident batches are not needed by the legs below
-    if not args.no_e2e:
+    if args.no_c2:   # profiling of the other legs only (e.g. the C3 rocprofv3 summary): no headline value
+        out = {"metric": "frames/sec ORB extract+match @1241x376 (1 GPU) + LocalBA keyframes/sec", "value": None,
+               "unit": "stereo frames/s", "n_gpus": world, "note": "--no-c2: headline leg skipped"}
+    else:
+        out = bench_c2(amd, args, dist, world, (nf, sf, nl, ith, mth, bf, mb), pool)
+    if not args.no_e2e and not args.no_c2:
         out.update(bench_e2e(amd, args, pool, bf, mb))
     if not args.no_latency and rank == 0:
         out.update(bench_latency(amd, args, pool, world == 1 and not args.no_cpu_baseline))
