@@ -77,6 +77,7 @@ __device__ __forceinline__ const uint8_t *level_ptr(const ExtractGeom &g, const 
 // ------------------------------------------------------------------------------------
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // dword of image bytes [x, x+4) of row `rowp` (x .. x+3 inside the row) from aligned loads
 __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
@@ -1281,15 +1282,18 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
         const uint8_t *img = level_ptr(g, in, pyr, b, l, &pitch);
         // IC_Angle over the circular patch (|u| <= umax[|v|]): rows v = -15..15 as 8 dwords
         // (u = -16..15), sum_u u*p = sum (u+16)*p - 16 * sum p with v_dot4_u32_u8 (exact)
-        const uint8_t *rowc = img + (long long)y * pitch + x - 16;
+        // lane -> dword w = lane % 8 of rows v0, v0 + 8, v0 + 16, v0 + 24 (v0 = lane / 8 - 15);
+        // unaligned dword loads (the rows start anywhere)
+        const int w = lane & 7, v0 = (lane >> 3) - 15;
+        const uint8_t *rowc = img + (long long)(y + v0) * pitch + x - 16 + 4 * w;
         int m01 = 0, m10 = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int j = lane + 64 * k;
-            if (j < 31 * 8) {
-                const int v = (j >> 3) - 15, w = j & 7;
+            const int v = v0 + 8 * k;
+            if (k < 3 || v <= 15) {
                 const uint2 wt = c_icw[(v < 0 ? -v : v) * 8 + w];
-                const uint32_t P = load_u32_unaligned(rowc + __mul24(v, pitch) + 4 * w);   // |v| <= 15: 24-bit multiply
+                uint32_t P;
+                __builtin_memcpy(&P, rowc + (long long)(8 * k) * pitch, 4);
                 const int su = (int)__builtin_amdgcn_udot4(P, wt.x, 0u, false);
                 const int sm = (int)__builtin_amdgcn_udot4(P, wt.y, 0u, false);
                 m10 += su - 16 * sm;
@@ -1308,15 +1312,13 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
         const long long a0 = c0 - sh;
         uint32_t *pt = patch[wv][r];
         if (a0 >= 0 && a0 + 36LL * bw + 40 <= amax + 4) {   // wave-uniform: no clamping needed
-            const uint32_t *src = (const uint32_t *)(blur + a0);
-            const int bw4 = bw >> 2;
+            // lanes 0..59 -> (row lane / 10, dword lane % 10), six rows per pass
+            const int bw4 = bw >> 2, rr0 = (lane * 205) >> 11, q = lane - 10 * rr0;
+            const uint32_t *src = (const uint32_t *)(blur + a0) + (long long)rr0 * bw4 + q;
+            if (lane < 60) {
 #pragma unroll
-            for (int k = 0; k < 6; k++) {
-                const int idx = lane + 64 * k;
-                if (idx < 370) {
-                    const int rr = idx / 10, q = idx - rr * 10;
-                    pt[idx] = src[__mul24(rr, bw4) + q];
-                }
+                for (int k = 0; k < 7; k++)
+                    if (k < 6 || rr0 == 0) pt[10 * (rr0 + 6 * k) + q] = src[(long long)(6 * k) * bw4];
             }
         } else {
 #pragma unroll
@@ -1341,15 +1343,14 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
         const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
         glibc_sincosf(ang * factorPI, &sa, &ca);
     }
-    // pattern coordinates of the lane's 4 test pairs as floats (int8 -> f32, exact)
-    float PX0[4], PY0[4], PX1[4], PY1[4];
+    // pattern coordinates of the lane's 4 test pairs as floats (int8 -> f32, exact), the two
+    // points of a pair packed for v_pk_mul_f32 / v_pk_add_f32
+    f32x2 PX[4], PY[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) {
         const uint32_t pw = ((const uint32_t *)c_pattern)[w * 64 + lane];   // x0 y0 x1 y1 as int8
-        PX0[w] = (float)(int8_t)(pw & 0xFF);
-        PY0[w] = (float)(int8_t)((pw >> 8) & 0xFF);
-        PX1[w] = (float)(int8_t)((pw >> 16) & 0xFF);
-        PY1[w] = (float)(int8_t)(pw >> 24);
+        PX[w] = f32x2{(float)(int8_t)(pw & 0xFF), (float)(int8_t)((pw >> 16) & 0xFF)};
+        PY[w] = f32x2{(float)(int8_t)((pw >> 8) & 0xFF), (float)(int8_t)(pw >> 24)};
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1362,14 +1363,23 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
         const float angle = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), r));
         const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), r));
         const float bs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), r));
-        const uint8_t *pc = (const uint8_t *)patch[wv][r] + 18 * 40 + 18 + PSH[r];   // (dy, dx) -> pc[dy * 40 + dx]
+        // GET_VALUE(idx) = center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)] (:158-160), the
+        // products and sums rounded one by one as on x86 (no contraction). cvRound (round half
+        // to even) as v + 1.5*2^23: for |v| < 2^22 the float sum holds round(v) in its low
+        // mantissa bits, bits = 0x4B400000 + round(v); the rotated offsets are within +-18, so
+        // the byte index (dy + 18) * 40 + dx + 18 + PSH = bits_y * 40 + bits_x - C (24-bit
+        // multiply of bits_y's low 24 bits 0x400000 + dy, unsigned wrap-around).
+        const uint8_t *pc = (const uint8_t *)patch[wv][r];
+        const uint32_t ib = (uint32_t)(18 * 40 + 18 + PSH[r]) - (0x400000u * 40u + 0x4B400000u);
+        const f32x2 av = {a, a}, bv = {bs, bs}, MAG = {12582912.0f, 12582912.0f};
         unsigned long long words[4];
 #pragma unroll
         for (int w = 0; w < 4; w++) {
-            // rotated offsets are within +-18: full-rate 24-bit multiplies for the row stride
-            const int t0 = pc[__mul24(cv_round_f(PX0[w] * bs + PY0[w] * a), 40) + cv_round_f(PX0[w] * a - PY0[w] * bs)];
-            const int t1 = pc[__mul24(cv_round_f(PX1[w] * bs + PY1[w] * a), 40) + cv_round_f(PX1[w] * a - PY1[w] * bs)];
-            words[w] = __ballot(t0 < t1);
+            const f32x2 qy = (PX[w] * bv + PY[w] * av) + MAG;
+            const f32x2 qx = (PX[w] * av - PY[w] * bv) + MAG;
+            const uint32_t i0 = __umul24(__float_as_uint(qy.x), 40u) + __float_as_uint(qx.x) + ib;
+            const uint32_t i1 = __umul24(__float_as_uint(qy.y), 40u) + __float_as_uint(qx.y) + ib;
+            words[w] = __ballot(pc[i0] < pc[i1]);
         }
         if (lane == 0) {
             const int l = d[r].l;

@@ -15,10 +15,12 @@ python3 - <<'PY'
 import csv, glob, collections, os
 for d in sorted(glob.glob('gpurun_out/pmcv_*')):
     if not os.path.isdir(d): continue
-    acc = collections.defaultdict(list)
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(d + '/**/*counter_collection.csv', recursive=True):
         for r in csv.DictReader(open(f)):
-            if 'fast_blur' in r['Kernel_Name']:
-                acc[r['Counter_Name']].append(float(r['Counter_Value']))
-    print(d, {k: round(sum(v) / len(v)) for k, v in acc.items()})
+            k = r['Kernel_Name'].split('(')[0].replace('void ', '').split('::')[-1]
+            if not k.startswith('__amd'):
+                acc[k][r['Counter_Name']].append(float(r['Counter_Value']))
+    for k, c in sorted(acc.items()):
+        print(d, k, {n: round(sum(v) / len(v)) for n, v in c.items()})
 PY
