@@ -253,8 +253,10 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 // ------------------------------------------------------------------------------------
 #define FB_TW 128
 #define FB_TH 16
-#define FB_LW (FB_TW + 8)   // LDS tile row bytes (cols x0-4 .. x0+131)
-#define FB_LD (FB_LW / 4)   // LDS tile row dwords
+#define FB_SB (FB_TW + 8)   // staged bytes per tile row (cols x0-4 .. x0+131)
+#define FB_SD (FB_SB / 4)   // staged dwords per tile row
+#define FB_LW (FB_TW + 8)   // LDS tile row stride in bytes (8-aligned rows for the blur's ds_read_b64)
+#define FB_LD (FB_LW / 4)   // LDS tile row stride in dwords
 #define FB_MR (FB_TH + 2)   // score rows y0-1 .. y0+16 (tile + NMS ring)
 #define FB_NG (FB_MR * FB_LD)   // score tile dwords
 #define FB_CCAP (FB_MR * (FB_TW + 2) + 64)   // candidate slots: every score pixel + one chunk of hot-list slack
@@ -295,10 +297,104 @@ __device__ __forceinline__ int fast_arc_score(const int *rg, int c, int xm) {
     return A;
 }
 
+// GaussianBlur 9x9 sigma 2 of one 128 x 16 tile as two banded integer products on
+// v_mfma_i32_16x16x32_i8 (lane maps: tools/microbench/mfma_i8_layout.hip). OpenCV's bit-exact
+// fixed-point path: exact row sums R = sum_k w_k p, then (sum_i w_i R + 2^15) >> 16
+// with w = [7,17,32,46,52,46,32,17,7] (sum 256).
+//  row pass, per 16-column block and 16-row block: R (rows x cols) = T (rows x staged cols) . W,
+//    A = staged pixels - 128 (byte XOR 0x80: the i8 MFMA is signed; 8 bytes per lane = the 32
+//    staged columns a 16-column block reads), B = band W[c][x] = w[c - x]; the accumulator is
+//    R - 2^15, whose low 16 bits are R ^ 0x8000: byte 1 is hi(R) - 128 and byte 0 is lo(R),
+//    R = 256 hi + lo;
+//  column pass: O^T (cols x out rows) = R^T . V on the hi and lo bytes (two MFMAs), the row-pass
+//    accumulators used in place as A (lane l holds rows 4 (l >> 4) + r and 16 + 4 (l >> 4) + r of
+//    column l & 15: the K order is permuted and V's rows follow it), B = band
+//    V[rho(k)][y] = w[rho(k) - y]; the hi product starts from 128 * 257 + 128 (the byte offsets,
+//    times 256, and the rounding 2^15 / 256), so out = (256 accH + accL) >> 16 is byte 2 of
+//    256 accH + accL.
+// 8 MFMAs and ~80 VALU instructions per wavefront replace ~160 VALU instructions of v_dot4 /
+// v_dot2 row and column passes.
+struct FbBlurTab {
+    unsigned long long wb[64];   // row-pass B fragment of lane l: W[k = 8 (l >> 4) + j][x = l & 15]
+    unsigned long long vb[64];   // column-pass B fragment: V[rho(k)][y = l & 15]
+};
+constexpr FbBlurTab make_fb_blur_tab() {
+    constexpr int K9[9] = {7, 17, 32, 46, 52, 46, 32, 17, 7};
+    FbBlurTab t{};
+    for (int l = 0; l < 64; l++) {
+        const int n = l & 15, gq = l >> 4;
+        for (int j = 0; j < 8; j++) {
+            const int tw = 8 * gq + j - n;
+            const int rho = j < 4 ? 4 * gq + j : 16 + 4 * gq + (j - 4);
+            const int tv = rho - n;
+            const unsigned long long bw = (tw >= 0 && tw <= 8) ? (unsigned long long)K9[tw] : 0ull;
+            const unsigned long long bv = (tv >= 0 && tv <= 8) ? (unsigned long long)K9[tv] : 0ull;
+            t.wb[l] |= bw << (8 * j);
+            t.vb[l] |= bv << (8 * j);
+        }
+    }
+    return t;
+}
+static __constant__ FbBlurTab c_fbblur = make_fb_blur_tab();
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// bytes `sel` (0..3) of four dwords gathered into one dword (a0 -> byte 0 .. a3 -> byte 3)
+template <int SEL>
+__device__ __forceinline__ uint32_t gather_byte(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+    const uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0000u | (uint32_t)(SEL + 4) << 8 | (uint32_t)SEL);
+    const uint32_t hi = __builtin_amdgcn_perm(a3, a2, (uint32_t)(SEL + 4) << 24 | (uint32_t)SEL << 16 | 0x0c0cu);
+    return lo | hi;
+}
+
+__device__ __forceinline__ long i8x8(uint32_t lo, uint32_t hi) { return (long)((unsigned long long)hi << 32 | lo); }
+
+__device__ __forceinline__ void fast_blur_mfma(const uint32_t *tin, uint8_t *dst, int bp, int x0, int y0, int w,
+                                               int h, int wv, int lane) {
+    const int n = lane & 15, gq = lane >> 4;
+    const long WB = (long)c_fbblur.wb[lane], VB = (long)c_fbblur.vb[lane];
+    const uint8_t *t8 = (const uint8_t *)tin;
+    // row-pass A: staged row 16 yb + n (rows past the 24 staged ones repeat row 23: their V
+    // weights are 0), columns 16 xb + 8 gq + 0..7 (the last block's upper columns fall past
+    // the staged row: W is 0 there)
+    const int r0 = n, r1 = min(16 + n, FB_TH + 7);
+    const uint32_t XM = 0x80808080u;
+    const int KH = 128 * 257 + 128;
+    const i32x4 z = {0, 0, 0, 0}, kh = {KH, KH, KH, KH};
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int xb = 2 * wv + q;
+        const int c = 16 * xb + 8 * gq;
+        const uint2 a0 = *(const uint2 *)(t8 + r0 * FB_LW + c);
+        const uint2 a1 = *(const uint2 *)(t8 + r1 * FB_LW + c);
+        const i32x4 R0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(i8x8(a0.x ^ XM, a0.y ^ XM), WB, z, 0, 0, 0);
+        const i32x4 R1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(i8x8(a1.x ^ XM, a1.y ^ XM), WB, z, 0, 0, 0);
+        // column-pass A fragments: K elements 0..3 = rows 4 gq + r (R0), 4..7 = rows 16 + 4 gq + r (R1)
+        const long AH = i8x8(gather_byte<1>((uint32_t)R0.x, (uint32_t)R0.y, (uint32_t)R0.z, (uint32_t)R0.w),
+                             gather_byte<1>((uint32_t)R1.x, (uint32_t)R1.y, (uint32_t)R1.z, (uint32_t)R1.w));
+        const long AL = i8x8(gather_byte<0>((uint32_t)R0.x, (uint32_t)R0.y, (uint32_t)R0.z, (uint32_t)R0.w) ^ XM,
+                             gather_byte<0>((uint32_t)R1.x, (uint32_t)R1.y, (uint32_t)R1.z, (uint32_t)R1.w) ^ XM);
+        const i32x4 OH = __builtin_amdgcn_mfma_i32_16x16x32_i8(AH, VB, kh, 0, 0, 0);
+        const i32x4 OL = __builtin_amdgcn_mfma_i32_16x16x32_i8(AL, VB, z, 0, 0, 0);
+        // lane: output row y0 + n, columns x0 + 16 xb + 4 gq + r
+        const uint32_t v0 = ((uint32_t)OH.x << 8) + (uint32_t)OL.x, v1 = ((uint32_t)OH.y << 8) + (uint32_t)OL.y;
+        const uint32_t v2 = ((uint32_t)OH.z << 8) + (uint32_t)OL.z, v3 = ((uint32_t)OH.w << 8) + (uint32_t)OL.w;
+        const uint32_t val = gather_byte<2>(v0, v1, v2, v3);
+        const int y = y0 + n, x = x0 + 16 * xb + 4 * gq;
+        if (y < h && x < w) {
+            uint8_t *o = dst + (long long)y * bp + x;
+            if (x + 3 < w) {
+                *(uint32_t *)o = val;
+            } else {
+                for (int k = 0; k < w - x; k++) o[k] = (uint8_t)(val >> (8 * k));
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
                                                         uint8_t *blur, int *cell_cnt, uint32_t *cell_keys) {
     __shared__ __align__(16) uint32_t tin[(FB_TH + 8) * FB_LD];
-    __shared__ uint32_t trowp[((FB_TH + 8) / 2) * FB_TW];
     __shared__ uint32_t mt[FB_NG];   // exact M bytes, (mrow, x - x0 + 4)
     __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets)
     __shared__ uint16_t bboth[4][128];     // per-wavefront queue of dual-polarity candidates
@@ -308,7 +404,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
     t -= g.blur_tile_base[l];
     const int tx = t % g.blur_tiles_x[l], ty = t / g.blur_tiles_x[l];
-    const int w = g.lw[l], h = g.lh[l], bp = g.bp[l];
+    const int w = g.lw[l], h = g.lh[l];
     const int x0 = tx * FB_TW, y0 = ty * FB_TH;
     int pitch;
     const uint8_t *src = level_ptr(g, in, pyr, b, l, &pitch);
@@ -319,8 +415,8 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     // that cross the left / right edge.
     {
         const bool inner_x = x0 >= 4 && x0 + FB_TW + 4 <= w;
-        for (int i = threadIdx.x; i < (FB_TH + 8) * (FB_LD / 2); i += 256) {
-            const int rr = i / (FB_LD / 2), jj = i - rr * (FB_LD / 2);
+        for (int i = threadIdx.x; i < (FB_TH + 8) * (FB_SD / 2); i += 256) {
+            const int rr = i / (FB_SD / 2), jj = i - rr * (FB_SD / 2);
             int yy = y0 - 4 + rr;
             yy = yy < 0 ? -yy : yy;
             yy = yy >= h ? 2 * h - 2 - yy : yy;
@@ -389,7 +485,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             uint32_t cA = 0, cB = 0;   // top bit of byte i: pixel xb+i (cA), xb+4+i (cB)
             if (active && y >= dy0 && y < dy1 && xb + 7 >= dx0 && xb < dx1) {
                 const uint32_t *row = tin + (mrow + 3) * FB_LD;
-                auto ld = [&](const uint32_t *rw, int i) { return (unsigned)i < (unsigned)FB_LD ? rw[i] : 0u; };
+                auto ld = [&](const uint32_t *rw, int i) { return (unsigned)i < (unsigned)FB_SD ? rw[i] : 0u; };
                 const uint32_t C0 = ld(row, d), C1 = ld(row, d + 1), C2 = ld(row, d + 2), C3 = ld(row, d + 3);
                 const uint32_t *rn = row - 3 * FB_LD, *rs = row + 3 * FB_LD;
                 cA = swar4(C1, C0, C2, ld(rn, d + 1), ld(rs, d + 1));
@@ -440,35 +536,10 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         }
 #endif
     }
-    // 4a. blur row pass: tile rows (2p, 2p+1) x output cols 4cg .. 4cg+3
+    // 4. GaussianBlur on the matrix cores: wavefront wv writes output columns 32 wv .. 32 wv + 31
+    // (two 16-column blocks) x the tile's 16 rows (fast_blur_mfma)
 #ifndef FB_SKIP_BLUR
-    {
-        const uint32_t K0123 = 7u | 17u << 8 | 32u << 16 | 46u << 24;
-        const uint32_t K4567 = 52u | 46u << 8 | 32u << 16 | 17u << 24;
-        for (int task = threadIdx.x; task < ((FB_TH + 8) / 2) * (FB_TW / 4); task += 256) {
-            const int p = task / (FB_TW / 4), cg = task % (FB_TW / 4);
-            uint32_t o[2][4];
-#pragma unroll
-            for (int rr = 0; rr < 2; rr++) {
-                const uint32_t *row = tin + (2 * p + rr) * FB_LD + cg;
-                const uint32_t D0 = row[0], D1 = row[1], D2 = row[2];
-#pragma unroll
-                for (int s = 0; s < 4; s++) {
-                    const uint32_t Wa = s ? __builtin_amdgcn_alignbyte(D1, D0, s) : D0;
-                    const uint32_t Wb = s ? __builtin_amdgcn_alignbyte(D2, D1, s) : D1;
-                    uint32_t acc = __builtin_amdgcn_udot4(Wa, K0123, 0u, false);
-                    acc = __builtin_amdgcn_udot4(Wb, K4567, acc, false);
-                    o[rr][s] = __builtin_amdgcn_udot4(D2, 7u << (8 * s), acc, false);
-                }
-            }
-            uint4 v;
-            v.x = o[0][0] | o[1][0] << 16;
-            v.y = o[0][1] | o[1][1] << 16;
-            v.z = o[0][2] | o[1][2] << 16;
-            v.w = o[0][3] | o[1][3] << 16;
-            *(uint4 *)&trowp[p * FB_TW + 4 * cg] = v;
-        }
-    }
+    fast_blur_mfma(tin, blur + (long long)b * g.blur_stride + g.blur_off[l], g.bp[l], x0, y0, w, h, wv, lane);
 #endif
     __syncthreads();
     // 3. exact M of the pooled candidates: wavefront wv takes chunks wv, wv + 4, ... of 64; its
@@ -550,44 +621,6 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         if (nb > 0) drain(nb);
         if (lane == 0) hcount[wv] = nh;
     }
-    // 4b. blur column pass: output rows 2rp, 2rp+1 x cols 4cg .. 4cg+3
-#ifndef FB_SKIP_BLUR
-    {
-        const int rp = threadIdx.x >> 5, cg = threadIdx.x & 31;
-        uint4 P[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) P[k] = *(const uint4 *)&trowp[(rp + k) * FB_TW + 4 * cg];
-        const uint32_t KE[5] = {7u | 17u << 16, 32u | 46u << 16, 52u | 46u << 16, 32u | 17u << 16, 7u};
-        const uint32_t KO[5] = {7u << 16, 17u | 32u << 16, 46u | 52u << 16, 46u | 32u << 16, 17u | 7u << 16};
-        uint32_t be = 0, bo = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            uint32_t ae = 32768u, ao = 32768u;
-#pragma unroll
-            for (int k = 0; k < 5; k++) {
-                const uint32_t pv = c == 0 ? P[k].x : c == 1 ? P[k].y : c == 2 ? P[k].z : P[k].w;
-                ae = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, pv), __builtin_bit_cast(u16x2, KE[k]), ae, false);
-                ao = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, pv), __builtin_bit_cast(u16x2, KO[k]), ao, false);
-            }
-            be |= (ae >> 16) << (8 * c);
-            bo |= (ao >> 16) << (8 * c);
-        }
-        uint8_t *dst = blur + (long long)b * g.blur_stride + g.blur_off[l];
-        const int x = x0 + 4 * cg;
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const int y = y0 + 2 * rp + e;
-            const uint32_t val = e ? bo : be;
-            if (y >= h || x >= w) continue;
-            uint8_t *o = dst + (long long)y * bp + x;
-            if (x + 3 < w) {
-                *(uint32_t *)o = val;
-            } else {
-                for (int k = 0; k < w - x; k++) o[k] = (uint8_t)(val >> (8 * k));
-            }
-        }
-    }
-#endif
     __syncthreads();
     // 5. 3x3 NMS of the hot pixels at tlo against their in-cell neighbours (others score 0),
     // survivors appended to their cell's slot list

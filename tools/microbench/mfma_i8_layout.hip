@@ -1,8 +1,8 @@
-// Operand / accumulator lane maps of v_mfma_i32_16x16x64_i8 on gfx950, checked with exact
-// asymmetric integer data against a host product (the MFMA blur of fast_blur_kernel relies on
-// them). Assumed maps: lane l holds A[m = l & 15][k = 16 (l >> 4) + j] and
-// B[k = 16 (l >> 4) + j][n = l & 15] in byte j = 0..15 of its 4-VGPR fragment; C/D element r of
-// lane l is C[m = 4 (l >> 4) + r][n = l & 15].
+// Operand / accumulator lane maps of v_mfma_i32_16x16x64_i8 and v_mfma_i32_16x16x32_i8 on gfx950,
+// checked with exact asymmetric integer data against a host product (the MFMA blur of
+// fast_blur_kernel relies on them). Assumed maps: lane l holds A[m = l & 15][k = KL (l >> 4) + j]
+// and B[k = KL (l >> 4) + j][n = l & 15] in byte j = 0..KL-1 of its fragment (KL = 16 for K = 64,
+// 8 for K = 32); C/D element r of lane l is C[m = 4 (l >> 4) + r][n = l & 15].
 // Build: hipcc -O2 --offload-arch=gfx950 -o mfma_i8_layout mfma_i8_layout.hip
 #include <hip/hip_runtime.h>
 
@@ -10,6 +10,21 @@
 #include <cstdio>
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// K = 32 form: 8 bytes per lane; A is read as the first 32 columns of the K = 64 data
+__global__ void probe32(const int8_t *A, const int8_t *B, const int *C0, int *D) {
+    const int l = threadIdx.x, m = l & 15, g = l >> 4;
+    long a = 0, b = 0;
+    int8_t *pa = (int8_t *)&a, *pb = (int8_t *)&b;
+    for (int j = 0; j < 8; j++) {
+        pa[j] = A[m * 64 + 8 * g + j];
+        pb[j] = B[(8 * g + j) * 16 + m];
+    }
+    i32x4 c;
+    for (int r = 0; r < 4; r++) c[r] = C0[(4 * g + r) * 16 + m];
+    c = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, b, c, 0, 0, 0);
+    for (int r = 0; r < 4; r++) D[(4 * g + r) * 16 + m] = c[r];
+}
 
 __global__ void probe(const int8_t *A, const int8_t *B, const int *C0, int *D) {
     const int l = threadIdx.x, m = l & 15, g = l >> 4;
@@ -51,6 +66,17 @@ int main() {
     if (hipMemcpy(hD, dD, sizeof hD, hipMemcpyDeviceToHost) != hipSuccess) return 3;
     int bad = 0;
     for (int i = 0; i < 256; i++) bad += hD[i] != ref[i];
-    printf("{\"mfma_i32_16x16x64_i8_layout_mismatches\": %d, \"d00\": %d, \"ref00\": %d}\n", bad, hD[0], ref[0]);
-    return bad ? 1 : 0;
+    int ref32[256];
+    for (int m = 0; m < 16; m++)
+        for (int n = 0; n < 16; n++) {
+            int s = hC[m * 16 + n];
+            for (int k = 0; k < 32; k++) s += hA[m * 64 + k] * hB[k * 16 + n];
+            ref32[m * 16 + n] = s;
+        }
+    probe32<<<1, 64>>>(dA, dB, dC, dD);
+    if (hipMemcpy(hD, dD, sizeof hD, hipMemcpyDeviceToHost) != hipSuccess) return 3;
+    int bad32 = 0;
+    for (int i = 0; i < 256; i++) bad32 += hD[i] != ref32[i];
+    printf("{\"mfma_i32_16x16x64_i8_layout_mismatches\": %d, \"mfma_i32_16x16x32_i8_layout_mismatches\": %d}\n", bad, bad32);
+    return bad || bad32 ? 1 : 0;
 }
