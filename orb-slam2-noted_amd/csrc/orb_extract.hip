@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 #define FB_LW (FB_TW + 8)   // LDS tile row stride in bytes (8-aligned rows for the blur's ds_read_b64)
 #define FB_LD (FB_LW / 4)   // LDS tile row stride in dwords
 #define FB_MR (FB_TH + 2)   // score rows y0-1 .. y0+16 (tile + NMS ring)
-#define FB_NG (FB_MR * FB_LD)   // score tile dwords
+#define FB_NG (FB_MR * FB_LD)   // score tile dwords (a multiple of 4, <= 1024: cleared as uint4 by 256 threads)
 #define FB_CCAP (FB_MR * (FB_TW + 2) + 64)   // candidate slots: every score pixel + one chunk of hot-list slack
 
 __device__ __forceinline__ int refl101(int i, int n) {
@@ -395,7 +395,7 @@ __device__ __forceinline__ void fast_blur_mfma(const uint32_t *tin, uint8_t *dst
 __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
                                                         uint8_t *blur, int *cell_cnt, uint32_t *cell_keys) {
     __shared__ __align__(16) uint32_t tin[(FB_TH + 8) * FB_LD];
-    __shared__ uint32_t mt[FB_NG];   // exact M bytes, (mrow, x - x0 + 4)
+    __shared__ __align__(16) uint32_t mt[FB_NG];   // exact M bytes, (mrow, x - x0 + 4)
     __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets)
     __shared__ uint16_t bboth[4][128];     // per-wavefront queue of dual-polarity candidates
     __shared__ int ncand_sh, hcount[4];
@@ -408,28 +408,23 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     const int x0 = tx * FB_TW, y0 = ty * FB_TH;
     int pitch;
     const uint8_t *src = level_ptr(g, in, pyr, b, l, &pitch);
-    // 1. stage rows y0-4 .. y0+19, cols x0-4 .. x0+131 as dword pairs: three aligned dword loads
-    // + two v_alignbyte per pair (the last load may read up to 4 bytes past a row's end: inputs
-    // carry a 16-byte readable tail, the pyramid allocation a 64-byte one); reflect-101 of rows
-    // (the 4-row halo never reaches past a level of >= 40 rows) and, per byte, of the few pairs
-    // that cross the left / right edge.
-    {
-        const bool inner_x = x0 >= 4 && x0 + FB_TW + 4 <= w;
-        for (int i = threadIdx.x; i < (FB_TH + 8) * (FB_SD / 2); i += 256) {
-            const int rr = i / (FB_SD / 2), jj = i - rr * (FB_SD / 2);
+    // 1. stage rows y0-4 .. y0+19, cols x0-4 .. x0+131 as 8-byte pairs: thread -> pair
+    // jj = tid % 17 of rows tid / 17 and tid / 17 + 15 (255 threads), one unaligned dwordx2 load
+    // per pair; reflect-101 of rows (the 4-row halo never reaches past a level of >= 40 rows)
+    // and, per byte, of the few pairs that cross the left / right edge.
+    static_assert(FB_SD / 2 == 17 && FB_TH + 8 <= 30, "staging map: 17 pairs x 15 rows per pass");
+    if (threadIdx.x < 255) {
+        const int rr0 = (threadIdx.x * 241) >> 12, jj = threadIdx.x - 17 * rr0;   // tid / 17 for tid < 255
+        const int xs = x0 - 4 + 8 * jj;
+        const bool fast = xs >= 0 && xs + 7 < w;
+        for (int rr = rr0; rr < FB_TH + 8; rr += 15) {
             int yy = y0 - 4 + rr;
             yy = yy < 0 ? -yy : yy;
             yy = yy >= h ? 2 * h - 2 - yy : yy;
             const uint8_t *rowp = src + (long long)yy * pitch;
-            const int xs = x0 - 4 + 8 * jj;
             uint2 v;
-            if (inner_x || (xs >= 0 && xs + 7 < w)) {
-                const uintptr_t a = (uintptr_t)(rowp + xs);
-                const uint32_t *pa = (const uint32_t *)(a & ~(uintptr_t)3);
-                const uint32_t sh = (uint32_t)(a & 3);
-                const uint32_t d0 = pa[0], d1 = pa[1], d2 = pa[2];
-                v.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
-                v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            if (fast) {
+                __builtin_memcpy(&v, rowp + xs, 8);
             } else {
                 v.x = v.y = 0;
 #pragma unroll
@@ -444,7 +439,8 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             *(uint2 *)&tin[rr * FB_LD + 2 * jj] = v;
         }
     }
-    for (int i = threadIdx.x; i < FB_NG; i += 256) mt[i] = 0u;
+    static_assert(FB_NG % 4 == 0 && FB_NG / 4 <= 256, "score tile cleared as one uint4 per thread");
+    if (threadIdx.x < FB_NG / 4) ((uint4 *)mt)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
     if (threadIdx.x == 0) ncand_sh = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = wave_id();
