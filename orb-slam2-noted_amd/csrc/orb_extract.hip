@@ -491,24 +491,26 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
                 cA &= (uint32_t)vm;
                 cB &= (uint32_t)(vm >> 32);
             }
-            // compaction into the pooled list: one LDS atomic per wavefront reserves its slots
+            // compaction into the pooled list: the lane's 8 candidate bits (v_dot4 gathers the
+            // byte top bits), an inclusive DPP scan of their counts over the wavefront, one LDS
+            // atomic per wavefront for the slots, then each lane writes its own candidates
             const int pos0 = mrow * FB_LW + 4 * d + 4;   // score-tile byte of pixel xb
-            unsigned long long bal[8];
-            int tot8 = 0;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                bal[i] = __ballot(((i < 4 ? cA : cB) >> (8 * (i & 3) + 7)) & 1u);
-                tot8 += __popcll(bal[i]);
-            }
+            const uint32_t m = __builtin_amdgcn_udot4(cB >> 7, 0x80402010u,
+                                                      __builtin_amdgcn_udot4(cA >> 7, 0x08040201u, 0u, false), false);
+            const int cnt = __builtin_popcount(m);
+            int inc = cnt;
+            inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xF, 0xF, false);   // row_shr:1
+            inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xF, 0xF, false);   // row_shr:2
+            inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xF, 0xF, false);   // row_shr:4
+            inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xF, 0xF, false);   // row_shr:8
+            inc += __builtin_amdgcn_update_dpp(0, inc, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+            inc += __builtin_amdgcn_update_dpp(0, inc, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+            const int tot8 = __builtin_amdgcn_readlane(inc, 63);
             if (tot8 == 0) return;   // wave-uniform
             int base = 0;
             if (lane == 0) base = atomicAdd(&ncand_sh, tot8);
-            base = __builtin_amdgcn_readfirstlane(base);
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                if (((i < 4 ? cA : cB) >> (8 * (i & 3) + 7)) & 1u) clist[base + lane_rank(bal[i])] = (uint16_t)(pos0 + i);
-                base += __popcll(bal[i]);
-            }
+            base = __builtin_amdgcn_readfirstlane(base) + inc - cnt;
+            for (uint32_t mm = m; mm; mm &= mm - 1) clist[base++] = (uint16_t)(pos0 + __builtin_ctz(mm));
         };
         const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;   // pixels (y0 + r, x0 + cb + i)
 #ifndef FB_SKIP_PRE   // instruction-count experiments (make variant VDEFS=-DFB_SKIP_...)
