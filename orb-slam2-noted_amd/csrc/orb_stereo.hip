@@ -200,10 +200,15 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
                     }
                 }
             }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) best = min(best, (unsigned)__shfl_xor((int)best, off, 64));
             if (__any(stop)) break;
         }
+        // (dist, index) minimum over the wavefront once, after the scan (DPP row mins, then rows)
+        best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x111, 0xF, 0xF, false));
+        best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x112, 0xF, 0xF, false));
+        best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x114, 0xF, 0xF, false));
+        best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x118, 0xF, 0xF, false));
+        best = min(min((unsigned)__builtin_amdgcn_readlane((int)best, 15), (unsigned)__builtin_amdgcn_readlane((int)best, 31)),
+                   min((unsigned)__builtin_amdgcn_readlane((int)best, 47), (unsigned)__builtin_amdgcn_readlane((int)best, 63)));
         if (best != 0xFFFFFFFFu && (int)(best >> 16) < bestDist) {
             bestDist = (int)(best >> 16);
             bestIdxR = (int)(best & 0xFFFF);
@@ -227,59 +232,60 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
         imR = side_level(g, a.R, imgR, oct, &pitchR);
     }
     if (ok) {
+        // SAD of (IL - IL(w, w)) and (IR - IR(w, w + incR)) over the 11 x 11 window (:989-1011):
+        // |(L + cr) - (R + cl)| per pixel, on packed u16 pairs with v_sad_u16 (a = L + cr - cl + 256,
+        // b = R + 256, both in [0, 766]). Lane 16 s + rr, pass p: window row rr (< 11), incR =
+        // 4 p + s - 5 (<= 5); the 16 lanes of a DPP row sum their rows, lane 15 holds incR's total.
         const int r0 = (int)scaledvL - 5, cL0 = (int)scaleduL - 5, cR = (int)scaleduR0;
         const int cl = imL[(long long)(r0 + 5) * pitchL + cL0 + 5];
-        // partial SAD of (incR, row) pairs t = (inc+5)*11 + rr: lane holds t = lane, lane+64
-        int part0 = 0, part1 = 0;
-        for (int h = 0; h < 2; h++) {
-            const int t = lane + 64 * h;
-            if (t >= 121) continue;
-            const int inc = t / 11 - 5, rr = t % 11;
-            const int cr = imR[(long long)(r0 + 5) * pitchR + cR + inc];
-            const uint8_t *pl = imL + (long long)(r0 + rr) * pitchL + cL0;
-            const uint8_t *pr = imR + (long long)(r0 + rr) * pitchR + cR + inc - 5;
-            int acc = 0;
+        const int rr = lane & 15, sgrp = lane >> 4, rrc = min(rr, 10);
+        uint32_t LD[3], RD[3];
+        __builtin_memcpy(LD, imL + (long long)(r0 + rrc) * pitchL + cL0, 12);   // 11 pixels + 1 (in the level)
+        const uint32_t Lp[6] = {__builtin_amdgcn_perm(0u, LD[0], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[0], 0x0c030c02u),
+                                __builtin_amdgcn_perm(0u, LD[1], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[1], 0x0c030c02u),
+                                __builtin_amdgcn_perm(0u, LD[2], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[2], 0x0c0c0c02u)};
+        const uint32_t ONES = 0x01010101u;
+        const uint8_t *rowR = imR + (long long)(r0 + rrc) * pitchR + cR - 5;
+        const uint8_t *rowC = imR + (long long)(r0 + 5) * pitchR + cR;
+        int sums[12];
 #pragma unroll
-            for (int xx = 0; xx < 11; xx++) {
-                const int d = (pl[xx] - cl) - (pr[xx] - cr);
-                acc += d < 0 ? -d : d;
-            }
-            if (h == 0) part0 = acc; else part1 = acc;
-        }
-        // lane k < 11 gathers the 11 rows of incR = k - 5
-        int sum = 0;
-        for (int rr = 0; rr < 11; rr++) {
-            const int src = min(lane, 10) * 11 + rr;
-            const int v0 = __shfl(part0, src & 63, 64);
-            const int v1 = __shfl(part1, src & 63, 64);
-            sum += src < 64 ? v0 : v1;
-        }
-        int sums[11];
+        for (int pss = 0; pss < 3; pss++) {
+            const int inc = 4 * pss + sgrp - 5, incc = min(inc, 5);
+            const uint32_t KA = (uint32_t)(rowC[incc] - cl + 256), KA2 = KA * 0x10001u;
+            __builtin_memcpy(RD, rowR + incc, 12);   // cols cR + inc - 5 .. + 6 (endu < width)
+            uint32_t acc = __builtin_amdgcn_sad_u16(Lp[0] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04010400u), 0u);
+            acc = __builtin_amdgcn_sad_u16(Lp[1] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04030402u), acc);
+            acc = __builtin_amdgcn_sad_u16(Lp[2] + KA2, __builtin_amdgcn_perm(ONES, RD[1], 0x04010400u), acc);
+            acc = __builtin_amdgcn_sad_u16(Lp[3] + KA2, __builtin_amdgcn_perm(ONES, RD[1], 0x04030402u), acc);
+            acc = __builtin_amdgcn_sad_u16(Lp[4] + KA2, __builtin_amdgcn_perm(ONES, RD[2], 0x04010400u), acc);
+            acc = __builtin_amdgcn_sad_u16(Lp[5] + KA, __builtin_amdgcn_perm(ONES, RD[2], 0x0c0c0402u), acc);
+            int v = (rr < 11 && inc <= 5) ? (int)acc : 0;
+            v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+            v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+            v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+            v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
 #pragma unroll
-        for (int k = 0; k < 11; k++) sums[k] = __shfl(sum, k, 64);
-        if (lane == 0) {
-            float vd[11];
-            int bestS = INT_MAX, bestinc = 0;
-            for (int inc = -5; inc <= 5; inc++) {
-                const float dist = (float)sums[inc + 5];
-                if (dist < (float)bestS) { bestS = (int)dist; bestinc = inc; }
-                vd[inc + 5] = dist;
-            }
-            if (bestinc != -5 && bestinc != 5) {
-                const float d1 = vd[5 + bestinc - 1], d2 = vd[5 + bestinc], d3 = vd[5 + bestinc + 1];
-                const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
-                if (!(deltaR < -1 || deltaR > 1)) {
-                    float bestuR = g.scale[oct] * ((float)scaleduR0 + (float)bestinc + deltaR);
-                    float disparity = uL - bestuR;
-                    if (disparity >= minD && disparity < maxD) {
-                        if (disparity <= 0) {
-                            disparity = (float)0.01;
-                            bestuR = (float)((double)uL - 0.01);
-                        }
-                        outD = a.mbf / disparity;
-                        outU = bestuR;
-                        outS = bestS;
+            for (int k = 0; k < 4; k++) sums[4 * pss + k] = __builtin_amdgcn_readlane(v, 16 * k + 15);
+        }
+        // wave-uniform tail (:1013-1063): first minimum over incR, parabola, disparity
+        int bestS = INT_MAX, bestinc = 0;
+#pragma unroll
+        for (int inc = -5; inc <= 5; inc++)
+            if (sums[inc + 5] < bestS) { bestS = sums[inc + 5]; bestinc = inc; }
+        if (bestinc != -5 && bestinc != 5) {
+            const float d1 = (float)sums[5 + bestinc - 1], d2 = (float)sums[5 + bestinc], d3 = (float)sums[5 + bestinc + 1];
+            const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
+            if (!(deltaR < -1 || deltaR > 1)) {
+                float bestuR = g.scale[oct] * ((float)scaleduR0 + (float)bestinc + deltaR);
+                float disparity = uL - bestuR;
+                if (disparity >= minD && disparity < maxD) {
+                    if (disparity <= 0) {
+                        disparity = (float)0.01;
+                        bestuR = (float)((double)uL - 0.01);
                     }
+                    outD = a.mbf / disparity;
+                    outU = bestuR;
+                    outS = bestS;
                 }
             }
         }
