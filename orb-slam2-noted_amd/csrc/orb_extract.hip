@@ -1248,30 +1248,64 @@ __device__ __forceinline__ int wave_sum_dpp(int v) {
 struct DescSlot {
     int valid, l, off;
     uint32_t key;
+    const uint8_t *img;   // level l of image b (IC_Angle reads), row pitch `pitch`
+    long long blur0;      // offset of level l of image b in the blurred pyramid, row pitch `bw`
+    int pitch, bw;
+    float scale;
+    int spatch;
 };
 
-__device__ __forceinline__ DescSlot desc_slot(const ExtractGeom &g, const uint32_t *sel, const int *sel_cnt, int *cnt,
-                                              int slot, int b, int lane) {
-    DescSlot d{0, 0, 0, 0u};
-    const int L = g.nlevels, cap = g.out_base[L];
-    if (slot >= cap) return d;
-    int l = 0;
-    while (l + 1 < L && slot >= g.out_base[l + 1]) l++;
-    const int idx = slot - g.out_base[l];
-    const int *sc = sel_cnt + b * L;
-    if (slot == 0 && lane == 0) {
-        int tot = 0;
-        for (int k = 0; k < L; k++) tot += sc[k];
-        cnt[b] = tot;
+// The wavefront's DESC_R output slots in one round trip: lanes k < L load the per-level
+// selected counts of image b, lanes r < DESC_R the slots' keys, a DPP scan over the first row
+// gives the level prefix (the output row of slot = keypoints of the lower levels + index).
+template <int DESC_R>
+__device__ __forceinline__ void desc_slots(const ExtractGeom &g, const uint8_t *in, const uint8_t *pyr,
+                                           const uint32_t *sel, const int *sel_cnt, int *cnt, int s0, int b, int lane,
+                                           DescSlot *d) {
+    const int L = g.nlevels, cap = g.out_base[L];   // L <= ORBX_MAXL = 16: one DPP row
+    const int scl = lane < L ? sel_cnt[(long long)b * L + lane] : 0;
+    const uint32_t keyl = (lane < DESC_R && s0 + lane < cap) ? sel[(long long)b * cap + s0 + lane] : 0u;
+    // per-level geometry on lane k (vector loads issued with the two above: no dependent
+    // scalar load once the slot's level is known)
+    const int kk = min(lane, L - 1);
+    const int obk = g.out_base[kk + 1];
+    const uint8_t *imgk = kk == 0 ? in + (long long)b * g.in_stride : pyr + (long long)b * g.pyr_stride + g.pyr_off[kk];
+    const long long blurk = (long long)b * g.blur_stride + g.blur_off[kk];
+    const int pitchk = kk == 0 ? g.in_pitch : g.bp[kk], bwk = g.bp[kk], spk = g.scaled_patch[kk];
+    const float sck = g.scale[kk];
+    int inc = scl;
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xF, 0xF, false);   // row_shr:1
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xF, 0xF, false);   // row_shr:2
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xF, 0xF, false);   // row_shr:4
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xF, 0xF, false);   // row_shr:8
+    if (s0 == 0) {
+        const int tot = __builtin_amdgcn_readlane(inc, L - 1);
+        if (lane == 0) cnt[b] = tot;
     }
-    if (idx >= sc[l]) return d;
-    int off = idx;
-    for (int k = 0; k < l; k++) off += sc[k];
-    d.valid = 1;
-    d.l = l;
-    d.off = off;
-    d.key = sel[(long long)b * cap + slot];
-    return d;
+#pragma unroll
+    for (int r = 0; r < DESC_R; r++) {
+        d[r] = DescSlot{};
+        const int slot = s0 + r;
+        if (slot >= cap) continue;
+        // level = number of levels k + 1 < L whose first slot out_base[k + 1] <= slot
+        const int l = __popcll(__ballot(lane + 1 < L && slot >= obk));
+        const int idx = slot - (l ? __builtin_amdgcn_readlane(obk, l - 1) : 0);
+        const int nl = __builtin_amdgcn_readlane(scl, l);
+        if (idx >= nl) continue;
+        d[r].valid = 1;
+        d[r].l = l;
+        d[r].off = __builtin_amdgcn_readlane(inc, l) - nl + idx;
+        d[r].key = (uint32_t)__builtin_amdgcn_readlane((int)keyl, r);
+        const unsigned long long ip = (unsigned long long)imgk;
+        d[r].img = (const uint8_t *)((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ip, l) |
+                                     (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(ip >> 32), l) << 32);
+        d[r].blur0 = (long long)((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)blurk, l) |
+                                 (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)((unsigned long long)blurk >> 32), l) << 32);
+        d[r].pitch = __builtin_amdgcn_readlane(pitchk, l);
+        d[r].bw = __builtin_amdgcn_readlane(bwk, l);
+        d[r].spatch = __builtin_amdgcn_readlane(spk, l);
+        d[r].scale = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sck), l));
+    }
 }
 
 // K5: IC_Angle (:94-141) + computeOrbDescriptor (:153-204) + keypoint assembly
@@ -1294,8 +1328,7 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
     __shared__ uint32_t patch[4][DESC_R][372];
     const int s0 = (bxr * 4 + wv) * DESC_R;
     DescSlot d[DESC_R];
-#pragma unroll
-    for (int r = 0; r < DESC_R; r++) d[r] = desc_slot(g, sel, sel_cnt, cnt, s0 + r, b, lane);
+    desc_slots<DESC_R>(g, in, pyr, sel, sel_cnt, cnt, s0, b, lane, d);
     bool any = false;
 #pragma unroll
     for (int r = 0; r < DESC_R; r++) any |= d[r].valid != 0;
@@ -1307,10 +1340,9 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
     for (int r = 0; r < DESC_R; r++) {
         M10[r] = M01[r] = PSH[r] = 0;
         if (!d[r].valid) continue;
-        const int l = d[r].l;
         const int x = key_x(d[r].key) + 16, y = key_y(d[r].key) + 16;  // + minBorderX/Y (:1177-1186)
-        int pitch;
-        const uint8_t *img = level_ptr(g, in, pyr, b, l, &pitch);
+        const uint8_t *img = d[r].img;
+        const int pitch = d[r].pitch;
         // IC_Angle over the circular patch (|u| <= umax[|v|]): rows v = -15..15 as 8 dwords
         // (u = -16..15), sum_u u*p = sum (u+16)*p - 16 * sum p with v_dot4_u32_u8 (exact)
         // lane -> dword w = lane % 8 of rows v0, v0 + 8, v0 + 16, v0 + 24 (v0 = lane / 8 - 15);
@@ -1336,8 +1368,8 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
         // the rotated pattern stays within +-18 pixels (|rot(p)| <= 13 sqrt 2): rows y-18 ..
         // y+18, bytes x-18 .. x+21 as 10 aligned dwords per row (the pitch is 16-aligned, so
         // every row has the same misalignment)
-        const int bw = g.bp[l];
-        const long long c0 = (long long)b * g.blur_stride + g.blur_off[l] + (long long)(y - 18) * bw + (x - 18);
+        const int bw = d[r].bw;
+        const long long c0 = d[r].blur0 + (long long)(y - 18) * bw + (x - 18);
         const int sh = (int)(c0 & 3);
         PSH[r] = sh;
         const long long a0 = c0 - sh;
@@ -1418,11 +1450,11 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
             unsigned long long *dd = (unsigned long long *)(desc + o * 32);
             dd[0] = words[0]; dd[1] = words[1]; dd[2] = words[2]; dd[3] = words[3];
             orbx_kp kp;
-            const float s = g.scale[l];
+            const float s = d[r].scale;
             kp.x = (float)(key_x(d[r].key) + 16);
             kp.y = (float)(key_y(d[r].key) + 16);
             if (l != 0) { kp.x *= s; kp.y *= s; }  // :1642-1651
-            kp.size = (float)g.scaled_patch[l];
+            kp.size = (float)d[r].spatch;
             kp.angle = angle;
             kp.response = (float)key_score(d[r].key);
             kp.octave = l;
