@@ -417,26 +417,37 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         const int rr0 = (threadIdx.x * 241) >> 12, jj = threadIdx.x - 17 * rr0;   // tid / 17 for tid < 255
         const int xs = x0 - 4 + 8 * jj;
         const bool fast = xs >= 0 && xs + 7 < w;
-        for (int rr = rr0; rr < FB_TH + 8; rr += 15) {
+        auto row_of = [&](int rr) {
             int yy = y0 - 4 + rr;
             yy = yy < 0 ? -yy : yy;
             yy = yy >= h ? 2 * h - 2 - yy : yy;
-            const uint8_t *rowp = src + (long long)yy * pitch;
-            uint2 v;
-            if (fast) {
-                __builtin_memcpy(&v, rowp + xs, 8);
-            } else {
-                v.x = v.y = 0;
-#pragma unroll
-                for (int e = 0; e < 8; e++) {
-                    int xx = xs + e;
-                    xx = xx < 0 ? -xx : xx;
-                    xx = xx >= w ? 2 * w - 2 - xx : xx;
-                    const uint32_t by = rowp[xx];
-                    if (e < 4) v.x |= by << (8 * e); else v.y |= by << (8 * (e - 4));
-                }
+            return src + (long long)yy * pitch;
+        };
+        if (__all(fast)) {   // wave-uniform: interior pairs only (keeps the edge code out of this path)
+            for (int rr = rr0; rr < FB_TH + 8; rr += 15) {
+                uint2 v;
+                __builtin_memcpy(&v, row_of(rr) + xs, 8);
+                *(uint2 *)&tin[rr * FB_LD + 2 * jj] = v;
             }
-            *(uint2 *)&tin[rr * FB_LD + 2 * jj] = v;
+        } else {
+            for (int rr = rr0; rr < FB_TH + 8; rr += 15) {
+                const uint8_t *rowp = row_of(rr);
+                uint2 v;
+                if (fast) {
+                    __builtin_memcpy(&v, rowp + xs, 8);
+                } else {
+                    v.x = v.y = 0;
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        int xx = xs + e;
+                        xx = xx < 0 ? -xx : xx;
+                        xx = xx >= w ? 2 * w - 2 - xx : xx;
+                        const uint32_t by = rowp[xx];
+                        if (e < 4) v.x |= by << (8 * e); else v.y |= by << (8 * (e - 4));
+                    }
+                }
+                *(uint2 *)&tin[rr * FB_LD + 2 * jj] = v;
+            }
         }
     }
     static_assert(FB_NG % 4 == 0 && FB_NG / 4 <= 256, "score tile cleared as one uint4 per thread");
