@@ -29,7 +29,7 @@ for s in $STEPS; do
     pmc)
       cd /tmp && export TMPDIR=/tmp
       for ctr in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU; do
-        timeout -k 10 600 rocprofv3 --kernel-trace --pmc $ctr -d "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-profile ${BENCH_ARGS:-} > /dev/null 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.err"
+        timeout -k 10 600 rocprofv3 --kernel-trace --pmc $ctr -d "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-profile ${PMC_ARGS:---no-lba --no-rgbd --no-track --no-pose --no-bow --no-bowmatch --no-newpts --no-e2e --no-latency} > /dev/null 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.err"
         rc=$?; echo "pmc $ctr rc=$rc" | tee -a "$GRAFT_REPO_ROOT/$OUT/session.log"; [ $rc -eq 0 ] || exit $rc
       done
       cd "$GRAFT_REPO_ROOT" ;;
