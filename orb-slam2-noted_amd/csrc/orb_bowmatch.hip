@@ -19,6 +19,7 @@
 #include <cstring>
 #include <vector>
 
+#include "orb_device.h"
 #include "orb_engine.h"
 #include "orbslam2_amd.h"
 
@@ -67,12 +68,6 @@ struct Work {
     int *pairs;        // [S][cap][2]
 };
 
-__device__ inline int hamming32(const uint8_t *a, const uint8_t *b) {
-    const uint4 *pa = (const uint4 *)a, *pb = (const uint4 *)b;
-    const uint4 x0 = pa[0], x1 = pa[1], y0 = pb[0], y1 = pb[1];
-    return __popc(x0.x ^ y0.x) + __popc(x0.y ^ y0.y) + __popc(x0.z ^ y0.z) + __popc(x0.w ^ y0.w) +
-           __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
-}
 
 __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

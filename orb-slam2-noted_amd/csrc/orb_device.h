@@ -16,6 +16,15 @@ namespace orbamd {
 
 __device__ __forceinline__ int cv_round_f(float v) { return (int)__builtin_rintf(v); }
 
+// ORBmatcher::DescriptorDistance (ORBmatcher.cc:2123-2143): popcount of the XOR of two 32-byte
+// descriptors (rows 16-byte aligned), as two 16-byte loads per side
+__device__ __forceinline__ int hamming32(const uint8_t *a, const uint8_t *b) {
+    const uint4 *pa = (const uint4 *)a, *pb = (const uint4 *)b;
+    const uint4 x0 = pa[0], x1 = pa[1], y0 = pb[0], y1 = pb[1];
+    return __popc(x0.x ^ y0.x) + __popc(x0.y ^ y0.y) + __popc(x0.z ^ y0.z) + __popc(x0.w ^ y0.w) +
+           __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
+}
+
 // XCD-aware workgroup remap (cdna_hip_programming.md §5.5 T1, bijective form). Workgroups are
 // dealt round-robin over the 8 XCDs (each with a private L2); remapping the linear id so every
 // XCD works one contiguous range of the grid keeps an image's pyramid / blurred pixels in one

@@ -64,12 +64,6 @@ __device__ __forceinline__ const uint8_t *side_level(const ExtractGeom &g, const
     return s.pyr + (long long)img * g.pyr_stride + g.pyr_off[l];
 }
 
-__device__ __forceinline__ int hamming32(const uint8_t *a, const uint8_t *b) {
-    const uint4 *pa = (const uint4 *)a, *pb = (const uint4 *)b;
-    const uint4 x0 = pa[0], x1 = pa[1], y0 = pb[0], y1 = pb[1];
-    return __popc(x0.x ^ y0.x) + __popc(x0.y ^ y0.y) + __popc(x0.z ^ y0.z) + __popc(x0.w ^ y0.w) +
-           __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
-}
 
 // ---- S1: right keypoints of each pair in (y, index) order, as 16-byte records
 // The scan of S2 reads one 16-byte record per right keypoint in y order: {y, x (float bits),
