@@ -259,7 +259,9 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 #define FB_LD (FB_LW / 4)   // LDS tile row stride in dwords
 #define FB_MR (FB_TH + 2)   // score rows y0-1 .. y0+16 (tile + NMS ring)
 #define FB_NG (FB_MR * FB_LD)   // score tile dwords (a multiple of 4, <= 1024: cleared as uint4 by 256 threads)
-#define FB_CCAP (FB_MR * (FB_TW + 2) + 64)   // candidate slots: every score pixel + one chunk of hot-list slack
+#define FB_CCAP (FB_MR * (FB_TW + 2))   // candidate slots: every score pixel
+#define FB_HCAP (((FB_CCAP + 255) / 256) * 64)   // hot entries per wavefront (<= the candidates it scores)
+#define FB_INTILE 0x8000   // candidate flag: a tile pixel (not the NMS ring)
 
 __device__ __forceinline__ int refl101(int i, int n) {
     if (n == 1) return 0;
@@ -396,7 +398,8 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
                                                         uint8_t *blur, int *cell_cnt, uint32_t *cell_keys) {
     __shared__ __align__(16) uint32_t tin[(FB_TH + 8) * FB_LD];
     __shared__ __align__(16) uint32_t mt[FB_NG];   // exact M bytes, (mrow, x - x0 + 4)
-    __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets)
+    __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets | FB_INTILE)
+    __shared__ uint16_t hlist[4][FB_HCAP];   // per-wavefront hot pixels (score-tile byte offsets)
     __shared__ uint16_t bboth[4][128];     // per-wavefront queue of dual-polarity candidates
     __shared__ int ncand_sh, hcount[4];
     const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
@@ -487,7 +490,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         };
         // candidates among the 8 pixels xb .. xb+7 of score row mrow (xb = x0 + 4 d): LDS dwords
         // d .. d+3 of the centre row (cols xb-4 .. xb+11), d+1 and d+2 of the rows 3 above / below
-        auto prefilter8 = [&](int mrow, int d, bool active) {
+        auto prefilter8 = [&](int mrow, int d, bool active, uint32_t tflag) {
             const int y = y0 - 1 + mrow, xb = x0 + 4 * d;
             uint32_t cA = 0, cB = 0;   // top bit of byte i: pixel xb+i (cA), xb+4+i (cB)
             if (active && y >= dy0 && y < dy1 && xb + 7 >= dx0 && xb < dx1) {
@@ -521,16 +524,16 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             int base = 0;
             if (lane == 0) base = atomicAdd(&ncand_sh, tot8);
             base = __builtin_amdgcn_readfirstlane(base) + inc - cnt;
-            for (uint32_t mm = m; mm; mm &= mm - 1) clist[base++] = (uint16_t)(pos0 + __builtin_ctz(mm));
+            for (uint32_t mm = m; mm; mm &= mm - 1) clist[base++] = (uint16_t)((pos0 + __builtin_ctz(mm)) | tflag);
         };
         const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;   // pixels (y0 + r, x0 + cb + i)
 #ifndef FB_SKIP_PRE   // instruction-count experiments (make variant VDEFS=-DFB_SKIP_...)
         if (y0 + 4 * wv + 3 >= dy0 && y0 + 4 * wv < dy1)   // wave-uniform: 4 tile rows per wavefront
-            prefilter8(r + 1, cb >> 2, true);
+            prefilter8(r + 1, cb >> 2, true, FB_INTILE);
         if (wv == 2) {   // ring rows: lanes 0..16 row y0-1, lanes 17..33 row y0+16
             const int hr = lane >= 17, j = lane - 17 * hr;
             if ((y0 - 1 >= dy0 && y0 - 1 < dy1) || (y0 + FB_TH >= dy0 && y0 + FB_TH < dy1))
-                prefilter8(hr ? FB_TH + 1 : 0, 2 * j - 1, lane < 34);
+                prefilter8(hr ? FB_TH + 1 : 0, 2 * j - 1, lane < 34, 0u);
         }
         if (wv == 3) {   // ring columns: lane -> (row y0 + (lane & 15), column x0-1 or x0+128)
             const int y = y0 + (lane & 15), x = lane < 16 ? x0 - 1 : x0 + FB_TW;
@@ -552,8 +555,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
 #endif
     __syncthreads();
     // 3. exact M of the pooled candidates: wavefront wv takes chunks wv, wv + 4, ... of 64; its
-    // hot pixels (tile pixels with M > tlo) go into the slots of chunks it has already consumed
-    // (hot entry n -> slot 64 (wv + 4 (n / 64)) + n % 64)
+    // hot pixels (tile pixels with M > tlo) go to its hot list
 #ifdef FB_SKIP_EXACT
     const int tot = 0;
 #else
@@ -573,38 +575,33 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             for (int k = 0; k < 16; k++) rg[k] = pc[RY[k] * FB_LW + RX[k]];
             return (int)pc[0];
         };
+        uint16_t *hl = hlist[wv];
         auto push_hot = [&](bool hot, int pos) {
             const unsigned long long bal = __ballot(hot);
-            if (hot) {
-                const int n = nh + (int)lane_rank(bal);
-                clist[64 * (wv + 4 * (n >> 6)) + (n & 63)] = (uint16_t)pos;
-            }
+            if (hot) hl[nh + (int)lane_rank(bal)] = (uint16_t)pos;
             nh += __popcll(bal);
-        };
-        auto in_tile = [&](int pos) {
-            const int mrow = pos / FB_LW, col = pos - mrow * FB_LW;
-            return mrow >= 1 && mrow <= FB_TH && col >= 4 && col < FB_TW + 4;
         };
         // the brighter score of queued candidates whose darker score is already in the tile
         auto drain = [&](int n) {
             const bool act = lane < n;
-            const int pos = act ? bb[lane] : 0;
+            const int e = act ? bb[lane] : 0, pos = e & (FB_INTILE - 1);
             bool hot = false;
             if (act) {
                 int rg[16];
                 const int v = ring(pos, rg);
                 const int Mv = max((int)m8[pos], fast_arc_score(rg, -v, 0));
                 m8[pos] = (uint8_t)Mv;
-                hot = Mv > tlo && in_tile(pos);
+                hot = Mv > tlo && (e & FB_INTILE);
             }
             push_hot(hot, pos);
         };
         for (int base = 64 * wv; base < tot; base += 256) {
             const int q = base + lane;
             bool hot = false, both = false;
-            int pos = 0;
+            int pos = 0, e = 0;
             if (q < tot) {
-                pos = clist[q];
+                e = clist[q];
+                pos = e & (FB_INTILE - 1);
                 int rg[16];
                 const int v = ring(pos, rg);
                 // polarity of the compass bound (step 2); candidates of both polarities (up to
@@ -614,11 +611,11 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
                 const int Mv = fast_arc_score(rg, pd ? v + 1 : -v, pd ? -1 : 0);
                 m8[pos] = (uint8_t)Mv;
                 both = pd && pb;
-                hot = !both && Mv > tlo && in_tile(pos);
+                hot = !both && Mv > tlo && (e & FB_INTILE);
             }
             push_hot(hot, pos);
             const unsigned long long bbal = __ballot(both);
-            if (both) bb[nb + lane_rank(bbal)] = (uint16_t)pos;
+            if (both) bb[nb + lane_rank(bbal)] = (uint16_t)e;
             nb += __popcll(bbal);
             if (nb >= 64) {
                 drain(64);
@@ -646,7 +643,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             hb = q >= h2 ? h2 : hb;
             hb = q >= h3 ? h3 : hb;
             const int n = q - hb;
-            const int pos = clist[64 * (ow + 4 * (n >> 6)) + (n & 63)];
+            const int pos = hlist[ow][n];
             const int mrow = pos / FB_LW, col = pos - mrow * FB_LW;
             const int y = y0 - 1 + mrow, x = x0 - 4 + col;
             // cell of (x, y): (v - 19) / cell side by a 20-bit reciprocal (exact for v < 2^20 / side)
