@@ -352,7 +352,7 @@ __device__ __forceinline__ uint32_t gather_byte(uint32_t a0, uint32_t a1, uint32
 __device__ __forceinline__ long i8x8(uint32_t lo, uint32_t hi) { return (long)((unsigned long long)hi << 32 | lo); }
 
 __device__ __forceinline__ void fast_blur_mfma(const uint32_t *tin, uint8_t *dst, int bp, int x0, int y0, int w,
-                                               int h, int wv, int lane) {
+                                               int h, int xb0, int xb1, int lane) {
     const int n = lane & 15, gq = lane >> 4;
     const long WB = (long)c_fbblur.wb[lane], VB = (long)c_fbblur.vb[lane];
     const uint8_t *t8 = (const uint8_t *)tin;
@@ -364,8 +364,7 @@ __device__ __forceinline__ void fast_blur_mfma(const uint32_t *tin, uint8_t *dst
     const int KH = 128 * 257 + 128;
     const i32x4 z = {0, 0, 0, 0}, kh = {KH, KH, KH, KH};
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const int xb = 2 * wv + q;
+    for (int xb = xb0; xb < xb1; xb++) {   // wave-uniform range of 16-column blocks
         const int c = 16 * xb + 8 * gq;
         const uint2 a0 = *(const uint2 *)(t8 + r0 * FB_LW + c);
         const uint2 a1 = *(const uint2 *)(t8 + r1 * FB_LW + c);
@@ -548,10 +547,15 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         }
 #endif
     }
-    // 4. GaussianBlur on the matrix cores: wavefront wv writes output columns 32 wv .. 32 wv + 31
-    // (two 16-column blocks) x the tile's 16 rows (fast_blur_mfma)
+    // 4. GaussianBlur on the matrix cores (fast_blur_mfma): 16-column blocks 0-2 on wavefront 0,
+    // 3-5 on wavefront 1, 6-7 on wavefront 3, x the tile's 16 rows
 #ifndef FB_SKIP_BLUR
-    fast_blur_mfma(tin, blur + (long long)b * g.blur_stride + g.blur_off[l], g.bp[l], x0, y0, w, h, wv, lane);
+    {
+        // column blocks per wavefront balance the pre-filter's extra work: wavefront 2 scores
+        // the ring rows (one more 8-pixel group per lane), wavefront 3 the ring columns
+        const int xb0 = wv == 0 ? 0 : wv == 1 ? 3 : 6, xb1 = wv == 0 ? 3 : wv == 1 ? 6 : wv == 2 ? 6 : 8;
+        fast_blur_mfma(tin, blur + (long long)b * g.blur_stride + g.blur_off[l], g.bp[l], x0, y0, w, h, xb0, xb1, lane);
+    }
 #endif
     __syncthreads();
     // 3. exact M of the pooled candidates: wavefront wv takes chunks wv, wv + 4, ... of 64; its
