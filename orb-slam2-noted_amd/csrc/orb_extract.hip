@@ -232,21 +232,22 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 // there as the reference list position (cell row-major, then row-major in the cell).
 //
 // The LDS halo tile (24x136 bytes, reflect-101 at the level edges) feeds:
-//  1. staging: aligned dword loads + v_alignbyte (per-byte reflection only at edges);
+//  1. staging: one unaligned dwordx2 load per 8-byte pair (per-byte reflection only for the
+//     pairs crossing a level edge, behind a wave-uniform branch);
 //  2. FAST pre-filter over the tile plus its one-pixel ring (the NMS neighbours): every
 //     9-arc holds two adjacent compass pixels (ring 0/4/8/12), so a pixel is a darker
-//     (brighter) candidate only if the sign-bit test below passes for an adjacent compass
-//     pair; packed int16 pairs, 4-pixel groups. Candidates (~12 % of the pixels of textured
-//     imagery, ~1.4 % are corners) join a per-wavefront list with their polarity flags;
-//  3. exact M per candidate: one 9-arc score (v_mad_i32_i24 signs the differences, so the
-//     darker and brighter scores run the same instructions; the ~0.4 % candidates of
-//     both polarities run it twice) into an LDS score tile (0 elsewhere: every M <= tlo
-//     behaves as 0). Tile pixels with M > tlo go to a hot list written into the
-//     wavefront's already consumed candidate slots;
+//     (brighter) candidate only if an adjacent compass pair passes the halved-difference test
+//     (SWAR on v_lerp_u8, four pixels per dword). Candidates (~20 % of the detection area,
+//     ~5 % score above tlo) are pooled per workgroup (DPP scan of the lanes' counts), flagged
+//     FB_INTILE when they are tile pixels;
+//  3. exact M per candidate: one 9-arc score for the polarity the compass test allows
+//     (v_xad signs the differences, v_min3 / v_max3 reduce the arcs; the candidates of both
+//     polarities get their brighter score in a queued pass) into an LDS score tile (0
+//     elsewhere: every M <= tlo behaves as 0). Tile pixels with M > tlo go to the wavefront's
+//     hot list;
 //  4. GaussianBlur 9x9 sigma 2 (bit-exact fixed-point path, SURVEY.md A.3 -- exact integer
-//     row sums, Q16 column sums, (acc + 2^15) >> 16): row pass with v_dot4_u32_u8 on byte
-//     quads, stored vertically pair-interleaved (rows 2p, 2p+1 in one dword) so the column
-//     pass runs on v_dot2_u32_u16; written with dword stores at the row pitch g.bp[l];
+//     row sums, Q16 column sums, (acc + 2^15) >> 16) as banded int8 products on the matrix
+//     cores (fast_blur_mfma), written with dword stores at the row pitch g.bp[l];
 //  5. NMS of the hot pixels against their in-cell neighbours and the atomic emission of
 //     the survivors' keys (pack_key: x, y relative to minBorder, score M - 1).
 // No strength map leaves the workgroup.
