@@ -175,26 +175,28 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
         const uint8_t *dL = a.L.desc + ((long long)imgL * a.cap + iL) * 32;
         const uint8_t *dR = a.R.desc + (long long)imgR * a.cap * 32;
         unsigned best = 0xFFFFFFFFu;
-        for (int base = lo; base < nR; base += 64) {
-            const int c = base + lane;
-            bool stop = false;
-            if (c < nR) {
-                const uint4 e = srt[c];
+        // two candidates per lane per pass (their record and descriptor loads in flight
+        // together: one dependent round trip per 128 candidates of the band)
+        for (int base = lo; base < nR; base += 128) {
+            const int c0 = base + lane, c1 = c0 + 64;
+            const uint4 e0 = c0 < nR ? srt[c0] : make_uint4(0x7f800000u, 0u, 0u, 0u);   // +inf y: past the band
+            const uint4 e1 = c1 < nR ? srt[c1] : make_uint4(0x7f800000u, 0u, 0u, 0u);
+            auto take = [&](const uint4 &e) {
                 const float ky = __uint_as_float(e.x);
-                if (ky > yhi) stop = true;
-                else {
-                    const int iR = (int)(e.w & 0xFFFFu), oct = (int)(e.w >> 16);
-                    const float kx = __uint_as_float(e.y);
-                    const int minr = (int)(int16_t)(e.z & 0xFFFFu), maxr = (int)(int16_t)(e.z >> 16);
-                    if (row >= minr && row <= maxr && oct >= levelL - 1 && oct <= levelL + 1 &&
-                        kx >= minU && kx <= maxU) {
-                        const int dist = hamming32(dL, dR + (long long)iR * 32);
-                        const unsigned key = ((unsigned)dist << 16) | (unsigned)iR;
-                        best = min(best, key);
-                    }
-                }
-            }
-            if (__any(stop)) break;
+                const int oct = (int)(e.w >> 16);
+                const float kx = __uint_as_float(e.y);
+                const int minr = (int)(int16_t)(e.z & 0xFFFFu), maxr = (int)(int16_t)(e.z >> 16);
+                return ky <= yhi && row >= minr && row <= maxr && oct >= levelL - 1 && oct <= levelL + 1 && kx >= minU &&
+                       kx <= maxU;
+            };
+            const bool t0 = take(e0), t1 = take(e1);
+            const int i0 = (int)(e0.w & 0xFFFFu), i1 = (int)(e1.w & 0xFFFFu);
+            const int d0 = t0 ? hamming32(dL, dR + (long long)i0 * 32) : 0;
+            const int d1 = t1 ? hamming32(dL, dR + (long long)i1 * 32) : 0;
+            if (t0) best = min(best, ((unsigned)d0 << 16) | (unsigned)i0);
+            if (t1) best = min(best, ((unsigned)d1 << 16) | (unsigned)i1);
+            // sorted by y: a record past yhi ends the band (ky > yhi, or c >= nR read as +inf)
+            if (__any(__uint_as_float(e1.x) > yhi)) break;
         }
         // (dist, index) minimum over the wavefront once, after the scan (DPP row mins, then rows)
         best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x111, 0xF, 0xF, false));
