@@ -793,6 +793,37 @@ __device__ void block_sort_desc(unsigned long long *a, int n) {
     }
 }
 
+// descending order of n distinct u64 values by rank counting: src[i] goes to
+// dst[#{j : src[j] > src[i]}]. Every lane of a wavefront reads the same src[j], so with src
+// in LDS each read is a broadcast and the whole sort is one dependent pass (the bitonic
+// network's 45 barrier-separated stages at n = 512 are latency bound). Two elements per
+// thread share each read, and sixteen reads (eight ds_read_b128) are in flight per step:
+// src is 16-byte aligned and zero-padded to a multiple of 16 (zeros never outrank a value).
+// Ends with a workgroup barrier.
+__device__ void block_rank_sort_desc(const unsigned long long *src, unsigned long long *dst, int n) {
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    const u64x2 *s2 = (const u64x2 *)src;
+    const int n16 = (n + 15) >> 4;
+    for (int i = threadIdx.x; i < n; i += 2 * ORBX_QT_THREADS) {
+        const int i2 = i + ORBX_QT_THREADS;
+        const unsigned long long v = src[i], w = i2 < n ? src[i2] : ~0ull;
+        int r = 0, r2 = 0;
+        for (int j = 0; j < n16; j++) {
+            u64x2 u[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) u[k] = s2[8 * j + k];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                r += (u[k].x > v) + (u[k].y > v);
+                r2 += (u[k].x > w) + (u[k].y > w);
+            }
+        }
+        dst[r] = v;
+        if (i2 < n) dst[r2] = w;
+    }
+    __syncthreads();
+}
+
 // Quadtree working set of one (image, level)
 struct QT {
     QNode *cur, *nxt;
@@ -1228,9 +1259,18 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     }
     QT_MARK(5);
     const int nout = min(S.n_out, NP);
-    for (int i = nout + tid; i < NP; i += ORBX_QT_THREADS) Q.outrec[i] = 0;
-    __syncthreads();
-    block_sort_desc(Q.outrec, NP);
+    if (12 * g.qt_kl >= 8 * ((nout + 15) & ~15)) {
+        // the output records are distinct (one per key): stage them in the key area of LDS,
+        // free after step 5, and rank-sort them back into outrec
+        unsigned long long *stage = (unsigned long long *)lds;
+        for (int i = tid; i < ((nout + 15) & ~15); i += ORBX_QT_THREADS) stage[i] = i < nout ? Q.outrec[i] : 0ull;
+        __syncthreads();
+        block_rank_sort_desc(stage, Q.outrec, nout);
+    } else {
+        for (int i = nout + tid; i < NP; i += ORBX_QT_THREADS) Q.outrec[i] = 0;
+        __syncthreads();
+        block_sort_desc(Q.outrec, NP);
+    }
     QT_MARK(6);
     const int ncap = min(nout, g.out_cap[l]);
     uint32_t *dst = sel + (long long)b * g.out_base[g.nlevels] + g.out_base[l];
