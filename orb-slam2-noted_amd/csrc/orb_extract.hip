@@ -1178,19 +1178,28 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         while (!done) {
             const int prev = S.live, na = S.n_act;
             const QCnt base = qt_prefix(S, Q, par);
+            // distinct keys (n, id, position): rank-sorted from an LDS stage -- the other key
+            // buffer, free until qt_move, or the whole key area when the keys live in global
+            // scratch -- into sortbuf; the bitonic network over sortbuf when neither fits
+            const int na16 = (na + 15) & ~15;
+            const bool keys_lds = M <= g.qt_kl;
+            const bool rank = na16 <= (keys_lds ? g.qt_kl / 2 : 12 * g.qt_kl / 8);
+            unsigned long long *stage = rank ? (keys_lds ? (unsigned long long *)Q.keys(Q.src ^ 1) : (unsigned long long *)lds) : Q.sortbuf;
             int np2 = 1;
             while (np2 < na) np2 <<= 1;
-            for (int i = tid; i < np2; i += ORBX_QT_THREADS) {
+            const int nfill = rank ? na16 : np2;
+            for (int i = tid; i < nfill; i += ORBX_QT_THREADS) {
                 unsigned long long v = 0;
                 if (i < na) {
                     const QNode &q = Q.cur[i];
                     v = ((unsigned long long)(uint32_t)q.n << 40) | ((unsigned long long)(uint32_t)(q.id & 0xFFFFFF) << 16) | (unsigned)i;
                 }
-                Q.sortbuf[i] = v;
+                stage[i] = v;
             }
             if (tid == 0) S.cross = na;
             __syncthreads();
-            block_sort_desc(Q.sortbuf, np2);
+            if (rank) block_rank_sort_desc(stage, Q.sortbuf, na);
+            else block_sort_desc(Q.sortbuf, np2);
             // first sorted position whose split brings the size to >= N
             {
                 const int Rn = (na + ORBX_QT_THREADS - 1) / ORBX_QT_THREADS;
