@@ -427,11 +427,13 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             return src + (long long)yy * pitch;
         };
         if (__all(fast)) {   // wave-uniform: interior pairs only (keeps the edge code out of this path)
-            for (int rr = rr0; rr < FB_TH + 8; rr += 15) {
-                uint2 v;
-                __builtin_memcpy(&v, row_of(rr) + xs, 8);
-                *(uint2 *)&tin[rr * FB_LD + 2 * jj] = v;
-            }
+            // both rows' loads in flight before either LDS write (one global round trip)
+            const bool two = rr0 + 15 < FB_TH + 8;
+            uint2 v0, v1 = make_uint2(0u, 0u);
+            __builtin_memcpy(&v0, row_of(rr0) + xs, 8);
+            if (two) __builtin_memcpy(&v1, row_of(rr0 + 15) + xs, 8);
+            *(uint2 *)&tin[rr0 * FB_LD + 2 * jj] = v0;
+            if (two) *(uint2 *)&tin[(rr0 + 15) * FB_LD + 2 * jj] = v1;
         } else {
             for (int rr = rr0; rr < FB_TH + 8; rr += 15) {
                 const uint8_t *rowp = row_of(rr);
