@@ -27,6 +27,17 @@ from pathlib import Path
 
 import numpy as np
 
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (HIP's default 4). The
+# host-batch leg runs 2 engine streams + an H2D and a D2H copy stream next to torch's stream;
+# with 4 queues copy streams share a queue with an engine, and the copies wait behind its
+# kernels (value_e2e 48.9k -> 58.1k stereo frames/s with 8 queues). Must be set
+# before the HIP runtime initialises; raised to at least 8 (a larger setting is kept).
+try:
+    _hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+except ValueError:
+    _hwq = 4
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(_hwq, 8))
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "orb-slam2-noted_amd" / "python"))
 
@@ -179,7 +190,7 @@ def bench_e2e(amd, args, pool, bf, mb):
                 L, R = np.roll(L, 7 * k, axis=1), np.roll(R, 7 * k, axis=1)
             a[2 * i], a[2 * i + 1] = L, R
         ins.append(a)
-    pl = amd.StereoPipeline(NFEAT, n_engines=args.engines)
+    pl = amd.StereoPipeline(NFEAT, n_engines=args.e2e_engines)
     pl.reserve(W, H, B)
     cap = pl.capacity()
     outs = [amd.StereoHostBatch(B, cap) for _ in range(2)]
@@ -203,6 +214,7 @@ def bench_e2e(amd, args, pool, bf, mb):
     pl.close()
     return {"value_e2e": round(B * args.steps / dt, 2),
             "e2e": {"ms_per_step": round(1000 * dt / args.steps, 4), "stereo_frames_per_step": B,
+                    "pipeline_engines": args.e2e_engines, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                     "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
                     "pcie_gbs": round((h2d + d2h) * args.steps / dt / 1e9, 2),
                     "note": "page-locked host images in, host keypoints / descriptors / mvuRight / mvDepth out; "
@@ -734,6 +746,9 @@ def main():
     ap.add_argument("--engines", type=int, default=3,
                     help="pipeline engines (HIP streams) the batch is split over (orbx_pipeline_*; "
                          "tools/pipeline_exp.py: 1 x 384 49.1k, 2 x 192 51.8k, 3 x 128 54.2k stereo fps)")
+    ap.add_argument("--e2e-engines", type=int, default=2,
+                    help="pipeline engines of the host-batch (value_e2e) leg (tools/e2e_queues.sh, 8 HW "
+                         "queues: 2 engines 57.8k, 3 engines 53.0k stereo fps)")
     ap.add_argument("--pool", type=int, default=8, help="distinct synthetic stereo pairs")
     ap.add_argument("--bufs", type=int, default=4, help="rotating resident input batches")
     ap.add_argument("--cpu-frames", type=int, default=96)
