@@ -738,16 +738,27 @@ struct QShared {
 
 // block-wide exclusive scan of one value per thread; two LDS slots alternate so
 // back-to-back scans need one barrier each
-__device__ __forceinline__ unsigned long long shfl_up64(unsigned long long v, int off) { return __shfl_up(v, off, 64); }
+
+// inclusive wavefront scan of u32 on DPP (row_shr 1/2/4/8, then row_bcast 15 / 31)
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
 
 __device__ __forceinline__ QCnt block_scan(QShared &S, QCnt v, QCnt *total, int &par) {
     const int lane = threadIdx.x & 63, wv = wave_id();
-    QCnt incl = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const QCnt t{shfl_up64(incl.a, off), shfl_up64(incl.b, off)};
-        if (lane >= off) incl += t;
-    }
+    // the four u32 counters scan independently (their sums stay below 2^32: no carries
+    // between the packed fields), on DPP instead of LDS permutes
+    auto sc64 = [](unsigned long long x) {
+        return (unsigned long long)wave_incl_scan_u32((uint32_t)x) |
+               (unsigned long long)wave_incl_scan_u32((uint32_t)(x >> 32)) << 32;
+    };
+    const QCnt incl{sc64(v.a), sc64(v.b)};
     if (lane == 63) S.wsum[par][wv] = incl;
     __syncthreads();
     QCnt base{0ull, 0ull}, tot{0ull, 0ull};
