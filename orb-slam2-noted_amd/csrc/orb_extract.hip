@@ -612,12 +612,14 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
                 int rg[16];
                 const int v = ring(pos, rg);
                 // polarity of the compass bound (step 2); candidates of both polarities (up to
-                // ~18 % on the noisier levels) get their brighter score in a queued pass
+                // ~18 % on the noisier levels) get their brighter score in a queued pass unless
+                // the darker one already exceeds tlo: a darker 9-arc above tlo meets every
+                // brighter 9-arc (9 + 9 > 16), so the brighter score is then 0
                 const bool pd = v - max(min(rg[0], rg[8]), min(rg[4], rg[12])) >= t1;
                 const bool pb = min(max(rg[0], rg[8]), max(rg[4], rg[12])) - v >= t1;
                 const int Mv = fast_arc_score(rg, pd ? v + 1 : -v, pd ? -1 : 0);
                 m8[pos] = (uint8_t)Mv;
-                both = pd && pb;
+                both = pd && pb && Mv <= tlo;
                 hot = !both && Mv > tlo && (e & FB_INTILE);
             }
             push_hot(hot, pos);
