@@ -58,6 +58,21 @@ def test_extract_noise_many_candidates(amd, oracle_mod):
     _assert_same_kps(ex(img), ref.extract(img), "noise")
 
 
+@pytest.mark.parametrize("env", [{"ORBX_QT_LDS_KB": "16"}, {"ORBX_QT_LDS_KB": "160"},
+                                 {"ORBX_QT_NODES_LDS": "1", "ORBX_QT_LDS_KB": "96"}])
+def test_extract_quadtree_layouts(amd, oracle_mod, monkeypatch, env):
+    """The quadtree's memory layouts (read when an engine sizes its geometry): keys in global
+    scratch for levels above a 16 KB LDS budget, every level in LDS at 160 KB, node arrays in LDS;
+    each with its rank-sort stage (the idle key buffer, or the key area) -- all bit-exact."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(8)
+    for img in (synth.textured_image(376, 1241, 31), rng.integers(0, 256, size=(376, 1241), dtype=np.uint8)):
+        ex = amd.ORBextractor(2000, 1.2, 8, 20, 7)
+        ref = oracle_mod.Extractor(2000, 1.2, 8, 20, 7)
+        _assert_same_kps(ex(img), ref.extract(img), str(env))
+
+
 def test_extract_flat_and_sparse(amd, oracle_mod):
     """Flat image: every cell retries at minThFAST and finds nothing -> 0 keypoints.
     Sparse image: a few isolated corners (tiny quadtree, size-1 roots)."""
