@@ -472,23 +472,31 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         const int dx0 = max(19, x0 - 1), dx1 = min(w - 19, x0 + FB_TW + 1);
         const int dy0 = max(19, y0 - 1), dy1 = min(h - 19, y0 + FB_TH + 1);
         // Compass bound on four pixels per dword (SWAR on v_lerp_u8, which adds two bytes and a
-        // rounding bit and halves, per byte): u = lerp(c, ~r, 1) = 128 + floor((c - r) / 2), so
-        // c - r >= T (T = tlo + 1) implies u >= 128 + floor(T / 2) (equivalent for even T), and
-        // lerp(u, ~K, 1) has its top bit set iff u >= K. Darker pass at compass pixel r:
-        // c - r >= T; brighter: r - c >= T. A pixel is a candidate iff (N or S) and (E or W)
-        // pass for one polarity (every 9-arc holds two adjacent compass pixels). The bound is
-        // only ever looser than the exact test, never tighter.
+        // rounding bit and halves, per byte): lerp(u, ~K, 1) has its top bit set iff u >= K.
+        // Darker pass at compass pixel r: c - r >= T (T = tlo + 1); brighter: r - c >= T. A
+        // pixel is a candidate iff (N or S) and (E or W) pass for one polarity (every 9-arc
+        // holds two adjacent compass pixels). The bound is only ever looser than the exact
+        // test, never tighter.
+        // One halved difference per compass pixel serves both polarities:
+        // u = lerp(r, ~c, 1) = 128 + floor((r - c) / 2); brighter (r - c >= T) implies u >= KB =
+        // 128 + floor(T / 2), darker (c - r >= T) implies u <= 128 - ceil(T / 2), i.e. NOT
+        // u >= KD = 129 - ceil(T / 2) -- so the darker pass of a direction pair is the complement
+        // of "both fail", and one NOT serves the four directions.
         const uint32_t ONE = 0x01010101u, HI = 0x80808080u;
-        const uint32_t NK = ~((uint32_t)min(128 + ((tlo + 1) >> 1), 255) * ONE);
+        const int T = tlo + 1;
+        const uint32_t NKB = ~((uint32_t)min(128 + (T >> 1), 255) * ONE);
+        const uint32_t NKD = ~((uint32_t)(129 - ((T + 1) >> 1)) * ONE);
         auto swar4 = [&](uint32_t C, uint32_t Cm, uint32_t Cp, uint32_t N, uint32_t S) {
             const uint32_t W = __builtin_amdgcn_alignbyte(C, Cm, 1);   // cols -3 .. 0
             const uint32_t E = __builtin_amdgcn_alignbyte(Cp, C, 3);   // cols +3 .. +6
             const uint32_t NC = ~C;
-            auto dk = [&](uint32_t r) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(C, ~r, ONE), NK, ONE); };
-            auto bk = [&](uint32_t r) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(r, NC, ONE), NK, ONE); };
-            const uint32_t dark = (dk(N) | dk(S)) & (dk(E) | dk(W));
-            const uint32_t bright = (bk(N) | bk(S)) & (bk(E) | bk(W));
-            return (dark | bright) & HI;
+            const uint32_t uN = __builtin_amdgcn_lerp(N, NC, ONE), uS = __builtin_amdgcn_lerp(S, NC, ONE);
+            const uint32_t uE = __builtin_amdgcn_lerp(E, NC, ONE), uW = __builtin_amdgcn_lerp(W, NC, ONE);
+            auto bk = [&](uint32_t u) { return __builtin_amdgcn_lerp(u, NKB, ONE); };   // top bit: u >= KB
+            auto df = [&](uint32_t u) { return __builtin_amdgcn_lerp(u, NKD, ONE); };   // top bit: u >= KD
+            const uint32_t bright = (bk(uN) | bk(uS)) & (bk(uE) | bk(uW));
+            const uint32_t dark_fail = (df(uN) & df(uS)) | (df(uE) & df(uW));
+            return (bright | ~dark_fail) & HI;
         };
         // candidates among the 8 pixels xb .. xb+7 of score row mrow (xb = x0 + 4 d): LDS dwords
         // d .. d+3 of the centre row (cols xb-4 .. xb+11), d+1 and d+2 of the rows 3 above / below
