@@ -510,10 +510,12 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
                 const uint32_t *rn = row - 3 * FB_LD, *rs = row + 3 * FB_LD;
                 cA = swar4(C1, C0, C2, ld(rn, d + 1), ld(rs, d + 1));
                 cB = swar4(C2, C1, C3, ld(rn, d + 2), ld(rs, d + 2));
-                const int lo = max(dx0 - xb, 0), hi = min(dx1 - xb, 8);   // valid pixels [lo, hi)
-                const unsigned long long vm = hi > lo ? (~0ull << (8 * lo)) & (~0ull >> (64 - 8 * hi)) : 0ull;
-                cA &= (uint32_t)vm;
-                cB &= (uint32_t)(vm >> 32);
+                if (xb < dx0 || xb + 8 > dx1) {   // only the lanes at the detection region's edge
+                    const int lo = max(dx0 - xb, 0), hi = min(dx1 - xb, 8);   // valid pixels [lo, hi)
+                    const unsigned long long vm = hi > lo ? (~0ull << (8 * lo)) & (~0ull >> (64 - 8 * hi)) : 0ull;
+                    cA &= (uint32_t)vm;
+                    cB &= (uint32_t)(vm >> 32);
+                }
             }
             // compaction into the pooled list: the lane's 8 candidate bits (v_dot4 gathers the
             // byte top bits), an inclusive DPP scan of their counts over the wavefront, one LDS
