@@ -500,12 +500,14 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         };
         // candidates among the 8 pixels xb .. xb+7 of score row mrow (xb = x0 + 4 d): LDS dwords
         // d .. d+3 of the centre row (cols xb-4 .. xb+11), d+1 and d+2 of the rows 3 above / below
-        auto prefilter8 = [&](int mrow, int d, bool active, uint32_t tflag) {
+        auto prefilter8 = [&](int mrow, int d, bool active, uint32_t tflag, bool chk) {
             const int y = y0 - 1 + mrow, xb = x0 + 4 * d;
             uint32_t cA = 0, cB = 0;   // top bit of byte i: pixel xb+i (cA), xb+4+i (cB)
             if (active && y >= dy0 && y < dy1 && xb + 7 >= dx0 && xb < dx1) {
                 const uint32_t *row = tin + (mrow + 3) * FB_LD;
-                auto ld = [&](const uint32_t *rw, int i) { return (unsigned)i < (unsigned)FB_SD ? rw[i] : 0u; };
+                // tile rows read dwords 0 .. 33 only; the ring rows' groups reach one dword past
+                // either end (chk: those read as 0)
+                auto ld = [&](const uint32_t *rw, int i) { return !chk || (unsigned)i < (unsigned)FB_SD ? rw[i] : 0u; };
                 const uint32_t C0 = ld(row, d), C1 = ld(row, d + 1), C2 = ld(row, d + 2), C3 = ld(row, d + 3);
                 const uint32_t *rn = row - 3 * FB_LD, *rs = row + 3 * FB_LD;
                 cA = swar4(C1, C0, C2, ld(rn, d + 1), ld(rs, d + 1));
@@ -541,11 +543,11 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;   // pixels (y0 + r, x0 + cb + i)
 #ifndef FB_SKIP_PRE   // instruction-count experiments (make variant VDEFS=-DFB_SKIP_...)
         if (y0 + 4 * wv + 3 >= dy0 && y0 + 4 * wv < dy1)   // wave-uniform: 4 tile rows per wavefront
-            prefilter8(r + 1, cb >> 2, true, FB_INTILE);
+            prefilter8(r + 1, cb >> 2, true, FB_INTILE, false);
         if (wv == 2) {   // ring rows: lanes 0..16 row y0-1, lanes 17..33 row y0+16
             const int hr = lane >= 17, j = lane - 17 * hr;
             if ((y0 - 1 >= dy0 && y0 - 1 < dy1) || (y0 + FB_TH >= dy0 && y0 + FB_TH < dy1))
-                prefilter8(hr ? FB_TH + 1 : 0, 2 * j - 1, lane < 34, 0u);
+                prefilter8(hr ? FB_TH + 1 : 0, 2 * j - 1, lane < 34, 0u, true);
         }
         if (wv == 3) {   // ring columns: lane -> (row y0 + (lane & 15), column x0-1 or x0+128)
             const int y = y0 + (lane & 15), x = lane < 16 ? x0 - 1 : x0 + FB_TW;
@@ -672,12 +674,16 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             const int rx0 = 19 + cj * wC, rx1 = min(rx0 + wC, rx_end);
             if (ci >= g.ncell_rows[l] || cj >= g.ncell_cols[l] || y >= ry1 || x >= rx1) continue;
             const bool up = y > ry0, dn = y + 1 < ry1, lf = x > rx0, rt = x + 1 < rx1;
+            // cv::FAST's NMS at tlo keeps p iff s_p > s_q for every in-cell neighbour q, with
+            // s = M > tlo ? M - 1 : 0. p is hot (M_p > tlo, so s_p = M_p - 1 >= tlo), and a
+            // neighbour with M_q <= tlo has M_q - 1 < tlo <= s_p: the test is M_p > max(M_q, 1)
+            // over the in-cell neighbours, on the raw M bytes (0 outside the candidates)
             const uint8_t *pm = m8 + pos;
             const int sp = (int)pm[0] - 1;
-            auto sc = [&](int off, bool in) { const int m = pm[off]; return in && m > tlo ? m - 1 : 0; };
-            const int sn = max(max(max(sc(-1, lf), sc(1, rt)), max(sc(-FB_LW - 1, up && lf), sc(-FB_LW, up))),
-                               max(max(sc(-FB_LW + 1, up && rt), sc(FB_LW - 1, dn && lf)), max(sc(FB_LW, dn), sc(FB_LW + 1, dn && rt))));
-            const bool keep = sp > sn;
+            auto mq = [&](int off, bool in) { return in ? (int)pm[off] : 0; };
+            const int mn = max(max(max(mq(-1, lf), mq(1, rt)), max(mq(-FB_LW - 1, up && lf), mq(-FB_LW, up))),
+                               max(max(mq(-FB_LW + 1, up && rt), mq(FB_LW - 1, dn && lf)), max(mq(FB_LW, dn), mq(FB_LW + 1, dn && rt))));
+            const bool keep = (int)pm[0] > max(mn, 1);
             if (keep) {
                 const long long cidx = (long long)b * g.ncell_total + g.cell_base[l] + ci * g.ncell_cols[l] + cj;
                 const int slot = atomicAdd(cell_cnt + cidx, 1);
