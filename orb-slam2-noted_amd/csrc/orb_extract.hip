@@ -281,6 +281,22 @@ __device__ __forceinline__ s16x2 byte_pair(const uint32_t *w, int j) {
     return __builtin_bit_cast(s16x2, r);
 }
 
+// inclusive wavefront scan of int as six fused DPP adds (row_shr 1/2/4/8 with zero-filled
+// out-of-row sources, row_bcast 15 / 31 on rows 1, 3 / 2, 3; unwritten rows keep v). Written
+// out because the compiler keeps update_dpp + add as a v_mov_b32_dpp, a v_add and a zeroed
+// old operand per step; the s_nop 1 covers the VALU-write -> DPP-read hazard.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    asm("s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(v));
+    return v;
+}
+
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
@@ -526,13 +542,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             const uint32_t m = __builtin_amdgcn_udot4(cB >> 7, 0x80402010u,
                                                       __builtin_amdgcn_udot4(cA >> 7, 0x08040201u, 0u, false), false);
             const int cnt = __builtin_popcount(m);
-            int inc = cnt;
-            inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xF, 0xF, false);   // row_shr:1
-            inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xF, 0xF, false);   // row_shr:2
-            inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xF, 0xF, false);   // row_shr:4
-            inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xF, 0xF, false);   // row_shr:8
-            inc += __builtin_amdgcn_update_dpp(0, inc, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
-            inc += __builtin_amdgcn_update_dpp(0, inc, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+            const int inc = wave_incl_scan_dpp(cnt);
             const int tot8 = __builtin_amdgcn_readlane(inc, 63);
             if (tot8 == 0) return;   // wave-uniform
             int base = 0;
