@@ -319,8 +319,43 @@ def bench_c2(amd, args, dist, world, params, pool):
             out["roofline"]["valu_insts_per_launch"] = valu
         # summed over the engines' launches, which overlap in time (so the sum exceeds ms_per_step)
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
+        # the same launch (per_launch pairs) on one engine with nothing beside it: under the
+        # pipeline a launch shares the CUs with the other engines' kernels, so its duration (and
+        # `frac` above) measures the overlap as much as the kernel
+        iso_ms = isolated_launch_ms(amd, params, bufs[0], round(per_launch), name)
+        if iso_ms:
+            iso = BYTES_PER_STEREO_FRAME * per_launch / (iso_ms / 1e3) / 1e9
+            out["roofline"]["isolated"] = {"avg_launch_ms": round(iso_ms, 4), "achieved": round(iso, 3),
+                                           "frac": round(iso / HBM_PEAK_GBS, 6)}
+            if valu:
+                out["roofline"]["isolated"]["valu_issue_frac"] = round(
+                    valu * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (iso_ms / 1e3), 4)
     del bufs   # the resident batches are not needed by the legs below
     return out
+
+
+def isolated_launch_ms(amd, params, buf, pairs, name, reps=5):
+    """Average duration (hipEvents) of kernel `name` when one engine runs `pairs` stereo pairs
+    of `buf` alone on the GPU (after the timed region; not part of `value`)."""
+    nf, sf, nl, ith, mth, bf, mb = params
+    ex1 = amd.StereoPipeline(int(nf), float(sf), int(nl), int(ith), int(mth), n_engines=1)
+    try:
+        ex1.reserve(W, H, pairs)
+        for _ in range(2):
+            ex1.stereo_batch(buf.data_ptr(), pairs, W, H, W, W * H, float(bf), mb)
+        amd.device_sync()
+        ex1.profile(True)
+        for _ in range(reps):
+            ex1.stereo_batch(buf.data_ptr(), pairs, W, H, W, W * H, float(bf), mb)
+            amd.device_sync()   # one launch at a time: nothing else on the GPU
+        pr = ex1.profile_read()
+        ex1.profile(False)
+    finally:
+        ex1.close()
+    if name not in pr:
+        return None
+    tot, n = pr[name]
+    return tot / n
 
 
 FP64_MFMA_PEAK_TFS = 75.08   # measured, tools/microbench/mfma_f64_peak.hip (profiles/r02_mfma_f64_peak.json)

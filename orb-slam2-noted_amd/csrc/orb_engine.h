@@ -128,6 +128,7 @@ struct orbx_engine {
     orbx_params p{};
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t fb_gate = nullptr;   // pipeline: fast_blur_kernel waits for this event (not the resize)
     // extractor tables (ORBextractor.cc:471-579)
     float scale[ORBX_MAXL]{}, inv_scale[ORBX_MAXL]{}, sigma2[ORBX_MAXL]{}, inv_sigma2[ORBX_MAXL]{};
     int nfeat[ORBX_MAXL]{};

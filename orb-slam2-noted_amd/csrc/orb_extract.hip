@@ -1844,6 +1844,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     }
     prof_end(e, s, ph, "resize_level_kernel");
     HIPCHK(hipMemsetAsync(e->d_cell_cnt.p, 0, sizeof(int) * (size_t)n * g.ncell_total, s));   // cell slot counters
+    if (e->fb_gate) HIPCHK(hipStreamWaitEvent(s, e->fb_gate, 0));
     ph = prof_begin(e, s);
     fast_blur_kernel<<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
                                                                    e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());

@@ -3,8 +3,9 @@
 //   phase 1 (pyramid + FAST strength map + blur: the VALU-bound half of ORBextractor::operator())
 //   phase 2 (cell NMS, DistributeOctTree, IC_Angle + rBRIEF: latency-bound)
 //   Frame::ComputeStereoMatches (latency-bound)
-// with the chunks' phase 1 in turn (chunk j's phase 1 waits for chunk j-1's, across batches
-// too), so one chunk's VALU-bound phase overlaps the others' latency-bound phases. The work and
+// with the chunks' fast_blur launches in turn (chunk j's waits for chunk j-1's, across batches
+// too), so one chunk's VALU-bound kernel overlaps the others' latency-bound ones (resize
+// chains, quadtree, describe, stereo). The work and
 // the results are the same as one engine over the whole batch (each chunk is an independent
 // ORBextractor pair; Frame.cc:144-153 runs the left / right extractors on two threads).
 // Measured on MI355X, 1241x376 pairs, bench.py C2 leg: one engine x 256 pairs 48.7k stereo
@@ -14,9 +15,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "orbslam2_amd.h"
+#include "orb_engine.h"
+
+static void orbx_engine_fb_gate(orbx_engine *e, hipEvent_t ev) { e->fb_gate = ev; }
 
 struct orbx_pipeline {
     std::vector<orbx_engine *> eng;
@@ -65,11 +70,19 @@ static int pipeline_run(orbx_pipeline *pl, const uint8_t *d_imgs, int n_pairs, i
         orbx_engine *e = pl->eng[j];
         const hipStream_t s = (hipStream_t)orbx_stream(e);
         if (hipStreamWaitEvent(s, host ? pl->ev_h2d[slot][j] : pl->ev_in, 0) != hipSuccess) return ORBX_EDEVICE;
-        if (pl->last_p1 >= 0 && pl->last_p1 != j && hipStreamWaitEvent(s, pl->ev_p1[pl->last_p1], 0) != hipSuccess)
-            return ORBX_EDEVICE;
+        // only the VALU-bound fast_blur launches run in turn: the engine's resize chain starts as
+        // soon as its input is there and overlaps the previous engine's fast_blur, and its
+        // fast_blur then starts the moment that one ends (measured against ordering the whole
+        // phase 1: 71.2-71.8k vs 68.1-69.6k stereo frames/s, and no pipeline phase that leaves
+        // describe without a fast_blur to overlap)
+        static const bool whole_p1 = [] { const char *ev = std::getenv("ORBX_PIPE_ORDER_P1"); return ev && std::atoi(ev); }();
+        const bool gate = pl->last_p1 >= 0 && pl->last_p1 != j;
+        if (gate && whole_p1 && hipStreamWaitEvent(s, pl->ev_p1[pl->last_p1], 0) != hipSuccess) return ORBX_EDEVICE;
         const uint8_t *src = d_imgs + (size_t)2 * pl->first[j] * image_stride;
         const int n_img = 2 * pl->count[j];
+        orbx_engine_fb_gate(e, gate && !whole_p1 ? pl->ev_p1[pl->last_p1] : nullptr);
         int rc = orbx_extract_batch_device_phase(e, src, n_img, w, h, pitch, image_stride, s, 1);
+        orbx_engine_fb_gate(e, nullptr);
         if (rc) return rc;
         if (hipEventRecord(pl->ev_p1[j], s) != hipSuccess) return ORBX_EDEVICE;
         pl->last_p1 = j;
