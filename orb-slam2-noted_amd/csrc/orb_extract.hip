@@ -886,22 +886,24 @@ __device__ QCnt qt_prefix(QShared &S, QT &Q, int &par) {
     const int i0 = threadIdx.x * R, i1 = min(i0 + R, Q.M);
     const uint32_t *K = Q.keys(Q.src);
     const int16_t *NO = Q.nodes_of(Q.src);
+    // a node's keys are contiguous: its midpoint is fetched once per run of keys (the node
+    // arrays sit in global scratch, so every fetch is a dependent L2 round trip)
     QCnt run{0ull, 0ull};
+    int last = -1, mx = 0, my = 0;
     for (int i = i0; i < i1; i++) {
         const int nd = NO[i];
         if (nd < 0) continue;
-        int mx, my;
-        qnode_mid(Q.cur[nd], &mx, &my);
+        if (nd != last) { qnode_mid(Q.cur[nd], &mx, &my); last = nd; }
         run += qone(quadrant(K[i], mx, my));
     }
     QCnt tot;
     const QCnt base = block_scan(S, run, &tot, par);
     QCnt p = base;
+    last = -1;
     for (int i = i0; i < i1; i++) {
         const int nd = NO[i];
         if (nd < 0) continue;
-        int mx, my;
-        qnode_mid(Q.cur[nd], &mx, &my);
+        if (nd != last) { qnode_mid(Q.cur[nd], &mx, &my); last = nd; }
         if (i == 0 || NO[i - 1] != nd) Q.tmp[nd].pstart = p;
         p += qone(quadrant(K[i], mx, my));
         if (i == Q.M - 1 || NO[i + 1] != nd) Q.tmp[nd].pend = p;
@@ -997,24 +999,29 @@ __device__ void qt_move(QShared &S, QT &Q, QCnt base) {
     uint32_t *Kd = Q.keys(d);
     int16_t *Nd = Q.nodes_of(d);
     QCnt p = base;
+    int last = -1, mx = 0, my = 0, qs = 0;
+    QTmp T{};
     for (int i = i0; i < i1; i++) {
         const int nd = Ns[i];
         if (nd < 0) { Nd[i] = -1; continue; }
         const uint32_t key = Ks[i];
-        const QNode q = Q.cur[nd];
-        int mx, my;
-        qnode_mid(q, &mx, &my);
+        if (nd != last) {   // once per run of the node's keys (see qt_prefix)
+            const QNode q = Q.cur[nd];
+            qnode_mid(q, &mx, &my);
+            qs = q.s;
+            T = Q.tmp[nd];
+            last = nd;
+        }
         const int k = quadrant(key, mx, my);
-        const QTmp &T = Q.tmp[nd];
         if (T.keep >= 0) {
             Kd[i] = key;
             Nd[i] = (int16_t)T.keep;
         } else {
             const QCnt c = T.pend - T.pstart;
-            int pos = q.s + (p - T.pstart).f(k);
+            int pos = qs + (p - T.pstart).f(k);
             for (int j = 0; j < k; j++) pos += c.f(j);
             Kd[pos] = key;
-            const int cmk = T.cm[k];
+            const int cmk = k < 2 ? (k ? T.cm[1] : T.cm[0]) : (k == 3 ? T.cm[3] : T.cm[2]);   // no private indexing
             if (cmk >= 0) {
                 Nd[pos] = (int16_t)cmk;
             } else {
@@ -1040,7 +1047,7 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     xcd_remap2(l, b);
     const int tid = threadIdx.x;
 #ifdef ORBX_QT_PROFILE
-    long long qt_t[8];
+    long long qt_t[8], qt_sub[3] = {0, 0, 0};
     int qt_rounds = 0;
     qt_t[0] = wall_clock64();
 #define QT_MARK(k) do { if (tid == 0) qt_t[k] = wall_clock64(); } while (0)
@@ -1200,12 +1207,23 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     bool finished = false, final_phase = false;
     while (!finished) {
         const int prev = S.live, na = S.n_act;
+#ifdef ORBX_QT_PROFILE
+        const long long ta = wall_clock64();
+#endif
         const QCnt base = qt_prefix(S, Q, par);
+#ifdef ORBX_QT_PROFILE
+        const long long tb = wall_clock64();
+#endif
         qt_assign(S, Q, na, order, na, par);
+#ifdef ORBX_QT_PROFILE
+        const long long tc = wall_clock64();
+#endif
         qt_move(S, Q, base);
         order = 1;
 #ifdef ORBX_QT_PROFILE
         qt_rounds++;
+        const long long td = wall_clock64();
+        qt_sub[0] += tb - ta; qt_sub[1] += tc - tb; qt_sub[2] += td - tc;
 #endif
         const int live = S.live, nToExpand = S.n_act;
         if (live >= N || live == prev) finished = true;
@@ -1328,9 +1346,9 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     if (tid == 0) sel_cnt[b * g.nlevels + l] = ncap;
 #ifdef ORBX_QT_PROFILE
     if (tid == 0 && (b < 2 || (b & 31) == 0))
-        printf("QTPROF b=%d l=%d M=%d NP=%d nout=%d rounds=%d start=%lld end=%lld gather=%lld roots=%lld ph1=%lld final=%lld best=%lld sort=%lld\n", b, l, M,
+        printf("QTPROF b=%d l=%d M=%d NP=%d nout=%d rounds=%d start=%lld end=%lld gather=%lld roots=%lld ph1=%lld final=%lld best=%lld sort=%lld prefix=%lld assign=%lld move=%lld\n", b, l, M,
                NP, nout, qt_rounds, qt_t[0], wall_clock64(), qt_t[1] - qt_t[0], qt_t[2] - qt_t[1], qt_t[3] - qt_t[2], qt_t[4] - qt_t[3],
-               qt_t[5] - qt_t[4], qt_t[6] - qt_t[5]);
+               qt_t[5] - qt_t[4], qt_t[6] - qt_t[5], qt_sub[0], qt_sub[1], qt_sub[2]);
 #endif
 }
 
