@@ -322,7 +322,7 @@ def bench_c2(amd, args, dist, world, params, pool):
         # the same launch (per_launch pairs) on one engine with nothing beside it: under the
         # pipeline a launch shares the CUs with the other engines' kernels, so its duration (and
         # `frac` above) measures the overlap as much as the kernel
-        iso_ms = isolated_launch_ms(amd, params, bufs[0], round(per_launch), name)
+        iso_ms = None if args.no_isolated else isolated_launch_ms(amd, params, bufs[0], round(per_launch), name)
         if iso_ms:
             iso = BYTES_PER_STEREO_FRAME * per_launch / (iso_ms / 1e3) / 1e9
             out["roofline"]["isolated"] = {"avg_launch_ms": round(iso_ms, 4), "achieved": round(iso, 3),
@@ -794,6 +794,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=96)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip roofline.isolated (its extra launches would enter a rocprofv3 average of the "
+                         "dominant kernel: tools/gpu_trace.sh passes this so the summary matches the line)")
     ap.add_argument("--lba-steps", type=int, default=10, help="timed LocalBA calls (C4 graph)")
     ap.add_argument("--no-lba", action="store_true")
     ap.add_argument("--rgbd-batch", type=int, default=256)
