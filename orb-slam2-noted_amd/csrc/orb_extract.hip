@@ -767,16 +767,8 @@ struct QShared {
 // block-wide exclusive scan of one value per thread; two LDS slots alternate so
 // back-to-back scans need one barrier each
 
-// inclusive wavefront scan of u32 on DPP (row_shr 1/2/4/8, then row_bcast 15 / 31)
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
-    return v;
-}
+// inclusive wavefront scan of u32 (wave_incl_scan_dpp: six fused DPP adds)
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) { return (uint32_t)wave_incl_scan_dpp((int)v); }
 
 __device__ __forceinline__ QCnt block_scan(QShared &S, QCnt v, QCnt *total, int &par) {
     const int lane = threadIdx.x & 63, wv = wave_id();
