@@ -1090,6 +1090,9 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         M += (int)tot;
     }
     Q.M = M;
+#ifdef ORBX_QT_PROFILE
+    const long long t_gm = wall_clock64();
+#endif
     if (M <= g.qt_kl) {
         Q.K[0] = (uint32_t *)lds;
         Q.K[1] = Q.K[0] + g.qt_kl;
@@ -1338,9 +1341,9 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     if (tid == 0) sel_cnt[b * g.nlevels + l] = ncap;
 #ifdef ORBX_QT_PROFILE
     if (tid == 0 && (b < 2 || (b & 31) == 0))
-        printf("QTPROF b=%d l=%d M=%d NP=%d nout=%d rounds=%d start=%lld end=%lld gather=%lld roots=%lld ph1=%lld final=%lld best=%lld sort=%lld prefix=%lld assign=%lld move=%lld\n", b, l, M,
+        printf("QTPROF b=%d l=%d M=%d NP=%d nout=%d rounds=%d start=%lld end=%lld gather=%lld roots=%lld ph1=%lld final=%lld best=%lld sort=%lld prefix=%lld assign=%lld move=%lld gatherM=%lld\n", b, l, M,
                NP, nout, qt_rounds, qt_t[0], wall_clock64(), qt_t[1] - qt_t[0], qt_t[2] - qt_t[1], qt_t[3] - qt_t[2], qt_t[4] - qt_t[3],
-               qt_t[5] - qt_t[4], qt_t[6] - qt_t[5], qt_sub[0], qt_sub[1], qt_sub[2]);
+               qt_t[5] - qt_t[4], qt_t[6] - qt_t[5], qt_sub[0], qt_sub[1], qt_sub[2], t_gm - qt_t[0]);
 #endif
 }
 
