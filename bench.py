@@ -326,7 +326,11 @@ def bench_c2(amd, args, dist, world, params, pool):
         if iso_ms:
             iso = BYTES_PER_STEREO_FRAME * per_launch / (iso_ms / 1e3) / 1e9
             out["roofline"]["isolated"] = {"avg_launch_ms": round(iso_ms, 4), "achieved": round(iso, 3),
-                                           "frac": round(iso / HBM_PEAK_GBS, 6)}
+                                           "frac": round(iso / HBM_PEAK_GBS, 6),
+                                           "note": "the same launch on one engine with nothing beside it; the "
+                                                   "pipelined launch above shares the CUs with the next chunk's "
+                                                   "resize and the previous chunk's quadtree / describe / stereo "
+                                                   "for its whole duration (DESIGN.md §5, §5a)"}
             if valu:
                 out["roofline"]["isolated"]["valu_issue_frac"] = round(
                     valu * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (iso_ms / 1e3), 4)
