@@ -54,9 +54,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_pool(n_pairs: int, seed0: int):
+def make_pool(n_pairs: int, rank: int, world: int):
+    """C2 (one GPU): frames t = 0.. of the seed-2 stream (left seed 2 + t). C5 (world > 1):
+    SURVEY §8d's eight independent streams, seeds 10..17, one per rank: rank r's frame t is
+    generated from seed 10 + r + 8 t, so no two ranks share a frame."""
     from orbslam2_amd import synth
-    return [synth.stereo_pair(H, W, seed0 + t) for t in range(n_pairs)]
+    if world == 1:
+        return [synth.stereo_pair(H, W, t) for t in range(n_pairs)]
+    return [synth.stereo_pair(H, W, 8 * t, base_seed=10 + rank) for t in range(n_pairs)]
 
 
 def host_cpu():
@@ -221,27 +226,33 @@ def bench_e2e(amd, args, pool, bf, mb):
                             "PCIe-inclusive rate (value is the HBM-resident rate)"}}
 
 
-def bench_c2(amd, args, dist, world, params, pool):
-    """C2 headline leg: B resident stereo pairs per step through the 3-engine pipeline."""
+def c2_buffers(B: int, nbufs: int, pool):
+    """`nbufs` rotating resident batches of B stereo pairs (batch k: the pool rolled by 7k px, so
+    no two batches are identical)."""
     import torch
-    from orbslam2_amd import dist as odist
-    nf, sf, nl, ith, mth, bf, mb = params
-    B = args.batch
     bufs = []
-    for k in range(args.bufs):
+    for k in range(nbufs):
         imgs = np.empty((2 * B, H, W), np.uint8)
         for i in range(B):
             L, R = pool[(i + 3 * k) % len(pool)]
-            if k:  # make rotating buffers differ (avoid identical cached inputs)
+            if k:
                 L = np.roll(L, 7 * k, axis=1)
                 R = np.roll(R, 7 * k, axis=1)
             imgs[2 * i], imgs[2 * i + 1] = L, R
         bufs.append(torch.from_numpy(imgs).cuda())
     torch.cuda.synchronize()
+    return bufs
 
-    ex = amd.StereoPipeline(int(nf), float(sf), int(nl), int(ith), int(mth), n_engines=args.engines)
+
+def time_c2(amd, args, dist, params, bufs, resize_mode, steps, profile=False):
+    """Warmup + `steps` timed batches of the C2 leg on a fresh pipeline; the timed region is
+    bracketed by a barrier + device synchronisation on both sides. -> (elapsed s, profile, pipeline)."""
+    import torch
+    nf, sf, nl, ith, mth, bf, mb = params
+    B = args.batch
+    ex = amd.StereoPipeline(int(nf), float(sf), int(nl), int(ith), int(mth), n_engines=args.engines,
+                            resize_mode=resize_mode)
     ex.reserve(W, H, B)
-    per_launch = B / len(ex.engines)   # stereo pairs one extraction / stereo launch processes
 
     def step(k):
         t = bufs[k % len(bufs)]
@@ -250,23 +261,36 @@ def bench_c2(amd, args, dist, world, params, pool):
     for k in range(args.warmup):
         step(k)
     amd.device_sync()
-    if not args.no_profile:
+    if profile:
         ex.profile(True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     amd.device_sync()
     t0 = time.perf_counter()
-    for k in range(args.steps):
+    for k in range(steps):
         step(k)
     amd.device_sync()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    prof = ex.profile_read() if not args.no_profile else {}
+    prof = ex.profile_read() if profile else {}
     ex.profile(False)
+    return elapsed, prof, ex
+
+
+def bench_c2(amd, args, dist, world, params, pool):
+    """C2 headline leg: B resident stereo pairs per step through the 3-engine pipeline, under
+    `--resize-mode` (SURVEY A.2 pin (a) by default); the same leg under the other resize variant is
+    reported beside it (`alt_resize_mode`)."""
+    from orbslam2_amd import dist as odist
+    B = args.batch
+    bufs = c2_buffers(B, args.bufs, pool)
+    elapsed, prof, ex = time_c2(amd, args, dist, params, bufs, args.resize_mode, args.steps,
+                                profile=not args.no_profile)
     elapsed = odist.max_over_ranks(elapsed, COLL_DEV, dist)
+    per_launch = B / len(ex.engines)   # stereo pairs one extraction / stereo launch processes
 
     # sanity: the batch produced keypoints and stereo matches
     k0 = ex.fetch(0)[0]
@@ -274,9 +298,12 @@ def bench_c2(amd, args, dist, world, params, pool):
     n_match = int((u0[: len(k0)] >= 0).sum())
     if len(k0) < 100 or n_match < 10:
         raise RuntimeError(f"implausible output: {len(k0)} keypoints, {n_match} stereo matches")
+    engines = len(ex.engines)
+    ex.close()
 
     frames = B * args.steps * world
     value = frames / elapsed
+    ms_step = 1000 * elapsed / args.steps
     out = {
         "metric": "frames/sec ORB extract+match @1241x376 (1 GPU) + LocalBA keyframes/sec",
         "value": round(value, 2),
@@ -284,7 +311,7 @@ def bench_c2(amd, args, dist, world, params, pool):
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1000 * elapsed / args.steps, 4),
+        "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -294,9 +321,13 @@ def bench_c2(amd, args, dist, world, params, pool):
             "workload": "C2: KITTI-like synthetic stereo 1241x376, ORBextractor(2000,1.2,8,20,7) L+R "
                         "+ Frame::ComputeStereoMatches",
             "stereo_frames_per_step_per_gpu": B,
-            "pipeline_engines": len(ex.engines),
+            "pipeline_engines": engines,
             "image": f"{W}x{H}",
             "nfeatures": NFEAT,
+            "resize_mode": args.resize_mode,
+            "resize_mode_meaning": "0 = scalar FixedPtCast vertical pass (SURVEY A.2 (a), the oracle's default pin); "
+                                   "1 = OpenCV 3.2 x86 SSE2 VResizeLinearVec_32s8u prefix (A.2 (b))",
+            "streams": "seed-2 C2 stream" if world == 1 else "C5: rank r = seed 10 + r stream (seeds 10..17)",
             "parallelism": f"independent sequence per GPU x{world}",
             "keypoints_img0": int(len(k0)),
             "stereo_matches_img0": n_match,
@@ -306,23 +337,44 @@ def bench_c2(amd, args, dist, world, params, pool):
         name, (tot, n) = max(prof.items(), key=lambda kv: kv[1][0])
         avg_s = tot / n / 1000.0
         achieved = BYTES_PER_STEREO_FRAME * per_launch / avg_s / 1e9
-        traffic = load_pmc(name, round(per_launch))
+        # counters from the committed PMC pass, only if it was measured on this library, batch and mode
+        pmc, pmc_note = load_pmc_doc("pmc_traffic.json", amd.build_id(), batch=round(per_launch),
+                                     resize_mode=args.resize_mode)
+        ent = (pmc or {}).get(name, {})
         out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 3),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                           "traffic": traffic, "avg_launch_ms": round(tot / n, 4),
+                           "traffic": ent.get("hbm_bytes_per_launch"), "avg_launch_ms": round(tot / n, 4),
                            "algorithmic_bytes_per_launch": round(BYTES_PER_STEREO_FRAME * per_launch),
-                           "pairs_per_launch": per_launch}
-        valu = load_pmc(name, round(per_launch), "valu_insts_per_launch")
+                           "pairs_per_launch": per_launch, "pmc_source": pmc_note}
+        valu = ent.get("valu_insts_per_launch")
         if valu:   # the ceiling this integer kernel actually sits against
             out["roofline"]["valu_issue_frac"] = round(
                 valu * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (tot / n / 1e3), 4)
             out["roofline"]["valu_insts_per_launch"] = valu
+        if pmc:
+            # the whole step against VALU issue: every kernel's VALU instructions per launch (PMC) x
+            # its launches per timed step (live profile) x 4 cycles / (1024 SIMDs x 2.4 GHz) / ms_per_step
+            insts = 0.0
+            missing = []
+            for k, (_, kn) in prof.items():
+                v = (pmc.get(k) or {}).get("valu_insts_per_launch")
+                if v is None:
+                    missing.append(k)
+                    continue
+                insts += v * kn / args.steps
+            out["roofline"]["step_valu_insts"] = int(insts)
+            out["roofline"]["step_valu_issue_frac"] = round(
+                insts * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (ms_step / 1e3), 4)
+            if missing:
+                out["roofline"]["step_valu_missing_kernels"] = missing
         # summed over the engines' launches, which overlap in time (so the sum exceeds ms_per_step)
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
+        out["kernel_launches_per_step"] = {k: round(v[1] / args.steps, 3) for k, v in sorted(prof.items())}
         # the same launch (per_launch pairs) on one engine with nothing beside it: under the
         # pipeline a launch shares the CUs with the other engines' kernels, so its duration (and
         # `frac` above) measures the overlap as much as the kernel
-        iso_ms = None if args.no_isolated else isolated_launch_ms(amd, params, bufs[0], round(per_launch), name)
+        iso_ms = None if args.no_isolated else isolated_launch_ms(amd, params, bufs[0], round(per_launch), name,
+                                                                   args.resize_mode)
         if iso_ms:
             iso = BYTES_PER_STEREO_FRAME * per_launch / (iso_ms / 1e3) / 1e9
             out["roofline"]["isolated"] = {"avg_launch_ms": round(iso_ms, 4), "achieved": round(iso, 3),
@@ -334,15 +386,25 @@ def bench_c2(amd, args, dist, world, params, pool):
             if valu:
                 out["roofline"]["isolated"]["valu_issue_frac"] = round(
                     valu * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (iso_ms / 1e3), 4)
+    if not args.no_alt_resize:
+        alt = 1 - args.resize_mode
+        a_el, _, a_ex = time_c2(amd, args, dist, params, bufs, alt, args.steps)
+        a_ex.close()
+        a_el = odist.max_over_ranks(a_el, COLL_DEV, dist)
+        out["alt_resize_mode"] = {"resize_mode": alt, "value": round(frames / a_el, 2),
+                                  "ms_per_step": round(1000 * a_el / args.steps, 4),
+                                  "note": "the same leg (batches, steps, engines) under the other SURVEY A.2 "
+                                          "vertical-pass variant; both variants are parity-tested on the GPU"}
     del bufs   # the resident batches are not needed by the legs below
     return out
 
 
-def isolated_launch_ms(amd, params, buf, pairs, name, reps=5):
+def isolated_launch_ms(amd, params, buf, pairs, name, resize_mode=0, reps=5):
     """Average duration (hipEvents) of kernel `name` when one engine runs `pairs` stereo pairs
     of `buf` alone on the GPU (after the timed region; not part of `value`)."""
     nf, sf, nl, ith, mth, bf, mb = params
-    ex1 = amd.StereoPipeline(int(nf), float(sf), int(nl), int(ith), int(mth), n_engines=1)
+    ex1 = amd.StereoPipeline(int(nf), float(sf), int(nl), int(ith), int(mth), n_engines=1,
+                             resize_mode=resize_mode)
     try:
         ex1.reserve(W, H, pairs)
         for _ in range(2):
@@ -378,17 +440,6 @@ def lba_flops(prob: dict) -> dict:
     schur = float((k * (k + 1) / 2 * 324 + k * 90 + 60).sum())
     chol = (6.0 * P) ** 3 / 3
     return {"linearize": lin, "schur": schur, "cholesky": chol, "per_trial": lin + schur + chol}
-
-
-def load_lba_pmc():
-    """MFMA PMC pass of the LocalBA kernels (profiles/r02_lba_pmc.json), if committed."""
-    f = ROOT / "profiles" / "r02_lba_pmc.json"
-    if not f.exists():
-        return None
-    try:
-        return json.loads(f.read_text()).get("kernels")
-    except ValueError:
-        return None
 
 
 def bench_localba(amd, args, dist, world, with_cpu):
@@ -435,7 +486,7 @@ def bench_localba(amd, args, dist, world, with_cpu):
     syrk_avg_s = syrk_ms / max(syrk_n, 1) / 1e3
     trial_s = gpu_ms_call / 1e3 / max(trials, 1)
     achieved = fl["per_trial"] / trial_s / 1e12
-    pmc = load_lba_pmc()
+    pmc, pmc_note = load_pmc_doc("lba_pmc.json", amd.build_id())
     res["localba"]["roofline"] = {
         "bound": "mfma", "kernel": "LM trial (linearize .. decide)", "achieved": round(achieved, 5),
         "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP64_MFMA_PEAK_TFS, 7), "traffic": None,
@@ -444,7 +495,7 @@ def bench_localba(amd, args, dist, world, with_cpu):
                  "achieved": round(fl["schur"] / syrk_avg_s / 1e12, 4) if syrk_avg_s > 0 else None,
                  "frac": round(fl["schur"] / syrk_avg_s / 1e12 / FP64_MFMA_PEAK_TFS, 5) if syrk_avg_s > 0 else None},
         "peak_source": "v_mfma_f64_16x16x4_f64 measured on this MI355X (tools/microbench/mfma_f64_peak.hip; AMD spec 78.6)",
-        "pmc": pmc}
+        "pmc": pmc, "pmc_source": pmc_note}
     res["localba"]["gpu_ms_per_call"] = round(gpu_ms_call, 4)
     res["localba"]["host_ms_per_call"] = round(1000 * dt / args.lba_steps - gpu_ms_call, 4)
     res["localba"]["kernel_ms_per_call"] = {k: round(v[0] / ncall, 4) for k, v in sorted(prof.items())}
@@ -756,19 +807,32 @@ def bench_newpts(amd, args, dist, world, with_cpu):
     return res
 
 
-def load_pmc(kernel: str, batch: int, field: str = "hbm_bytes_per_launch"):
-    """Per-launch figure of `kernel` from the committed rocprofv3 PMC summary, if any."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
+def kernel_base(name: str) -> str:
+    """rocprofv3 kernel name -> the engine profiler's name (template arguments dropped)."""
+    return name.split("(")[0].split("<")[0].split("::")[-1]
+
+
+def load_pmc_doc(fname: str, build_id: str, **expect):
+    """A committed rocprofv3 PMC summary under profiles/ and whether it describes the library
+    being run: its `stamp.src_hash` (tools/src_hash.py at profiling time) must equal
+    orbx_build_id() of the loaded library and every `expect` key (batch, resize_mode, ...) must
+    match the stamp. -> (kernels by base name or None, note)."""
+    f = ROOT / "profiles" / fname
     if not f.exists():
-        return None
+        return None, f"profiles/{fname} absent"
     try:
-        d = json.loads(f.read_text())
-        ent = d.get("kernels", {}).get(kernel)
-        if ent and int(d.get("batch", -1)) == batch:
-            return ent.get(field)
-    except Exception:
-        return None
-    return None
+        doc = json.loads(f.read_text())
+    except ValueError:
+        return None, f"profiles/{fname} unreadable"
+    stamp = doc.get("stamp") or {}
+    if stamp.get("src_hash") != build_id:
+        return None, (f"profiles/{fname} was measured on library sources {stamp.get('src_hash')} "
+                      f"(commit {stamp.get('commit')}), this library is {build_id}: counters not reported")
+    for k, v in expect.items():
+        if stamp.get(k) != v:
+            return None, f"profiles/{fname} stamp {k}={stamp.get(k)}, this run {k}={v}: counters not reported"
+    kern = {kernel_base(k): v for k, v in doc.get("kernels", {}).items()}
+    return kern, f"profiles/{fname} (src_hash {build_id}, commit {stamp.get('commit')})"
 
 
 # VALU issue ceiling: a wave64 VALU instruction occupies one 16-lane SIMD for 4 cycles;
@@ -794,6 +858,9 @@ def main():
                     help="pipeline engines of the host-batch (value_e2e) leg (tools/e2e_queues.sh, 8 HW "
                          "queues: 2 engines 57.8k, 3 engines 53.0k stereo fps)")
     ap.add_argument("--pool", type=int, default=8, help="distinct synthetic stereo pairs")
+    ap.add_argument("--resize-mode", type=int, default=0, choices=(0, 1),
+                    help="SURVEY A.2 vertical-pass variant of the headline value (0: FixedPtCast, 1: SSE2)")
+    ap.add_argument("--no-alt-resize", action="store_true", help="skip the other resize variant's line")
     ap.add_argument("--bufs", type=int, default=4, help="rotating resident input batches")
     ap.add_argument("--cpu-frames", type=int, default=96)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -856,7 +923,7 @@ def main():
         [NFEAT, 1.2, 8, 20, 7, KITTI_BF, KITTI_FX, W, H] if rank == 0 else [0] * 9, COLL_DEV, dist)
     mb = float(np.float32(bf) / np.float32(fx))
 
-    pool = make_pool(args.pool, 2 + 100 * rank)
+    pool = make_pool(args.pool, rank, world)
     if args.no_c2:   # profiling of the other legs only (e.g. the C3 rocprofv3 summary): no headline value
         out = {"metric": "frames/sec ORB extract+match @1241x376 (1 GPU) + LocalBA keyframes/sec", "value": None,
                "unit": "stereo frames/s", "n_gpus": world, "note": "--no-c2: headline leg skipped"}

@@ -117,6 +117,11 @@ int orbm_stereo_match(orbx_engine *left, orbx_engine *right, float mbf, float mb
  * pair p. Results stay on device: u_right / depth [n_pairs][cap]. */
 int orbm_stereo_match_batch_device(orbx_engine *e, int n_pairs, float mbf, float mb, void *stream);
 
+/* Provenance: 16 hex digits of SHA-256 over the library's sources (tools/src_hash.py), baked in
+ * at build time. Not a reference interface: profiles/ summaries carry it so a benchmark can tell
+ * whether committed counter figures were measured on the library it runs. */
+const char *orbx_build_id(void);
+
 /* -------- stereo batch pipeline (Frame::Frame stereo constructor, Frame.cc:144-160, over a batch
  * of pairs) -------- */
 typedef struct orbx_pipeline orbx_pipeline;

@@ -72,6 +72,7 @@ def lib() -> C.CDLL:
         L.orc_orb_descriptor.argtypes = [P, C.c_int, C.c_float, C.c_float, C.c_float, P, P]
         L.orc_descriptor_distance.argtypes = [P, P]
         L.orc_level_candidates.argtypes = [C.POINTER(OrcExtractor), C.c_int, P, C.c_int]
+        L.orc_level_candidates_cells.argtypes = [C.POINTER(OrcExtractor), C.c_int, P, C.c_int, P, P]
         L.orc_distribute_octtree.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]
         L.orc_stereo_matches.argtypes = [C.POINTER(OrcExtractor), C.POINTER(OrcExtractor), P, P, C.c_int,
                                          P, P, C.c_int, C.c_float, C.c_float, P, P]
@@ -173,6 +174,16 @@ class Extractor:
         out = np.zeros(cap, KP_DTYPE)
         n = lib().orc_level_candidates(C.byref(self.s), l, _p(out), cap)
         return out[:n].copy()
+
+    def level_candidates_cells(self, l: int):
+        """(candidates, per-visited-cell candidate counts) of level l after extract()."""
+        w, h = self.s.lw[l], self.s.lh[l]
+        cap = w * h // 2 + 16
+        out = np.zeros(cap, KP_DTYPE)
+        counts = np.zeros((w // 30 + 2) * (h // 30 + 2), np.int32)
+        nc = C.c_int()
+        n = lib().orc_level_candidates_cells(C.byref(self.s), l, _p(out), cap, _p(counts), C.byref(nc))
+        return out[:n].copy(), counts[: nc.value].copy()
 
 
 def stereo_matches(exL: Extractor, exR: Extractor, kL, dL, kR, dR, mbf, mb):

@@ -391,13 +391,26 @@ int orc_fast_roi(const uint8_t *img, int stride, int rows, int cols, int thresho
 /* ------------------------------------------------------------------------------------
  * ComputeKeyPointsOctTree cell loop (ORBextractor.cc:1046-1153), one level.
  * ----------------------------------------------------------------------------------*/
+static int level_candidates(const orc_extractor *ex, int level, orc_kp *out, int cap, int *cell_counts,
+                            int *ncells);
 int orc_level_candidates(const orc_extractor *ex, int level, orc_kp *out, int cap) {
+    return level_candidates(ex, level, out, cap, NULL, NULL);
+}
+/* the same, plus the candidate count of every FAST cell in visiting order (cells skipped by the
+ * bounds tests at :1094 / :1112 are not visited); cell_counts holds nRows * nCols entries */
+int orc_level_candidates_cells(const orc_extractor *ex, int level, orc_kp *out, int cap, int *cell_counts,
+                               int *ncells) {
+    return level_candidates(ex, level, out, cap, cell_counts, ncells);
+}
+static int level_candidates(const orc_extractor *ex, int level, orc_kp *out, int cap, int *cell_counts,
+                            int *ncells) {
     const float W = 30;
     const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
     const int maxBorderX = ex->lw[level] - EDGE_THRESHOLD + 3;
     const int maxBorderY = ex->lh[level] - EDGE_THRESHOLD + 3;
     const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
     const int nCols = (int)(width / W), nRows = (int)(height / W);
+    if (ncells) *ncells = 0;
     if (nCols <= 0 || nRows <= 0) return 0;
     const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
     const uint8_t *img = ex->level[level];
@@ -420,6 +433,7 @@ int orc_level_candidates(const orc_extractor *ex, int level, orc_kp *out, int ca
             const uint8_t *roi = img + (size_t)r0 * stride + c0;
             int m = orc_fast_roi(roi, stride, r1 - r0, c1 - c0, ex->iniThFAST, xs, ys, sc, tmpcap);
             if (m == 0) m = orc_fast_roi(roi, stride, r1 - r0, c1 - c0, ex->minThFAST, xs, ys, sc, tmpcap);
+            if (cell_counts) cell_counts[(*ncells)++] = m;
             for (int k = 0; k < m; k++) {
                 if (n < cap) {
                     orc_kp kp = {(float)xs[k], (float)ys[k], 7.f, -1.f, (float)sc[k], 0, -1};

@@ -73,6 +73,11 @@ int  orc_descriptor_distance(const uint8_t *a, const uint8_t *b);
 /* level-wise candidates: FAST cell grid of one level (ORBextractor.cc:1046-1153).
  * Returns the candidate count (candidate coordinates are cell-offset, origin minBorder). */
 int  orc_level_candidates(const orc_extractor *ex, int level, orc_kp *out, int cap);
+/* + the candidate count of each visited FAST cell, in visiting order (*ncells of them; cell_counts
+ * holds at least nRows * nCols ints): the allocation pattern of the per-cell vKeysCell vectors,
+ * for the glibc pointer-order harness (oracle/tools/qt_glibc_order.cpp) */
+int  orc_level_candidates_cells(const orc_extractor *ex, int level, orc_kp *out, int cap,
+                                int *cell_counts, int *ncells);
 /* DistributeOctTree (ORBextractor.cc:696-1042); returns kept count. */
 int  orc_distribute_octtree(const orc_kp *keys, int nkeys, int minX, int maxX, int minY,
                             int maxY, int N, orc_kp *out, int cap);

@@ -33,6 +33,10 @@ using namespace orbamd;
 namespace orbframe {
 
 constexpr int GRID_COLS = 64, GRID_ROWS = 48;   // Frame.h:55-60
+// LDS of one search_init_resolve_kernel workgroup: list stage + per-F1 prefix + vMatchedDistance /
+// v21 / M12 (u16) + rotation bins (i8). 64 KB holds a 4096-keypoint frame (fixed part 45,076 B,
+// stage 5,115 entries >= cap0); two workgroups still fit a CU's 160 KB.
+constexpr size_t kSearchLds = 64 * 1024;
 
 struct Camera {
     double fx, fy, cx, cy;
@@ -557,9 +561,9 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
     a.check_ori = check_ori;
     a.list = S.list.as<uint32_t>();
     a.lcnt = S.lcnt.as<int>();
-    // phase B LDS: stage + prefix + vMD/v21/M12 (u16) + bins (i8); stage gets the rest of 60 KB
+    // phase B LDS: stage + prefix + vMD/v21/M12 (u16) + bins (i8); stage gets the rest of kSearchLds
     const size_t fixed = 4 * ((size_t)cap0 + 1) + 7 * (size_t)cap + 16;
-    a.stage_cap = (int)std::min<size_t>(16384, (60 * 1024 - fixed) / 4);
+    a.stage_cap = (int)std::min<size_t>(16384, (kSearchLds - fixed) / 4);
     if (a.stage_cap < cap0) return ORBX_EINVAL;
     const size_t lds = 4 * (size_t)a.stage_cap + fixed;
     ph = prof_begin(e, s);
@@ -624,9 +628,9 @@ int orbm_search_for_initialization(orbm_matcher *m, const orbm_frame *F1, const 
     if (sort_cap > 4096) return ORBX_EINVAL;   // one workgroup's LDS sort of F2's grid keys
     const int cap0 = cap;                     // every F1 keypoint may be of octave 0
     const size_t fixed = 4 * ((size_t)cap0 + 1) + 7 * (size_t)cap + 16;
-    if (fixed >= 60 * 1024) return ORBX_EINVAL;
+    if (fixed >= kSearchLds) return ORBX_EINVAL;
     SearchArgs a;
-    a.stage_cap = (int)std::min<size_t>(16384, (60 * 1024 - fixed) / 4);
+    a.stage_cap = (int)std::min<size_t>(16384, (kSearchLds - fixed) / 4);
     if (a.stage_cap < cap0) return ORBX_EINVAL;
     FR_CHK(hipSetDevice(m->device));
     const hipStream_t s = m->stream;

@@ -20,6 +20,7 @@
 
 #include "orbslam2_amd.h"
 #include "orb_engine.h"
+#include "build_id.h"   // ORBX_SRC_HASH (Makefile, tools/src_hash.py)
 
 static void orbx_engine_fb_gate(orbx_engine *e, hipEvent_t ev) { e->fb_gate = ev; }
 
@@ -37,6 +38,7 @@ struct orbx_pipeline {
     void *slot_buf[2] = {nullptr, nullptr};
     size_t slot_bytes = 0;
     int next_slot = 0;
+    int slot_pairs[2] = {0, 0};          // pair count of the last batch uploaded into each slot
     std::vector<hipEvent_t> ev_h2d[2];   // chunk j of slot s uploaded
     std::vector<hipEvent_t> ev_free[2];  // engine j finished reading slot s (stereo done)
     std::vector<bool> free_rec[2];
@@ -86,7 +88,9 @@ static int pipeline_run(orbx_pipeline *pl, const uint8_t *d_imgs, int n_pairs, i
         if (rc) return rc;
         if (hipEventRecord(pl->ev_p1[j], s) != hipSuccess) return ORBX_EDEVICE;
         pl->last_p1 = j;
-        if (host && pl->d2h_rec[j] && hipStreamWaitEvent(s, pl->ev_d2h[j], 0) != hipSuccess) return ORBX_EDEVICE;
+        // phase 2 overwrites the engine's keypoint / descriptor / stereo buffers: whatever mode this
+        // batch is in, they may still be draining to the host from an earlier host-mode batch
+        if (j < (int)pl->d2h_rec.size() && pl->d2h_rec[j] && hipStreamWaitEvent(s, pl->ev_d2h[j], 0) != hipSuccess) return ORBX_EDEVICE;
         rc = orbx_extract_batch_device_phase(e, src, n_img, w, h, pitch, image_stride, s, 2);
         if (rc) return rc;
         rc = orbm_stereo_match_batch_device(e, pl->count[j], mbf, mb, s);
@@ -118,6 +122,8 @@ static int pipeline_run(orbx_pipeline *pl, const uint8_t *d_imgs, int n_pairs, i
 }
 
 extern "C" {
+
+const char *orbx_build_id(void) { return ORBX_SRC_HASH; }
 
 int orbx_pipeline_create(const orbx_params *p, int n_engines, orbx_pipeline **out) {
     if (!p || !out) return ORBX_EINVAL;
@@ -237,6 +243,16 @@ int orbx_pipeline_stereo_batch_host(orbx_pipeline *pl, const uint8_t *h_imgs, in
     const int sl = pl->next_slot;
     pl->next_slot ^= 1;
     uint8_t *dev = (uint8_t *)pl->slot_buf[sl];
+    // Chunk j's upload overwrites the range engine j read in this slot's previous batch. With the
+    // same pair count the chunk ranges coincide and waiting for engines 0..j suffices (the waits
+    // pile up on the H2D stream); with a different count chunk j can cover an old range of any
+    // engine, so the first upload waits for every engine's last read of the slot.
+    if (pl->slot_pairs[sl] != n_pairs) {
+        for (int j = 0; j < k; j++)
+            if (pl->free_rec[sl][j] && hipStreamWaitEvent(pl->h2d, pl->ev_free[sl][j], 0) != hipSuccess)
+                return ORBX_EDEVICE;
+        pl->slot_pairs[sl] = n_pairs;
+    }
     for (int j = 0; j < k; j++) {
         const int first = (int)((long long)n_pairs * j / k), cnt = (int)((long long)n_pairs * (j + 1) / k) - first;
         if (pl->free_rec[sl][j] && hipStreamWaitEvent(pl->h2d, pl->ev_free[sl][j], 0) != hipSuccess) return ORBX_EDEVICE;

@@ -83,6 +83,7 @@ SIGNATURES = [
     ("orbm_hamming_best2_cand_device", _I, [_P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
     ("orbm_search_for_initialization", _I, [_P, _P, _P, _P, _P, _I, _P]),
     ("orbslam2_amd_version", C.c_char_p, []),
+    ("orbx_build_id", C.c_char_p, []),
     ("orbslam2_amd_device_count", _I, []),
     ("orbslam2_amd_device_sync", _I, []),
     ("orbslam2_amd_set_device", _I, [_I]),
@@ -200,6 +201,11 @@ def _check(rc: int, what: str):
 
 def _p(a: np.ndarray) -> C.c_void_p:
     return C.c_void_p(a.ctypes.data)
+
+
+def build_id() -> str:
+    """Hash of the sources the loaded library was built from (tools/src_hash.py)."""
+    return lib().orbx_build_id().decode()
 
 
 def device_count() -> int:
@@ -482,8 +488,12 @@ class StereoPipeline:
     def stereo_batch_host(self, h_imgs: np.ndarray, n_pairs: int, w: int, h: int, pitch: int, image_stride: int,
                           mbf: float, mb: float, out: "StereoHostBatch"):
         """Host images in (ideally host_empty memory), host outputs into `out`; asynchronous until wait()."""
+        # the C side uploads whole image_stride blocks (2 * n_pairs of them) and writes
+        # 2 * n_pairs * capacity() records into out's page-locked arrays, with no sizes to check against
         if not h_imgs.flags.c_contiguous or h_imgs.nbytes < 2 * n_pairs * image_stride:
             raise ValueError("h_imgs must be a contiguous buffer of 2 * n_pairs images")
+        if not isinstance(out, StereoHostBatch) or out.n_pairs < n_pairs or out.cap != self.capacity():
+            raise ValueError("out must be a StereoHostBatch of >= n_pairs pairs with cap == capacity()")
         _check(lib().orbx_pipeline_stereo_batch_host(self._h, C.c_void_p(h_imgs.ctypes.data), n_pairs, w, h, pitch,
                                                      image_stride, mbf, mb, C.byref(out.c)),
                "orbx_pipeline_stereo_batch_host")
@@ -603,7 +613,11 @@ class ORBmatcher:
         off = idx = None
         if cand_off is not None:
             off = np.ascontiguousarray(cand_off, np.int32)
+            if off.ndim != 1 or len(off) != n + 1:
+                raise ValueError("cand_off must hold len(q) + 1 offsets")
             idx = np.ascontiguousarray(cand_idx if cand_idx is not None else np.zeros(0), np.int32)
+            if off[0] < 0 or np.any(np.diff(off) < 0) or off[-1] > len(idx):
+                raise ValueError("cand_off must be non-decreasing offsets into cand_idx")
             if len(idx) == 0:
                 idx = np.zeros(1, np.int32)
         _check(lib().orbm_hamming_best2_cand(self._h, _p(q), n, _p(db), len(db), _p(off) if off is not None else None,
@@ -623,7 +637,8 @@ class ORBmatcher:
                              *[float(v) for v in b]), (ku, de)
         f1, keep1 = frame(F1)
         f2, keep2 = frame(F2)
-        if vbPrevMatched.dtype != np.float32 or not vbPrevMatched.flags.c_contiguous:
+        if (vbPrevMatched.dtype != np.float32 or not vbPrevMatched.flags.c_contiguous
+                or vbPrevMatched.size < 2 * f1.n):
             raise ValueError("vbPrevMatched must be a C-contiguous float32 (n1, 2) array (updated in place)")
         m12 = np.full(max(f1.n, 1), -1, np.int32)
         n = C.c_int32()

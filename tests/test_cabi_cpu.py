@@ -52,3 +52,14 @@ def test_pipeline_argument_errors_without_gpu():
     assert lib.orbx_pipeline_chunk(None, 0, None, None, None) == einval
     assert lib.orbx_pipeline_engines(None) == 0
     assert lib.orbx_extract_batch_device_phase(None, None, 2, 1241, 376, 1241, 1241 * 376, None, 1) == einval
+
+
+def test_build_id_matches_sources():
+    """The library carries the hash of the sources it was built from (orbx_build_id); the tree's
+    library must be built from the tree's sources, so profiles/ stamps can be matched against it."""
+    import subprocess
+    import sys
+    import orbslam2_amd as amd
+    want = subprocess.run([sys.executable, str(ROOT / "tools" / "src_hash.py")], capture_output=True, text=True,
+                          check=True).stdout.strip()
+    assert amd.build_id() == want

@@ -123,3 +123,44 @@ def test_hamming_best2_candidate_lists(amd):
     fi, fd, fs = amd.ORBmatcher.hamming_best2(q, db)
     assert np.array_equal(bi2, fi) and np.array_equal(bd2, fd) and np.array_equal(sd2, fs)
     m.close()
+
+
+def _random_frame(rng, n, bounds):
+    """n keypoints spread over the image, every third of octave 0 (the ones SearchForInitialization
+    queries), random angles / descriptors."""
+    k = np.zeros(n, dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+    k["x"] = rng.uniform(bounds[0], bounds[1], n).astype(np.float32)
+    k["y"] = rng.uniform(bounds[2], bounds[3], n).astype(np.float32)
+    k["size"] = 31
+    k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+    k["octave"] = np.where(np.arange(n) % 3 == 0, 0, rng.integers(1, 8, n))
+    k["class_id"] = -1
+    d = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    return k, d
+
+
+@pytest.mark.parametrize("n", [4094, 4096])
+def test_search_for_initialization_max_frame(amd, oracle_mod, n):
+    """The documented limit F1->n, F2->n <= 4096 (orbslam2_amd.h) holds at the limit; 4097 is refused."""
+    rng = np.random.default_rng(n)
+    bounds = oracle_mod.image_bounds(640, 480, K_TUM, D_TUM)
+    k1, d1 = _random_frame(rng, n, bounds)
+    k2 = k1.copy()                                   # F2: F1 shifted by < 2 px, descriptors with a few flips
+    k2["x"] += rng.uniform(-2, 2, n).astype(np.float32)
+    k2["y"] += rng.uniform(-2, 2, n).astype(np.float32)
+    k2["angle"] = np.mod(k2["angle"] + rng.uniform(-5, 5, n), 360).astype(np.float32)
+    d2 = d1.copy()
+    d2[:, 3] ^= rng.integers(0, 256, n, dtype=np.uint8) & 0x21
+    G1, G2 = oracle_mod.Grid(k1, d1, bounds), oracle_mod.Grid(k2, d2, bounds)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    nm, r12, prev_ref = oracle_mod.search_for_initialization(G1, G2, prev.copy(), 20, 0.9, True)
+    m = amd.ORBmatcher(0.9, True)
+    gn, g12 = m.SearchForInitialization((k1, d1, bounds), (k2, d2, bounds), prev, 20)
+    assert gn == nm and nm > n // 6
+    np.testing.assert_array_equal(g12, r12)
+    assert prev.tobytes() == prev_ref.tobytes()
+    k3, d3 = _random_frame(rng, 4097, bounds)
+    with pytest.raises(amd.OrbslamError):
+        m.SearchForInitialization((k3, d3, bounds), (k2, d2, bounds), np.zeros((4097, 2), np.float32), 20)
+    m.close()

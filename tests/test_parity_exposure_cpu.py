@@ -39,3 +39,26 @@ def test_parity_exposure_quick(oracle_mod, monkeypatch, capsys):
     # the instruments are off again: the pinned oracle is unchanged
     img_ok = rep["C1"]["quadtree_levels"] == 8
     assert img_ok
+
+
+def test_glibc_pointer_order_harness(oracle_mod):
+    """oracle/tools/qt_glibc_order.cpp: with creation-order ties it reproduces
+    orc_distribute_octtree exactly; with real heap addresses (std::list<ExtractorNode> in fresh
+    std::threads) the result is a quadtree output of (within the cut's overshoot) the same size that shares >= 95 % of
+    each image's keypoints with the pin. Full run: tools/qt_glibc_order.py ->
+    profiles/r02_parity_exposure.json["glibc_pointer_order"]."""
+    import qt_glibc_order as q
+    from orbslam2_amd import synth
+    L = q.harness()
+    inputs = [q.level_inputs(im) for im in synth.stereo_pair(376, 1241, 0)]
+    pin, _ = q.run(L, inputs, 0, 1)
+    for i, levels in enumerate(inputs):
+        for l, (cand, _, b, N, _) in enumerate(levels):
+            assert oracle_mod.distribute_octtree(cand, b[0], b[1], b[2], b[3], N).tobytes() == pin[i][l].tobytes()
+    for ctx in (0, 1, 2):
+        real, st = q.run(L, inputs, ctx, 0)
+        c = q.compare(real, pin)
+        assert st["levels_reaching_final_phase"] == 16 and st["equal_size_pairs"] > 0
+        assert c["min_keypoint_set_shared"] >= 0.95
+        # the final-phase cut may overshoot N by up to 3 nodes, differently per order
+        assert all(abs(len(a) - len(b)) <= 3 for a, b in zip(real[0], pin[0]))

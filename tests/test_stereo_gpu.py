@@ -149,3 +149,40 @@ def _check_pair(got, ref, what):
     assert gkL.tobytes() == kL.tobytes() and np.array_equal(gdL, dL), what + " left"
     assert gkR.tobytes() == kR.tobytes() and np.array_equal(gdR, dR), what + " right"
     assert gu.tobytes() == u.tobytes() and gd.tobytes() == d.tobytes(), what + " stereo"
+
+
+def test_stereo_pipeline_host_mode_varying_batches(amd, oracle_mod):
+    """Host-mode batches of 10, 5 and 8 pairs (slot 0, slot 1, slot 0 again): the third batch's
+    chunk ranges in slot 0 straddle the first batch's, so its uploads must wait for every engine's
+    reads of the first batch, not only engines 0..j. Then a device-input batch is enqueued before
+    wait(): its phase 2 must not overwrite outputs still draining to the host."""
+    import torch
+    h, w, k = 376, 1241, 3
+    pairs = [synth.stereo_pair(h, w, 60 + p) for p in range(10)]
+    refs = [_stereo_ref_full(oracle_mod, *pr) for pr in pairs]
+    sizes = (10, 5, 8)
+    order = [[(p * 3 + b) % 10 for p in range(P)] for b, P in enumerate(sizes)]
+    ins = []
+    for b, P in enumerate(sizes):
+        a = amd.host_empty((2 * P, h, w), np.uint8)
+        for p, q in enumerate(order[b]):
+            a[2 * p], a[2 * p + 1] = pairs[q]
+        ins.append(a)
+    pl = amd.StereoPipeline(2000, n_engines=k)
+    pl.reserve(w, h, 10)
+    cap = pl.capacity()
+    outs = [amd.StereoHostBatch(P, cap) for P in sizes]
+    with pytest.raises(ValueError):
+        pl.stereo_batch_host(ins[0], 10, w, h, w, w * h, KITTI_BF, 0.5, amd.StereoHostBatch(4, cap))
+    mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    for b, P in enumerate(sizes):
+        pl.stereo_batch_host(ins[b], P, w, h, w, w * h, KITTI_BF, mb, outs[b])
+    dev = torch.from_numpy(np.flip(ins[0], axis=0).copy()).cuda()   # reversed: other content per engine
+    torch.cuda.synchronize()
+    pl.stereo_batch(dev.data_ptr(), 10, w, h, w, h * w, KITTI_BF, mb)
+    pl.wait()
+    for b, P in enumerate(sizes):
+        for p, q in enumerate(order[b]):
+            _check_pair(outs[b].pair(p), refs[q], f"batch {b} pair {p}")
+    torch.cuda.synchronize()
+    pl.close()

@@ -8,6 +8,10 @@ single-workgroup kernels, on the one CU that runs them (4 SIMDs).
 import csv
 import json
 import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from stamp import stamp  # noqa: E402
 from collections import defaultdict
 
 CLK, SIMDS = 2.4e9, 1024
@@ -39,7 +43,7 @@ for k, v in cnt.items():
     if wgs == 1:
         e["mfma_util_own_cu"] = round(busy / (d * CLK * 4), 4)
     out[k] = e
-rep = {"source": sys.argv[1:3], "clock_hz": CLK, "kernels": out}
+rep = {"stamp": stamp(), "source": sys.argv[1:3], "clock_hz": CLK, "kernels": out}
 txt = json.dumps(rep, indent=1)
 if len(sys.argv) > 3:
     open(sys.argv[3], "w").write(txt + "\n")

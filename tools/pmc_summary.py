@@ -8,12 +8,18 @@ are uncalibrated there, so the figure is an estimate; ratios between variants ar
 Usage: pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <batch> <out.json> [<pmc_SQ_INSTS_VALU dir>]
 With the optional SQ_INSTS_VALU pass, each kernel also gets its VALU wave-instructions per
 launch (a wave64 VALU instruction occupies a 16-lane SIMD for 4 cycles).
+The summary is stamped (tools/stamp.py) with the library's source hash, the commit (GIT_HEAD in
+the environment), the batch per launch and the resize mode (RESIZE_MODE, default 0): bench.py
+reports these counters only for the library and configuration they were measured on.
 """
 import csv
 import json
 import sys
 from collections import defaultdict
 from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from stamp import stamp  # noqa: E402
 
 
 def short(name: str) -> str:
@@ -45,7 +51,7 @@ def main():
                   "hbm_bytes_per_launch": int((2 * f_avg + w_avg) * 1024)}
         if valu.get(k):
             res[k]["valu_insts_per_launch"] = int(sum(valu[k]) / len(valu[k]))
-    doc = {"batch": batch, "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE read correction)",
+    doc = {"stamp": stamp(batch=batch), "batch": batch, "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE read correction)",
            "kernels": res}
     out.write_text(json.dumps(doc, indent=1))
     print(json.dumps(doc, indent=1))
