@@ -59,9 +59,15 @@ def make_pool(n_pairs: int, rank: int, world: int):
     SURVEY §8d's eight independent streams, seeds 10..17, one per rank: rank r's frame t is
     generated from seed 10 + r + 8 t, so no two ranks share a frame."""
     from orbslam2_amd import synth
+    POOL_SEEDS.clear()
     if world == 1:
+        POOL_SEEDS.extend(2 + t for t in range(n_pairs))
         return [synth.stereo_pair(H, W, t) for t in range(n_pairs)]
+    POOL_SEEDS.extend(10 + rank + 8 * t for t in range(n_pairs))
     return [synth.stereo_pair(H, W, 8 * t, base_seed=10 + rank) for t in range(n_pairs)]
+
+
+POOL_SEEDS = []   # left-image generator seed of each pool pair (make_pool)
 
 
 def host_cpu():
@@ -299,6 +305,7 @@ def bench_c2(amd, args, dist, world, params, pool):
     if len(k0) < 100 or n_match < 10:
         raise RuntimeError(f"implausible output: {len(k0)} keypoints, {n_match} stereo matches")
     engines = len(ex.engines)
+    parity = c2_parity(ex, args, params, pool) if args.check_parity else None
     ex.close()
 
     frames = B * args.steps * world
@@ -351,22 +358,16 @@ def bench_c2(amd, args, dist, world, params, pool):
             out["roofline"]["valu_issue_frac"] = round(
                 valu * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (tot / n / 1e3), 4)
             out["roofline"]["valu_insts_per_launch"] = valu
-        if pmc:
-            # the whole step against VALU issue: every kernel's VALU instructions per launch (PMC) x
-            # its launches per timed step (live profile) x 4 cycles / (1024 SIMDs x 2.4 GHz) / ms_per_step
-            insts = 0.0
-            missing = []
-            for k, (_, kn) in prof.items():
-                v = (pmc.get(k) or {}).get("valu_insts_per_launch")
-                if v is None:
-                    missing.append(k)
-                    continue
-                insts += v * kn / args.steps
+        steps_prof = (pmc or {}).get("__stamp__", {}).get("steps_profiled")
+        if pmc and steps_prof:
+            # the whole step against VALU issue: every kernel dispatch of a step in the PMC pass (its
+            # VALU instructions per dispatch x dispatches per step; the rocclr setup copies excluded)
+            # x 4 cycles / (1024 SIMDs x 2.4 GHz), over this run's ms_per_step
+            insts = sum(v["valu_insts_per_launch"] * v["launches"] / steps_prof for k, v in pmc.items()
+                        if k != "__stamp__" and not k.startswith("__amd_rocclr_copy") and "valu_insts_per_launch" in v)
             out["roofline"]["step_valu_insts"] = int(insts)
             out["roofline"]["step_valu_issue_frac"] = round(
                 insts * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (ms_step / 1e3), 4)
-            if missing:
-                out["roofline"]["step_valu_missing_kernels"] = missing
         # summed over the engines' launches, which overlap in time (so the sum exceeds ms_per_step)
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
         out["kernel_launches_per_step"] = {k: round(v[1] / args.steps, 3) for k, v in sorted(prof.items())}
@@ -386,6 +387,8 @@ def bench_c2(amd, args, dist, world, params, pool):
             if valu:
                 out["roofline"]["isolated"]["valu_issue_frac"] = round(
                     valu * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (iso_ms / 1e3), 4)
+    if parity is not None:
+        out["parity_check"] = {"c2": gather_ranks(parity, dist)}
     if not args.no_alt_resize:
         alt = 1 - args.resize_mode
         a_el, _, a_ex = time_c2(amd, args, dist, params, bufs, alt, args.steps)
@@ -397,6 +400,50 @@ def bench_c2(amd, args, dist, world, params, pool):
                                           "vertical-pass variant; both variants are parity-tested on the GPU"}
     del bufs   # the resident batches are not needed by the legs below
     return out
+
+
+def gather_ranks(obj, dist):
+    """Every rank's `obj`, in rank order (one all_gather_object; outside the timed regions)."""
+    if dist is None:
+        return [obj]
+    lst = [None] * dist.get_world_size()
+    dist.all_gather_object(lst, obj)
+    return lst
+
+
+def c2_parity(ex, args, params, pool):
+    """--check-parity (C5 rehearsal): every pair of this rank's last timed batch
+    against the CPU oracle (extract L + R + ComputeStereoMatches on the same pair, same resize
+    mode): keypoints, descriptors, mvuRight and mvDepth bit-exact. After the timed region."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    nf, sf, nl, ith, mth, bf, mb = params
+    kb = (args.steps - 1) % args.bufs   # c2_buffers' batch the last timed step ran on
+    cache, bad = {}, []
+    for i in range(args.batch):
+        j = (i + 3 * kb) % len(pool)
+        if j not in cache:
+            L, R = pool[j]
+            if kb:
+                L, R = np.roll(L, 7 * kb, axis=1), np.roll(R, 7 * kb, axis=1)
+            oL = oracle.Extractor(int(nf), float(sf), int(nl), int(ith), int(mth), resize_mode=args.resize_mode)
+            oR = oracle.Extractor(int(nf), float(sf), int(nl), int(ith), int(mth), resize_mode=args.resize_mode)
+            kL, dL = oL.extract(L)
+            kR, dR = oR.extract(R)
+            u, d = oracle.stereo_matches(oL, oR, kL, dL, kR, dR, float(bf), mb)
+            cache[j] = (kL, dL, kR, dR, u, d)
+        rkL, rdL, rkR, rdR, ru, rd = cache[j]
+        gkL, gdL, gkR, gdR = ex.fetch(i)
+        gu, gd = ex.stereo_fetch(i)
+        n = len(rkL)
+        ok = (gkL.tobytes() == rkL.tobytes() and np.array_equal(gdL, rdL) and gkR.tobytes() == rkR.tobytes()
+              and np.array_equal(gdR, rdR) and gu[:n].tobytes() == ru.tobytes() and gd[:n].tobytes() == rd.tobytes())
+        if not ok:
+            bad.append(i)
+    rank = int(os.environ.get("RANK", "0"))
+    return {"rank": rank, "pairs_checked": args.batch, "pairs_bit_exact": args.batch - len(bad),
+            "first_mismatch": bad[:4], "distinct_pairs": len(cache), "left_seed_first_pair": POOL_SEEDS[0],
+            "resize_mode": args.resize_mode}
 
 
 def isolated_launch_ms(amd, params, buf, pairs, name, resize_mode=0, reps=5):
@@ -463,6 +510,21 @@ def bench_localba(amd, args, dist, world, with_cpu):
         r = lba.solve(prob)
     dt = time.perf_counter() - t0
     dt = odist.max_over_ranks(dt, COLL_DEV, dist)
+    parity = None
+    if args.check_parity:   # this rank's LocalBA on the broadcast map vs the oracle (1e-4, same LM, same erase set)
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+        ref = oracle.lba_solve(prob)
+
+        def rel(a, b):
+            a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+            return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-12))
+        pr, xr = rel(r["pose_Tcw"], ref["pose_Tcw"]), rel(r["point_Xw"], ref["point_Xw"])
+        parity = {"rank": rank, "map_bytes": map_bytes, "pose_rel": pr, "point_rel": xr,
+                  "same_lm_iterations": list(r["iterations"]) == list(ref["iterations"]),
+                  "same_erase_set": bool(np.array_equal(r["edge_erase"], ref["edge_erase"])),
+                  "within_1e-4": pr < 1e-4 and xr < 1e-4}
+        parity = gather_ranks(parity, dist)
     res = {"localba_kf_per_s": round(world * args.lba_steps / dt, 3),
            "localba": {"ms_per_call": round(1000 * dt / args.lba_steps, 3), "edges": int(len(prob["edge_point"])),
                        "keyframes": 20, "map_points": 3000, "lm_iterations": list(r["iterations"]),
@@ -470,7 +532,8 @@ def bench_localba(amd, args, dist, world, with_cpu):
                        "dtype": "f64", "lm_control": "device-resident LM state, decided in lba_errors' last block; "
                                                      "one host readback per chunk of trials",
                        "map_snapshot_bytes": map_bytes,
-                       "map_source": "rank 0, RCCL broadcast" if dist is not None else "local"}}
+                       "map_source": (f"rank 0, {'RCCL' if DIST_BACKEND == 'nccl' else DIST_BACKEND} broadcast"
+                                      if dist is not None else "local")}}
     # roofline: algorithmic FP64 flops per LM trial over the measured device time of
     # one trial, against the FP64 matrix peak; the Schur SYRK alone against the same peak
     ncall = 5
@@ -496,6 +559,8 @@ def bench_localba(amd, args, dist, world, with_cpu):
                  "frac": round(fl["schur"] / syrk_avg_s / 1e12 / FP64_MFMA_PEAK_TFS, 5) if syrk_avg_s > 0 else None},
         "peak_source": "v_mfma_f64_16x16x4_f64 measured on this MI355X (tools/microbench/mfma_f64_peak.hip; AMD spec 78.6)",
         "pmc": pmc, "pmc_source": pmc_note}
+    if parity is not None:
+        res["localba"]["parity_check"] = parity
     res["localba"]["gpu_ms_per_call"] = round(gpu_ms_call, 4)
     res["localba"]["host_ms_per_call"] = round(1000 * dt / args.lba_steps - gpu_ms_call, 4)
     res["localba"]["kernel_ms_per_call"] = {k: round(v[0] / ncall, 4) for k, v in sorted(prof.items())}
@@ -832,6 +897,7 @@ def load_pmc_doc(fname: str, build_id: str, **expect):
         if stamp.get(k) != v:
             return None, f"profiles/{fname} stamp {k}={stamp.get(k)}, this run {k}={v}: counters not reported"
     kern = {kernel_base(k): v for k, v in doc.get("kernels", {}).items()}
+    kern["__stamp__"] = stamp
     return kern, f"profiles/{fname} (src_hash {build_id}, commit {stamp.get('commit')})"
 
 
@@ -861,6 +927,9 @@ def main():
     ap.add_argument("--resize-mode", type=int, default=0, choices=(0, 1),
                     help="SURVEY A.2 vertical-pass variant of the headline value (0: FixedPtCast, 1: SSE2)")
     ap.add_argument("--no-alt-resize", action="store_true", help="skip the other resize variant's line")
+    ap.add_argument("--check-parity", action="store_true",
+                    help="after timing, check every rank's last C2 batch bit-exact and its LocalBA within 1e-4 "
+                         "against the CPU oracle (C5 rehearsal)")
     ap.add_argument("--bufs", type=int, default=4, help="rotating resident input batches")
     ap.add_argument("--cpu-frames", type=int, default=96)
     ap.add_argument("--no-cpu-baseline", action="store_true")

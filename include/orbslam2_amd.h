@@ -72,6 +72,12 @@ int orbx_extract(orbx_engine *e, const uint8_t *img, int w, int h, int stride, o
 /* mvImagePyramid[level] (ORBextractor.h:158) copied to host (dst may be NULL to query w/h). */
 int orbx_pyramid_level(orbx_engine *e, int image, int level, uint8_t *dst, int *w, int *h);
 
+/* The blurred working copy of mvImagePyramid[level] that computeDescriptors samples:
+ * GaussianBlur(workingMat, workingMat, Size(9, 9), 2, 2, BORDER_REFLECT_101) on a clone of the level
+ * (ORBextractor.cc:1617-1625), copied to host (dst may be NULL to query w/h). Not a reference
+ * interface (the reference keeps it in a local cv::Mat): exposed so the blur is checked directly. */
+int orbx_blurred_level(orbx_engine *e, int image, int level, uint8_t *dst, int *w, int *h);
+
 /* -------- batched device-resident path (many frames per launch) -------- */
 
 /* Size device buffers for up to max_images images of w x h. */

@@ -2154,4 +2154,19 @@ int orbx_pyramid_level(orbx_engine *e, int image, int level, uint8_t *dst, int *
     return ORBX_OK;
 }
 
+int orbx_blurred_level(orbx_engine *e, int image, int level, uint8_t *dst, int *w, int *h) {
+    if (!e || level < 0 || level >= e->p.nlevels) return ORBX_EINVAL;
+    if (e->last_n == 0 || image < 0 || image >= e->last_n) return ORBX_ESTATE;
+    const int lw = e->g.lw[level], lh = e->g.lh[level];
+    if (w) *w = lw;
+    if (h) *h = lh;
+    if (!dst) return ORBX_OK;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamWaitEvent(e->stream, e->done, 0));
+    HIPCHK(hipMemcpy2DAsync(dst, lw, e->d_blur.as<uint8_t>() + image * e->g.blur_stride + e->g.blur_off[level],
+                            e->g.bp[level], lw, lh, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return ORBX_OK;
+}
+
 }  // extern "C"

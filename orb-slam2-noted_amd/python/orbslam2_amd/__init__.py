@@ -53,6 +53,7 @@ SIGNATURES = [
     ("orbx_levels", _I, [_P, _P, _P, _P, _P, _P, _P]),
     ("orbx_extract", _I, [_P, _P, _I, _I, _I, _P, _P, _I, _P]),
     ("orbx_pyramid_level", _I, [_P, _I, _I, _P, _P, _P]),
+    ("orbx_blurred_level", _I, [_P, _I, _I, _P, _P, _P]),
     ("orbx_reserve", _I, [_P, _I, _I, _I]),
     ("orbx_extract_batch_device", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _P]),
     ("orbx_extract_batch_device_phase", _I, [_P, _P, _I, _I, _I, _I, C.c_size_t, _P, _I]),
@@ -292,6 +293,14 @@ class ORBextractor:
         _check(lib().orbx_pyramid_level(self._h, image, level, None, C.byref(w), C.byref(h)), "pyramid")
         out = np.zeros((h.value, w.value), np.uint8)
         _check(lib().orbx_pyramid_level(self._h, image, level, _p(out), None, None), "pyramid")
+        return out
+
+    def blurred_level(self, level: int, image: int = 0) -> np.ndarray:
+        """The 9x9 GaussianBlur of pyramid level `level` that the descriptors sample."""
+        w, h = C.c_int(), C.c_int()
+        _check(lib().orbx_blurred_level(self._h, image, level, None, C.byref(w), C.byref(h)), "blurred")
+        out = np.zeros((h.value, w.value), np.uint8)
+        _check(lib().orbx_blurred_level(self._h, image, level, _p(out), None, None), "blurred")
         return out
 
 

@@ -1,0 +1,50 @@
+"""C5 rehearsal: bench.py's multi-rank path at world size 2 on the one GPU of
+the box, launched as the driver launches it (torch.distributed.run, one process per rank), over
+gloo (ORBSLAM_DIST_BACKEND=gloo: ranks share the card, RCCL needs one GPU per rank). Each rank runs
+its own C2 stream (SURVEY §8d C5 seeds: rank r = seed 10 + r), receives the LocalBA map from rank 0
+by broadcast, and checks with --check-parity its whole last 384-pair batch bit-exact and its
+LocalBA on the broadcast map within 1e-4 (same LM iterations, same erase set) against the oracle.
+The multi-rank timing is a rehearsal, not a measurement (two ranks share one GPU)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_c5_two_ranks_parity():
+    env = dict(os.environ, ORBSLAM_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--check-parity", "--no-cpu-baseline", "--no-latency",
+           "--no-e2e", "--no-rgbd", "--no-track", "--no-pose", "--no-bow", "--no-bowmatch", "--no-newpts",
+           "--no-isolated", "--no-alt-resize", "--lba-steps", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    log = ROOT / "gpurun_out"
+    if log.is_dir():
+        (log / "c5_rehearsal.log").write_text(r.stdout + "\n--- stderr ---\n" + r.stderr)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    print(json.dumps({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "parity_check")}))
+    assert line["n_gpus"] == 2 and "C5" in line["config"]["streams"]
+    c2 = line["parity_check"]["c2"]
+    assert [p["rank"] for p in c2] == [0, 1]
+    assert [p["left_seed_first_pair"] for p in c2] == [10, 11]
+    for p in c2:
+        assert p["pairs_checked"] == 384 and p["pairs_bit_exact"] == 384, p
+    lba = line["localba"]["parity_check"]
+    assert len(lba) == 2 and lba[0]["map_bytes"] == lba[1]["map_bytes"] > 0
+    for p in lba:
+        assert p["within_1e-4"] and p["same_lm_iterations"] and p["same_erase_set"], p

@@ -45,8 +45,32 @@ def test_extract_parity(amd, oracle_mod, name, h, w, nf, mode, seed):
     got = ex(img)
     want = ref.extract(img)
     for l in range(8):
-        np.testing.assert_array_equal(ex.pyramid_level(l), ref.level(l), err_msg=f"pyramid level {l}")
+        lev = ref.level(l)
+        np.testing.assert_array_equal(ex.pyramid_level(l), lev, err_msg=f"pyramid level {l}")
+        # E6 directly: the MFMA blur's every pixel, borders included, against the
+        # GaussianBlur restatement (ORBextractor.cc:1617-1625)
+        np.testing.assert_array_equal(ex.blurred_level(l), oracle_mod.gaussian_blur9(lev), err_msg=f"blurred level {l}")
     _assert_same_kps(got, want, name)
+
+
+@pytest.mark.parametrize("h,w", [(376, 1241), (480, 640), (145, 149), (201, 333), (150, 1024)])
+def test_blurred_pyramid_noise(amd, oracle_mod, h, w):
+    """Blurred pyramid of uniform noise (every byte value) and of 0/255 vertical stripes (the largest
+    row sums, full-scale outputs), byte for byte at every level, odd sizes included (smallest level
+    >= 40 px, the extractor's limit)."""
+    rng = np.random.default_rng(h * 1000 + w)
+    for img in (rng.integers(0, 256, size=(h, w), dtype=np.uint8),
+                np.broadcast_to(((np.arange(w) // 8) % 2 * 255).astype(np.uint8), (h, w)).copy()):
+        ex = amd.ORBextractor(1000, 1.2, 8, 20, 7)
+        ex(img)
+        ref = oracle_mod.Extractor(1000, 1.2, 8, 20, 7)
+        ref.extract(img)
+        for l in range(8):
+            lev = ref.level(l)
+            if lev.size == 0:
+                continue
+            np.testing.assert_array_equal(ex.blurred_level(l), oracle_mod.gaussian_blur9(lev),
+                                          err_msg=f"{h}x{w} blurred level {l}")
 
 
 def test_extract_noise_many_candidates(amd, oracle_mod):

@@ -57,3 +57,14 @@ def test_lba_mono_only_and_fixed(amd, oracle_mod):
     assert _rel(got["pose_Tcw"], ref["pose_Tcw"]) < RTOL
     assert _rel(got["point_Xw"], ref["point_Xw"]) < RTOL
     assert np.array_equal(got["edge_erase"], ref["edge_erase"])
+
+
+def test_golden_c4_on_device(amd):
+    """HIP LocalBA == the committed fixture tests/golden/c4_localba.npz within 1e-4, same LM
+    iterations and erase set (no oracle at run time)."""
+    from test_golden_cpu import load_c4
+    prob, g = load_c4()
+    got = amd.LocalBundleAdjustment().solve(prob)
+    assert tuple(got["iterations"]) == tuple(g["iterations"])
+    assert _rel(got["pose_Tcw"], g["pose_Tcw"]) < RTOL and _rel(got["point_Xw"], g["point_Xw"]) < RTOL
+    assert np.array_equal(got["edge_erase"], g["edge_erase"])

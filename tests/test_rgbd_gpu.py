@@ -106,3 +106,85 @@ def test_search_init_variants(amd, oracle_mod, window, nnratio, check_ori, gap):
         np.testing.assert_array_equal(gm[:n1], m12)
         assert gn == nm
         assert gxy[:n1].tobytes() == prev_out.tobytes()
+
+
+def test_c3_production_shape(amd, oracle_mod):
+    """C3 at bench.py's production shape: batches of 256 TUM RGB-D frames,
+    consecutive batches alternating over 3 engines on their own streams with no synchronisation
+    between them (bench_rgbd), each batch = extract(1000) + UndistortKeyPoints + ComputeStereoFromRGBD
+    + SearchForInitialization over its 255 consecutive pairs. Four batches (engine 0 reused while
+    engines 1 and 2 are in flight), batch b from the 8-frame pool shifted by 3b: every frame's
+    keysUn / mvuRight / mvDepth and every pair's vnMatches12 / vbPrevMatched / count bit-exact.
+    Reference: Frame.cc:725-776, 1131-1169; ORBmatcher.cc:580-748."""
+    import torch
+    T, E, NB = 256, 3, 4
+    pool = [synth.rgbd_frame(480, 640, t) for t in range(8)]
+    ref = [_oracle_frame(oracle_mod, g, d, K_TUM, D_TUM) for g, d in pool]
+    bounds = oracle_mod.image_bounds(640, 480, K_TUM, D_TUM)
+    pair_ref = {}
+    for a in range(8):
+        b = (a + 1) % 8
+        k1, d1, ku1, _, _ = ref[a]
+        _, d2, ku2, _, _ = ref[b]
+        prev = np.stack([ku1["x"], ku1["y"]], 1)
+        pair_ref[a] = oracle_mod.search_for_initialization(oracle_mod.Grid(ku1, d1, bounds),
+                                                           oracle_mod.Grid(ku2, d2, bounds), prev, 100, 0.9, True)
+    ins = []
+    for bi in range(NB):
+        idx = [(t + 3 * bi) % 8 for t in range(T)]
+        g = torch.from_numpy(np.stack([pool[i][0] for i in idx])).cuda()
+        d = torch.from_numpy(np.stack([pool[i][1] for i in idx])).cuda()
+        ins.append((idx, g, d))
+    exs = [amd.BatchExtractor(1000) for _ in range(E)]
+    for ex in exs:
+        ex.reserve(640, 480, T)
+    torch.cuda.synchronize()
+    for bi in range(NB):   # bench_rgbd's step, back to back
+        _, g, d = ins[bi]
+        ex = exs[bi % E]
+        ex.extract_device(g.data_ptr(), T, 640, 480, 640, 640 * 480)
+        ex.rgbd_device(d.data_ptr(), 640 * 480, 640, K_TUM, D_TUM, BF_TUM)
+        ex.search_init_device(T - 1, 0, 1, 1, 1, K_TUM, D_TUM, 100, 0.9, True)
+    amd.device_sync()
+    for bi in range(1, NB):   # batch 0's engine was reused by batch 3
+        idx, _, _ = ins[bi]
+        ex = exs[bi % E]
+        for t in range(T):
+            k, _, ku, u, dep = ref[idx[t]]
+            gku, gu, gd = ex.rgbd_fetch(t)
+            n = len(k)
+            assert gku[:n].tobytes() == ku.tobytes(), f"keysUn batch {bi} frame {t}"
+            assert gu[:n].tobytes() == u.tobytes() and gd[:n].tobytes() == dep.tobytes(), f"depth batch {bi} frame {t}"
+        for p in range(T - 1):
+            nm, m12, prev_out = pair_ref[idx[p]]
+            gn, gm, gxy = ex.search_init_fetch(p)
+            n1 = len(ref[idx[p]][0])
+            assert gn == nm, f"batch {bi} pair {p}"
+            np.testing.assert_array_equal(gm[:n1], m12)
+            assert gxy[:n1].tobytes() == prev_out.tobytes(), f"vbPrevMatched batch {bi} pair {p}"
+
+
+def test_golden_c3_on_device(amd):
+    """HIP C3 path == the committed fixture tests/golden/c3_rgbd_640x480.npz (no oracle at run time)."""
+    import torch
+    from test_golden_cpu import load_c3
+    frames, g = load_c3()
+    cam = g["camera"]
+    K, D, bf = list(cam[:4]), list(cam[4:9]), float(cam[9])
+    dg = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    dd = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    ex = amd.BatchExtractor(1000)
+    ex.reserve(640, 480, 2)
+    torch.cuda.synchronize()
+    ex.extract_device(dg.data_ptr(), 2, 640, 480, 640, 640 * 480)
+    ex.rgbd_device(dd.data_ptr(), 640 * 480, 640, K, D, bf)
+    ex.search_init_device(1, 0, 1, 1, 1, K, D, 100, 0.9, True)
+    for t in (0, 1):
+        gku, gu, gd = ex.rgbd_fetch(t)
+        n = len(g[f"keys_un{t}"])
+        assert gku[:n].tobytes() == g[f"keys_un{t}"].tobytes()
+        assert gu[:n].tobytes() == g[f"u_right{t}"].tobytes() and gd[:n].tobytes() == g[f"depth_out{t}"].tobytes()
+    gn, gm, gxy = ex.search_init_fetch(0)
+    n1 = len(g["matches12"])
+    assert gn == int(g["nmatches"])
+    assert gm[:n1].tobytes() == g["matches12"].tobytes() and gxy[:n1].tobytes() == g["prev_matched"].tobytes()

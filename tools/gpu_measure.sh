@@ -25,7 +25,7 @@ for s in $STEPS; do
         timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $ctr -d "$O/m_pmc_$ctr" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-profile $C2ONLY ${BENCH_ARGS:-} > /dev/null 2> "$O/m_pmc_$ctr.err"
         rc=$?; echo "pmc $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done
-      python3 "$R/tools/pmc_summary.py" "$O/m_pmc_FETCH_SIZE" "$O/m_pmc_WRITE_SIZE" 128 "$O/pmc_traffic.json" "$O/m_pmc_SQ_INSTS_VALU" > /dev/null
+      STEPS_PROFILED=4 python3 "$R/tools/pmc_summary.py" "$O/m_pmc_FETCH_SIZE" "$O/m_pmc_WRITE_SIZE" 128 "$O/pmc_traffic.json" "$O/m_pmc_SQ_INSTS_VALU" > /dev/null
       rc=$?; echo "pmc summary rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     lba)
       timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/m_lba_stats" -o run -- python3 "$R/tools/lba_prof.py" 5 > "$O/m_lba_stats.txt" 2>&1

@@ -14,6 +14,7 @@ reports these counters only for the library and configuration they were measured
 """
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -51,7 +52,10 @@ def main():
                   "hbm_bytes_per_launch": int((2 * f_avg + w_avg) * 1024)}
         if valu.get(k):
             res[k]["valu_insts_per_launch"] = int(sum(valu[k]) / len(valu[k]))
-    doc = {"stamp": stamp(batch=batch), "batch": batch, "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE read correction)",
+    st = stamp(batch=batch)
+    if os.environ.get("STEPS_PROFILED"):   # bench steps (warmup included) the PMC run executed
+        st["steps_profiled"] = int(os.environ["STEPS_PROFILED"])
+    doc = {"stamp": st, "batch": batch, "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE read correction)",
            "kernels": res}
     out.write_text(json.dumps(doc, indent=1))
     print(json.dumps(doc, indent=1))
