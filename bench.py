@@ -545,7 +545,7 @@ def bench_localba(amd, args, dist, world, with_cpu):
     trials = sum(r["trials"])
     fl = lba_flops(prob)
     gpu_ms_call = sum(v[0] for v in prof.values()) / ncall
-    syrk_ms, syrk_n = prof.get("lba_syrk_mfma", (0.0, 1))
+    syrk_ms, syrk_n = prof.get("lba_schur_tiles", (0.0, 1))
     syrk_avg_s = syrk_ms / max(syrk_n, 1) / 1e3
     trial_s = gpu_ms_call / 1e3 / max(trials, 1)
     achieved = fl["per_trial"] / trial_s / 1e12
@@ -554,7 +554,7 @@ def bench_localba(amd, args, dist, world, with_cpu):
         "bound": "mfma", "kernel": "LM trial (linearize .. decide)", "achieved": round(achieved, 5),
         "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP64_MFMA_PEAK_TFS, 7), "traffic": None,
         "algorithmic_flops_per_trial": fl["per_trial"], "flops_split": fl, "trial_ms": round(trial_s * 1e3, 4),
-        "syrk": {"avg_launch_ms": round(syrk_avg_s * 1e3, 4),
+        "schur": {"kernel": "lba_schur_tiles", "avg_launch_ms": round(syrk_avg_s * 1e3, 4),
                  "achieved": round(fl["schur"] / syrk_avg_s / 1e12, 4) if syrk_avg_s > 0 else None,
                  "frac": round(fl["schur"] / syrk_avg_s / 1e12 / FP64_MFMA_PEAK_TFS, 5) if syrk_avg_s > 0 else None},
         "peak_source": "v_mfma_f64_16x16x4_f64 measured on this MI355X (tools/microbench/mfma_f64_peak.hip; AMD spec 78.6)",

@@ -12,11 +12,10 @@
 //                     on the device); one thread per active edge: its 6x3 block of Y = Hpl L
 //                     with L = chol(Dinv); one thread per landmark: Dinv = (Hll + lambda I)^-1
 //                     (Eigen cofactor inverse), w_l = L^T b_l
-//   lba_syrk_mfma     Y [Y; w]^T on FP64 matrix cores (v_mfma_f64_16x16x4f64), Y stored
-//                     transposed, one 4-wave workgroup per 16x16 upper tile per K slice,
-//                     partial slabs reduced in fixed order
-//   lba_schur_reduce  Hschur = Hpp + lambda I - sum(slabs), b_schur = b_p - Y w (one workgroup
-//                     per row: the 1.2 MB of slabs is read by n6 CUs, not one)
+//   lba_schur_tiles   Hschur = Hpp + lambda I - Y Y^T block-sparse on FP64 matrix cores
+//                     (v_mfma_f64_16x16x4f64) over the landmark rows each upper 16 x 16 tile
+//                     pair shares, Y stored transposed, chunks of 32 MFMA steps per 4-wave
+//                     workgroup, lba_schur_finish sums a pair's chunk tiles; b_schur = b_p - Y w
 //   lba_chol_tiled    (6P <= 128) dense Cholesky in LDS over 16-column panels (DPP diagonal
 //                     tiles, FP64 MFMA panel / trailing updates) + the two solves
 //   lba_chol_panel/_update/_solve_blocked  blocked Cholesky for 6P > 128
@@ -35,6 +34,8 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -87,6 +88,7 @@ struct Graph {
     const EdgeDev *E;
     double *err;           // [ne][3] g2o _error
     const int *act;        // active edge indices (edge order)
+    const uint8_t *on;     // per active slot: 1 = level 0; 0 = set to level 1 by the phase-1 outlier test
     int nact;
     const int *pose_hidx;  // per pose vertex, -1 = fixed / inactive
     const int *point_hidx;
@@ -94,6 +96,8 @@ struct Graph {
     int P, Lm;
     const int *pt_start, *pt_items;  // per active point: active slots (all edges of the point)
     const int *ps_start, *ps_items;  // per free pose: active slots
+    const int *slot_ppos;            // per active slot: its position in ps_items (-1 fixed pose)
+    double *ywp;                     // [ps_items][6]: the slot's Y block times w_l (b_schur pieces)
     const int *slot_pt, *slot_ph;    // per active slot: hessian point / pose index (-1 fixed)
     // system
     double *con;           // [nact][36] per-slot Hll(6) bl(3) Hpp(21) bp(6)
@@ -104,16 +108,21 @@ struct Graph {
     double *Lc;            // [Lm][6] chol(Dinv): L00 L10 L20 L11 L21 L22
     double *Y;             // [Kpad][NPW] (point columns major: Y^T); column wrow = w
     double *w;             // = Y + wrow, stride NPW
-    double *slab;          // [S][NP][NPW], NPW = NP + 16 (column wrow: partial Y w)
     double *Hs, *bs;       // [NP][NP], [NP]
     double *x;             // [6P + 3Lm]
     double *partial;       // [4][kRedBlocks]
     double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok, lambda
     LMState *lm;
     unsigned *arrive;      // lba_errors block-arrival counter (the last block runs the LM decision)
-    int Kpad, S;
+    int Kpad;              // Y^T rows 3 Lm rounded up to 4; row Kpad (and up to Kpad + 3) is zero
     int NP;                // Schur dimension 6P padded to a multiple of kCB
-    int NPW, wrow;         // slab leading dimension; Y row holding w (16 * ceil(6P / 16))
+    const int2 *tp_ij;     // upper tile pairs (I, J) of the Schur matrix
+    const int *tp_start, *tp_rows;   // per pair: Y^T rows of the landmarks seen from both tiles (CSR)
+    const int4 *tp_chunk;  // per chunk workgroup: pair, first step, steps, chunk index in the pair
+    const int2 *tp_nch;    // per pair: first chunk, chunk count
+    double *tp_part;       // [nchunks][256] chunk tiles (MFMA C layout)
+    int npairs, nchunks;
+    int NPW, wrow;         // Y^T leading dimension (NP + 16); Y^T column holding w (16 * ceil(6P / 16))
 };
 
 __device__ inline void edge_error(const Graph &g, const EdgeDev &e, const Pose *T, const double *X, double err[3]) {
@@ -164,7 +173,11 @@ __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
     if (g.lm->done || !g.lm->newiter) return;
     const int s = blockIdx.x * 256 + threadIdx.x;
     double rchi = 0;
-    if (s < g.nact) {
+    if (s < g.nact && !g.on[s]) {   // a level-1 edge: no share of the system (its stale _error is kept)
+        double *c = g.con + (long long)s * 36, *hp = g.hpl + (long long)s * 18;
+        for (int u = 0; u < 36; u++) c[u] = 0.0;
+        for (int u = 0; u < 18; u++) hp[u] = 0.0;
+    } else if (s < g.nact) {
         const int k = g.act[s];
         const EdgeDev e = g.E[k];
         double err[3];
@@ -404,12 +417,18 @@ __global__ __launch_bounds__(256) void lba_prep_slots(Graph g, int n0, int n1, i
         point_factor(g, l, lambda, Di, L);
         const double *B = g.hpl + (long long)t * 18;
         double *y = g.Y + 3LL * l * W + 6 * ph;   // Y^T rows 3l..3l+2, columns 6ph..6ph+5
+        // w_l = L^T b_l exactly as the landmark threads form it, for this block's share of Y w
+        const double *bl = g.bl + 3 * l;
+        const double w0 = L[0] * bl[0] + L[1] * bl[1] + L[2] * bl[2], w1 = L[3] * bl[1] + L[4] * bl[2], w2 = L[5] * bl[2];
+        double *yw = g.ywp + 6LL * g.slot_ppos[t];
 #pragma unroll
         for (int r = 0; r < 6; r++) {
             const double b0 = B[3 * r], b1 = B[3 * r + 1], b2 = B[3 * r + 2];
-            y[r] = b0 * L[0] + b1 * L[1] + b2 * L[2];
-            y[W + r] = b1 * L[3] + b2 * L[4];
-            y[2 * W + r] = b2 * L[5];
+            const double y0 = b0 * L[0] + b1 * L[1] + b2 * L[2], y1 = b1 * L[3] + b2 * L[4], y2 = b2 * L[5];
+            y[r] = y0;
+            y[W + r] = y1;
+            y[2 * W + r] = y2;
+            yw[r] = y0 * w0 + y1 * w1 + y2 * w2;
         }
     } else if (t < g.nact + g.Lm) {
         const int l = t - g.nact;
@@ -425,63 +444,115 @@ __global__ __launch_bounds__(256) void lba_prep_slots(Graph g, int n0, int n1, i
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
-// Y [Y; w]^T on FP64 MFMA: one 4-wave workgroup per (upper tile pair, K slice), the waves
-// interleaving 4-column steps of the slice and summing in LDS; slab[s] = partial tile sums.
-// Tile pairs run over ntile + 1 tile rows (the last one holds w) without the (w, w) tile.
-__global__ __launch_bounds__(256) void lba_syrk_mfma(Graph g, int ntile1, int kchunk) {
+// Schur complement Hs = Hpp + lambda I - Y Y^T and b_schur = b_p - Y w (BlockSolver::buildSystem +
+// schur, block_solver.hpp:354-439) over the 16 x 16 tiles of the 6P x 6P matrix, block-sparse on
+// FP64 MFMA (v_mfma_f64_16x16x4f64): for every upper tile pair (I <= J) only the Y^T rows of the
+// landmarks that have a free pose in both tile I's and tile J's columns are multiplied (tp_rows: 3
+// rows per landmark, lists padded to 4-row steps with the zero row Kpad, built on the host per
+// LocalBA call: build_schur_tiles). On C4 that issues 1.4x the algorithmic pair products instead of
+// the dense SYRK's 10x. A pair's steps are cut into chunks of kSCH steps, one 4-wave workgroup per
+// chunk (each wave 8 steps: the row indices in flight, then the 16 Y^T loads in flight, then 8
+// MFMAs), the waves' accumulators summed in LDS in wave order into the chunk's tile (tp_part);
+// lba_schur_finish sums each pair's chunk tiles in chunk order and writes tile (I, J) and its
+// transpose (a last-arrival reduction in this kernel measured 77 us against 32 us: 420 agent-scope
+// release fences), with Hpp on the pose-
+// diagonal 6 x 6 blocks and lambda on the diagonal (setLambda). Workgroups past the chunks form
+// b_schur, one wave per row: b_p - the sum of the pose's slot pieces Y_block w_l (ywp, written
+// pose-major by lba_prep_slots).
+constexpr int kSCH = 32;   // MFMA steps (4 Y^T rows each) per chunk workgroup
+__global__ __launch_bounds__(256) void lba_schur_tiles(Graph g) {
     if (g.lm->done) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int pair = blockIdx.x, I = 0;
-    while (pair >= ntile1 - I) { pair -= ntile1 - I; I++; }
-    const int J = I + pair;
-    const int s = blockIdx.y;
-    const long long K = g.Kpad, W = g.NPW;
-    const int k0 = s * kchunk, k1 = min((int)K, k0 + kchunk);
-    // Y^T layout: one load instruction = 4 k-rows x 16 consecutive columns (4 full lines)
-    const double *ya = g.Y + 16 * I + (lane & 15) + (lane >> 4) * W;
-    const double *yb = g.Y + 16 * J + (lane & 15) + (lane >> 4) * W;
-    double4_t acc = {0, 0, 0, 0};
-    int kk = k0 + 4 * wv;   // K % 4 == 0: every lane runs every step
-    for (; kk + 48 < k1; kk += 64) {   // 4 steps (8 loads) in flight
-        double a[4], b[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) { a[u] = ya[(kk + 16 * u) * W]; b[u] = yb[(kk + 16 * u) * W]; }
-#pragma unroll
-        for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
-    }
-    for (; kk < k1; kk += 16) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[kk * W], yb[kk * W], acc, 0, 0, 0);
-    __shared__ double red[3][4][64];
-    if (wv > 0)
-        for (int r = 0; r < 4; r++) red[wv - 1][r][lane] = acc[r];
-    __syncthreads();
-    if (wv > 0) return;
-    const long long NPW = g.NPW;
-    double *out = g.slab + (long long)s * g.NP * NPW;
-    // C/D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * reg
-    for (int r = 0; r < 4; r++) {
-        const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
-        out[(long long)row * NPW + col] = ((acc[r] + red[0][r][lane]) + red[1][r][lane]) + red[2][r][lane];
-    }
-}
-__global__ __launch_bounds__(256) void lba_schur_reduce(Graph g) {
-    if (g.lm->done) return;
-    const double lambda = g.scalars[5];
     const int n6 = 6 * g.P;
-    const int r = blockIdx.x;  // row
-    const long long NP = g.NP, NPW = g.NPW, SL = NP * NPW;
-    if (threadIdx.x == 0) {   // b_schur[r] = b_p[r] - (Y w)[r]
+    const long long W = g.NPW;
+    if ((int)blockIdx.x >= g.nchunks) {   // b_schur rows 4 (blockIdx - nchunks) + wv
+        const int row = 4 * ((int)blockIdx.x - g.nchunks) + wv;
+        if (row >= n6) return;
+        const int ph = row / 6, a = row % 6, i0 = g.ps_start[ph], i1 = g.ps_start[ph + 1];
         double v = 0;
-        for (int s = 0; s < g.S; s++) v += g.slab[s * SL + (long long)r * NPW + g.wrow];
-        g.bs[r] = g.bp[r] - v;
+        for (int i = i0 + lane; i < i1; i += 256) {
+            double q[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) q[u] = i + 64 * u < i1 ? g.ywp[6LL * (i + 64 * u) + a] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) v += q[u];
+        }
+        // fixed-order wave sum (DPP-free: through LDS, lane order)
+        __shared__ double bsum[4][64];
+        bsum[wv][lane] = v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0) {
+            double sum = 0;
+            for (int k = 0; k < 64; k++) sum += bsum[wv][k];
+            g.bs[row] = g.bp[row] - sum;
+        }
+        return;
     }
-    for (int c = threadIdx.x; c < n6; c += 256) {
-        const int lo = min(r, c), hi = max(r, c);   // slabs hold upper tiles
-        double v = 0;
-        for (int s = 0; s < g.S; s++) v += g.slab[s * SL + (long long)lo * NPW + hi];
+    const int4 ch = g.tp_chunk[blockIdx.x];   // pair, first step, steps, chunk index within the pair
+    const int2 ij = g.tp_ij[ch.x];
+    const int I = ij.x, J = ij.y;
+    const double *ya = g.Y + 16 * I + (lane & 15), *yb = g.Y + 16 * J + (lane & 15);
+    const int *rows = g.tp_rows + g.tp_start[ch.x] + 4 * ch.y + (lane >> 4);   // rows[4 * step]
+    const int nst = ch.z;
+    double4_t acc = {0, 0, 0, 0};
+    constexpr int kSB = kSCH / 4;   // steps per wave: wv, wv + 4, ...
+    {
+        int r[kSB];
+#pragma unroll
+        for (int u = 0; u < kSB; u++) r[u] = wv + 4 * u < nst ? rows[4 * (wv + 4 * u)] : g.Kpad;
+        double av[kSB], bv[kSB];
+#pragma unroll
+        for (int u = 0; u < kSB; u++) { av[u] = ya[r[u] * W]; bv[u] = yb[r[u] * W]; }
+#pragma unroll
+        for (int u = 0; u < kSB; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+    }
+    __shared__ double red[4][4][64];
+#pragma unroll
+    for (int q = 0; q < 4; q++) red[wv][q][lane] = acc[q];
+    __syncthreads();
+    if (wv != 0) return;
+    double *part = g.tp_part + 256LL * blockIdx.x;
+#pragma unroll
+    for (int q = 0; q < 4; q++) part[64 * q + lane] = ((red[0][q][lane] + red[1][q][lane]) + red[2][q][lane]) + red[3][q][lane];
+}
+
+// one wave per tile pair: the pair's chunk tiles summed in chunk order, Hpp on the pose-diagonal
+// 6 x 6 blocks, lambda on the diagonal; tile (I, J) and its transpose into Hs
+__global__ __launch_bounds__(64) void lba_schur_finish(Graph g) {
+    if (g.lm->done) return;
+    const int lane = threadIdx.x, p = blockIdx.x;
+    const int2 ij = g.tp_ij[p], nc = g.tp_nch[p];   // (I, J); first chunk, chunk count
+    const int I = ij.x, J = ij.y, n6 = 6 * g.P;
+    const long long NP = g.NP;
+    const double lambda = g.scalars[5];
+    // chunk tiles in chunk order, 8 chunks x 4 registers of loads in flight per round
+    double v[4] = {0, 0, 0, 0};
+    const double *tp = g.tp_part + 256LL * nc.x + lane;
+    for (int c0 = 0; c0 < nc.y; c0 += 8) {
+        double t[8][4];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) t[u][q] = c0 + u < nc.y ? tp[256LL * (c0 + u) + 64 * q] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (c0 + u < nc.y) v[q] += t[u][q];
+    }
+    // C/D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * q
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int row = 16 * I + (lane >> 4) + 4 * q, col = 16 * J + (lane & 15);
+        if (row >= n6 || col >= n6) continue;
         double h = 0;
-        if (r / 6 == c / 6) h = g.Hpp[36 * (r / 6) + 6 * (r % 6) + (c % 6)];
-        if (r == c) h += lambda;
-        g.Hs[(long long)r * NP + c] = h - v;
+        if (row / 6 == col / 6) h = g.Hpp[36 * (row / 6) + 6 * (row % 6) + (col % 6)];
+        if (row == col) h += lambda;
+        h -= v[q];
+        g.Hs[row * NP + col] = h;
+        if (I != J) g.Hs[(long long)col * NP + row] = h;
     }
 }
 
@@ -910,7 +981,7 @@ __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part, int nbu
     if (g.lm->done) return;
     const int s = blockIdx.x * 256 + threadIdx.x;
     double r0 = 0;
-    if (s < g.nact) {
+    if (s < g.nact && g.on[s]) {
         const int k = g.act[s];
         const EdgeDev e = g.E[k];
         double err[3];
@@ -1023,11 +1094,27 @@ __global__ __launch_bounds__(1024) void lba_decide(Graph g, int nbu, int nbe, in
     lm_decide(g, nbu, nbe, np, nq, 1024);
 }
 
-// Optimizer.cc:925-962: after optimize(5) every edge drops its robust kernel; outliers (flag)
-// go to level 1. In place on the device edges (was a 1.7 MB re-upload of the edge array).
-__global__ __launch_bounds__(256) void lba_drop_robust(EdgeDev *E, int ne) {
+// the EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ records of Optimizer.cc:750-848 from the
+// caller's arrays: observation (stereo iff ur >= 0), information inv_sigma2 * I, Huber delta
+// sqrt(5.991) / sqrt(7.815) (float, as the reference's thHuberMono / thHuberStereo), the
+// keyframe's camera
+__global__ __launch_bounds__(256) void lba_build_edges(EdgeDev *E, int ne, const int *ep, const int *eq, const float *obs,
+                                                       const float *isg, const float *cam, float thMono, float thStereo) {
     const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k < ne) E[k].robust = 0;
+    if (k >= ne) return;
+    EdgeDev d;
+    const float *ob = obs + 3 * k;
+    d.point = eq[k];
+    d.pose = ep[k];
+    d.stereo = ob[2] >= 0;
+    d.obs[0] = ob[0]; d.obs[1] = ob[1]; d.obs[2] = d.stereo ? ob[2] : 0;
+    d.info = isg[k];
+    d.robust = 1;
+    d.delta = d.stereo ? thStereo : thMono;
+    d.dsqr = d.delta * d.delta;
+    const float *c = cam + 5 * d.pose;
+    d.fx = c[0]; d.fy = c[1]; d.cx = c[2]; d.cy = c[3]; d.bf = c[4];
+    E[k] = d;
 }
 
 // outlier test of Optimizer.cc:925-962 / 977-1008: chi2 (stale _error) + depth sign
@@ -1042,6 +1129,27 @@ __global__ __launch_bounds__(256) void lba_outliers(const EdgeDev *E, const doub
     pose_map(T[e.pose], X + 3 * e.point, p);
     const double th = e.stereo ? 7.815 : 5.991;
     flag[k] = (chi > th || !(p[2] > 0.0)) ? 1 : 0;
+}
+
+// Optimizer.cc:925-962 between the two optimize() calls, on the device: the outlier test of every
+// active edge against the current estimate (stale _error, depth sign) moves it to level 1 (on = 0)
+// and every edge drops its robust kernel. The second optimize() then runs over the same slots,
+// hessian indices and Schur tile lists: a level-1 slot contributes zeros (lba_linearize) and no
+// chi2 (lba_errors), and a vertex left without level-0 edges keeps a zero Hessian block and a zero
+// update -- the results g2o gives by leaving it out of initializeOptimization(0).
+__global__ __launch_bounds__(256) void lba_phase2_mark(Graph g, EdgeDev *E, uint8_t *on, int ne) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s < g.nact) {
+        const int k = g.act[s];
+        const bool cur = g.lm->cur;
+        const EdgeDev e = E[k];
+        const double chi = edge_chi2(e, g.err + 3 * k);
+        double p[3];
+        pose_map((cur ? g.T2 : g.T)[e.pose], (cur ? g.X2 : g.X) + 3 * e.point, p);
+        const double th = e.stereo ? 7.815 : 5.991;
+        if (chi > th || !(p[2] > 0.0)) on[s] = 0;
+    }
+    if (s < ne) E[s].robust = 0;
 }
 
 // b vector in hessian order for computeScale: [b_p (6P) | b_l (3Lm)]
@@ -1070,7 +1178,7 @@ struct lba_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     DBuf T, T2, X, X2, E, err, act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items,
-        ps_start, ps_items, slot_pt, slot_ph, con, hpl, Hll, bl, Hpp, bp, Dinv, Lc, Y, slab, Hs, bs, x, partial,
+        ps_start, ps_items, slot_pt, slot_ph, con, hpl, Hll, bl, Hpp, bp, Dinv, Lc, Y, ywp, on, tp_part, Hs, bs, x, partial,
         scalars, flags, lm, arrive, arenaA, arenaB;
     double *h_scalars = nullptr;  // pinned
     LMState *h_lm = nullptr;      // pinned
@@ -1107,7 +1215,7 @@ namespace {
 
 struct HostGraph {
     int np, nq, ne;
-    std::vector<int> level, robust_on;
+
     const int32_t *pose_id, *point_id;
     const uint8_t *fixed;
     std::vector<int> edge_point, edge_pose;
@@ -1115,19 +1223,96 @@ struct HostGraph {
 
 struct ActiveSet {
     int P = 0, Lm = 0;
-    std::vector<int> act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items, ps_start, ps_items, slot_pt, slot_ph;
+    std::vector<int> act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items, ps_start, ps_items, slot_pt, slot_ph,
+        slot_ppos;
+    std::vector<int2> tp_ij, tp_nch;     // Schur tile pairs (build_schur_tiles)
+    std::vector<int> tp_start, tp_rows;
+    std::vector<int4> tp_chunk;
+    std::vector<char> scratch_p, scratch_q;
+    std::vector<int> scratch_l, scratch_f, scratch_cnt, scratch_tiles, scratch_fill;
 };
 
+// Block structure of the Schur product Y Y^T over 16-column tiles: for every upper tile pair
+// (I <= J) the Y^T rows (3 per landmark, hessian order) of the landmarks with a free pose in both
+// tiles' columns, each list padded to a multiple of 4 rows with the zero row `zero_row`
+// (block_solver.hpp:354-439 visits the same pose pairs per landmark). Two passes over the
+// landmarks (count, fill); a landmark's tiles come from its free poses' 6-column blocks.
+void build_schur_tiles(ActiveSet &A, int zero_row) {
+    const int ntile = std::max(1, (6 * A.P + 15) / 16);
+    const int npairs = ntile * (ntile + 1) / 2;
+    auto pid = [&](int I, int J) { return I * ntile - I * (I - 1) / 2 + (J - I); };
+    A.tp_ij.resize(npairs);
+    for (int I = 0; I < ntile; I++)
+        for (int J = I; J < ntile; J++) A.tp_ij[pid(I, J)] = make_int2(I, J);
+    std::vector<int> &cnt = A.scratch_cnt, &tiles = A.scratch_tiles;
+    cnt.assign(npairs + 1, 0);
+    auto point_tiles = [&](int l) {
+        tiles.clear();
+        for (int i = A.pt_start[l]; i < A.pt_start[l + 1]; i++) {
+            const int ph = A.slot_ph[A.pt_items[i]];
+            if (ph < 0) continue;
+            tiles.push_back(6 * ph / 16);
+            tiles.push_back((6 * ph + 5) / 16);
+        }
+        std::sort(tiles.begin(), tiles.end());
+        tiles.erase(std::unique(tiles.begin(), tiles.end()), tiles.end());
+    };
+    for (int l = 0; l < A.Lm; l++) {
+        point_tiles(l);
+        for (size_t a = 0; a < tiles.size(); a++)
+            for (size_t b = a; b < tiles.size(); b++) cnt[pid(tiles[a], tiles[b])] += 3;
+    }
+    A.tp_start.assign(npairs + 1, 0);
+    for (int p = 0; p < npairs; p++) A.tp_start[p + 1] = A.tp_start[p] + ((cnt[p] + 3) & ~3);
+    A.tp_rows.assign(std::max(1, A.tp_start[npairs]), zero_row);
+    std::vector<int> &fill = A.scratch_fill;
+    fill.assign(A.tp_start.begin(), A.tp_start.end() - 1);
+    for (int l = 0; l < A.Lm; l++) {
+        point_tiles(l);
+        for (size_t a = 0; a < tiles.size(); a++)
+            for (size_t b = a; b < tiles.size(); b++) {
+                int &f = fill[pid(tiles[a], tiles[b])];
+                A.tp_rows[f++] = 3 * l;
+                A.tp_rows[f++] = 3 * l + 1;
+                A.tp_rows[f++] = 3 * l + 2;
+            }
+    }
+    // chunk workgroups: kSCH steps each, at least one per pair (empty pairs still write their tile)
+    A.tp_chunk.clear();
+    A.tp_nch.assign(npairs, make_int2(0, 0));
+    for (int p = 0; p < npairs; p++) {
+        const int steps = (A.tp_start[p + 1] - A.tp_start[p]) / 4;
+        const int nc = std::max(1, (steps + kSCH - 1) / kSCH);
+        A.tp_nch[p] = make_int2((int)A.tp_chunk.size(), nc);
+        for (int c = 0; c < nc; c++) A.tp_chunk.push_back(make_int4(p, c * kSCH, std::min(kSCH, steps - c * kSCH), c));
+    }
+}
+
 // SparseOptimizer::initializeOptimization(level) + buildIndexMapping + block structure
+// Every edge starts at level 0, so the active slots of the first optimize() are all edges in edge
+// order (the second reuses them: lba_phase2_mark). The vectors of A keep their capacity from call
+// to call (lba_solve's thread_local set).
 void build_active(const HostGraph &h, ActiveSet &A) {
-    A = ActiveSet();
-    std::vector<char> pa(h.np, 0), qa(h.nq, 0);
-    for (int k = 0; k < h.ne; k++)
-        if (h.level[k] == 0) { A.act.push_back(k); pa[h.edge_pose[k]] = 1; qa[h.edge_point[k]] = 1; }
+    A.act.resize(h.ne);
+    for (int k = 0; k < h.ne; k++) A.act[k] = k;
+    std::vector<char> &pa = A.scratch_p, &qa = A.scratch_q;
+    pa.assign(h.np, 0);
+    qa.assign(h.nq, 0);
+    for (int k = 0; k < h.ne; k++) { pa[h.edge_pose[k]] = 1; qa[h.edge_point[k]] = 1; }
+    A.hpose.clear();
+    A.hpoint.clear();
     for (int i = 0; i < h.np; i++) if (pa[i] && !h.fixed[i]) A.hpose.push_back(i);
     for (int i = 0; i < h.nq; i++) if (qa[i]) A.hpoint.push_back(i);
-    std::stable_sort(A.hpose.begin(), A.hpose.end(), [&](int a, int b) { return h.pose_id[a] < h.pose_id[b]; });
-    std::stable_sort(A.hpoint.begin(), A.hpoint.end(), [&](int a, int b) { return h.point_id[a] < h.point_id[b]; });
+    // vertex ids order the hessian (g2o's buildIndexMapping); callers usually pass them sorted
+    auto by_id = [](std::vector<int> &v, const int32_t *id) {
+        for (size_t i = 1; i < v.size(); i++)
+            if (id[v[i]] < id[v[i - 1]]) {
+                std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return id[a] < id[b]; });
+                return;
+            }
+    };
+    by_id(A.hpose, h.pose_id);
+    by_id(A.hpoint, h.point_id);
     A.P = (int)A.hpose.size();
     A.Lm = (int)A.hpoint.size();
     A.pose_hidx.assign(h.np, -1);
@@ -1146,9 +1331,12 @@ void build_active(const HostGraph &h, ActiveSet &A) {
     for (int i = 0; i < A.P; i++) A.ps_start[i + 1] += A.ps_start[i];
     A.pt_items.assign(std::max(1, A.pt_start[A.Lm]), 0);
     A.ps_items.assign(std::max(1, A.ps_start[A.P]), 0);
-    std::vector<int> fl(A.Lm, 0), fp(A.P, 0);
+    std::vector<int> &fl = A.scratch_l, &fp = A.scratch_f;
+    fl.assign(A.Lm, 0);
+    fp.assign(A.P, 0);
     A.slot_pt.assign(std::max<size_t>(1, A.act.size()), 0);
     A.slot_ph.assign(std::max<size_t>(1, A.act.size()), -1);
+    A.slot_ppos.assign(std::max<size_t>(1, A.act.size()), -1);
     for (int s = 0; s < (int)A.act.size(); s++) {
         const int k = A.act[s];
         const int l = A.point_hidx[h.edge_point[k]];
@@ -1156,7 +1344,11 @@ void build_active(const HostGraph &h, ActiveSet &A) {
         const int ph = A.pose_hidx[h.edge_pose[k]];
         A.slot_pt[s] = l;
         A.slot_ph[s] = ph;
-        if (ph >= 0) A.ps_items[A.ps_start[ph] + fp[ph]++] = s;
+        A.slot_ppos[s] = -1;
+        if (ph >= 0) {
+            A.slot_ppos[s] = A.ps_start[ph] + fp[ph];
+            A.ps_items[A.ps_start[ph] + fp[ph]++] = s;
+        }
     }
 }
 
@@ -1208,8 +1400,6 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
     if (A.P > kMaxPoses) return -2;
     const int nact = (int)A.act.size();
     const int n6 = 6 * A.P;
-    const int ntile1 = std::max(1, (n6 + 15) / 16) + 1;        // + the w tile row
-    const int npair = ntile1 * (ntile1 + 1) / 2 - 1;           // without (w, w)
     const int nbu = nblk(A.P + A.Lm), nbe = nblk(nact);
     auto slot = [&]() {
         int ph = lprof_begin(e);
@@ -1218,16 +1408,17 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
         ph = lprof_begin(e);
         lba_reduce_points<<<nblk(A.Lm), 256, 0, s>>>(g);
         if (A.P > 0) lba_reduce_poses<<<A.P, 1024, 0, s>>>(g);
+        lprof_end(e, ph, "lba_reduce");
+        ph = lprof_begin(e);
         lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nblk(nact), nblk(A.Lm), A.P);
-        lprof_end(e, ph, "lba_reduce_prep");
+        lprof_end(e, ph, "lba_prep_slots");
         if (A.P > 0) {
-            const int kchunk = (((g.Kpad + g.S - 1) / g.S + 3) / 4) * 4;  // S * kchunk >= Kpad
             ph = lprof_begin(e);
-            lba_syrk_mfma<<<dim3(npair, g.S), 256, 0, s>>>(g, ntile1, kchunk);
-            lprof_end(e, ph, "lba_syrk_mfma");
+            lba_schur_tiles<<<g.nchunks + (n6 + 3) / 4, 256, 0, s>>>(g);
+            lprof_end(e, ph, "lba_schur_tiles");
             ph = lprof_begin(e);
-            lba_schur_reduce<<<n6, 256, 0, s>>>(g);   // slab sums: spread over n6 workgroups
-            lprof_end(e, ph, "lba_schur_reduce");
+            lba_schur_finish<<<g.npairs, 64, 0, s>>>(g);
+            lprof_end(e, ph, "lba_schur_finish");
             ph = lprof_begin(e);
             if (n6 <= kSmallNP) {
                 lba_chol_tiled<<<1, kCT, chol_tiled_lds(n6), s>>>(g);
@@ -1251,8 +1442,10 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
         // scalars[8..): the update's computeScale block sums, then the trial chi2 block sums
         ph = lprof_begin(e);
         lba_update<<<nbu, 256, 0, s>>>(g, g.scalars + 8);
+        lprof_end(e, ph, "lba_update");
+        ph = lprof_begin(e);
         lba_errors<<<nbe, 256, 0, s>>>(g, g.scalars + 8 + nbu, nbu, nbe, np, nq);   // + the LM decision
-        lprof_end(e, ph, "lba_update_errors_decide");
+        lprof_end(e, ph, "lba_errors_decide");
     };
     lba_lm_init<<<1, 1, 0, s>>>(g, iterations);
     // first chunk: one trial per iteration (the common case: every first trial accepted); then
@@ -1308,8 +1501,27 @@ void lba_destroy(lba_engine *e) {
     delete e;
 }
 
+// host-phase wall clock of lba_solve (ORBX_LBA_HOSTPROF=1: one line per call on stderr)
+struct HostProf {
+    bool on;
+    std::chrono::steady_clock::time_point t0, t;
+    std::string line;
+    HostProf() : on(std::getenv("ORBX_LBA_HOSTPROF") != nullptr), t0(std::chrono::steady_clock::now()), t(t0) {}
+    void mark(const char *what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        line += std::string(" ") + what + "=" + std::to_string(std::chrono::duration<double, std::micro>(n - t).count());
+        t = n;
+    }
+    ~HostProf() {
+        if (on)
+            fprintf(stderr, "LBAHOST total=%.1f%s\n", std::chrono::duration<double, std::micro>(t - t0).count(), line.c_str());
+    }
+};
+
 int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile uint8_t *stop) {
     if (!e || !p || !r || p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0) return ORBX_EINVAL;
+    HostProf hp;
     LBA_CHK(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     const int np = p->n_poses, nq = p->n_points, ne = p->n_edges;
@@ -1340,28 +1552,18 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     h.pose_id = p->pose_id; h.point_id = p->point_id; h.fixed = p->pose_fixed;
     h.edge_point.assign(p->edge_point, p->edge_point + ne);
     h.edge_pose.assign(p->edge_pose, p->edge_pose + ne);
-    h.level.assign(ne, 0);
     for (int k = 0; k < ne; k++)
         if (h.edge_point[k] < 0 || h.edge_point[k] >= nq || h.edge_pose[k] < 0 || h.edge_pose[k] >= np) return ORBX_EINVAL;
-    const float thMono = (float)std::sqrt(5.991), thStereo = (float)std::sqrt(7.815);
-    std::vector<EdgeDev> E(ne);
-    for (int k = 0; k < ne; k++) {
-        EdgeDev &d = E[k];
-        const float *ob = p->edge_obs + 3 * k;
-        d.point = h.edge_point[k];
-        d.pose = h.edge_pose[k];
-        d.stereo = ob[2] >= 0;
-        d.obs[0] = ob[0]; d.obs[1] = ob[1]; d.obs[2] = d.stereo ? ob[2] : 0;
-        d.info = p->edge_inv_sigma2[k];
-        d.robust = 1;
-        d.delta = d.stereo ? thStereo : thMono;
-        d.dsqr = d.delta * d.delta;
-        const float *cam = p->pose_cam + 5 * d.pose;
-        d.fx = cam[0]; d.fy = cam[1]; d.cx = cam[2]; d.cy = cam[3]; d.bf = cam[4];
-    }
+    hp.mark("build");
+    // the caller's edge arrays go up as they are (24 B per edge); lba_build_edges forms the device
+    // edge records (112 B) there
     UploadSet ua;
-    const size_t oT = ua.add(T), oT2 = ua.add(T), oX = ua.add(X), oX2 = ua.add(X), oE = ua.add(E);
-    if (upload_set(e, e->arenaA, ua, s) || e->err.ensure(sizeof(double) * 3 * std::max(ne, 1)) ||
+    const size_t oT = ua.add(T), oT2 = ua.add(T), oX = ua.add(X), oX2 = ua.add(X);
+    const size_t oep = ua.add(p->edge_pose, sizeof(int32_t) * ne), oeq = ua.add(p->edge_point, sizeof(int32_t) * ne),
+                 oobs = ua.add(p->edge_obs, sizeof(float) * 3 * ne), oisg = ua.add(p->edge_inv_sigma2, sizeof(float) * ne),
+                 ocam = ua.add(p->pose_cam, sizeof(float) * 5 * np);
+    if (upload_set(e, e->arenaA, ua, s) || e->E.ensure(sizeof(EdgeDev) * std::max(ne, 1)) ||
+        e->err.ensure(sizeof(double) * 3 * std::max(ne, 1)) ||
         e->flags.ensure(std::max(ne, 1)) || e->scalars.ensure((8 + 2 * kRedBlocks) * sizeof(double)) ||
         e->partial.ensure(sizeof(double) * 4 * kRedBlocks) || e->lm.ensure(sizeof(LMState)) || e->arrive.ensure(64))
         return ORBX_EDEVICE;
@@ -1372,7 +1574,12 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     Graph g{};
     g.T = at<Pose>(e->arenaA, oT); g.T2 = at<Pose>(e->arenaA, oT2);
     g.X = at<double>(e->arenaA, oX); g.X2 = at<double>(e->arenaA, oX2);
-    g.E = at<EdgeDev>(e->arenaA, oE);
+    if (ne > 0)
+        lba_build_edges<<<nblk(ne), 256, 0, s>>>(e->E.as<EdgeDev>(), ne, at<int>(e->arenaA, oep), at<int>(e->arenaA, oeq),
+                                                 at<float>(e->arenaA, oobs), at<float>(e->arenaA, oisg),
+                                                 at<float>(e->arenaA, ocam), (float)std::sqrt(5.991), (float)std::sqrt(7.815));   // thHuberMono / Stereo
+    LBA_CHK(hipGetLastError());
+    g.E = e->E.as<EdgeDev>();
     g.arrive = e->arrive.as<unsigned>();
     g.err = e->err.as<double>();
     g.scalars = e->scalars.as<double>();
@@ -1381,15 +1588,22 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     // per optimize(): the active-set index arrays (and, for the second phase, the edges with their
     // robust kernels removed) in one upload
     auto setup = [&](ActiveSet &A, const std::vector<EdgeDev> *edges) -> int {
+        const int Kpad = std::max(4, ((3 * A.Lm + 3) / 4) * 4);
+        build_schur_tiles(A, Kpad);
         UploadSet ub;
         const size_t o_act = ub.add(A.act), o_pose_hidx = ub.add(A.pose_hidx), o_point_hidx = ub.add(A.point_hidx),
                      o_hpose = ub.add(A.hpose), o_hpoint = ub.add(A.hpoint), o_pt_start = ub.add(A.pt_start),
                      o_pt_items = ub.add(A.pt_items), o_ps_start = ub.add(A.ps_start), o_ps_items = ub.add(A.ps_items),
                      o_slot_pt = ub.add(A.slot_pt), o_slot_ph = ub.add(A.slot_ph);
+        const size_t o_slot_ppos = ub.add(A.slot_ppos);
+        const size_t o_tp_ij = ub.add(A.tp_ij), o_tp_start = ub.add(A.tp_start), o_tp_rows = ub.add(A.tp_rows),
+                     o_tp_chunk = ub.add(A.tp_chunk), o_tp_nch = ub.add(A.tp_nch);
         const size_t o_E = edges ? ub.add(*edges) : 0;
         if (upload_set(e, e->arenaB, ub, s)) return -1;
         const int nact = (int)A.act.size();
         g.act = at<int>(e->arenaB, o_act); g.nact = nact;
+        if (e->on.ensure(std::max(nact, 1)) || hipMemsetAsync(e->on.p, 1, std::max(nact, 1), s) != hipSuccess) return -1;
+        g.on = e->on.as<uint8_t>();
         g.pose_hidx = at<int>(e->arenaB, o_pose_hidx); g.point_hidx = at<int>(e->arenaB, o_point_hidx);
         g.hpose = at<int>(e->arenaB, o_hpose); g.hpoint = at<int>(e->arenaB, o_hpoint);
         g.P = A.P; g.Lm = A.Lm;
@@ -1397,19 +1611,27 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.ps_start = at<int>(e->arenaB, o_ps_start); g.ps_items = at<int>(e->arenaB, o_ps_items);
         g.slot_pt = at<int>(e->arenaB, o_slot_pt); g.slot_ph = at<int>(e->arenaB, o_slot_ph);
         if (edges) g.E = at<EdgeDev>(e->arenaB, o_E);
-        g.Kpad = std::max(4, ((3 * A.Lm + 3) / 4) * 4);
+        g.slot_ppos = at<int>(e->arenaB, o_slot_ppos);
+        g.tp_ij = at<int2>(e->arenaB, o_tp_ij);
+        g.tp_start = at<int>(e->arenaB, o_tp_start);
+        g.tp_rows = at<int>(e->arenaB, o_tp_rows);
+        g.npairs = (int)A.tp_ij.size();
+        g.tp_chunk = at<int4>(e->arenaB, o_tp_chunk);
+        g.tp_nch = at<int2>(e->arenaB, o_tp_nch);
+        g.nchunks = (int)A.tp_chunk.size();
+        if (e->tp_part.ensure(sizeof(double) * 256 * std::max(g.nchunks, 1))) return -1;
+        g.tp_part = e->tp_part.as<double>();
+        g.Kpad = Kpad;
         g.NP = std::max(kCB, ((6 * A.P + kCB - 1) / kCB) * kCB);
         const size_t NP = (size_t)g.NP, NPW = NP + 16;
         g.NPW = (int)NPW;
         g.wrow = 16 * std::max(1, (6 * A.P + 15) / 16);
-        // K slices of the SYRK (4 waves each): enough waves to fill the chip, slabs capped at ~1 GB
-        g.S = std::max(1, std::min({16, g.Kpad / 1024, (int)std::max<size_t>(1, (size_t(1) << 27) / (NP * NPW))}));
         if (e->con.ensure(sizeof(double) * 36 * std::max(nact, 1)) || e->hpl.ensure(sizeof(double) * 18 * std::max(nact, 1)) ||
             e->Hll.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) || e->bl.ensure(sizeof(double) * 3 * std::max(A.Lm, 1)) ||
             e->Hpp.ensure(sizeof(double) * 36 * std::max(A.P, 1)) || e->bp.ensure(sizeof(double) * 6 * std::max(A.P, 1)) ||
             e->Dinv.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) || e->Lc.ensure(sizeof(double) * 6 * std::max(A.Lm, 1)) ||
-            e->Y.ensure(sizeof(double) * NPW * (size_t)g.Kpad) ||
-            e->slab.ensure(sizeof(double) * (size_t)g.S * NP * NPW) || e->Hs.ensure(sizeof(double) * NP * NP) ||
+            e->Y.ensure(sizeof(double) * NPW * (size_t)(g.Kpad + 4)) || e->Hs.ensure(sizeof(double) * NP * NP) ||
+            e->ywp.ensure(sizeof(double) * 6 * std::max<size_t>(1, A.ps_items.size())) ||
             e->bs.ensure(sizeof(double) * NP) || e->x.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)))
             return -1;
         g.con = e->con.as<double>(); g.hpl = e->hpl.as<double>();
@@ -1417,10 +1639,9 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.Hpp = e->Hpp.as<double>(); g.bp = e->bp.as<double>();
         g.Dinv = e->Dinv.as<double>(); g.Lc = e->Lc.as<double>(); g.Y = e->Y.as<double>();
         g.w = g.Y + g.wrow;
-        g.slab = e->slab.as<double>(); g.Hs = e->Hs.as<double>(); g.bs = e->bs.as<double>();
+        g.Hs = e->Hs.as<double>(); g.bs = e->bs.as<double>(); g.ywp = e->ywp.as<double>();
         g.x = e->x.as<double>();
-        if (hipMemsetAsync(g.Y, 0, sizeof(double) * NPW * (size_t)g.Kpad, s) != hipSuccess ||
-            hipMemsetAsync(g.slab, 0, sizeof(double) * (size_t)g.S * NP * NPW, s) != hipSuccess ||
+        if (hipMemsetAsync(g.Y, 0, sizeof(double) * NPW * (size_t)(g.Kpad + 4), s) != hipSuccess ||
             hipMemsetAsync(g.Hs, 0, sizeof(double) * NP * NP, s) != hipSuccess ||
             hipMemsetAsync(g.x, 0, sizeof(double) * (6 * A.P + 3 * A.Lm + 8), s) != hipSuccess)
             return -1;
@@ -1430,29 +1651,29 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
             return -1;
         return 0;
     };
-    ActiveSet A;
+    hp.mark("upload");
+    static thread_local ActiveSet A;
     build_active(h, A);
+    hp.mark("active1");
     if (setup(A, nullptr)) return ORBX_EDEVICE;
+    hp.mark("setup1");
     // lba_optimize: >= 0 iterations, -1 = the pre-LM error evaluation failed (g2o's optimize()
     // returning -1, a valid outcome), -3 = HIP runtime error
     r->iterations[0] = lba_optimize(e, g, A, 5, np, nq, stop, &r->chi2[0], &r->trials[0], &cur);
     if (r->iterations[0] == -3) return ORBX_EDEVICE;
     if (r->iterations[0] < -1) return ORBX_EINVAL;
+    hp.mark("opt1");
     const bool bDoMore = !(stop && *stop);
-    std::vector<uint8_t> flag(std::max(ne, 1));
     if (bDoMore) {
-        lba_outliers<<<nblk(ne), 256, 0, s>>>(g.E, g.err, cur ? g.T2 : g.T, cur ? g.X2 : g.X, ne, e->flags.as<uint8_t>());
-        LBA_CHK(hipMemcpyAsync(flag.data(), e->flags.p, ne, hipMemcpyDeviceToHost, s));
-        LBA_CHK(hipStreamSynchronize(s));
-        for (int k = 0; k < ne; k++)
-            if (flag[k]) h.level[k] = 1;
-        lba_drop_robust<<<nblk(ne), 256, 0, s>>>(const_cast<EdgeDev *>(g.E), ne);
+        // phase 1 ran with every edge at level 0 (its slots are all edges): the level-1 moves and
+        // the robust-kernel drop stay on the device, no host round trip between the optimizations
+        lba_phase2_mark<<<nblk(std::max(ne, (int)A.act.size())), 256, 0, s>>>(g, const_cast<EdgeDev *>(g.E),
+                                                                              e->on.as<uint8_t>(), ne);
         LBA_CHK(hipGetLastError());
-        build_active(h, A);
-        if (setup(A, nullptr)) return ORBX_EDEVICE;
         r->iterations[1] = lba_optimize(e, g, A, 10, np, nq, stop, &r->chi2[1], &r->trials[1], &cur);
         if (r->iterations[1] == -3) return ORBX_EDEVICE;
         if (r->iterations[1] < -1) return ORBX_EINVAL;
+        hp.mark("opt2");
     } else {
         r->stopped = 1;
     }
@@ -1462,6 +1683,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     LBA_CHK(hipMemcpyAsync(T.data(), cur ? g.T2 : g.T, sizeof(Pose) * np, hipMemcpyDeviceToHost, s));
     LBA_CHK(hipMemcpyAsync(X.data(), cur ? g.X2 : g.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, s));
     LBA_CHK(hipStreamSynchronize(s));
+    hp.mark("final_wait");
     for (int i = 0; i < np; i++) {  // Converter::toCvMat(SE3Quat)
         double R[9];
         quat_to_R(T[i].q, R);
@@ -1473,6 +1695,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         o[12] = 0; o[13] = 0; o[14] = 0; o[15] = 1;
     }
     for (int i = 0; i < 3 * nq; i++) r->point_Xw[i] = (float)X[i];
+    hp.mark("convert");
     return ORBX_OK;
 }
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -13,6 +14,15 @@
 #define ORBX_QT_THREADS 256   // quadtree workgroup
 
 namespace orbamd {
+
+// Marginal-cost experiments (tools/skip_exp.py): ORBX_EXP_TWICE = bit mask of idempotent kernels
+// launched twice per batch (1 resize chain, 2 quadtree, 4 describe, 8 stereo_match_left); the
+// step time difference against 0 is that kernel's marginal cost inside the pipeline. 0 (unset)
+// in every product run.
+inline int exp_twice() {
+    static const int v = [] { const char *ev = std::getenv("ORBX_EXP_TWICE"); return ev ? std::atoi(ev) : 0; }();
+    return v;
+}
 
 // One FAST cell of ComputeKeyPointsOctTree's grid (ORBextractor.cc:1084-1153): the ROI
 // [r0, r0+rh) x [c0, c0+rw) of level `level`, and the cell offset (j*wCell, i*hCell) that

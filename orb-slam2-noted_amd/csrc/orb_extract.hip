@@ -107,6 +107,9 @@ template <bool SIMD>
 __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, int tiles_x, const int2 *cxt,
                                                            const int4 *ryt, const uint8_t *in, uint8_t *pyr) {
     extern __shared__ uint4 rz_h[];   // [source row][32 column groups] horizontal sums
+#ifdef EXP_SKIP_RESIZE   // marginal-cost experiments only (tools/skip_exp.py): levels left unwritten
+    return;
+#endif
     const int dw = g.lw[l], dh = g.lh[l];
     const int b = blockIdx.y;   // streaming: the XCD remap measured no gain here
     const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
@@ -301,18 +304,59 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
 
-// 9-arc score max(0, max_arc min_k d_k) with d_k = (ring_k ^ xm) + c: darker d = v - ring
-// (xm = -1, c = v + 1), brighter d = ring - v (xm = 0, c = -v) -- one v_xad_u32 per ring pixel
-__device__ __forceinline__ int fast_arc_score(const int *rg, int c, int xm) {
-    int d[16];
+// Two candidates per lane in packed f16 (candidate a: low half, b: high half). A pixel byte is
+// kept as the f16 bit pattern of the byte, i.e. the denormal x * 2^-24: sums and differences of
+// such values are exact fixed-point arithmetic (fp16 denormals are preserved, the kernel's
+// float_denorm_mode_16_64), the packed min3 / max3 keep their order, and a score M in [0, 255]
+// comes back as the integer bits of its half. VOP3P min3 / max3 have no compiler builtin here.
+__device__ __forceinline__ uint32_t pk_min3h(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_max3h(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_fmah(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_pk_fma_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_subh(uint32_t a, uint32_t b) {   // a - b per half
+    uint32_t r;
+    asm("v_pk_add_f16 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// the 16 Bresenham ring bytes and the centre byte of two score-tile pixels (pa, pb = the pixel's
+// LDS tile byte - 3, the score row being LDS tile row + 3) packed into f16 halves: two ds_read_u8
+// and one v_perm per ring pixel (ds_read_u8_d16 / _d16_hi cannot pack them here: on this gfx950
+// the d16 loads zero the other half, tools/microbench/f16_denorm_probe.hip)
+__device__ __forceinline__ void ring2(const uint8_t *pa, const uint8_t *pb, uint32_t (&R)[16], uint32_t &V) {
+    constexpr int OFF[16] = {(3 + 3) * FB_LW + 0 + 3,  (3 + 3) * FB_LW + 1 + 3,  (3 + 2) * FB_LW + 2 + 3,
+                             (3 + 1) * FB_LW + 3 + 3,  (3 + 0) * FB_LW + 3 + 3,  (3 - 1) * FB_LW + 3 + 3,
+                             (3 - 2) * FB_LW + 2 + 3,  (3 - 3) * FB_LW + 1 + 3,  (3 - 3) * FB_LW + 0 + 3,
+                             (3 - 3) * FB_LW - 1 + 3,  (3 - 2) * FB_LW - 2 + 3,  (3 - 1) * FB_LW - 3 + 3,
+                             (3 + 0) * FB_LW - 3 + 3,  (3 + 1) * FB_LW - 3 + 3,  (3 + 2) * FB_LW - 2 + 3,
+                             (3 + 3) * FB_LW - 1 + 3};
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = (rg[k] ^ xm) + c;
-    int n3[16];
+    for (int k = 0; k < 16; k++) R[k] = (uint32_t)pa[OFF[k]] | (uint32_t)pb[OFF[k]] << 16;
+    V = (uint32_t)pa[3 * FB_LW + 3] | (uint32_t)pb[3 * FB_LW + 3] << 16;
+}
+// max(0, max_arc min_k d_k) of both halves, d_k = S * ring_k + C (S = +-1: brighter / darker)
+__device__ __forceinline__ uint32_t fast_arc_score2(const uint32_t (&R)[16], uint32_t S, uint32_t C) {
+    uint32_t d[16], n3[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) n3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-    int A = 0;
+    for (int k = 0; k < 16; k++) d[k] = pk_fmah(R[k], S, C);
 #pragma unroll
-    for (int k = 0; k < 16; k++) A = max(A, min(min(n3[k], n3[(k + 3) & 15]), n3[(k + 6) & 15]));
+    for (int k = 0; k < 16; k++) n3[k] = pk_min3h(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+    uint32_t n9[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) n9[k] = pk_min3h(n3[k], n3[(k + 3) & 15], n3[(k + 6) & 15]);
+    uint32_t A = pk_max3h(0u, n9[0], n9[1]);
+#pragma unroll
+    for (int k = 2; k < 16; k += 2) A = pk_max3h(A, n9[k], n9[k + 1]);
     return A;
 }
 
@@ -416,7 +460,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     __shared__ __align__(16) uint32_t mt[FB_NG];   // exact M bytes, (mrow, x - x0 + 4)
     __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets | FB_INTILE)
     __shared__ uint16_t hlist[4][FB_HCAP];   // per-wavefront hot pixels (score-tile byte offsets)
-    __shared__ uint16_t bboth[4][128];     // per-wavefront queue of dual-polarity candidates
+    __shared__ uint16_t bboth[4][256];     // per-wavefront queue of dual-polarity candidates (< 128 + 128)
     __shared__ int ncand_sh, hcount[4];
     const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
     int t = blockIdx.x, l = 0;
@@ -591,68 +635,80 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     const int tot = ncand_sh;
 #endif
     {
-        const uint8_t *t8 = (const uint8_t *)tin;
         uint8_t *m8 = (uint8_t *)mt;
-        const int RX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-        const int RY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-        const int t1 = tlo + 1;
+        const uint8_t *t8 = (const uint8_t *)tin;
+        const uint32_t T1 = (uint32_t)(tlo + 1) * 0x00010001u;   // t1 = tlo + 1 in both halves
         uint16_t *bb = bboth[wv];
         int nh = 0, nb = 0;   // hot entries, queued dual-polarity candidates (wave-uniform)
-        auto ring = [&](int pos, int *rg) {
-            const uint8_t *pc = t8 + pos + 3 * FB_LW;   // LDS tile row = score row + 3
-#pragma unroll
-            for (int k = 0; k < 16; k++) rg[k] = pc[RY[k] * FB_LW + RX[k]];
-            return (int)pc[0];
-        };
         uint16_t *hl = hlist[wv];
         auto push_hot = [&](bool hot, int pos) {
             const unsigned long long bal = __ballot(hot);
             if (hot) hl[nh + (int)lane_rank(bal)] = (uint16_t)pos;
             nh += __popcll(bal);
         };
-        // the brighter score of queued candidates whose darker score is already in the tile
+        // a dummy position for idle halves: a tile pixel whose ring stays inside the staged rows
+        constexpr int kIdle = 4;
+        // the brighter score of queued candidates (entries lane and lane + 64) whose darker score
+        // is already in the tile
         auto drain = [&](int n) {
-            const bool act = lane < n;
-            const int e = act ? bb[lane] : 0, pos = e & (FB_INTILE - 1);
-            bool hot = false;
-            if (act) {
-                int rg[16];
-                const int v = ring(pos, rg);
-                const int Mv = max((int)m8[pos], fast_arc_score(rg, -v, 0));
-                m8[pos] = (uint8_t)Mv;
-                hot = Mv > tlo && (e & FB_INTILE);
-            }
-            push_hot(hot, pos);
+            const bool xa = lane < n, xb = lane + 64 < n;
+            const int ea = xa ? bb[lane] : 0, eb = xb ? bb[lane + 64] : 0;
+            const int pa = xa ? ea & (FB_INTILE - 1) : kIdle, pb = xb ? eb & (FB_INTILE - 1) : kIdle;
+            uint32_t R[16], V;
+            ring2(t8 + pa - 3, t8 + pb - 3, R, V);
+            const uint32_t A = fast_arc_score2(R, 0x3C003C00u, V ^ 0x80008000u);   // ring - v
+            const int Ma = max((int)m8[pa], (int)(A & 0xFFFFu)), Mb = max((int)m8[pb], (int)(A >> 16));
+            if (xa) m8[pa] = (uint8_t)Ma;
+            if (xb) m8[pb] = (uint8_t)Mb;
+            push_hot(xa && Ma > tlo && (ea & FB_INTILE), pa);
+            push_hot(xb && Mb > tlo && (eb & FB_INTILE), pb);
         };
-        for (int base = 64 * wv; base < tot; base += 256) {
-            const int q = base + lane;
-            bool hot = false, both = false;
-            int pos = 0, e = 0;
-            if (q < tot) {
-                e = clist[q];
-                pos = e & (FB_INTILE - 1);
-                int rg[16];
-                const int v = ring(pos, rg);
-                // polarity of the compass bound (step 2); candidates of both polarities (up to
-                // ~18 % on the noisier levels) get their brighter score in a queued pass unless
-                // the darker one already exceeds tlo: a darker 9-arc above tlo meets every
-                // brighter 9-arc (9 + 9 > 16), so the brighter score is then 0
-                const bool pd = v - max(min(rg[0], rg[8]), min(rg[4], rg[12])) >= t1;
-                const bool pb = min(max(rg[0], rg[8]), max(rg[4], rg[12])) - v >= t1;
-                const int Mv = fast_arc_score(rg, pd ? v + 1 : -v, pd ? -1 : 0);
-                m8[pos] = (uint8_t)Mv;
-                both = pd && pb && Mv <= tlo;
-                hot = !both && Mv > tlo && (e & FB_INTILE);
-            }
-            push_hot(hot, pos);
-            const unsigned long long bbal = __ballot(both);
-            if (both) bb[nb + lane_rank(bbal)] = (uint16_t)e;
-            nb += __popcll(bbal);
-            if (nb >= 64) {
-                drain(64);
-                nb -= 64;
-                const int rest = lane < nb ? bb[64 + lane] : 0;
-                if (lane < nb) bb[lane] = (uint16_t)rest;
+        // wavefront wv takes the candidate chunks [128 wv, 128 wv + 128), + 512, ...: entries
+        // base + lane (half a) and base + 64 + lane (half b)
+        for (int base = 128 * wv; base < tot; base += 512) {
+            const int qa = base + lane, qb = base + 64 + lane;
+            const bool xa = qa < tot, xb = qb < tot;
+            const int ea = xa ? clist[qa] : 0, eb = xb ? clist[qb] : 0;
+            const int pa = xa ? ea & (FB_INTILE - 1) : kIdle, pb = xb ? eb & (FB_INTILE - 1) : kIdle;
+            uint32_t R[16], V;
+            ring2(t8 + pa - 3, t8 + pb - 3, R, V);
+            // polarity of the compass bound (step 2), per half: darker iff v - max(min(r0, r8),
+            // min(r4, r12)) >= t1 (the sign of that difference minus t1), else brighter;
+            // candidates of both polarities (up to ~18 % on the noisier levels) get their
+            // brighter score in a queued pass unless the darker one already exceeds tlo: a darker
+            // 9-arc above tlo meets every brighter 9-arc (9 + 9 > 16), so the brighter score is 0
+            uint32_t lo1, lo2, hi1, hi2;
+            asm("v_pk_min_f16 %0, %1, %2" : "=v"(lo1) : "v"(R[0]), "v"(R[8]));
+            asm("v_pk_min_f16 %0, %1, %2" : "=v"(lo2) : "v"(R[4]), "v"(R[12]));
+            asm("v_pk_max_f16 %0, %1, %2" : "=v"(hi1) : "v"(R[0]), "v"(R[8]));
+            asm("v_pk_max_f16 %0, %1, %2" : "=v"(hi2) : "v"(R[4]), "v"(R[12]));
+            const uint32_t mxlo = pk_max3h(lo1, lo2, lo2), mnhi = pk_min3h(hi1, hi2, hi2);
+            const uint32_t Dd = pk_subh(pk_subh(V, mxlo), T1);   // >= 0 per half: darker
+            const uint32_t Db = pk_subh(pk_subh(mnhi, V), T1);   // >= 0 per half: brighter
+            // S = -1 (darker) / +1 (brighter) per half; C = -S * v
+            const uint32_t S = 0xBC00BC00u ^ (Dd & 0x80008000u);
+            const uint32_t C = V ^ 0x80008000u ^ (S & 0x80008000u);
+            const uint32_t A = fast_arc_score2(R, S, C);
+            const int Ma = (int)(A & 0xFFFFu), Mb = (int)(A >> 16);
+            if (xa) m8[pa] = (uint8_t)Ma;
+            if (xb) m8[pb] = (uint8_t)Mb;
+            const bool pda = !(Dd & 0x8000u), pdb = !(Dd & 0x80000000u);
+            const bool pba = !(Db & 0x8000u), pbb = !(Db & 0x80000000u);
+            const bool botha = xa && pda && pba && Ma <= tlo, bothb = xb && pdb && pbb && Mb <= tlo;
+            push_hot(xa && !botha && Ma > tlo && (ea & FB_INTILE), pa);
+            push_hot(xb && !bothb && Mb > tlo && (eb & FB_INTILE), pb);
+            const unsigned long long bala = __ballot(botha);
+            if (botha) bb[nb + lane_rank(bala)] = (uint16_t)ea;
+            nb += __popcll(bala);
+            const unsigned long long balb = __ballot(bothb);
+            if (bothb) bb[nb + lane_rank(balb)] = (uint16_t)eb;
+            nb += __popcll(balb);
+            if (nb >= 128) {
+                drain(128);
+                nb -= 128;   // < 128 left: move them to the front
+                const int ra = lane < nb ? bb[128 + lane] : 0, rb = lane + 64 < nb ? bb[192 + lane] : 0;
+                if (lane < nb) bb[lane] = (uint16_t)ra;
+                if (lane + 64 < nb) bb[64 + lane] = (uint16_t)rb;
             }
         }
         if (nb > 0) drain(nb);
@@ -1558,7 +1614,11 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
             const f32x2 qx = (PX[w] * av - PY[w] * bv) + MAG;
             const uint32_t i0 = __umul24(__float_as_uint(qy.x), 40u) + __float_as_uint(qx.x) + ib;
             const uint32_t i1 = __umul24(__float_as_uint(qy.y), 40u) + __float_as_uint(qx.y) + ib;
+#ifdef EXP_SKIP_BRIEF   // marginal-cost experiments only (tools/skip_exp.py)
+            words[w] = i0 == i1;
+#else
             words[w] = __ballot(pc[i0] < pc[i1]);
+#endif
         }
         if (lane == 0) {
             const int l = d[r].l;
@@ -1844,6 +1904,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     HIPCHK(order_after_done(e, s));
     if (phase & 1) {
     int ph = prof_begin(e, s);
+    for (int rep = 0; rep < ((exp_twice() & 1) ? 2 : 1); rep++)
     for (int l = 1; l < L; l++) {
         const int tiles_x = (g.lw[l] + RZ_TW - 1) / RZ_TW, tiles_y = (g.lh[l] + RZ_TH - 1) / RZ_TH;
         const size_t lds = sizeof(uint4) * 32 * (size_t)e->rz_rows[l];
@@ -1867,6 +1928,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     int ph = prof_begin(e, s);
     size_t lds = 12 * (size_t)g.qt_kl;
     if (g.qt_nodes_in_lds) lds += (2 * sizeof(QNode) + sizeof(QTmp)) * g.node_cap + 16 * (size_t)g.node_pow2;
+    for (int rep = 0; rep < ((exp_twice() & 2) ? 2 : 1); rep++)
     quadtree_kernel<<<dim3(L, n), ORBX_QT_THREADS, lds, s>>>(
         g, e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>(), e->d_qt.as<uint32_t>(),
         e->d_qt_nodes.as<unsigned char>(), e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>());
@@ -1880,6 +1942,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     orbx_kp *d_kps = e->d_kps.as<orbx_kp>();
     uint8_t *d_desc = e->d_desc.as<uint8_t>();
     int *d_cnt = e->d_cnt.as<int>();
+    for (int rep = 0; rep < ((exp_twice() & 4) ? 2 : 1); rep++)
     switch (desc_r) {
     case 2: describe_kernel<2><<<dg2, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
     default: describe_kernel<3><<<dg3, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;

@@ -374,6 +374,7 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
     stereo_sort_right<<<n_pairs, ST_THREADS, sort_lds, s>>>(g, a, store->d_st_sorted.as<uint4>());
     prof_end(store, s, ph, "stereo_sort_right");
     ph = prof_begin(store, s);
+    for (int rep = 0; rep < ((exp_twice() & 8) ? 2 : 1); rep++)
     stereo_match_left<<<dim3((a.cap + 3) / 4, n_pairs), 256, 0, s>>>(
         g, a, store->d_st_sorted.as<uint4>(), u, d, sad);
     prof_end(store, s, ph, "stereo_match_left");
