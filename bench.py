@@ -353,6 +353,10 @@ def bench_c2(amd, args, dist, world, params, pool):
                            "traffic": ent.get("hbm_bytes_per_launch"), "avg_launch_ms": round(tot / n, 4),
                            "algorithmic_bytes_per_launch": round(BYTES_PER_STEREO_FRAME * per_launch),
                            "pairs_per_launch": per_launch, "pmc_source": pmc_note}
+        if ent.get("hbm_bytes_per_launch") is not None:
+            out["roofline"]["traffic_formula"] = (f"(FETCH_SIZE x {ent.get('read_factor', 2.0)} + WRITE_SIZE) per launch, read factor "
+                                                  "calibrated for this kernel's access pattern (profiles/fetch_calib.json)")
+            out["roofline"]["traffic_x2_rule"] = ent.get("hbm_bytes_per_launch_x2_rule")
         valu = ent.get("valu_insts_per_launch")
         if valu:   # the ceiling this integer kernel actually sits against
             out["roofline"]["valu_issue_frac"] = round(

@@ -107,6 +107,7 @@ template <bool SIMD>
 __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, int tiles_x, const int2 *cxt,
                                                            const int4 *ryt, const uint8_t *in, uint8_t *pyr) {
     extern __shared__ uint4 rz_h[];   // [source row][32 column groups] horizontal sums
+    lat_prio<1>();
 #ifdef EXP_SKIP_RESIZE   // marginal-cost experiments only (tools/skip_exp.py): levels left unwritten
     return;
 #endif
@@ -462,6 +463,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     __shared__ uint16_t hlist[4][FB_HCAP];   // per-wavefront hot pixels (score-tile byte offsets)
     __shared__ uint16_t bboth[4][256];     // per-wavefront queue of dual-polarity candidates (< 128 + 128)
     __shared__ int ncand_sh, hcount[4];
+    lat_prio<16>();
     const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
     int t = blockIdx.x, l = 0;
     while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
@@ -1091,6 +1093,7 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     unsigned char *qt_nodes, uint32_t *sel, int *sel_cnt) {
     extern __shared__ __align__(16) unsigned char qt_lds[];
     __shared__ QShared S;
+    lat_prio<2>();
     int l, b;
     xcd_remap2(l, b);
     const int tid = threadIdx.x;
@@ -1494,6 +1497,7 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
                                                        const uint8_t *pyr, const uint8_t *blur,
                                                        const uint32_t *sel, const int *sel_cnt,
                                                        orbx_kp *kps, uint8_t *desc, int *cnt) {
+    lat_prio<4>();
     const int lane = threadIdx.x & 63, wv = wave_id();
     int bxr, b;
     xcd_remap2(bxr, b);
@@ -1637,6 +1641,265 @@ __global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint
             kp.class_id = -1;
             kps[o] = kp;
         }
+    }
+}
+
+// K5, software-pipelined form: NS output slots per wavefront (same arithmetic, same outputs as
+// describe_kernel). describe_kernel spends a dependent global round trip on every 3 slots and
+// runs its per-wavefront fixed work (slot resolution, fastAtan2 + glibc sincosf on 3 lanes) for
+// 3 keypoints; here
+//  1. the NS slots are resolved lane-parallel (lane r = slot s0 + r: level, output row, key,
+//     IC_Angle row base, blurred-patch base) in one round trip;
+//  2. the IC_Angle rows of all NS slots and the steered-BRIEF patches of the first G slots are
+//     issued together (second round trip); the moments (v_dot4 + DPP wave sums) land in lane r;
+//  3. fastAtan2 + glibc sincosf run once for all NS slots (lanes 0..NS-1);
+//  4. G slots at a time: the group's patch registers go to LDS, the next group's patch loads are
+//     issued, and the 256 tests of each slot run from LDS; the ballot words collect in lanes
+//     4r + w;
+//  5. one store per lane: descriptor word w of slot r by lane 4r + w, keypoint r by lane r.
+// v_writelane_b32: lane `r` of `old` := the wave-uniform `v`. The s_nop covers the hazard of a
+// VALU write of the SGPR source (a v_cmp's VCC) right before: without it the writelane read the
+// previous VCC on MI355X (tools/dbg/desc_diff.py: word 3 of every descriptor carried word 2's low half)
+__device__ __forceinline__ int write_lane(int v, int r, int old) {
+    asm volatile("s_nop 3\n\tv_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(v), "i"(r));
+    return old;
+}
+
+template <int NS, int G>
+__global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
+                                                        const uint8_t *blur, const uint32_t *sel, const int *sel_cnt,
+                                                        orbx_kp *kps, uint8_t *desc, int *cnt) {
+    static_assert(NS % G == 0 && NS <= 8, "slot groups; the moment butterfly holds 8 slots");
+    constexpr int NG = NS / G;
+    lat_prio<4>();
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    int bxr, b;
+    xcd_remap2(bxr, b);
+    __shared__ uint32_t patch[4][G][372];
+    const int L = g.nlevels, cap = g.out_base[L];   // L <= ORBX_MAXL = 16: one DPP row
+    const int s0 = (bxr * 4 + wv) * NS;
+    // IC_Angle byte weights of the lane's four rows (the same for every slot): issued first, with
+    // the slot loads, instead of after each slot's rows
+    const int w8 = lane & 7, vr = lane >> 3;
+    uint2 wt[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int v = vr - 15 + 8 * k;
+        wt[k] = (k < 3 || vr <= 6) ? c_icw[(v < 0 ? -v : v) * 8 + w8] : make_uint2(0u, 0u);
+    }
+    // 1. lane k < L: selected keypoints of level k; lane r < NS: slot s0 + r
+    const int scl = lane < L ? sel_cnt[(long long)b * L + lane] : 0;
+    const int slot = s0 + lane;
+    const bool inr = lane < NS && slot < cap;
+    const uint32_t key = inr ? sel[(long long)b * cap + slot] : 0u;
+    int inc = scl;   // inclusive level prefix on row 0
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xF, 0xF, false);   // row_shr:1
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xF, 0xF, false);   // row_shr:2
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xF, 0xF, false);   // row_shr:4
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xF, 0xF, false);   // row_shr:8
+    if (s0 == 0) {
+        const int tot = __builtin_amdgcn_readlane(inc, L - 1);
+        if (lane == 0) cnt[b] = tot;
+    }
+    // level of the slot = the last k with out_base[k] <= slot (out_base is increasing)
+    int l = 0, lbase = 0;
+#pragma unroll
+    for (int k = 1; k < ORBX_MAXL; k++)
+        if (k < L && slot >= g.out_base[k]) { l = k; lbase = g.out_base[k]; }
+    const int idx = slot - lbase;
+    const int nl = __shfl(scl, l), incl = __shfl(inc, l);
+    const bool valid = inr && idx < nl;
+    const unsigned long long vmask = __ballot(valid);
+    if (vmask == 0) return;
+    const int off = incl - nl + idx;
+    const int kx = key_x(key) + 16, ky = key_y(key) + 16;   // + minBorderX/Y (:1177-1186)
+    const uint8_t *img = l == 0 ? in + (long long)b * g.in_stride : pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
+    const int pitch = l == 0 ? g.in_pitch : g.bp[l];
+    const unsigned long long icb = (unsigned long long)(img + (long long)(ky - 15) * pitch + kx - 16);
+    const int bw = g.bp[l];
+    const long long c0 = (long long)b * g.blur_stride + g.blur_off[l] + (long long)(ky - 18) * bw + (kx - 18);
+    const int psh = (int)(c0 & 3);
+    const long long a0 = c0 - psh;
+    const long long amax = (long long)g.nimg * g.blur_stride - 4;
+    const unsigned long long smask = __ballot(valid && a0 >= 0 && a0 + 36LL * bw + 40 <= amax + 4);
+    auto rl64 = [](unsigned long long v, int r) {
+        return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, r) |
+               (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), r) << 32;
+    };
+    // 2. IC_Angle rows of every slot: lane -> dword w = lane % 8 of rows v0, v0 + 8, v0 + 16,
+    // v0 + 24 (v0 = lane / 8 - 15), unaligned dword loads
+    // (buffer loads: the slot's row base in the descriptor, rows 8k apart in soffset, the lane's
+    // row / dword in voffset -- no 64-bit address arithmetic per load)
+    uint32_t P[NS][4];
+#pragma unroll
+    for (int r = 0; r < NS; r++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) P[r][k] = 0u;
+        if (!((vmask >> r) & 1)) continue;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)rl64(icb, r), 0, 0x7fffffff, 0x00020000);
+        const int pr = __builtin_amdgcn_readlane(pitch, r);
+        const int vo = vr * pr + 4 * w8;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k < 3 || vr <= 6) P[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 8 * k * pr, 0);
+    }
+    // steered-BRIEF patch of slot r (rows y-18 .. y+18, bytes x-18 .. x+21 as 10 aligned dwords
+    // per row; lanes 0..59 -> (row lane / 10, dword lane % 10), six rows per pass) into registers
+    const int rr0 = (lane * 205) >> 11, q10 = lane - 10 * rr0;
+    uint32_t T[2][G][7];
+    auto issue_patch = [&](int gi, uint32_t (&dst)[G][7]) {
+#pragma unroll
+        for (int j = 0; j < G; j++) {
+            const int r = gi * G + j;
+#pragma unroll
+            for (int k = 0; k < 7; k++) dst[j][k] = 0u;
+            if (!((smask >> r) & 1)) continue;
+            const int bwr = __builtin_amdgcn_readlane(bw, r);
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(blur + (long long)rl64((unsigned long long)a0, r)), 0, 0x7fffffff, 0x00020000);
+            const int vo = rr0 * bwr + 4 * q10;
+            if (lane < 60) {
+#pragma unroll
+                for (int k = 0; k < 7; k++)
+                    if (k < 6 || rr0 == 0) dst[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 6 * k * bwr, 0);
+            }
+        }
+    };
+    issue_patch(0, T[0]);
+    // moments: the lane's partial sums of every slot (x[r] = m10, x[8 + r] = m01; exact integers),
+    // then one butterfly reduction of the 16 values over the wavefront. Each DPP pairing inside a
+    // row halves the values a lane holds; partners always hold the same value indices: the row
+    // mirror (lanes i, 15 - i, split by bit 3) while every lane still holds all 16, then the
+    // half-row mirror (i, 7 - i: same bit 3, split by bit 2), lane ^ 2 and lane ^ 1, so lane j of
+    // every row ends with value j & 15 summed over its row; two cross-row xor shuffles finish the
+    // sums. Lane r < 8 then holds m10 of slot r, lane 8 + r its m01.
+    int x[16];
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        int m01 = 0, m10 = 0;
+        if (r < NS && ((vmask >> r) & 1)) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int v = vr - 15 + 8 * k;
+                if (k < 3 || vr <= 6) {
+                    const int su = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].x, 0u, false);
+                    const int sm = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].y, 0u, false);
+                    m10 += su - 16 * sm;
+                    m01 += v * sm;
+                }
+            }
+        }
+        x[r] = m10;
+        x[8 + r] = m01;
+    }
+    int msum;
+    {
+        int y[8], z[4], u[2];
+        const bool b0 = lane & 1, b1 = (lane >> 1) & 1, b2 = (lane >> 2) & 1, b3 = (lane >> 3) & 1;
+#pragma unroll
+        for (int m = 0; m < 8; m++)   // row mirror: keep x[8 b3 + m]
+            y[m] = (b3 ? x[8 + m] : x[m]) + __builtin_amdgcn_update_dpp(0, b3 ? x[m] : x[8 + m], 0x140, 0xF, 0xF, false);
+#pragma unroll
+        for (int m = 0; m < 4; m++)   // half-row mirror: keep y[4 b2 + m]
+            z[m] = (b2 ? y[4 + m] : y[m]) + __builtin_amdgcn_update_dpp(0, b2 ? y[m] : y[4 + m], 0x141, 0xF, 0xF, false);
+#pragma unroll
+        for (int m = 0; m < 2; m++)   // lane ^ 2: keep z[2 b1 + m]
+            u[m] = (b1 ? z[2 + m] : z[m]) + __builtin_amdgcn_update_dpp(0, b1 ? z[m] : z[2 + m], 0x4E, 0xF, 0xF, false);
+        msum = (b0 ? u[1] : u[0]) + __builtin_amdgcn_update_dpp(0, b0 ? u[0] : u[1], 0xB1, 0xF, 0xF, false);
+        msum += __shfl_xor(msum, 16);
+        msum += __shfl_xor(msum, 32);
+    }
+    const int m10v = msum;
+    const int m01v = __builtin_amdgcn_update_dpp(0, msum, 0x108, 0xF, 0xF, false);   // row_shl:8: lane r <- lane r + 8
+    // 3. angle = fastAtan2(m01, m10) and (float) cos / sin of every slot, lane r
+    const float ang = fast_atan2_deg((float)m01v, (float)m10v);
+    float sa, ca;
+    glibc_sincosf(ang * (float)(3.1415926535897932384626433832795 / 180.f), &sa, &ca);
+    // pattern coordinates of the lane's 4 test pairs as floats (int8 -> f32, exact), the two
+    // points of a pair packed for v_pk_mul_f32 / v_pk_add_f32
+    f32x2 PX[4], PY[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const uint32_t pw = ((const uint32_t *)c_pattern)[w * 64 + lane];   // x0 y0 x1 y1 as int8
+        PX[w] = f32x2{(float)(int8_t)(pw & 0xFF), (float)(int8_t)((pw >> 16) & 0xFF)};
+        PY[w] = f32x2{(float)(int8_t)((pw >> 8) & 0xFF), (float)(int8_t)(pw >> 24)};
+    }
+    // 4. groups of G slots
+    uint32_t dlo = 0u, dhi = 0u;   // descriptor word (lane 4r + w = word w of slot r)
+#pragma unroll
+    for (int gi = 0; gi < NG; gi++) {
+#pragma unroll
+        for (int j = 0; j < G; j++) {
+            const int r = gi * G + j;
+            if (!((vmask >> r) & 1)) continue;
+            uint32_t *pt = patch[wv][j];
+            if ((smask >> r) & 1) {
+                if (lane < 60) {
+#pragma unroll
+                    for (int k = 0; k < 7; k++)
+                        if (k < 6 || rr0 == 0) pt[10 * (rr0 + 6 * k) + q10] = T[gi & 1][j][k];
+                }
+            } else {   // near the end of the blurred buffer: clamped loads, staged directly
+                const long long ar = (long long)rl64((unsigned long long)a0, r);
+                const int bwr = __builtin_amdgcn_readlane(bw, r);
+#pragma unroll
+                for (int k = 0; k < 6; k++) {
+                    const int id = lane + 64 * k;
+                    if (id < 370) {
+                        const int rr = id / 10, q = id - rr * 10;
+                        long long ad = ar + (long long)rr * bwr + 4 * q;
+                        ad = ad < 0 ? 0 : (ad > amax ? amax & ~3LL : ad);
+                        pt[id] = *(const uint32_t *)(blur + ad);
+                    }
+                }
+            }
+        }
+        wave_lds_sync();
+        if (gi + 1 < NG) issue_patch(gi + 1, T[(gi + 1) & 1]);
+#pragma unroll
+        for (int j = 0; j < G; j++) {
+            const int r = gi * G + j;
+            if (!((vmask >> r) & 1)) continue;
+            const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), r));
+            const float bs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), r));
+            // GET_VALUE(idx) = center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)] (:158-160), as
+            // in describe_kernel: cvRound by + 1.5*2^23, byte index from the float bits
+            const uint8_t *pc = (const uint8_t *)patch[wv][j];
+            const uint32_t ib = (uint32_t)(18 * 40 + 18 + __builtin_amdgcn_readlane(psh, r)) - (0x400000u * 40u + 0x4B400000u);
+            const f32x2 av = {a, a}, bv = {bs, bs}, MAG = {12582912.0f, 12582912.0f};
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const f32x2 qy = (PX[w] * bv + PY[w] * av) + MAG;
+                const f32x2 qx = (PX[w] * av - PY[w] * bv) + MAG;
+                const uint32_t i0 = __umul24(__float_as_uint(qy.x), 40u) + __float_as_uint(qx.x) + ib;
+                const uint32_t i1 = __umul24(__float_as_uint(qy.y), 40u) + __float_as_uint(qx.y) + ib;
+#ifdef EXP_SKIP_BRIEF   // marginal-cost experiments only (tools/skip_exp.py)
+                const unsigned long long word = i0 == i1;
+#else
+                const unsigned long long word = __ballot(pc[i0] < pc[i1]);
+#endif
+                dlo = (uint32_t)write_lane((int)(uint32_t)word, 4 * r + w, (int)dlo);
+                dhi = (uint32_t)write_lane((int)(uint32_t)(word >> 32), 4 * r + w, (int)dhi);
+            }
+        }
+        if (gi + 1 < NG) wave_lds_sync();   // this group's reads before the next group's writes
+    }
+    // 5. outputs
+    const int rd = lane >> 2;
+    const int offd = __shfl(off, rd);
+    if (lane < 4 * NS && ((vmask >> rd) & 1))
+        *(uint2 *)(desc + ((long long)b * cap + offd) * 32 + 8 * (lane & 3)) = make_uint2(dlo, dhi);
+    if (valid) {
+        orbx_kp kp;
+        kp.x = (float)kx;
+        kp.y = (float)ky;
+        if (l != 0) { const float s = g.scale[l]; kp.x *= s; kp.y *= s; }   // :1642-1651
+        kp.size = (float)g.scaled_patch[l];
+        kp.angle = ang;
+        kp.response = (float)key_score(key);
+        kp.octave = l;
+        kp.class_id = -1;
+        kps[(long long)b * cap + off] = kp;
     }
 }
 
@@ -1942,7 +2205,18 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     orbx_kp *d_kps = e->d_kps.as<orbx_kp>();
     uint8_t *d_desc = e->d_desc.as<uint8_t>();
     int *d_cnt = e->d_cnt.as<int>();
+    // describe2_kernel<NS, G> (default 8 slots per wavefront in groups of 2); ORBX_DESC_V=0 runs
+    // describe_kernel<ORBX_DESC_R> instead
+    static const int desc_v = [] { const char *ev = std::getenv("ORBX_DESC_V"); return ev ? std::atoi(ev) : 82; }();
     for (int rep = 0; rep < ((exp_twice() & 4) ? 2 : 1); rep++)
+    if (desc_v != 0) {
+        switch (desc_v) {
+        case 62: describe2_kernel<6, 2><<<dim3((cap + 23) / 24, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 84: describe2_kernel<8, 4><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 42: describe2_kernel<4, 2><<<dim3((cap + 15) / 16, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        default: describe2_kernel<8, 2><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        }
+    } else
     switch (desc_r) {
     case 2: describe_kernel<2><<<dg2, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
     default: describe_kernel<3><<<dg3, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;

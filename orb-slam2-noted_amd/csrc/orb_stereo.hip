@@ -144,6 +144,7 @@ __global__ __launch_bounds__(ST_THREADS) void stereo_sort_right(ExtractGeom g, S
 __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoArgs a,
                                                          const uint4 *sorted,
                                                          float *u_right, float *depth, int *sad) {
+    lat_prio<8>();
     const int lane = threadIdx.x & 63, wv = wave_id();
     int bxr, p;
     xcd_remap2(bxr, p);

@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs into profiles/pmc_traffic.json.
 
-HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, following
-MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE (KB) reports half the bytes of wide coalesced
-reads (double it); WRITE_SIZE reads exact for streaming stores. Narrow/gather access widths
-are uncalibrated there, so the figure is an estimate; ratios between variants are exact.
+HBM bytes per launch = (f * FETCH_SIZE + WRITE_SIZE) * 1024 with the read factor f of the kernel's
+access pattern, calibrated on this MI355X (profiles/fetch_calib.json, tools/fetch_calib.sh):
+MI355X_MICROARCH.md §HBM has FETCH_SIZE (KB) tally half the bytes of coalesced streaming reads
+(f = 2, measured here for 4, 8 and 16 B per lane) and asks for a calibration of other patterns;
+fast_blur_kernel's tile staging tallies every request at full size (f = 1). WRITE_SIZE is exact
+for the stores measured. Other kernels keep f = 2 (uncalibrated); ratios between variants are exact.
 Usage: pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <batch> <out.json> [<pmc_SQ_INSTS_VALU dir>]
 With the optional SQ_INSTS_VALU pass, each kernel also gets its VALU wave-instructions per
 launch (a wave64 VALU instruction occupies a 16-lane SIMD for 4 cycles).
@@ -42,6 +44,8 @@ def main():
     fdir, wdir, batch, out = Path(sys.argv[1]), Path(sys.argv[2]), int(sys.argv[3]), Path(sys.argv[4])
     fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
     valu = load(Path(sys.argv[5]), "SQ_INSTS_VALU") if len(sys.argv) > 5 else {}
+    calib = Path(__file__).resolve().parent.parent / "profiles" / "fetch_calib.json"
+    rf = json.loads(calib.read_text())["read_factor"] if calib.exists() else {"default": 2.0}
     res = {}
     for k in sorted(set(fetch) | set(write)):
         fv, wv = fetch.get(k, []), write.get(k, [])
@@ -49,13 +53,15 @@ def main():
         w_avg = sum(wv) / len(wv) if wv else 0.0
         res[k] = {"launches": max(len(fv), len(wv)), "FETCH_SIZE_KB": round(f_avg, 3),
                   "WRITE_SIZE_KB": round(w_avg, 3),
-                  "hbm_bytes_per_launch": int((2 * f_avg + w_avg) * 1024)}
+                  "read_factor": rf.get(k, rf["default"]),
+                  "hbm_bytes_per_launch": int((rf.get(k, rf["default"]) * f_avg + w_avg) * 1024),
+                  "hbm_bytes_per_launch_x2_rule": int((2 * f_avg + w_avg) * 1024)}
         if valu.get(k):
             res[k]["valu_insts_per_launch"] = int(sum(valu[k]) / len(valu[k]))
     st = stamp(batch=batch)
     if os.environ.get("STEPS_PROFILED"):   # bench steps (warmup included) the PMC run executed
         st["steps_profiled"] = int(os.environ["STEPS_PROFILED"])
-    doc = {"stamp": st, "batch": batch, "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE read correction)",
+    doc = {"stamp": st, "batch": batch, "formula": "(read_factor*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (read_factor: profiles/fetch_calib.json; hbm_bytes_per_launch_x2_rule = the guide's streaming-read rule applied to every kernel)",
            "kernels": res}
     out.write_text(json.dumps(doc, indent=1))
     print(json.dumps(doc, indent=1))
