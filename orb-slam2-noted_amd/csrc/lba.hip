@@ -169,19 +169,26 @@ __device__ inline void block_sum_to(double v, double *dst) {
 }
 
 // ---- linearize: errors + robust chi2 + per-edge quadratic-form pieces
+// Active slot s is edge s: every optimize() runs on all edges in edge order (build_active; the
+// second one marks its level-1 edges in `on`), so the kernels index the edges by slot directly and
+// issue the edge record with the LM-state load instead of after it.
 __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
-    if (g.lm->done || !g.lm->newiter) return;
     const int s = blockIdx.x * 256 + threadIdx.x;
+    const bool in = s < g.nact;
+    const uint8_t on = in ? g.on[s] : 0;
+    EdgeDev e{};
+    if (in) e = g.E[s];
+    const LMState lm = *g.lm;
+    if (lm.done || !lm.newiter) return;
     double rchi = 0;
-    if (s < g.nact && !g.on[s]) {   // a level-1 edge: no share of the system (its stale _error is kept)
+    if (in && !on) {   // a level-1 edge: no share of the system (its stale _error is kept)
         double *c = g.con + (long long)s * 36, *hp = g.hpl + (long long)s * 18;
         for (int u = 0; u < 36; u++) c[u] = 0.0;
         for (int u = 0; u < 18; u++) hp[u] = 0.0;
-    } else if (s < g.nact) {
-        const int k = g.act[s];
-        const EdgeDev e = g.E[k];
+    } else if (in) {
+        const int k = s;
         double err[3];
-        const bool cur = g.lm->cur;
+        const bool cur = lm.cur;
         const Pose *Tc = cur ? g.T2 : g.T;
         const double *Xc = cur ? g.X2 : g.X;
         edge_error(g, e, Tc, Xc, err);
@@ -268,9 +275,9 @@ __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
     block_sum_to(rchi, g.partial + blockIdx.x);
 }
 
-__global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
-    if (g.lm->done || !g.lm->newiter) return;
-    const int l = blockIdx.x * 256 + threadIdx.x;
+// Hll (3x3), b_l of one landmark (thread) -- the edges of a point are a CSR segment, summed in
+// order -- and the |diagonal| maximum of the block's 256-thread quarter -> partial[kRedBlocks + q]
+__device__ __forceinline__ void reduce_points_body(Graph &g, int l, int q, double *sh) {
     double dmax = 0;
     if (l < g.Lm) {
         double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
@@ -294,22 +301,21 @@ __global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
         g.bl[3 * l] = b[0]; g.bl[3 * l + 1] = b[1]; g.bl[3 * l + 2] = b[2];
         dmax = fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5])));
     }
-    __shared__ double sh[256];
     sh[threadIdx.x] = dmax;
     __syncthreads();
+    const int t = threadIdx.x & 255, base = threadIdx.x - t;
     for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
+        if (t < s) sh[base + t] = fmax(sh[base + t], sh[base + t + s]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) g.partial[kRedBlocks + blockIdx.x] = sh[0];
+    if (t == 0) g.partial[kRedBlocks + q] = sh[base];
 }
 
-// one 1024-thread workgroup per free pose: 32 slot groups x 32 lanes, lane k < 27 of a group
-// accumulates component k (Hpp upper 21 + b_p 6) of every 32nd slot, coalesced 216-byte slot
-// reads; the 32 group partials are summed in LDS in fixed order
-__global__ __launch_bounds__(1024) void lba_reduce_poses(Graph g) {
-    if (g.lm->done || !g.lm->newiter) return;
-    const int i = blockIdx.x, k = threadIdx.x & 31, grp = threadIdx.x >> 5;
+// Hpp (6x6), b_p of one free pose on a 1024-thread workgroup: 32 slot groups x 32 lanes, lane
+// k < 27 of a group accumulates component k (Hpp upper 21 + b_p 6) of every 32nd slot, coalesced
+// 216-byte slot reads; the 32 group partials are summed in LDS in fixed order
+__device__ __forceinline__ void reduce_poses_body(Graph &g, int i, double (*sh)[33]) {
+    const int k = threadIdx.x & 31, grp = threadIdx.x >> 5;
     const int t0 = g.ps_start[i], t1 = g.ps_start[i + 1];
     double acc = 0;
     if (k < 27) {
@@ -322,7 +328,6 @@ __global__ __launch_bounds__(1024) void lba_reduce_poses(Graph g) {
         }
         for (; t < t1; t += 32) acc += g.con[(long long)g.ps_items[t] * 36 + 9 + k];
     }
-    __shared__ double sh[32][33];
     sh[grp][k] = acc;
     __syncthreads();
     if (threadIdx.x < 27) {
@@ -346,6 +351,20 @@ __global__ __launch_bounds__(1024) void lba_reduce_poses(Graph g) {
         }
         g.partial[2 * kRedBlocks + i] = m;
     }
+}
+
+// the landmark reductions on 256-thread workgroups (one landmark per thread: a merged launch with
+// the pose reductions on 1024-thread workgroups spread the landmarks over 4x fewer CUs and took
+// 22 us against 8 + 10), the pose reductions one 1024-thread workgroup per free pose
+__global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
+    if (g.lm->done || !g.lm->newiter) return;
+    __shared__ double shp[256];
+    reduce_points_body(g, blockIdx.x * 256 + threadIdx.x, blockIdx.x, shp);
+}
+__global__ __launch_bounds__(1024) void lba_reduce_poses(Graph g) {
+    if (g.lm->done || !g.lm->newiter) return;
+    __shared__ double shq[32][33];
+    reduce_poses_body(g, blockIdx.x, shq);
 }
 
 // ---- Schur: per landmark Dinv, L = chol(Dinv), Y block and w
@@ -459,7 +478,10 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 // diagonal 6 x 6 blocks and lambda on the diagonal (setLambda). Workgroups past the chunks form
 // b_schur, one wave per row: b_p - the sum of the pose's slot pieces Y_block w_l (ywp, written
 // pose-major by lba_prep_slots).
-constexpr int kSCH = 32;   // MFMA steps (4 Y^T rows each) per chunk workgroup
+#ifndef LBA_KSCH
+#define LBA_KSCH 32
+#endif
+constexpr int kSCH = LBA_KSCH;   // MFMA steps (4 Y^T rows each) per chunk workgroup
 __global__ __launch_bounds__(256) void lba_schur_tiles(Graph g) {
     if (g.lm->done) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -498,15 +520,18 @@ __global__ __launch_bounds__(256) void lba_schur_tiles(Graph g) {
     const int nst = ch.z;
     double4_t acc = {0, 0, 0, 0};
     constexpr int kSB = kSCH / 4;   // steps per wave: wv, wv + 4, ...
-    {
-        int r[kSB];
+    constexpr int kSU = kSB < 8 ? kSB : 8;   // steps per batch of loads in flight
 #pragma unroll
-        for (int u = 0; u < kSB; u++) r[u] = wv + 4 * u < nst ? rows[4 * (wv + 4 * u)] : g.Kpad;
-        double av[kSB], bv[kSB];
+    for (int u0 = 0; u0 < kSB; u0 += kSU) {
+        if (wv + 4 * u0 >= nst) break;   // wave-uniform
+        int r[kSU];
 #pragma unroll
-        for (int u = 0; u < kSB; u++) { av[u] = ya[r[u] * W]; bv[u] = yb[r[u] * W]; }
+        for (int u = 0; u < kSU; u++) r[u] = wv + 4 * (u0 + u) < nst ? rows[4 * (wv + 4 * (u0 + u))] : g.Kpad;
+        double av[kSU], bv[kSU];
 #pragma unroll
-        for (int u = 0; u < kSB; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+        for (int u = 0; u < kSU; u++) { av[u] = ya[r[u] * W]; bv[u] = yb[r[u] * W]; }
+#pragma unroll
+        for (int u = 0; u < kSU; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
     }
     __shared__ double red[4][4][64];
 #pragma unroll
@@ -925,8 +950,12 @@ __global__ void lba_set_ok(Graph g) {
 // T <- exp(x_p) T (SE3Quat::exp, left-multiplied), X <- X + x_l into the trial buffers and the
 // computeScale pieces x (lambda x + b) of the thread's own entries, block sums -> part[]
 __global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
-    if (g.lm->done) return;
     const int t = blockIdx.x * 256 + threadIdx.x;
+    // the landmark's edge range goes out with the LM-state loads (no dependence on them)
+    const int lt = t - g.P;
+    const bool isp = lt >= 0 && lt < g.Lm;
+    const int i0p = isp ? g.pt_start[lt] : 0, i1p = isp ? g.pt_start[lt + 1] : 0;
+    if (g.lm->done) return;
     const double lambda = g.scalars[5];
     const bool cur = g.lm->cur;   // current estimate -> trial buffer
     const Pose *Tc = cur ? g.T2 : g.T;
@@ -942,7 +971,7 @@ __global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
     } else if (t < g.P + g.Lm) {
         const int l = t - g.P, v = g.hpoint[l];
         double c[3] = {g.bl[3 * l], g.bl[3 * l + 1], g.bl[3 * l + 2]};
-        const int i0 = g.pt_start[l], i1 = g.pt_start[l + 1];
+        const int i0 = i0p, i1 = i1p;
         for (int i = i0; i < i1; i += 4) {   // 4 edges' index chains in flight, applied in order
             int sl[4], ph[4];
 #pragma unroll
@@ -978,14 +1007,17 @@ __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthrea
 // block to arrive (agent-scope release by every wave, one counter; the arriving block acquires,
 // cdna_hip_programming.md G16) sums the partials and runs lm_decide -- one launch fewer per trial.
 __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part, int nbu, int nbe, int np, int nq) {
-    if (g.lm->done) return;
     const int s = blockIdx.x * 256 + threadIdx.x;
+    const bool in = s < g.nact;
+    const uint8_t on = in ? g.on[s] : 0;
+    EdgeDev e{};
+    if (in) e = g.E[s];   // slot s = edge s (lba_linearize)
+    const bool done = g.lm->done, cur = g.lm->cur;
+    if (done) return;
     double r0 = 0;
-    if (s < g.nact && g.on[s]) {
-        const int k = g.act[s];
-        const EdgeDev e = g.E[k];
+    if (in && on) {
+        const int k = s;
         double err[3];
-        const bool cur = g.lm->cur;
         edge_error(g, e, cur ? g.T : g.T2, cur ? g.X : g.X2, err);
         g.err[3 * k] = err[0]; g.err[3 * k + 1] = err[1]; g.err[3 * k + 2] = err[2];
         const double chi = edge_chi2(e, err);
@@ -1184,6 +1216,8 @@ struct lba_engine {
     LMState *h_lm = nullptr;      // pinned
     void *h_stage = nullptr;      // pinned upload staging (grow-only)
     size_t h_stage_bytes = 0;
+    void *h_down = nullptr;       // pinned download staging of the results (grow-only)
+    size_t h_down_bytes = 0;
     // per-kernel hipEvent timing on the engine stream (lba_profile; bench.py localba roofline)
     bool prof = false;
     struct ProfRec { const char *name; hipEvent_t a, b; };
@@ -1230,6 +1264,7 @@ struct ActiveSet {
     std::vector<int4> tp_chunk;
     std::vector<char> scratch_p, scratch_q;
     std::vector<int> scratch_l, scratch_f, scratch_cnt, scratch_tiles, scratch_fill;
+    std::vector<unsigned long long> scratch_mask;
 };
 
 // Block structure of the Schur product Y Y^T over 16-column tiles: for every upper tile pair
@@ -1246,6 +1281,39 @@ void build_schur_tiles(ActiveSet &A, int zero_row) {
         for (int J = I; J < ntile; J++) A.tp_ij[pid(I, J)] = make_int2(I, J);
     std::vector<int> &cnt = A.scratch_cnt, &tiles = A.scratch_tiles;
     cnt.assign(npairs + 1, 0);
+    if (ntile <= 64) {
+        // common case (6P <= 1024): a landmark's tiles as one 64-bit mask, formed once and read by
+        // both passes; pairs in (I, J) order, I <= J, like the sorted-list path below
+        std::vector<unsigned long long> &mask = A.scratch_mask;
+        mask.assign(A.Lm, 0ull);
+        for (int l = 0; l < A.Lm; l++) {
+            unsigned long long m = 0;
+            for (int i = A.pt_start[l]; i < A.pt_start[l + 1]; i++) {
+                const int ph = A.slot_ph[A.pt_items[i]];
+                if (ph >= 0) m |= 1ull << (6 * ph / 16) | 1ull << ((6 * ph + 5) / 16);
+            }
+            mask[l] = m;
+            for (unsigned long long ma = m; ma; ma &= ma - 1) {
+                const int I = __builtin_ctzll(ma);
+                for (unsigned long long mb = ma; mb; mb &= mb - 1) cnt[pid(I, __builtin_ctzll(mb))] += 3;
+            }
+        }
+        A.tp_start.assign(npairs + 1, 0);
+        for (int p = 0; p < npairs; p++) A.tp_start[p + 1] = A.tp_start[p] + ((cnt[p] + 3) & ~3);
+        A.tp_rows.assign(std::max(1, A.tp_start[npairs]), zero_row);
+        std::vector<int> &fill = A.scratch_fill;
+        fill.assign(A.tp_start.begin(), A.tp_start.end() - 1);
+        for (int l = 0; l < A.Lm; l++)
+            for (unsigned long long ma = mask[l]; ma; ma &= ma - 1) {
+                const int I = __builtin_ctzll(ma);
+                for (unsigned long long mb = ma; mb; mb &= mb - 1) {
+                    int &f = fill[pid(I, __builtin_ctzll(mb))];
+                    A.tp_rows[f++] = 3 * l;
+                    A.tp_rows[f++] = 3 * l + 1;
+                    A.tp_rows[f++] = 3 * l + 2;
+                }
+            }
+    } else {
     auto point_tiles = [&](int l) {
         tiles.clear();
         for (int i = A.pt_start[l]; i < A.pt_start[l + 1]; i++) {
@@ -1276,6 +1344,7 @@ void build_schur_tiles(ActiveSet &A, int zero_row) {
                 A.tp_rows[f++] = 3 * l + 1;
                 A.tp_rows[f++] = 3 * l + 2;
             }
+    }
     }
     // chunk workgroups: kSCH steps each, at least one per pair (empty pairs still write their tile)
     A.tp_chunk.clear();
@@ -1497,6 +1566,7 @@ void lba_destroy(lba_engine *e) {
     if (e->h_scalars) (void)hipHostFree(e->h_scalars);
     if (e->h_lm) (void)hipHostFree(e->h_lm);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_down) (void)hipHostFree(e->h_down);
     for (hipEvent_t ev : e->pool) (void)hipEventDestroy(ev);
     delete e;
 }
@@ -1679,10 +1749,24 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     }
     lba_outliers<<<nblk(ne), 256, 0, s>>>(g.E, g.err, cur ? g.T2 : g.T, cur ? g.X2 : g.X, ne, e->flags.as<uint8_t>());
     LBA_CHK(hipGetLastError());
-    LBA_CHK(hipMemcpyAsync(r->edge_erase, e->flags.p, ne, hipMemcpyDeviceToHost, s));
-    LBA_CHK(hipMemcpyAsync(T.data(), cur ? g.T2 : g.T, sizeof(Pose) * np, hipMemcpyDeviceToHost, s));
-    LBA_CHK(hipMemcpyAsync(X.data(), cur ? g.X2 : g.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, s));
+    // the three results through one page-locked staging buffer (DMA straight into it, one wait;
+    // D2H copies into the caller's pageable arrays were staged and serialised by the runtime)
+    const size_t oTd = 0, oXd = sizeof(Pose) * np, oFd = oXd + sizeof(double) * 3 * nq, down = oFd + ne + 16;
+    if (down > e->h_down_bytes) {
+        if (e->h_down) (void)hipHostFree(e->h_down);
+        e->h_down = nullptr;
+        e->h_down_bytes = 0;
+        LBA_CHK(hipHostMalloc(&e->h_down, down, hipHostMallocDefault));
+        e->h_down_bytes = down;
+    }
+    char *hd = (char *)e->h_down;
+    if (np) LBA_CHK(hipMemcpyAsync(hd + oTd, cur ? g.T2 : g.T, sizeof(Pose) * np, hipMemcpyDeviceToHost, s));
+    if (nq) LBA_CHK(hipMemcpyAsync(hd + oXd, cur ? g.X2 : g.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, s));
+    if (ne) LBA_CHK(hipMemcpyAsync(hd + oFd, e->flags.p, ne, hipMemcpyDeviceToHost, s));
     LBA_CHK(hipStreamSynchronize(s));
+    std::memcpy(T.data(), hd + oTd, sizeof(Pose) * np);
+    std::memcpy(X.data(), hd + oXd, sizeof(double) * 3 * nq);
+    std::memcpy(r->edge_erase, hd + oFd, ne);
     hp.mark("final_wait");
     for (int i = 0; i < np; i++) {  // Converter::toCvMat(SE3Quat)
         double R[9];

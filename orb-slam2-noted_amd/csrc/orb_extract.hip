@@ -100,8 +100,12 @@ __device__ __forceinline__ uint32_t resize_px_simd(int S0, int S1, int4 ry) {  /
 }
 
 #define RZ_TW 128   // output columns per tile (32 column groups of 4)
+#ifndef RZ_TH
 #define RZ_TH 32    // output rows per tile
+#endif
+#ifndef RZ_HJ
 #define RZ_HJ 6     // source rows per thread per load batch
+#endif
 
 template <bool SIMD>
 __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, int tiles_x, const int2 *cxt,
@@ -1665,7 +1669,7 @@ __device__ __forceinline__ int write_lane(int v, int r, int old) {
     return old;
 }
 
-template <int NS, int G>
+template <int NS, int G, int NB, int PRE>
 __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
                                                         const uint8_t *blur, const uint32_t *sel, const int *sel_cnt,
                                                         orbx_kp *kps, uint8_t *desc, int *cnt) {
@@ -1746,7 +1750,7 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     // steered-BRIEF patch of slot r (rows y-18 .. y+18, bytes x-18 .. x+21 as 10 aligned dwords
     // per row; lanes 0..59 -> (row lane / 10, dword lane % 10), six rows per pass) into registers
     const int rr0 = (lane * 205) >> 11, q10 = lane - 10 * rr0;
-    uint32_t T[2][G][7];
+    uint32_t T[NB][G][7];   // NB groups' patches in flight (prefetch distance NB)
     auto issue_patch = [&](int gi, uint32_t (&dst)[G][7]) {
 #pragma unroll
         for (int j = 0; j < G; j++) {
@@ -1765,7 +1769,9 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
             }
         }
     };
-    issue_patch(0, T[0]);
+    // PRE groups issued with the IC rows, the rest of the NB once P is consumed
+#pragma unroll
+    for (int q = 0; q < PRE && q < NG; q++) issue_patch(q, T[q]);
     // moments: the lane's partial sums of every slot (x[r] = m10, x[8 + r] = m01; exact integers),
     // then one butterfly reduction of the 16 values over the wavefront. Each DPP pairing inside a
     // row halves the values a lane holds; partners always hold the same value indices: the row
@@ -1811,6 +1817,8 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     }
     const int m10v = msum;
     const int m01v = __builtin_amdgcn_update_dpp(0, msum, 0x108, 0xF, 0xF, false);   // row_shl:8: lane r <- lane r + 8
+#pragma unroll
+    for (int q = PRE; q < NB && q < NG; q++) issue_patch(q, T[q]);
     // 3. angle = fastAtan2(m01, m10) and (float) cos / sin of every slot, lane r
     const float ang = fast_atan2_deg((float)m01v, (float)m10v);
     float sa, ca;
@@ -1837,7 +1845,7 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
                 if (lane < 60) {
 #pragma unroll
                     for (int k = 0; k < 7; k++)
-                        if (k < 6 || rr0 == 0) pt[10 * (rr0 + 6 * k) + q10] = T[gi & 1][j][k];
+                        if (k < 6 || rr0 == 0) pt[10 * (rr0 + 6 * k) + q10] = T[gi % NB][j][k];
                 }
             } else {   // near the end of the blurred buffer: clamped loads, staged directly
                 const long long ar = (long long)rl64((unsigned long long)a0, r);
@@ -1855,7 +1863,7 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
             }
         }
         wave_lds_sync();
-        if (gi + 1 < NG) issue_patch(gi + 1, T[(gi + 1) & 1]);
+        if (gi + NB < NG) issue_patch(gi + NB, T[gi % NB]);   // the buffer just staged
 #pragma unroll
         for (int j = 0; j < G; j++) {
             const int r = gi * G + j;
@@ -2211,10 +2219,12 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     for (int rep = 0; rep < ((exp_twice() & 4) ? 2 : 1); rep++)
     if (desc_v != 0) {
         switch (desc_v) {
-        case 62: describe2_kernel<6, 2><<<dim3((cap + 23) / 24, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 84: describe2_kernel<8, 4><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 42: describe2_kernel<4, 2><<<dim3((cap + 15) / 16, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        default: describe2_kernel<8, 2><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 62: describe2_kernel<6, 2, 2, 1><<<dim3((cap + 23) / 24, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 8222: describe2_kernel<8, 2, 2, 2><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 8242: describe2_kernel<8, 2, 4, 2><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 42: describe2_kernel<4, 2, 2, 1><<<dim3((cap + 15) / 16, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 8241: describe2_kernel<8, 2, 4, 1><<<(dim3((cap + 31) / 32, n)), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        default: describe2_kernel<8, 2, 2, 1><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
         }
     } else
     switch (desc_r) {
