@@ -1132,25 +1132,50 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     //         (:1119-1135). The order inside a cell is restated in step 5.
     const int *cnt = cell_cnt + (long long)b * g.ncell_total + cb0;
     const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
+    // A thread owns cells c0 + tid; its cell's slot row (cell_cap is a multiple of 4) is read 16
+    // keys per batch of four uint4 loads in flight: the count pass keeps, per owned cell, the
+    // kept count and threshold in registers (up to QG_IT cells per thread) for the copy pass.
+    constexpr int QG_IT = 4;
+    auto cell_keys4 = [&](int c) {
+        return (const uint4 *)(cell_keys + ((long long)b * g.ncell_total + cb0 + c) * g.cell_cap);
+    };
     auto cell_take = [&](int c, int *th) {   // keypoints of cell c, threshold in *th
-        const uint32_t *src = cell_keys + ((long long)b * g.ncell_total + cb0 + c) * g.cell_cap;
+        const uint4 *src = cell_keys4(c);
         const int v = min(cnt[c], g.cell_cap);
         int na = 0, nb = 0;
-        for (int i = 0; i < v; i++) {
-            const int sc = key_score(src[i]);
-            na += sc >= th_a;
-            nb += sc >= th_b;
+        for (int i = 0; i < v; i += 16) {
+            uint4 q[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) q[u] = i + 4 * u < v ? src[(i >> 2) + u] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t kk[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const bool in = i + 4 * u + e < v;
+                    const int sc = key_score(kk[e]);
+                    na += in && sc >= th_a;
+                    nb += in && sc >= th_b;
+                }
+            }
         }
         *th = na > 0 ? th_a : th_b;
         return na > 0 ? na : nb;
     };
+    int kept_r[QG_IT], th_r[QG_IT];
     int M = 0;
-    for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS) {
-        const int c = c0 + tid;
-        int th;
-        unsigned long long tot;
-        block_scan64(S, c < ncell ? (unsigned)cell_take(c, &th) : 0u, &tot, par);
-        M += (int)tot;
+    {
+        int it = 0;
+        for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS, it++) {
+            const int c = c0 + tid;
+            int th = 0;
+            const int v = c < ncell ? cell_take(c, &th) : 0;
+#pragma unroll
+            for (int k = 0; k < QG_IT; k++) if (k == it) { kept_r[k] = v; th_r[k] = th; }
+            unsigned long long tot;
+            block_scan64(S, (unsigned)v, &tot, par);
+            M += (int)tot;
+        }
     }
     Q.M = M;
 #ifdef ORBX_QT_PROFILE
@@ -1170,21 +1195,34 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
         Q.NO[1] = Q.NO[0] + cap;
     }
     {
-        int base = 0;
-        for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS) {
+        int base = 0, it = 0;
+        for (int c0 = 0; c0 < ncell; c0 += ORBX_QT_THREADS, it++) {
             const int c = c0 + tid;
-            int th = 0;
-            const int v = c < ncell ? cell_take(c, &th) : 0;
+            int th = 0, v = 0;
+            if (it < QG_IT) {
+#pragma unroll
+                for (int k = 0; k < QG_IT; k++) if (k == it) { v = kept_r[k]; th = th_r[k]; }
+            } else if (c < ncell) {
+                v = cell_take(c, &th);
+            }
             unsigned long long tot;
             const int pre = (int)block_scan64(S, (unsigned)v, &tot, par);
             if (v > 0) {
-                const uint32_t *src = cell_keys + ((long long)b * g.ncell_total + cb0 + c) * g.cell_cap;
+                const uint4 *src = cell_keys4(c);
                 const int nv = min(cnt[c], g.cell_cap);
                 uint32_t *dk = Q.K[0] + base + pre;
                 int o = 0;
-                for (int i = 0; i < nv; i++) {
-                    const uint32_t k = src[i];
-                    if (key_score(k) >= th) dk[o++] = k;
+                for (int i = 0; i < nv; i += 16) {
+                    uint4 q[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) q[u] = i + 4 * u < nv ? src[(i >> 2) + u] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t kk[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+                        for (int e = 0; e < 4; e++)
+                            if (i + 4 * u + e < nv && key_score(kk[e]) >= th) dk[o++] = kk[e];
+                    }
                 }
             }
             base += (int)tot;
@@ -2024,7 +2062,7 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             if (nCols <= 0 || nRows <= 0) return ORBX_EINVAL;
             const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
             if (wCell + 6 > ORBX_TMAX || hCell + 6 > ORBX_TMAX) return ORBX_EINVAL;
-            cell_cap = std::max(cell_cap, ((wCell + 1) / 2) * ((hCell + 1) / 2));
+            cell_cap = std::max(cell_cap, ((((wCell + 1) / 2) * ((hCell + 1) / 2) + 3) & ~3));   // uint4 slot rows
             g.cell_base[l] = ncells;
             int rows = 0, cols = 0;
             for (int i = 0; i < nRows; i++)

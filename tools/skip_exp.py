@@ -24,7 +24,7 @@ torch.cuda.init()
 import orbslam2_amd as amd
 from orbslam2_amd import synth
 import os
-W, H, B, K = 1241, 376, 384, int(os.environ.get("EXP_ENGINES", "3"))
+W, H, B, K = 1241, 376, int(os.environ.get("EXP_B", "384")), int(os.environ.get("EXP_ENGINES", "3"))
 pool = [synth.stereo_pair(H, W, t) for t in range(8)]
 bufs = [torch.from_numpy(np.stack([im for i in range(B) for im in pool[(i + 3 * k) % 8]])).cuda() for k in range(2)]
 mb = float(np.float32(386.1448) / np.float32(718.856))
