@@ -1707,7 +1707,11 @@ __device__ __forceinline__ int write_lane(int v, int r, int old) {
     return old;
 }
 
-template <int NS, int G, int NB, int PRE>
+// WIDE: the IC_Angle rows as one 16-byte load per lane (two lanes per 32-byte row segment) and
+// the patch as two 16-byte loads per lane (three lanes per 48-byte row, LDS rows of 12 dwords):
+// 3 vector-memory instructions per slot instead of 11 (the texture pipeline, TA / TD, is ~88 %
+// busy under describe2 with dword loads: tools/pmc_mem.sh)
+template <int NS, int G, int NB, int PRE, bool WIDE>
 __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
                                                         const uint8_t *blur, const uint32_t *sel, const int *sel_cnt,
                                                         orbx_kp *kps, uint8_t *desc, int *cnt) {
@@ -1717,17 +1721,25 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     const int lane = threadIdx.x & 63, wv = wave_id();
     int bxr, b;
     xcd_remap2(bxr, b);
-    __shared__ uint32_t patch[4][G][372];
+    constexpr int PW = WIDE ? 12 : 10;   // patch row stride in dwords (LDS)
+    constexpr int PSZ = WIDE ? 444 : 372;
+    __shared__ __align__(16) uint32_t patch[4][G][PSZ];
     const int L = g.nlevels, cap = g.out_base[L];   // L <= ORBX_MAXL = 16: one DPP row
     const int s0 = (bxr * 4 + wv) * NS;
     // IC_Angle byte weights of the lane's four rows (the same for every slot): issued first, with
     // the slot loads, instead of after each slot's rows
     const int w8 = lane & 7, vr = lane >> 3;
+    // WIDE: lane -> row lane / 2 (v = row - 15; row 31 unused), bytes 16 (lane & 1) .. + 15
+    const int wrow = lane >> 1, wh = lane & 1, wv15 = wrow - 15;
     uint2 wt[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int v = vr - 15 + 8 * k;
-        wt[k] = (k < 3 || vr <= 6) ? c_icw[(v < 0 ? -v : v) * 8 + w8] : make_uint2(0u, 0u);
+        if constexpr (WIDE) {
+            wt[k] = wrow <= 30 ? c_icw[(wv15 < 0 ? -wv15 : wv15) * 8 + 4 * wh + k] : make_uint2(0u, 0u);
+        } else {
+            const int v = vr - 15 + 8 * k;
+            wt[k] = (k < 3 || vr <= 6) ? c_icw[(v < 0 ? -v : v) * 8 + w8] : make_uint2(0u, 0u);
+        }
     }
     // 1. lane k < L: selected keypoints of level k; lane r < NS: slot s0 + r
     const int scl = lane < L ? sel_cnt[(long long)b * L + lane] : 0;
@@ -1763,7 +1775,7 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     const int psh = (int)(c0 & 3);
     const long long a0 = c0 - psh;
     const long long amax = (long long)g.nimg * g.blur_stride - 4;
-    const unsigned long long smask = __ballot(valid && a0 >= 0 && a0 + 36LL * bw + 40 <= amax + 4);
+    const unsigned long long smask = __ballot(valid && a0 >= 0 && a0 + 36LL * bw + 4 * PW <= amax + 4);
     auto rl64 = [](unsigned long long v, int r) {
         return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, r) |
                (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), r) << 32;
@@ -1780,30 +1792,50 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
         if (!((vmask >> r) & 1)) continue;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)rl64(icb, r), 0, 0x7fffffff, 0x00020000);
         const int pr = __builtin_amdgcn_readlane(pitch, r);
-        const int vo = vr * pr + 4 * w8;
+        if constexpr (WIDE) {
+            if (wrow <= 30) {
+                const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, wrow * pr + 16 * wh, 0, 0));
+                P[r][0] = q.x; P[r][1] = q.y; P[r][2] = q.z; P[r][3] = q.w;
+            }
+        } else {
+            const int vo = vr * pr + 4 * w8;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (k < 3 || vr <= 6) P[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 8 * k * pr, 0);
+            for (int k = 0; k < 4; k++)
+                if (k < 3 || vr <= 6) P[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 8 * k * pr, 0);
+        }
     }
     // steered-BRIEF patch of slot r (rows y-18 .. y+18, bytes x-18 .. x+21 as 10 aligned dwords
     // per row; lanes 0..59 -> (row lane / 10, dword lane % 10), six rows per pass) into registers
     const int rr0 = (lane * 205) >> 11, q10 = lane - 10 * rr0;
-    uint32_t T[NB][G][7];   // NB groups' patches in flight (prefetch distance NB)
-    auto issue_patch = [&](int gi, uint32_t (&dst)[G][7]) {
+    constexpr int TK = WIDE ? 8 : 7;   // patch registers per slot and lane
+    uint32_t T[NB][G][TK];   // NB groups' patches in flight (prefetch distance NB)
+    auto issue_patch = [&](int gi, uint32_t (&dst)[G][TK]) {
 #pragma unroll
         for (int j = 0; j < G; j++) {
             const int r = gi * G + j;
 #pragma unroll
-            for (int k = 0; k < 7; k++) dst[j][k] = 0u;
+            for (int k = 0; k < TK; k++) dst[j][k] = 0u;
             if (!((smask >> r) & 1)) continue;
             const int bwr = __builtin_amdgcn_readlane(bw, r);
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc((void *)(blur + (long long)rl64((unsigned long long)a0, r)), 0, 0x7fffffff, 0x00020000);
-            const int vo = rr0 * bwr + 4 * q10;
-            if (lane < 60) {
+            if constexpr (WIDE) {
+                // lane t = lane + 64 k (k = 0, 1) -> row t / 3, bytes 16 (t % 3) .. + 15 of the 48
 #pragma unroll
-                for (int k = 0; k < 7; k++)
-                    if (k < 6 || rr0 == 0) dst[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 6 * k * bwr, 0);
+                for (int k = 0; k < 2; k++) {
+                    const int t = lane + 64 * k, pr3 = (t * 171) >> 9, pj = t - 3 * pr3;   // t / 3 for t < 128
+                    if (pr3 < 37) {
+                        const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, pr3 * bwr + 16 * pj, 0, 0));
+                        dst[j][4 * k] = q.x; dst[j][4 * k + 1] = q.y; dst[j][4 * k + 2] = q.z; dst[j][4 * k + 3] = q.w;
+                    }
+                }
+            } else {
+                const int vo = rr0 * bwr + 4 * q10;
+                if (lane < 60) {
+#pragma unroll
+                    for (int k = 0; k < 7; k++)
+                        if (k < 6 || rr0 == 0) dst[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 6 * k * bwr, 0);
+                }
             }
         }
     };
@@ -1822,14 +1854,26 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     for (int r = 0; r < 8; r++) {
         int m01 = 0, m10 = 0;
         if (r < NS && ((vmask >> r) & 1)) {
+            if constexpr (WIDE) {
+                int sms = 0;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int v = vr - 15 + 8 * k;
-                if (k < 3 || vr <= 6) {
+                for (int k = 0; k < 4; k++) {
                     const int su = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].x, 0u, false);
                     const int sm = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].y, 0u, false);
                     m10 += su - 16 * sm;
-                    m01 += v * sm;
+                    sms += sm;
+                }
+                m01 = wv15 * sms;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int v = vr - 15 + 8 * k;
+                    if (k < 3 || vr <= 6) {
+                        const int su = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].x, 0u, false);
+                        const int sm = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].y, 0u, false);
+                        m10 += su - 16 * sm;
+                        m01 += v * sm;
+                    }
                 }
             }
         }
@@ -1880,7 +1924,15 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
             if (!((vmask >> r) & 1)) continue;
             uint32_t *pt = patch[wv][j];
             if ((smask >> r) & 1) {
-                if (lane < 60) {
+                if constexpr (WIDE) {
+#pragma unroll
+                    for (int k = 0; k < 2; k++) {
+                        const int t = lane + 64 * k, pr3 = (t * 171) >> 9, pj = t - 3 * pr3;
+                        if (pr3 < 37)
+                            *(uint4 *)&pt[PW * pr3 + 4 * pj] = make_uint4(T[gi % NB][j][4 * k], T[gi % NB][j][4 * k + 1],
+                                                                          T[gi % NB][j][4 * k + 2], T[gi % NB][j][4 * k + 3]);
+                    }
+                } else if (lane < 60) {
 #pragma unroll
                     for (int k = 0; k < 7; k++)
                         if (k < 6 || rr0 == 0) pt[10 * (rr0 + 6 * k) + q10] = T[gi % NB][j][k];
@@ -1889,10 +1941,10 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
                 const long long ar = (long long)rl64((unsigned long long)a0, r);
                 const int bwr = __builtin_amdgcn_readlane(bw, r);
 #pragma unroll
-                for (int k = 0; k < 6; k++) {
+                for (int k = 0; k < 7; k++) {
                     const int id = lane + 64 * k;
-                    if (id < 370) {
-                        const int rr = id / 10, q = id - rr * 10;
+                    if (id < 37 * PW) {
+                        const int rr = id / PW, q = id - rr * PW;
                         long long ad = ar + (long long)rr * bwr + 4 * q;
                         ad = ad < 0 ? 0 : (ad > amax ? amax & ~3LL : ad);
                         pt[id] = *(const uint32_t *)(blur + ad);
@@ -1911,14 +1963,14 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
             // GET_VALUE(idx) = center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)] (:158-160), as
             // in describe_kernel: cvRound by + 1.5*2^23, byte index from the float bits
             const uint8_t *pc = (const uint8_t *)patch[wv][j];
-            const uint32_t ib = (uint32_t)(18 * 40 + 18 + __builtin_amdgcn_readlane(psh, r)) - (0x400000u * 40u + 0x4B400000u);
+            const uint32_t ib = (uint32_t)(18 * 4 * PW + 18 + __builtin_amdgcn_readlane(psh, r)) - (0x400000u * 4u * PW + 0x4B400000u);
             const f32x2 av = {a, a}, bv = {bs, bs}, MAG = {12582912.0f, 12582912.0f};
 #pragma unroll
             for (int w = 0; w < 4; w++) {
                 const f32x2 qy = (PX[w] * bv + PY[w] * av) + MAG;
                 const f32x2 qx = (PX[w] * av - PY[w] * bv) + MAG;
-                const uint32_t i0 = __umul24(__float_as_uint(qy.x), 40u) + __float_as_uint(qx.x) + ib;
-                const uint32_t i1 = __umul24(__float_as_uint(qy.y), 40u) + __float_as_uint(qx.y) + ib;
+                const uint32_t i0 = __umul24(__float_as_uint(qy.x), 4u * PW) + __float_as_uint(qx.x) + ib;
+                const uint32_t i1 = __umul24(__float_as_uint(qy.y), 4u * PW) + __float_as_uint(qx.y) + ib;
 #ifdef EXP_SKIP_BRIEF   // marginal-cost experiments only (tools/skip_exp.py)
                 const unsigned long long word = i0 == i1;
 #else
@@ -2257,12 +2309,14 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     for (int rep = 0; rep < ((exp_twice() & 4) ? 2 : 1); rep++)
     if (desc_v != 0) {
         switch (desc_v) {
-        case 62: describe2_kernel<6, 2, 2, 1><<<dim3((cap + 23) / 24, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 8222: describe2_kernel<8, 2, 2, 2><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 8242: describe2_kernel<8, 2, 4, 2><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 42: describe2_kernel<4, 2, 2, 1><<<dim3((cap + 15) / 16, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 8241: describe2_kernel<8, 2, 4, 1><<<(dim3((cap + 31) / 32, n)), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        default: describe2_kernel<8, 2, 2, 1><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 62: describe2_kernel<6, 2, 2, 1, false><<<dim3((cap + 23) / 24, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 8222: describe2_kernel<8, 2, 2, 2, false><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 8242: describe2_kernel<8, 2, 4, 2, false><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 42: describe2_kernel<4, 2, 2, 1, false><<<dim3((cap + 15) / 16, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 8241: describe2_kernel<8, 2, 4, 1, false><<<(dim3((cap + 31) / 32, n)), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 83: describe2_kernel<8, 2, 2, 1, true><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        case 832: describe2_kernel<8, 4, 2, 1, true><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
+        default: describe2_kernel<8, 2, 2, 1, false><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
         }
     } else
     switch (desc_r) {
