@@ -268,9 +268,10 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 #define FB_LD (FB_LW / 4)   // LDS tile row stride in dwords
 #define FB_MR (FB_TH + 2)   // score rows y0-1 .. y0+16 (tile + NMS ring)
 #define FB_NG (FB_MR * FB_LD)   // score tile dwords (a multiple of 4, <= 1024: cleared as uint4 by 256 threads)
-#define FB_CCAP (FB_MR * (FB_TW + 2))   // candidate slots: every score pixel
-#define FB_HCAP (((FB_CCAP + 255) / 256) * 64)   // hot entries per wavefront (<= the candidates it scores)
+#define FB_CCAP (2 * FB_MR * (FB_TW + 2))   // candidate entries: both polarities of every score pixel
 #define FB_INTILE 0x8000   // candidate flag: a tile pixel (not the NMS ring)
+#define FB_BRIGHT 0x4000   // candidate flag: score the brighter polarity (else the darker)
+#define FB_POS 0x0FFF      // candidate: score-tile byte offset
 
 __device__ __forceinline__ int refl101(int i, int n) {
     if (n == 1) return 0;
@@ -464,9 +465,8 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     __shared__ __align__(16) uint32_t tin[(FB_TH + 8) * FB_LD];
     __shared__ __align__(16) uint32_t mt[FB_NG];   // exact M bytes, (mrow, x - x0 + 4)
     __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets | FB_INTILE)
-    __shared__ uint16_t hlist[4][FB_HCAP];   // per-wavefront hot pixels (score-tile byte offsets)
-    __shared__ uint16_t bboth[4][256];     // per-wavefront queue of dual-polarity candidates (< 128 + 128)
-    __shared__ int ncand_sh, hcount[4];
+    __shared__ uint16_t hlist[FB_TW * FB_TH];   // hot tile pixels (score-tile byte offsets; each at most once)
+    __shared__ int ncand_sh, hcnt_sh;
     lat_prio<16>();
     const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
     int t = blockIdx.x, l = 0;
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     }
     static_assert(FB_NG % 4 == 0 && FB_NG / 4 <= 256, "score tile cleared as one uint4 per thread");
     if (threadIdx.x < FB_NG / 4) ((uint4 *)mt)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
-    if (threadIdx.x == 0) ncand_sh = 0;
+    if (threadIdx.x == 0) { ncand_sh = 0; hcnt_sh = 0; }
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = wave_id();
     const int th_a = min(max(g.ini_th, 0), 255), th_b = min(max(g.min_th, 0), 255);
@@ -562,13 +562,13 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             auto df = [&](uint32_t u) { return __builtin_amdgcn_lerp(u, NKD, ONE); };   // top bit: u >= KD
             const uint32_t bright = (bk(uN) | bk(uS)) & (bk(uE) | bk(uW));
             const uint32_t dark_fail = (df(uN) & df(uS)) | (df(uE) & df(uW));
-            return (bright | ~dark_fail) & HI;
+            return make_uint2(bright & HI, ~dark_fail & HI);   // (brighter, darker) candidate bits
         };
         // candidates among the 8 pixels xb .. xb+7 of score row mrow (xb = x0 + 4 d): LDS dwords
         // d .. d+3 of the centre row (cols xb-4 .. xb+11), d+1 and d+2 of the rows 3 above / below
         auto prefilter8 = [&](int mrow, int d, bool active, uint32_t tflag, bool chk) {
             const int y = y0 - 1 + mrow, xb = x0 + 4 * d;
-            uint32_t cA = 0, cB = 0;   // top bit of byte i: pixel xb+i (cA), xb+4+i (cB)
+            uint2 cA = make_uint2(0u, 0u), cB = cA;   // top bit of byte i: pixel xb+i (cA), xb+4+i (cB); .x brighter, .y darker
             if (active && y >= dy0 && y < dy1 && xb + 7 >= dx0 && xb < dx1) {
                 const uint32_t *row = tin + (mrow + 3) * FB_LD;
                 // tile rows read dwords 0 .. 33 only; the ring rows' groups reach one dword past
@@ -581,24 +581,29 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
                 if (xb < dx0 || xb + 8 > dx1) {   // only the lanes at the detection region's edge
                     const int lo = max(dx0 - xb, 0), hi = min(dx1 - xb, 8);   // valid pixels [lo, hi)
                     const unsigned long long vm = hi > lo ? (~0ull << (8 * lo)) & (~0ull >> (64 - 8 * hi)) : 0ull;
-                    cA &= (uint32_t)vm;
-                    cB &= (uint32_t)(vm >> 32);
+                    cA.x &= (uint32_t)vm; cA.y &= (uint32_t)vm;
+                    cB.x &= (uint32_t)(vm >> 32); cB.y &= (uint32_t)(vm >> 32);
                 }
             }
             // compaction into the pooled list: the lane's 8 candidate bits (v_dot4 gathers the
             // byte top bits), an inclusive DPP scan of their counts over the wavefront, one LDS
             // atomic per wavefront for the slots, then each lane writes its own candidates
             const int pos0 = mrow * FB_LW + 4 * d + 4;   // score-tile byte of pixel xb
-            const uint32_t m = __builtin_amdgcn_udot4(cB >> 7, 0x80402010u,
-                                                      __builtin_amdgcn_udot4(cA >> 7, 0x08040201u, 0u, false), false);
-            const int cnt = __builtin_popcount(m);
+            // one entry per (pixel, polarity) that passes: a pixel of both polarities gets two
+            // (at most one of its two scores is nonzero, see step 3)
+            const uint32_t mb = __builtin_amdgcn_udot4(cB.x >> 7, 0x80402010u,
+                                                       __builtin_amdgcn_udot4(cA.x >> 7, 0x08040201u, 0u, false), false);
+            const uint32_t md = __builtin_amdgcn_udot4(cB.y >> 7, 0x80402010u,
+                                                       __builtin_amdgcn_udot4(cA.y >> 7, 0x08040201u, 0u, false), false);
+            const int cnt = __builtin_popcount(mb) + __builtin_popcount(md);
             const int inc = wave_incl_scan_dpp(cnt);
             const int tot8 = __builtin_amdgcn_readlane(inc, 63);
             if (tot8 == 0) return;   // wave-uniform
             int base = 0;
             if (lane == 0) base = atomicAdd(&ncand_sh, tot8);
             base = __builtin_amdgcn_readfirstlane(base) + inc - cnt;
-            for (uint32_t mm = m; mm; mm &= mm - 1) clist[base++] = (uint16_t)((pos0 + __builtin_ctz(mm)) | tflag);
+            for (uint32_t mm = mb; mm; mm &= mm - 1) clist[base++] = (uint16_t)((pos0 + __builtin_ctz(mm)) | tflag | FB_BRIGHT);
+            for (uint32_t mm = md; mm; mm &= mm - 1) clist[base++] = (uint16_t)((pos0 + __builtin_ctz(mm)) | tflag);
         };
         const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;   // pixels (y0 + r, x0 + cb + i)
 #ifndef FB_SKIP_PRE   // instruction-count experiments (make variant VDEFS=-DFB_SKIP_...)
@@ -613,11 +618,15 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             const int y = y0 + (lane & 15), x = lane < 16 ? x0 - 1 : x0 + FB_TW;
             const bool f = lane < 32 && y >= dy0 && y < dy1 && x >= dx0 && x < dx1;
             const unsigned long long bal = __ballot(f);
-            if (bal) {
+            if (bal) {   // both polarities: entries base + 2 rank (darker), + 1 (brighter)
                 int base = 0;
-                if (lane == 0) base = atomicAdd(&ncand_sh, __popcll(bal));
+                if (lane == 0) base = atomicAdd(&ncand_sh, 2 * __popcll(bal));
                 base = __builtin_amdgcn_readfirstlane(base);
-                if (f) clist[base + lane_rank(bal)] = (uint16_t)(((lane & 15) + 1) * FB_LW + (x - x0 + 4));
+                const uint16_t e = (uint16_t)(((lane & 15) + 1) * FB_LW + (x - x0 + 4));
+                if (f) {
+                    clist[base + 2 * lane_rank(bal)] = e;
+                    clist[base + 2 * lane_rank(bal) + 1] = (uint16_t)(e | FB_BRIGHT);
+                }
             }
         }
 #endif
@@ -633,8 +642,12 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     }
 #endif
     __syncthreads();
-    // 3. exact M of the pooled candidates: wavefront wv takes chunks wv, wv + 4, ... of 64; its
-    // hot pixels (tile pixels with M > tlo) go to its hot list
+    // 3. exact M of the pooled (pixel, polarity) entries, two per lane (halves a, b): wavefront wv
+    // takes entries [128 wv, 128 wv + 128), + 512, ...; tile pixels with M > tlo go to its hot
+    // list. At most one polarity of a pixel scores above 0 (a darker 9-arc with every difference
+    // > 0 meets every brighter 9-arc in >= 2 pixels: 9 + 9 > 16), so the two entries of a pixel
+    // that passed both compass tests never both write: a score is stored only when nonzero (the
+    // score tile is zero elsewhere) and only the nonzero one can be hot.
 #ifdef FB_SKIP_EXACT
     const int tot = 0;
 #else
@@ -643,100 +656,46 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     {
         uint8_t *m8 = (uint8_t *)mt;
         const uint8_t *t8 = (const uint8_t *)tin;
-        const uint32_t T1 = (uint32_t)(tlo + 1) * 0x00010001u;   // t1 = tlo + 1 in both halves
-        uint16_t *bb = bboth[wv];
-        int nh = 0, nb = 0;   // hot entries, queued dual-polarity candidates (wave-uniform)
-        uint16_t *hl = hlist[wv];
-        auto push_hot = [&](bool hot, int pos) {
+        auto push_hot = [&](bool hot, int pos) {   // one LDS atomic per wavefront batch
             const unsigned long long bal = __ballot(hot);
-            if (hot) hl[nh + (int)lane_rank(bal)] = (uint16_t)pos;
-            nh += __popcll(bal);
+            if (bal == 0) return;   // wave-uniform
+            int hb = 0;
+            if (lane == 0) hb = atomicAdd(&hcnt_sh, __popcll(bal));
+            hb = __builtin_amdgcn_readfirstlane(hb);
+            if (hot) hlist[hb + (int)lane_rank(bal)] = (uint16_t)pos;
         };
         // a dummy position for idle halves: a tile pixel whose ring stays inside the staged rows
         constexpr int kIdle = 4;
-        // the brighter score of queued candidates (entries lane and lane + 64) whose darker score
-        // is already in the tile
-        auto drain = [&](int n) {
-            const bool xa = lane < n, xb = lane + 64 < n;
-            const int ea = xa ? bb[lane] : 0, eb = xb ? bb[lane + 64] : 0;
-            const int pa = xa ? ea & (FB_INTILE - 1) : kIdle, pb = xb ? eb & (FB_INTILE - 1) : kIdle;
-            uint32_t R[16], V;
-            ring2(t8 + pa - 3, t8 + pb - 3, R, V);
-            const uint32_t A = fast_arc_score2(R, 0x3C003C00u, V ^ 0x80008000u);   // ring - v
-            const int Ma = max((int)m8[pa], (int)(A & 0xFFFFu)), Mb = max((int)m8[pb], (int)(A >> 16));
-            if (xa) m8[pa] = (uint8_t)Ma;
-            if (xb) m8[pb] = (uint8_t)Mb;
-            push_hot(xa && Ma > tlo && (ea & FB_INTILE), pa);
-            push_hot(xb && Mb > tlo && (eb & FB_INTILE), pb);
-        };
-        // wavefront wv takes the candidate chunks [128 wv, 128 wv + 128), + 512, ...: entries
-        // base + lane (half a) and base + 64 + lane (half b)
         for (int base = 128 * wv; base < tot; base += 512) {
             const int qa = base + lane, qb = base + 64 + lane;
             const bool xa = qa < tot, xb = qb < tot;
             const int ea = xa ? clist[qa] : 0, eb = xb ? clist[qb] : 0;
-            const int pa = xa ? ea & (FB_INTILE - 1) : kIdle, pb = xb ? eb & (FB_INTILE - 1) : kIdle;
+            const int pa = xa ? ea & FB_POS : kIdle, pb = xb ? eb & FB_POS : kIdle;
             uint32_t R[16], V;
             ring2(t8 + pa - 3, t8 + pb - 3, R, V);
-            // polarity of the compass bound (step 2), per half: darker iff v - max(min(r0, r8),
-            // min(r4, r12)) >= t1 (the sign of that difference minus t1), else brighter;
-            // candidates of both polarities (up to ~18 % on the noisier levels) get their
-            // brighter score in a queued pass unless the darker one already exceeds tlo: a darker
-            // 9-arc above tlo meets every brighter 9-arc (9 + 9 > 16), so the brighter score is 0
-            uint32_t lo1, lo2, hi1, hi2;
-            asm("v_pk_min_f16 %0, %1, %2" : "=v"(lo1) : "v"(R[0]), "v"(R[8]));
-            asm("v_pk_min_f16 %0, %1, %2" : "=v"(lo2) : "v"(R[4]), "v"(R[12]));
-            asm("v_pk_max_f16 %0, %1, %2" : "=v"(hi1) : "v"(R[0]), "v"(R[8]));
-            asm("v_pk_max_f16 %0, %1, %2" : "=v"(hi2) : "v"(R[4]), "v"(R[12]));
-            const uint32_t mxlo = pk_max3h(lo1, lo2, lo2), mnhi = pk_min3h(hi1, hi2, hi2);
-            const uint32_t Dd = pk_subh(pk_subh(V, mxlo), T1);   // >= 0 per half: darker
-            const uint32_t Db = pk_subh(pk_subh(mnhi, V), T1);   // >= 0 per half: brighter
-            // S = -1 (darker) / +1 (brighter) per half; C = -S * v
-            const uint32_t S = 0xBC00BC00u ^ (Dd & 0x80008000u);
+            // S = +1 (brighter) / -1 (darker) per half, C = -S * v
+            const uint32_t S = ((ea & FB_BRIGHT) ? 0x3C00u : 0xBC00u) | ((eb & FB_BRIGHT) ? 0x3C000000u : 0xBC000000u);
             const uint32_t C = V ^ 0x80008000u ^ (S & 0x80008000u);
             const uint32_t A = fast_arc_score2(R, S, C);
             const int Ma = (int)(A & 0xFFFFu), Mb = (int)(A >> 16);
-            if (xa) m8[pa] = (uint8_t)Ma;
-            if (xb) m8[pb] = (uint8_t)Mb;
-            const bool pda = !(Dd & 0x8000u), pdb = !(Dd & 0x80000000u);
-            const bool pba = !(Db & 0x8000u), pbb = !(Db & 0x80000000u);
-            const bool botha = xa && pda && pba && Ma <= tlo, bothb = xb && pdb && pbb && Mb <= tlo;
-            push_hot(xa && !botha && Ma > tlo && (ea & FB_INTILE), pa);
-            push_hot(xb && !bothb && Mb > tlo && (eb & FB_INTILE), pb);
-            const unsigned long long bala = __ballot(botha);
-            if (botha) bb[nb + lane_rank(bala)] = (uint16_t)ea;
-            nb += __popcll(bala);
-            const unsigned long long balb = __ballot(bothb);
-            if (bothb) bb[nb + lane_rank(balb)] = (uint16_t)eb;
-            nb += __popcll(balb);
-            if (nb >= 128) {
-                drain(128);
-                nb -= 128;   // < 128 left: move them to the front
-                const int ra = lane < nb ? bb[128 + lane] : 0, rb = lane + 64 < nb ? bb[192 + lane] : 0;
-                if (lane < nb) bb[lane] = (uint16_t)ra;
-                if (lane + 64 < nb) bb[64 + lane] = (uint16_t)rb;
-            }
+            if (xa && Ma > 0) m8[pa] = (uint8_t)Ma;
+            if (xb && Mb > 0) m8[pb] = (uint8_t)Mb;
+            push_hot(xa && Ma > tlo && (ea & FB_INTILE), pa);
+            push_hot(xb && Mb > tlo && (eb & FB_INTILE), pb);
         }
-        if (nb > 0) drain(nb);
-        if (lane == 0) hcount[wv] = nh;
     }
     __syncthreads();
     // 5. 3x3 NMS of the hot pixels at tlo against their in-cell neighbours (others score 0),
     // survivors appended to their cell's slot list
     {
-        const int h1 = hcount[0], h2 = h1 + hcount[1], h3 = h2 + hcount[2], htot = h3 + hcount[3];
+        const int htot = hcnt_sh;
         const uint8_t *m8 = (const uint8_t *)mt;
         const int hC = g.hcell[l], wC = g.wcell[l];
         const int ry_end = g.maxBY[l] - 3, rx_end = g.maxBX[l] - 3;
         for (int base = 64 * wv; base < htot; base += 256) {
             const int q = base + lane;
             if (q >= htot) continue;
-            const int ow = (int)(q >= h1) + (int)(q >= h2) + (int)(q >= h3);
-            int hb = q >= h1 ? h1 : 0;
-            hb = q >= h2 ? h2 : hb;
-            hb = q >= h3 ? h3 : hb;
-            const int n = q - hb;
-            const int pos = hlist[ow][n];
+            const int pos = hlist[q];
             const int mrow = pos / FB_LW, col = pos - mrow * FB_LW;
             const int y = y0 - 1 + mrow, x = x0 - 4 + col;
             // cell of (x, y): (v - 19) / cell side by a 20-bit reciprocal (exact for v < 2^20 / side)
@@ -751,10 +710,18 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             // neighbour with M_q <= tlo has M_q - 1 < tlo <= s_p: the test is M_p > max(M_q, 1)
             // over the in-cell neighbours, on the raw M bytes (0 outside the candidates)
             const uint8_t *pm = m8 + pos;
+            // the 8 neighbours read unconditionally (a hot pixel is a tile pixel: rows 1..16,
+            // columns 4..131 of the 18 x 136-byte score tile, so every neighbour is inside it) and
+            // masked to their cell: no divergent branch per neighbour
+            int nb[8];
+            const int noff[8] = {-1, 1, -FB_LW - 1, -FB_LW, -FB_LW + 1, FB_LW - 1, FB_LW, FB_LW + 1};
+#pragma unroll
+            for (int k = 0; k < 8; k++) nb[k] = pm[noff[k]];
             const int sp = (int)pm[0] - 1;
-            auto mq = [&](int off, bool in) { return in ? (int)pm[off] : 0; };
-            const int mn = max(max(max(mq(-1, lf), mq(1, rt)), max(mq(-FB_LW - 1, up && lf), mq(-FB_LW, up))),
-                               max(max(mq(-FB_LW + 1, up && rt), mq(FB_LW - 1, dn && lf)), max(mq(FB_LW, dn), mq(FB_LW + 1, dn && rt))));
+            const bool nin[8] = {lf, rt, up && lf, up, up && rt, dn && lf, dn, dn && rt};
+#pragma unroll
+            for (int k = 0; k < 8; k++) nb[k] = nin[k] ? nb[k] : 0;
+            const int mn = max(max(max(nb[0], nb[1]), max(nb[2], nb[3])), max(max(nb[4], nb[5]), max(nb[6], nb[7])));
             const bool keep = (int)pm[0] > max(mn, 1);
             if (keep) {
                 const long long cidx = (long long)b * g.ncell_total + g.cell_base[l] + ci * g.ncell_cols[l] + cj;
