@@ -99,9 +99,13 @@ struct Graph {
     const int *slot_ppos;            // per active slot: its position in ps_items (-1 fixed pose)
     double *ywp;                     // [ps_items][6]: the slot's Y block times w_l (b_schur pieces)
     const int *slot_pt, *slot_ph;    // per active slot: hessian point / pose index (-1 fixed)
-    // system
-    double *con;           // [nact][36] per-slot Hll(6) bl(3) Hpp(21) bp(6)
-    double *hpl;           // [nact][18]
+    const int *slot_lpos;            // per active slot: its position in pt_items
+    const int *lpos_ph;              // per pt_items position: the slot's hessian pose index (-1 fixed)
+    // system; the per-slot linearisation is kept per estimate buffer (index = LMState::cur of the
+    // estimate it was formed at): lba_errors linearises the trial, and accepting it swaps both
+    double *conl[2];       // [pt_items][9]: Hll upper (6) bl (3), landmark-major (point CSR order)
+    double *conp[2];       // [ps_items][27]: Hpp upper (21) bp (6), pose-major
+    double *hpl[2];        // [pt_items][18]: Hpl, landmark-major
     double *Hll, *bl;      // [Lm][9], [Lm][3]
     double *Hpp, *bp;      // [P][36], [P][6]
     double *Dinv;          // [Lm][9]
@@ -110,7 +114,8 @@ struct Graph {
     double *w;             // = Y + wrow, stride NPW
     double *Hs, *bs;       // [NP][NP], [NP]
     double *x;             // [6P + 3Lm]
-    double *partial;       // [4][kRedBlocks]
+    double *partial;       // [4][kRedBlocks]: robust chi2 block sums of linearisation set 0 | point
+                           // maxDiagonal | pose maxDiagonal | robust chi2 block sums of set 1
     double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok, lambda
     LMState *lm;
     unsigned *arrive;      // lba_errors block-arrival counter (the last block runs the LM decision)
@@ -156,8 +161,8 @@ __device__ inline void huber(const EdgeDev &e, double chi, double &rho0, double 
     else { const double s = sqrt(chi); rho0 = 2 * s * e.delta - e.dsqr; rho1 = e.delta / s; }
 }
 
-// block sum of one double per thread into partial[blockIdx.x]
-__device__ inline void block_sum_to(double v, double *dst) {
+// block sum of one double per thread into *dst (also returned, to every thread)
+__device__ inline double block_sum_to(double v, double *dst) {
     __shared__ double sh[256];
     sh[threadIdx.x] = v;
     __syncthreads();
@@ -166,167 +171,197 @@ __device__ inline void block_sum_to(double v, double *dst) {
         __syncthreads();
     }
     if (threadIdx.x == 0) *dst = sh[0];
+    return sh[0];
 }
 
 // ---- linearize: errors + robust chi2 + per-edge quadratic-form pieces
 // Active slot s is edge s: every optimize() runs on all edges in edge order (build_active; the
 // second one marks its level-1 edges in `on`), so the kernels index the edges by slot directly and
 // issue the edge record with the LM-state load instead of after it.
+__device__ __forceinline__ int chi_off(int set) { return set ? 3 * kRedBlocks : 0; }
+
+// One slot's share of the system at estimate (Tc, Xc) into linearisation set `set`: the
+// residual (g2o _error), Huber weight, analytic 2x9 / 3x9 Jacobians (types_six_dof_expmap.cpp
+// :103-139, 188-234) and the quadratic-form pieces, landmark part at the slot's pt_items position
+// `lpos`, pose part at its ps_items position `ppos` (-1: fixed pose, no pose part). A level-1 slot
+// (on = 0) keeps its stale _error and contributes zeros. Returns the robust chi2.
+__device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &e, bool on, int s, int lpos, int ppos,
+                                                 const Pose *Tc, const double *Xc, int set) {
+    double *cl = g.conl[set] + 9LL * lpos, *hp = g.hpl[set] + 18LL * lpos;
+    double *cp = g.conp[set] + 27LL * (ppos < 0 ? 0 : ppos);
+    if (!on) {
+        for (int u = 0; u < 9; u++) cl[u] = 0.0;
+        for (int u = 0; u < 18; u++) hp[u] = 0.0;
+        if (ppos >= 0)
+            for (int u = 0; u < 27; u++) cp[u] = 0.0;
+        return 0.0;
+    }
+    double err[3];
+    edge_error(g, e, Tc, Xc, err);
+    g.err[3 * s] = err[0]; g.err[3 * s + 1] = err[1]; g.err[3 * s + 2] = err[2];
+    const double chi = edge_chi2(e, err);
+    double r0 = chi, r1 = 1.0;
+    if (e.robust) huber(e, chi, r0, r1);
+    const Pose T = Tc[e.pose];
+    double p[3], R[9];
+    pose_map(T, Xc + 3 * e.point, p);
+    quat_to_R(T.q, R);
+    const double x = p[0], y = p[1], z = p[2], z2 = z * z, fx = e.fx, fy = e.fy, bf = e.bf;
+    double Jp[9], Jt[18];
+    if (!e.stereo) {
+        const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++)
+                Jp[3 * i + j] = (-1. / z * tmp[3 * i]) * R[j] + (-1. / z * tmp[3 * i + 1]) * R[3 + j] +
+                                (-1. / z * tmp[3 * i + 2]) * R[6 + j];
+    } else {
+        for (int j = 0; j < 3; j++) {
+            Jp[j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
+            Jp[3 + j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
+            Jp[6 + j] = Jp[j] - bf * R[6 + j] / z2;
+        }
+    }
+    Jt[0] = x * y / z2 * fx; Jt[1] = -(1 + (x * x / z2)) * fx; Jt[2] = y / z * fx;
+    Jt[3] = -1. / z * fx; Jt[4] = 0; Jt[5] = x / z2 * fx;
+    Jt[6] = (1 + y * y / z2) * fy; Jt[7] = -x * y / z2 * fy; Jt[8] = -x / z * fy;
+    Jt[9] = 0; Jt[10] = -1. / z * fy; Jt[11] = y / z2 * fy;
+    if (e.stereo) {
+        Jt[12] = Jt[0] - bf * y / z2; Jt[13] = Jt[1] + bf * x / z2; Jt[14] = Jt[2];
+        Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf / z2;
+    }
+    const int D = e.stereo ? 3 : 2;
+    const double wW = r1 * e.info;
+    double omr[3];
+    _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) omr[i] = -(e.info * err[i]) * r1;
+    int u = 0;
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = a; b < 3; b++) {
+            double h = 0;
+            _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jp[3 * i + a] * wW * Jp[3 * i + b];
+            cl[u++] = h;
+        }
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        double v = 0;
+        _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) v += Jp[3 * i + a] * omr[i];
+        cl[6 + a] = v;
+    }
+    if (ppos >= 0) {
+        u = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+            for (int b = a; b < 6; b++) {
+                double h = 0;
+                _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jt[6 * i + a] * wW * Jt[6 * i + b];
+                cp[u++] = h;
+            }
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+            double v = 0;
+            _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) v += Jt[6 * i + a] * omr[i];
+            cp[21 + a] = v;
+        }
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+                double h = 0;
+                _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jt[6 * i + a] * wW * Jp[3 * i + b];
+                hp[3 * a + b] = h;
+            }
+    }
+    return r0;
+}
+
+// the linearisation at the current estimate -- only the first trial slot of an optimize() runs it:
+// every later iteration starts from the linearisation lba_errors formed for the accepted trial
+// (or, after an iteration that ended on a rejected trial, from the unchanged current one)
 __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     const bool in = s < g.nact;
     const uint8_t on = in ? g.on[s] : 0;
     EdgeDev e{};
-    if (in) e = g.E[s];
+    int lpos = 0, ppos = -1;
+    if (in) { e = g.E[s]; lpos = g.slot_lpos[s]; ppos = g.slot_ppos[s]; }
     const LMState lm = *g.lm;
     if (lm.done || !lm.newiter) return;
     double rchi = 0;
-    if (in && !on) {   // a level-1 edge: no share of the system (its stale _error is kept)
-        double *c = g.con + (long long)s * 36, *hp = g.hpl + (long long)s * 18;
-        for (int u = 0; u < 36; u++) c[u] = 0.0;
-        for (int u = 0; u < 18; u++) hp[u] = 0.0;
-    } else if (in) {
-        const int k = s;
-        double err[3];
-        const bool cur = lm.cur;
-        const Pose *Tc = cur ? g.T2 : g.T;
-        const double *Xc = cur ? g.X2 : g.X;
-        edge_error(g, e, Tc, Xc, err);
-        g.err[3 * k] = err[0]; g.err[3 * k + 1] = err[1]; g.err[3 * k + 2] = err[2];
-        const double chi = edge_chi2(e, err);
-        double r0 = chi, r1 = 1.0;
-        if (e.robust) huber(e, chi, r0, r1);
-        rchi = r0;
-        // Jacobians (types_six_dof_expmap.cpp:103-139, 188-234)
-        const Pose T = Tc[e.pose];
-        double p[3], R[9];
-        pose_map(T, Xc + 3 * e.point, p);
-        quat_to_R(T.q, R);
-        const double x = p[0], y = p[1], z = p[2], z2 = z * z, fx = e.fx, fy = e.fy, bf = e.bf;
-        double Jp[9], Jt[18];
-        if (!e.stereo) {
-            const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
-            for (int i = 0; i < 2; i++)
-                for (int j = 0; j < 3; j++)
-                    Jp[3 * i + j] = (-1. / z * tmp[3 * i]) * R[j] + (-1. / z * tmp[3 * i + 1]) * R[3 + j] +
-                                    (-1. / z * tmp[3 * i + 2]) * R[6 + j];
-        } else {
-            for (int j = 0; j < 3; j++) {
-                Jp[j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
-                Jp[3 + j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
-                Jp[6 + j] = Jp[j] - bf * R[6 + j] / z2;
-            }
-        }
-        Jt[0] = x * y / z2 * fx; Jt[1] = -(1 + (x * x / z2)) * fx; Jt[2] = y / z * fx;
-        Jt[3] = -1. / z * fx; Jt[4] = 0; Jt[5] = x / z2 * fx;
-        Jt[6] = (1 + y * y / z2) * fy; Jt[7] = -x * y / z2 * fy; Jt[8] = -x / z * fy;
-        Jt[9] = 0; Jt[10] = -1. / z * fy; Jt[11] = y / z2 * fy;
-        if (e.stereo) {
-            Jt[12] = Jt[0] - bf * y / z2; Jt[13] = Jt[1] + bf * x / z2; Jt[14] = Jt[2];
-            Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf / z2;
-        }
-        const int D = e.stereo ? 3 : 2;
-        const double wW = r1 * e.info;
-        double omr[3];
-        _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) omr[i] = -(e.info * err[i]) * r1;
-        double *c = g.con + (long long)s * 36;
-        int u = 0;
-#pragma unroll
-        for (int a = 0; a < 3; a++)
-#pragma unroll
-            for (int b = a; b < 3; b++) {
-                double h = 0;
-                _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jp[3 * i + a] * wW * Jp[3 * i + b];
-                c[u++] = h;
-            }
-#pragma unroll
-        for (int a = 0; a < 3; a++) {
-            double v = 0;
-            _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) v += Jp[3 * i + a] * omr[i];
-            c[6 + a] = v;
-        }
-        if (g.pose_hidx[e.pose] >= 0) {
-            u = 9;
-#pragma unroll
-            for (int a = 0; a < 6; a++)
-#pragma unroll
-                for (int b = a; b < 6; b++) {
-                    double h = 0;
-                    _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jt[6 * i + a] * wW * Jt[6 * i + b];
-                    c[u++] = h;
-                }
-#pragma unroll
-            for (int a = 0; a < 6; a++) {
-                double v = 0;
-                _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) v += Jt[6 * i + a] * omr[i];
-                c[30 + a] = v;
-            }
-            double *hp = g.hpl + (long long)s * 18;
-#pragma unroll
-            for (int a = 0; a < 6; a++)
-#pragma unroll
-                for (int b = 0; b < 3; b++) {
-                    double h = 0;
-                    _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jt[6 * i + a] * wW * Jp[3 * i + b];
-                    hp[3 * a + b] = h;
-                }
-        }
-    }
-    block_sum_to(rchi, g.partial + blockIdx.x);
+    if (in) rchi = linearize_slot(g, e, on, s, lpos, ppos, lm.cur ? g.T2 : g.T, lm.cur ? g.X2 : g.X, lm.cur);
+    block_sum_to(rchi, g.partial + chi_off(lm.cur) + blockIdx.x);
 }
 
-// Hll (3x3), b_l of one landmark (thread) -- the edges of a point are a CSR segment, summed in
-// order -- and the |diagonal| maximum of the block's 256-thread quarter -> partial[kRedBlocks + q]
-__device__ __forceinline__ void reduce_points_body(Graph &g, int l, int q, double *sh) {
+// Hll (3x3), b_l: one 16-lane group per landmark, lane k < 9 sums component k (Hll upper 6,
+// bl 3) of the landmark's contiguous run of landmark-major records (conl) in CSR order, 8 records
+// in flight; the |diagonal| maximum of the block's 16 landmarks -> partial[kRedBlocks + blockIdx]
+constexpr int kRPL = 16;   // landmarks per lba_reduce_points workgroup
+__device__ __forceinline__ void reduce_points_body(Graph &g, int set, double *sh) {
+    const int l = blockIdx.x * kRPL + (threadIdx.x >> 4), k = threadIdx.x & 15;
     double dmax = 0;
-    if (l < g.Lm) {
-        double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+    if (l < g.Lm && k < 9) {
         const int i0 = g.pt_start[l], i1 = g.pt_start[l + 1];
-        for (int i = i0; i < i1; i += 4) {   // 4 slot indices in flight, summed in order
-            int sl[4];
+        const double *cl = g.conl[set] + k;
+        double v = 0;
+        for (int i = i0; i < i1; i += 8) {
+            double r[8];
 #pragma unroll
-            for (int u = 0; u < 4; u++) sl[u] = i + u < i1 ? g.pt_items[i + u] : -1;
+            for (int u = 0; u < 8; u++) r[u] = i + u < i1 ? cl[9LL * (i + u)] : 0.0;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (sl[u] < 0) continue;
-                const double *c = g.con + (long long)sl[u] * 36;
-                for (int k = 0; k < 6; k++) h[k] += c[k];
-                for (int k = 0; k < 3; k++) b[k] += c[6 + k];
-            }
+            for (int u = 0; u < 8; u++)
+                if (i + u < i1) v += r[u];
         }
         double *H = g.Hll + 9 * l;
-        H[0] = h[0]; H[1] = h[1]; H[2] = h[2];
-        H[3] = h[1]; H[4] = h[3]; H[5] = h[4];
-        H[6] = h[2]; H[7] = h[4]; H[8] = h[5];
-        g.bl[3 * l] = b[0]; g.bl[3 * l + 1] = b[1]; g.bl[3 * l + 2] = b[2];
-        dmax = fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5])));
+        switch (k) {   // packed upper 00 01 02 11 12 22 -> the symmetric 3 x 3
+            case 0: H[0] = v; break;
+            case 1: H[1] = v; H[3] = v; break;
+            case 2: H[2] = v; H[6] = v; break;
+            case 3: H[4] = v; break;
+            case 4: H[5] = v; H[7] = v; break;
+            case 5: H[8] = v; break;
+            default: g.bl[3 * l + k - 6] = v;
+        }
+        if (k == 0 || k == 3 || k == 5) dmax = fabs(v);
     }
     sh[threadIdx.x] = dmax;
     __syncthreads();
-    const int t = threadIdx.x & 255, base = threadIdx.x - t;
     for (int s = 128; s > 0; s >>= 1) {
-        if (t < s) sh[base + t] = fmax(sh[base + t], sh[base + t + s]);
+        if ((int)threadIdx.x < s) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
         __syncthreads();
     }
-    if (t == 0) g.partial[kRedBlocks + q] = sh[base];
+    if (threadIdx.x == 0) g.partial[kRedBlocks + blockIdx.x] = sh[0];
 }
 
 // Hpp (6x6), b_p of one free pose on a 1024-thread workgroup: 32 slot groups x 32 lanes, lane
-// k < 27 of a group accumulates component k (Hpp upper 21 + b_p 6) of every 32nd slot, coalesced
-// 216-byte slot reads; the 32 group partials are summed in LDS in fixed order
-__device__ __forceinline__ void reduce_poses_body(Graph &g, int i, double (*sh)[33]) {
+// k < 27 of a group accumulates component k (Hpp upper 21 + b_p 6) of every 32nd slot of the
+// pose's contiguous run of pose-major records (conp: coalesced 216-byte record reads, no index
+// loads, the next 8 records in flight while the current 8 are summed); the 32 group partials are
+// summed in LDS in fixed order
+__device__ __forceinline__ void reduce_poses_body(Graph &g, int i, int set, double (*sh)[33]) {
     const int k = threadIdx.x & 31, grp = threadIdx.x >> 5;
     const int t0 = g.ps_start[i], t1 = g.ps_start[i + 1];
     double acc = 0;
     if (k < 27) {
-        int t = t0 + grp;
-        for (; t + 96 < t1; t += 128) {   // 4 slots in flight
-            const int s0 = g.ps_items[t], s1 = g.ps_items[t + 32], s2 = g.ps_items[t + 64], s3 = g.ps_items[t + 96];
-            const double v0 = g.con[(long long)s0 * 36 + 9 + k], v1 = g.con[(long long)s1 * 36 + 9 + k];
-            const double v2 = g.con[(long long)s2 * 36 + 9 + k], v3 = g.con[(long long)s3 * 36 + 9 + k];
-            acc += v0; acc += v1; acc += v2; acc += v3;
+        const double *cp = g.conp[set] + k;
+        double a[8], nx[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int t = t0 + grp + 32 * u;
+            a[u] = t < t1 ? cp[27LL * t] : 0.0;
         }
-        for (; t < t1; t += 32) acc += g.con[(long long)g.ps_items[t] * 36 + 9 + k];
+        for (int tb = t0 + grp; tb < t1; tb += 256) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int t = tb + 256 + 32 * u;
+                nx[u] = t < t1 ? cp[27LL * t] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (tb + 32 * u < t1) acc += a[u];
+#pragma unroll
+            for (int u = 0; u < 8; u++) a[u] = nx[u];
+        }
     }
     sh[grp][k] = acc;
     __syncthreads();
@@ -357,14 +392,16 @@ __device__ __forceinline__ void reduce_poses_body(Graph &g, int i, double (*sh)[
 // the pose reductions on 1024-thread workgroups spread the landmarks over 4x fewer CUs and took
 // 22 us against 8 + 10), the pose reductions one 1024-thread workgroup per free pose
 __global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
-    if (g.lm->done || !g.lm->newiter) return;
+    const LMState lm = *g.lm;
+    if (lm.done || !lm.newiter) return;
     __shared__ double shp[256];
-    reduce_points_body(g, blockIdx.x * 256 + threadIdx.x, blockIdx.x, shp);
+    reduce_points_body(g, lm.cur, shp);
 }
 __global__ __launch_bounds__(1024) void lba_reduce_poses(Graph g) {
-    if (g.lm->done || !g.lm->newiter) return;
+    const LMState lm = *g.lm;
+    if (lm.done || !lm.newiter) return;
     __shared__ double shq[32][33];
-    reduce_poses_body(g, blockIdx.x, shq);
+    reduce_poses_body(g, blockIdx.x, lm.cur, shq);
 }
 
 // ---- Schur: per landmark Dinv, L = chol(Dinv), Y block and w
@@ -403,13 +440,20 @@ __device__ inline void point_factor(const Graph &g, int l, double lambda, double
 // uses lambda = tau * maxDiagonal (tau = 1e-5, optimization_algorithm_levenberg.cpp:179-191);
 // otherwise lambda = the LM state's. Block 0 publishes lambda in scalars[5].
 __global__ __launch_bounds__(256) void lba_prep_slots(Graph g, int n0, int n1, int n2) {
-    if (g.lm->done) return;
-    const int mode = g.lm->newiter ? (g.lm->it == 0 ? 2 : 1) : 0;
-    double lambda = g.lm->lambda;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    // the slot's index entries go out with the LM-state load (no dependence on it)
+    const bool ist = t < g.nact;
+    const int ph = ist ? g.slot_ph[t] : -1, l_t = ist ? g.slot_pt[t] : 0, lpos = ist ? g.slot_lpos[t] : 0,
+              ppos = ist ? g.slot_ppos[t] : 0;
+    const LMState lm = *g.lm;
+    if (lm.done) return;
+    const int mode = lm.newiter ? (lm.it == 0 ? 2 : 1) : 0;
+    double lambda = lm.lambda;
     if (mode == 2 || (mode == 1 && blockIdx.x == 0)) {   // uniform per block
         __shared__ double sa[256], sb[256];
         double a = 0, b = 0;
-        for (int i = threadIdx.x; i < n0; i += 256) a += g.partial[i];
+        const double *chi = g.partial + chi_off(lm.cur);   // the current linearisation's chi2 sums
+        for (int i = threadIdx.x; i < n0; i += 256) a += chi[i];
         for (int i = threadIdx.x; i < n1; i += 256) b = fmax(b, g.partial[kRedBlocks + i]);
         for (int i = threadIdx.x; i < n2; i += 256) b = fmax(b, g.partial[2 * kRedBlocks + i]);
         sa[threadIdx.x] = a;
@@ -425,21 +469,19 @@ __global__ __launch_bounds__(256) void lba_prep_slots(Graph g, int n0, int n1, i
         if (mode == 2) lambda = 1e-5 * sb[0];
         if (blockIdx.x == 0 && threadIdx.x == 0) { g.scalars[0] = sa[0]; g.scalars[1] = sb[0]; }
     }
-    const int t = blockIdx.x * 256 + threadIdx.x;
     if (t == 0) g.scalars[5] = lambda;
     const long long W = g.NPW;
     double Di[9], L[6];
-    if (t < g.nact) {
-        const int ph = g.slot_ph[t];
+    if (ist) {
         if (ph < 0) return;
-        const int l = g.slot_pt[t];
+        const int l = l_t;
         point_factor(g, l, lambda, Di, L);
-        const double *B = g.hpl + (long long)t * 18;
+        const double *B = g.hpl[lm.cur] + 18LL * lpos;
         double *y = g.Y + 3LL * l * W + 6 * ph;   // Y^T rows 3l..3l+2, columns 6ph..6ph+5
         // w_l = L^T b_l exactly as the landmark threads form it, for this block's share of Y w
         const double *bl = g.bl + 3 * l;
         const double w0 = L[0] * bl[0] + L[1] * bl[1] + L[2] * bl[2], w1 = L[3] * bl[1] + L[4] * bl[2], w2 = L[5] * bl[2];
-        double *yw = g.ywp + 6LL * g.slot_ppos[t];
+        double *yw = g.ywp + 6LL * ppos;
 #pragma unroll
         for (int r = 0; r < 6; r++) {
             const double b0 = B[3 * r], b1 = B[3 * r + 1], b2 = B[3 * r + 2];
@@ -543,42 +585,35 @@ __global__ __launch_bounds__(256) void lba_schur_tiles(Graph g) {
     for (int q = 0; q < 4; q++) part[64 * q + lane] = ((red[0][q][lane] + red[1][q][lane]) + red[2][q][lane]) + red[3][q][lane];
 }
 
-// one wave per tile pair: the pair's chunk tiles summed in chunk order, Hpp on the pose-diagonal
-// 6 x 6 blocks, lambda on the diagonal; tile (I, J) and its transpose into Hs
-__global__ __launch_bounds__(64) void lba_schur_finish(Graph g) {
-    if (g.lm->done) return;
-    const int lane = threadIdx.x, p = blockIdx.x;
+// one 4-wave workgroup per tile pair, wave q = rows 4q..4q+3 of the MFMA C tile: the pair's
+// chunk tiles summed in chunk order (up to 32 chunk loads in flight per lane), Hpp on the
+// pose-diagonal 6 x 6 blocks, lambda on the diagonal; tile (I, J) and its transpose into Hs
+__global__ __launch_bounds__(256) void lba_schur_finish(Graph g) {
+    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6, p = blockIdx.x;
     const int2 ij = g.tp_ij[p], nc = g.tp_nch[p];   // (I, J); first chunk, chunk count
+    if (g.lm->done) return;
     const int I = ij.x, J = ij.y, n6 = 6 * g.P;
     const long long NP = g.NP;
     const double lambda = g.scalars[5];
-    // chunk tiles in chunk order, 8 chunks x 4 registers of loads in flight per round
-    double v[4] = {0, 0, 0, 0};
-    const double *tp = g.tp_part + 256LL * nc.x + lane;
-    for (int c0 = 0; c0 < nc.y; c0 += 8) {
-        double t[8][4];
+    double v = 0;
+    const double *tp = g.tp_part + 256LL * nc.x + 64 * q + lane;
+    for (int c0 = 0; c0 < nc.y; c0 += 32) {
+        double t[32];
 #pragma unroll
-        for (int u = 0; u < 8; u++)
+        for (int u = 0; u < 32; u++) t[u] = c0 + u < nc.y ? tp[256LL * (c0 + u)] : 0.0;
 #pragma unroll
-            for (int q = 0; q < 4; q++) t[u][q] = c0 + u < nc.y ? tp[256LL * (c0 + u) + 64 * q] : 0.0;
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (c0 + u < nc.y) v[q] += t[u][q];
+        for (int u = 0; u < 32; u++)
+            if (c0 + u < nc.y) v += t[u];
     }
     // C/D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * q
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int row = 16 * I + (lane >> 4) + 4 * q, col = 16 * J + (lane & 15);
-        if (row >= n6 || col >= n6) continue;
-        double h = 0;
-        if (row / 6 == col / 6) h = g.Hpp[36 * (row / 6) + 6 * (row % 6) + (col % 6)];
-        if (row == col) h += lambda;
-        h -= v[q];
-        g.Hs[row * NP + col] = h;
-        if (I != J) g.Hs[(long long)col * NP + row] = h;
-    }
+    const int row = 16 * I + (lane >> 4) + 4 * q, col = 16 * J + (lane & 15);
+    if (row >= n6 || col >= n6) return;
+    double h = 0;
+    if (row / 6 == col / 6) h = g.Hpp[36 * (row / 6) + 6 * (row % 6) + (col % 6)];
+    if (row == col) h += lambda;
+    h -= v;
+    g.Hs[row * NP + col] = h;
+    if (I != J) g.Hs[(long long)col * NP + row] = h;
 }
 
 // Dense Cholesky of the n6 x n6 Schur matrix + forward / back substitution (replaces
@@ -613,12 +648,36 @@ template <int C> __device__ __forceinline__ double row_bcast(double v) {
 #define LBA_DIAG_PRIO 0    // s_setprio of wave 0 while it factors a diagonal tile (critical path)
 #endif
 
-template <int J, int C> __device__ __forceinline__ void chol16_update(double (&row)[16], double (&li)[16]) {
+#ifndef LBA_DPP_FMAC
+#define LBA_DPP_FMAC 1   // 1: the column updates as v_fmac_f64 with a DPP64 row_newbcast source
+#endif
+// acc += (value of lane C of each 16-lane row of src) * m: the broadcast folded into the FMA
+// (v_fmac_f64_dpp, DPP64 row_newbcast). NOP: two wait states first for a DPP read of a VGPR a
+// VALU has just written (the compiler does not track hazards across inline asm)
+template <int C, bool NOP> __device__ __forceinline__ void fmac_bcast(double &acc, double src, double m) {
+    if constexpr (NOP)
+        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                     : "+v"(acc) : "v"(src), "v"(m), "i"(C));
+    else
+        asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(src), "v"(m), "i"(C));
+}
+template <int C> __device__ __forceinline__ double bcast64(double src) {
+    double d;
+    asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(d) : "v"(src), "i"(C));
+    return d;
+}
+
+template <int J, int C> __device__ __forceinline__ void chol16_update(double (&row)[16], double (&li)[16], double nr, double nl) {
     if constexpr (C < 16) {
+#if LBA_DPP_FMAC
+        fmac_bcast<C, C == J + 1>(row[C], row[J], nr);   // row[C] -= L[C][J] row[J]
+        fmac_bcast<C, false>(li[C], row[J], nl);         // li[C] -= L[C][J] li[J]
+#else
         const double l = row_bcast<C>(row[J]);   // L[C][J]
         row[C] = __builtin_fma(-row[J], l, row[C]);
         li[C] = __builtin_fma(-l, li[J], li[C]);
-        chol16_update<J, C + 1>(row, li);
+#endif
+        chol16_update<J, C + 1>(row, li, nr, nl);
     }
 }
 
@@ -629,7 +688,11 @@ template <int J, int C> __device__ __forceinline__ void chol16_update(double (&r
 template <int J> __device__ __forceinline__ void chol16_factor(double (&row)[16], double (&li)[16], int i, int lim,
                                                                bool &bad) {
     if constexpr (J < 16) {
+#if LBA_DPP_FMAC
+        double d = bcast64<J>(row[J]);
+#else
         double d = row_bcast<J>(row[J]);
+#endif
         if (J >= lim) d = 1.0;
         bad |= !(d > 0);
         const double h = 0.5 * d;
@@ -640,7 +703,7 @@ template <int J> __device__ __forceinline__ void chol16_factor(double (&row)[16]
 #endif
         row[J] = i == J ? d * y : row[J] * y;
         li[J] = (i == J ? 1.0 + li[J] : li[J]) * y;   // li[J] held -sum L[J][k] li[k]
-        chol16_update<J, J + 1>(row, li);
+        chol16_update<J, J + 1>(row, li, -row[J], -li[J]);
         chol16_factor<J + 1>(row, li, i, lim, bad);
     }
 }
@@ -707,7 +770,8 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
         double *LK = Linv + K * 16 * 17;
         double row[16], li[16];   // li: column i of L_kk^-1
 #pragma unroll
-        for (int c = 0; c < 16; c++) row[c] = c <= i ? A[(k0 + i) * LDA + k0 + c] : 0.0;
+        for (int c = 0; c < 16; c++) row[c] = A[(k0 + i) * LDA + k0 + c];   // the upper part (never written:
+        // any bits) only ever meets lane i's own columns > i, which no broadcast reads
 #pragma unroll
         for (int r = 0; r < 16; r++) li[r] = 0.0;
         bool bad = false;
@@ -955,9 +1019,10 @@ __global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
     const int lt = t - g.P;
     const bool isp = lt >= 0 && lt < g.Lm;
     const int i0p = isp ? g.pt_start[lt] : 0, i1p = isp ? g.pt_start[lt + 1] : 0;
-    if (g.lm->done) return;
+    const LMState lm = *g.lm;
+    if (lm.done) return;
     const double lambda = g.scalars[5];
-    const bool cur = g.lm->cur;   // current estimate -> trial buffer
+    const bool cur = lm.cur;   // current estimate -> trial buffer
     const Pose *Tc = cur ? g.T2 : g.T;
     Pose *Tt = cur ? g.T : g.T2;
     const double *Xc = cur ? g.X2 : g.X;
@@ -972,16 +1037,15 @@ __global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
         const int l = t - g.P, v = g.hpoint[l];
         double c[3] = {g.bl[3 * l], g.bl[3 * l + 1], g.bl[3 * l + 2]};
         const int i0 = i0p, i1 = i1p;
-        for (int i = i0; i < i1; i += 4) {   // 4 edges' index chains in flight, applied in order
-            int sl[4], ph[4];
+        const double *hpL = g.hpl[cur];
+        for (int i = i0; i < i1; i += 4) {   // 4 records (landmark-major, contiguous) in flight, applied in order
+            int ph[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) sl[u] = i + u < i1 ? g.pt_items[i + u] : -1;
-#pragma unroll
-            for (int u = 0; u < 4; u++) ph[u] = sl[u] >= 0 ? g.slot_ph[sl[u]] : -1;
+            for (int u = 0; u < 4; u++) ph[u] = i + u < i1 ? g.lpos_ph[i + u] : -1;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 if (ph[u] < 0) continue;
-                const double *B = g.hpl + (long long)sl[u] * 18;
+                const double *B = hpL + 18LL * (i + u);
                 const double *xp = g.x + 6 * ph[u];
                 for (int cc = 0; cc < 3; cc++) {
                     double v = 0;
@@ -1006,26 +1070,22 @@ __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthrea
 // Trial chi2 of the active edges (block sums -> part[]) fused with the LM decision: the last
 // block to arrive (agent-scope release by every wave, one counter; the arriving block acquires,
 // cdna_hip_programming.md G16) sums the partials and runs lm_decide -- one launch fewer per trial.
+// Each slot also linearises the trial estimate into the trial's linearisation set (the chi2 it
+// needs is the trial chi2 itself): an accepted trial swaps the sets with the estimates, so the
+// next iteration starts at its reductions without a lba_linearize launch.
 __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part, int nbu, int nbe, int np, int nq) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     const bool in = s < g.nact;
     const uint8_t on = in ? g.on[s] : 0;
     EdgeDev e{};
-    if (in) e = g.E[s];   // slot s = edge s (lba_linearize)
+    int lpos = 0, ppos = -1;
+    if (in) { e = g.E[s]; lpos = g.slot_lpos[s]; ppos = g.slot_ppos[s]; }   // slot s = edge s (lba_linearize)
     const bool done = g.lm->done, cur = g.lm->cur;
     if (done) return;
     double r0 = 0;
-    if (in && on) {
-        const int k = s;
-        double err[3];
-        edge_error(g, e, cur ? g.T : g.T2, cur ? g.X : g.X2, err);
-        g.err[3 * k] = err[0]; g.err[3 * k + 1] = err[1]; g.err[3 * k + 2] = err[2];
-        const double chi = edge_chi2(e, err);
-        double r1 = 1;
-        r0 = chi;
-        if (e.robust) huber(e, chi, r0, r1);
-    }
-    block_sum_to(r0, part + blockIdx.x);
+    if (in) r0 = linearize_slot(g, e, on, s, lpos, ppos, cur ? g.T : g.T2, cur ? g.X : g.X2, !cur);
+    const double bsum = block_sum_to(r0, part + blockIdx.x);
+    if (threadIdx.x == 0) g.partial[chi_off(!cur) + blockIdx.x] = bsum;
     __shared__ int last;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this wave's stores (err, part) reach L2 / memory
     __syncthreads();
@@ -1258,7 +1318,7 @@ struct HostGraph {
 struct ActiveSet {
     int P = 0, Lm = 0;
     std::vector<int> act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items, ps_start, ps_items, slot_pt, slot_ph,
-        slot_ppos;
+        slot_ppos, slot_lpos, lpos_ph;
     std::vector<int2> tp_ij, tp_nch;     // Schur tile pairs (build_schur_tiles)
     std::vector<int> tp_start, tp_rows;
     std::vector<int4> tp_chunk;
@@ -1406,11 +1466,16 @@ void build_active(const HostGraph &h, ActiveSet &A) {
     A.slot_pt.assign(std::max<size_t>(1, A.act.size()), 0);
     A.slot_ph.assign(std::max<size_t>(1, A.act.size()), -1);
     A.slot_ppos.assign(std::max<size_t>(1, A.act.size()), -1);
+    A.slot_lpos.assign(std::max<size_t>(1, A.act.size()), 0);
+    A.lpos_ph.assign(std::max<size_t>(1, A.act.size()), -1);
     for (int s = 0; s < (int)A.act.size(); s++) {
         const int k = A.act[s];
         const int l = A.point_hidx[h.edge_point[k]];
-        A.pt_items[A.pt_start[l] + fl[l]++] = s;
+        const int lpos = A.pt_start[l] + fl[l]++;
+        A.pt_items[lpos] = s;
+        A.slot_lpos[s] = lpos;
         const int ph = A.pose_hidx[h.edge_pose[k]];
+        A.lpos_ph[lpos] = ph;
         A.slot_pt[s] = l;
         A.slot_ph[s] = ph;
         A.slot_ppos[s] = -1;
@@ -1467,26 +1532,30 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
     auto term = [&]() { return stop && *stop; };
     if (A.P + A.Lm == 0) return -1;
     if (A.P > kMaxPoses) return -2;
+    if (nblk((int)A.act.size()) > kRedBlocks || (A.Lm + kRPL - 1) / kRPL > kRedBlocks) return -2;   // partial regions
     const int nact = (int)A.act.size();
     const int n6 = 6 * A.P;
     const int nbu = nblk(A.P + A.Lm), nbe = nblk(nact);
-    auto slot = [&]() {
-        int ph = lprof_begin(e);
-        lba_linearize<<<nblk(nact), 256, 0, s>>>(g);
-        lprof_end(e, ph, "lba_linearize");
+    auto slot = [&](bool first) {
+        int ph;
+        if (first) {   // later iterations start from lba_errors' linearisation of the accepted trial
+            ph = lprof_begin(e);
+            lba_linearize<<<nblk(nact), 256, 0, s>>>(g);
+            lprof_end(e, ph, "lba_linearize");
+        }
         ph = lprof_begin(e);
-        lba_reduce_points<<<nblk(A.Lm), 256, 0, s>>>(g);
+        lba_reduce_points<<<std::max(1, (A.Lm + kRPL - 1) / kRPL), 256, 0, s>>>(g);
         if (A.P > 0) lba_reduce_poses<<<A.P, 1024, 0, s>>>(g);
         lprof_end(e, ph, "lba_reduce");
         ph = lprof_begin(e);
-        lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nblk(nact), nblk(A.Lm), A.P);
+        lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nblk(nact), std::max(1, (A.Lm + kRPL - 1) / kRPL), A.P);
         lprof_end(e, ph, "lba_prep_slots");
         if (A.P > 0) {
             ph = lprof_begin(e);
             lba_schur_tiles<<<g.nchunks + (n6 + 3) / 4, 256, 0, s>>>(g);
             lprof_end(e, ph, "lba_schur_tiles");
             ph = lprof_begin(e);
-            lba_schur_finish<<<g.npairs, 64, 0, s>>>(g);
+            lba_schur_finish<<<g.npairs, 256, 0, s>>>(g);
             lprof_end(e, ph, "lba_schur_finish");
             ph = lprof_begin(e);
             if (n6 <= kSmallNP) {
@@ -1522,7 +1591,7 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
     int chunk = iterations, slots = 0;
     LMState st{};
     while (true) {
-        for (int k = 0; k < chunk; k++) slot();
+        for (int k = 0; k < chunk; k++) slot(slots + k == 0);
         slots += chunk;
         if (hipMemcpyAsync(e->h_lm, g.lm, sizeof(LMState), hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
@@ -1665,7 +1734,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
                      o_hpose = ub.add(A.hpose), o_hpoint = ub.add(A.hpoint), o_pt_start = ub.add(A.pt_start),
                      o_pt_items = ub.add(A.pt_items), o_ps_start = ub.add(A.ps_start), o_ps_items = ub.add(A.ps_items),
                      o_slot_pt = ub.add(A.slot_pt), o_slot_ph = ub.add(A.slot_ph);
-        const size_t o_slot_ppos = ub.add(A.slot_ppos);
+        const size_t o_slot_ppos = ub.add(A.slot_ppos), o_slot_lpos = ub.add(A.slot_lpos), o_lpos_ph = ub.add(A.lpos_ph);
         const size_t o_tp_ij = ub.add(A.tp_ij), o_tp_start = ub.add(A.tp_start), o_tp_rows = ub.add(A.tp_rows),
                      o_tp_chunk = ub.add(A.tp_chunk), o_tp_nch = ub.add(A.tp_nch);
         const size_t o_E = edges ? ub.add(*edges) : 0;
@@ -1682,6 +1751,8 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.slot_pt = at<int>(e->arenaB, o_slot_pt); g.slot_ph = at<int>(e->arenaB, o_slot_ph);
         if (edges) g.E = at<EdgeDev>(e->arenaB, o_E);
         g.slot_ppos = at<int>(e->arenaB, o_slot_ppos);
+        g.slot_lpos = at<int>(e->arenaB, o_slot_lpos);
+        g.lpos_ph = at<int>(e->arenaB, o_lpos_ph);
         g.tp_ij = at<int2>(e->arenaB, o_tp_ij);
         g.tp_start = at<int>(e->arenaB, o_tp_start);
         g.tp_rows = at<int>(e->arenaB, o_tp_rows);
@@ -1696,7 +1767,8 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         const size_t NP = (size_t)g.NP, NPW = NP + 16;
         g.NPW = (int)NPW;
         g.wrow = 16 * std::max(1, (6 * A.P + 15) / 16);
-        if (e->con.ensure(sizeof(double) * 36 * std::max(nact, 1)) || e->hpl.ensure(sizeof(double) * 18 * std::max(nact, 1)) ||
+        const size_t nl = std::max(nact, 1), npp = std::max<size_t>(1, A.ps_items.size());
+        if (e->con.ensure(sizeof(double) * 2 * (9 * nl + 27 * npp)) || e->hpl.ensure(sizeof(double) * 2 * 18 * nl) ||
             e->Hll.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) || e->bl.ensure(sizeof(double) * 3 * std::max(A.Lm, 1)) ||
             e->Hpp.ensure(sizeof(double) * 36 * std::max(A.P, 1)) || e->bp.ensure(sizeof(double) * 6 * std::max(A.P, 1)) ||
             e->Dinv.ensure(sizeof(double) * 9 * std::max(A.Lm, 1)) || e->Lc.ensure(sizeof(double) * 6 * std::max(A.Lm, 1)) ||
@@ -1704,7 +1776,9 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
             e->ywp.ensure(sizeof(double) * 6 * std::max<size_t>(1, A.ps_items.size())) ||
             e->bs.ensure(sizeof(double) * NP) || e->x.ensure(sizeof(double) * (6 * A.P + 3 * A.Lm + 8)))
             return -1;
-        g.con = e->con.as<double>(); g.hpl = e->hpl.as<double>();
+        g.conl[0] = e->con.as<double>(); g.conl[1] = g.conl[0] + 9 * nl;
+        g.conp[0] = g.conl[1] + 9 * nl; g.conp[1] = g.conp[0] + 27 * npp;
+        g.hpl[0] = e->hpl.as<double>(); g.hpl[1] = g.hpl[0] + 18 * nl;
         g.Hll = e->Hll.as<double>(); g.bl = e->bl.as<double>();
         g.Hpp = e->Hpp.as<double>(); g.bp = e->bp.as<double>();
         g.Dinv = e->Dinv.as<double>(); g.Lc = e->Lc.as<double>(); g.Y = e->Y.as<double>();

@@ -5,14 +5,16 @@
 set -u
 cd /tmp && export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
-timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU --output-format csv -d "$R/gpurun_out/pmc_stall" -o run -- python3 "$R/tools/prof_extract.py" 128 2 > "$R/gpurun_out/pmc_stall.log" 2>&1
+TAG="${TAG:-pmc_stall}"   # TAG=lba_stall DRV="lba_prof.py 3": the LocalBA kernels
+DRV="${DRV:-prof_extract.py 128 2}"
+timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU --output-format csv -d "$R/gpurun_out/$TAG" -o run -- python3 "$R/tools/"$DRV > "$R/gpurun_out/$TAG.log" 2>&1
 rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc
-cd "$R" && python3 - <<'PY'
-import csv, glob, collections
+cd "$R" && TAG="$TAG" python3 - <<'PY'
+import csv, glob, collections, os
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
-for f in glob.glob('gpurun_out/pmc_stall/**/*counter_collection.csv', recursive=True):
+for f in glob.glob(f"gpurun_out/{os.environ['TAG']}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r['Kernel_Name'].split('(')[0].replace('void ', '').split('::')[-1]
+        k = r['Kernel_Name'].split('(')[0].replace('void ', '').split('::')[-1][:28]
         if not k.startswith('__amd'):
             acc[k][r['Counter_Name']] += float(r['Counter_Value'])
 for k, c in sorted(acc.items()):
