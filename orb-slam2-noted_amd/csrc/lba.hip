@@ -184,21 +184,40 @@ __device__ __forceinline__ int chi_off(int set) { return set ? 3 * kRedBlocks : 
 // residual (g2o _error), Huber weight, analytic 2x9 / 3x9 Jacobians (types_six_dof_expmap.cpp
 // :103-139, 188-234) and the quadratic-form pieces, landmark part at the slot's pt_items position
 // `lpos`, pose part at its ps_items position `ppos` (-1: fixed pose, no pose part). A level-1 slot
-// (on = 0) keeps its stale _error and contributes zeros. Returns the robust chi2.
+// (on = 0) keeps its stale _error and contributes zeros. Two wave-uniform roles share a slot
+// (twice the waves, each with about half the FP64 chain): role 0 writes the residual, Hll / bl
+// and Hpl and returns the robust chi2; role 1 writes Hpp / bp (and returns 0).
+#ifndef LBA_LIN_ROLES
+#define LBA_LIN_ROLES 1   // 2: two wave-uniform roles per slot (more waves, each half the FP64 chain)
+#endif
+constexpr int kLinEdges = LBA_LIN_ROLES == 2 ? 128 : 256;   // slots per 256-thread workgroup
+__device__ __forceinline__ void lin_thread(int &s, int &role) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+#if LBA_LIN_ROLES == 2
+    s = (t >> 7) * 64 + (t & 63);
+    role = (t >> 6) & 1;   // wave-uniform
+#else
+    s = t;
+    role = 2;
+#endif
+}
 __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &e, bool on, int s, int lpos, int ppos,
-                                                 const Pose *Tc, const double *Xc, int set) {
+                                                 const Pose *Tc, const double *Xc, int set, int role) {
     double *cl = g.conl[set] + 9LL * lpos, *hp = g.hpl[set] + 18LL * lpos;
     double *cp = g.conp[set] + 27LL * (ppos < 0 ? 0 : ppos);
+    if (role == 1 && ppos < 0) return 0.0;   // no pose part
     if (!on) {
-        for (int u = 0; u < 9; u++) cl[u] = 0.0;
-        for (int u = 0; u < 18; u++) hp[u] = 0.0;
-        if (ppos >= 0)
+        if (role != 1) {
+            for (int u = 0; u < 9; u++) cl[u] = 0.0;
+            for (int u = 0; u < 18; u++) hp[u] = 0.0;
+        }
+        if (role != 0 && ppos >= 0)
             for (int u = 0; u < 27; u++) cp[u] = 0.0;
         return 0.0;
     }
     double err[3];
     edge_error(g, e, Tc, Xc, err);
-    g.err[3 * s] = err[0]; g.err[3 * s + 1] = err[1]; g.err[3 * s + 2] = err[2];
+    if (role != 1) { g.err[3 * s] = err[0]; g.err[3 * s + 1] = err[1]; g.err[3 * s + 2] = err[2]; }
     const double chi = edge_chi2(e, err);
     double r0 = chi, r1 = 1.0;
     if (e.robust) huber(e, chi, r0, r1);
@@ -207,7 +226,38 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
     pose_map(T, Xc + 3 * e.point, p);
     quat_to_R(T.q, R);
     const double x = p[0], y = p[1], z = p[2], z2 = z * z, fx = e.fx, fy = e.fy, bf = e.bf;
-    double Jp[9], Jt[18];
+    double Jt[18];
+    Jt[0] = x * y / z2 * fx; Jt[1] = -(1 + (x * x / z2)) * fx; Jt[2] = y / z * fx;
+    Jt[3] = -1. / z * fx; Jt[4] = 0; Jt[5] = x / z2 * fx;
+    Jt[6] = (1 + y * y / z2) * fy; Jt[7] = -x * y / z2 * fy; Jt[8] = -x / z * fy;
+    Jt[9] = 0; Jt[10] = -1. / z * fy; Jt[11] = y / z2 * fy;
+    if (e.stereo) {
+        Jt[12] = Jt[0] - bf * y / z2; Jt[13] = Jt[1] + bf * x / z2; Jt[14] = Jt[2];
+        Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf / z2;
+    }
+    const int D = e.stereo ? 3 : 2;
+    const double wW = r1 * e.info;
+    double omr[3];
+    _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) omr[i] = -(e.info * err[i]) * r1;
+    if (role != 0 && ppos >= 0) {
+        int u = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+            for (int b = a; b < 6; b++) {
+                double h = 0;
+                _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jt[6 * i + a] * wW * Jt[6 * i + b];
+                cp[u++] = h;
+            }
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+            double v = 0;
+            _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) v += Jt[6 * i + a] * omr[i];
+            cp[21 + a] = v;
+        }
+    }
+    if (role == 1) return 0.0;
+    double Jp[9];
     if (!e.stereo) {
         const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
         for (int i = 0; i < 2; i++)
@@ -221,18 +271,6 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
             Jp[6 + j] = Jp[j] - bf * R[6 + j] / z2;
         }
     }
-    Jt[0] = x * y / z2 * fx; Jt[1] = -(1 + (x * x / z2)) * fx; Jt[2] = y / z * fx;
-    Jt[3] = -1. / z * fx; Jt[4] = 0; Jt[5] = x / z2 * fx;
-    Jt[6] = (1 + y * y / z2) * fy; Jt[7] = -x * y / z2 * fy; Jt[8] = -x / z * fy;
-    Jt[9] = 0; Jt[10] = -1. / z * fy; Jt[11] = y / z2 * fy;
-    if (e.stereo) {
-        Jt[12] = Jt[0] - bf * y / z2; Jt[13] = Jt[1] + bf * x / z2; Jt[14] = Jt[2];
-        Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf / z2;
-    }
-    const int D = e.stereo ? 3 : 2;
-    const double wW = r1 * e.info;
-    double omr[3];
-    _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) omr[i] = -(e.info * err[i]) * r1;
     int u = 0;
 #pragma unroll
     for (int a = 0; a < 3; a++)
@@ -249,21 +287,6 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
         cl[6 + a] = v;
     }
     if (ppos >= 0) {
-        u = 0;
-#pragma unroll
-        for (int a = 0; a < 6; a++)
-#pragma unroll
-            for (int b = a; b < 6; b++) {
-                double h = 0;
-                _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) h += Jt[6 * i + a] * wW * Jt[6 * i + b];
-                cp[u++] = h;
-            }
-#pragma unroll
-        for (int a = 0; a < 6; a++) {
-            double v = 0;
-            _Pragma("unroll") for (int i = 0; i < 3; i++) if (i < D) v += Jt[6 * i + a] * omr[i];
-            cp[21 + a] = v;
-        }
 #pragma unroll
         for (int a = 0; a < 6; a++)
 #pragma unroll
@@ -280,7 +303,8 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
 // every later iteration starts from the linearisation lba_errors formed for the accepted trial
 // (or, after an iteration that ended on a rejected trial, from the unchanged current one)
 __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
-    const int s = blockIdx.x * 256 + threadIdx.x;
+    int s, role;
+    lin_thread(s, role);
     const bool in = s < g.nact;
     const uint8_t on = in ? g.on[s] : 0;
     EdgeDev e{};
@@ -289,7 +313,7 @@ __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
     const LMState lm = *g.lm;
     if (lm.done || !lm.newiter) return;
     double rchi = 0;
-    if (in) rchi = linearize_slot(g, e, on, s, lpos, ppos, lm.cur ? g.T2 : g.T, lm.cur ? g.X2 : g.X, lm.cur);
+    if (in) rchi = linearize_slot(g, e, on, s, lpos, ppos, lm.cur ? g.T2 : g.T, lm.cur ? g.X2 : g.X, lm.cur, role);
     block_sum_to(rchi, g.partial + chi_off(lm.cur) + blockIdx.x);
 }
 
@@ -336,31 +360,27 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, double *sh
 // Hpp (6x6), b_p of one free pose on a 1024-thread workgroup: 32 slot groups x 32 lanes, lane
 // k < 27 of a group accumulates component k (Hpp upper 21 + b_p 6) of every 32nd slot of the
 // pose's contiguous run of pose-major records (conp: coalesced 216-byte record reads, no index
-// loads, the next 8 records in flight while the current 8 are summed); the 32 group partials are
-// summed in LDS in fixed order
+// loads, LBA_RP records per lane in flight); the 32 group partials are summed in LDS in fixed order
+#ifndef LBA_RP
+#define LBA_RP 32   // records per lane per batch in reduce_poses_body
+#endif
 __device__ __forceinline__ void reduce_poses_body(Graph &g, int i, int set, double (*sh)[33]) {
     const int k = threadIdx.x & 31, grp = threadIdx.x >> 5;
     const int t0 = g.ps_start[i], t1 = g.ps_start[i + 1];
     double acc = 0;
-    if (k < 27) {
+    if (k < 27) {   // batches of RP records per lane, all in flight (one batch up to 32 RP slots per pose)
+        constexpr int RP = LBA_RP;
         const double *cp = g.conp[set] + k;
-        double a[8], nx[8];
+        for (int tb = t0 + grp; tb < t1; tb += 32 * RP) {
+            double a[RP];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int t = t0 + grp + 32 * u;
-            a[u] = t < t1 ? cp[27LL * t] : 0.0;
-        }
-        for (int tb = t0 + grp; tb < t1; tb += 256) {
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int t = tb + 256 + 32 * u;
-                nx[u] = t < t1 ? cp[27LL * t] : 0.0;
+            for (int u = 0; u < RP; u++) {
+                const int t = tb + 32 * u;
+                a[u] = t < t1 ? cp[27LL * t] : 0.0;
             }
 #pragma unroll
-            for (int u = 0; u < 8; u++)
+            for (int u = 0; u < RP; u++)
                 if (tb + 32 * u < t1) acc += a[u];
-#pragma unroll
-            for (int u = 0; u < 8; u++) a[u] = nx[u];
         }
     }
     sh[grp][k] = acc;
@@ -521,7 +541,7 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 // b_schur, one wave per row: b_p - the sum of the pose's slot pieces Y_block w_l (ywp, written
 // pose-major by lba_prep_slots).
 #ifndef LBA_KSCH
-#define LBA_KSCH 32
+#define LBA_KSCH 64
 #endif
 constexpr int kSCH = LBA_KSCH;   // MFMA steps (4 Y^T rows each) per chunk workgroup
 __global__ __launch_bounds__(256) void lba_schur_tiles(Graph g) {
@@ -684,16 +704,19 @@ template <int J, int C> __device__ __forceinline__ void chol16_update(double (&r
 // Lane i (of each 16-lane row) holds row i of the tile; column J is pivoted, scaled by the
 // reciprocal square root (v_rsq_f64 + 2 Newton steps) and subtracted from columns > J.
 // li carries column i of L^-1 by forward substitution, fed by the same broadcasts.
-// Pivots at J >= lim (rows >= n: padding and the appended right-hand side) are forced to 1.
-template <int J> __device__ __forceinline__ void chol16_factor(double (&row)[16], double (&li)[16], int i, int lim,
-                                                               bool &bad) {
+// FULL (every tile but the last, all 16 rows < n): li starts as the unit column e_i and lane
+// J's own row[J] is the pivot d, so the pivot step is two products; otherwise pivots at
+// J >= lim (rows >= n: padding and the appended right-hand side) are forced to 1, li starts at 0
+// and lane J takes the unit diagonal term at its pivot.
+template <int J, bool FULL> __device__ __forceinline__ void chol16_factor(double (&row)[16], double (&li)[16], int i, int lim,
+                                                                          bool &bad) {
     if constexpr (J < 16) {
 #if LBA_DPP_FMAC
         double d = bcast64<J>(row[J]);
 #else
         double d = row_bcast<J>(row[J]);
 #endif
-        if (J >= lim) d = 1.0;
+        if (!FULL && J >= lim) d = 1.0;
         bad |= !(d > 0);
         const double h = 0.5 * d;
         double y = __builtin_amdgcn_rsq(d);
@@ -701,10 +724,15 @@ template <int J> __device__ __forceinline__ void chol16_factor(double (&row)[16]
 #if LBA_RSQ_NEWTON > 1
         y = __builtin_fma(y, __builtin_fma(-(h * y), y, 0.5), y);
 #endif
-        row[J] = i == J ? d * y : row[J] * y;
-        li[J] = (i == J ? 1.0 + li[J] : li[J]) * y;   // li[J] held -sum L[J][k] li[k]
+        if constexpr (FULL) {
+            row[J] = row[J] * y;   // lane J: d * y
+            li[J] = li[J] * y;     // lane J: 1 * y
+        } else {
+            row[J] = i == J ? d * y : row[J] * y;
+            li[J] = (i == J ? 1.0 + li[J] : li[J]) * y;   // li[J] held -sum L[J][k] li[k]
+        }
         chol16_update<J, J + 1>(row, li, -row[J], -li[J]);
-        chol16_factor<J + 1>(row, li, i, lim, bad);
+        chol16_factor<J + 1, FULL>(row, li, i, lim, bad);
     }
 }
 
@@ -772,10 +800,19 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
 #pragma unroll
         for (int c = 0; c < 16; c++) row[c] = A[(k0 + i) * LDA + k0 + c];   // the upper part (never written:
         // any bits) only ever meets lane i's own columns > i, which no broadcast reads
+#ifdef LBA_DIAG_FULL   // tried: a second instantiation for the full tiles made the kernel 5 us slower
+        const bool full = n - k0 >= 16;   // wave-uniform
+#pragma unroll
+        for (int r = 0; r < 16; r++) li[r] = full && r == i ? 1.0 : 0.0;
+        bool bad = false;
+        if (full) chol16_factor<0, true>(row, li, i, 16, bad);
+        else chol16_factor<0, false>(row, li, i, n - k0, bad);
+#else
 #pragma unroll
         for (int r = 0; r < 16; r++) li[r] = 0.0;
         bool bad = false;
-        chol16_factor<0>(row, li, i, n - k0, bad);
+        chol16_factor<0, false>(row, li, i, n - k0, bad);
+#endif
         // every 16-lane row computed the same tile: all lanes store (same values), so the
         // compiler cannot sink the li chain into a lane < 16 branch and keep every broadcast
         // live until there
@@ -1012,13 +1049,19 @@ __global__ void lba_set_ok(Graph g) {
 
 // landmark back substitution x_l = Dinv (b_l - Hpl^T x_p) fused with the update
 // T <- exp(x_p) T (SE3Quat::exp, left-multiplied), X <- X + x_l into the trial buffers and the
-// computeScale pieces x (lambda x + b) of the thread's own entries, block sums -> part[]
-__global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
+// computeScale pieces x (lambda x + b) of the thread's own entries, block sums -> part[].
+// Blocks [0, nbp): one thread per free pose. Blocks [nbp, ..): kUL lanes per landmark, lane r
+// forms the Hpl^T x_p terms of records r, r + kUL, ... of the landmark's contiguous run, and the
+// group's lane 0 adds them in record order (through LDS, the group is inside one wavefront)
+constexpr int kUL = 8;
+__global__ __launch_bounds__(256) void lba_update(Graph g, double *part, int nbp) {
+    const bool pblk = (int)blockIdx.x < nbp;
     const int t = blockIdx.x * 256 + threadIdx.x;
-    // the landmark's edge range goes out with the LM-state loads (no dependence on them)
-    const int lt = t - g.P;
-    const bool isp = lt >= 0 && lt < g.Lm;
-    const int i0p = isp ? g.pt_start[lt] : 0, i1p = isp ? g.pt_start[lt + 1] : 0;
+    const int l = pblk ? -1 : (t - nbp * 256) / kUL, r = threadIdx.x & (kUL - 1);
+    const bool isl = l >= 0 && l < g.Lm;
+    // the landmark's record range and this lane's first index entry go out with the LM-state load
+    const int i0 = isl ? g.pt_start[l] : 0, i1 = isl ? g.pt_start[l + 1] : 0;
+    int ph = i0 + r < i1 ? g.lpos_ph[i0 + r] : -1;
     const LMState lm = *g.lm;
     if (lm.done) return;
     const double lambda = g.scalars[5];
@@ -1028,44 +1071,66 @@ __global__ __launch_bounds__(256) void lba_update(Graph g, double *part) {
     const double *Xc = cur ? g.X2 : g.X;
     double *Xt = cur ? g.X : g.X2;
     double sc = 0;
-    if (t < g.P) {
-        const int v = g.hpose[t];
-        const double *xp = g.x + 6 * t;
-        Tt[v] = pose_oplus(Tc[v], xp);
-        for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + g.bp[6 * t + k]);
-    } else if (t < g.P + g.Lm) {
-        const int l = t - g.P, v = g.hpoint[l];
-        double c[3] = {g.bl[3 * l], g.bl[3 * l + 1], g.bl[3 * l + 2]};
-        const int i0 = i0p, i1 = i1p;
+    if (pblk) {
+        if (t < g.P) {
+            const int v = g.hpose[t];
+            const double *xp = g.x + 6 * t;
+            Tt[v] = pose_oplus(Tc[v], xp);
+            for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + g.bp[6 * t + k]);
+        }
+    } else {
+        __shared__ double vsh[256][3];
+        __shared__ int vok[256];
+        double c[3] = {0, 0, 0};
+        if (isl && r == 0) { c[0] = g.bl[3 * l]; c[1] = g.bl[3 * l + 1]; c[2] = g.bl[3 * l + 2]; }
         const double *hpL = g.hpl[cur];
-        for (int i = i0; i < i1; i += 4) {   // 4 records (landmark-major, contiguous) in flight, applied in order
-            int ph[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) ph[u] = i + u < i1 ? g.lpos_ph[i + u] : -1;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (ph[u] < 0) continue;
-                const double *B = hpL + 18LL * (i + u);
-                const double *xp = g.x + 6 * ph[u];
+        for (int base = i0; base < i1; base += kUL) {   // the group's lanes run the same trips
+            const int i = base + r;
+            if (base != i0) ph = i < i1 ? g.lpos_ph[i] : -1;
+            double v[3] = {0, 0, 0};
+            if (ph >= 0) {
+                const double *B = hpL + 18LL * i;
+                const double *xp = g.x + 6 * ph;
                 for (int cc = 0; cc < 3; cc++) {
-                    double v = 0;
-                    for (int a = 0; a < 6; a++) v += B[3 * a + cc] * (-xp[a]);
-                    c[cc] += v;
+                    double a = 0;
+                    for (int k = 0; k < 6; k++) a += B[3 * k + cc] * (-xp[k]);
+                    v[cc] = a;
                 }
             }
+            vsh[threadIdx.x][0] = v[0]; vsh[threadIdx.x][1] = v[1]; vsh[threadIdx.x][2] = v[2];
+            vok[threadIdx.x] = ph >= 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (r == 0)
+                for (int k = 0; k < kUL; k++)
+                    if (vok[threadIdx.x + k])
+                        for (int cc = 0; cc < 3; cc++) c[cc] += vsh[threadIdx.x + k][cc];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        const double *Di = g.Dinv + 9 * l;
-        double *xl = g.x + 6 * g.P + 3 * l;
-        for (int a = 0; a < 3; a++) {
-            const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
-            xl[a] = xa;
-            Xt[3 * v + a] = Xc[3 * v + a] + xa;
-            sc += xa * (lambda * xa + g.bl[3 * l + a]);
+        if (isl && r == 0) {
+            const int v = g.hpoint[l];
+            const double *Di = g.Dinv + 9 * l;
+            double *xl = g.x + 6 * g.P + 3 * l;
+            for (int a = 0; a < 3; a++) {
+                const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
+                xl[a] = xa;
+                Xt[3 * v + a] = Xc[3 * v + a] + xa;
+                sc += xa * (lambda * xa + g.bl[3 * l + a]);
+            }
         }
     }
     block_sum_to(sc, part + blockIdx.x);
 }
 __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthreads);
+#ifndef LBA_SEP_DECIDE
+#define LBA_SEP_DECIDE 1   // 1: the LM decision as its own one-block launch after lba_errors
+#endif
+#ifndef LBA_FENCE_W0
+#define LBA_FENCE_W0 0     // 1: only wave 0 of each lba_errors block releases (its partial)
+#endif
 
 // Trial chi2 of the active edges (block sums -> part[]) fused with the LM decision: the last
 // block to arrive (agent-scope release by every wave, one counter; the arriving block acquires,
@@ -1074,7 +1139,8 @@ __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthrea
 // needs is the trial chi2 itself): an accepted trial swaps the sets with the estimates, so the
 // next iteration starts at its reductions without a lba_linearize launch.
 __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part, int nbu, int nbe, int np, int nq) {
-    const int s = blockIdx.x * 256 + threadIdx.x;
+    int s, role;
+    lin_thread(s, role);
     const bool in = s < g.nact;
     const uint8_t on = in ? g.on[s] : 0;
     EdgeDev e{};
@@ -1083,10 +1149,16 @@ __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part, int nbu
     const bool done = g.lm->done, cur = g.lm->cur;
     if (done) return;
     double r0 = 0;
-    if (in) r0 = linearize_slot(g, e, on, s, lpos, ppos, cur ? g.T : g.T2, cur ? g.X : g.X2, !cur);
+    if (in) r0 = linearize_slot(g, e, on, s, lpos, ppos, cur ? g.T : g.T2, cur ? g.X : g.X2, !cur, role);
     const double bsum = block_sum_to(r0, part + blockIdx.x);
     if (threadIdx.x == 0) g.partial[chi_off(!cur) + blockIdx.x] = bsum;
+#if LBA_SEP_DECIDE
+    return;   // lba_decide follows
+#endif
     __shared__ int last;
+#if LBA_FENCE_W0
+    if (threadIdx.x < 64)   // wave 0 wrote the block's partial: the only store the deciding block reads
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this wave's stores (err, part) reach L2 / memory
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1112,17 +1184,26 @@ __global__ void lba_lm_init(Graph g, int iterations) {
 }
 
 // End of one LM trial (optimization_algorithm_levenberg.cpp:96-164 + the ORB-SLAM2 stop rule
-// :155-161): thread 0 sums the update's computeScale block sums and the trial chi2 block sums
-// in block order, decides, and advances the state; an accepted trial becomes the current
-// estimate (copy T2 -> T, X2 -> X by the whole workgroup).
+// :155-161): wave 0 sums the update's computeScale block sums and the trial chi2 block sums,
+// thread 0 decides and advances the state; an accepted trial becomes the current estimate by
+// swapping the estimate buffers (LMState::cur).
 __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthreads) {
-    // the block partials come into LDS with one load per thread (a dependent chain of global
-    // loads on thread 0 cost ~10 us); thread 0 then sums them in block order as before
-    __shared__ double part_s[1024];
-    const int npart = nbu + nbe;
-    const bool staged = npart <= 1024;
-    if (staged)
-        for (int b = threadIdx.x; b < npart; b += nthreads) part_s[b] = g.scalars[8 + b];
+    // wave 0 sums the block partials in a fixed order (lane k: blocks k, k + 64, ... in order, then
+    // an xor butterfly) -- a serial sum on thread 0 was ~3 us on the trial's critical path
+    __shared__ double sums_s[2];
+    if (threadIdx.x < 64) {
+        const int k = threadIdx.x;
+        const double *pp = g.scalars + 8;
+        double a = 0, b = 0;
+        for (int i = k; i < nbu; i += 64) a += pp[i];
+        for (int i = k; i < nbe; i += 64) b += pp[nbu + i];
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) {
+            a += __shfl_xor(a, m);
+            b += __shfl_xor(b, m);
+        }
+        if (k == 0) { sums_s[0] = a; sums_s[1] = b; }
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         LMState s = *g.lm;
@@ -1131,10 +1212,7 @@ __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthrea
             s.currentChi = s.iniChi = sc[0];
             if (s.it == 0) s.lambda = sc[5];   // tau * maxDiagonal, formed by lba_prep_slots
         }
-        const double *pp = staged ? part_s : sc + 8;
-        double sc_sum = 0, chi_sum = 0;
-        for (int b = 0; b < nbu; b++) sc_sum += pp[b];
-        for (int b = 0; b < nbe; b++) chi_sum += pp[nbu + b];
+        const double sc_sum = sums_s[0], chi_sum = sums_s[1];
         const double tempChi = sc[4] != 0 ? chi_sum : DBL_MAX;
         double rho = s.currentChi - tempChi;
         const double scale = sc_sum + 1e-3;
@@ -1181,9 +1259,9 @@ __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthrea
 // in block order, decides, and advances the state; an accepted trial becomes the current
 // estimate by swapping the roles of the two estimate buffers (LMState::cur). Standalone form (unused by
 // lba_optimize, which runs the decision in lba_errors' last block).
-__global__ __launch_bounds__(1024) void lba_decide(Graph g, int nbu, int nbe, int np, int nq) {
+__global__ __launch_bounds__(64) void lba_decide(Graph g, int nbu, int nbe, int np, int nq) {
     if (g.lm->done) return;
-    lm_decide(g, nbu, nbe, np, nq, 1024);
+    lm_decide(g, nbu, nbe, np, nq, 64);
 }
 
 // the EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ records of Optimizer.cc:750-848 from the
@@ -1532,15 +1610,17 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
     auto term = [&]() { return stop && *stop; };
     if (A.P + A.Lm == 0) return -1;
     if (A.P > kMaxPoses) return -2;
-    if (nblk((int)A.act.size()) > kRedBlocks || (A.Lm + kRPL - 1) / kRPL > kRedBlocks) return -2;   // partial regions
+    if (((int)A.act.size() + kLinEdges - 1) / kLinEdges > kRedBlocks || (A.Lm + kRPL - 1) / kRPL > kRedBlocks)
+        return -2;   // partial regions
     const int nact = (int)A.act.size();
     const int n6 = 6 * A.P;
-    const int nbu = nblk(A.P + A.Lm), nbe = nblk(nact);
+    const int nbp = nblk(A.P), nbu = nbp + std::max(1, (A.Lm * kUL + 255) / 256);   // lba_update blocks
+    const int nbe = std::max(1, (nact + kLinEdges - 1) / kLinEdges);   // linearize / errors blocks
     auto slot = [&](bool first) {
         int ph;
         if (first) {   // later iterations start from lba_errors' linearisation of the accepted trial
             ph = lprof_begin(e);
-            lba_linearize<<<nblk(nact), 256, 0, s>>>(g);
+            lba_linearize<<<nbe, 256, 0, s>>>(g);
             lprof_end(e, ph, "lba_linearize");
         }
         ph = lprof_begin(e);
@@ -1548,7 +1628,7 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
         if (A.P > 0) lba_reduce_poses<<<A.P, 1024, 0, s>>>(g);
         lprof_end(e, ph, "lba_reduce");
         ph = lprof_begin(e);
-        lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nblk(nact), std::max(1, (A.Lm + kRPL - 1) / kRPL), A.P);
+        lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nbe, std::max(1, (A.Lm + kRPL - 1) / kRPL), A.P);
         lprof_end(e, ph, "lba_prep_slots");
         if (A.P > 0) {
             ph = lprof_begin(e);
@@ -1579,10 +1659,11 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
         }
         // scalars[8..): the update's computeScale block sums, then the trial chi2 block sums
         ph = lprof_begin(e);
-        lba_update<<<nbu, 256, 0, s>>>(g, g.scalars + 8);
+        lba_update<<<nbu, 256, 0, s>>>(g, g.scalars + 8, nbp);
         lprof_end(e, ph, "lba_update");
         ph = lprof_begin(e);
         lba_errors<<<nbe, 256, 0, s>>>(g, g.scalars + 8 + nbu, nbu, nbe, np, nq);   // + the LM decision
+        if (LBA_SEP_DECIDE) lba_decide<<<1, 64, 0, s>>>(g, nbu, nbe, np, nq);
         lprof_end(e, ph, "lba_errors_decide");
     };
     lba_lm_init<<<1, 1, 0, s>>>(g, iterations);
