@@ -101,6 +101,7 @@ struct Graph {
     const int *slot_pt, *slot_ph;    // per active slot: hessian point / pose index (-1 fixed)
     const int *slot_lpos;            // per active slot: its position in pt_items
     const int *lpos_ph;              // per pt_items position: the slot's hessian pose index (-1 fixed)
+    const int *lpos_ppos;            // per pt_items position: the slot's ps_items position (-1 fixed)
     // system; the per-slot linearisation is kept per estimate buffer (index = LMState::cur of the
     // estimate it was formed at): lba_errors linearises the trial, and accepting it swaps both
     double *conl[2];       // [pt_items][9]: Hll upper (6) bl (3), landmark-major (point CSR order)
@@ -317,17 +318,80 @@ __global__ __launch_bounds__(256) void lba_linearize(Graph g) {
     block_sum_to(rchi, g.partial + chi_off(lm.cur) + blockIdx.x);
 }
 
+// ---- Schur: per landmark Dinv, L = chol(Dinv), Y block and w
+__device__ inline void inv3(const double m[9], double o[9]) {
+    const double c00 = m[4] * m[8] - m[5] * m[7];
+    const double c10 = m[5] * m[6] - m[3] * m[8];
+    const double c20 = m[3] * m[7] - m[4] * m[6];
+    const double det = m[0] * c00 + m[1] * c10 + m[2] * c20;
+    const double id = 1.0 / det;
+    o[0] = c00 * id; o[1] = (m[2] * m[7] - m[1] * m[8]) * id; o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+    o[3] = c10 * id; o[4] = (m[0] * m[8] - m[2] * m[6]) * id; o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    o[6] = c20 * id; o[7] = (m[1] * m[6] - m[0] * m[7]) * id; o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+// (Hll + lambda I)^-1 (Eigen cofactor inverse) and L = chol(Dinv) of one landmark
+__device__ inline void point_factor_of(const double H[9], double lambda, double Di[9], double L[6]) {
+    double D[9];
+    for (int k = 0; k < 9; k++) D[k] = H[k];
+    D[0] += lambda; D[4] += lambda; D[8] += lambda;
+    inv3(D, Di);
+    // Dinv = L L^T (symmetrised)
+    const double a00 = Di[0], a10 = 0.5 * (Di[3] + Di[1]), a11 = Di[4];
+    const double a20 = 0.5 * (Di[6] + Di[2]), a21 = 0.5 * (Di[7] + Di[5]), a22 = Di[8];
+    L[0] = sqrt(a00); L[1] = a10 / L[0]; L[2] = a20 / L[0];
+    L[3] = sqrt(a11 - L[1] * L[1]); L[4] = (a21 - L[2] * L[1]) / L[3];
+    L[5] = sqrt(a22 - L[2] * L[2] - L[4] * L[4]);
+}
+__device__ inline void point_factor(const Graph &g, int l, double lambda, double Di[9], double L[6]) {
+    double H[9];
+    for (int k = 0; k < 9; k++) H[k] = g.Hll[9 * l + k];
+    point_factor_of(H, lambda, Di, L);
+}
+
+// The 6x3 Y block (Y = Hpl L: the pose's rows, the point's columns of Y^T) of one slot and its
+// b_schur piece Y w (w = L^T b_l), from the slot's Hpl record B
+__device__ __forceinline__ void slot_y(const Graph &g, int l, int ph, int ppos, const double *B, const double L[6],
+                                       const double *bl) {
+    const long long W = g.NPW;
+    double *y = g.Y + 3LL * l * W + 6 * ph;   // Y^T rows 3l..3l+2, columns 6ph..6ph+5
+    const double w0 = L[0] * bl[0] + L[1] * bl[1] + L[2] * bl[2], w1 = L[3] * bl[1] + L[4] * bl[2], w2 = L[5] * bl[2];
+    double *yw = g.ywp + 6LL * ppos;
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+        const double b0 = B[3 * r], b1 = B[3 * r + 1], b2 = B[3 * r + 2];
+        const double y0 = b0 * L[0] + b1 * L[1] + b2 * L[2], y1 = b1 * L[3] + b2 * L[4], y2 = b2 * L[5];
+        y[r] = y0;
+        y[W + r] = y1;
+        y[2 * W + r] = y2;
+        yw[r] = y0 * w0 + y1 * w1 + y2 * w2;
+    }
+}
+
 // Hll (3x3), b_l: one 16-lane group per landmark, lane k < 9 sums component k (Hll upper 6,
 // bl 3) of the landmark's contiguous run of landmark-major records (conl) in CSR order, 8 records
 // in flight; the |diagonal| maximum of the block's 16 landmarks -> partial[kRedBlocks + blockIdx]
 constexpr int kRPL = 16;   // landmarks per lba_reduce_points workgroup
-__device__ __forceinline__ void reduce_points_body(Graph &g, int set, double *sh) {
+#ifndef LBA_FUSED_PREP
+#define LBA_FUSED_PREP 1   // 1: with lambda known (a new iteration after the first), the landmark half
+                           // of the Schur step runs here and lba_prep_slots returns at once
+#endif
+// fused (lambda = the LM state's): after the sums, the group's lanes gather the landmark's 9
+// values through LDS, each factors (Hll + lambda I)^-1 = L L^T (point_factor_of: the bits
+// lba_prep_slots forms) and lane r writes the Y blocks of records r, r + 16, ...; lane 0 writes
+// Dinv and w. Block 0 also does lba_prep_slots' mode-1 work (chi2 sum -> scalars[0], lambda ->
+// scalars[5]).
+__device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused, double lambda, int n0, double *sh) {
     const int l = blockIdx.x * kRPL + (threadIdx.x >> 4), k = threadIdx.x & 15;
-    double dmax = 0;
+    __shared__ double hv_s[256];
+    double dmax = 0, v = 0;
+    int i0 = 0, i1 = 0;
+    if (l < g.Lm) {
+        i0 = g.pt_start[l];
+        i1 = g.pt_start[l + 1];
+    }
     if (l < g.Lm && k < 9) {
-        const int i0 = g.pt_start[l], i1 = g.pt_start[l + 1];
         const double *cl = g.conl[set] + k;
-        double v = 0;
         for (int i = i0; i < i1; i += 8) {
             double r[8];
 #pragma unroll
@@ -348,6 +412,7 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, double *sh
         }
         if (k == 0 || k == 3 || k == 5) dmax = fabs(v);
     }
+    hv_s[threadIdx.x] = v;
     sh[threadIdx.x] = dmax;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
@@ -355,12 +420,39 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, double *sh
         __syncthreads();
     }
     if (threadIdx.x == 0) g.partial[kRedBlocks + blockIdx.x] = sh[0];
+    if (!fused) return;   // uniform
+    if (blockIdx.x == 0) {   // lba_prep_slots mode 1: the same tree over the chi2 block sums
+        __shared__ double sa[256];
+        double a = 0;
+        const double *chi = g.partial + chi_off(set);
+        for (int i = threadIdx.x; i < n0; i += 256) a += chi[i];
+        sa[threadIdx.x] = a;
+        __syncthreads();
+        for (int s = 128; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) sa[threadIdx.x] += sa[threadIdx.x + s];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) { g.scalars[0] = sa[0]; g.scalars[5] = lambda; }
+    }
+    if (l >= g.Lm) return;
+    const double *hv = hv_s + (threadIdx.x & ~15);
+    const double Hm[9] = {hv[0], hv[1], hv[2], hv[1], hv[3], hv[4], hv[2], hv[4], hv[5]}, bl[3] = {hv[6], hv[7], hv[8]};
+    double Di[9], L[6];
+    point_factor_of(Hm, lambda, Di, L);
+    if (k == 0) {
+        const long long W = g.NPW, c0 = 3LL * l;
+        for (int q = 0; q < 9; q++) g.Dinv[9 * l + q] = Di[q];
+        g.w[c0 * W] = L[0] * bl[0] + L[1] * bl[1] + L[2] * bl[2];
+        g.w[(c0 + 1) * W] = L[3] * bl[1] + L[4] * bl[2];
+        g.w[(c0 + 2) * W] = L[5] * bl[2];
+    }
+    for (int i = i0 + k; i < i1; i += 16) {
+        const int ph = g.lpos_ph[i];
+        if (ph < 0) continue;
+        slot_y(g, l, ph, g.lpos_ppos[i], g.hpl[set] + 18LL * i, L, bl);
+    }
 }
 
-// Hpp (6x6), b_p of one free pose on a 1024-thread workgroup: 32 slot groups x 32 lanes, lane
-// k < 27 of a group accumulates component k (Hpp upper 21 + b_p 6) of every 32nd slot of the
-// pose's contiguous run of pose-major records (conp: coalesced 216-byte record reads, no index
-// loads, LBA_RP records per lane in flight); the 32 group partials are summed in LDS in fixed order
 #ifndef LBA_RP
 #define LBA_RP 32   // records per lane per batch in reduce_poses_body
 #endif
@@ -411,43 +503,17 @@ __device__ __forceinline__ void reduce_poses_body(Graph &g, int i, int set, doub
 // the landmark reductions on 256-thread workgroups (one landmark per thread: a merged launch with
 // the pose reductions on 1024-thread workgroups spread the landmarks over 4x fewer CUs and took
 // 22 us against 8 + 10), the pose reductions one 1024-thread workgroup per free pose
-__global__ __launch_bounds__(256) void lba_reduce_points(Graph g) {
+__global__ __launch_bounds__(256) void lba_reduce_points(Graph g, int n0) {
     const LMState lm = *g.lm;
     if (lm.done || !lm.newiter) return;
     __shared__ double shp[256];
-    reduce_points_body(g, lm.cur, shp);
+    reduce_points_body(g, lm.cur, LBA_FUSED_PREP && lm.it > 0, lm.lambda, n0, shp);
 }
 __global__ __launch_bounds__(1024) void lba_reduce_poses(Graph g) {
     const LMState lm = *g.lm;
     if (lm.done || !lm.newiter) return;
     __shared__ double shq[32][33];
     reduce_poses_body(g, blockIdx.x, lm.cur, shq);
-}
-
-// ---- Schur: per landmark Dinv, L = chol(Dinv), Y block and w
-__device__ inline void inv3(const double m[9], double o[9]) {
-    const double c00 = m[4] * m[8] - m[5] * m[7];
-    const double c10 = m[5] * m[6] - m[3] * m[8];
-    const double c20 = m[3] * m[7] - m[4] * m[6];
-    const double det = m[0] * c00 + m[1] * c10 + m[2] * c20;
-    const double id = 1.0 / det;
-    o[0] = c00 * id; o[1] = (m[2] * m[7] - m[1] * m[8]) * id; o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
-    o[3] = c10 * id; o[4] = (m[0] * m[8] - m[2] * m[6]) * id; o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
-    o[6] = c20 * id; o[7] = (m[1] * m[6] - m[0] * m[7]) * id; o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
-}
-
-// (Hll + lambda I)^-1 (Eigen cofactor inverse) and L = chol(Dinv) of one landmark
-__device__ inline void point_factor(const Graph &g, int l, double lambda, double Di[9], double L[6]) {
-    double D[9];
-    for (int k = 0; k < 9; k++) D[k] = g.Hll[9 * l + k];
-    D[0] += lambda; D[4] += lambda; D[8] += lambda;
-    inv3(D, Di);
-    // Dinv = L L^T (symmetrised)
-    const double a00 = Di[0], a10 = 0.5 * (Di[3] + Di[1]), a11 = Di[4];
-    const double a20 = 0.5 * (Di[6] + Di[2]), a21 = 0.5 * (Di[7] + Di[5]), a22 = Di[8];
-    L[0] = sqrt(a00); L[1] = a10 / L[0]; L[2] = a20 / L[0];
-    L[3] = sqrt(a11 - L[1] * L[1]); L[4] = (a21 - L[2] * L[1]) / L[3];
-    L[5] = sqrt(a22 - L[2] * L[2] - L[4] * L[4]);
 }
 
 // First kernel of an LM trial (setLambda + the landmark half of the Schur complement).
@@ -466,7 +532,7 @@ __global__ __launch_bounds__(256) void lba_prep_slots(Graph g, int n0, int n1, i
     const int ph = ist ? g.slot_ph[t] : -1, l_t = ist ? g.slot_pt[t] : 0, lpos = ist ? g.slot_lpos[t] : 0,
               ppos = ist ? g.slot_ppos[t] : 0;
     const LMState lm = *g.lm;
-    if (lm.done) return;
+    if (lm.done || (LBA_FUSED_PREP && lm.newiter && lm.it > 0)) return;   // lba_reduce_points did it
     const int mode = lm.newiter ? (lm.it == 0 ? 2 : 1) : 0;
     double lambda = lm.lambda;
     if (mode == 2 || (mode == 1 && blockIdx.x == 0)) {   // uniform per block
@@ -496,21 +562,8 @@ __global__ __launch_bounds__(256) void lba_prep_slots(Graph g, int n0, int n1, i
         if (ph < 0) return;
         const int l = l_t;
         point_factor(g, l, lambda, Di, L);
-        const double *B = g.hpl[lm.cur] + 18LL * lpos;
-        double *y = g.Y + 3LL * l * W + 6 * ph;   // Y^T rows 3l..3l+2, columns 6ph..6ph+5
         // w_l = L^T b_l exactly as the landmark threads form it, for this block's share of Y w
-        const double *bl = g.bl + 3 * l;
-        const double w0 = L[0] * bl[0] + L[1] * bl[1] + L[2] * bl[2], w1 = L[3] * bl[1] + L[4] * bl[2], w2 = L[5] * bl[2];
-        double *yw = g.ywp + 6LL * ppos;
-#pragma unroll
-        for (int r = 0; r < 6; r++) {
-            const double b0 = B[3 * r], b1 = B[3 * r + 1], b2 = B[3 * r + 2];
-            const double y0 = b0 * L[0] + b1 * L[1] + b2 * L[2], y1 = b1 * L[3] + b2 * L[4], y2 = b2 * L[5];
-            y[r] = y0;
-            y[W + r] = y1;
-            y[2 * W + r] = y2;
-            yw[r] = y0 * w0 + y1 * w1 + y2 * w2;
-        }
+        slot_y(g, l, ph, ppos, g.hpl[lm.cur] + 18LL * lpos, L, g.bl + 3 * l);
     } else if (t < g.nact + g.Lm) {
         const int l = t - g.nact;
         point_factor(g, l, lambda, Di, L);
@@ -672,18 +725,32 @@ template <int C> __device__ __forceinline__ double row_bcast(double v) {
 #define LBA_DPP_FMAC 1   // 1: the column updates as v_fmac_f64 with a DPP64 row_newbcast source
 #endif
 // acc += (value of lane C of each 16-lane row of src) * m: the broadcast folded into the FMA
-// (v_fmac_f64_dpp, DPP64 row_newbcast). NOP: two wait states first for a DPP read of a VGPR a
-// VALU has just written (the compiler does not track hazards across inline asm)
+// (v_fmac_f64_dpp, DPP64 row_newbcast). The compiler does not track hazards across inline asm:
+// every VALU write of a VGPR that a DPP then reads passes a dpp_gate (two wait states, and the
+// readers depend on it), so the asm itself can stay non-volatile and the scheduler may overlap a
+// pivot's column updates with the next pivot's chain (LBA_DPP_VOLATILE=1: the old fixed order)
+#ifndef LBA_DPP_VOLATILE
+#define LBA_DPP_VOLATILE 0
+#endif
+__device__ __forceinline__ void dpp_gate(double &v) { asm volatile("s_nop 1" : "+v"(v)); }
 template <int C, bool NOP> __device__ __forceinline__ void fmac_bcast(double &acc, double src, double m) {
+#if LBA_DPP_VOLATILE
     if constexpr (NOP)
         asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
                      : "+v"(acc) : "v"(src), "v"(m), "i"(C));
     else
         asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(src), "v"(m), "i"(C));
+#else
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(src), "v"(m), "i"(C));
+#endif
 }
 template <int C> __device__ __forceinline__ double bcast64(double src) {
     double d;
+#if LBA_DPP_VOLATILE
     asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(d) : "v"(src), "i"(C));
+#else
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(d) : "v"(src), "i"(C));
+#endif
     return d;
 }
 
@@ -712,6 +779,9 @@ template <int J, bool FULL> __device__ __forceinline__ void chol16_factor(double
                                                                           bool &bad) {
     if constexpr (J < 16) {
 #if LBA_DPP_FMAC
+#if !LBA_DPP_VOLATILE
+        dpp_gate(row[J]);   // row[J] was last written by a VALU (the pivot J - 1 update, or the load)
+#endif
         double d = bcast64<J>(row[J]);
 #else
         double d = row_bcast<J>(row[J]);
@@ -731,6 +801,9 @@ template <int J, bool FULL> __device__ __forceinline__ void chol16_factor(double
             row[J] = i == J ? d * y : row[J] * y;
             li[J] = (i == J ? 1.0 + li[J] : li[J]) * y;   // li[J] held -sum L[J][k] li[k]
         }
+#if LBA_DPP_FMAC && !LBA_DPP_VOLATILE
+        dpp_gate(row[J]);   // the scaled row[J] is the DPP source of every column update
+#endif
         chol16_update<J, J + 1>(row, li, -row[J], -li[J]);
         chol16_factor<J + 1, FULL>(row, li, i, lim, bad);
     }
@@ -760,46 +833,28 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
 #define LBA_T(acc) do {} while (0)
 #endif
     const long long NP = g.NP;
-    // load: lower triangle of Hs, bs as row n, identity padding; 128 rows per pass (128 / kCW
-    // per wave, lanes along the row; N2 <= kSmallNP = 128), all loads of a pass in flight
-    constexpr int RU = 128 / kCW;
-    for (int rb = 0; rb < N2; rb += 128) {
-        double v[RU][2];
-#pragma unroll
-        for (int u = 0; u < RU; u++)
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int r = rb + wv + kCW * u, c = lane + 64 * h;
-                v[u][h] = 0.0;
-                if (r < N2 && c <= r) {
-                    if (r < n) v[u][h] = g.Hs[r * NP + c];
-                    else if (r == n) v[u][h] = c < n ? g.bs[c] : 0.0;
-                    else v[u][h] = r == c ? 1.0 : 0.0;
-                }
-            }
-#pragma unroll
-        for (int u = 0; u < RU; u++)
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int r = rb + wv + kCW * u, c = lane + 64 * h;
-                if (r < N2 && c <= r) A[r * LDA + c] = v[u][h];
-            }
-    }
+    // element (r, c <= r) of the system [Hs bs; bs^T 0] padded with identity rows
+    auto sys = [&](int r, int c) -> double {
+        if (r < n) return g.Hs[r * NP + c];
+        if (r == n) return c < n ? g.bs[c] : 0.0;
+        return r == c ? 1.0 : 0.0;
+    };
     if (tid == 0) fail = 0;
-    __syncthreads();
-#ifdef LBA_PROFILE
-    const long long t_load = clock64() - t0;
-    ta = clock64();
-#endif
-    // wave 0: factor + invert diagonal tile K (lane i of each 16-lane row = row i)
+    // wave 0: factor + invert diagonal tile K (lane i of each 16-lane row = row i); tile 0 comes
+    // straight from global memory while waves 1.. load the rest of the matrix into LDS
     auto diag = [&](int K) {
         if (LBA_DIAG_PRIO) __builtin_amdgcn_s_setprio(LBA_DIAG_PRIO);
         const int k0 = 16 * K, i = lane & 15;
         double *LK = Linv + K * 16 * 17;
         double row[16], li[16];   // li: column i of L_kk^-1
+        if (K == 0) {
 #pragma unroll
-        for (int c = 0; c < 16; c++) row[c] = A[(k0 + i) * LDA + k0 + c];   // the upper part (never written:
-        // any bits) only ever meets lane i's own columns > i, which no broadcast reads
+            for (int c = 0; c < 16; c++) row[c] = c <= i ? sys(i, c) : 0.0;
+        } else {
+#pragma unroll
+            for (int c = 0; c < 16; c++) row[c] = A[(k0 + i) * LDA + k0 + c];   // the upper part (never written:
+            // any bits) only ever meets lane i's own columns > i, which no broadcast reads
+        }
 #ifdef LBA_DIAG_FULL   // tried: a second instantiation for the full tiles made the kernel 5 us slower
         const bool full = n - k0 >= 16;   // wave-uniform
 #pragma unroll
@@ -823,8 +878,31 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
         if (lane == 0 && bad) fail = 1;
         if (LBA_DIAG_PRIO) __builtin_amdgcn_s_setprio(0);
     };
-    if (wv == 0) diag(0);
+    if (wv == 0) {
+        diag(0);
+    } else {   // waves 1..: the lower triangle of rows 16.. (N2 <= kSmallNP = 128), all loads in flight
+        constexpr int RU = (128 - 16 + kCW - 2) / (kCW - 1);
+        double v[RU][2];
+#pragma unroll
+        for (int u = 0; u < RU; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int r = 16 + wv - 1 + (kCW - 1) * u, c = lane + 64 * h;
+                v[u][h] = r < N2 && c <= r ? sys(r, c) : 0.0;
+            }
+#pragma unroll
+        for (int u = 0; u < RU; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int r = 16 + wv - 1 + (kCW - 1) * u, c = lane + 64 * h;
+                if (r < N2 && c <= r) A[r * LDA + c] = v[u][h];
+            }
+    }
     __syncthreads();
+#ifdef LBA_PROFILE
+    const long long t_load = 0;   // the load overlaps diag(0): both in "diag"
+    ta = t0;
+#endif
     LBA_T(t_diag);
     // look-ahead: diagonal tile K + 1 is factored by wave 0 right after its own trailing
     // update, while waves 1-7 update the rest of the trailing matrix; 2 barriers per panel
@@ -883,21 +961,31 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
     // the last block then contribute exactly 0 and every block runs fixed 16-term sums
     for (int j = tid; j < N2; j += kCT) yv[j] = j < n ? A[n * LDA + j] : 0.0;
     __syncthreads();
+    // Each block step as 4-term partial dot products reduced across lanes (a 16-term dependent
+    // FMA chain per step before): x_K by wave 0, lane (column c, quarter p) over rows 4p..4p+3;
+    // the rows above by 4 lanes each
+    static_assert(kCT / 4 >= kSmallNP, "one pass of row quads");
     for (int K = (n - 1) / 16; K >= 0; K--) {
         const int k0 = 16 * K;
-        if (tid < 16) {   // x_K = L_KK^-T y_K
+        if (wv == 0) {   // x_K = L_KK^-T y_K
             const double *LK = Linv + K * 16 * 17;
+            const int c = lane & 15, p4 = 4 * (lane >> 4);
             double s = 0.0;
 #pragma unroll
-            for (int r = 0; r < 16; r++) s += LK[r * 17 + tid] * yv[k0 + r];   // LK[r][c] = 0 for r < c
-            xv[k0 + tid] = s;
+            for (int r = 0; r < 4; r++) s += LK[(p4 + r) * 17 + c] * yv[k0 + p4 + r];   // LK[r][c] = 0 for r < c
+            s += __shfl_xor(s, 16);
+            s += __shfl_xor(s, 32);
+            if (lane < 16) xv[k0 + c] = s;
         }
         __syncthreads();
-        for (int j = tid; j < k0; j += kCT) {
-            double s = yv[j];
+        const int j = tid >> 2, q4 = 4 * (tid & 3);
+        if (j < k0) {   // a row's 4 lanes are a quad: all in or all out
+            double s = 0.0;
 #pragma unroll
-            for (int k = 0; k < 16; k++) s -= A[(k0 + k) * LDA + j] * xv[k0 + k];
-            yv[j] = s;
+            for (int k = 0; k < 4; k++) s += A[(k0 + q4 + k) * LDA + j] * xv[k0 + q4 + k];
+            s += __shfl_xor(s, 1);
+            s += __shfl_xor(s, 2);
+            if ((tid & 3) == 0) yv[j] -= s;
         }
         __syncthreads();
     }
@@ -1396,7 +1484,7 @@ struct HostGraph {
 struct ActiveSet {
     int P = 0, Lm = 0;
     std::vector<int> act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items, ps_start, ps_items, slot_pt, slot_ph,
-        slot_ppos, slot_lpos, lpos_ph;
+        slot_ppos, slot_lpos, lpos_ph, lpos_ppos;
     std::vector<int2> tp_ij, tp_nch;     // Schur tile pairs (build_schur_tiles)
     std::vector<int> tp_start, tp_rows;
     std::vector<int4> tp_chunk;
@@ -1546,6 +1634,7 @@ void build_active(const HostGraph &h, ActiveSet &A) {
     A.slot_ppos.assign(std::max<size_t>(1, A.act.size()), -1);
     A.slot_lpos.assign(std::max<size_t>(1, A.act.size()), 0);
     A.lpos_ph.assign(std::max<size_t>(1, A.act.size()), -1);
+    A.lpos_ppos.assign(std::max<size_t>(1, A.act.size()), -1);
     for (int s = 0; s < (int)A.act.size(); s++) {
         const int k = A.act[s];
         const int l = A.point_hidx[h.edge_point[k]];
@@ -1559,6 +1648,7 @@ void build_active(const HostGraph &h, ActiveSet &A) {
         A.slot_ppos[s] = -1;
         if (ph >= 0) {
             A.slot_ppos[s] = A.ps_start[ph] + fp[ph];
+            A.lpos_ppos[lpos] = A.slot_ppos[s];
             A.ps_items[A.ps_start[ph] + fp[ph]++] = s;
         }
     }
@@ -1624,7 +1714,7 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
             lprof_end(e, ph, "lba_linearize");
         }
         ph = lprof_begin(e);
-        lba_reduce_points<<<std::max(1, (A.Lm + kRPL - 1) / kRPL), 256, 0, s>>>(g);
+        lba_reduce_points<<<std::max(1, (A.Lm + kRPL - 1) / kRPL), 256, 0, s>>>(g, nbe);
         if (A.P > 0) lba_reduce_poses<<<A.P, 1024, 0, s>>>(g);
         lprof_end(e, ph, "lba_reduce");
         ph = lprof_begin(e);
@@ -1815,7 +1905,8 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
                      o_hpose = ub.add(A.hpose), o_hpoint = ub.add(A.hpoint), o_pt_start = ub.add(A.pt_start),
                      o_pt_items = ub.add(A.pt_items), o_ps_start = ub.add(A.ps_start), o_ps_items = ub.add(A.ps_items),
                      o_slot_pt = ub.add(A.slot_pt), o_slot_ph = ub.add(A.slot_ph);
-        const size_t o_slot_ppos = ub.add(A.slot_ppos), o_slot_lpos = ub.add(A.slot_lpos), o_lpos_ph = ub.add(A.lpos_ph);
+        const size_t o_slot_ppos = ub.add(A.slot_ppos), o_slot_lpos = ub.add(A.slot_lpos), o_lpos_ph = ub.add(A.lpos_ph),
+                     o_lpos_ppos = ub.add(A.lpos_ppos);
         const size_t o_tp_ij = ub.add(A.tp_ij), o_tp_start = ub.add(A.tp_start), o_tp_rows = ub.add(A.tp_rows),
                      o_tp_chunk = ub.add(A.tp_chunk), o_tp_nch = ub.add(A.tp_nch);
         const size_t o_E = edges ? ub.add(*edges) : 0;
@@ -1834,6 +1925,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.slot_ppos = at<int>(e->arenaB, o_slot_ppos);
         g.slot_lpos = at<int>(e->arenaB, o_slot_lpos);
         g.lpos_ph = at<int>(e->arenaB, o_lpos_ph);
+        g.lpos_ppos = at<int>(e->arenaB, o_lpos_ppos);
         g.tp_ij = at<int2>(e->arenaB, o_tp_ij);
         g.tp_start = at<int>(e->arenaB, o_tp_start);
         g.tp_rows = at<int>(e->arenaB, o_tp_rows);
