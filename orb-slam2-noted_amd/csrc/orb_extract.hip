@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <type_traits>
 
 #include "orb_device.h"
 #include "orb_engine.h"
@@ -269,8 +270,8 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 #define FB_MR (FB_TH + 2)   // score rows y0-1 .. y0+16 (tile + NMS ring)
 #define FB_NG (FB_MR * FB_LD)   // score tile dwords (a multiple of 4, <= 1024: cleared as uint4 by 256 threads)
 #define FB_CCAP (2 * FB_MR * (FB_TW + 2))   // candidate entries: both polarities of every score pixel
+                                          // (brighter from the front, darker from the back)
 #define FB_INTILE 0x8000   // candidate flag: a tile pixel (not the NMS ring)
-#define FB_BRIGHT 0x4000   // candidate flag: score the brighter polarity (else the darker)
 #define FB_POS 0x0FFF      // candidate: score-tile byte offset
 
 __device__ __forceinline__ int refl101(int i, int n) {
@@ -350,20 +351,25 @@ __device__ __forceinline__ void ring2(const uint8_t *pa, const uint8_t *pb, uint
     for (int k = 0; k < 16; k++) R[k] = (uint32_t)pa[OFF[k]] | (uint32_t)pb[OFF[k]] << 16;
     V = (uint32_t)pa[3 * FB_LW + 3] | (uint32_t)pb[3 * FB_LW + 3] << 16;
 }
-// max(0, max_arc min_k d_k) of both halves, d_k = S * ring_k + C (S = +-1: brighter / darker)
-__device__ __forceinline__ uint32_t fast_arc_score2(const uint32_t (&R)[16], uint32_t S, uint32_t C) {
-    uint32_t d[16], n3[16];
+// M of both halves, all of one polarity: brighter max(0, max_arc min_k ring_k - v) (min3 over
+// the arcs, max3 over the 16 starts), darker max(0, v - min_arc max_k ring_k) (the mirror) --
+// exact on the denormal-encoded bytes, no per-pixel difference pass
+template <bool BRIGHT>
+__device__ __forceinline__ uint32_t fast_arc_score2(const uint32_t (&R)[16], uint32_t V) {
+    auto op3 = [](uint32_t a, uint32_t b, uint32_t c) { return BRIGHT ? pk_min3h(a, b, c) : pk_max3h(a, b, c); };
+    auto red3 = [](uint32_t a, uint32_t b, uint32_t c) { return BRIGHT ? pk_max3h(a, b, c) : pk_min3h(a, b, c); };
+    uint32_t n3[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = pk_fmah(R[k], S, C);
-#pragma unroll
-    for (int k = 0; k < 16; k++) n3[k] = pk_min3h(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+    for (int k = 0; k < 16; k++) n3[k] = op3(R[k], R[(k + 1) & 15], R[(k + 2) & 15]);
     uint32_t n9[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) n9[k] = pk_min3h(n3[k], n3[(k + 3) & 15], n3[(k + 6) & 15]);
-    uint32_t A = pk_max3h(0u, n9[0], n9[1]);
+    for (int k = 0; k < 16; k++) n9[k] = op3(n3[k], n3[(k + 3) & 15], n3[(k + 6) & 15]);
+    uint32_t A = red3(n9[0], n9[1], n9[2]);
 #pragma unroll
-    for (int k = 2; k < 16; k += 2) A = pk_max3h(A, n9[k], n9[k + 1]);
-    return A;
+    for (int k = 3; k < 15; k += 2) A = red3(A, n9[k], n9[k + 1]);
+    A = red3(A, n9[15], n9[15]);
+    const uint32_t d = BRIGHT ? pk_subh(A, V) : pk_subh(V, A);
+    return pk_max3h(d, 0u, 0u);   // -0 / negative halves -> +0
 }
 
 // GaussianBlur 9x9 sigma 2 of one 128 x 16 tile as two banded integer products on
@@ -466,7 +472,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     __shared__ __align__(16) uint32_t mt[FB_NG];   // exact M bytes, (mrow, x - x0 + 4)
     __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets | FB_INTILE)
     __shared__ uint16_t hlist[FB_TW * FB_TH];   // hot tile pixels (score-tile byte offsets; each at most once)
-    __shared__ int ncand_sh, hcnt_sh;
+    __shared__ int ncand_sh, hcnt_sh;   // ncand_sh: brighter count | darker count << 16
     lat_prio<16>();
     const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
     int t = blockIdx.x, l = 0;
@@ -595,15 +601,16 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
                                                        __builtin_amdgcn_udot4(cA.x >> 7, 0x08040201u, 0u, false), false);
             const uint32_t md = __builtin_amdgcn_udot4(cB.y >> 7, 0x80402010u,
                                                        __builtin_amdgcn_udot4(cA.y >> 7, 0x08040201u, 0u, false), false);
-            const int cnt = __builtin_popcount(mb) + __builtin_popcount(md);
+            const int cnt = __builtin_popcount(mb) | __builtin_popcount(md) << 16;   // both counts, one scan
             const int inc = wave_incl_scan_dpp(cnt);
             const int tot8 = __builtin_amdgcn_readlane(inc, 63);
             if (tot8 == 0) return;   // wave-uniform
             int base = 0;
             if (lane == 0) base = atomicAdd(&ncand_sh, tot8);
             base = __builtin_amdgcn_readfirstlane(base) + inc - cnt;
-            for (uint32_t mm = mb; mm; mm &= mm - 1) clist[base++] = (uint16_t)((pos0 + __builtin_ctz(mm)) | tflag | FB_BRIGHT);
-            for (uint32_t mm = md; mm; mm &= mm - 1) clist[base++] = (uint16_t)((pos0 + __builtin_ctz(mm)) | tflag);
+            int bb = base & 0xFFFF, bd = FB_CCAP - 1 - (base >> 16);
+            for (uint32_t mm = mb; mm; mm &= mm - 1) clist[bb++] = (uint16_t)((pos0 + __builtin_ctz(mm)) | tflag);
+            for (uint32_t mm = md; mm; mm &= mm - 1) clist[bd--] = (uint16_t)((pos0 + __builtin_ctz(mm)) | tflag);
         };
         const int r = threadIdx.x >> 4, cb = (threadIdx.x & 15) * 8;   // pixels (y0 + r, x0 + cb + i)
 #ifndef FB_SKIP_PRE   // instruction-count experiments (make variant VDEFS=-DFB_SKIP_...)
@@ -618,14 +625,14 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             const int y = y0 + (lane & 15), x = lane < 16 ? x0 - 1 : x0 + FB_TW;
             const bool f = lane < 32 && y >= dy0 && y < dy1 && x >= dx0 && x < dx1;
             const unsigned long long bal = __ballot(f);
-            if (bal) {   // both polarities: entries base + 2 rank (darker), + 1 (brighter)
+            if (bal) {   // both polarities: one brighter and one darker entry per pixel
                 int base = 0;
-                if (lane == 0) base = atomicAdd(&ncand_sh, 2 * __popcll(bal));
+                if (lane == 0) base = atomicAdd(&ncand_sh, __popcll(bal) * 0x10001);
                 base = __builtin_amdgcn_readfirstlane(base);
                 const uint16_t e = (uint16_t)(((lane & 15) + 1) * FB_LW + (x - x0 + 4));
                 if (f) {
-                    clist[base + 2 * lane_rank(bal)] = e;
-                    clist[base + 2 * lane_rank(bal) + 1] = (uint16_t)(e | FB_BRIGHT);
+                    clist[(base & 0xFFFF) + lane_rank(bal)] = e;
+                    clist[FB_CCAP - 1 - ((base >> 16) + lane_rank(bal))] = e;
                 }
             }
         }
@@ -642,46 +649,51 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     }
 #endif
     __syncthreads();
-    // 3. exact M of the pooled (pixel, polarity) entries, two per lane (halves a, b): wavefront wv
-    // takes entries [128 wv, 128 wv + 128), + 512, ...; tile pixels with M > tlo go to its hot
-    // list. At most one polarity of a pixel scores above 0 (a darker 9-arc with every difference
-    // > 0 meets every brighter 9-arc in >= 2 pixels: 9 + 9 > 16), so the two entries of a pixel
-    // that passed both compass tests never both write: a score is stored only when nonzero (the
-    // score tile is zero elsewhere) and only the nonzero one can be hot.
+    // 3. exact M of the pooled (pixel, polarity) entries, two per lane (halves a, b), one polarity
+    // per 128-entry chunk (the brighter chunks, then the darker ones from the list's back):
+    // wavefront wv takes chunks wv, wv + 4, ...; tile pixels with M > tlo go to the hot list. At
+    // most one polarity of a pixel scores above 0 (a darker 9-arc with every difference > 0 meets
+    // every brighter 9-arc in >= 2 pixels: 9 + 9 > 16), so the two entries of a pixel that passed
+    // both compass tests never both write: a score is stored only when nonzero (the score tile is
+    // zero elsewhere) and only the nonzero one can be hot.
 #ifdef FB_SKIP_EXACT
-    const int tot = 0;
+    const int ncd = 0;
 #else
-    const int tot = ncand_sh;
+    const int ncd = ncand_sh;
 #endif
     {
         uint8_t *m8 = (uint8_t *)mt;
         const uint8_t *t8 = (const uint8_t *)tin;
-        auto push_hot = [&](bool hot, int pos) {   // one LDS atomic per wavefront batch
-            const unsigned long long bal = __ballot(hot);
-            if (bal == 0) return;   // wave-uniform
-            int hb = 0;
-            if (lane == 0) hb = atomicAdd(&hcnt_sh, __popcll(bal));
-            hb = __builtin_amdgcn_readfirstlane(hb);
-            if (hot) hlist[hb + (int)lane_rank(bal)] = (uint16_t)pos;
+        auto push_hot = [&](bool ha, int pa, bool hb, int pb) {   // both halves, one LDS atomic per chunk
+            const unsigned long long ba = __ballot(ha), bb = __ballot(hb);
+            if ((ba | bb) == 0) return;   // wave-uniform
+            const int na = __popcll(ba);
+            int h0 = 0;
+            if (lane == 0) h0 = atomicAdd(&hcnt_sh, na + __popcll(bb));
+            h0 = __builtin_amdgcn_readfirstlane(h0);
+            if (ha) hlist[h0 + (int)lane_rank(ba)] = (uint16_t)pa;
+            if (hb) hlist[h0 + na + (int)lane_rank(bb)] = (uint16_t)pb;
         };
         // a dummy position for idle halves: a tile pixel whose ring stays inside the staged rows
         constexpr int kIdle = 4;
-        for (int base = 128 * wv; base < tot; base += 512) {
-            const int qa = base + lane, qb = base + 64 + lane;
-            const bool xa = qa < tot, xb = qb < tot;
-            const int ea = xa ? clist[qa] : 0, eb = xb ? clist[qb] : 0;
+        const int nb = ncd & 0xFFFF, nd = ncd >> 16, chb = (nb + 127) >> 7, chd = (nd + 127) >> 7;
+        auto chunk = [&](auto bright_tag, int q0, int n) {
+            constexpr bool BR = decltype(bright_tag)::value;
+            const int qa = q0 + lane, qb = q0 + 64 + lane;
+            const bool xa = qa < n, xb = qb < n;
+            const int ea = xa ? clist[BR ? qa : FB_CCAP - 1 - qa] : 0, eb = xb ? clist[BR ? qb : FB_CCAP - 1 - qb] : 0;
             const int pa = xa ? ea & FB_POS : kIdle, pb = xb ? eb & FB_POS : kIdle;
             uint32_t R[16], V;
             ring2(t8 + pa - 3, t8 + pb - 3, R, V);
-            // S = +1 (brighter) / -1 (darker) per half, C = -S * v
-            const uint32_t S = ((ea & FB_BRIGHT) ? 0x3C00u : 0xBC00u) | ((eb & FB_BRIGHT) ? 0x3C000000u : 0xBC000000u);
-            const uint32_t C = V ^ 0x80008000u ^ (S & 0x80008000u);
-            const uint32_t A = fast_arc_score2(R, S, C);
+            const uint32_t A = fast_arc_score2<BR>(R, V);
             const int Ma = (int)(A & 0xFFFFu), Mb = (int)(A >> 16);
             if (xa && Ma > 0) m8[pa] = (uint8_t)Ma;
             if (xb && Mb > 0) m8[pb] = (uint8_t)Mb;
-            push_hot(xa && Ma > tlo && (ea & FB_INTILE), pa);
-            push_hot(xb && Mb > tlo && (eb & FB_INTILE), pb);
+            push_hot(xa && Ma > tlo && (ea & FB_INTILE), pa, xb && Mb > tlo && (eb & FB_INTILE), pb);
+        };
+        for (int c = wv; c < chb + chd; c += 4) {
+            if (c < chb) chunk(std::true_type{}, 128 * c, nb);   // wave-uniform
+            else chunk(std::false_type{}, 128 * (c - chb), nd);
         }
     }
     __syncthreads();
