@@ -1,35 +1,38 @@
 // MI355X-native Optimizer::LocalBundleAdjustment core (Optimizer.cc:900-1008) over the
 // g2o LM + Schur path it uses (BlockSolver_6_3 + OptimizationAlgorithmLevenberg), FP64.
 //
-// Device work per LM iteration (N10-N13 of SURVEY.md §2.1):
-//   lba_linearize     one thread per active edge: residual, Huber weight, analytic 2x9 /
-//                     3x9 Jacobians, per-edge quadratic-form pieces (Hpl block kept)
-//   lba_reduce_points one thread per landmark: Hll (3x3), b_l  (edges of a point are a CSR
-//                     segment -> deterministic order)
+// Device work per LM trial (N10-N13 of SURVEY.md §2.1); the per-slot linearisation is kept
+// per estimate buffer, so a new iteration starts from the one lba_errors formed for the
+// accepted trial:
+//   lba_linearize     (first slot of an optimize() only) one thread per active edge: residual,
+//                     Huber weight, analytic 2x9 / 3x9 Jacobians, the quadratic-form pieces as
+//                     landmark-major (Hll, bl, Hpl) and pose-major (Hpp, bp) records
+//   lba_reduce_points 16 lanes per landmark: Hll (3x3), b_l over the landmark's contiguous
+//                     records in CSR order; in a new iteration after the first (lambda known)
+//                     also the landmark half of the Schur step: Dinv = (Hll + lambda I)^-1,
+//                     L = chol(Dinv), w = L^T b_l and every edge's 6x3 block of Y = Hpl L
 //   lba_reduce_poses  one 1024-thread workgroup per free pose: Hpp (6x6), b_p, fixed-order sums
-// per LM trial (6 kernels for 6P <= 128):
-//   lba_prep_slots    finishes the linearisation's chi2 / maxDiagonal reductions (first lambda
-//                     on the device); one thread per active edge: its 6x3 block of Y = Hpl L
-//                     with L = chol(Dinv); one thread per landmark: Dinv = (Hll + lambda I)^-1
-//                     (Eigen cofactor inverse), w_l = L^T b_l
+//   lba_prep_slots    the landmark half of the Schur step when lba_reduce_points did not do it
+//                     (the first iteration: lambda = tau * maxDiagonal; retried trials)
 //   lba_schur_tiles   Hschur = Hpp + lambda I - Y Y^T block-sparse on FP64 matrix cores
 //                     (v_mfma_f64_16x16x4f64) over the landmark rows each upper 16 x 16 tile
-//                     pair shares, Y stored transposed, chunks of 32 MFMA steps per 4-wave
+//                     pair shares, Y stored transposed, chunks of 64 MFMA steps per 4-wave
 //                     workgroup, lba_schur_finish sums a pair's chunk tiles; b_schur = b_p - Y w
-//   lba_chol_tiled    (6P <= 128) dense Cholesky in LDS over 16-column panels (DPP diagonal
-//                     tiles, FP64 MFMA panel / trailing updates) + the two solves
+//   lba_chol_tiled    (6P <= 128) dense Cholesky in LDS over 16-column panels (diagonal tiles by
+//                     DPP64 broadcasts folded into v_fmac_f64, FP64 MFMA panel / trailing
+//                     updates) + the two solves
 //   lba_chol_panel/_update/_solve_blocked  blocked Cholesky for 6P > 128
-//   lba_update        x_l = Dinv (b_l - Hpl^T x_p), T <- exp(x_p) T (SE3Quat::exp,
-//                     left-multiplied), X <- X + x_l, computeScale block sums
-//   lba_errors        trial residuals (kept as g2o's stale _error) + robust chi2 block sums
+//   lba_update        x_l = Dinv (b_l - Hpl^T x_p) (8 lanes per landmark), T <- exp(x_p) T
+//                     (SE3Quat::exp, left-multiplied), X <- X + x_l, computeScale block sums
+//   lba_errors        trial residuals (kept as g2o's stale _error), robust chi2 block sums and
+//                     the trial's linearisation into the trial estimate's record set
 //   lba_decide        the LM accept/reject/lambda logic (optimization_algorithm_levenberg.cpp
-//                     :61-164) and SparseOptimizer::optimize's stop rules on one thread: block
-//                     sums in block order, rho, lambda / nu, nBad; the accepted trial is copied
-//                     into the current estimate
+//                     :61-164) and SparseOptimizer::optimize's stop rules: rho, lambda / nu,
+//                     nBad; an accepted trial swaps the estimate (and linearisation) buffers
 // The LM state lives on the device (LMState): every kernel of a trial slot reads it and
-// returns at once when the optimisation has finished (the linearisation kernels also when the
-// slot is a retry of the same iteration). The host enqueues slots in chunks and reads the
-// state back once per chunk instead of once per trial.
+// returns at once when the optimisation has finished (the reductions also when the slot is a
+// retry of the same iteration). The host enqueues slots in chunks and reads the state back
+// once per chunk instead of once per trial.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
