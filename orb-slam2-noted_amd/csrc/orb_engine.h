@@ -54,6 +54,7 @@ struct ExtractGeom {
     int qt_nodes_in_lds;
     int qt_kl;                         // LDS key capacity (candidates) of the quadtree workgroup
     float scale[ORBX_MAXL];
+    float inv_scale[ORBX_MAXL];        // mvInvScaleFactors = 1.0f / mvScaleFactor (ORBextractor.cc:503)
     int scaled_patch[ORBX_MAXL];
     int ini_th, min_th, resize_mode;
     int rz_col_off[ORBX_MAXL], rz_row_off[ORBX_MAXL], rz_simd_end[ORBX_MAXL];

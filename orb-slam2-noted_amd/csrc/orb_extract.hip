@@ -2076,6 +2076,7 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             g.blur_off[l] = blur;
             blur += ((long long)g.bp[l] * g.lh[l] + 63) & ~63LL;
             g.scale[l] = e->scale[l];
+            g.inv_scale[l] = e->inv_scale[l];
             g.scaled_patch[l] = (int)(31 * e->scale[l]);
         }
         g.pyr_stride = std::max(pyr, 64LL);

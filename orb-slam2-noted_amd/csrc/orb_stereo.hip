@@ -2,12 +2,16 @@
 // Hamming core (ORBmatcher.cc:2123-2143).
 //
 // Three kernels per batch of stereo pairs:
-//   S1 stereo_sort_right  one workgroup per pair: right keypoints sorted by y (LDS bitonic)
-//                         -> replaces the vRowIndices row buckets (:858-888)
-//   S2 stereo_match_left  one wavefront per left keypoint: row-band candidates from the
-//                         sorted list, 64-wide popcount Hamming + (dist, index) min-reduce
-//                         (= first minimum in right-index order, :912-978), then the 11x11
-//                         SAD over incR in [-5, 5] (:981-1063), parabola fit and depth
+//   S1 stereo_sort_right  one workgroup per pair: right keypoints sorted by y (counting sort)
+//                         -> replaces the vRowIndices row buckets (:858-888); a second
+//                         workgroup per pair buckets the left keypoints by row
+//   S2 stereo_match_staged  one workgroup per 32 left keypoints of nearby rows: the union of
+//                         their row bands (sorted right records + right descriptors) staged in
+//                         LDS once, then per keypoint on one wavefront: 64-wide popcount Hamming
+//                         + (dist, index) min-reduce (= first minimum in right-index order,
+//                         :912-978), the 11x11 SAD over incR in [-5, 5] (:981-1063), parabola
+//                         fit and depth (stereo_match_left: the same with one keypoint per
+//                         wavefront reading global memory, ORBX_ST_V=0)
 //   S3 stereo_median_cut  one workgroup per pair: median of the SAD distances and the
 //                         1.5*1.4*median rejection (:1112-1127)
 #include <hip/hip_runtime.h>
@@ -55,6 +59,7 @@ struct StereoArgs {
     float rmax;              // 2 * max scale factor (row-band half-width bound)
     int nrows;               // row table entries per pair (image height + 2)
     int *rowtab;             // [pair][nrows]: first sorted right keypoint with y >= row
+    float maxD;              // mbf / minZ (Frame.cc:897-899), divided once on the host
 };
 
 __device__ __forceinline__ const uint8_t *side_level(const ExtractGeom &g, const StereoSide &s, int img,
@@ -74,17 +79,23 @@ __device__ __forceinline__ const uint8_t *side_level(const ExtractGeom &g, const
 // keypoint's final slot = bucket start + its rank among the bucket's few members by (y, index).
 // Replaces a 4096-key bitonic sort in LDS (86 -> ~10 us for one pair: the single-frame latency).
 #define ST_THREADS 512
-__global__ __launch_bounds__(ST_THREADS) void stereo_sort_right(ExtractGeom g, StereoArgs a, uint4 *sorted) {
+// Workgroups n_pairs .. 2 n_pairs - 1 (ORBX_ST_V = 1) bucket the LEFT keypoints of pair
+// blockIdx.x - n_pairs by image row into lidx (any order inside a row: S2 writes each result to
+// the keypoint's own slot, so the order only groups keypoints of nearby rows into workgroups).
+__global__ __launch_bounds__(ST_THREADS) void stereo_sort_right(ExtractGeom g, StereoArgs a, uint4 *sorted,
+                                                                int n_pairs, int *lidx) {
     extern __shared__ int st_lds[];
     int *cnt = st_lds;                       // [nrows] bucket sizes, then fill counters
     int *start = cnt + a.nrows;              // [nrows] exclusive prefix = row table
     int *mem = start + a.nrows;              // [cap] bucket members (keypoint index)
     float *yk = (float *)(mem + a.cap);      // [cap] y of keypoint i
     __shared__ int wsum[ST_THREADS / 64];
-    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = wave_id();
-    const int imgR = a.R.img_base + a.R.img_step * p;
-    const int nR = min(a.R.cnt[imgR], a.cap);
-    const orbx_kp *kR = a.R.kps + (long long)imgR * a.cap;
+    const bool left = (int)blockIdx.x >= n_pairs;
+    const int p = left ? blockIdx.x - n_pairs : blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+    const StereoSide &sd = left ? a.L : a.R;
+    const int imgR = sd.img_base + sd.img_step * p;
+    const int nR = min(sd.cnt[imgR], a.cap);
+    const orbx_kp *kR = sd.kps + (long long)imgR * a.cap;
     const int nrows = a.nrows;
     for (int r = tid; r < nrows; r += ST_THREADS) cnt[r] = 0;
     __syncthreads();
@@ -111,12 +122,19 @@ __global__ __launch_bounds__(ST_THREADS) void stereo_sort_right(ExtractGeom g, S
     for (int r = r0; r < r1; r++) {
         const int c = cnt[r];
         start[r] = run;
-        a.rowtab[(long long)p * nrows + r] = run;
+        if (!left) a.rowtab[(long long)p * nrows + r] = run;
         run += c;
     }
     __syncthreads();
     for (int r = tid; r < nrows; r += ST_THREADS) cnt[r] = 0;
     __syncthreads();
+    if (left) {
+        for (int i = tid; i < nR; i += ST_THREADS) {
+            const int b = min(max((int)yk[i], 0), nrows - 1);
+            lidx[(long long)p * a.sort_cap + start[b] + atomicAdd(&cnt[b], 1)] = i;
+        }
+        return;
+    }
     for (int i = tid; i < nR; i += ST_THREADS) {
         const int b = min(max((int)yk[i], 0), nrows - 1);
         mem[start[b] + atomicAdd(&cnt[b], 1)] = i;
@@ -140,6 +158,94 @@ __global__ __launch_bounds__(ST_THREADS) void stereo_sort_right(ExtractGeom g, S
     }
 }
 
+// SAD refinement of one left keypoint given its best Hamming candidate (Frame.cc:979-1063), on one
+// wavefront: 11x11 window SAD over incR in [-5, 5], parabola fit, disparity and depth; lane 0
+// writes slot o (uR, depth, SAD distance or -1 each). The caller passes the level-dependent
+// values (level images and pitches, width, scale, inverse scale of the keypoint's octave) as
+// scalars: indexing the geometry structs by reference here made the compiler copy them to scratch.
+__device__ __forceinline__ void stereo_refine(const orbx_kp &kpL, bool matched, float uR0, const uint8_t *imL,
+                                              int pitchL, const uint8_t *imR, int pitchR, int lw, float scale,
+                                              float sf, float mbf, float maxD, int lane, long long o,
+                                              float *u_right, float *depth, int *sad) {
+    float outU = -1.0f, outD = -1.0f;
+    int outS = -1;
+    const float uL = kpL.x;
+    const float minD = 0;
+    bool ok = matched;
+    float scaleduR0 = 0, scaledvL = 0, scaleduL = 0;
+    if (ok) {
+        scaleduL = roundf(kpL.x * sf);   // sf = mvInvScaleFactors[octave] (ORBextractor.cc:503)
+        scaledvL = roundf(kpL.y * sf);
+        scaleduR0 = roundf(uR0 * sf);
+        const float iniu = scaleduR0 - 5 - 5, endu = scaleduR0 + 5 + 5 + 1;
+        if (iniu < 0 || endu >= lw) ok = false;
+    }
+    if (ok) {
+        // SAD of (IL - IL(w, w)) and (IR - IR(w, w + incR)) over the 11 x 11 window (:989-1011):
+        // |(L + cr) - (R + cl)| per pixel, on packed u16 pairs with v_sad_u16 (a = L + cr - cl + 256,
+        // b = R + 256, both in [0, 766]). Lane 16 s + rr, pass p: window row rr (< 11), incR =
+        // 4 p + s - 5 (<= 5); the 16 lanes of a DPP row sum their rows, lane 15 holds incR's total.
+        const int r0 = (int)scaledvL - 5, cL0 = (int)scaleduL - 5, cR = (int)scaleduR0;
+        const int cl = imL[(long long)(r0 + 5) * pitchL + cL0 + 5];
+        const int rr = lane & 15, sgrp = lane >> 4, rrc = min(rr, 10);
+        uint32_t LD[3], RD[3];
+        __builtin_memcpy(LD, imL + (long long)(r0 + rrc) * pitchL + cL0, 12);   // 11 pixels + 1 (in the level)
+        const uint32_t Lp[6] = {__builtin_amdgcn_perm(0u, LD[0], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[0], 0x0c030c02u),
+                                __builtin_amdgcn_perm(0u, LD[1], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[1], 0x0c030c02u),
+                                __builtin_amdgcn_perm(0u, LD[2], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[2], 0x0c0c0c02u)};
+        const uint32_t ONES = 0x01010101u;
+        const uint8_t *rowR = imR + (long long)(r0 + rrc) * pitchR + cR - 5;
+        const uint8_t *rowC = imR + (long long)(r0 + 5) * pitchR + cR;
+        int sums[12];
+#pragma unroll
+        for (int pss = 0; pss < 3; pss++) {
+            const int inc = 4 * pss + sgrp - 5, incc = min(inc, 5);
+            const uint32_t KA = (uint32_t)(rowC[incc] - cl + 256), KA2 = KA * 0x10001u;
+            __builtin_memcpy(RD, rowR + incc, 12);   // cols cR + inc - 5 .. + 6 (endu < width)
+            uint32_t acc = __builtin_amdgcn_sad_u16(Lp[0] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04010400u), 0u);
+            acc = __builtin_amdgcn_sad_u16(Lp[1] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04030402u), acc);
+            acc = __builtin_amdgcn_sad_u16(Lp[2] + KA2, __builtin_amdgcn_perm(ONES, RD[1], 0x04010400u), acc);
+            acc = __builtin_amdgcn_sad_u16(Lp[3] + KA2, __builtin_amdgcn_perm(ONES, RD[1], 0x04030402u), acc);
+            acc = __builtin_amdgcn_sad_u16(Lp[4] + KA2, __builtin_amdgcn_perm(ONES, RD[2], 0x04010400u), acc);
+            acc = __builtin_amdgcn_sad_u16(Lp[5] + KA, __builtin_amdgcn_perm(ONES, RD[2], 0x0c0c0402u), acc);
+            int v = (rr < 11 && inc <= 5) ? (int)acc : 0;
+            v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+            v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+            v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+            v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
+#pragma unroll
+            for (int k = 0; k < 4; k++) sums[4 * pss + k] = __builtin_amdgcn_readlane(v, 16 * k + 15);
+        }
+        // wave-uniform tail (:1013-1063): first minimum over incR, parabola, disparity
+        int bestS = INT_MAX, bestinc = 0;
+#pragma unroll
+        for (int inc = -5; inc <= 5; inc++)
+            if (sums[inc + 5] < bestS) { bestS = sums[inc + 5]; bestinc = inc; }
+        if (bestinc != -5 && bestinc != 5) {
+            const float d1 = (float)sums[5 + bestinc - 1], d2 = (float)sums[5 + bestinc], d3 = (float)sums[5 + bestinc + 1];
+            const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
+            if (!(deltaR < -1 || deltaR > 1)) {
+                float bestuR = scale * ((float)scaleduR0 + (float)bestinc + deltaR);
+                float disparity = uL - bestuR;
+                if (disparity >= minD && disparity < maxD) {
+                    if (disparity <= 0) {
+                        disparity = (float)0.01;
+                        bestuR = (float)((double)uL - 0.01);
+                    }
+                    outD = mbf / disparity;
+                    outU = bestuR;
+                    outS = bestS;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        u_right[o] = outU;
+        depth[o] = outD;
+        sad[o] = outS;
+    }
+}
+
 // ---- S2: per left keypoint
 __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoArgs a,
                                                          const uint4 *sorted,
@@ -154,13 +260,11 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
     const int nL = min(a.L.cnt[imgL], a.cap), nR = min(a.R.cnt[imgR], a.cap);
     const long long o = (long long)p * a.cap + iL;
     if (iL >= nL) return;
-    float outU = -1.0f, outD = -1.0f;
-    int outS = -1;
     const orbx_kp kpL = a.L.kps[(long long)imgL * a.cap + iL];
     const orbx_kp *kR = a.R.kps + (long long)imgR * a.cap;
     const int levelL = kpL.octave;
     const float vL = kpL.y, uL = kpL.x;
-    const float minZ = a.mb, minD = 0, maxD = a.mbf / minZ;
+    const float minD = 0, maxD = a.maxD;
     const float minU = uL - maxD, maxU = uL - minD;
     const int row = (int)vL;
     int bestDist = 100;  // ORBmatcher::TH_HIGH
@@ -211,86 +315,154 @@ __global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoAr
             bestIdxR = (int)(best & 0xFFFF);
         }
     }
-    const int thOrbDist = (100 + 50) / 2;
-    bool ok = maxU >= 0 && bestDist < thOrbDist;
-    int oct = levelL;
-    float scaleduR0 = 0, scaledvL = 0, scaleduL = 0;
-    int pitchL = 0, pitchR = 0;
-    const uint8_t *imL = nullptr, *imR = nullptr;
-    if (ok) {
-        const float uR0 = kR[bestIdxR].x;
-        const float sf = 1.0f / g.scale[oct];  // mvInvScaleFactors (ORBextractor.cc:503)
-        scaleduL = roundf(kpL.x * sf);
-        scaledvL = roundf(kpL.y * sf);
-        scaleduR0 = roundf(uR0 * sf);
-        const float iniu = scaleduR0 - 5 - 5, endu = scaleduR0 + 5 + 5 + 1;
-        if (iniu < 0 || endu >= g.lw[oct]) ok = false;
-        imL = side_level(g, a.L, imgL, oct, &pitchL);
-        imR = side_level(g, a.R, imgR, oct, &pitchR);
-    }
-    if (ok) {
-        // SAD of (IL - IL(w, w)) and (IR - IR(w, w + incR)) over the 11 x 11 window (:989-1011):
-        // |(L + cr) - (R + cl)| per pixel, on packed u16 pairs with v_sad_u16 (a = L + cr - cl + 256,
-        // b = R + 256, both in [0, 766]). Lane 16 s + rr, pass p: window row rr (< 11), incR =
-        // 4 p + s - 5 (<= 5); the 16 lanes of a DPP row sum their rows, lane 15 holds incR's total.
-        const int r0 = (int)scaledvL - 5, cL0 = (int)scaleduL - 5, cR = (int)scaleduR0;
-        const int cl = imL[(long long)(r0 + 5) * pitchL + cL0 + 5];
-        const int rr = lane & 15, sgrp = lane >> 4, rrc = min(rr, 10);
-        uint32_t LD[3], RD[3];
-        __builtin_memcpy(LD, imL + (long long)(r0 + rrc) * pitchL + cL0, 12);   // 11 pixels + 1 (in the level)
-        const uint32_t Lp[6] = {__builtin_amdgcn_perm(0u, LD[0], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[0], 0x0c030c02u),
-                                __builtin_amdgcn_perm(0u, LD[1], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[1], 0x0c030c02u),
-                                __builtin_amdgcn_perm(0u, LD[2], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[2], 0x0c0c0c02u)};
-        const uint32_t ONES = 0x01010101u;
-        const uint8_t *rowR = imR + (long long)(r0 + rrc) * pitchR + cR - 5;
-        const uint8_t *rowC = imR + (long long)(r0 + 5) * pitchR + cR;
-        int sums[12];
-#pragma unroll
-        for (int pss = 0; pss < 3; pss++) {
-            const int inc = 4 * pss + sgrp - 5, incc = min(inc, 5);
-            const uint32_t KA = (uint32_t)(rowC[incc] - cl + 256), KA2 = KA * 0x10001u;
-            __builtin_memcpy(RD, rowR + incc, 12);   // cols cR + inc - 5 .. + 6 (endu < width)
-            uint32_t acc = __builtin_amdgcn_sad_u16(Lp[0] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04010400u), 0u);
-            acc = __builtin_amdgcn_sad_u16(Lp[1] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04030402u), acc);
-            acc = __builtin_amdgcn_sad_u16(Lp[2] + KA2, __builtin_amdgcn_perm(ONES, RD[1], 0x04010400u), acc);
-            acc = __builtin_amdgcn_sad_u16(Lp[3] + KA2, __builtin_amdgcn_perm(ONES, RD[1], 0x04030402u), acc);
-            acc = __builtin_amdgcn_sad_u16(Lp[4] + KA2, __builtin_amdgcn_perm(ONES, RD[2], 0x04010400u), acc);
-            acc = __builtin_amdgcn_sad_u16(Lp[5] + KA, __builtin_amdgcn_perm(ONES, RD[2], 0x0c0c0402u), acc);
-            int v = (rr < 11 && inc <= 5) ? (int)acc : 0;
-            v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
-            v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
-            v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
-            v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
-#pragma unroll
-            for (int k = 0; k < 4; k++) sums[4 * pss + k] = __builtin_amdgcn_readlane(v, 16 * k + 15);
+    const bool matched = maxU >= 0 && bestDist < (100 + 50) / 2;   // thOrbDist (Frame.cc:842)
+    int pitchL, pitchR;
+    const uint8_t *imL = side_level(g, a.L, imgL, levelL, &pitchL), *imR = side_level(g, a.R, imgR, levelL, &pitchR);
+    stereo_refine(kpL, matched, matched ? kR[bestIdxR].x : 0.0f, imL, pitchL, imR, pitchR, g.lw[levelL], g.scale[levelL],
+                  g.inv_scale[levelL], a.mbf, a.maxD, lane, o, u_right, depth, sad);
+}
+
+// ---- S2, staged form (ORBX_ST_V = 1): one workgroup per ST_NK left keypoints of nearby rows
+// (S1's row buckets), whose candidate bands overlap: the union of their bands -- the sorted right
+// records and the right descriptors they index -- is staged in LDS once (one global round trip
+// per workgroup instead of a record and a descriptor load per keypoint), then each wavefront scans
+// ORBX_ST_KPW keypoints from LDS. The candidate set and the (dist, index) minimum are those of the
+// per-keypoint form: band [first record with y >= floor(row - rmax - 2), first with
+// y >= floor(row + rmax + 2) + 1) and the same per-record test; a union wider than ST_SCAP records
+// scans global memory instead.
+#ifndef ORBX_ST_V
+#define ORBX_ST_V 1
+#endif
+#ifndef ORBX_ST_KPW
+#define ORBX_ST_KPW 8
+#endif
+#define ST_NW 4
+#define ST_NK (ST_NW * ORBX_ST_KPW)
+#define ST_SCAP 256
+
+__device__ __forceinline__ int hamming_v(const uint4 &x0, const uint4 &x1, const uint4 &y0, const uint4 &y1) {
+    return __popc(x0.x ^ y0.x) + __popc(x0.y ^ y0.y) + __popc(x0.z ^ y0.z) + __popc(x0.w ^ y0.w) +
+           __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
+}
+
+__global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g, StereoArgs a, const uint4 *sorted,
+                                                                  const int *lidx, float *u_right, float *depth,
+                                                                  int *sad) {
+    __shared__ uint4 s_rec[ST_SCAP], s_d0[ST_SCAP], s_d1[ST_SCAP];
+    __shared__ int s_kp[ST_NK][3];   // left keypoint index (-1: none), band [lo, hi)
+    __shared__ int s_lo, s_hi;
+    lat_prio<8>();
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+    int bxr, p;
+    xcd_remap2(bxr, p);
+    const int imgL = a.L.img_base + a.L.img_step * p, imgR = a.R.img_base + a.R.img_step * p;
+    const int nL = min(a.L.cnt[imgL], a.cap), nR = min(a.R.cnt[imgR], a.cap);
+    const int s0 = bxr * ST_NK;
+    if (s0 >= nL) return;   // workgroup-uniform, before any barrier
+    const orbx_kp *kL = a.L.kps + (long long)imgL * a.cap;
+    const orbx_kp *kR = a.R.kps + (long long)imgR * a.cap;
+    const uint4 *srt = sorted + (long long)p * a.sort_cap;
+    const int *rowtab = a.rowtab + (long long)p * a.nrows;
+    if (tid == 0) { s_lo = INT_MAX; s_hi = INT_MIN; }
+    __syncthreads();
+    if (tid < ST_NK) {
+        int iL = -1, lo = 0, hi = 0;
+        if (s0 + tid < nL) {
+            iL = lidx[(long long)p * a.sort_cap + s0 + tid];
+            const int row = (int)kL[iL].y;
+            const float ylo = (float)row - a.rmax - 2.0f, yhi = (float)row + a.rmax + 2.0f;
+            lo = rowtab[min(max((int)floorf(ylo), 0), a.nrows - 1)];
+            const int hr = (int)floorf(yhi) + 1;
+            hi = hr >= a.nrows ? nR : min(rowtab[max(hr, 0)], nR);
+            lo = min(lo, hi);
+            atomicMin(&s_lo, lo);
+            atomicMax(&s_hi, hi);
         }
-        // wave-uniform tail (:1013-1063): first minimum over incR, parabola, disparity
-        int bestS = INT_MAX, bestinc = 0;
-#pragma unroll
-        for (int inc = -5; inc <= 5; inc++)
-            if (sums[inc + 5] < bestS) { bestS = sums[inc + 5]; bestinc = inc; }
-        if (bestinc != -5 && bestinc != 5) {
-            const float d1 = (float)sums[5 + bestinc - 1], d2 = (float)sums[5 + bestinc], d3 = (float)sums[5 + bestinc + 1];
-            const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
-            if (!(deltaR < -1 || deltaR > 1)) {
-                float bestuR = g.scale[oct] * ((float)scaleduR0 + (float)bestinc + deltaR);
-                float disparity = uL - bestuR;
-                if (disparity >= minD && disparity < maxD) {
-                    if (disparity <= 0) {
-                        disparity = (float)0.01;
-                        bestuR = (float)((double)uL - 0.01);
-                    }
-                    outD = a.mbf / disparity;
-                    outU = bestuR;
-                    outS = bestS;
+        s_kp[tid][0] = iL;
+        s_kp[tid][1] = lo;
+        s_kp[tid][2] = hi;
+    }
+    __syncthreads();
+    const int ulo = s_lo, un = s_hi - s_lo;
+    const bool staged = un <= ST_SCAP;   // workgroup-uniform
+    if (staged) {
+        const uint4 *dR4 = (const uint4 *)(a.R.desc + (long long)imgR * a.cap * 32);
+        for (int j = tid; j < un; j += ST_NW * 64) {
+            const uint4 r = srt[ulo + j];
+            const int i = (int)(r.w & 0xFFFFu);
+            s_rec[j] = r;
+            s_d0[j] = dR4[2 * i];
+            s_d1[j] = dR4[2 * i + 1];
+        }
+    }
+    __syncthreads();
+    const uint8_t *dRg = a.R.desc + (long long)imgR * a.cap * 32;
+    for (int k = 0; k < ORBX_ST_KPW; k++) {
+        const int slot = wv * ORBX_ST_KPW + k;
+        const int iL = __builtin_amdgcn_readfirstlane(s_kp[slot][0]);
+        if (iL < 0) break;   // the workgroup's last slots past nL
+        const int lo = __builtin_amdgcn_readfirstlane(s_kp[slot][1]), hi = __builtin_amdgcn_readfirstlane(s_kp[slot][2]);
+        const orbx_kp kpL = kL[iL];
+        const int levelL = kpL.octave;
+        const float vL = kpL.y, uL = kpL.x;
+        const float minD = 0, maxD = a.maxD;
+        const float minU = uL - maxD, maxU = uL - minD;
+        const int row = (int)vL;
+        const float yhi = (float)row + a.rmax + 2.0f;
+        int bestDist = 100;  // ORBmatcher::TH_HIGH
+        int bestIdxR = 0;
+        if (maxU >= 0) {
+            const uint4 *dL4 = (const uint4 *)(a.L.desc + ((long long)imgL * a.cap + iL) * 32);
+            const uint4 q0 = dL4[0], q1 = dL4[1];
+            unsigned best = 0xFFFFFFFFu;
+            // the per-record test as one branch-free predicate (bitwise: no short-circuit branches)
+            auto take = [&](const uint4 &e) {
+                const float ky = __uint_as_float(e.x);
+                const int oct = (int)(e.w >> 16);
+                const float kx = __uint_as_float(e.y);
+                const int minr = (int)(int16_t)(e.z & 0xFFFFu), maxr = (int)(int16_t)(e.z >> 16);
+                return (ky <= yhi) & (row >= minr) & (row <= maxr) & ((unsigned)(oct - levelL + 1) <= 2u) & (kx >= minU) &
+                       (kx <= maxU);
+            };
+            const uint4 NONE = make_uint4(0x7f800000u, 0u, 0u, 0u);
+            if (staged) {
+                // LDS slots past the band are read anyway (clamped into the array) and masked
+                const int end = hi - ulo;
+                for (int base = lo - ulo; base < end; base += 128) {
+                    const int c0 = base + lane, c1 = c0 + 64;
+                    const int j0 = min(c0, ST_SCAP - 1), j1 = min(c1, ST_SCAP - 1);
+                    const uint4 e0 = s_rec[j0], e1 = s_rec[j1];
+                    const bool t0 = (c0 < end) & take(e0), t1 = (c1 < end) & take(e1);
+                    if (t0) best = min(best, ((unsigned)hamming_v(q0, q1, s_d0[j0], s_d1[j0]) << 16) | (e0.w & 0xFFFFu));
+                    if (t1) best = min(best, ((unsigned)hamming_v(q0, q1, s_d0[j1], s_d1[j1]) << 16) | (e1.w & 0xFFFFu));
+                }
+            } else {
+                for (int base = lo; base < hi; base += 128) {
+                    const int c0 = base + lane, c1 = c0 + 64;
+                    const uint4 e0 = c0 < hi ? srt[c0] : NONE, e1 = c1 < hi ? srt[c1] : NONE;
+                    const bool t0 = take(e0), t1 = take(e1);
+                    const int i0 = (int)(e0.w & 0xFFFFu), i1 = (int)(e1.w & 0xFFFFu);
+                    if (t0) best = min(best, ((unsigned)hamming32((const uint8_t *)dL4, dRg + (long long)i0 * 32) << 16) | (unsigned)i0);
+                    if (t1) best = min(best, ((unsigned)hamming32((const uint8_t *)dL4, dRg + (long long)i1 * 32) << 16) | (unsigned)i1);
                 }
             }
+            best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x111, 0xF, 0xF, false));
+            best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x112, 0xF, 0xF, false));
+            best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x114, 0xF, 0xF, false));
+            best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x118, 0xF, 0xF, false));
+            best = min(min((unsigned)__builtin_amdgcn_readlane((int)best, 15), (unsigned)__builtin_amdgcn_readlane((int)best, 31)),
+                       min((unsigned)__builtin_amdgcn_readlane((int)best, 47), (unsigned)__builtin_amdgcn_readlane((int)best, 63)));
+            if (best != 0xFFFFFFFFu && (int)(best >> 16) < bestDist) {
+                bestDist = (int)(best >> 16);
+                bestIdxR = (int)(best & 0xFFFF);
+            }
         }
-    }
-    if (lane == 0) {
-        u_right[o] = outU;
-        depth[o] = outD;
-        sad[o] = outS;
+        const bool matched = maxU >= 0 && bestDist < (100 + 50) / 2;   // thOrbDist (Frame.cc:842)
+        int pitchL, pitchR;
+        const uint8_t *imL = side_level(g, a.L, imgL, levelL, &pitchL), *imR = side_level(g, a.R, imgR, levelL, &pitchR);
+        stereo_refine(kpL, matched, matched ? kR[bestIdxR].x : 0.0f, imL, pitchL, imR, pitchR, g.lw[levelL],
+                      g.scale[levelL], g.inv_scale[levelL], a.mbf, a.maxD, lane, (long long)p * a.cap + iL, u_right, depth,
+                      sad);
     }
 }
 
@@ -359,6 +531,8 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
     float smax = 0;
     for (int l = 0; l < g.nlevels; l++) smax = std::max(smax, g.scale[l]);
     a.rmax = 2.0f * smax;
+    // the same IEEE single divisions the reference makes per frame / per extractor
+    a.maxD = a.mbf / a.mb;
     const size_t slots = (size_t)n_pairs * a.cap;
     a.nrows = g.H + 2;
     HIPCHK(order_after_done(store, s));
@@ -372,13 +546,22 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
     const size_t sort_lds = 4 * (2 * (size_t)a.nrows + 2 * (size_t)a.cap);
     if (sort_lds > 64 * 1024) return ORBX_EINVAL;
     int ph = prof_begin(store, s);
-    stereo_sort_right<<<n_pairs, ST_THREADS, sort_lds, s>>>(g, a, store->d_st_sorted.as<uint4>());
+    const bool staged = ORBX_ST_V == 1;
+    if (staged && store->d_st_res.ensure(4 * (size_t)n_pairs * sc)) return ORBX_EDEVICE;
+    int *lidx = store->d_st_res.as<int>();
+    stereo_sort_right<<<staged ? 2 * n_pairs : n_pairs, ST_THREADS, sort_lds, s>>>(g, a, store->d_st_sorted.as<uint4>(),
+                                                                                  n_pairs, lidx);
     prof_end(store, s, ph, "stereo_sort_right");
     ph = prof_begin(store, s);
-    for (int rep = 0; rep < ((exp_twice() & 8) ? 2 : 1); rep++)
-    stereo_match_left<<<dim3((a.cap + 3) / 4, n_pairs), 256, 0, s>>>(
-        g, a, store->d_st_sorted.as<uint4>(), u, d, sad);
-    prof_end(store, s, ph, "stereo_match_left");
+    for (int rep = 0; rep < ((exp_twice() & 8) ? 2 : 1); rep++) {
+        if (staged)
+            stereo_match_staged<<<dim3((a.cap + ST_NK - 1) / ST_NK, n_pairs), ST_NW * 64, 0, s>>>(
+                g, a, store->d_st_sorted.as<uint4>(), lidx, u, d, sad);
+        else
+            stereo_match_left<<<dim3((a.cap + 3) / 4, n_pairs), 256, 0, s>>>(g, a, store->d_st_sorted.as<uint4>(), u, d,
+                                                                           sad);
+    }
+    prof_end(store, s, ph, staged ? "stereo_match_staged" : "stereo_match_left");
     ph = prof_begin(store, s);
     stereo_median_cut<<<n_pairs, ST_THREADS, 0, s>>>(a, u, d, sad);
     prof_end(store, s, ph, "stereo_median_cut");

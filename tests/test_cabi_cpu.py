@@ -63,3 +63,37 @@ def test_build_id_matches_sources():
     want = subprocess.run([sys.executable, str(ROOT / "tools" / "src_hash.py")], capture_output=True, text=True,
                           check=True).stdout.strip()
     assert amd.build_id() == want
+
+
+def test_no_kernel_uses_scratch(tmp_path):
+    """Every gfx950 kernel of the library runs without private (scratch) memory: a dynamically
+    indexed local or a kernel-argument struct the compiler copies to the stack turns a kernel's
+    register work into memory traffic (a by-value geometry struct indexed through a reference once
+    cost the stereo matcher 40x). Read from the code object's metadata notes, no GPU needed."""
+    import shutil
+    import subprocess
+    llvm = Path("/opt/rocm/llvm/bin")
+    if not (llvm / "llvm-objdump").exists() or not LIB.exists():
+        import pytest
+        pytest.skip("ROCm llvm tools or the library missing")
+    lib = tmp_path / LIB.name
+    shutil.copy(LIB, lib)
+    subprocess.run([str(llvm / "llvm-objdump"), "--offloading", str(lib)], cwd=tmp_path, check=True,
+                   capture_output=True)
+    objs = sorted(tmp_path.glob("*gfx950*"))
+    assert objs, "no gfx950 code object in the library"
+    kernels = {}
+    for obj in objs:
+        notes = subprocess.run([str(llvm / "llvm-readelf"), "--notes", str(obj)], check=True, capture_output=True,
+                               text=True).stdout
+        scratch = None
+        for line in notes.splitlines():   # each kernel map: ... .private_segment_fixed_size ... .symbol
+            m = re.match(r"\s+\.private_segment_fixed_size:\s+(\d+)", line)
+            if m:
+                scratch = int(m.group(1))
+            m = re.match(r"\s+\.symbol:\s+(\S+)\.kd", line)
+            if m:
+                kernels[m.group(1)] = scratch
+    assert len(kernels) > 40, kernels
+    using = {k: v for k, v in kernels.items() if v != 0}
+    assert not using, f"kernels with scratch memory: {using}"

@@ -36,6 +36,30 @@ def test_stereo_single_pair(amd, oracle_mod, t):
     np.testing.assert_array_equal(d.view(np.uint32), d_ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("rows", [36, 160])
+def test_stereo_dense_rows(amd, oracle_mod, rows):
+    """Keypoints packed into a band of rows: with 36 rows every candidate band holds far more
+    right keypoints than a workgroup stages (ST_SCAP, orb_stereo.hip), so the staged matcher
+    takes its global-memory scan; with 160 rows both forms occur."""
+    h, w = 376, 1241
+    rng = np.random.default_rng(rows)
+    L = np.full((h, w), 40, np.uint8)
+    y0 = (h - rows) // 2
+    L[y0:y0 + rows] = rng.integers(0, 256, size=(rows, w), dtype=np.uint8)
+    R = np.roll(L, -17, axis=1)
+    R[:, -17:] = 40
+    kL, u_ref, d_ref, mb = _stereo_ref(oracle_mod, L, R, 2000)
+    exL = amd.ORBextractor(2000)
+    exR = amd.ORBextractor(2000)
+    k, _ = exL(L)
+    exR(R)
+    assert len(k) == len(kL)
+    u, d = amd.compute_stereo_matches(exL, exR, len(k), KITTI_BF, mb)
+    assert (u_ref >= 0).sum() > 50
+    np.testing.assert_array_equal(u.view(np.uint32), u_ref.view(np.uint32))
+    np.testing.assert_array_equal(d.view(np.uint32), d_ref.view(np.uint32))
+
+
 def test_stereo_batch(amd, oracle_mod):
     import torch
     h, w, P = 376, 1241, 3
