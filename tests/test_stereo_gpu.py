@@ -36,6 +36,22 @@ def test_stereo_single_pair(amd, oracle_mod, t):
     np.testing.assert_array_equal(d.view(np.uint32), d_ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("nf", [90, 300])
+def test_stereo_few_features(amd, oracle_mod, nf):
+    """Keypoint counts that leave the last staged workgroup (32 left keypoints, 8 per wavefront)
+    partly filled, and images with few candidates per band."""
+    L, R = synth.stereo_pair(376, 1241, 5)
+    kL, u_ref, d_ref, mb = _stereo_ref(oracle_mod, L, R, nf)
+    exL = amd.ORBextractor(nf)
+    exR = amd.ORBextractor(nf)
+    k, _ = exL(L)
+    exR(R)
+    assert len(k) == len(kL)
+    u, d = amd.compute_stereo_matches(exL, exR, len(k), KITTI_BF, mb)
+    np.testing.assert_array_equal(u.view(np.uint32), u_ref.view(np.uint32))
+    np.testing.assert_array_equal(d.view(np.uint32), d_ref.view(np.uint32))
+
+
 @pytest.mark.parametrize("rows", [36, 160])
 def test_stereo_dense_rows(amd, oracle_mod, rows):
     """Keypoints packed into a band of rows: with 36 rows every candidate band holds far more
