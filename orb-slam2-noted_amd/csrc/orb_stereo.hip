@@ -79,6 +79,9 @@ __device__ __forceinline__ const uint8_t *side_level(const ExtractGeom &g, const
 // keypoint's final slot = bucket start + its rank among the bucket's few members by (y, index).
 // Replaces a 4096-key bitonic sort in LDS (86 -> ~10 us for one pair: the single-frame latency).
 #define ST_THREADS 512
+#ifndef ORBX_ST_WIN
+#define ORBX_ST_WIN 1   // SAD window: one 20-byte right load per lane, centre pixels by ds_bpermute
+#endif
 // Workgroups n_pairs .. 2 n_pairs - 1 (ORBX_ST_V = 1) bucket the LEFT keypoints of pair
 // blockIdx.x - n_pairs by image row into lidx (any order inside a row: S2 writes each result to
 // the keypoint's own slot, so the order only groups keypoints of nearby rows into workgroups).
@@ -186,22 +189,45 @@ __device__ __forceinline__ void stereo_refine(const orbx_kp &kpL, bool matched, 
         // b = R + 256, both in [0, 766]). Lane 16 s + rr, pass p: window row rr (< 11), incR =
         // 4 p + s - 5 (<= 5); the 16 lanes of a DPP row sum their rows, lane 15 holds incR's total.
         const int r0 = (int)scaledvL - 5, cL0 = (int)scaleduL - 5, cR = (int)scaleduR0;
-        const int cl = imL[(long long)(r0 + 5) * pitchL + cL0 + 5];
         const int rr = lane & 15, sgrp = lane >> 4, rrc = min(rr, 10);
-        uint32_t LD[3], RD[3];
+        uint32_t LD[3];
         __builtin_memcpy(LD, imL + (long long)(r0 + rrc) * pitchL + cL0, 12);   // 11 pixels + 1 (in the level)
+#if ORBX_ST_WIN
+        // the lane's right-window bytes of all three passes in one 20-byte load: pass p reads cols
+        // cR + 4 p + s - 10 .. + 11, i.e. dwords p .. p + 2 of the block at cR + s - 10 (its last
+        // bytes reach at most one column past the reference's window, still inside the level's
+        // row storage: the window's rows end >= 14 rows above the level's last). The centre
+        // pixels IL(w, w) and IR(w, w + incR) are bytes of window row 5: taken from lane 16 s + 5
+        // by ds_bpermute instead of four more byte loads.
+        uint32_t WR[5];
+        __builtin_memcpy(WR, imR + (long long)(r0 + rrc) * pitchR + cR - 10 + sgrp, 20);
+        const int c5 = ((lane & ~15) | 5) << 2;
+        const int cl = (int)((__builtin_amdgcn_ds_bpermute(c5, (int)LD[1]) >> 8) & 0xFF);   // col cL0 + 5
+#else
+        const int cl = imL[(long long)(r0 + 5) * pitchL + cL0 + 5];
+        uint32_t RD[3];
+#endif
         const uint32_t Lp[6] = {__builtin_amdgcn_perm(0u, LD[0], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[0], 0x0c030c02u),
                                 __builtin_amdgcn_perm(0u, LD[1], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[1], 0x0c030c02u),
                                 __builtin_amdgcn_perm(0u, LD[2], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[2], 0x0c0c0c02u)};
         const uint32_t ONES = 0x01010101u;
+#if !ORBX_ST_WIN
         const uint8_t *rowR = imR + (long long)(r0 + rrc) * pitchR + cR - 5;
         const uint8_t *rowC = imR + (long long)(r0 + 5) * pitchR + cR;
+#endif
         int sums[12];
 #pragma unroll
         for (int pss = 0; pss < 3; pss++) {
-            const int inc = 4 * pss + sgrp - 5, incc = min(inc, 5);
+            const int inc = 4 * pss + sgrp - 5;
+#if ORBX_ST_WIN
+            const uint32_t RD[3] = {WR[pss], WR[pss + 1], WR[pss + 2]};
+            const int kc = (int)((__builtin_amdgcn_ds_bpermute(c5, (int)WR[pss + 1]) >> 8) & 0xFF);   // col cR + inc
+            const uint32_t KA = (uint32_t)(kc - cl + 256), KA2 = KA * 0x10001u;
+#else
+            const int incc = min(inc, 5);
             const uint32_t KA = (uint32_t)(rowC[incc] - cl + 256), KA2 = KA * 0x10001u;
             __builtin_memcpy(RD, rowR + incc, 12);   // cols cR + inc - 5 .. + 6 (endu < width)
+#endif
             uint32_t acc = __builtin_amdgcn_sad_u16(Lp[0] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04010400u), 0u);
             acc = __builtin_amdgcn_sad_u16(Lp[1] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04030402u), acc);
             acc = __builtin_amdgcn_sad_u16(Lp[2] + KA2, __builtin_amdgcn_perm(ONES, RD[1], 0x04010400u), acc);
