@@ -1,0 +1,61 @@
+"""bench.py publishes committed PMC counters (profiles/pmc_traffic.json, profiles/lba_pmc.json) only
+for the library they were measured on: the summary's stamp.src_hash (tools/src_hash.py at profiling
+time) must equal the loaded library's orbx_build_id(), and the stamped configuration must match the
+run. CPU only: the stamp check itself and the committed summaries' shape."""
+import json
+from pathlib import Path
+
+import pytest
+
+import bench
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.fixture
+def profiles(tmp_path, monkeypatch):
+    (tmp_path / "profiles").mkdir()
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+
+    def write(name, stamp, kernels):
+        (tmp_path / "profiles" / name).write_text(json.dumps({"stamp": stamp, "kernels": kernels}))
+    return write
+
+
+def test_matching_stamp_publishes_counters(profiles):
+    profiles("p.json", {"src_hash": "abc", "commit": "c0ffee", "batch": 128, "resize_mode": 0},
+             {"orbamd::fast_blur_kernel(orbamd::ExtractGeom, ...)": {"valu_insts_per_launch": 7}})
+    kern, note = bench.load_pmc_doc("p.json", "abc", batch=128, resize_mode=0)
+    assert kern is not None and kern["fast_blur_kernel"]["valu_insts_per_launch"] == 7
+    assert "abc" in note and "c0ffee" in note
+
+
+def test_other_sources_withhold_counters(profiles):
+    profiles("p.json", {"src_hash": "abc", "commit": "c0ffee", "batch": 128}, {"k": {}})
+    kern, note = bench.load_pmc_doc("p.json", "def", batch=128)
+    assert kern is None and "not reported" in note
+
+
+def test_other_configuration_withholds_counters(profiles):
+    profiles("p.json", {"src_hash": "abc", "commit": "c0ffee", "batch": 128, "resize_mode": 0}, {"k": {}})
+    kern, note = bench.load_pmc_doc("p.json", "abc", batch=256, resize_mode=0)
+    assert kern is None and "batch" in note
+    kern, note = bench.load_pmc_doc("p.json", "abc", batch=128, resize_mode=1)
+    assert kern is None and "resize_mode" in note
+
+
+def test_missing_or_unstamped_summary(profiles):
+    kern, note = bench.load_pmc_doc("absent.json", "abc")
+    assert kern is None and "absent" in note
+    profiles("old.json", None, {"k": {}})
+    kern, note = bench.load_pmc_doc("old.json", "abc")
+    assert kern is None
+
+
+@pytest.mark.parametrize("fname", ["pmc_traffic.json", "lba_pmc.json"])
+def test_committed_summaries_are_stamped(fname):
+    doc = json.loads((ROOT / "profiles" / fname).read_text())
+    st = doc["stamp"]
+    assert len(st["src_hash"]) == 16 and int(st["src_hash"], 16) >= 0
+    assert st["commit"] and st["commit"] != "unknown"
+    assert doc["kernels"]
