@@ -59,6 +59,7 @@ struct ExtractGeom {
     int ini_th, min_th, resize_mode;
     int rz_col_off[ORBX_MAXL], rz_row_off[ORBX_MAXL], rz_simd_end[ORBX_MAXL];
     int blur_tiles_x[ORBX_MAXL], blur_tiles_y[ORBX_MAXL], blur_tile_base[ORBX_MAXL + 1];
+    unsigned blur_tx_rcp[ORBX_MAXL];   // ceil(2^31 / blur_tiles_x): tile row = umulhi(2 t, rcp) on the SALU
     // FAST cell grid per level (ORBextractor.cc:1084-1118): cell sides, the cells kept by the
     // row / column bounds, and ceil(2^20 / side) for the pixel -> cell division
     int hcell[ORBX_MAXL], wcell[ORBX_MAXL], ncell_rows[ORBX_MAXL], ncell_cols[ORBX_MAXL];

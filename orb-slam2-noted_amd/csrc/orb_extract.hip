@@ -478,7 +478,9 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     int t = blockIdx.x, l = 0;
     while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
     t -= g.blur_tile_base[l];
-    const int tx = t % g.blur_tiles_x[l], ty = t / g.blur_tiles_x[l];
+    // t / blur_tiles_x by the rounded-up reciprocal (exact while t * blur_tiles_x < 2^31): scalar
+    // multiplies instead of the compiler's VALU reciprocal for a scalar division
+    const int ty = (int)__umulhi(2u * (unsigned)t, g.blur_tx_rcp[l]), tx = t - ty * g.blur_tiles_x[l];
     const int w = g.lw[l], h = g.lh[l];
     const int x0 = tx * FB_TW, y0 = ty * FB_TH;
     int pitch;
@@ -502,8 +504,16 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             // both rows' loads in flight before either LDS write (one global round trip)
             const bool two = rr0 + 15 < FB_TH + 8;
             uint2 v0, v1 = make_uint2(0u, 0u);
-            __builtin_memcpy(&v0, row_of(rr0) + xs, 8);
-            if (two) __builtin_memcpy(&v1, row_of(rr0 + 15) + xs, 8);
+            const uint8_t *p0, *p1;
+            if (y0 >= 4 && y0 + FB_TH + 4 <= h) {   // workgroup-uniform: all 24 staged rows inside the level
+                p0 = src + (long long)(y0 - 4) * pitch + (rr0 * pitch + xs);
+                p1 = p0 + 15 * (long long)pitch;
+            } else {
+                p0 = row_of(rr0) + xs;
+                p1 = row_of(min(rr0 + 15, FB_TH + 7)) + xs;
+            }
+            __builtin_memcpy(&v0, p0, 8);
+            if (two) __builtin_memcpy(&v1, p1, 8);
             *(uint2 *)&tin[rr0 * FB_LD + 2 * jj] = v0;
             if (two) *(uint2 *)&tin[(rr0 + 15) * FB_LD + 2 * jj] = v1;
         } else {
@@ -2196,6 +2206,7 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         g.blur_tile_base[0] = 0;
         for (int l = 0; l < L; l++) {
             g.blur_tiles_x[l] = (g.lw[l] + FB_TW - 1) / FB_TW;
+            g.blur_tx_rcp[l] = (unsigned)(((1ull << 31) + g.blur_tiles_x[l] - 1) / g.blur_tiles_x[l]);
             g.blur_tiles_y[l] = (g.lh[l] + FB_TH - 1) / FB_TH;
             g.blur_tile_base[l + 1] = g.blur_tile_base[l] + g.blur_tiles_x[l] * g.blur_tiles_y[l];
         }
