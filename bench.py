@@ -915,9 +915,94 @@ DIST_BACKEND = os.environ.get("ORBSLAM_DIST_BACKEND", "nccl")
 COLL_DEV = "cuda" if DIST_BACKEND == "nccl" else "cpu"
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n: int, argv, timeout_s: float, script=None) -> int:
+    """`bench.py --gpus N` started as a plain process (no WORLD_SIZE in the environment): start
+    `python -m torch.distributed.run --nproc-per-node N` over this script as a CHILD process, one
+    rank per GPU. This process never touches the GPU (no torch import, no HIP call)
+    and never execs: it relays the ranks' stderr as it comes, rank 0's JSON line on stdout, and
+    returns non-zero when any rank fails (torchrun's exit status), when no JSON line arrives, or
+    when the job outlives `timeout_s` (the whole process group is then killed, status 124)."""
+    import signal
+    import subprocess
+    import threading
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           str(script or Path(__file__).resolve()), *argv]
+    env = dict(os.environ, ORBSLAM_BENCH_LAUNCH="self", MASTER_ADDR="127.0.0.1")
+    log(f"bench.py: self-launching {n} ranks: {' '.join(cmd)}")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, start_new_session=True)
+    lines = []
+
+    def pump():
+        for ln in p.stdout:
+            lines.append(ln.rstrip("\n"))
+            if not ln.startswith("{"):
+                sys.stderr.write(ln)   # the ranks' own stdout chatter goes to stderr: stdout is the line
+                sys.stderr.flush()
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    try:
+        rc = p.wait(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        log(f"bench.py: ranks still running after {timeout_s:.0f} s: killing the process group")
+        for sig, grace in ((signal.SIGTERM, 15), (signal.SIGKILL, 15)):
+            try:
+                os.killpg(p.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                p.wait(timeout=grace)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        th.join(timeout=5)
+        return 124
+    th.join(timeout=30)
+    if rc != 0:
+        log(f"bench.py: torch.distributed.run exited with status {rc} (a rank failed)")
+        return rc
+    for ln in reversed(lines):
+        if ln.startswith("{"):
+            try:
+                doc = json.loads(ln)
+            except ValueError:
+                continue
+            if "metric" in doc:
+                print(json.dumps(doc), flush=True)
+                return 0
+    log("bench.py: the ranks exited 0 but rank 0 printed no JSON line")
+    return 1
+
+
+def rank_topology(dist, device):
+    """This rank's (rank, local rank, device, PCI bus) for `config`; every rank's when distributed."""
+    import torch
+    me = {"rank": int(os.environ.get("RANK", "0")), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+          "device": int(device)}
+    try:
+        pr = torch.cuda.get_device_properties(device)
+        me["pci_bus_id"] = f"{getattr(pr, 'pci_domain_id', 0):04x}:{getattr(pr, 'pci_bus_id', 0):02x}:" \
+                           f"{getattr(pr, 'pci_device_id', 0):02x}"
+        me["name"] = pr.name
+    except Exception:   # informational only
+        pass
+    return gather_ranks(me, dist)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU). Without WORLD_SIZE in the environment and N > 1, bench.py "
+                         "starts torch.distributed.run with N ranks as a child process and relays rank 0's line")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="self-launch: seconds before the ranks' process group is killed (status 124)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=384, help="stereo frames per step")
@@ -971,12 +1056,26 @@ def main():
     ap.add_argument("--no-c2", action="store_true", help="skip the headline leg (profiling the other legs)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:   # before anything touches the GPU: the ranks are child processes
+            sys.exit(self_launch(args.gpus, sys.argv[1:], args.launch_timeout))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        ap.error(f"WORLD_SIZE={os.environ['WORLD_SIZE']} (launcher) but --gpus {args.gpus}: refusing to run a "
+                 f"world size the caller did not ask for")
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
-    device = local_rank % max(torch.cuda.device_count(), 1)   # one GPU per rank (wraps only in rehearsals)
+    ndev = torch.cuda.device_count()
+    if world > 1 and DIST_BACKEND == "nccl" and ndev < int(os.environ.get("LOCAL_WORLD_SIZE", world)):
+        raise SystemExit(f"bench.py: {os.environ.get('LOCAL_WORLD_SIZE', world)} ranks on this node but {ndev} "
+                         f"visible GPUs: RCCL needs one GPU per rank (ORBSLAM_DIST_BACKEND=gloo rehearses several "
+                         f"ranks on one GPU)")
+    device = local_rank % max(ndev, 1)   # one GPU per rank (wraps only in gloo rehearsals)
     torch.cuda.set_device(device)
     torch.cuda.init()
     dist = None
@@ -995,13 +1094,21 @@ def main():
     nf, sf, nl, ith, mth, bf, fx, w, h = odist.broadcast_shared(
         [NFEAT, 1.2, 8, 20, 7, KITTI_BF, KITTI_FX, W, H] if rank == 0 else [0] * 9, COLL_DEV, dist)
     mb = float(np.float32(bf) / np.float32(fx))
+    topo = rank_topology(dist, device)
 
     pool = make_pool(args.pool, rank, world)
     if args.no_c2:   # profiling of the other legs only (e.g. the C3 rocprofv3 summary): no headline value
         out = {"metric": "frames/sec ORB extract+match @1241x376 (1 GPU) + LocalBA keyframes/sec", "value": None,
-               "unit": "stereo frames/s", "n_gpus": world, "note": "--no-c2: headline leg skipped"}
+               "unit": "stereo frames/s", "n_gpus": world, "note": "--no-c2: headline leg skipped", "config": {}}
     else:
         out = bench_c2(amd, args, dist, world, (nf, sf, nl, ith, mth, bf, mb), pool)
+    out["config"].update({
+        "world_size": dist.get_world_size() if dist is not None else 1,
+        "dist_backend": (("rccl (torch nccl)" if DIST_BACKEND == "nccl" else DIST_BACKEND) if dist is not None
+                         else None),
+        "launch": ("bench.py self-launch (torch.distributed.run child)" if os.environ.get("ORBSLAM_BENCH_LAUNCH") == "self"
+                   else "external torch.distributed.run" if world > 1 else "single process"),
+        "rank_devices": topo})
     if not args.no_e2e and not args.no_c2:
         out.update(bench_e2e(amd, args, pool, bf, mb))
     if not args.no_latency and rank == 0:

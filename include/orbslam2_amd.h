@@ -619,7 +619,8 @@ typedef struct {
     double chi2[2];              /* active robust chi2 after each phase */
     int32_t stopped;             /* 2 = *stop set before optimising: early return, outputs =
                                     inputs, nothing to write back (Optimizer.cc:902-904);
-                                    1 = set after phase 1: phase 2 skipped (:913-917) */
+                                    1 = raised during the optimisation: phase 2 skipped (:913-917)
+                                    or cut short; 0 = both phases ran to their own end */
     int32_t trials[2];           /* LM trials (solve + update + chi2 evaluations) per phase */
 } lba_result;
 
@@ -629,11 +630,24 @@ typedef struct lba_engine lba_engine;
  * Optimizer.cc:646-1049) minus the map walk / write-back, which stay in the caller's
  * adapter: two Levenberg-Marquardt runs (5 iterations with Huber kernels, then 10 without
  * the outliers, optimization_algorithm_levenberg.cpp:61-164) with the Schur complement onto
- * the poses (block_solver.hpp:354-486) on the GPU. `stop` is pbStopFlag itself (a C++ bool, read as one byte): polled
- * before each LM iteration and trial (sparse_optimizer.cpp:376, levenberg.cpp:149). */
+ * the poses (block_solver.hpp:354-486) on the GPU. `stop` is pbStopFlag itself (a C++ bool, read
+ * as one byte; NULL = none), with the reference's semantics: checked before optimising
+ * (Optimizer.cc:902-904) and between the phases (:913-917) on the host, and inside each
+ * optimize() where g2o checks SparseOptimizer::terminate() -- after every rejected LM trial
+ * (optimization_algorithm_levenberg.cpp:149) and before every iteration (sparse_optimizer.cpp:376)
+ * -- by the device itself: while the call runs, the host copies *stop into a page-locked,
+ * device-mapped word that the LM decision kernel reads with a system-scope load, so a flag raised
+ * by another thread mid-call ends the optimisation after the trial in flight. With a non-NULL
+ * `stop` the call polls its stream instead of blocking in hipStreamSynchronize. */
 int lba_create(lba_engine **out);
 void lba_destroy(lba_engine *e);
 int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile uint8_t *stop);
+/* Test hook (no reference counterpart): every later lba_solve on `e` behaves as if pbStopFlag were
+ * raised the moment trial `trial` (1-based; 0 = before the first iteration) of optimize() call
+ * `phase` (1 = optimize(5), 2 = optimize(10)) has completed, and stayed raised. phase 0 removes
+ * the hook. The CPU oracle has the same hook (lba_oracle_solve_hook), so a stop at any (phase,
+ * trial) is parity-tested deterministically. */
+int lba_set_stop_hook(lba_engine *e, int phase, int trial);
 /* Per-kernel hipEvent timing of lba_solve's trial chain on the engine stream (bench.py localba
  * roofline); same semantics as orbx_profile / orbx_profile_read. */
 int lba_profile(lba_engine *e, int enable);

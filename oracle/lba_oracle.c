@@ -177,9 +177,22 @@ typedef struct {
     int *pose_hidx, *point_hidx; /* -1 if not in index mapping */
     int *hpose, *hpoint;  /* hessian index -> vertex */
     const volatile uint8_t *stop;
+    /* deterministic stand-in for pbStopFlag (test hook): the flag is raised the moment trial
+     * `hook_trial` of optimize() call `hook_phase` (1 or 2) has completed, and stays raised;
+     * hook_trial = 0 raises it before that call's first iteration */
+    int hook_phase, hook_trial, phase, trials;
+    int seen;   /* a terminate() check of the current optimize() call found the flag raised */
 } graph_t;
 
-static int terminate_flag(const graph_t *g) { return g->stop ? (*g->stop != 0) : 0; }
+static int hook_raised(const graph_t *g) {
+    return g->hook_phase > 0 && (g->phase > g->hook_phase || (g->phase == g->hook_phase && g->trials >= g->hook_trial));
+}
+/* SparseOptimizer::terminate() (sparse_optimizer.h: *_forceStopFlag) */
+static int terminate_flag(graph_t *g) {
+    const int t = (g->stop ? (*g->stop != 0) : 0) || hook_raised(g);
+    if (t) g->seen = 1;
+    return t;
+}
 
 /* EdgeSE3ProjectXYZ::computeError / EdgeStereoSE3ProjectXYZ::computeError */
 static void edge_error(const graph_t *g, edge_t *e) {
@@ -524,8 +537,9 @@ static int optimize(graph_t *g, int iterations, double *final_chi) {
     se3 *saveT = (se3 *)malloc(sizeof(se3) * (g->np + 1));
     double (*saveX)[3] = (double (*)[3])malloc(sizeof(double) * 3 * (g->nq + 1));
     double lambda = 0, ni = 2;
-    int nBad = 0, it = 0;
-    for (int i = 0; i < iterations && !terminate_flag(g); i++) {
+    int nBad = 0, it = 0, result_ok = 1;
+    /* sparse_optimizer.cpp:376: terminate() is evaluated before `ok`, after every iteration */
+    for (int i = 0; i < iterations && !terminate_flag(g) && result_ok; i++) {
         compute_active_errors(g);
         double currentChi = active_robust_chi2(g), iniChi = currentChi, tempChi;
         build_system(g, &S);
@@ -561,16 +575,15 @@ static int optimize(graph_t *g, int iterations, double *final_chi) {
                 memcpy(g->X, saveX, sizeof(double) * 3 * g->nq);
             }
             qmax++;
+            g->trials++;
         } while (rho < 0 && qmax < 10 && !terminate_flag(g));
         it++;
         *final_chi = currentChi;
-        int result_ok = 1;
         if (qmax == 10 || rho == 0) result_ok = 0;
         else {
             if ((iniChi - currentChi) * 1e3 < iniChi) nBad++; else nBad = 0;
             if (nBad >= 3) result_ok = 0;
         }
-        if (!result_ok) break;
     }
     free(S.Hpp); free(S.Hll); free(S.Hpl); free(S.b); free(S.x); free(S.diag_backup_p); free(S.diag_backup_l);
     free(saveT); free(saveX);
@@ -583,9 +596,14 @@ static int depth_positive(const graph_t *g, const edge_t *e) {
     return p[2] > 0.0;
 }
 
-int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint8_t *stop) {
+/* hook_phase / hook_trial: see graph_t (0 = no hook); the live `stop` flag is read as the
+ * reference reads pbStopFlag (Optimizer.cc:902-917, sparse_optimizer.cpp:376, levenberg.cpp:149) */
+int lba_oracle_solve_hook(const lba_problem *pr, lba_result *res, const volatile uint8_t *stop, int hook_phase,
+                          int hook_trial) {
     graph_t g;
     memset(&g, 0, sizeof(g));
+    g.hook_phase = hook_phase;
+    g.hook_trial = hook_trial;
     g.np = pr->n_poses; g.nq = pr->n_points; g.ne = pr->n_edges;
     g.fixed = pr->pose_fixed; g.pose_id = pr->pose_id; g.point_id = pr->point_id;
     g.stop = stop;
@@ -625,7 +643,7 @@ int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint
     res->iterations[0] = res->iterations[1] = 0;
     res->chi2[0] = res->chi2[1] = 0;
     res->stopped = 0;
-    res->trials[0] = res->trials[1] = 0;   /* not counted by the oracle */
+    res->trials[0] = res->trials[1] = 0;
     int rc = 0;
     if (stop && *stop) {                  /* Optimizer.cc:902-904: return before optimising */
         res->stopped = 2;
@@ -636,8 +654,12 @@ int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint
         return rc;
     } else {
         initialize(&g, 0);
+        g.phase = 1;
+        g.trials = 0;
+        g.seen = 0;
         res->iterations[0] = optimize(&g, 5, &res->chi2[0]);
-        int bDoMore = !(stop && *stop);
+        res->trials[0] = g.trials;
+        int bDoMore = !terminate_flag(&g);   /* if(pbStopFlag) if(*pbStopFlag) bDoMore = false */
         if (bDoMore) {
             for (int k = 0; k < g.ne; k++) {   /* :925-962 (stale _error) */
                 edge_t *e = &g.E[k];
@@ -646,7 +668,12 @@ int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint
                 e->robust = 0;
             }
             initialize(&g, 0);
+            g.phase = 2;
+            g.trials = 0;
+            g.seen = 0;
             res->iterations[1] = optimize(&g, 10, &res->chi2[1]);
+            res->trials[1] = g.trials;
+            if (g.seen) res->stopped = 1;   /* phase 2 cut short by the flag */
         } else {
             res->stopped = 1;
         }
@@ -670,6 +697,10 @@ int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint
         for (int j = 0; j < 3; j++) res->point_Xw[3 * i + j] = (float)g.X[i][j];
     free(g.T); free(g.X); free(g.E); free(g.pose_hidx); free(g.point_hidx); free(g.hpose); free(g.hpoint);
     return rc;
+}
+
+int lba_oracle_solve(const lba_problem *pr, lba_result *res, const volatile uint8_t *stop) {
+    return lba_oracle_solve_hook(pr, res, stop, 0, 0);
 }
 
 /* ==========================================================================================

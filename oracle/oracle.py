@@ -365,17 +365,21 @@ def lba_chol_stats(reset: bool = False) -> dict:
     return {"schur_solves": int(a[0]), "nonpositive_pivot": int(a[1]), "min_pivot_ratio": r.value}
 
 
-def lba_solve(prob: dict, stop: bool = False):
-    """Optimizer::LocalBundleAdjustment optimisation core on the CPU (double precision)."""
+def lba_solve(prob: dict, stop: bool = False, hook=None):
+    """Optimizer::LocalBundleAdjustment optimisation core on the CPU (double precision).
+    hook = (phase, trial): pbStopFlag raised after LM trial `trial` of optimize() call `phase`
+    (lba_oracle_solve_hook; the GPU's lba_set_stop_hook)."""
     L = lib()
-    L.lba_oracle_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.lba_oracle_solve_hook.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
     P, keep = make_lba_structs(prob)
     R, out = make_lba_result(prob)
     flag = C.c_uint8(1 if stop else 0)
-    L.lba_oracle_solve(C.byref(P), C.byref(R), C.byref(flag))
+    hp, ht = hook if hook else (0, 0)
+    L.lba_oracle_solve_hook(C.byref(P), C.byref(R), C.byref(flag), int(hp), int(ht))
     out["iterations"] = tuple(R.iterations)
     out["chi2"] = tuple(R.chi2)
     out["stopped"] = R.stopped
+    out["trials"] = tuple(R.trials)
     return out
 
 

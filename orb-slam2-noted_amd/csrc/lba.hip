@@ -41,9 +41,11 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
+#include <climits>
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "orb_engine.h"
@@ -72,7 +74,10 @@ constexpr int kRedBlocks = 16384;    // partial-sum region stride (blocks) for s
 struct LMState {
     double lambda, ni, currentChi, iniChi, rho, final_chi;
     int qmax, nBad, it, iterations, done, newiter, accepted, trials;   // trials: LM trials decided
-    int cur, pad;   // estimate buffers: cur = 0 -> (T, X) current, (T2, X2) trial; 1 -> swapped
+    int cur;        // estimate buffers: cur = 0 -> (T, X) current, (T2, X2) trial; 1 -> swapped
+    int stop_at;    // test hook: pbStopFlag counts as raised once `trials` reaches it (INT_MAX: never)
+    int seen;       // a terminate() check of this optimize() found pbStopFlag raised
+    int pad;
 };
 
 struct EdgeDev {
@@ -122,6 +127,7 @@ struct Graph {
                            // maxDiagonal | pose maxDiagonal | robust chi2 block sums of set 1
     double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok, lambda
     LMState *lm;
+    const unsigned *stopf; // pbStopFlag mirrored by lba_solve's host loop into page-locked, device-mapped memory
     unsigned *arrive;      // lba_errors block-arrival counter (the last block runs the LM decision)
     int Kpad;              // Y^T rows 3 Lm rounded up to 4; row Kpad (and up to Kpad + 3) is zero
     int NP;                // Schur dimension 6P padded to a multiple of kCB
@@ -1263,14 +1269,23 @@ __global__ __launch_bounds__(256) void lba_errors(Graph g, double *part, int nbu
     lm_decide(g, nbu, nbe, np, nq, 256);
 }
 
-// SparseOptimizer::optimize(iterations) start: lambda / nu / nBad reset (levenberg.cpp:66-72)
-__global__ void lba_lm_init(Graph g, int iterations) {
+// SparseOptimizer::terminate(): *_forceStopFlag (sparse_optimizer.h), read live from the mapped word
+// the host keeps equal to the caller's pbStopFlag, or the deterministic test hook
+__device__ inline bool stop_raised(const Graph &g, const LMState &s) {
+    return __hip_atomic_load(g.stopf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u || s.trials >= s.stop_at;
+}
+
+// SparseOptimizer::optimize(iterations) start: lambda / nu / nBad reset (levenberg.cpp:66-72), and
+// the loop's first `i < iterations && !terminate()` check (sparse_optimizer.cpp:376)
+__global__ void lba_lm_init(Graph g, int iterations, int stop_at) {
     LMState s{};
     s.cur = g.lm->cur;   // which buffer holds the estimate carries over between optimize() calls
     s.ni = 2;
     s.iterations = iterations;
     s.newiter = 1;
+    s.stop_at = stop_at;
     s.done = iterations <= 0;
+    if (!s.done && stop_raised(g, s)) s.seen = s.done = 1;
     *g.lm = s;
 }
 
@@ -1324,7 +1339,16 @@ __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthrea
         s.trials++;
         s.rho = rho;
         s.accepted = a;
+        // pbStopFlag, read where g2o reads it: the trial loop's `rho < 0 && qmax < max &&
+        // !terminate()` (levenberg.cpp:149, evaluated only after a rejected trial) and the iteration
+        // loop's `i < iterations && !terminate() && ok` (sparse_optimizer.cpp:376, before `ok`)
+        const bool raised = stop_raised(g, s);
+        bool retry = false;
         if (rho < 0 && s.qmax < 10) {
+            if (raised) s.seen = 1;
+            else retry = true;
+        }
+        if (retry) {
             s.newiter = 0;                     // retry the same linearisation
         } else {
             s.it++;
@@ -1337,7 +1361,9 @@ __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthrea
             }
             s.newiter = 1;
             s.qmax = 0;
-            if (!ok || s.it >= s.iterations) s.done = 1;
+            bool term = false;
+            if (s.it < s.iterations && raised) term = s.seen = 1;
+            if (!ok || s.it >= s.iterations || term) s.done = 1;
         }
         if (a) s.cur ^= 1;   // the trial buffers become the current estimate (no copy)
         *g.lm = s;
@@ -1447,6 +1473,12 @@ struct lba_engine {
     size_t h_stage_bytes = 0;
     void *h_down = nullptr;       // pinned download staging of the results (grow-only)
     size_t h_down_bytes = 0;
+    // pbStopFlag as the device sees it: a page-locked, device-mapped, coherent word the host loop
+    // keeps equal to the caller's flag while a chunk of trials runs (lba_optimize)
+    unsigned *h_stop = nullptr;
+    unsigned *d_stop = nullptr;
+    hipEvent_t ev_chunk = nullptr;
+    int hook_phase = 0, hook_trial = 0;   // lba_set_stop_hook
     // per-kernel hipEvent timing on the engine stream (lba_profile; bench.py localba roofline)
     bool prof = false;
     struct ProfRec { const char *name; hipEvent_t a, b; };
@@ -1696,11 +1728,18 @@ int nblk(int n) { return std::max(1, (n + 255) / 256); }
 // One SparseOptimizer::optimize(iterations) on the device; returns iterations run.
 // Trial slots (linearisation + setLambda/Schur/solve/update/errors + lba_decide) are enqueued
 // in chunks without host synchronisation; the device LM state turns the slots after the
-// last trial into no-ops. One state readback per chunk (the stop flag is polled there).
+// last trial into no-ops. One state readback per chunk. pbStopFlag is read by the device itself,
+// at every point where g2o reads it (lba_lm_init, lm_decide): while a chunk runs, the host loop
+// copies *stop into the mapped word the kernels load with system scope, so a flag raised mid-call
+// ends the optimisation after the trial in flight, as SparseOptimizer::terminate() does.
+// stop_at: the test hook's trial count for this optimize() (INT_MAX: none).
 static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterations, int np, int nq,
-                        const volatile uint8_t *stop, double *final_chi, int *trials, int *cur) {
+                        const volatile uint8_t *stop, int stop_at, double *final_chi, int *trials, int *cur,
+                        int *seen) {
     hipStream_t s = e->stream;
-    auto term = [&]() { return stop && *stop; };
+    auto mirror = [&]() {
+        if (stop) __atomic_store_n(e->h_stop, (unsigned)(*stop != 0), __ATOMIC_RELAXED);
+    };
     if (A.P + A.Lm == 0) return -1;
     if (A.P > kMaxPoses) return -2;
     if (((int)A.act.size() + kLinEdges - 1) / kLinEdges > kRedBlocks || (A.Lm + kRPL - 1) / kRPL > kRedBlocks)
@@ -1759,7 +1798,8 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
         if (LBA_SEP_DECIDE) lba_decide<<<1, 64, 0, s>>>(g, nbu, nbe, np, nq);
         lprof_end(e, ph, "lba_errors_decide");
     };
-    lba_lm_init<<<1, 1, 0, s>>>(g, iterations);
+    mirror();
+    lba_lm_init<<<1, 1, 0, s>>>(g, iterations, stop_at);
     // first chunk: one trial per iteration (the common case: every first trial accepted); then
     // two slots per chunk while retries remain
     int chunk = iterations, slots = 0;
@@ -1767,21 +1807,28 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
     while (true) {
         for (int k = 0; k < chunk; k++) slot(slots + k == 0);
         slots += chunk;
-        if (hipMemcpyAsync(e->h_lm, g.lm, sizeof(LMState), hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return -3;
+        if (hipMemcpyAsync(e->h_lm, g.lm, sizeof(LMState), hipMemcpyDeviceToHost, s) != hipSuccess) return -3;
+        if (!stop) {
+            if (hipStreamSynchronize(s) != hipSuccess) return -3;
+        } else {   // poll the chunk, keeping the device's copy of the flag current
+            if (hipEventRecord(e->ev_chunk, s) != hipSuccess) return -3;
+            while (true) {
+                mirror();
+                const hipError_t q = hipEventQuery(e->ev_chunk);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) return -3;
+                std::this_thread::yield();
+            }
+        }
         st = *e->h_lm;
         if (st.done) break;
-        if (term()) {   // stop flag: the trial loop and the iteration loop end here
-            if (!st.newiter) { st.it++; st.final_chi = st.currentChi; }
-            break;
-        }
         if (slots > 10 * iterations + 1) return -3;   // cannot happen: <= 10 trials per iteration
         chunk = 2;
     }
     *final_chi = st.final_chi;
     *trials = st.trials;
     *cur = st.cur;
+    *seen = st.seen;
     return st.it;
 }
 
@@ -1794,7 +1841,10 @@ int lba_create(lba_engine **out) {
     lba_engine *e = new lba_engine();
     if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void **)&e->h_scalars, (8 + 2 * kRedBlocks) * sizeof(double)) != hipSuccess ||
-        hipHostMalloc((void **)&e->h_lm, sizeof(LMState)) != hipSuccess) {
+        hipHostMalloc((void **)&e->h_lm, sizeof(LMState)) != hipSuccess ||
+        hipHostMalloc((void **)&e->h_stop, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&e->d_stop, e->h_stop, 0) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_chunk, hipEventDisableTiming) != hipSuccess) {
         delete e;
         return ORBX_EDEVICE;
     }
@@ -1808,6 +1858,8 @@ void lba_destroy(lba_engine *e) {
     if (e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
     if (e->h_scalars) (void)hipHostFree(e->h_scalars);
     if (e->h_lm) (void)hipHostFree(e->h_lm);
+    if (e->h_stop) (void)hipHostFree(e->h_stop);
+    if (e->ev_chunk) (void)hipEventDestroy(e->ev_chunk);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_down) (void)hipHostFree(e->h_down);
     for (hipEvent_t ev : e->pool) (void)hipEventDestroy(ev);
@@ -1884,7 +1936,9 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     LBA_CHK(hipMemsetAsync(e->arrive.p, 0, 64, s));
     LBA_CHK(hipMemsetAsync(e->lm.p, 0, sizeof(LMState), s));   // cur = 0: (T, X) hold the estimate
     int cur = 0;
+    *e->h_stop = 0u;
     Graph g{};
+    g.stopf = e->d_stop;
     g.T = at<Pose>(e->arenaA, oT); g.T2 = at<Pose>(e->arenaA, oT2);
     g.X = at<double>(e->arenaA, oX); g.X2 = at<double>(e->arenaA, oX2);
     if (ne > 0)
@@ -1979,20 +2033,25 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     hp.mark("setup1");
     // lba_optimize: >= 0 iterations, -1 = the pre-LM error evaluation failed (g2o's optimize()
     // returning -1, a valid outcome), -3 = HIP runtime error
-    r->iterations[0] = lba_optimize(e, g, A, 5, np, nq, stop, &r->chi2[0], &r->trials[0], &cur);
+    int seen = 0;
+    const int hook1 = e->hook_phase == 1 ? e->hook_trial : INT_MAX, hook2 = e->hook_phase == 2 ? e->hook_trial : INT_MAX;
+    r->iterations[0] = lba_optimize(e, g, A, 5, np, nq, stop, hook1, &r->chi2[0], &r->trials[0], &cur, &seen);
     if (r->iterations[0] == -3) return ORBX_EDEVICE;
     if (r->iterations[0] < -1) return ORBX_EINVAL;
     hp.mark("opt1");
-    const bool bDoMore = !(stop && *stop);
+    // if(pbStopFlag) if(*pbStopFlag) bDoMore = false (Optimizer.cc:913-917); the hook's flag stays
+    // raised once its trial has run
+    const bool bDoMore = !(stop && *stop) && !(e->hook_phase == 1 && r->trials[0] >= e->hook_trial);
     if (bDoMore) {
         // phase 1 ran with every edge at level 0 (its slots are all edges): the level-1 moves and
         // the robust-kernel drop stay on the device, no host round trip between the optimizations
         lba_phase2_mark<<<nblk(std::max(ne, (int)A.act.size())), 256, 0, s>>>(g, const_cast<EdgeDev *>(g.E),
                                                                               e->on.as<uint8_t>(), ne);
         LBA_CHK(hipGetLastError());
-        r->iterations[1] = lba_optimize(e, g, A, 10, np, nq, stop, &r->chi2[1], &r->trials[1], &cur);
+        r->iterations[1] = lba_optimize(e, g, A, 10, np, nq, stop, hook2, &r->chi2[1], &r->trials[1], &cur, &seen);
         if (r->iterations[1] == -3) return ORBX_EDEVICE;
         if (r->iterations[1] < -1) return ORBX_EINVAL;
+        if (seen) r->stopped = 1;   // phase 2 cut short by the flag
         hp.mark("opt2");
     } else {
         r->stopped = 1;
@@ -2030,6 +2089,13 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     }
     for (int i = 0; i < 3 * nq; i++) r->point_Xw[i] = (float)X[i];
     hp.mark("convert");
+    return ORBX_OK;
+}
+
+int lba_set_stop_hook(lba_engine *e, int phase, int trial) {
+    if (!e || phase < 0 || phase > 2 || trial < 0) return ORBX_EINVAL;
+    e->hook_phase = phase;
+    e->hook_trial = trial;
     return ORBX_OK;
 }
 

@@ -19,8 +19,24 @@ namespace orbamd {
 // launched twice per batch (1 resize chain, 2 quadtree, 4 describe, 8 stereo_match_left); the
 // step time difference against 0 is that kernel's marginal cost inside the pipeline. 0 (unset)
 // in every product run.
+// Experiment knobs (tools/gpu_*.sh) are read from the environment only by `make variant`
+// builds (-DORBX_EXPERIMENTS=1, a build id of their own): the product library ignores them, so a
+// stray variable cannot change its results or its speed.
+#ifndef ORBX_EXPERIMENTS
+#define ORBX_EXPERIMENTS 0
+#endif
+inline int orbx_knob(const char *name, int dflt) {
+#if ORBX_EXPERIMENTS
+    const char *ev = std::getenv(name);
+    return ev ? std::atoi(ev) : dflt;
+#else
+    (void)name;
+    return dflt;
+#endif
+}
+
 inline int exp_twice() {
-    static const int v = [] { const char *ev = std::getenv("ORBX_EXP_TWICE"); return ev ? std::atoi(ev) : 0; }();
+    static const int v = orbx_knob("ORBX_EXP_TWICE", 0);
     return v;
 }
 

@@ -681,8 +681,14 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             int h0 = 0;
             if (lane == 0) h0 = atomicAdd(&hcnt_sh, na + __popcll(bb));
             h0 = __builtin_amdgcn_readfirstlane(h0);
-            if (ha) hlist[h0 + (int)lane_rank(ba)] = (uint16_t)pa;
-            if (hb) hlist[h0 + na + (int)lane_rank(bb)] = (uint16_t)pb;
+            // Invariant: a tile pixel is pushed at most once -- only a pixel's nonzero-scoring
+            // polarity can be hot (step 3's comment; tlo >= 0), and a pixel has one entry per
+            // polarity -- so hcnt_sh <= FB_TW * FB_TH. The bound check keeps a future change to the
+            // pre-filter or the threshold clamp from writing past hlist silently (LDS writes out of
+            // range do not fault); step 5 reads min(hcnt_sh, capacity) entries.
+            const int ia = h0 + (int)lane_rank(ba), ib = h0 + na + (int)lane_rank(bb);
+            if (ha && ia < FB_TW * FB_TH) hlist[ia] = (uint16_t)pa;
+            if (hb && ib < FB_TW * FB_TH) hlist[ib] = (uint16_t)pb;
         };
         // a dummy position for idle halves: a tile pixel whose ring stays inside the staged rows
         constexpr int kIdle = 4;
@@ -710,7 +716,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     // 5. 3x3 NMS of the hot pixels at tlo against their in-cell neighbours (others score 0),
     // survivors appended to their cell's slot list
     {
-        const int htot = hcnt_sh;
+        const int htot = min(hcnt_sh, FB_TW * FB_TH);
         const uint8_t *m8 = (const uint8_t *)mt;
         const int hC = g.hcell[l], wC = g.wcell[l];
         const int ry_end = g.maxBY[l] - 3, rx_end = g.maxBX[l] - 3;
@@ -2153,10 +2159,10 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         // (5 per CU) 0.52 ms, 32 KB (4 per CU) 0.57 ms, 16 KB 0.59 ms. ORBX_QT_NODES_LDS=1 /
         // ORBX_QT_LDS_KB=<k> are tuning knobs.
         g.qt_nodes_in_lds = 0;
-        if (const char *ev = std::getenv("ORBX_QT_NODES_LDS")) g.qt_nodes_in_lds = std::atoi(ev) != 0 && node_bytes <= 48 * 1024;
+        g.qt_nodes_in_lds = orbx_knob("ORBX_QT_NODES_LDS", 0) != 0 && node_bytes <= 48 * 1024;
         g.qt_node_stride = (long long)((node_bytes + 15) / 16) * 4;
         long long qt_lds = 28 * 1024;
-        if (const char *ev = std::getenv("ORBX_QT_LDS_KB")) qt_lds = std::max(16, std::min(160, std::atoi(ev))) * 1024LL;
+        qt_lds = std::max(16, std::min(160, orbx_knob("ORBX_QT_LDS_KB", 28))) * 1024LL;
         const long long kl_bytes = qt_lds - (long long)sizeof(QShared) - 256 -
                                    (g.qt_nodes_in_lds ? (long long)node_bytes : 0);
         g.qt_kl = (int)std::max<long long>(256, (kl_bytes / 12) & ~63LL);
@@ -2286,7 +2292,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
         e->d_qt_nodes.as<unsigned char>(), e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>());
     prof_end(e, s, ph, "quadtree_kernel");
     ph = prof_begin(e, s);
-    static const int desc_r = [] { const char *ev = std::getenv("ORBX_DESC_R"); return ev ? std::atoi(ev) : 3; }();  // tuning knob: 2 0.92 ms, 3 0.88, 4 0.97, 6 1.18 per 256 pairs
+    static const int desc_r = orbx_knob("ORBX_DESC_R", 3);  // tuning knob: 2 0.92 ms, 3 0.88, 4 0.97, 6 1.18 per 256 pairs
     const dim3 dg4((cap + 15) / 16, n), dg3((cap + 11) / 12, n), dg2((cap + 7) / 8, n), dg6((cap + 23) / 24, n);
     uint8_t *d_blur = e->d_blur.as<uint8_t>();
     const uint32_t *d_sel = e->d_sel.as<uint32_t>();
@@ -2296,7 +2302,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     int *d_cnt = e->d_cnt.as<int>();
     // describe2_kernel<NS, G> (default 8 slots per wavefront in groups of 2); ORBX_DESC_V=0 runs
     // describe_kernel<ORBX_DESC_R> instead
-    static const int desc_v = [] { const char *ev = std::getenv("ORBX_DESC_V"); return ev ? std::atoi(ev) : 82; }();
+    static const int desc_v = orbx_knob("ORBX_DESC_V", 82);
     for (int rep = 0; rep < ((exp_twice() & 4) ? 2 : 1); rep++)
     if (desc_v != 0) {
         switch (desc_v) {

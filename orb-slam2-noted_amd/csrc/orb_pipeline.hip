@@ -38,7 +38,8 @@ struct orbx_pipeline {
     void *slot_buf[2] = {nullptr, nullptr};
     size_t slot_bytes = 0;
     int next_slot = 0;
-    int slot_pairs[2] = {0, 0};          // pair count of the last batch uploaded into each slot
+    int slot_pairs[2] = {0, 0};          // chunk layout of the last batch uploaded into each slot:
+    size_t slot_stride[2] = {0, 0};      // pair count and image stride (they fix every chunk's byte range)
     std::vector<hipEvent_t> ev_h2d[2];   // chunk j of slot s uploaded
     std::vector<hipEvent_t> ev_free[2];  // engine j finished reading slot s (stereo done)
     std::vector<bool> free_rec[2];
@@ -77,7 +78,7 @@ static int pipeline_run(orbx_pipeline *pl, const uint8_t *d_imgs, int n_pairs, i
         // fast_blur then starts the moment that one ends (measured against ordering the whole
         // phase 1: 71.2-71.8k vs 68.1-69.6k stereo frames/s, and no pipeline phase that leaves
         // describe without a fast_blur to overlap)
-        static const bool whole_p1 = [] { const char *ev = std::getenv("ORBX_PIPE_ORDER_P1"); return ev && std::atoi(ev); }();
+        static const bool whole_p1 = orbamd::orbx_knob("ORBX_PIPE_ORDER_P1", 0) != 0;
         const bool gate = pl->last_p1 >= 0 && pl->last_p1 != j;
         if (gate && whole_p1 && hipStreamWaitEvent(s, pl->ev_p1[pl->last_p1], 0) != hipSuccess) return ORBX_EDEVICE;
         const uint8_t *src = d_imgs + (size_t)2 * pl->first[j] * image_stride;
@@ -123,7 +124,13 @@ static int pipeline_run(orbx_pipeline *pl, const uint8_t *d_imgs, int n_pairs, i
 
 extern "C" {
 
-const char *orbx_build_id(void) { return ORBX_SRC_HASH; }
+// the hash of the library's sources (tools/src_hash.py); a build with other compile settings than
+// the product's (EXTRA flags, `make variant` defines) carries a suffix naming them, so counters
+// measured on it never pass for the product's (bench.py load_pmc_doc, tools/stamp.py)
+#ifndef ORBX_BUILD_SUFFIX
+#define ORBX_BUILD_SUFFIX ""
+#endif
+const char *orbx_build_id(void) { return ORBX_SRC_HASH ORBX_BUILD_SUFFIX; }
 
 int orbx_pipeline_create(const orbx_params *p, int n_engines, orbx_pipeline **out) {
     if (!p || !out) return ORBX_EINVAL;
@@ -244,14 +251,16 @@ int orbx_pipeline_stereo_batch_host(orbx_pipeline *pl, const uint8_t *h_imgs, in
     pl->next_slot ^= 1;
     uint8_t *dev = (uint8_t *)pl->slot_buf[sl];
     // Chunk j's upload overwrites the range engine j read in this slot's previous batch. With the
-    // same pair count the chunk ranges coincide and waiting for engines 0..j suffices (the waits
-    // pile up on the H2D stream); with a different count chunk j can cover an old range of any
-    // engine, so the first upload waits for every engine's last read of the slot.
-    if (pl->slot_pairs[sl] != n_pairs) {
+    // same pair count and image stride the chunk byte ranges coincide and waiting for engines 0..j
+    // suffices (the waits pile up on the H2D stream); with a different count or stride chunk j can
+    // cover an old range of any engine, so the first upload waits for every engine's last read of
+    // the slot.
+    if (pl->slot_pairs[sl] != n_pairs || pl->slot_stride[sl] != image_stride) {
         for (int j = 0; j < k; j++)
             if (pl->free_rec[sl][j] && hipStreamWaitEvent(pl->h2d, pl->ev_free[sl][j], 0) != hipSuccess)
                 return ORBX_EDEVICE;
         pl->slot_pairs[sl] = n_pairs;
+        pl->slot_stride[sl] = image_stride;
     }
     for (int j = 0; j < k; j++) {
         const int first = (int)((long long)n_pairs * j / k), cnt = (int)((long long)n_pairs * (j + 1) / k) - first;

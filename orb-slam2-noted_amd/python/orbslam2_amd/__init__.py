@@ -99,6 +99,7 @@ SIGNATURES = [
     ("lba_create", _I, [C.POINTER(C.c_void_p)]),
     ("lba_destroy", None, [_P]),
     ("lba_solve", _I, [_P, _P, _P, _P]),
+    ("lba_set_stop_hook", _I, [_P, _I, _I]),
     ("orbx_profile_read", _I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     ("orbt_create", _I, [C.POINTER(C.c_void_p)]),
     ("orbt_destroy", None, [_P]),
@@ -701,7 +702,14 @@ class LocalBundleAdjustment:
         except Exception:
             pass
 
-    def solve(self, prob: dict, stop: bool = False) -> dict:
+    def set_stop_hook(self, phase: int = 0, trial: int = 0):
+        """lba_set_stop_hook: act as if pbStopFlag were raised after trial `trial` of optimize() call
+        `phase` (1 or 2; 0 removes the hook)."""
+        _check(lib().lba_set_stop_hook(self._h, int(phase), int(trial)), "lba_set_stop_hook")
+
+    def solve(self, prob: dict, stop=False) -> dict:
+        """`stop`: a bool (the flag's value for the whole call) or a ctypes.c_uint8 shared with
+        another thread that may raise it while the call runs (ctypes releases the GIL)."""
         keep = {k: np.ascontiguousarray(prob[k], _LBA_DTYPES[k]) for k in _LBA_FIELDS}
         P = LbaProblem(len(keep["pose_id"]), keep["pose_id"].ctypes.data, keep["pose_fixed"].ctypes.data,
                        keep["pose_Tcw"].ctypes.data, keep["pose_cam"].ctypes.data, len(keep["point_id"]),
@@ -712,7 +720,7 @@ class LocalBundleAdjustment:
                "point_Xw": np.zeros((len(keep["point_id"]), 3), np.float32),
                "edge_erase": np.zeros(len(keep["edge_point"]), np.uint8)}
         R = LbaResult(out["pose_Tcw"].ctypes.data, out["point_Xw"].ctypes.data, out["edge_erase"].ctypes.data)
-        flag = C.c_uint8(1 if stop else 0)
+        flag = stop if isinstance(stop, C.c_uint8) else C.c_uint8(1 if stop else 0)
         _check(lib().lba_solve(self._h, C.byref(P), C.byref(R), C.byref(flag)), "lba_solve")
         out["iterations"] = tuple(R.iterations)
         out["chi2"] = tuple(R.chi2)

@@ -1,13 +1,13 @@
 """C5 rehearsal: bench.py's multi-rank path at world size 2 on the one GPU of
-the box, launched as the driver launches it (torch.distributed.run, one process per rank), over
-gloo (ORBSLAM_DIST_BACKEND=gloo: ranks share the card, RCCL needs one GPU per rank). Each rank runs
+the box, launched by bench.py itself: `bench.py --gpus 2` without WORLD_SIZE starts
+torch.distributed.run with two ranks as a child process and relays rank 0's line,
+over gloo (ORBSLAM_DIST_BACKEND=gloo: ranks share the card, RCCL needs one GPU per rank). Each rank runs
 its own C2 stream (SURVEY §8d C5 seeds: rank r = seed 10 + r), receives the LocalBA map from rank 0
 by broadcast, and checks with --check-parity its whole last 384-pair batch bit-exact and its
 LocalBA on the broadcast map within 1e-4 (same LM iterations, same erase set) against the oracle.
 The multi-rank timing is a rehearsal, not a measurement (two ranks share one GPU)."""
 import json
 import os
-import socket
 import subprocess
 import sys
 from pathlib import Path
@@ -18,17 +18,11 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def test_c5_two_ranks_parity():
     env = dict(os.environ, ORBSLAM_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
-           "--gpus", "2", "--steps", "3", "--warmup", "1", "--check-parity", "--no-cpu-baseline", "--no-latency",
+    env = {k: v for k, v in env.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--launch-timeout", "220",
+           "--steps", "3", "--warmup", "1", "--check-parity", "--no-cpu-baseline", "--no-latency",
            "--no-e2e", "--no-rgbd", "--no-track", "--no-pose", "--no-bow", "--no-bowmatch", "--no-newpts",
            "--no-isolated", "--no-alt-resize", "--lba-steps", "2"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
@@ -39,6 +33,10 @@ def test_c5_two_ranks_parity():
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     print(json.dumps({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "parity_check")}))
     assert line["n_gpus"] == 2 and "C5" in line["config"]["streams"]
+    cfg = line["config"]
+    assert cfg["world_size"] == 2 and cfg["dist_backend"] == "gloo", cfg
+    assert cfg["launch"].startswith("bench.py self-launch"), cfg
+    assert [d["rank"] for d in cfg["rank_devices"]] == [0, 1], cfg
     c2 = line["parity_check"]["c2"]
     assert [p["rank"] for p in c2] == [0, 1]
     assert [p["left_seed_first_pair"] for p in c2] == [10, 11]

@@ -24,3 +24,37 @@ def test_lba_oracle_stop_flag(oracle_mod):
     r = oracle_mod.lba_solve(prob, stop=True)
     assert r["stopped"] == 2
     assert np.array_equal(r["pose_Tcw"], prob["pose_Tcw"].reshape(-1, 16))
+
+
+def _rejecting_problem(seed, sigma, n_kf=8, n_points=300):
+    """A C4-shaped graph whose points are scattered by `sigma` m: LM trials get rejected (rho < 0),
+    so the trial loop's terminate() check (levenberg.cpp:149) is reached."""
+    prob = synth.localba_problem(seed=seed, n_kf=n_kf, n_points=n_points)
+    rng = np.random.default_rng(seed)
+    prob["point_Xw"] = (prob["point_Xw"] + rng.normal(0, sigma, prob["point_Xw"].shape)).astype(np.float32)
+    return prob
+
+
+def test_lba_oracle_stop_hook_semantics(oracle_mod):
+    """The oracle's pbStopFlag hook (lba_oracle_solve_hook) against g2o's control flow
+    (sparse_optimizer.cpp:376, optimization_algorithm_levenberg.cpp:96-164, Optimizer.cc:902-917):
+    a flag raised after trial T of phase 1 ends phase 1 with the iteration holding trial T and skips
+    phase 2; raised in phase 2, it ends phase 2 the same way; a trial count the phase never reaches
+    changes nothing."""
+    prob = _rejecting_problem(61, 3.0)
+    full = oracle_mod.lba_solve(prob)
+    assert full["trials"][0] > full["iterations"][0], "the problem must reject a phase-1 trial"
+    assert oracle_mod.lba_solve(prob, hook=(2, 99))["pose_Tcw"].tobytes() == full["pose_Tcw"].tobytes()
+    r0 = oracle_mod.lba_solve(prob, hook=(1, 0))
+    assert r0["iterations"] == (0, 0) and r0["stopped"] == 1
+    rej = None
+    for T in range(1, full["trials"][0] + 1):
+        r = oracle_mod.lba_solve(prob, hook=(1, T))
+        assert r["trials"] == (T, 0) and r["stopped"] == 1 and r["iterations"][1] == 0
+        prev = oracle_mod.lba_solve(prob, hook=(1, T - 1))
+        if r["iterations"][0] == prev["iterations"][0] + 1 and r["chi2"][0] == prev["chi2"][0] and T > 1:
+            rej = T   # trial T was rejected and the flag ended its iteration there
+    assert rej is not None
+    for T in range(0, full["trials"][1]):
+        r = oracle_mod.lba_solve(prob, hook=(2, T))
+        assert r["trials"] == (full["trials"][0], T) and r["stopped"] == 1

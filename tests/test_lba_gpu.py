@@ -68,3 +68,74 @@ def test_golden_c4_on_device(amd):
     assert tuple(got["iterations"]) == tuple(g["iterations"])
     assert _rel(got["pose_Tcw"], g["pose_Tcw"]) < RTOL and _rel(got["point_Xw"], g["point_Xw"]) < RTOL
     assert np.array_equal(got["edge_erase"], g["edge_erase"])
+
+
+def _rejecting_problem(seed, sigma, n_kf=8, n_points=300):
+    from test_lba_cpu import _rejecting_problem as mk
+    return mk(seed, sigma, n_kf, n_points)
+
+
+def _same(got, ref, what):
+    assert got["iterations"] == ref["iterations"], (what, got["iterations"], ref["iterations"])
+    assert got["trials"] == ref["trials"], (what, got["trials"], ref["trials"])
+    assert got["stopped"] == ref["stopped"], (what, got["stopped"], ref["stopped"])
+    assert _rel(got["pose_Tcw"], ref["pose_Tcw"]) < RTOL, what
+    assert _rel(got["point_Xw"], ref["point_Xw"]) < RTOL, what
+    assert np.array_equal(got["edge_erase"], ref["edge_erase"]), what
+
+
+@pytest.mark.parametrize("case", ["c4", "reject1", "reject2"])
+def test_lba_stop_hook_every_trial(amd, oracle_mod, case):
+    """pbStopFlag raised after every LM trial of both phases: the device's LM
+    decision reads the flag where g2o does (levenberg.cpp:149 after a rejected trial,
+    sparse_optimizer.cpp:376 before each iteration) and the host skips phase 2 (Optimizer.cc:913-917).
+    `reject1` / `reject2` reject a trial in phase 1 / phase 2, so the trial-loop check is reached.
+    GPU == oracle within 1e-4 with the same iterations, trials, stopped code and erase set."""
+    if case == "c4":
+        prob = synth.localba_problem(seed=4)
+    else:
+        prob = _rejecting_problem(61, 3.0) if case == "reject1" else _rejecting_problem(78, 4.0)
+    full = oracle_mod.lba_solve(prob)
+    if case != "c4":
+        p = 0 if case == "reject1" else 1
+        assert full["trials"][p] > full["iterations"][p]
+    lba = amd.LocalBundleAdjustment()
+    for phase in (1, 2):
+        for T in range(0, full["trials"][phase - 1] + 2):
+            lba.set_stop_hook(phase, T)
+            _same(lba.solve(prob), oracle_mod.lba_solve(prob, hook=(phase, T)), (case, phase, T))
+    lba.set_stop_hook(0, 0)
+    _same(lba.solve(prob), full, (case, "no hook"))
+
+
+def test_lba_stop_flag_live(amd, oracle_mod):
+    """A second thread raises the flag while lba_solve runs (LocalMapping's mbAbortBA, set by
+    Tracking::NeedNewKeyFrame / InsertKeyFrame): the call returns early with stopped = 1, and its
+    result equals the oracle stopped at the same point (the trial the device observed)."""
+    import ctypes
+    import threading
+    import time
+    prob = synth.localba_problem(seed=12, n_kf=64, n_points=6000)
+    lba = amd.LocalBundleAdjustment()
+    full = lba.solve(prob)
+    t0 = time.perf_counter()
+    lba.solve(prob, stop=ctypes.c_uint8(0))
+    t_full = time.perf_counter() - t0
+    stopped_early = 0
+    for frac in (0.5, 0.3, 0.15, 0.05):
+        flag = ctypes.c_uint8(0)
+        th = threading.Timer(frac * t_full, lambda: setattr(flag, "value", 1))
+        th.start()
+        got = lba.solve(prob, stop=flag)
+        th.join()
+        assert flag.value == 1
+        if got["stopped"] == 0:
+            assert got["trials"] == full["trials"]   # raised after the last check: a complete run
+            continue
+        assert got["stopped"] == 1
+        stopped_early += 1
+        hook = (1, got["trials"][0]) if got["iterations"][1] == 0 and got["trials"][1] == 0 else (2, got["trials"][1])
+        ref = oracle_mod.lba_solve(prob, hook=hook)   # (2, 0) and (1, all) give the same outputs
+        _same(got, ref, ("live", frac, hook))
+        print("live stop", frac, t_full, got["iterations"], got["trials"])
+    assert stopped_early >= 1, f"no attempt observed the flag mid-call (call {t_full * 1e3:.2f} ms)"

@@ -191,6 +191,38 @@ def _check_pair(got, ref, what):
     assert gu.tobytes() == u.tobytes() and gd.tobytes() == d.tobytes(), what + " stereo"
 
 
+def test_stereo_pipeline_host_mode_varying_stride(amd, oracle_mod):
+    """host-mode batches (10 pairs, stride S), (5, S), (10, S), (5, 2S) -- slot 1 is reused
+    with the same pair count but a larger image stride while it is already big enough, so chunk j's
+    upload covers byte ranges that engines j+1.. read in slot 1's previous batch: the upload must wait
+    for every engine's reads, not only engines 0..j (the layout is keyed on count and stride)."""
+    h, w, k = 376, 1241, 3
+    S = w * h
+    pairs = [synth.stereo_pair(h, w, 80 + p) for p in range(10)]
+    refs = [_stereo_ref_full(oracle_mod, *pr) for pr in pairs]
+    plan = ((10, 1), (5, 1), (10, 1), (5, 2))   # (pairs, stride in images)
+    order = [[(p * 7 + b) % 10 for p in range(P)] for b, (P, _) in enumerate(plan)]
+    ins = []
+    for b, (P, m) in enumerate(plan):
+        a = amd.host_empty((2 * P, m * h, w), np.uint8)
+        a[...] = 0xA5                             # the gap rows of the wide stride are never read
+        for p, q in enumerate(order[b]):
+            a[2 * p, :h], a[2 * p + 1, :h] = pairs[q]
+        ins.append(a)
+    pl = amd.StereoPipeline(2000, n_engines=k)
+    pl.reserve(w, h, 10)
+    cap = pl.capacity()
+    outs = [amd.StereoHostBatch(P, cap) for P, _ in plan]
+    mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    for b, (P, m) in enumerate(plan):
+        pl.stereo_batch_host(ins[b], P, w, h, w, m * S, KITTI_BF, mb, outs[b])
+    pl.wait()
+    for b, (P, _) in enumerate(plan):
+        for p, q in enumerate(order[b]):
+            _check_pair(outs[b].pair(p), refs[q], f"batch {b} pair {p}")
+    pl.close()
+
+
 def test_stereo_pipeline_host_mode_varying_batches(amd, oracle_mod):
     """Host-mode batches of 10, 5 and 8 pairs (slot 0, slot 1, slot 0 again): the third batch's
     chunk ranges in slot 0 straddle the first batch's, so its uploads must wait for every engine's

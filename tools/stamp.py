@@ -12,12 +12,15 @@ LIB = Path(__file__).resolve().parent.parent / "orb-slam2-noted_amd" / "liborbsl
 
 
 def stamp(**config) -> dict:
+    """The library checked is the one the profiled run loaded: ORBSLAM_AMD_LIB when set (the Python
+    binding's override), else the product build. Its build id must be the bare source hash: a
+    variant or EXTRA-flag build carries a suffix (Makefile) and is refused."""
     h = src_hash()
-    built = ctypes.CDLL(str(LIB))
+    built = ctypes.CDLL(os.environ.get("ORBSLAM_AMD_LIB") or str(LIB))
     built.orbx_build_id.restype = ctypes.c_char_p
     lib_id = built.orbx_build_id().decode()
     if lib_id != h:
-        raise SystemExit(f"library built from sources {lib_id}, tree is {h}: rebuild before profiling")
+        raise SystemExit(f"library build id {lib_id}, tree is {h}: profile a product build of this tree")
     st = {"src_hash": h, "commit": os.environ.get("GIT_HEAD", "unknown"),
           "resize_mode": int(os.environ.get("RESIZE_MODE", "0"))}
     st.update(config)
