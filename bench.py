@@ -250,14 +250,14 @@ def c2_buffers(B: int, nbufs: int, pool):
     return bufs
 
 
-def time_c2(amd, args, dist, params, bufs, resize_mode, steps, profile=False):
+def time_c2(amd, args, dist, params, bufs, resize_mode, steps, profile=False, blur_mode=None):
     """Warmup + `steps` timed batches of the C2 leg on a fresh pipeline; the timed region is
     bracketed by a barrier + device synchronisation on both sides. -> (elapsed s, profile, pipeline)."""
     import torch
     nf, sf, nl, ith, mth, bf, mb = params
     B = args.batch
     ex = amd.StereoPipeline(int(nf), float(sf), int(nl), int(ith), int(mth), n_engines=args.engines,
-                            resize_mode=resize_mode)
+                            resize_mode=resize_mode, blur_mode=args.blur_mode if blur_mode is None else blur_mode)
     ex.reserve(W, H, B)
 
     def step(k):
@@ -332,6 +332,9 @@ def bench_c2(amd, args, dist, world, params, pool):
             "image": f"{W}x{H}",
             "nfeatures": NFEAT,
             "resize_mode": args.resize_mode,
+            "blur_mode": args.blur_mode,
+            "blur_mode_meaning": "0 = OpenCV >= 3.4 fixed-point GaussianBlur rounding (SURVEY A.3 pin); 1 = OpenCV 3.2 "
+                                 "SSE2 half-even column pass",
             "resize_mode_meaning": "0 = scalar FixedPtCast vertical pass (SURVEY A.2 (a), the oracle's default pin); "
                                    "1 = OpenCV 3.2 x86 SSE2 VResizeLinearVec_32s8u prefix (A.2 (b))",
             "streams": "seed-2 C2 stream" if world == 1 else "C5: rank r = seed 10 + r stream (seeds 10..17)",
@@ -346,7 +349,7 @@ def bench_c2(amd, args, dist, world, params, pool):
         achieved = BYTES_PER_STEREO_FRAME * per_launch / avg_s / 1e9
         # counters from the committed PMC pass, only if it was measured on this library, batch and mode
         pmc, pmc_note = load_pmc_doc("pmc_traffic.json", amd.build_id(), batch=round(per_launch),
-                                     resize_mode=args.resize_mode)
+                                     resize_mode=args.resize_mode, blur_mode=args.blur_mode)
         ent = (pmc or {}).get(name, {})
         out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 3),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
@@ -402,6 +405,14 @@ def bench_c2(amd, args, dist, world, params, pool):
                                   "ms_per_step": round(1000 * a_el / args.steps, 4),
                                   "note": "the same leg (batches, steps, engines) under the other SURVEY A.2 "
                                           "vertical-pass variant; both variants are parity-tested on the GPU"}
+        # the reference's documented platform (OpenCV 3.2.0 on x86-64, README.md:9): both SSE2 variants
+        c_el, _, c_ex = time_c2(amd, args, dist, params, bufs, 1, args.steps, blur_mode=1)
+        c_ex.close()
+        c_el = odist.max_over_ranks(c_el, COLL_DEV, dist)
+        out["alt_opencv32"] = {"resize_mode": 1, "blur_mode": 1, "value": round(frames / c_el, 2),
+                               "ms_per_step": round(1000 * c_el / args.steps, 4),
+                               "note": "the same leg under OpenCV 3.2's x86 SSE2 resize and GaussianBlur column "
+                                       "passes (SURVEY A.2 (b) + A.3), the reference's documented platform"}
     del bufs   # the resident batches are not needed by the legs below
     return out
 
@@ -430,8 +441,10 @@ def c2_parity(ex, args, params, pool):
             L, R = pool[j]
             if kb:
                 L, R = np.roll(L, 7 * kb, axis=1), np.roll(R, 7 * kb, axis=1)
-            oL = oracle.Extractor(int(nf), float(sf), int(nl), int(ith), int(mth), resize_mode=args.resize_mode)
-            oR = oracle.Extractor(int(nf), float(sf), int(nl), int(ith), int(mth), resize_mode=args.resize_mode)
+            oL = oracle.Extractor(int(nf), float(sf), int(nl), int(ith), int(mth), resize_mode=args.resize_mode,
+                                  blur_mode=args.blur_mode)
+            oR = oracle.Extractor(int(nf), float(sf), int(nl), int(ith), int(mth), resize_mode=args.resize_mode,
+                                  blur_mode=args.blur_mode)
             kL, dL = oL.extract(L)
             kR, dR = oR.extract(R)
             u, d = oracle.stereo_matches(oL, oR, kL, dL, kR, dR, float(bf), mb)
@@ -447,7 +460,7 @@ def c2_parity(ex, args, params, pool):
     rank = int(os.environ.get("RANK", "0"))
     return {"rank": rank, "pairs_checked": args.batch, "pairs_bit_exact": args.batch - len(bad),
             "first_mismatch": bad[:4], "distinct_pairs": len(cache), "left_seed_first_pair": POOL_SEEDS[0],
-            "resize_mode": args.resize_mode}
+            "resize_mode": args.resize_mode, "blur_mode": args.blur_mode}
 
 
 def isolated_launch_ms(amd, params, buf, pairs, name, resize_mode=0, reps=5):
@@ -1015,7 +1028,10 @@ def main():
     ap.add_argument("--pool", type=int, default=8, help="distinct synthetic stereo pairs")
     ap.add_argument("--resize-mode", type=int, default=0, choices=(0, 1),
                     help="SURVEY A.2 vertical-pass variant of the headline value (0: FixedPtCast, 1: SSE2)")
-    ap.add_argument("--no-alt-resize", action="store_true", help="skip the other resize variant's line")
+    ap.add_argument("--blur-mode", type=int, default=0, choices=(0, 1),
+                    help="SURVEY A.3 GaussianBlur variant of the headline value (0: >= 3.4 fixed point, 1: 3.2 SSE2)")
+    ap.add_argument("--no-alt-resize", action="store_true",
+                    help="skip the alternative variant lines (other resize mode; OpenCV 3.2 resize + blur)")
     ap.add_argument("--check-parity", action="store_true",
                     help="after timing, check every rank's last C2 batch bit-exact and its LocalBA within 1e-4 "
                          "against the CPU oracle (C5 rehearsal)")

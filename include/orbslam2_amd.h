@@ -30,9 +30,19 @@ typedef struct {
 } orbx_kp;
 
 /* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
- * -- include/ORBextractor.h:89 (ORBextractor.cc:471-579). resize_mode selects the pinned
- * cv::resize INTER_LINEAR vertical-pass variant: 0 scalar FixedPtCast
- * (default), 1 SSE2 VResizeLinearVec_32s8u layout. */
+ * -- include/ORBextractor.h:89 (ORBextractor.cc:471-579). The two OpenCV-version choices the
+ * reference leaves to its OpenCV build, each 0 or 1 (else ORBX_EINVAL):
+ *   resize_mode: cv::resize INTER_LINEAR vertical pass -- 0 scalar FixedPtCast (default),
+ *                1 the OpenCV 3.2 SSE2 VResizeLinearVec_32s8u layout;
+ *   blur_mode:   cv::GaussianBlur(9x9, 2) column pass (ORBextractor.cc:1617-1625) -- 0 the
+ *                OpenCV >= 3.4 fixed-point rounding (default), 1 OpenCV 3.2's SSE2
+ *                SymmColumnVec_32s8u (round half to even over each row's prefix [0, w & ~3)).
+ * resize_mode 1 + blur_mode 1 is the reference's documented platform (OpenCV 3.2.0 on x86-64,
+ * /root/reference/README.md:9).
+ * Input range (checked by orbx_reserve / orbx_extract, ORBX_EINVAL otherwise): image width and
+ * height <= 4000 (keys carry 12-bit coordinates), every pyramid level >= 40 x 40 pixels (the
+ * 19-pixel FAST border plus the blur halo; ORBextractor.cc:1084-1100 detects nothing in a
+ * smaller level), and scaleFactor <= 2 (the resize kernel's 4 outputs span <= 8 source bytes). */
 typedef struct {
     int32_t nfeatures;
     float scale_factor;
@@ -40,6 +50,7 @@ typedef struct {
     int32_t ini_th_fast;
     int32_t min_th_fast;
     int32_t resize_mode;
+    int32_t blur_mode;
 } orbx_params;
 
 typedef struct orbx_engine orbx_engine;

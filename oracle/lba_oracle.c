@@ -182,10 +182,12 @@ typedef struct {
      * hook_trial = 0 raises it before that call's first iteration */
     int hook_phase, hook_trial, phase, trials;
     int seen;   /* a terminate() check of the current optimize() call found the flag raised */
+    int hook_fired;
 } graph_t;
 
-static int hook_raised(const graph_t *g) {
-    return g->hook_phase > 0 && (g->phase > g->hook_phase || (g->phase == g->hook_phase && g->trials >= g->hook_trial));
+static int hook_raised(graph_t *g) {   /* raised once its trial has run; a phase short of it never raises */
+    if (g->hook_phase > 0 && g->phase == g->hook_phase && g->trials >= g->hook_trial) g->hook_fired = 1;
+    return g->hook_fired;
 }
 /* SparseOptimizer::terminate() (sparse_optimizer.h: *_forceStopFlag) */
 static int terminate_flag(graph_t *g) {

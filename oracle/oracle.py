@@ -24,7 +24,7 @@ MAXL = 16
 class OrcExtractor(C.Structure):
     _fields_ = [
         ("nfeatures", C.c_int), ("scaleFactor", C.c_double), ("nlevels", C.c_int),
-        ("iniThFAST", C.c_int), ("minThFAST", C.c_int), ("resize_mode", C.c_int),
+        ("iniThFAST", C.c_int), ("minThFAST", C.c_int), ("resize_mode", C.c_int), ("blur_mode", C.c_int),
         ("mvScaleFactor", C.c_float * MAXL), ("mvInvScaleFactor", C.c_float * MAXL),
         ("mvLevelSigma2", C.c_float * MAXL), ("mvInvLevelSigma2", C.c_float * MAXL),
         ("mnFeaturesPerLevel", C.c_int * MAXL), ("umax", C.c_int * 16), ("pattern", C.c_int * 1024),
@@ -61,6 +61,7 @@ def lib() -> C.CDLL:
         L.orc_resize_linear.argtypes = [P, C.c_int, C.c_int, C.c_int, P, C.c_int, C.c_int, C.c_int, C.c_int]
         L.orc_fast_roi.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int]
         L.orc_gaussian_blur9.argtypes = [P, C.c_int, C.c_int, P]
+        L.orc_gaussian_blur9_mode.argtypes = [P, C.c_int, C.c_int, P, C.c_int]
         L.orc_fast_atan2.argtypes = [C.c_float, C.c_float]
         L.orc_fast_atan2.restype = C.c_float
         L.orc_cosf.argtypes = [C.c_float]
@@ -118,12 +119,13 @@ def set_blur_mode(mode: int):
 class Extractor:
     """Python face of the oracle ORBextractor (ORBextractor.h:89-158)."""
 
-    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, resize_mode=0):
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, resize_mode=0, blur_mode=0):
         self.s = OrcExtractor()
         rc = lib().orc_extractor_init(C.byref(self.s), nfeatures, scale_factor, nlevels, ini_th, min_th)
         if rc != 0:
             raise ValueError("bad extractor params")
         self.s.resize_mode = resize_mode
+        self.s.blur_mode = blur_mode   # SURVEY A.3: 1 = OpenCV 3.2's half-even SSE2 column pass
         self.nfeatures = nfeatures
         self.nlevels = nlevels
 
@@ -290,10 +292,14 @@ def fast_roi(roi: np.ndarray, th: int):
     return xs[:n].copy(), ys[:n].copy(), sc[:n].copy()
 
 
-def gaussian_blur9(img: np.ndarray) -> np.ndarray:
+def gaussian_blur9(img: np.ndarray, mode: int | None = None) -> np.ndarray:
+    """mode None: the process-wide set_blur_mode(); 0 / 1: that variant."""
     img = np.ascontiguousarray(img, np.uint8)
     out = np.zeros_like(img)
-    lib().orc_gaussian_blur9(_p(img), img.shape[1], img.shape[0], _p(out))
+    if mode is None:
+        lib().orc_gaussian_blur9(_p(img), img.shape[1], img.shape[0], _p(out))
+    else:
+        lib().orc_gaussian_blur9_mode(_p(img), img.shape[1], img.shape[0], _p(out), int(mode))
     return out
 
 

@@ -716,7 +716,10 @@ static int simd_end16_4(int width) {
     return x;
 }
 void orc_gaussian_blur9(const uint8_t *src, int w, int h, uint8_t *dst) {
-    const int simd_end = g_blur_mode == 1 ? simd_end16_4(w) : 0;
+    orc_gaussian_blur9_mode(src, w, h, dst, g_blur_mode);
+}
+void orc_gaussian_blur9_mode(const uint8_t *src, int w, int h, uint8_t *dst, int mode) {
+    const int simd_end = mode == 1 ? simd_end16_4(w) : 0;
     int *rows = (int *)malloc(sizeof(int) * (size_t)w * h);
     for (int y = 0; y < h; y++) {
         const uint8_t *s = src + (size_t)y * w;
@@ -801,7 +804,7 @@ int orc_extract(orc_extractor *ex, const uint8_t *img, int w, int h, int stride,
     int offset = 0;
     for (int l = 0; l < ex->nlevels; l++) {
         if (nlev[l] == 0) { free(lev[l]); continue; }
-        orc_gaussian_blur9(ex->level[l], ex->lw[l], ex->lh[l], ex->blurred[l]);
+        orc_gaussian_blur9_mode(ex->level[l], ex->lw[l], ex->lh[l], ex->blurred[l], ex->blur_mode);
         for (int i = 0; i < nlev[l]; i++) {
             orc_kp kp = lev[l][i];
             if (ret >= 0) orc_orb_descriptor(ex->blurred[l], ex->lw[l], kp.x, kp.y, kp.angle, ex->pattern,

@@ -34,6 +34,7 @@ typedef struct {
     double scaleFactor;          /* ORBextractor.h:203 stores it as double */
     int nlevels, iniThFAST, minThFAST;
     int resize_mode;             /* 0 = scalar FixedPtCast (default pin), 1 = SSE2 VResizeLinearVec layout */
+    int blur_mode;               /* 0 = OpenCV >= 3.4 fixed point (default pin), 1 = OpenCV 3.2 half-even prefix */
     float mvScaleFactor[ORC_MAX_LEVELS], mvInvScaleFactor[ORC_MAX_LEVELS];
     float mvLevelSigma2[ORC_MAX_LEVELS], mvInvLevelSigma2[ORC_MAX_LEVELS];
     int mnFeaturesPerLevel[ORC_MAX_LEVELS];
@@ -62,6 +63,7 @@ int  orc_fast_roi(const uint8_t *img, int stride, int rows, int cols, int thresh
                   int *xs, int *ys, int *scores, int cap);
 int  orc_corner_score16(const uint8_t *ptr, int stride, int threshold);
 void orc_gaussian_blur9(const uint8_t *src, int w, int h, uint8_t *dst);
+void orc_gaussian_blur9_mode(const uint8_t *src, int w, int h, uint8_t *dst, int mode);
 float orc_fast_atan2(float y, float x);
 float orc_ic_angle(const uint8_t *img, int stride, float px, float py, const int *umax);
 void orc_orb_descriptor(const uint8_t *img, int stride, float px, float py, float angle,

@@ -35,6 +35,14 @@ inline int orbx_knob(const char *name, int dflt) {
 #endif
 }
 
+// Memory-layout knobs of the quadtree (ORBX_QT_LDS_KB, ORBX_QT_NODES_LDS) stay readable in the
+// product: every layout gives the same results (tests/test_extract_gpu.py::
+// test_extract_quadtree_layouts runs each one against the oracle), only the speed differs.
+inline int orbx_layout_knob(const char *name, int dflt) {
+    const char *ev = std::getenv(name);
+    return ev ? std::atoi(ev) : dflt;
+}
+
 inline int exp_twice() {
     static const int v = orbx_knob("ORBX_EXP_TWICE", 0);
     return v;
@@ -72,7 +80,7 @@ struct ExtractGeom {
     float scale[ORBX_MAXL];
     float inv_scale[ORBX_MAXL];        // mvInvScaleFactors = 1.0f / mvScaleFactor (ORBextractor.cc:503)
     int scaled_patch[ORBX_MAXL];
-    int ini_th, min_th, resize_mode;
+    int ini_th, min_th, resize_mode, blur_mode;
     int rz_col_off[ORBX_MAXL], rz_row_off[ORBX_MAXL], rz_simd_end[ORBX_MAXL];
     int blur_tiles_x[ORBX_MAXL], blur_tiles_y[ORBX_MAXL], blur_tile_base[ORBX_MAXL + 1];
     unsigned blur_tx_rcp[ORBX_MAXL];   // ceil(2^31 / blur_tiles_x): tile row = umulhi(2 t, rcp) on the SALU
@@ -190,7 +198,7 @@ struct orbx_engine {
     std::string err;
     // per-kernel hipEvent profiling (bench.py roofline), recorded on the launch stream
     bool prof = false;
-    struct ProfRec { const char *name; hipEvent_t a, b; };
+    struct ProfRec { const char *name; hipEvent_t a, b; int launches; };   // launches: kernels inside the span
     std::vector<ProfRec> prof_recs;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
@@ -213,7 +221,7 @@ namespace orbamd {
 // profiling helpers: prof_begin records a start event (returns a handle), prof_end the
 // matching stop event; both are no-ops when profiling is off.
 int prof_begin(orbx_engine *e, hipStream_t s);
-void prof_end(orbx_engine *e, hipStream_t s, int h, const char *name);
+void prof_end(orbx_engine *e, hipStream_t s, int h, const char *name, int launches = 1);
 int engine_reserve(orbx_engine *e, int w, int h, int max_images);
 int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitch,
                           long long stride, hipStream_t s, int phase);

@@ -424,6 +424,12 @@ __device__ __forceinline__ uint32_t gather_byte(uint32_t a0, uint32_t a1, uint32
 
 __device__ __forceinline__ long i8x8(uint32_t lo, uint32_t hi) { return (long)((unsigned long long)hi << 32 | lo); }
 
+// BM32 (blur_mode 1): OpenCV 3.2's column pass (SymmColumnVec_32s8u, README.md:9) accumulates in
+// float and rounds half to EVEN (_mm_cvtps_epi32) over the columns it vectorises -- the prefix
+// [0, w & ~3) of each row (16, then 4 at a time) -- while its scalar tail and OpenCV >= 3.4 round
+// half up. 256 accH + accL is exactly acc + 2^15, so an exact tie (acc mod 2^17 = 2^15) reads
+// as low 17 bits == 0x10000, and half-even takes one off the (odd) output byte there.
+template <bool BM32>
 __device__ __forceinline__ void fast_blur_mfma(const uint32_t *tin, uint8_t *dst, int bp, int x0, int y0, int w,
                                                int h, int xb0, int xb1, int lane) {
     const int n = lane & 15, gq = lane >> 4;
@@ -451,10 +457,17 @@ __device__ __forceinline__ void fast_blur_mfma(const uint32_t *tin, uint8_t *dst
         const i32x4 OH = __builtin_amdgcn_mfma_i32_16x16x32_i8(AH, VB, kh, 0, 0, 0);
         const i32x4 OL = __builtin_amdgcn_mfma_i32_16x16x32_i8(AL, VB, z, 0, 0, 0);
         // lane: output row y0 + n, columns x0 + 16 xb + 4 gq + r
-        const uint32_t v0 = ((uint32_t)OH.x << 8) + (uint32_t)OL.x, v1 = ((uint32_t)OH.y << 8) + (uint32_t)OL.y;
-        const uint32_t v2 = ((uint32_t)OH.z << 8) + (uint32_t)OL.z, v3 = ((uint32_t)OH.w << 8) + (uint32_t)OL.w;
-        const uint32_t val = gather_byte<2>(v0, v1, v2, v3);
+        uint32_t v0 = ((uint32_t)OH.x << 8) + (uint32_t)OL.x, v1 = ((uint32_t)OH.y << 8) + (uint32_t)OL.y;
+        uint32_t v2 = ((uint32_t)OH.z << 8) + (uint32_t)OL.z, v3 = ((uint32_t)OH.w << 8) + (uint32_t)OL.w;
         const int y = y0 + n, x = x0 + 16 * xb + 4 * gq;
+        if (BM32) {
+            const int se = w & ~3;   // OpenCV 3.2's vectorised prefix of the row
+            v0 -= ((v0 & 0x1FFFFu) == 0x10000u && x + 0 < se) ? 0x10000u : 0u;
+            v1 -= ((v1 & 0x1FFFFu) == 0x10000u && x + 1 < se) ? 0x10000u : 0u;
+            v2 -= ((v2 & 0x1FFFFu) == 0x10000u && x + 2 < se) ? 0x10000u : 0u;
+            v3 -= ((v3 & 0x1FFFFu) == 0x10000u && x + 3 < se) ? 0x10000u : 0u;
+        }
+        const uint32_t val = gather_byte<2>(v0, v1, v2, v3);
         if (y < h && x < w) {
             uint8_t *o = dst + (long long)y * bp + x;
             if (x + 3 < w) {
@@ -466,6 +479,7 @@ __device__ __forceinline__ void fast_blur_mfma(const uint32_t *tin, uint8_t *dst
     }
 }
 
+template <bool BM32>
 __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
                                                         uint8_t *blur, int *cell_cnt, uint32_t *cell_keys) {
     __shared__ __align__(16) uint32_t tin[(FB_TH + 8) * FB_LD];
@@ -655,7 +669,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         // column blocks per wavefront balance the pre-filter's extra work: wavefront 2 scores
         // the ring rows (one more 8-pixel group per lane), wavefront 3 the ring columns
         const int xb0 = wv == 0 ? 0 : wv == 1 ? 3 : 6, xb1 = wv == 0 ? 3 : wv == 1 ? 6 : wv == 2 ? 6 : 8;
-        fast_blur_mfma(tin, blur + (long long)b * g.blur_stride + g.blur_off[l], g.bp[l], x0, y0, w, h, xb0, xb1, lane);
+        fast_blur_mfma<BM32>(tin, blur + (long long)b * g.blur_stride + g.blur_off[l], g.bp[l], x0, y0, w, h, xb0, xb1, lane);
     }
 #endif
     __syncthreads();
@@ -2054,10 +2068,10 @@ int prof_begin(orbx_engine *e, hipStream_t s) {
     return h;
 }
 
-void prof_end(orbx_engine *e, hipStream_t s, int h, const char *name) {
+void prof_end(orbx_engine *e, hipStream_t s, int h, const char *name, int launches) {
     if (!e->prof || h < 0) return;
     (void)hipEventRecord(e->ev_pool[h + 1], s);
-    e->prof_recs.push_back({name, e->ev_pool[h], e->ev_pool[h + 1]});
+    e->prof_recs.push_back({name, e->ev_pool[h], e->ev_pool[h + 1], launches});
 }
 
 static int simd_end_for(int width) {
@@ -2159,16 +2173,17 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
         // (5 per CU) 0.52 ms, 32 KB (4 per CU) 0.57 ms, 16 KB 0.59 ms. ORBX_QT_NODES_LDS=1 /
         // ORBX_QT_LDS_KB=<k> are tuning knobs.
         g.qt_nodes_in_lds = 0;
-        g.qt_nodes_in_lds = orbx_knob("ORBX_QT_NODES_LDS", 0) != 0 && node_bytes <= 48 * 1024;
+        g.qt_nodes_in_lds = orbx_layout_knob("ORBX_QT_NODES_LDS", 0) != 0 && node_bytes <= 48 * 1024;
         g.qt_node_stride = (long long)((node_bytes + 15) / 16) * 4;
         long long qt_lds = 28 * 1024;
-        qt_lds = std::max(16, std::min(160, orbx_knob("ORBX_QT_LDS_KB", 28))) * 1024LL;
+        qt_lds = std::max(16, std::min(160, orbx_layout_knob("ORBX_QT_LDS_KB", 28))) * 1024LL;
         const long long kl_bytes = qt_lds - (long long)sizeof(QShared) - 256 -
                                    (g.qt_nodes_in_lds ? (long long)node_bytes : 0);
         g.qt_kl = (int)std::max<long long>(256, (kl_bytes / 12) & ~63LL);
         g.ini_th = e->p.ini_th_fast;
         g.min_th = e->p.min_th_fast;
         g.resize_mode = e->p.resize_mode;
+        g.blur_mode = e->p.blur_mode;
         // resize coefficient tables
         std::vector<int2> rzc;
         std::vector<int4> rzr;
@@ -2274,12 +2289,16 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
         else
             resize_level_kernel<false><<<grid, 256, lds, s>>>(g, l, tiles_x, cx, ry, d_imgs, pyr);
     }
-    prof_end(e, s, ph, "resize_level_kernel");
+    prof_end(e, s, ph, "resize_level_kernel", (L - 1) * ((exp_twice() & 1) ? 2 : 1));   // one launch per level
     HIPCHK(hipMemsetAsync(e->d_cell_cnt.p, 0, sizeof(int) * (size_t)n * g.ncell_total, s));   // cell slot counters
     if (e->fb_gate) HIPCHK(hipStreamWaitEvent(s, e->fb_gate, 0));
     ph = prof_begin(e, s);
-    fast_blur_kernel<<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
-                                                                   e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
+    if (g.blur_mode)
+        fast_blur_kernel<true><<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
+                                                                         e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
+    else
+        fast_blur_kernel<false><<<dim3(g.blur_tile_base[L], n), 256, 0, s>>>(g, d_imgs, pyr, e->d_blur.as<uint8_t>(),
+                                                                          e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>());
     prof_end(e, s, ph, "fast_blur_kernel");
     }
     if (phase & 2) {
@@ -2322,7 +2341,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     case 6: describe_kernel<6><<<dg6, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
     case 4: describe_kernel<4><<<dg4, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
     }
-    prof_end(e, s, ph, "describe_kernel");
+    prof_end(e, s, ph, desc_v != 0 ? "describe2_kernel" : "describe_kernel");
     }
     HIPCHK(hipGetLastError());
     HIPCHK(mark_done(e, s));
@@ -2354,6 +2373,7 @@ int orbx_create(const orbx_params *p, orbx_engine **out) {
     *out = nullptr;
     if (p->nlevels < 1 || p->nlevels > ORBX_MAXL || p->nfeatures < 0 || !(p->scale_factor > 1.0f))
         return ORBX_EINVAL;
+    if ((unsigned)p->resize_mode > 1u || (unsigned)p->blur_mode > 1u) return ORBX_EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ORBX_EDEVICE;
     orbx_engine *e = new orbx_engine();
@@ -2453,7 +2473,7 @@ int orbx_profile_read(orbx_engine *e, int idx, char *name, int name_cap, double 
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, r.a, r.b));
         tot += ms;
-        cnt++;
+        cnt += r.launches;
     }
     if (name && name_cap > 0) {
         std::snprintf(name, (size_t)name_cap, "%s", names[idx].c_str());

@@ -569,7 +569,7 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
     ph = prof_begin(e, s);
     search_init_cand_kernel<<<dim3((cap0 + 3) / 4, n_pairs), 256, 0, s>>>(a, S.prev.as<float>());
     search_init_resolve_kernel<<<n_pairs, 256, lds, s>>>(a, S.prev.as<float>(), S.m12.as<int>(), S.nmatch.as<int>());
-    prof_end(e, s, ph, "search_init_kernel");
+    prof_end(e, s, ph, "search_init_cand+resolve_kernel", 2);
     FR_CHK(hipGetLastError());
     FR_CHK(mark_done(e, s));
     S.si_pairs = n_pairs;

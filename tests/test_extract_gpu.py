@@ -24,9 +24,14 @@ def _assert_same_kps(got, ref, tag=""):
     assert bad.size == 0, f"{tag}: descriptor rows differ at {bad[:8]}"
 
 
+# mode = resize_mode + 2 * blur_mode (SURVEY A.2 / A.3 variants; 3 = the OpenCV 3.2 x86 platform of
+# README.md:9: SSE2 resize prefix and half-even blur prefix)
 CASES = [
     ("kitti", 376, 1241, 2000, 0, 2),
     ("kitti_sse", 376, 1241, 2000, 1, 5),
+    ("kitti_cv32", 376, 1241, 2000, 3, 2),
+    ("tum_blur32", 480, 640, 1000, 2, 3),
+    ("odd_cv32", 333, 517, 800, 3, 26),
     ("tum", 480, 640, 1000, 0, 3),
     ("tum_b", 480, 640, 1000, 0, 11),
     ("kitti_04", 370, 1226, 2000, 0, 21),    # KITTI04-12.yaml resolution
@@ -40,28 +45,34 @@ CASES = [
 @pytest.mark.parametrize("name,h,w,nf,mode,seed", CASES)
 def test_extract_parity(amd, oracle_mod, name, h, w, nf, mode, seed):
     img = synth.textured_image(h, w, seed)
-    ex = amd.ORBextractor(nf, 1.2, 8, 20, 7, resize_mode=mode)
-    ref = oracle_mod.Extractor(nf, 1.2, 8, 20, 7, resize_mode=mode)
+    rm, bm = mode & 1, mode >> 1
+    ex = amd.ORBextractor(nf, 1.2, 8, 20, 7, resize_mode=rm, blur_mode=bm)
+    ref = oracle_mod.Extractor(nf, 1.2, 8, 20, 7, resize_mode=rm, blur_mode=bm)
     got = ex(img)
     want = ref.extract(img)
     for l in range(8):
         lev = ref.level(l)
         np.testing.assert_array_equal(ex.pyramid_level(l), lev, err_msg=f"pyramid level {l}")
         # E6 directly: the MFMA blur's every pixel, borders included, against the
-        # GaussianBlur restatement (ORBextractor.cc:1617-1625)
-        np.testing.assert_array_equal(ex.blurred_level(l), oracle_mod.gaussian_blur9(lev), err_msg=f"blurred level {l}")
+        # GaussianBlur restatement (ORBextractor.cc:1617-1625) in the same variant
+        np.testing.assert_array_equal(ex.blurred_level(l), oracle_mod.gaussian_blur9(lev, bm),
+                                      err_msg=f"blurred level {l}")
     _assert_same_kps(got, want, name)
 
 
+@pytest.mark.parametrize("blur_mode", [0, 1])
 @pytest.mark.parametrize("h,w", [(376, 1241), (480, 640), (240, 320), (333, 517), (241, 1023)])
-def test_blurred_pyramid_noise(amd, oracle_mod, h, w):
+def test_blurred_pyramid_noise(amd, oracle_mod, h, w, blur_mode):
     """Blurred pyramid of uniform noise (every byte value) and of 0/255 vertical stripes (the largest
     row sums, full-scale outputs), byte for byte at every level, odd sizes included (smallest level
-    >= 62 rows, the extractor's limit for one FAST cell row)."""
+    >= 62 rows, the extractor's limit for one FAST cell row), in both SURVEY A.3 variants. Noise
+    holds exact rounding ties, where the OpenCV 3.2 variant (blur_mode 1) differs from the
+    default: the test checks that it does somewhere, so both roundings are really exercised."""
     rng = np.random.default_rng(h * 1000 + w)
+    ties = 0
     for img in (rng.integers(0, 256, size=(h, w), dtype=np.uint8),
                 np.broadcast_to(((np.arange(w) // 8) % 2 * 255).astype(np.uint8), (h, w)).copy()):
-        ex = amd.ORBextractor(1000, 1.2, 8, 20, 7)
+        ex = amd.ORBextractor(1000, 1.2, 8, 20, 7, blur_mode=blur_mode)
         ex(img)
         ref = oracle_mod.Extractor(1000, 1.2, 8, 20, 7)
         ref.extract(img)
@@ -69,8 +80,10 @@ def test_blurred_pyramid_noise(amd, oracle_mod, h, w):
             lev = ref.level(l)
             if lev.size == 0:
                 continue
-            np.testing.assert_array_equal(ex.blurred_level(l), oracle_mod.gaussian_blur9(lev),
-                                          err_msg=f"{h}x{w} blurred level {l}")
+            want = oracle_mod.gaussian_blur9(lev, blur_mode)
+            ties += int((want != oracle_mod.gaussian_blur9(lev, 1 - blur_mode)).sum())
+            np.testing.assert_array_equal(ex.blurred_level(l), want, err_msg=f"{h}x{w} blurred level {l}")
+    assert ties > 0
 
 
 def test_extract_noise_many_candidates(amd, oracle_mod):
@@ -182,3 +195,22 @@ def test_golden_c1_c2_on_device(amd):
     bf, fx, mb = g2["camera"]
     u, dep = amd.compute_stereo_matches(exL, exR, len(kL), float(bf), float(mb))
     assert u.tobytes() == g2["u_right"].tobytes() and dep.tobytes() == g2["depth"].tobytes()
+
+
+@pytest.mark.parametrize("case", ["wide", "tall", "small_level", "scale_factor", "bad_mode"])
+def test_extract_input_limits(amd, case):
+    """The extractor's documented input range (include/orbslam2_amd.h, orbx_params): width / height
+    <= 4000, every pyramid level >= 40 x 40, scaleFactor <= 2, resize_mode / blur_mode in {0, 1}.
+    Outside it the call fails with ORBX_EINVAL (status -1) and the engine stays usable."""
+    if case == "bad_mode":
+        with pytest.raises(amd.OrbslamError, match="status -1"):
+            amd.ORBextractor(1000, blur_mode=2)
+        return
+    shape, kw = {"wide": ((400, 4001), {}), "tall": ((4001, 400), {}), "small_level": ((120, 160), {}),
+                 "scale_factor": ((480, 640), {"scaleFactor": 2.5, "nlevels": 3})}[case]
+    ex = amd.ORBextractor(1000, **kw)
+    with pytest.raises(amd.OrbslamError, match="status -1"):
+        ex(np.zeros(shape, np.uint8))
+    if case != "scale_factor":   # a refused size leaves the engine usable
+        k, _ = ex(synth.textured_image(480, 640, 3))
+        assert len(k) > 0

@@ -44,7 +44,9 @@ def test_lba_oracle_stop_hook_semantics(oracle_mod):
     prob = _rejecting_problem(61, 3.0)
     full = oracle_mod.lba_solve(prob)
     assert full["trials"][0] > full["iterations"][0], "the problem must reject a phase-1 trial"
-    assert oracle_mod.lba_solve(prob, hook=(2, 99))["pose_Tcw"].tobytes() == full["pose_Tcw"].tobytes()
+    for never in ((2, 99), (1, full["trials"][0] + 1)):   # a trial the phase never reaches raises nothing
+        r = oracle_mod.lba_solve(prob, hook=never)
+        assert r["pose_Tcw"].tobytes() == full["pose_Tcw"].tobytes() and r["stopped"] == 0, never
     r0 = oracle_mod.lba_solve(prob, hook=(1, 0))
     assert r0["iterations"] == (0, 0) and r0["stopped"] == 1
     rej = None

@@ -139,6 +139,32 @@ def test_stereo_pipeline(amd, oracle_mod, P, k):
     pl.close()
 
 
+def test_stereo_pipeline_opencv32(amd, oracle_mod):
+    """The pipeline under the reference's documented platform (OpenCV 3.2 on x86-64, README.md:9):
+    the SSE2 resize layout (resize_mode 1) and the half-even GaussianBlur column pass (blur_mode 1),
+    12 pairs over 3 engines: keypoints, descriptors, mvuRight and mvDepth bit-exact against the
+    oracle in the same variants."""
+    import torch
+    h, w, P, k = 376, 1241, 12, 3
+    pairs = [synth.stereo_pair(h, w, 50 + p) for p in range(P)]
+    dev = torch.from_numpy(np.stack([im for pr in pairs for im in pr])).cuda()
+    pl = amd.StereoPipeline(2000, n_engines=k, resize_mode=1, blur_mode=1)
+    pl.reserve(w, h, P)
+    mb = float(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    torch.cuda.synchronize()
+    pl.stereo_batch(dev.data_ptr(), P, w, h, w, h * w, KITTI_BF, mb)
+    torch.cuda.synchronize()
+    for p in range(P):
+        L, R = pairs[p]
+        exL = oracle_mod.Extractor(2000, resize_mode=1, blur_mode=1)
+        exR = oracle_mod.Extractor(2000, resize_mode=1, blur_mode=1)
+        kL, dL = exL.extract(L)
+        kR, dR = exR.extract(R)
+        u, d = oracle_mod.stereo_matches(exL, exR, kL, dL, kR, dR, KITTI_BF, mb)
+        _check_pair((*pl.fetch(p), *[a[:len(kL)] for a in pl.stereo_fetch(p)]), (kL, dL, kR, dR, u, d), f"pair {p}")
+    pl.close()
+
+
 def test_stereo_pipeline_host_mode(amd, oracle_mod):
     """orbx_pipeline_stereo_batch_host: host (pinned) images in, host outputs out, the H2D of the
     next batch overlapping the current one, three batches back to back into two output buffers

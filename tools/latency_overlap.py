@@ -14,7 +14,7 @@ from statistics import median
 rows = list(csv.DictReader(open(sys.argv[1])))
 key = "Stream_Id" if rows and "Stream_Id" in rows[0] else "Queue_Id"
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-EXTRACT = ("resize_level_kernel", "fast_blur_kernel", "fast_nms_kernel", "quadtree_kernel", "describe_kernel")
+EXTRACT = ("resize_level_kernel", "fast_blur_kernel", "quadtree_kernel", "describe2_kernel", "describe_kernel")
 frames, cur = [], []
 for r in rows:
     name = r["Kernel_Name"].split("(")[0].split("<")[0].split(" ")[-1].split("::")[-1]

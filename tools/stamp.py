@@ -22,6 +22,7 @@ def stamp(**config) -> dict:
     if lib_id != h:
         raise SystemExit(f"library build id {lib_id}, tree is {h}: profile a product build of this tree")
     st = {"src_hash": h, "commit": os.environ.get("GIT_HEAD", "unknown"),
-          "resize_mode": int(os.environ.get("RESIZE_MODE", "0"))}
+          "resize_mode": int(os.environ.get("RESIZE_MODE", "0")),
+          "blur_mode": int(os.environ.get("BLUR_MODE", "0"))}
     st.update(config)
     return st
