@@ -97,6 +97,8 @@ struct Graph {
     double *err;           // [ne][3] g2o _error
     const int *act;        // active edge indices (edge order)
     const uint8_t *on;     // per active slot: 1 = level 0; 0 = set to level 1 by the phase-1 outlier test
+    EdgeDev *E_lm;         // the edge records in landmark-major (pt_items) order: lba_lin_points reads
+    uint8_t *on_lm;        // them and the level flags by record position, one dependent load fewer
     int nact;
     const int *pose_hidx;  // per pose vertex, -1 = fixed / inactive
     const int *point_hidx;
@@ -126,7 +128,9 @@ struct Graph {
     double *partial;       // [4][kRedBlocks]: robust chi2 block sums of linearisation set 0 | point
                            // maxDiagonal | pose maxDiagonal | robust chi2 block sums of set 1
     double *scalars;       // [8]: chi2, maxdiag, tempChi, scale, ok, lambda
-    LMState *lm;
+    LMState *lm;           // the LM state this launch reads (and, for a deciding launch, writes)
+    const LMState *lm_src; // a deciding lba_reduce_points: the state before the decision (ping-pong)
+    LMState *lm_buf[2];    // the two state buffers (host bookkeeping: lm is one of them)
     const unsigned *stopf; // pbStopFlag mirrored by lba_solve's host loop into page-locked, device-mapped memory
     unsigned *arrive;      // lba_errors block-arrival counter (the last block runs the LM decision)
     int Kpad;              // Y^T rows 3 Lm rounded up to 4; row Kpad (and up to Kpad + 3) is zero
@@ -140,9 +144,12 @@ struct Graph {
     int NPW, wrow;         // Y^T leading dimension (NP + 16); Y^T column holding w (16 * ceil(6P / 16))
 };
 
-__device__ inline void edge_error(const Graph &g, const EdgeDev &e, const Pose *T, const double *X, double err[3]) {
+__device__ inline void decide_sums(const Graph &g, int nbt, double *sums_s);
+__device__ LMState lm_next(const Graph &g, LMState s, double sc_sum, double chi_sum);
+
+__device__ inline void edge_error_at(const EdgeDev &e, const Pose &T, const double *Xp, double err[3]) {
     double p[3];
-    pose_map(T[e.pose], X + 3 * e.point, p);
+    pose_map(T, Xp, p);
     if (!e.stereo) {
         const double u = p[0] / p[2], v = p[1] / p[2];
         err[0] = e.obs[0] - (u * e.fx + e.cx);
@@ -158,6 +165,9 @@ __device__ inline void edge_error(const Graph &g, const EdgeDev &e, const Pose *
         err[1] = e.obs[1] - r1;
         err[2] = e.obs[2] - r2;
     }
+}
+__device__ inline void edge_error(const Graph &g, const EdgeDev &e, const Pose *T, const double *X, double err[3]) {
+    edge_error_at(e, T[e.pose], X + 3 * e.point, err);
 }
 
 __device__ inline double edge_chi2(const EdgeDev &e, const double err[3]) {
@@ -197,22 +207,8 @@ __device__ __forceinline__ int chi_off(int set) { return set ? 3 * kRedBlocks : 
 // (on = 0) keeps its stale _error and contributes zeros. Two wave-uniform roles share a slot
 // (twice the waves, each with about half the FP64 chain): role 0 writes the residual, Hll / bl
 // and Hpl and returns the robust chi2; role 1 writes Hpp / bp (and returns 0).
-#ifndef LBA_LIN_ROLES
-#define LBA_LIN_ROLES 1   // 2: two wave-uniform roles per slot (more waves, each half the FP64 chain)
-#endif
-constexpr int kLinEdges = LBA_LIN_ROLES == 2 ? 128 : 256;   // slots per 256-thread workgroup
-__device__ __forceinline__ void lin_thread(int &s, int &role) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-#if LBA_LIN_ROLES == 2
-    s = (t >> 7) * 64 + (t & 63);
-    role = (t >> 6) & 1;   // wave-uniform
-#else
-    s = t;
-    role = 2;
-#endif
-}
-__device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &e, bool on, int s, int lpos, int ppos,
-                                                 const Pose *Tc, const double *Xc, int set, int role) {
+__device__ __forceinline__ double linearize_slot_at(const Graph &g, const EdgeDev &e, bool on, int s, int lpos, int ppos,
+                                                    const Pose &T, const double *Xp, int set, int role) {
     double *cl = g.conl[set] + 9LL * lpos, *hp = g.hpl[set] + 18LL * lpos;
     double *cp = g.conp[set] + 27LL * (ppos < 0 ? 0 : ppos);
     if (role == 1 && ppos < 0) return 0.0;   // no pose part
@@ -226,14 +222,13 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
         return 0.0;
     }
     double err[3];
-    edge_error(g, e, Tc, Xc, err);
+    edge_error_at(e, T, Xp, err);
     if (role != 1) { g.err[3 * s] = err[0]; g.err[3 * s + 1] = err[1]; g.err[3 * s + 2] = err[2]; }
     const double chi = edge_chi2(e, err);
     double r0 = chi, r1 = 1.0;
     if (e.robust) huber(e, chi, r0, r1);
-    const Pose T = Tc[e.pose];
     double p[3], R[9];
-    pose_map(T, Xc + 3 * e.point, p);
+    pose_map(T, Xp, p);
     quat_to_R(T.q, R);
     const double x = p[0], y = p[1], z = p[2], z2 = z * z, fx = e.fx, fy = e.fy, bf = e.bf;
     double Jt[18];
@@ -308,23 +303,102 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
     }
     return r0;
 }
+__device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &e, bool on, int s, int lpos, int ppos,
+                                                 const Pose *Tc, const double *Xc, int set, int role) {
+    return linearize_slot_at(g, e, on, s, lpos, ppos, Tc[e.pose], Xc + 3 * e.point, set, role);
+}
 
-// the linearisation at the current estimate -- only the first trial slot of an optimize() runs it:
-// every later iteration starts from the linearisation lba_errors formed for the accepted trial
-// (or, after an iteration that ended on a rejected trial, from the unchanged current one)
-__global__ __launch_bounds__(256) void lba_linearize(Graph g) {
-    int s, role;
-    lin_thread(s, role);
-    const bool in = s < g.nact;
-    const uint8_t on = in ? g.on[s] : 0;
-    EdgeDev e{};
-    int lpos = 0, ppos = -1;
-    if (in) { e = g.E[s]; lpos = g.slot_lpos[s]; ppos = g.slot_ppos[s]; }
+// Landmark-major linearisation, kLPL lanes per landmark (kLPB landmarks per workgroup): lane r
+// takes records r, r + kLPL, ... of the landmark's contiguous run (CSR, pt_items) and linearises
+// those slots (linearize_slot_at: residual, Huber weight, Jacobians, the quadratic-form pieces at
+// the record's landmark-major and pose-major positions). Workgroups [0, nbl): landmarks;
+// [nbl, nbt): free poses (UPDATE only). Chi2 block sums -> chi_part[b] and the set's partials.
+//  !UPDATE (the first slot of an optimize(), was lba_linearize): at the current estimate, into
+//          the current linearisation set.
+//   UPDATE (every trial, was lba_update + lba_errors): the landmark back substitution x_l =
+//          Dinv (b_l - Hpl^T x_p) (a fixed-order butterfly over the group), X_t = X + x_l, and each
+//          slot's pose T_t = exp(x_p) T formed in the lane (pose_oplus, the same bits the pose
+//          workgroups store), then the trial's residuals and linearisation into the trial set;
+//          computeScale pieces x (lambda x + b) -> scale_part[b]. One launch instead of two, and
+//          no grid-wide wait between the update and the residuals.
+constexpr int kLPL = 8, kLPB = 256 / kLPL;
+template <bool UPDATE>
+__global__ __launch_bounds__(256) void lba_lin_points(Graph g, double *scale_part, double *chi_part, int nbl) {
+    const int grp = threadIdx.x / kLPL, r = threadIdx.x % kLPL;
+    const int l = blockIdx.x * kLPB + grp;
+    const bool isl = (int)blockIdx.x < nbl && l < g.Lm;
+    // the landmark's record range goes out with the LM-state load
+    const int i0 = isl ? g.pt_start[l] : 0, i1 = isl ? g.pt_start[l + 1] : 0;
     const LMState lm = *g.lm;
-    if (lm.done || !lm.newiter) return;
-    double rchi = 0;
-    if (in) rchi = linearize_slot(g, e, on, s, lpos, ppos, lm.cur ? g.T2 : g.T, lm.cur ? g.X2 : g.X, lm.cur, role);
-    block_sum_to(rchi, g.partial + chi_off(lm.cur) + blockIdx.x);
+    if (lm.done || (!UPDATE && !lm.newiter)) return;
+    const bool cur = lm.cur;
+    const int set = UPDATE ? !cur : cur;
+    const Pose *Tc = cur ? g.T2 : g.T;
+    const double *Xc = cur ? g.X2 : g.X;
+    const double lambda = UPDATE ? lm.lambda : 0.0;
+    // pbStopFlag snapshot for the decision of this trial (every workgroup of the deciding launch
+    // must see the same value): one read of the mapped word, into device memory
+    if (UPDATE && blockIdx.x == 0 && threadIdx.x == 0)
+        g.scalars[6] = __hip_atomic_load(g.stopf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ? 1.0 : 0.0;
+    double sc = 0, chi = 0;
+    if ((int)blockIdx.x >= nbl) {   // free poses (UPDATE): T_t = exp(x_p) T, computeScale pieces
+        const int t = ((int)blockIdx.x - nbl) * 256 + threadIdx.x;
+        if (UPDATE && t < g.P) {
+            Pose *Tt = cur ? g.T : g.T2;
+            const int v = g.hpose[t];
+            const double *xp = g.x + 6 * t;
+            Tt[v] = pose_oplus(Tc[v], xp);
+            for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + g.bp[6 * t + k]);
+        }
+    } else if (isl) {
+        const int v = g.hpoint[l];
+        double Xn[3] = {Xc[3 * v], Xc[3 * v + 1], Xc[3 * v + 2]};
+        if (UPDATE) {
+            double c[3] = {0, 0, 0};
+            const double *hpL = g.hpl[cur];
+            for (int i = i0 + r; i < i1; i += kLPL) {
+                const int ph = g.lpos_ph[i];
+                if (ph < 0) continue;
+                const double *B = hpL + 18LL * i;
+                const double *xp = g.x + 6 * ph;
+                for (int cc = 0; cc < 3; cc++) {
+                    double a = 0;
+                    for (int k = 0; k < 6; k++) a += B[3 * k + cc] * (-xp[k]);
+                    c[cc] += a;
+                }
+            }
+#pragma unroll
+            for (int m = kLPL / 2; m > 0; m >>= 1)
+#pragma unroll
+                for (int cc = 0; cc < 3; cc++) c[cc] += __shfl_xor(c[cc], m);
+            const double *bl = g.bl + 3 * l, *Di = g.Dinv + 9 * l;
+            c[0] += bl[0]; c[1] += bl[1]; c[2] += bl[2];
+            double *Xt = cur ? g.X : g.X2;
+            double *xl = g.x + 6 * g.P + 3 * l;
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
+                Xn[a] += xa;
+                if (r == 0) {
+                    xl[a] = xa;
+                    Xt[3 * v + a] = Xn[a];
+                    sc += xa * (lambda * xa + bl[a]);
+                }
+            }
+        }
+        for (int i = i0 + r; i < i1; i += kLPL) {
+            const int s = g.pt_items[i], ph = g.lpos_ph[i];
+            const EdgeDev e = g.E_lm[i];
+            const Pose T = (UPDATE && ph >= 0) ? pose_oplus(Tc[e.pose], g.x + 6 * ph) : Tc[e.pose];
+            chi += linearize_slot_at(g, e, g.on_lm[i] != 0, s, i, ph >= 0 ? g.lpos_ppos[i] : -1, T, Xn, set, 2);
+        }
+    }
+    if (UPDATE) {
+        block_sum_to(sc, scale_part + blockIdx.x);
+        __syncthreads();   // block_sum_to's LDS is reused: every thread has read the first sum
+    }
+    const double bsum = block_sum_to(chi, chi_part + blockIdx.x);
+    if (threadIdx.x == 0) g.partial[chi_off(set) + blockIdx.x] = bsum;
 }
 
 // ---- Schur: per landmark Dinv, L = chol(Dinv), Y block and w
@@ -385,12 +459,16 @@ constexpr int kRPL = 16;   // landmarks per lba_reduce_points workgroup
 #define LBA_FUSED_PREP 1   // 1: with lambda known (a new iteration after the first), the landmark half
                            // of the Schur step runs here and lba_prep_slots returns at once
 #endif
+static_assert(LBA_FUSED_PREP == 1, "lba_prep_slots runs only in the first slot of an optimize()");
 // fused (lambda = the LM state's): after the sums, the group's lanes gather the landmark's 9
 // values through LDS, each factors (Hll + lambda I)^-1 = L L^T (point_factor_of: the bits
 // lba_prep_slots forms) and lane r writes the Y blocks of records r, r + 16, ...; lane 0 writes
 // Dinv and w. Block 0 also does lba_prep_slots' mode-1 work (chi2 sum -> scalars[0], lambda ->
 // scalars[5]).
-__device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused, double lambda, int n0, double *sh) {
+// retry (a rejected trial's next slot: same linearisation, new lambda): no sums -- the landmark's
+// stored Hll / b_l feed the same fused tail (what lba_prep_slots' mode 0 formed before)
+__device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused, bool retry, double lambda, int n0,
+                                                   double *sh) {
     const int l = blockIdx.x * kRPL + (threadIdx.x >> 4), k = threadIdx.x & 15;
     __shared__ double hv_s[256];
     double dmax = 0, v = 0;
@@ -399,6 +477,14 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused
         i0 = g.pt_start[l];
         i1 = g.pt_start[l + 1];
     }
+    if (retry) {   // uniform
+        if (l < g.Lm && k < 9) {
+            // packed upper 00 01 02 11 12 22 -> the stored symmetric 3 x 3 (0, 1, 2, 4, 5, 8)
+            v = k < 6 ? g.Hll[9 * l + (k < 3 ? k : k == 5 ? 8 : k + 1)] : g.bl[3 * l + k - 6];
+        }
+        hv_s[threadIdx.x] = v;
+        __syncthreads();
+    } else {
     if (l < g.Lm && k < 9) {
         const double *cl = g.conl[set] + k;
         for (int i = i0; i < i1; i += 8) {
@@ -430,18 +516,6 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused
     }
     if (threadIdx.x == 0) g.partial[kRedBlocks + blockIdx.x] = sh[0];
     if (!fused) return;   // uniform
-    if (blockIdx.x == 0) {   // lba_prep_slots mode 1: the same tree over the chi2 block sums
-        __shared__ double sa[256];
-        double a = 0;
-        const double *chi = g.partial + chi_off(set);
-        for (int i = threadIdx.x; i < n0; i += 256) a += chi[i];
-        sa[threadIdx.x] = a;
-        __syncthreads();
-        for (int s = 128; s > 0; s >>= 1) {
-            if ((int)threadIdx.x < s) sa[threadIdx.x] += sa[threadIdx.x + s];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) { g.scalars[0] = sa[0]; g.scalars[5] = lambda; }
     }
     if (l >= g.Lm) return;
     const double *hv = hv_s + (threadIdx.x & ~15);
@@ -462,67 +536,84 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused
     }
 }
 
-#ifndef LBA_RP
-#define LBA_RP 32   // records per lane per batch in reduce_poses_body
-#endif
-__device__ __forceinline__ void reduce_poses_body(Graph &g, int i, int set, double (*sh)[33]) {
-    const int k = threadIdx.x & 31, grp = threadIdx.x >> 5;
-    const int t0 = g.ps_start[i], t1 = g.ps_start[i + 1];
+// One component `comp` of a free pose's quadratic form (Hpp upper 0..20, b_p 21..26): the pose's
+// contiguous run of pose-major records (conp), lane-strided with 8 loads in flight, then an xor
+// butterfly -- a fixed order, so lba_pose_sums (first slot) and lba_schur_tiles (every slot) form
+// the same bits. Returns the sum to every lane.
+__device__ __forceinline__ double pose_comp_sum(const Graph &g, int set, int ph, int comp, int lane) {
+    const int t0 = g.ps_start[ph], t1 = g.ps_start[ph + 1];
+    const double *cp = g.conp[set] + comp;
     double acc = 0;
-    if (k < 27) {   // batches of RP records per lane, all in flight (one batch up to 32 RP slots per pose)
-        constexpr int RP = LBA_RP;
-        const double *cp = g.conp[set] + k;
-        for (int tb = t0 + grp; tb < t1; tb += 32 * RP) {
-            double a[RP];
+    for (int tb = t0 + lane; tb < t1; tb += 64 * 8) {
+        double a[8];
 #pragma unroll
-            for (int u = 0; u < RP; u++) {
-                const int t = tb + 32 * u;
-                a[u] = t < t1 ? cp[27LL * t] : 0.0;
-            }
+        for (int u = 0; u < 8; u++) a[u] = tb + 64 * u < t1 ? cp[27LL * (tb + 64 * u)] : 0.0;
 #pragma unroll
-            for (int u = 0; u < RP; u++)
-                if (tb + 32 * u < t1) acc += a[u];
-        }
+        for (int u = 0; u < 8; u++) acc += a[u];
     }
-    sh[grp][k] = acc;
-    __syncthreads();
-    if (threadIdx.x < 27) {
-        double v = 0;
-        for (int q = 0; q < 32; q++) v += sh[q][threadIdx.x];
-        sh[0][threadIdx.x] = v;   // row 0 entry threadIdx.x is read only by this thread above
-    }
-    __syncthreads();
-    if (threadIdx.x < 36) {
-        const int a = threadIdx.x / 6, b = threadIdx.x % 6;
-        const int lo = min(a, b), hi = max(a, b);
-        const int u = lo * 6 - lo * (lo - 1) / 2 + (hi - lo);   // packed upper index
-        g.Hpp[36 * i + threadIdx.x] = sh[0][u];
-    }
-    if (threadIdx.x < 6) g.bp[6 * i + threadIdx.x] = sh[0][21 + threadIdx.x];
-    if (threadIdx.x == 0) {
-        double m = 0;
-        for (int a = 0; a < 6; a++) {
-            const int u = a * 6 - a * (a - 1) / 2;
-            m = fmax(m, fabs(sh[0][u]));
-        }
-        g.partial[2 * kRedBlocks + i] = m;
-    }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
+    return acc;
+}
+// packed upper index u of a 6 x 6 -> (a, b), a <= b
+__device__ __forceinline__ void upper6(int u, int &a, int &b) {
+    a = 0;
+    int start = 0;
+    while (u >= start + 6 - a) { start += 6 - a; a++; }
+    b = a + (u - start);
+}
+// Hpp (6x6) and b_p of every free pose, one wave per (pose, component): Hpp entries (comp < 21,
+// both triangles), b_p (comp >= 21) and, for the 6 diagonal entries, |H| into the maxDiagonal
+// partials. Only the first trial slot of an optimize() launches it (lambda init); later slots get
+// the same sums from lba_schur_tiles' pose waves.
+__device__ __forceinline__ void pose_comp_store(Graph &g, int set, int w, int lane, bool maxdiag) {
+    const int ph = w / 27, comp = w - 27 * ph;
+    if (ph >= g.P) return;
+    const double v = pose_comp_sum(g, set, ph, comp, lane);
+    if (lane != 0) return;
+    if (comp >= 21) { g.bp[6 * ph + comp - 21] = v; return; }
+    int a, b;
+    upper6(comp, a, b);
+    g.Hpp[36 * ph + 6 * a + b] = v;
+    g.Hpp[36 * ph + 6 * b + a] = v;
+    if (maxdiag && a == b) g.partial[2 * kRedBlocks + 6 * ph + a] = fabs(v);
+}
+__global__ __launch_bounds__(256) void lba_pose_sums(Graph g) {
+    const LMState lm = *g.lm;
+    if (lm.done || !lm.newiter) return;
+    pose_comp_store(g, lm.cur, 4 * blockIdx.x + (threadIdx.x >> 6), threadIdx.x & 63, true);
 }
 
 // the landmark reductions on 256-thread workgroups (one landmark per thread: a merged launch with
 // the pose reductions on 1024-thread workgroups spread the landmarks over 4x fewer CUs and took
 // 22 us against 8 + 10), the pose reductions one 1024-thread workgroup per free pose
-__global__ __launch_bounds__(256) void lba_reduce_points(Graph g, int n0) {
-    const LMState lm = *g.lm;
-    if (lm.done || !lm.newiter) return;
+// A deciding launch (lm_src set: every trial slot of a chunk but its first) first runs the previous
+// trial's LM decision: every workgroup forms the same state from lm_src (same sums, same flag
+// snapshot, a pure function), workgroup 0 stores it into lm -- the other buffer, so no workgroup
+// can read a state another one already advanced. One launch per trial fewer than a separate
+// lba_decide.
+__global__ __launch_bounds__(256) void lba_reduce_points(Graph g, int n0, int nbt) {
     __shared__ double shp[256];
-    reduce_points_body(g, lm.cur, LBA_FUSED_PREP && lm.it > 0, lm.lambda, n0, shp);
-}
-__global__ __launch_bounds__(1024) void lba_reduce_poses(Graph g) {
-    const LMState lm = *g.lm;
-    if (lm.done || !lm.newiter) return;
-    __shared__ double shq[32][33];
-    reduce_poses_body(g, blockIdx.x, lm.cur, shq);
+    __shared__ LMState lm_s;
+    LMState lm;
+    if (g.lm_src) {   // uniform
+        const LMState s0 = *g.lm_src;
+        if (!s0.done) {
+            decide_sums(g, nbt, shp);
+            __syncthreads();
+            if (threadIdx.x == 0) lm_s = lm_next(g, s0, shp[0], shp[1]);
+        } else if (threadIdx.x == 0) {
+            lm_s = s0;
+        }
+        __syncthreads();
+        lm = lm_s;
+        if (blockIdx.x == 0 && threadIdx.x == 0) *g.lm = lm;
+        __syncthreads();   // shp is reused below
+    } else {
+        lm = *g.lm;
+    }
+    if (lm.done) return;
+    reduce_points_body(g, lm.cur, LBA_FUSED_PREP && lm.it > 0, !lm.newiter, lm.lambda, n0, shp);
 }
 
 // First kernel of an LM trial (setLambda + the landmark half of the Schur complement).
@@ -564,7 +655,10 @@ __global__ __launch_bounds__(256) void lba_prep_slots(Graph g, int n0, int n1, i
         if (mode == 2) lambda = 1e-5 * sb[0];
         if (blockIdx.x == 0 && threadIdx.x == 0) { g.scalars[0] = sa[0]; g.scalars[1] = sb[0]; }
     }
-    if (t == 0) g.scalars[5] = lambda;
+    if (t == 0) {
+        g.scalars[5] = lambda;
+        if (mode == 2) g.lm->lambda = lambda;   // the trial's lambda lives in the LM state; no block reads
+    }                                           // this field (mode 2 forms lambda itself)
     const long long W = g.NPW;
     double Di[9], L[6];
     if (ist) {
@@ -611,10 +705,17 @@ __global__ __launch_bounds__(256) void lba_schur_tiles(Graph g) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int n6 = 6 * g.P;
     const long long W = g.NPW;
+    if ((int)blockIdx.x >= g.nchunks + (n6 + 3) / 4) {   // Hpp: one wave per (pose, upper component)
+        const int w = 4 * ((int)blockIdx.x - g.nchunks - (n6 + 3) / 4) + wv, ph = w / 21;
+        if (ph < g.P) pose_comp_store(g, g.lm->cur, 27 * ph + (w - 21 * ph), lane, false);
+        return;
+    }
     if ((int)blockIdx.x >= g.nchunks) {   // b_schur rows 4 (blockIdx - nchunks) + wv
         const int row = 4 * ((int)blockIdx.x - g.nchunks) + wv;
         if (row >= n6) return;
         const int ph = row / 6, a = row % 6, i0 = g.ps_start[ph], i1 = g.ps_start[ph + 1];
+        const double bpv = pose_comp_sum(g, g.lm->cur, ph, 21 + a, lane);   // b_p, the order lba_pose_sums uses
+        if (lane == 0) g.bp[row] = bpv;
         double v = 0;
         for (int i = i0 + lane; i < i1; i += 256) {
             double q[4];
@@ -632,7 +733,7 @@ __global__ __launch_bounds__(256) void lba_schur_tiles(Graph g) {
         if (lane == 0) {
             double sum = 0;
             for (int k = 0; k < 64; k++) sum += bsum[wv][k];
-            g.bs[row] = g.bp[row] - sum;
+            g.bs[row] = bpv - sum;
         }
         return;
     }
@@ -676,7 +777,7 @@ __global__ __launch_bounds__(256) void lba_schur_finish(Graph g) {
     if (g.lm->done) return;
     const int I = ij.x, J = ij.y, n6 = 6 * g.P;
     const long long NP = g.NP;
-    const double lambda = g.scalars[5];
+    const double lambda = g.lm->lambda;
     double v = 0;
     const double *tp = g.tp_part + 256LL * nc.x + 64 * q + lane;
     for (int c0 = 0; c0 < nc.y; c0 += 32) {
@@ -1144,131 +1245,6 @@ __global__ void lba_set_ok(Graph g) {
     if (!g.lm->done) g.scalars[4] = 1;
 }
 
-// landmark back substitution x_l = Dinv (b_l - Hpl^T x_p) fused with the update
-// T <- exp(x_p) T (SE3Quat::exp, left-multiplied), X <- X + x_l into the trial buffers and the
-// computeScale pieces x (lambda x + b) of the thread's own entries, block sums -> part[].
-// Blocks [0, nbp): one thread per free pose. Blocks [nbp, ..): kUL lanes per landmark, lane r
-// forms the Hpl^T x_p terms of records r, r + kUL, ... of the landmark's contiguous run, and the
-// group's lane 0 adds them in record order (through LDS, the group is inside one wavefront)
-constexpr int kUL = 8;
-__global__ __launch_bounds__(256) void lba_update(Graph g, double *part, int nbp) {
-    const bool pblk = (int)blockIdx.x < nbp;
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    const int l = pblk ? -1 : (t - nbp * 256) / kUL, r = threadIdx.x & (kUL - 1);
-    const bool isl = l >= 0 && l < g.Lm;
-    // the landmark's record range and this lane's first index entry go out with the LM-state load
-    const int i0 = isl ? g.pt_start[l] : 0, i1 = isl ? g.pt_start[l + 1] : 0;
-    int ph = i0 + r < i1 ? g.lpos_ph[i0 + r] : -1;
-    const LMState lm = *g.lm;
-    if (lm.done) return;
-    const double lambda = g.scalars[5];
-    const bool cur = lm.cur;   // current estimate -> trial buffer
-    const Pose *Tc = cur ? g.T2 : g.T;
-    Pose *Tt = cur ? g.T : g.T2;
-    const double *Xc = cur ? g.X2 : g.X;
-    double *Xt = cur ? g.X : g.X2;
-    double sc = 0;
-    if (pblk) {
-        if (t < g.P) {
-            const int v = g.hpose[t];
-            const double *xp = g.x + 6 * t;
-            Tt[v] = pose_oplus(Tc[v], xp);
-            for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + g.bp[6 * t + k]);
-        }
-    } else {
-        __shared__ double vsh[256][3];
-        __shared__ int vok[256];
-        double c[3] = {0, 0, 0};
-        if (isl && r == 0) { c[0] = g.bl[3 * l]; c[1] = g.bl[3 * l + 1]; c[2] = g.bl[3 * l + 2]; }
-        const double *hpL = g.hpl[cur];
-        for (int base = i0; base < i1; base += kUL) {   // the group's lanes run the same trips
-            const int i = base + r;
-            if (base != i0) ph = i < i1 ? g.lpos_ph[i] : -1;
-            double v[3] = {0, 0, 0};
-            if (ph >= 0) {
-                const double *B = hpL + 18LL * i;
-                const double *xp = g.x + 6 * ph;
-                for (int cc = 0; cc < 3; cc++) {
-                    double a = 0;
-                    for (int k = 0; k < 6; k++) a += B[3 * k + cc] * (-xp[k]);
-                    v[cc] = a;
-                }
-            }
-            vsh[threadIdx.x][0] = v[0]; vsh[threadIdx.x][1] = v[1]; vsh[threadIdx.x][2] = v[2];
-            vok[threadIdx.x] = ph >= 0;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (r == 0)
-                for (int k = 0; k < kUL; k++)
-                    if (vok[threadIdx.x + k])
-                        for (int cc = 0; cc < 3; cc++) c[cc] += vsh[threadIdx.x + k][cc];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        if (isl && r == 0) {
-            const int v = g.hpoint[l];
-            const double *Di = g.Dinv + 9 * l;
-            double *xl = g.x + 6 * g.P + 3 * l;
-            for (int a = 0; a < 3; a++) {
-                const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
-                xl[a] = xa;
-                Xt[3 * v + a] = Xc[3 * v + a] + xa;
-                sc += xa * (lambda * xa + g.bl[3 * l + a]);
-            }
-        }
-    }
-    block_sum_to(sc, part + blockIdx.x);
-}
-__device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthreads);
-#ifndef LBA_SEP_DECIDE
-#define LBA_SEP_DECIDE 1   // 1: the LM decision as its own one-block launch after lba_errors
-#endif
-#ifndef LBA_FENCE_W0
-#define LBA_FENCE_W0 0     // 1: only wave 0 of each lba_errors block releases (its partial)
-#endif
-
-// Trial chi2 of the active edges (block sums -> part[]) fused with the LM decision: the last
-// block to arrive (agent-scope release by every wave, one counter; the arriving block acquires,
-// cdna_hip_programming.md G16) sums the partials and runs lm_decide -- one launch fewer per trial.
-// Each slot also linearises the trial estimate into the trial's linearisation set (the chi2 it
-// needs is the trial chi2 itself): an accepted trial swaps the sets with the estimates, so the
-// next iteration starts at its reductions without a lba_linearize launch.
-__global__ __launch_bounds__(256) void lba_errors(Graph g, double *part, int nbu, int nbe, int np, int nq) {
-    int s, role;
-    lin_thread(s, role);
-    const bool in = s < g.nact;
-    const uint8_t on = in ? g.on[s] : 0;
-    EdgeDev e{};
-    int lpos = 0, ppos = -1;
-    if (in) { e = g.E[s]; lpos = g.slot_lpos[s]; ppos = g.slot_ppos[s]; }   // slot s = edge s (lba_linearize)
-    const bool done = g.lm->done, cur = g.lm->cur;
-    if (done) return;
-    double r0 = 0;
-    if (in) r0 = linearize_slot(g, e, on, s, lpos, ppos, cur ? g.T : g.T2, cur ? g.X : g.X2, !cur, role);
-    const double bsum = block_sum_to(r0, part + blockIdx.x);
-    if (threadIdx.x == 0) g.partial[chi_off(!cur) + blockIdx.x] = bsum;
-#if LBA_SEP_DECIDE
-    return;   // lba_decide follows
-#endif
-    __shared__ int last;
-#if LBA_FENCE_W0
-    if (threadIdx.x < 64)   // wave 0 wrote the block's partial: the only store the deciding block reads
-#endif
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this wave's stores (err, part) reach L2 / memory
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add(g.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == gridDim.x - 1;
-        if (last) __hip_atomic_store(g.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next trial
-    }
-    __syncthreads();
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other blocks' partials
-    lm_decide(g, nbu, nbe, np, nq, 256);
-}
-
 // SparseOptimizer::terminate(): *_forceStopFlag (sparse_optimizer.h), read live from the mapped word
 // the host keeps equal to the caller's pbStopFlag, or the deterministic test hook
 __device__ inline bool stop_raised(const Graph &g, const LMState &s) {
@@ -1293,16 +1269,16 @@ __global__ void lba_lm_init(Graph g, int iterations, int stop_at) {
 // :155-161): wave 0 sums the update's computeScale block sums and the trial chi2 block sums,
 // thread 0 decides and advances the state; an accepted trial becomes the current estimate by
 // swapping the estimate buffers (LMState::cur).
-__device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthreads) {
-    // wave 0 sums the block partials in a fixed order (lane k: blocks k, k + 64, ... in order, then
-    // an xor butterfly) -- a serial sum on thread 0 was ~3 us on the trial's critical path
-    __shared__ double sums_s[2];
+// The decision's two sums (wave 0): the trial's computeScale block sums and chi2 block sums (nbt
+// each, scalars[8..]) in a fixed order -- lane k: blocks k, k + 64, ... in order, then an xor
+// butterfly (a serial sum on one thread was ~3 us on the trial's critical path)
+__device__ inline void decide_sums(const Graph &g, int nbt, double *sums_s) {
     if (threadIdx.x < 64) {
         const int k = threadIdx.x;
         const double *pp = g.scalars + 8;
         double a = 0, b = 0;
-        for (int i = k; i < nbu; i += 64) a += pp[i];
-        for (int i = k; i < nbe; i += 64) b += pp[nbu + i];
+        for (int i = k; i < nbt; i += 64) a += pp[i];
+        for (int i = k; i < nbt; i += 64) b += pp[nbt + i];
 #pragma unroll
         for (int m = 32; m > 0; m >>= 1) {
             a += __shfl_xor(a, m);
@@ -1310,75 +1286,84 @@ __device__ void lm_decide(Graph &g, int nbu, int nbe, int np, int nq, int nthrea
         }
         if (k == 0) { sums_s[0] = a; sums_s[1] = b; }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        LMState s = *g.lm;
-        const double *sc = g.scalars;
-        if (s.qmax == 0) {
-            s.currentChi = s.iniChi = sc[0];
-            if (s.it == 0) s.lambda = sc[5];   // tau * maxDiagonal, formed by lba_prep_slots
-        }
-        const double sc_sum = sums_s[0], chi_sum = sums_s[1];
-        const double tempChi = sc[4] != 0 ? chi_sum : DBL_MAX;
-        double rho = s.currentChi - tempChi;
-        const double scale = sc_sum + 1e-3;
-        rho /= scale;
-        int a = 0;
-        if (rho > 0 && isfinite(tempChi)) {   // good step: discardTop
-            double alpha = 1. - pow((2 * rho - 1), 3.0);
-            alpha = fmin(alpha, 2. / 3.);
-            s.lambda *= fmax(1. / 3., alpha);
-            s.ni = 2;
-            s.currentChi = tempChi;
-            a = 1;
-        } else {                               // bad step: pop
-            s.lambda *= s.ni;
-            s.ni *= 2;
-        }
-        s.qmax++;
-        s.trials++;
-        s.rho = rho;
-        s.accepted = a;
-        // pbStopFlag, read where g2o reads it: the trial loop's `rho < 0 && qmax < max &&
-        // !terminate()` (levenberg.cpp:149, evaluated only after a rejected trial) and the iteration
-        // loop's `i < iterations && !terminate() && ok` (sparse_optimizer.cpp:376, before `ok`)
-        const bool raised = stop_raised(g, s);
-        bool retry = false;
-        if (rho < 0 && s.qmax < 10) {
-            if (raised) s.seen = 1;
-            else retry = true;
-        }
-        if (retry) {
-            s.newiter = 0;                     // retry the same linearisation
-        } else {
-            s.it++;
-            s.final_chi = s.currentChi;
-            bool ok = true;
-            if (s.qmax == 10 || rho == 0) ok = false;
-            else {
-                if ((s.iniChi - s.currentChi) * 1e3 < s.iniChi) s.nBad++; else s.nBad = 0;
-                if (s.nBad >= 3) ok = false;
-            }
-            s.newiter = 1;
-            s.qmax = 0;
-            bool term = false;
-            if (s.it < s.iterations && raised) term = s.seen = 1;
-            if (!ok || s.it >= s.iterations || term) s.done = 1;
-        }
-        if (a) s.cur ^= 1;   // the trial buffers become the current estimate (no copy)
-        *g.lm = s;
-    }
-    (void)np; (void)nq; (void)nthreads;
 }
 
 // End of one LM trial (optimization_algorithm_levenberg.cpp:96-164 + the ORB-SLAM2 stop rule
-// :155-161): thread 0 sums the update's computeScale block sums and the trial chi2 block sums
-// in block order, decides, and advances the state; an accepted trial becomes the current
-// estimate by swapping the roles of the two estimate buffers (LMState::cur). Standalone form (unused by
-// lba_optimize, which runs the decision in lba_errors' last block).
-__global__ __launch_bounds__(64) void lba_decide(Graph g, int nbu, int nbe, int np, int nq) {
-    if (g.lm->done) return;
-    lm_decide(g, nbu, nbe, np, nq, 64);
+// :155-161) as a pure function of the state before it: rho, lambda / nu, the retry / new-iteration
+// choice, nBad; an accepted trial becomes the current estimate by swapping the roles of the two
+// estimate buffers (LMState::cur). currentChi at an iteration's first trial: the first
+// iteration's comes from the linearisation (scalars[0], lba_prep_slots), every later one is the
+// accepted trial's chi2 itself -- the value g2o's activeRobustChi2() recomputes there.
+__device__ LMState lm_next(const Graph &g, LMState s, double sc_sum, double chi_sum) {
+    const double *sc = g.scalars;
+    if (s.qmax == 0) {
+        if (s.it == 0) s.currentChi = sc[0];
+        s.iniChi = s.currentChi;
+    }
+    const double tempChi = sc[4] != 0 ? chi_sum : DBL_MAX;
+    double rho = s.currentChi - tempChi;
+    const double scale = sc_sum + 1e-3;
+    rho /= scale;
+    int a = 0;
+    if (rho > 0 && isfinite(tempChi)) {   // good step: discardTop
+        double alpha = 1. - pow((2 * rho - 1), 3.0);
+        alpha = fmin(alpha, 2. / 3.);
+        s.lambda *= fmax(1. / 3., alpha);
+        s.ni = 2;
+        s.currentChi = tempChi;
+        a = 1;
+    } else {                               // bad step: pop
+        s.lambda *= s.ni;
+        s.ni *= 2;
+    }
+    s.qmax++;
+    s.trials++;
+    s.rho = rho;
+    s.accepted = a;
+    // pbStopFlag, read where g2o reads it: the trial loop's `rho < 0 && qmax < max && !terminate()`
+    // (levenberg.cpp:149, evaluated only after a rejected trial) and the iteration loop's
+    // `i < iterations && !terminate() && ok` (sparse_optimizer.cpp:376, before `ok`). The flag is
+    // the snapshot lba_lin_points took at the end of this trial (scalars[6]): one value for every
+    // workgroup of a deciding launch.
+    const bool raised = sc[6] != 0.0 || s.trials >= s.stop_at;
+    bool retry = false;
+    if (rho < 0 && s.qmax < 10) {
+        if (raised) s.seen = 1;
+        else retry = true;
+    }
+    if (retry) {
+        s.newiter = 0;                     // retry the same linearisation
+    } else {
+        s.it++;
+        s.final_chi = s.currentChi;
+        bool ok = true;
+        if (s.qmax == 10 || rho == 0) ok = false;
+        else {
+            if ((s.iniChi - s.currentChi) * 1e3 < s.iniChi) s.nBad++; else s.nBad = 0;
+            if (s.nBad >= 3) ok = false;
+        }
+        s.newiter = 1;
+        s.qmax = 0;
+        bool term = false;
+        if (s.it < s.iterations && raised) term = s.seen = 1;
+        if (!ok || s.it >= s.iterations || term) s.done = 1;
+    }
+    if (a) s.cur ^= 1;   // the trial buffers become the current estimate (no copy)
+    return s;
+}
+
+// The decision as a launch of its own: after the last trial slot of a chunk (the state the host
+// reads back). Inside a chunk the next slot's lba_reduce_points decides instead.
+__global__ __launch_bounds__(64) void lba_decide(Graph g, int nbt) {
+    __shared__ double sums_s[2];
+    const LMState s0 = *g.lm_src;
+    if (s0.done) {
+        if (threadIdx.x == 0) *g.lm = s0;
+        return;
+    }
+    decide_sums(g, nbt, sums_s);
+    __syncthreads();
+    if (threadIdx.x == 0) *g.lm = lm_next(g, s0, sums_s[0], sums_s[1]);
 }
 
 // the EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ records of Optimizer.cc:750-848 from the
@@ -1427,16 +1412,27 @@ __global__ __launch_bounds__(256) void lba_outliers(const EdgeDev *E, const doub
 __global__ __launch_bounds__(256) void lba_phase2_mark(Graph g, EdgeDev *E, uint8_t *on, int ne) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (s < g.nact) {
-        const int k = g.act[s];
+        const int k = s;   // every edge is active in slot order (build_active)
         const bool cur = g.lm->cur;
         const EdgeDev e = E[k];
         const double chi = edge_chi2(e, g.err + 3 * k);
         double p[3];
         pose_map((cur ? g.T2 : g.T)[e.pose], (cur ? g.X2 : g.X) + 3 * e.point, p);
         const double th = e.stereo ? 7.815 : 5.991;
-        if (chi > th || !(p[2] > 0.0)) on[s] = 0;
+        const int lpos = g.slot_lpos[s];
+        if (chi > th || !(p[2] > 0.0)) { on[s] = 0; g.on_lm[lpos] = 0; }
+        g.E_lm[lpos].robust = 0;
     }
     if (s < ne) E[s].robust = 0;
+}
+
+// the landmark-major copy of the edge records (lba_lin_points), once per LocalBA call
+__global__ __launch_bounds__(256) void lba_gather_edges(EdgeDev *E_lm, uint8_t *on_lm, const EdgeDev *E, const int *pt_items,
+                                                        int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    E_lm[i] = E[pt_items[i]];
+    on_lm[i] = 1;
 }
 
 // b vector in hessian order for computeScale: [b_p (6P) | b_l (3Lm)]
@@ -1464,13 +1460,15 @@ struct DBuf {
 struct lba_engine {
     int device = 0;
     hipStream_t stream = nullptr;
-    DBuf T, T2, X, X2, E, err, act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items,
+    DBuf T, T2, X, X2, E, E_lm, on_lm, err, act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items,
         ps_start, ps_items, slot_pt, slot_ph, con, hpl, Hll, bl, Hpp, bp, Dinv, Lc, Y, ywp, on, tp_part, Hs, bs, x, partial,
         scalars, flags, lm, arrive, arenaA, arenaB;
     double *h_scalars = nullptr;  // pinned
     LMState *h_lm = nullptr;      // pinned
-    void *h_stage = nullptr;      // pinned upload staging (grow-only)
-    size_t h_stage_bytes = 0;
+    void *h_stage[2] = {nullptr, nullptr};   // pinned upload staging per arena (grow-only)
+    size_t h_stage_bytes[2] = {0, 0};
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};   // the last DMA out of each staging buffer
+    bool stage_rec[2] = {false, false};
     void *h_down = nullptr;       // pinned download staging of the results (grow-only)
     size_t h_down_bytes = 0;
     // pbStopFlag as the device sees it: a page-locked, device-mapped, coherent word the host loop
@@ -1623,8 +1621,7 @@ void build_schur_tiles(ActiveSet &A, int zero_row) {
 // order (the second reuses them: lba_phase2_mark). The vectors of A keep their capacity from call
 // to call (lba_solve's thread_local set).
 void build_active(const HostGraph &h, ActiveSet &A) {
-    A.act.resize(h.ne);
-    for (int k = 0; k < h.ne; k++) A.act[k] = k;
+    A.act.resize(h.ne);   // slot s = edge s: only the size is used
     std::vector<char> &pa = A.scratch_p, &qa = A.scratch_q;
     pa.assign(h.np, 0);
     qa.assign(h.nq, 0);
@@ -1652,7 +1649,7 @@ void build_active(const HostGraph &h, ActiveSet &A) {
     A.pt_start.assign(A.Lm + 1, 0);
     A.ps_start.assign(A.P + 1, 0);
     for (int s = 0; s < (int)A.act.size(); s++) {
-        const int k = A.act[s];
+        const int k = s;
         A.pt_start[A.point_hidx[h.edge_point[k]] + 1]++;
         const int ph = A.pose_hidx[h.edge_pose[k]];
         if (ph >= 0) A.ps_start[ph + 1]++;
@@ -1664,14 +1661,16 @@ void build_active(const HostGraph &h, ActiveSet &A) {
     std::vector<int> &fl = A.scratch_l, &fp = A.scratch_f;
     fl.assign(A.Lm, 0);
     fp.assign(A.P, 0);
-    A.slot_pt.assign(std::max<size_t>(1, A.act.size()), 0);
-    A.slot_ph.assign(std::max<size_t>(1, A.act.size()), -1);
-    A.slot_ppos.assign(std::max<size_t>(1, A.act.size()), -1);
-    A.slot_lpos.assign(std::max<size_t>(1, A.act.size()), 0);
-    A.lpos_ph.assign(std::max<size_t>(1, A.act.size()), -1);
-    A.lpos_ppos.assign(std::max<size_t>(1, A.act.size()), -1);
+    // every entry of these is written by the fill loop below (size only, no initialisation pass)
+    A.slot_pt.resize(std::max<size_t>(1, A.act.size()));
+    A.slot_ph.resize(std::max<size_t>(1, A.act.size()));
+    A.slot_ppos.resize(std::max<size_t>(1, A.act.size()));
+    A.slot_lpos.resize(std::max<size_t>(1, A.act.size()));
+    A.lpos_ph.resize(std::max<size_t>(1, A.act.size()));
+    A.lpos_ppos.resize(std::max<size_t>(1, A.act.size()));
+    if (A.act.empty()) { A.slot_pt[0] = 0; A.slot_ph[0] = -1; A.slot_ppos[0] = -1; A.slot_lpos[0] = 0; A.lpos_ph[0] = -1; A.lpos_ppos[0] = -1; }
     for (int s = 0; s < (int)A.act.size(); s++) {
-        const int k = A.act[s];
+        const int k = s;
         const int l = A.point_hidx[h.edge_point[k]];
         const int lpos = A.pt_start[l] + fl[l]++;
         A.pt_items[lpos] = s;
@@ -1681,6 +1680,7 @@ void build_active(const HostGraph &h, ActiveSet &A) {
         A.slot_pt[s] = l;
         A.slot_ph[s] = ph;
         A.slot_ppos[s] = -1;
+        A.lpos_ppos[lpos] = -1;
         if (ph >= 0) {
             A.slot_ppos[s] = A.ps_start[ph] + fp[ph];
             A.lpos_ppos[lpos] = A.slot_ppos[s];
@@ -1704,20 +1704,26 @@ struct UploadSet {
         return off;
     }
 };
-int upload_set(lba_engine *e, DBuf &arena, const UploadSet &u, hipStream_t s) {
-    // the staging buffer is reused: the previous upload from it must have landed
-    if (hipStreamSynchronize(s) != hipSuccess) return -1;
-    if (u.total > e->h_stage_bytes) {
-        if (e->h_stage) (void)hipHostFree(e->h_stage);
-        e->h_stage = nullptr;
-        e->h_stage_bytes = 0;
-        if (hipHostMalloc(&e->h_stage, u.total, hipHostMallocDefault) != hipSuccess) return -1;
-        e->h_stage_bytes = u.total;
+// Two staging buffers (one per arena): an upload waits only for the previous DMA out of its own
+// buffer (an event), not for the stream -- the second upload of a call no longer stalls on the first.
+int upload_set(lba_engine *e, int k, DBuf &arena, const UploadSet &u, hipStream_t s) {
+    if (e->stage_rec[k] && hipEventSynchronize(e->ev_stage[k]) != hipSuccess) return -1;
+    if (u.total > e->h_stage_bytes[k]) {
+        if (e->h_stage[k]) (void)hipHostFree(e->h_stage[k]);
+        e->h_stage[k] = nullptr;
+        e->h_stage_bytes[k] = 0;
+        if (hipHostMalloc(&e->h_stage[k], u.total, hipHostMallocDefault) != hipSuccess) return -1;
+        e->h_stage_bytes[k] = u.total;
     }
     for (const auto &it : u.items)
-        if (it.bytes) std::memcpy((char *)e->h_stage + it.off, it.src, it.bytes);
+        if (it.bytes) std::memcpy((char *)e->h_stage[k] + it.off, it.src, it.bytes);
+    if (u.total > arena.n && hipStreamSynchronize(s) != hipSuccess) return -1;   // the old arena may be in use
     if (arena.ensure(u.total)) return -1;
-    return hipMemcpyAsync(arena.p, e->h_stage, u.total, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : -1;
+    if (hipMemcpyAsync(arena.p, e->h_stage[k], u.total, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipEventRecord(e->ev_stage[k], s) != hipSuccess)
+        return -1;
+    e->stage_rec[k] = true;
+    return 0;
 }
 template <class T> T *at(DBuf &arena, size_t off) { return (T *)((char *)arena.p + off); }
 
@@ -1742,29 +1748,49 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
     };
     if (A.P + A.Lm == 0) return -1;
     if (A.P > kMaxPoses) return -2;
-    if (((int)A.act.size() + kLinEdges - 1) / kLinEdges > kRedBlocks || (A.Lm + kRPL - 1) / kRPL > kRedBlocks)
-        return -2;   // partial regions
+    if ((A.Lm + kRPL - 1) / kRPL > kRedBlocks) return -2;   // partial regions
     const int nact = (int)A.act.size();
     const int n6 = 6 * A.P;
-    const int nbp = nblk(A.P), nbu = nbp + std::max(1, (A.Lm * kUL + 255) / 256);   // lba_update blocks
-    const int nbe = std::max(1, (nact + kLinEdges - 1) / kLinEdges);   // linearize / errors blocks
-    auto slot = [&](bool first) {
+    // lba_lin_points workgroups: landmarks (kLPB each), then free poses (256 each); its chi2 and
+    // computeScale block sums are the partials every reduction of the LM state reads (nbt of each)
+    const int nbl = std::max(1, (A.Lm + kLPB - 1) / kLPB), nbt = nbl + nblk(A.P);
+    if (nbt > kRedBlocks) return -2;
+    // the LM state ping-pongs between g.lm_buf[0 / 1] at every decision: a deciding launch reads one
+    // buffer and writes the other, and every later launch reads the new one
+    auto advance = [&](Graph &gd) {
+        gd = g;
+        gd.lm_src = g.lm;
+        gd.lm = g.lm == g.lm_buf[0] ? g.lm_buf[1] : g.lm_buf[0];
+        g.lm = gd.lm;
+    };
+    // `decide`: the previous trial of this chunk is undecided; this slot's lba_reduce_points decides it
+    auto slot = [&](bool first, bool decide) {
         int ph;
-        if (first) {   // later iterations start from lba_errors' linearisation of the accepted trial
+        if (first) {   // later iterations start from the linearisation of the accepted trial
             ph = lprof_begin(e);
-            lba_linearize<<<nbe, 256, 0, s>>>(g);
+            lba_lin_points<false><<<nbt, 256, 0, s>>>(g, nullptr, g.scalars + 8 + nbt, nbl);
             lprof_end(e, ph, "lba_linearize");
         }
         ph = lprof_begin(e);
-        lba_reduce_points<<<std::max(1, (A.Lm + kRPL - 1) / kRPL), 256, 0, s>>>(g, nbe);
-        if (A.P > 0) lba_reduce_poses<<<A.P, 1024, 0, s>>>(g);
-        lprof_end(e, ph, "lba_reduce");
-        ph = lprof_begin(e);
-        lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nbe, std::max(1, (A.Lm + kRPL - 1) / kRPL), A.P);
-        lprof_end(e, ph, "lba_prep_slots");
+        if (decide) {
+            Graph gd;
+            advance(gd);
+            lba_reduce_points<<<std::max(1, (A.Lm + kRPL - 1) / kRPL), 256, 0, s>>>(gd, nbt, nbt);
+        } else {
+            lba_reduce_points<<<std::max(1, (A.Lm + kRPL - 1) / kRPL), 256, 0, s>>>(g, nbt, nbt);
+        }
+        lprof_end(e, ph, "lba_reduce_points");
+        if (first) {   // lambda init (levenberg.cpp:179-191): the maxDiagonal needs Hpp before the Schur
+            ph = lprof_begin(e);
+            if (A.P > 0) lba_pose_sums<<<(27 * A.P + 3) / 4, 256, 0, s>>>(g);
+            lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nbt, std::max(1, (A.Lm + kRPL - 1) / kRPL), 6 * A.P);
+            lprof_end(e, ph, "lba_pose_sums_prep");
+        }
         if (A.P > 0) {
             ph = lprof_begin(e);
-            lba_schur_tiles<<<g.nchunks + (n6 + 3) / 4, 256, 0, s>>>(g);
+            // chunk workgroups, then b_p / b_schur rows (one wave each), then Hpp (one wave per
+            // (pose, upper component))
+            lba_schur_tiles<<<g.nchunks + (n6 + 3) / 4 + (21 * A.P + 3) / 4, 256, 0, s>>>(g);
             lprof_end(e, ph, "lba_schur_tiles");
             ph = lprof_begin(e);
             lba_schur_finish<<<g.npairs, 256, 0, s>>>(g);
@@ -1789,14 +1815,10 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
         } else {
             lba_set_ok<<<1, 1, 0, s>>>(g);
         }
-        // scalars[8..): the update's computeScale block sums, then the trial chi2 block sums
+        // scalars[8..): the trial's computeScale block sums, then its chi2 block sums (nbt each)
         ph = lprof_begin(e);
-        lba_update<<<nbu, 256, 0, s>>>(g, g.scalars + 8, nbp);
-        lprof_end(e, ph, "lba_update");
-        ph = lprof_begin(e);
-        lba_errors<<<nbe, 256, 0, s>>>(g, g.scalars + 8 + nbu, nbu, nbe, np, nq);   // + the LM decision
-        if (LBA_SEP_DECIDE) lba_decide<<<1, 64, 0, s>>>(g, nbu, nbe, np, nq);
-        lprof_end(e, ph, "lba_errors_decide");
+        lba_lin_points<true><<<nbt, 256, 0, s>>>(g, g.scalars + 8, g.scalars + 8 + nbt, nbl);
+        lprof_end(e, ph, "lba_update_errors");
     };
     mirror();
     lba_lm_init<<<1, 1, 0, s>>>(g, iterations, stop_at);
@@ -1805,8 +1827,15 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
     int chunk = iterations, slots = 0;
     LMState st{};
     while (true) {
-        for (int k = 0; k < chunk; k++) slot(slots + k == 0);
+        for (int k = 0; k < chunk; k++) slot(slots + k == 0, k > 0);
         slots += chunk;
+        {   // the chunk's last trial: its decision as a launch of its own (the state read back)
+            const int ph = lprof_begin(e);
+            Graph gd;
+            advance(gd);
+            lba_decide<<<1, 64, 0, s>>>(gd, nbt);
+            lprof_end(e, ph, "lba_decide");
+        }
         if (hipMemcpyAsync(e->h_lm, g.lm, sizeof(LMState), hipMemcpyDeviceToHost, s) != hipSuccess) return -3;
         if (!stop) {
             if (hipStreamSynchronize(s) != hipSuccess) return -3;
@@ -1817,7 +1846,7 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
                 const hipError_t q = hipEventQuery(e->ev_chunk);
                 if (q == hipSuccess) break;
                 if (q != hipErrorNotReady) return -3;
-                std::this_thread::yield();
+                for (int k = 0; k < 64; k++) __builtin_ia32_pause();   // stay on the core: a chunk is ~0.5 ms
             }
         }
         st = *e->h_lm;
@@ -1844,7 +1873,9 @@ int lba_create(lba_engine **out) {
         hipHostMalloc((void **)&e->h_lm, sizeof(LMState)) != hipSuccess ||
         hipHostMalloc((void **)&e->h_stop, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void **)&e->d_stop, e->h_stop, 0) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_chunk, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&e->ev_chunk, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_stage[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_stage[1], hipEventDisableTiming) != hipSuccess) {
         delete e;
         return ORBX_EDEVICE;
     }
@@ -1860,7 +1891,10 @@ void lba_destroy(lba_engine *e) {
     if (e->h_lm) (void)hipHostFree(e->h_lm);
     if (e->h_stop) (void)hipHostFree(e->h_stop);
     if (e->ev_chunk) (void)hipEventDestroy(e->ev_chunk);
-    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    for (int k = 0; k < 2; k++) {
+        if (e->h_stage[k]) (void)hipHostFree(e->h_stage[k]);
+        if (e->ev_stage[k]) (void)hipEventDestroy(e->ev_stage[k]);
+    }
     if (e->h_down) (void)hipHostFree(e->h_down);
     for (hipEvent_t ev : e->pool) (void)hipEventDestroy(ev);
     delete e;
@@ -1927,14 +1961,14 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     const size_t oep = ua.add(p->edge_pose, sizeof(int32_t) * ne), oeq = ua.add(p->edge_point, sizeof(int32_t) * ne),
                  oobs = ua.add(p->edge_obs, sizeof(float) * 3 * ne), oisg = ua.add(p->edge_inv_sigma2, sizeof(float) * ne),
                  ocam = ua.add(p->pose_cam, sizeof(float) * 5 * np);
-    if (upload_set(e, e->arenaA, ua, s) || e->E.ensure(sizeof(EdgeDev) * std::max(ne, 1)) ||
+    if (upload_set(e, 0, e->arenaA, ua, s) || e->E.ensure(sizeof(EdgeDev) * std::max(ne, 1)) ||
         e->err.ensure(sizeof(double) * 3 * std::max(ne, 1)) ||
         e->flags.ensure(std::max(ne, 1)) || e->scalars.ensure((8 + 2 * kRedBlocks) * sizeof(double)) ||
-        e->partial.ensure(sizeof(double) * 4 * kRedBlocks) || e->lm.ensure(sizeof(LMState)) || e->arrive.ensure(64))
+        e->partial.ensure(sizeof(double) * 4 * kRedBlocks) || e->lm.ensure(2 * sizeof(LMState)) || e->arrive.ensure(64))
         return ORBX_EDEVICE;
     LBA_CHK(hipMemsetAsync(e->err.p, 0, sizeof(double) * 3 * std::max(ne, 1), s));
     LBA_CHK(hipMemsetAsync(e->arrive.p, 0, 64, s));
-    LBA_CHK(hipMemsetAsync(e->lm.p, 0, sizeof(LMState), s));   // cur = 0: (T, X) hold the estimate
+    LBA_CHK(hipMemsetAsync(e->lm.p, 0, 2 * sizeof(LMState), s));   // cur = 0: (T, X) hold the estimate
     int cur = 0;
     *e->h_stop = 0u;
     Graph g{};
@@ -1951,14 +1985,17 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     g.err = e->err.as<double>();
     g.scalars = e->scalars.as<double>();
     g.partial = e->partial.as<double>();
-    g.lm = e->lm.as<LMState>();
+    g.lm_buf[0] = e->lm.as<LMState>();
+    g.lm_buf[1] = g.lm_buf[0] + 1;
+    g.lm = g.lm_buf[0];
+    g.lm_src = nullptr;
     // per optimize(): the active-set index arrays (and, for the second phase, the edges with their
     // robust kernels removed) in one upload
     auto setup = [&](ActiveSet &A, const std::vector<EdgeDev> *edges) -> int {
         const int Kpad = std::max(4, ((3 * A.Lm + 3) / 4) * 4);
         build_schur_tiles(A, Kpad);
         UploadSet ub;
-        const size_t o_act = ub.add(A.act), o_pose_hidx = ub.add(A.pose_hidx), o_point_hidx = ub.add(A.point_hidx),
+        const size_t o_pose_hidx = ub.add(A.pose_hidx), o_point_hidx = ub.add(A.point_hidx),
                      o_hpose = ub.add(A.hpose), o_hpoint = ub.add(A.hpoint), o_pt_start = ub.add(A.pt_start),
                      o_pt_items = ub.add(A.pt_items), o_ps_start = ub.add(A.ps_start), o_ps_items = ub.add(A.ps_items),
                      o_slot_pt = ub.add(A.slot_pt), o_slot_ph = ub.add(A.slot_ph);
@@ -1967,11 +2004,14 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         const size_t o_tp_ij = ub.add(A.tp_ij), o_tp_start = ub.add(A.tp_start), o_tp_rows = ub.add(A.tp_rows),
                      o_tp_chunk = ub.add(A.tp_chunk), o_tp_nch = ub.add(A.tp_nch);
         const size_t o_E = edges ? ub.add(*edges) : 0;
-        if (upload_set(e, e->arenaB, ub, s)) return -1;
+        if (upload_set(e, 1, e->arenaB, ub, s)) return -1;
         const int nact = (int)A.act.size();
-        g.act = at<int>(e->arenaB, o_act); g.nact = nact;
+        g.nact = nact;
         if (e->on.ensure(std::max(nact, 1)) || hipMemsetAsync(e->on.p, 1, std::max(nact, 1), s) != hipSuccess) return -1;
         g.on = e->on.as<uint8_t>();
+        if (e->E_lm.ensure(sizeof(EdgeDev) * std::max(nact, 1)) || e->on_lm.ensure(std::max(nact, 1))) return -1;
+        g.E_lm = e->E_lm.as<EdgeDev>();
+        g.on_lm = e->on_lm.as<uint8_t>();
         g.pose_hidx = at<int>(e->arenaB, o_pose_hidx); g.point_hidx = at<int>(e->arenaB, o_point_hidx);
         g.hpose = at<int>(e->arenaB, o_hpose); g.hpoint = at<int>(e->arenaB, o_hpoint);
         g.P = A.P; g.Lm = A.Lm;
@@ -2019,6 +2059,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
             hipMemsetAsync(g.Hs, 0, sizeof(double) * NP * NP, s) != hipSuccess ||
             hipMemsetAsync(g.x, 0, sizeof(double) * (6 * A.P + 3 * A.Lm + 8), s) != hipSuccess)
             return -1;
+        if (nact > 0) lba_gather_edges<<<nblk(nact), 256, 0, s>>>(g.E_lm, g.on_lm, g.E, g.pt_items, nact);
         // trial buffers start equal to the current estimate (inactive vertices never change)
         if (hipMemcpyAsync(cur ? g.T : g.T2, cur ? g.T2 : g.T, sizeof(Pose) * std::max(np, 1), hipMemcpyDeviceToDevice, s) != hipSuccess ||
             hipMemcpyAsync(cur ? g.X : g.X2, cur ? g.X2 : g.X, sizeof(double) * 3 * std::max(nq, 1), hipMemcpyDeviceToDevice, s) != hipSuccess)

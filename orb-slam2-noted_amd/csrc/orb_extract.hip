@@ -90,6 +90,14 @@ __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
+// bytes `sel` (0..3) of four dwords gathered into one dword (a0 -> byte 0 .. a3 -> byte 3)
+template <int SEL>
+__device__ __forceinline__ uint32_t gather_byte(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+    const uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0000u | (uint32_t)(SEL + 4) << 8 | (uint32_t)SEL);
+    const uint32_t hi = __builtin_amdgcn_perm(a3, a2, (uint32_t)(SEL + 4) << 24 | (uint32_t)SEL << 16 | 0x0c0cu);
+    return lo | hi;
+}
+
 __device__ __forceinline__ uint32_t resize_px_simd(int S0, int S1, int4 ry) {  // SSE2 lane arithmetic
     int x0 = S0 >> 4, y0 = S1 >> 4;
     x0 = min(max(x0, -32768), 32767);
@@ -124,6 +132,21 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
     int sp;
     const uint8_t *src = level_ptr(g, in, pyr, b, l - 1, &sp);
     const int cg = threadIdx.x & 31, dx0 = x0 + 4 * cg;
+    // the thread's output rows' table entries (r0, r1, b0, b1), loaded before the horizontal
+    // pass so their latency hides behind it
+    int4 ryv[RZ_TH / 8];
+#pragma unroll
+    for (int i = 0; i < RZ_TH / 8; i++) {
+        const int dy = y0 + (threadIdx.x >> 5) + 8 * i;
+        ryv[i] = ryt[min(dy, y1 - 1)];
+    }
+    // workgroup-uniform buffer descriptors over the source level and the output level: row
+    // offsets as 32-bit VGPR offsets (no per-row 64-bit address arithmetic, no flat loads)
+    // (the source descriptor starts at the dword holding the level's first byte: the input image of a
+    // batch may start at any byte)
+    const uint32_t s0 = (uint32_t)((uintptr_t)src & 3);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(src - s0), 0, 0x7fffffff, 0x00020000);
     // 1. horizontal pass
     {
         int2 c[4];
@@ -159,10 +182,10 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
             for (int u = 0; u < RZ_HJ; u++) {
                 const int j = jb + 8 * u;
                 if (j < nsr) {
-                    const uintptr_t a = (uintptr_t)(src + (long long)(sr0 + j) * sp + sxa);
-                    const uint32_t *pa = (const uint32_t *)(a & ~(uintptr_t)3);
-                    mis[u] = (int)(a & 3);
-                    D[u][0] = pa[0]; D[u][1] = pa[1]; D[u][2] = pa[2];
+                    const uint32_t a = (uint32_t)(sr0 + j) * (uint32_t)sp + (uint32_t)sxa + s0;
+                    mis[u] = (int)(a & 3u);
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rsrc, (int)(a & ~3u), 0, 0);
+                    D[u][0] = v[0]; D[u][1] = v[1]; D[u][2] = v[2];
                 }
             }
 #pragma unroll
@@ -194,25 +217,40 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
     __syncthreads();
     // 2. vertical pass
     uint8_t *dst = pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
+    const __amdgpu_buffer_rsrc_t rdst = __builtin_amdgcn_make_buffer_rsrc((void *)dst, 0, 0x7fffffff, 0x00020000);
     const int n = min(4, dw - dx0);
     if (n <= 0) return;
-    for (int dy = y0 + (threadIdx.x >> 5); dy < y1; dy += 8) {
-        const int4 ry = ryt[dy];   // r0, r1, b0, b1
+    const uint32_t bpl = (uint32_t)g.bp[l];
+#pragma unroll
+    for (int i = 0; i < RZ_TH / 8; i++) {
+        const int dy = y0 + (threadIdx.x >> 5) + 8 * i;
+        if (dy >= y1) break;
+        const int4 ry = ryv[i];   // r0, r1, b0, b1
         const uint4 A = rz_h[(ry.x - sr0) * 32 + cg], B = rz_h[(ry.y - sr0) * 32 + cg];
         const uint32_t S0[4] = {A.x, A.y, A.z, A.w}, S1[4] = {B.x, B.y, B.z, B.w};
         uint32_t out = 0;
+        if (!SIMD) {
+            // FixedPtCast (b0 S0 + b1 S1 + 2^21) >> 22 as byte 3 of 4 (b0 S0 + b1 S1) + 2^23: S <= 255 * 2^11
+            // and b0 + b1 = 2^11 keep the sum below 2^30, so two full-rate v_mad_u32_u24 per pixel and
+            // one byte gather per 4 pixels (the result is <= 255: no clamp)
+            const uint32_t b0 = (uint32_t)ry.z << 2, b1 = (uint32_t)ry.w << 2;
+            uint32_t t[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            // S < 2^20 (Q11 sums of bytes), weights <= 2^11: full-rate 24-bit multiplies
-            uint32_t v = min((__umul24(S0[k], (uint32_t)ry.z) + __umul24(S1[k], (uint32_t)ry.w) + (1u << 21)) >> 22, 255u);
-            if (SIMD && dx0 + k < g.rz_simd_end[l]) v = resize_px_simd((int)S0[k], (int)S1[k], ry);
-            out |= v << (8 * k);
-        }
-        uint8_t *drow = dst + (long long)dy * g.bp[l];
-        if (n == 4) {
-            *(uint32_t *)(drow + dx0) = out;
+            for (int k = 0; k < 4; k++) t[k] = __umul24(S0[k], b0) + (__umul24(S1[k], b1) + (1u << 23));
+            out = gather_byte<3>(t[0], t[1], t[2], t[3]);
         } else {
-            for (int k = 0; k < n; k++) drow[dx0 + k] = (uint8_t)(out >> (8 * k));
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t v = (__umul24(S0[k], (uint32_t)ry.z) + __umul24(S1[k], (uint32_t)ry.w) + (1u << 21)) >> 22;
+                if (dx0 + k < g.rz_simd_end[l]) v = resize_px_simd((int)S0[k], (int)S1[k], ry);
+                out |= v << (8 * k);
+            }
+        }
+        const uint32_t o = (uint32_t)dy * bpl + (uint32_t)dx0;
+        if (n == 4) {
+            __builtin_amdgcn_raw_buffer_store_b32(out, rdst, (int)o, 0, 0);
+        } else {
+            for (int k = 0; k < n; k++) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(out >> (8 * k)), rdst, (int)(o + k), 0, 0);
         }
     }
 }
@@ -261,6 +299,9 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 //     the survivors' keys (pack_key: x, y relative to minBorder, score M - 1).
 // No strength map leaves the workgroup.
 // ------------------------------------------------------------------------------------
+#ifndef ORBX_BOUNDS_CHECK
+#define ORBX_BOUNDS_CHECK 0
+#endif
 #define FB_TW 128
 #define FB_TH 16
 #define FB_SB (FB_TW + 8)   // staged bytes per tile row (cols x0-4 .. x0+131)
@@ -414,13 +455,6 @@ static __constant__ FbBlurTab c_fbblur = make_fb_blur_tab();
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-// bytes `sel` (0..3) of four dwords gathered into one dword (a0 -> byte 0 .. a3 -> byte 3)
-template <int SEL>
-__device__ __forceinline__ uint32_t gather_byte(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
-    const uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0000u | (uint32_t)(SEL + 4) << 8 | (uint32_t)SEL);
-    const uint32_t hi = __builtin_amdgcn_perm(a3, a2, (uint32_t)(SEL + 4) << 24 | (uint32_t)SEL << 16 | 0x0c0cu);
-    return lo | hi;
-}
 
 __device__ __forceinline__ long i8x8(uint32_t lo, uint32_t hi) { return (long)((unsigned long long)hi << 32 | lo); }
 
@@ -697,12 +731,16 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
             h0 = __builtin_amdgcn_readfirstlane(h0);
             // Invariant: a tile pixel is pushed at most once -- only a pixel's nonzero-scoring
             // polarity can be hot (step 3's comment; tlo >= 0), and a pixel has one entry per
-            // polarity -- so hcnt_sh <= FB_TW * FB_TH. The bound check keeps a future change to the
-            // pre-filter or the threshold clamp from writing past hlist silently (LDS writes out of
-            // range do not fault); step 5 reads min(hcnt_sh, capacity) entries.
+            // polarity -- so hcnt_sh <= FB_TW * FB_TH (hlist's size). A change to the pre-filter or to
+            // the threshold clamp must keep it: LDS writes out of range do not fault. ORBX_BOUNDS_CHECK
+            // builds (make variant VDEFS=-DORBX_BOUNDS_CHECK=1) trap on a violation; the product
+            // build does not pay the 5 VALU per chunk (1.4 % of the kernel, measured).
             const int ia = h0 + (int)lane_rank(ba), ib = h0 + na + (int)lane_rank(bb);
-            if (ha && ia < FB_TW * FB_TH) hlist[ia] = (uint16_t)pa;
-            if (hb && ib < FB_TW * FB_TH) hlist[ib] = (uint16_t)pb;
+#if ORBX_BOUNDS_CHECK
+            if ((ha && ia >= FB_TW * FB_TH) || (hb && ib >= FB_TW * FB_TH)) __builtin_trap();
+#endif
+            if (ha) hlist[ia] = (uint16_t)pa;
+            if (hb) hlist[ib] = (uint16_t)pb;
         };
         // a dummy position for idle halves: a tile pixel whose ring stays inside the staged rows
         constexpr int kIdle = 4;
@@ -730,7 +768,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     // 5. 3x3 NMS of the hot pixels at tlo against their in-cell neighbours (others score 0),
     // survivors appended to their cell's slot list
     {
-        const int htot = min(hcnt_sh, FB_TW * FB_TH);
+        const int htot = hcnt_sh;   // <= FB_TW * FB_TH (the invariant at push_hot)
         const uint8_t *m8 = (const uint8_t *)mt;
         const int hC = g.hcell[l], wC = g.wcell[l];
         const int ry_end = g.maxBY[l] - 3, rx_end = g.maxBX[l] - 3;

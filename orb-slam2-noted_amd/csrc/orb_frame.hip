@@ -264,6 +264,20 @@ __device__ __forceinline__ void min2_merge(uint32_t &k1, uint32_t &k2, uint32_t 
     k1 = lo;
     k2 = min(hi, min(k2, o2));
 }
+// (k1, k2) = the two smallest keys over the 16 lanes of each row: four DPP merge steps (lane ^ 1,
+// lane ^ 2, half-row mirror, row mirror) -- VALU latency per step instead of a ds_bpermute round
+// trip; every lane of a row ends with its row's pair
+template <int CTRL> __device__ __forceinline__ void min2_dpp_step(uint32_t &k1, uint32_t &k2) {
+    const uint32_t o1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)k1, CTRL, 0xF, 0xF, false);
+    const uint32_t o2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)k2, CTRL, 0xF, 0xF, false);
+    min2_merge(k1, k2, o1, o2);
+}
+__device__ __forceinline__ void min2_row(uint32_t &k1, uint32_t &k2) {
+    min2_dpp_step<0xB1>(k1, k2);    // quad_perm [1, 0, 3, 2]
+    min2_dpp_step<0x4E>(k1, k2);    // quad_perm [2, 3, 0, 1]
+    min2_dpp_step<0x141>(k1, k2);   // row_half_mirror
+    min2_dpp_step<0x140>(k1, k2);   // row_mirror
+}
 
 __global__ __launch_bounds__(256) void search_init_resolve_kernel(SearchArgs a, float *prev_xy, int *m12, int *nmatch) {
     extern __shared__ uint32_t rs_lds[];
@@ -271,14 +285,14 @@ __global__ __launch_bounds__(256) void search_init_resolve_kernel(SearchArgs a, 
     const int i1img = a.f1_base + a.f1_step * p, i2img = a.f2_base + a.f2_step * p;
     const int N1 = min(a.cnt[i1img], a.cap);
     const int n1s = min(N1, a.cap0);   // F1 keypoints with a list (octave 0 is a prefix)
-    // LDS: stage[stage_cap] u32 | pre[cap0 + 1] i32 | vMD[cap] u16 | v21[cap] i16 | M12[cap] i16 | bin[cap] i8
+    // LDS: stage[stage_cap] u32 | pre[cap0 + 1] i32 | vst[cap] u32 (vMatchedDistance u16 | vnMatches21
+    // i16 << 16: one load gives a candidate's both) | M12[cap] i16 | bin[cap] i8
     uint32_t *stage = rs_lds;
     int *pre = (int *)(stage + a.stage_cap);
-    uint16_t *vMD = (uint16_t *)(pre + a.cap0 + 1);
-    int16_t *v21 = (int16_t *)(vMD + a.cap);
-    int16_t *M12 = v21 + a.cap;
+    uint32_t *vst = (uint32_t *)(pre + a.cap0 + 1);
+    int16_t *M12 = (int16_t *)(vst + a.cap);
     int8_t *bin_of = (int8_t *)(M12 + a.cap);
-    for (int i = tid; i < a.cap; i += 256) { vMD[i] = 0xFFFF; v21[i] = -1; M12[i] = -1; bin_of[i] = -1; }
+    for (int i = tid; i < a.cap; i += 256) { vst[i] = 0xFFFFFFFFu; M12[i] = -1; bin_of[i] = -1; }
     const int *lc = a.lcnt + (long long)p * a.cap0;
     if (wv == 0) {   // exclusive prefix of list lengths
         int carry = 0;
@@ -311,38 +325,89 @@ __global__ __launch_bounds__(256) void search_init_resolve_kernel(SearchArgs a, 
         }
         __syncthreads();
         if (wv == 0) {
+            // The walk is one wave's dependent chain and shares its CU with other engines'
+            // VALU-bound extraction waves (C3 runs batches on three streams): issue priority keeps
+            // each of its instructions from queueing behind theirs
+            __builtin_amdgcn_s_setprio(3);
+            // The greedy walk, one F1 keypoint after another, as a software pipeline: the next
+            // keypoint's list entries and the (vMatchedDistance, vnMatches21) word of each of its
+            // candidates are loaded while this one is decided; the loads are issued after every
+            // earlier state write (in-order LDS), and the one write they can miss -- this
+            // keypoint's claim -- is patched in by comparing with the claimed index. Lists of up
+            // to 64 entries (the common case) reduce their two smallest (dist << 12 | position)
+            // keys with DPP inside each 16-lane row and a scalar merge over the rows in use.
+            auto load = [&](int i1, uint32_t &ent, uint32_t &st) {
+                const int n = i1 < e0 ? pre[i1 + 1] - pre[i1] : 0, o = i1 < e0 ? pre[i1] - pre[s0] : 0;
+                ent = lane < n ? stage[o + lane] : 0xFFFFFFFFu;
+                st = lane < n ? vst[ent & 0xFFFFu] : 0u;
+            };
+            uint32_t ent, st;
+            load(s0, ent, st);
             for (int i1 = s0; i1 < e0; i1++) {
                 const int n = pre[i1 + 1] - pre[i1], o = pre[i1] - pre[s0];
-                if (n == 0) continue;
+                if (n == 0) {
+                    load(i1 + 1, ent, st);
+                    continue;
+                }
                 uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;   // two smallest (dist << 12 | position)
-                for (int j = lane; j < n; j += 64) {
-                    const uint32_t ent = stage[o + j];
-                    const int i2 = (int)(ent & 0xFFFFu), dist = (int)((ent >> 16) & 0x1FFu);
-                    if (!((int)vMD[i2] <= dist)) min2_merge(k1, k2, (uint32_t)dist << 12 | (uint32_t)j, 0xFFFFFFFFu);
+                if (n <= 64) {
+                    if (lane < n) {
+                        const int dist = (int)((ent >> 16) & 0x1FFu);
+                        if (!((int)(st & 0xFFFFu) <= dist)) k1 = (uint32_t)dist << 12 | (uint32_t)lane;
+                    }
+                    min2_row(k1, k2);
+                    uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)k1, 0);
+                    uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)k2, 0);
+                    for (int row = 1; row < (n + 15) / 16; row++)
+                        min2_merge(r1, r2, (uint32_t)__builtin_amdgcn_readlane((int)k1, 16 * row),
+                                   (uint32_t)__builtin_amdgcn_readlane((int)k2, 16 * row));
+                    k1 = r1;
+                    k2 = r2;
+                } else {   // long list: per-lane pairs over 64-entry groups, then the butterfly
+                    for (int j = lane; j < n; j += 64) {
+                        const uint32_t e2 = stage[o + j];
+                        const int i2 = (int)(e2 & 0xFFFFu), dist = (int)((e2 >> 16) & 0x1FFu);
+                        if (!((int)(vst[i2] & 0xFFFFu) <= dist)) min2_merge(k1, k2, (uint32_t)dist << 12 | (uint32_t)j, 0xFFFFFFFFu);
+                    }
+                    for (int off = 32; off > 0; off >>= 1) {
+                        const uint32_t o1 = (uint32_t)__shfl_xor((int)k1, off, 64), o2 = (uint32_t)__shfl_xor((int)k2, off, 64);
+                        min2_merge(k1, k2, o1, o2);
+                    }
+                    k1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
+                    k2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k2);
                 }
-                for (int off = 32; off > 0; off >>= 1) {
-                    const uint32_t o1 = (uint32_t)__shfl_xor((int)k1, off, 64), o2 = (uint32_t)__shfl_xor((int)k2, off, 64);
-                    min2_merge(k1, k2, o1, o2);
+                // the winner's entry and state word, before the next keypoint's loads replace them
+                uint32_t went = 0, wst = 0;
+                if (k1 != 0xFFFFFFFFu) {
+                    const int jw = (int)(k1 & 0xFFFu);
+                    if (n <= 64) {
+                        went = (uint32_t)__builtin_amdgcn_readlane((int)ent, jw);
+                        wst = (uint32_t)__builtin_amdgcn_readlane((int)st, jw);
+                    } else {
+                        went = stage[o + jw];
+                        wst = vst[went & 0xFFFFu];
+                    }
                 }
+                load(i1 + 1, ent, st);   // issued after every earlier claim's writes
                 if (k1 == 0xFFFFFFFFu) continue;
                 const int bestDist = (int)(k1 >> 12);
                 const int bestDist2 = k2 == 0xFFFFFFFFu ? INT_MAX : (int)(k2 >> 12);
                 if (bestDist <= 50 && bestDist < (float)bestDist2 * a.nnratio) {   // TH_LOW, mfNNratio
-                    const uint32_t ent = stage[o + (int)(k1 & 0xFFFu)];
-                    const int bestIdx2 = (int)(ent & 0xFFFFu);
-                    const int prev = v21[bestIdx2];
+                    const int bestIdx2 = (int)(went & 0xFFFFu);
+                    const int prev = (int)(int16_t)(wst >> 16);
                     if (prev >= 0) nmatches--;
                     nmatches++;
+                    const uint32_t nst = (uint32_t)(uint16_t)bestDist | (uint32_t)(uint16_t)(int16_t)i1 << 16;
                     if (lane == 0) {
                         if (prev >= 0) M12[prev] = -1;
                         M12[i1] = (int16_t)bestIdx2;
-                        v21[bestIdx2] = (int16_t)i1;
-                        vMD[bestIdx2] = (uint16_t)bestDist;
-                        if (a.check_ori) bin_of[i1] = (int8_t)(ent >> 25);
+                        vst[bestIdx2] = nst;   // vMatchedDistance | vnMatches21 << 16
+                        if (a.check_ori) bin_of[i1] = (int8_t)(went >> 25);
                     }
-                    wave_lds_sync();
+                    if ((ent & 0xFFFFu) == (uint32_t)bestIdx2 && ent != 0xFFFFFFFFu) st = nst;   // patch the prefetch
                 }
             }
+            __builtin_amdgcn_s_setprio(0);
         }
         __syncthreads();
         s0 = e0;

@@ -189,7 +189,10 @@ def lib() -> C.CDLL:
             raise OrbslamError(f"{LIB_PATH} missing: build it with `make -C {PKG_ROOT}` "
                                "(or __graft_entry__.build())")
         L = C.CDLL(str(LIB_PATH))
+        ab = bool(os.environ.get("ORBSLAM_AMD_LIB"))   # an A/B or variant build may predate some entries
         for name, res, args in SIGNATURES:
+            if ab and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

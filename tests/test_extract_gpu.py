@@ -162,6 +162,30 @@ def test_batch_device_matches_single(amd, oracle_mod):
         _assert_same_kps(ex.fetch(i), ref.extract(imgs[i]), f"batch[{i}]")
 
 
+@pytest.mark.parametrize("h,w,pitch,off", [(333, 517, 517, 1), (333, 517, 519, 3), (240, 322, 322, 2)])
+def test_batch_device_unaligned(amd, oracle_mod, h, w, pitch, off):
+    """Images at any byte: an odd image stride (w * h odd), an odd row pitch and a batch starting
+    `off` bytes into the allocation put every image's first pixel, and its rows, at every
+    alignment modulo 4 (the level-1 resize reads its source rows as aligned dwords through a
+    buffer descriptor starting at the dword of the image's first byte)."""
+    import torch
+    n = 5
+    stride = pitch * (h - 1) + w + (1 if (pitch * (h - 1) + w) % 2 == 0 else 0)   # odd stride
+    imgs = [synth.textured_image(h, w, 90 + i) for i in range(n)]
+    buf = np.full(off + n * stride + 64, 0x5A, np.uint8)
+    for i, im in enumerate(imgs):
+        for y in range(h):
+            buf[off + i * stride + y * pitch: off + i * stride + y * pitch + w] = im[y]
+    dev = torch.from_numpy(buf).cuda()
+    ex = amd.BatchExtractor(800, 1.2, 8, 20, 7)
+    ex.reserve(w, h, n)
+    torch.cuda.synchronize()
+    ex.extract_device(dev.data_ptr() + off, n, w, h, pitch, stride)
+    ref = oracle_mod.Extractor(800, 1.2, 8, 20, 7)
+    for i in range(n):
+        _assert_same_kps(ex.fetch(i), ref.extract(imgs[i]), f"unaligned[{i}]")
+
+
 def test_large_batch_matches_oracle(amd, oracle_mod):
     """A bench-sized batch (160 images, more workgroups than the chip holds at once): every
     image must still equal the oracle."""
