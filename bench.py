@@ -356,10 +356,26 @@ def bench_c2(amd, args, dist, world, params, pool):
                            "traffic": ent.get("hbm_bytes_per_launch"), "avg_launch_ms": round(tot / n, 4),
                            "algorithmic_bytes_per_launch": round(BYTES_PER_STEREO_FRAME * per_launch),
                            "pairs_per_launch": per_launch, "pmc_source": pmc_note}
-        if ent.get("hbm_bytes_per_launch") is not None:
+        if ent.get("read_bytes_per_launch") is not None:
+            out["roofline"]["traffic_formula"] = (
+                "exact L2->fabric bytes per launch from the request-size counters: 32 RDREQ_32B + 64 RDREQ_64B + "
+                "128 RDREQ_128B + 64 WRREQ_64B + 32 (WRREQ - WRREQ_64B) (tools/pmc_reqsize.sh)")
+            out["roofline"]["traffic_read"] = ent["read_bytes_per_launch"]
+            out["roofline"]["traffic_write"] = ent["write_bytes_per_launch"]
+            out["roofline"]["read_factor_measured"] = ent.get("read_factor")
+            out["roofline"]["traffic_x2_rule"] = ent.get("hbm_bytes_per_launch_x2_rule")
+        elif ent.get("hbm_bytes_per_launch") is not None:
             out["roofline"]["traffic_formula"] = (f"(FETCH_SIZE x {ent.get('read_factor', 2.0)} + WRITE_SIZE) per launch, read factor "
                                                   "calibrated for this kernel's access pattern (profiles/fetch_calib.json)")
             out["roofline"]["traffic_x2_rule"] = ent.get("hbm_bytes_per_launch_x2_rule")
+        step_tr = (pmc or {}).get("__step_traffic__")
+        if step_tr:
+            # every dispatch of a step (request-size counters), against SURVEY §8d's algorithmic bytes
+            alg_step = BYTES_PER_STEREO_FRAME * B
+            out["roofline"]["step_traffic_bytes"] = step_tr
+            out["roofline"]["step_algorithmic_bytes"] = alg_step
+            out["roofline"]["step_traffic_ratio"] = round(step_tr / alg_step, 3)
+            out["roofline"]["step_traffic_gbs"] = round(step_tr / (ms_step / 1e3) / 1e9, 1)
         valu = ent.get("valu_insts_per_launch")
         if valu:   # the ceiling this integer kernel actually sits against
             out["roofline"]["valu_issue_frac"] = round(
@@ -371,7 +387,7 @@ def bench_c2(amd, args, dist, world, params, pool):
             # VALU instructions per dispatch x dispatches per step; the rocclr setup copies excluded)
             # x 4 cycles / (1024 SIMDs x 2.4 GHz), over this run's ms_per_step
             insts = sum(v["valu_insts_per_launch"] * v["launches"] / steps_prof for k, v in pmc.items()
-                        if k != "__stamp__" and not k.startswith("__amd_rocclr_copy") and "valu_insts_per_launch" in v)
+                        if k != "__stamp__" and isinstance(v, dict) and not k.startswith("__amd_rocclr_copy") and "valu_insts_per_launch" in v)
             out["roofline"]["step_valu_insts"] = int(insts)
             out["roofline"]["step_valu_issue_frac"] = round(
                 insts * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_CLOCK_HZ) / (ms_step / 1e3), 4)
@@ -915,6 +931,8 @@ def load_pmc_doc(fname: str, build_id: str, **expect):
             return None, f"profiles/{fname} stamp {k}={stamp.get(k)}, this run {k}={v}: counters not reported"
     kern = {kernel_base(k): v for k, v in doc.get("kernels", {}).items()}
     kern["__stamp__"] = stamp
+    if doc.get("step_traffic_bytes"):
+        kern["__step_traffic__"] = doc["step_traffic_bytes"]
     return kern, f"profiles/{fname} (src_hash {build_id}, commit {stamp.get('commit')})"
 
 

@@ -3,7 +3,8 @@
 # GIT_HEAD=<commit> in the environment):
 #   1. C2-only rocprofv3 --kernel-trace --stats (the bench line's kernel durations; no isolated
 #      or alternate-resize launches, so the CSV average is the line's avg_launch_ms)
-#   2. C2-only PMC passes FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU, one counter per pass
+#   2. C2-only PMC passes FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU, one counter per pass, and the
+#      three request-size passes of tools/pmc_reqsize.sh (exact read / write bytes per kernel)
 #      -> gpurun_out/pmc_traffic.json (stamped: tools/stamp.py)
 #   3. LocalBA MFMA PMC pass + its kernel stats -> gpurun_out/lba_pmc.json (stamped)
 # Copy gpurun_out/{pmc_traffic,lba_pmc}.json and the stats CSVs into profiles/ afterwards.
@@ -25,7 +26,9 @@ for s in $STEPS; do
         timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $ctr -d "$O/m_pmc_$ctr" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-profile $C2ONLY ${BENCH_ARGS:-} > /dev/null 2> "$O/m_pmc_$ctr.err"
         rc=$?; echo "pmc $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done
-      STEPS_PROFILED=4 python3 "$R/tools/pmc_summary.py" "$O/m_pmc_FETCH_SIZE" "$O/m_pmc_WRITE_SIZE" 128 "$O/pmc_traffic.json" "$O/m_pmc_SQ_INSTS_VALU" > /dev/null
+      bash "$R/tools/pmc_reqsize.sh" m python3 "$R/bench.py" --steps 3 --warmup 1 --no-profile $C2ONLY ${BENCH_ARGS:-}
+      rc=$?; echo "pmc reqsize rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      REQSIZE_DIR="$O" REQSIZE_TAG=m STEPS_PROFILED=4 python3 "$R/tools/pmc_summary.py" "$O/m_pmc_FETCH_SIZE" "$O/m_pmc_WRITE_SIZE" 128 "$O/pmc_traffic.json" "$O/m_pmc_SQ_INSTS_VALU" > /dev/null
       rc=$?; echo "pmc summary rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     lba)
       timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/m_lba_stats" -o run -- python3 "$R/tools/lba_prof.py" 5 > "$O/m_lba_stats.txt" 2>&1
