@@ -562,8 +562,9 @@ def bench_localba(amd, args, dist, world, with_cpu):
            "localba": {"ms_per_call": round(1000 * dt / args.lba_steps, 3), "edges": int(len(prob["edge_point"])),
                        "keyframes": 20, "map_points": 3000, "lm_iterations": list(r["iterations"]),
                        "lm_trials": list(r["trials"]),
-                       "dtype": "f64", "lm_control": "device-resident LM state, decided by a one-block lba_decide launch "
-                                                     "after lba_errors; one host readback per chunk of trials",
+                       "dtype": "f64", "lm_control": "device-resident LM state (ping-pong buffers): each trial's decision runs "
+                                                     "inside the next trial's lba_reduce_points, the chunk's last in a "
+                                                     "one-block lba_decide; one host readback per chunk of trials",
                        "map_snapshot_bytes": map_bytes,
                        "map_source": (f"rank 0, {'RCCL' if DIST_BACKEND == 'nccl' else DIST_BACKEND} broadcast"
                                       if dist is not None else "local")}}
