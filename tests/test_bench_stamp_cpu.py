@@ -59,3 +59,38 @@ def test_committed_summaries_are_stamped(fname):
     assert len(st["src_hash"]) == 16 and int(st["src_hash"], 16) >= 0
     assert st["commit"] and st["commit"] != "unknown"
     assert doc["kernels"]
+
+
+def _counter_csv(d: Path, rows):
+    d.mkdir(parents=True)
+    lines = ["Kernel_Name,Counter_Name,Counter_Value"] + [f'"{k}",{c},{v}' for k, c, v in rows]
+    (d / "run_counter_collection.csv").write_text("\n".join(lines) + "\n")
+
+
+def test_reqsize_summary_bytes(tmp_path):
+    """Exact traffic from the request-size passes: 32/64/128-B read requests and 64-B / other write
+    requests, averaged per dispatch (tools/reqsize_summary.py)."""
+    import sys
+    sys.path.insert(0, str(ROOT / "tools"))
+    from reqsize_summary import summarize
+    k = "void orbamd::fast_blur_kernel<false>(orbamd::ExtractGeom, ...)"
+    _counter_csv(tmp_path / "rq_t_rd32_64", [(k, "TCC_EA0_RDREQ_32B", 10), (k, "TCC_EA0_RDREQ_64B", 100),
+                                               (k, "TCC_EA0_RDREQ_32B", 30), (k, "TCC_EA0_RDREQ_64B", 300)])
+    _counter_csv(tmp_path / "rq_t_rd128_all", [(k, "TCC_EA0_RDREQ_128B", 1000), (k, "TCC_EA0_RDREQ", 1220),
+                                                (k, "TCC_EA0_RDREQ_128B", 1000), (k, "TCC_EA0_RDREQ", 1220)])
+    _counter_csv(tmp_path / "rq_t_wr", [(k, "TCC_EA0_WRREQ", 500), (k, "TCC_EA0_WRREQ_64B", 400)])
+    e = summarize(tmp_path, "t")["fast_blur_kernel<false>"]
+    assert e["launches"] == 2
+    assert e["read_bytes"] == 32 * 20 + 64 * 200 + 128 * 1000
+    assert e["write_bytes"] == 64 * 400 + 32 * 100
+    assert e["traffic_bytes"] == e["read_bytes"] + e["write_bytes"]
+    assert e["fetch_size_equiv_bytes"] == 64 * 1220
+
+
+def test_step_traffic_published(profiles):
+    """A summary carrying step_traffic_bytes (every dispatch of a step) hands it to the bench line."""
+    (Path(bench.ROOT) / "profiles" / "p.json").write_text(json.dumps(
+        {"stamp": {"src_hash": "abc", "commit": "c0ffee", "batch": 128}, "step_traffic_bytes": 12345,
+         "kernels": {"k": {"read_bytes_per_launch": 1, "write_bytes_per_launch": 2}}}))
+    kern, _ = bench.load_pmc_doc("p.json", "abc", batch=128)
+    assert kern["__step_traffic__"] == 12345 and kern["k"]["write_bytes_per_launch"] == 2
