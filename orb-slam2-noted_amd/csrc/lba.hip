@@ -825,7 +825,7 @@ template <int C> __device__ __forceinline__ double row_bcast(double v) {
 }
 
 #ifndef LBA_RSQ_NEWTON
-#define LBA_RSQ_NEWTON 2   // Newton steps after v_rsq_f64 on the pivot (the diagonal chain's latency)
+#define LBA_RSQ_NEWTON 1   // Newton steps after v_rsq_f64 on the pivot (the diagonal chain's latency; 2: 0.5 us per trial slower, same LM path, profiles/r04_ab_lba_rsq1.log)
 #endif
 #ifndef LBA_DIAG_PRIO
 #define LBA_DIAG_PRIO 0    // s_setprio of wave 0 while it factors a diagonal tile (critical path)
