@@ -658,7 +658,7 @@ def bench_rgbd(amd, args, dist, world):
                    "hbm_frac": round(fps / world * bpf / 1e9 / HBM_PEAK_GBS, 6),
                    "note": "GB/s per GPU of SURVEY §8d's compulsory bytes (640x480 u8 in, 1000 x 60 B keypoints + "
                            "descriptors out, 1000 x 12 B depth gather + uR / depth out); the rocprofv3 summary of "
-                           "this leg alone is profiles/r02_kernel_stats_c3.csv (bench.py --no-c2)"}}
+                           "this leg alone is profiles/r04_kernel_stats_c3.csv (tools/gpu_c3_sweep.sh)"}}
 
 
 def bench_track(amd, args, dist, world, with_cpu):
@@ -1064,9 +1064,12 @@ def main():
     ap.add_argument("--lba-steps", type=int, default=10, help="timed LocalBA calls (C4 graph)")
     ap.add_argument("--no-lba", action="store_true")
     ap.add_argument("--rgbd-batch", type=int, default=256)
-    ap.add_argument("--rgbd-steps", type=int, default=10)
-    ap.add_argument("--rgbd-engines", type=int, default=3,
-                    help="engines the C3 batches alternate over (one HIP stream each; 1: 167.6k, 2: 199k, 3: 204k frames/s)")
+    ap.add_argument("--rgbd-steps", type=int, default=40,
+                    help="timed C3 batches (10 timed batches read 3-4 %% low: the pipeline fill and drain of the "
+                         "engines weigh on a 11 ms region; profiles/r04_c3_sweep.log)")
+    ap.add_argument("--rgbd-engines", type=int, default=4,
+                    help="engines the C3 batches alternate over (one HIP stream each; round 4, 40 batches: "
+                         "2: 217k, 3: 230-233k, 4: 236-237k frames/s, profiles/r04_c3_sweep.log)")
     ap.add_argument("--no-rgbd", action="store_true")
     ap.add_argument("--track-batch", type=int, default=256)
     ap.add_argument("--track-steps", type=int, default=10)
