@@ -476,8 +476,11 @@ __device__ __forceinline__ void fast_blur_mfma(const uint32_t *tin, uint8_t *dst
     const uint32_t XM = 0x80808080u;
     const int KH = 128 * 257 + 128;
     const i32x4 z = {0, 0, 0, 0}, kh = {KH, KH, KH, KH};
+    // blocks past the level's right edge hold no output column (the last tile of a row: 10 % of the
+    // tile area over C2's levels, 16 % over C3's) -- not computed
+    const int xbe = min(xb1, (w - x0 + 15) >> 4);
 #pragma unroll
-    for (int xb = xb0; xb < xb1; xb++) {   // wave-uniform range of 16-column blocks
+    for (int xb = xb0; xb < xbe; xb++) {   // wave-uniform range of 16-column blocks
         const int c = 16 * xb + 8 * gq;
         const uint2 a0 = *(const uint2 *)(t8 + r0 * FB_LW + c);
         const uint2 a1 = *(const uint2 *)(t8 + r1 * FB_LW + c);
@@ -541,7 +544,13 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     if (threadIdx.x < 255) {
         const int rr0 = (threadIdx.x * 241) >> 12, jj = threadIdx.x - 17 * rr0;   // tid / 17 for tid < 255
         const int xs = x0 - 4 + 8 * jj;
-        const bool fast = xs >= 0 && xs + 7 < w;
+        // a pair wholly past column w + 3 feeds no output: the blur of column x < w reads up to x + 4,
+        // the FAST ring and the pre-filter stop inside the detection region (x < w - 19). Not staged
+        // (its LDS bytes only meet the masked outputs of a partial blur block), so the right edge's
+        // reflected per-byte path runs for the one or two pairs that straddle w instead of every
+        // pair of the tile's overhang
+        const bool skip = xs > w + 3;
+        const bool fast = skip || (xs >= 0 && xs + 7 < w);
         auto row_of = [&](int rr) {
             int yy = y0 - 4 + rr;
             yy = yy < 0 ? -yy : yy;
@@ -560,11 +569,13 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
                 p0 = row_of(rr0) + xs;
                 p1 = row_of(min(rr0 + 15, FB_TH + 7)) + xs;
             }
-            __builtin_memcpy(&v0, p0, 8);
-            if (two) __builtin_memcpy(&v1, p1, 8);
-            *(uint2 *)&tin[rr0 * FB_LD + 2 * jj] = v0;
-            if (two) *(uint2 *)&tin[(rr0 + 15) * FB_LD + 2 * jj] = v1;
-        } else {
+            if (!skip) {
+                __builtin_memcpy(&v0, p0, 8);
+                if (two) __builtin_memcpy(&v1, p1, 8);
+                *(uint2 *)&tin[rr0 * FB_LD + 2 * jj] = v0;
+                if (two) *(uint2 *)&tin[(rr0 + 15) * FB_LD + 2 * jj] = v1;
+            }
+        } else if (!skip) {
             for (int rr = rr0; rr < FB_TH + 8; rr += 15) {
                 const uint8_t *rowp = row_of(rr);
                 uint2 v;
