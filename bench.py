@@ -1117,7 +1117,10 @@ def main():
     torch.cuda.set_device(device)
     torch.cuda.init()
     dist = None
-    if world > 1:
+    # ORBSLAM_DIST_FORCE=1: the process group (and every collective of the multi-rank path: the shared
+    # parameters, the LocalBA map broadcast, the max-over-ranks timing) at world size 1 too -- the RCCL
+    # path on the one GPU of a test box (tests/test_c5_rehearsal_gpu.py::test_rccl_single_rank)
+    if world > 1 or os.environ.get("ORBSLAM_DIST_FORCE") == "1":
         import torch.distributed as dist
         if DIST_BACKEND == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
@@ -1145,7 +1148,7 @@ def main():
         "dist_backend": (("rccl (torch nccl)" if DIST_BACKEND == "nccl" else DIST_BACKEND) if dist is not None
                          else None),
         "launch": ("bench.py self-launch (torch.distributed.run child)" if os.environ.get("ORBSLAM_BENCH_LAUNCH") == "self"
-                   else "external torch.distributed.run" if world > 1 else "single process"),
+                   else "external torch.distributed.run" if dist is not None else "single process"),
         "rank_devices": topo})
     if not args.no_e2e and not args.no_c2:
         out.update(bench_e2e(amd, args, pool, bf, mb))
