@@ -77,7 +77,8 @@ struct LMState {
     int cur;        // estimate buffers: cur = 0 -> (T, X) current, (T2, X2) trial; 1 -> swapped
     int stop_at;    // test hook: pbStopFlag counts as raised once `trials` reaches it (INT_MAX: never)
     int seen;       // a terminate() check of this optimize() found pbStopFlag raised
-    int pad;
+    int gate;       // the second optimize()'s start (lba_phase2_begin): 0 run, 1 deferred (enqueued before the
+                    // first optimize() had ended), 2 skipped (bDoMore false, Optimizer.cc:913-917)
 };
 
 struct EdgeDev {
@@ -1265,6 +1266,33 @@ __global__ void lba_lm_init(Graph g, int iterations, int stop_at) {
     *g.lm = s;
 }
 
+// The second optimize()'s start, reading the first one's final state p1 on the device, so it can be
+// enqueued behind the first one's chunk without a host round trip (lba_solve): `spec` and p1 not
+// yet done -> deferred (every launch of the enqueued phase-2 chunk is a no-op, the host re-enqueues
+// the phase after the first one's retries); bDoMore false -- pbStopFlag raised, or the test hook's
+// trial reached in the first optimize() (Optimizer.cc:913-917) -> skipped; else lba_lm_init's reset
+// and first terminate() check, with the estimate buffer carried over (p1->cur).
+__global__ void lba_phase2_begin(Graph g, const LMState *p1, int iterations, int stop_at, int spec) {
+    const LMState s1 = *p1;
+    LMState s{};
+    s.cur = s1.cur;
+    s.ni = 2;
+    s.iterations = iterations;
+    s.newiter = 1;
+    s.stop_at = stop_at;
+    if (spec && !s1.done) {
+        s.done = 1;
+        s.gate = 1;
+    } else if (__hip_atomic_load(g.stopf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u || s1.trials >= s1.stop_at) {
+        s.done = 1;
+        s.gate = 2;
+    } else {
+        s.done = iterations <= 0;
+        if (!s.done && stop_raised(g, s)) s.seen = s.done = 1;
+    }
+    *g.lm = s;
+}
+
 // End of one LM trial (optimization_algorithm_levenberg.cpp:96-164 + the ORB-SLAM2 stop rule
 // :155-161): wave 0 sums the update's computeScale block sums and the trial chi2 block sums,
 // thread 0 decides and advances the state; an accepted trial becomes the current estimate by
@@ -1390,9 +1418,14 @@ __global__ __launch_bounds__(256) void lba_build_edges(EdgeDev *E, int ne, const
 }
 
 // outlier test of Optimizer.cc:925-962 / 977-1008: chi2 (stale _error) + depth sign
+// the call's results packed for one download: the estimate's poses (nT doubles), points (nX
+// doubles) and the erase flags of every edge, each thread one double of T, one of X and one flag
 __global__ __launch_bounds__(256) void lba_outliers(const EdgeDev *E, const double *err, const Pose *T,
-                                                    const double *X, int ne, uint8_t *flag) {
+                                                    const double *X, int ne, int nT, int nX, double *outT,
+                                                    double *outX, uint8_t *flag) {
     const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k < nT) outT[k] = ((const double *)T)[k];
+    if (k < nX) outX[k] = X[k];
     if (k >= ne) return;
     const EdgeDev e = E[k];
     const double *er = err + 3 * k;
@@ -1403,6 +1436,46 @@ __global__ __launch_bounds__(256) void lba_outliers(const EdgeDev *E, const doub
     flag[k] = (chi > th || !(p[2] > 0.0)) ? 1 : 0;
 }
 
+// The per-call buffer initialisation in one launch (was seven memsets and two device copies, each
+// a launch of its own on the path to the first LM trial): range r = blockIdx.y fills `bytes` bytes
+// at dst with the byte `value`, or copies them from src. dst / src 16-byte aligned (hipMalloc /
+// 256-byte arena offsets); the tail past the last 16-byte chunk byte by byte.
+struct InitRange { void *dst; const void *src; unsigned long long bytes; int value, pad; };
+constexpr int kInitRanges = 10;
+struct InitRanges { InitRange r[kInitRanges]; };
+__global__ __launch_bounds__(256) void lba_init_buffers(InitRanges R) {
+    // fields read with constant indices only (a dynamic index copies the argument to scratch)
+    void *dst = nullptr;
+    const void *src = nullptr;
+    unsigned long long bytes = 0;
+    int value = 0;
+    switch (blockIdx.y) {
+#define LBA_INIT_CASE(i) \
+    case i: dst = R.r[i].dst; src = R.r[i].src; bytes = R.r[i].bytes; value = R.r[i].value; break;
+        LBA_INIT_CASE(0) LBA_INIT_CASE(1) LBA_INIT_CASE(2) LBA_INIT_CASE(3) LBA_INIT_CASE(4)
+        LBA_INIT_CASE(5) LBA_INIT_CASE(6) LBA_INIT_CASE(7) LBA_INIT_CASE(8) LBA_INIT_CASE(9)
+#undef LBA_INIT_CASE
+        default: return;
+    }
+    static_assert(kInitRanges == 10, "one case per range");
+    const InitRange q = {dst, src, bytes, value, 0};
+    const unsigned long long n16 = q.bytes >> 4;
+    const unsigned v8 = (unsigned)(q.value & 0xFF) * 0x01010101u;
+    const uint4 fill = make_uint4(v8, v8, v8, v8);
+    // two loops, not a select: `src ? src[i] : fill` becomes a load through a pointer select, and
+    // `fill` a private (scratch) variable
+    const unsigned long long i0 = (unsigned long long)blockIdx.x * 256 + threadIdx.x, di = (unsigned long long)gridDim.x * 256;
+    if (q.src) {
+        for (unsigned long long i = i0; i < n16; i += di) ((uint4 *)q.dst)[i] = ((const uint4 *)q.src)[i];
+    } else {
+        for (unsigned long long i = i0; i < n16; i += di) ((uint4 *)q.dst)[i] = fill;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (q.bytes & 15)) {
+        const unsigned long long b = (n16 << 4) + threadIdx.x;
+        ((uint8_t *)q.dst)[b] = q.src ? ((const uint8_t *)q.src)[b] : (uint8_t)q.value;
+    }
+}
+
 // Optimizer.cc:925-962 between the two optimize() calls, on the device: the outlier test of every
 // active edge against the current estimate (stale _error, depth sign) moves it to level 1 (on = 0)
 // and every edge drops its robust kernel. The second optimize() then runs over the same slots,
@@ -1411,6 +1484,7 @@ __global__ __launch_bounds__(256) void lba_outliers(const EdgeDev *E, const doub
 // update -- the results g2o gives by leaving it out of initializeOptimization(0).
 __global__ __launch_bounds__(256) void lba_phase2_mark(Graph g, EdgeDev *E, uint8_t *on, int ne) {
     const int s = blockIdx.x * 256 + threadIdx.x;
+    if (g.lm->gate != 0) return;   // lba_phase2_begin: the second optimize() does not run (now)
     if (s < g.nact) {
         const int k = s;   // every edge is active in slot order (build_active)
         const bool cur = g.lm->cur;
@@ -1464,7 +1538,7 @@ struct lba_engine {
         ps_start, ps_items, slot_pt, slot_ph, con, hpl, Hll, bl, Hpp, bp, Dinv, Lc, Y, ywp, on, tp_part, Hs, bs, x, partial,
         scalars, flags, lm, arrive, arenaA, arenaB;
     double *h_scalars = nullptr;  // pinned
-    LMState *h_lm = nullptr;      // pinned
+    LMState *h_lm = nullptr;      // pinned, one per optimize() of a call
     void *h_stage[2] = {nullptr, nullptr};   // pinned upload staging per arena (grow-only)
     size_t h_stage_bytes[2] = {0, 0};
     hipEvent_t ev_stage[2] = {nullptr, nullptr};   // the last DMA out of each staging buffer
@@ -1475,7 +1549,7 @@ struct lba_engine {
     // keeps equal to the caller's flag while a chunk of trials runs (lba_optimize)
     unsigned *h_stop = nullptr;
     unsigned *d_stop = nullptr;
-    hipEvent_t ev_chunk = nullptr;
+    hipEvent_t ev_chunk[2] = {nullptr, nullptr};   // per optimize(): its last chunk's state readback
     int hook_phase = 0, hook_trial = 0;   // lba_set_stop_hook
     // per-kernel hipEvent timing on the engine stream (lba_profile; bench.py localba roofline)
     bool prof = false;
@@ -1731,40 +1805,57 @@ int nblk(int n) { return std::max(1, (n + 255) / 256); }
 
 }  // namespace
 
-// One SparseOptimizer::optimize(iterations) on the device; returns iterations run.
-// Trial slots (linearisation + setLambda/Schur/solve/update/errors + lba_decide) are enqueued
-// in chunks without host synchronisation; the device LM state turns the slots after the
-// last trial into no-ops. One state readback per chunk. pbStopFlag is read by the device itself,
-// at every point where g2o reads it (lba_lm_init, lm_decide): while a chunk runs, the host loop
-// copies *stop into the mapped word the kernels load with system scope, so a flag raised mid-call
-// ends the optimisation after the trial in flight, as SparseOptimizer::terminate() does.
+// One SparseOptimizer::optimize(iterations) on the device (LmPhase): trial slots (linearisation +
+// setLambda/Schur/solve/update/errors, each decided inside the next slot's lba_reduce_points) are
+// enqueued in chunks without host synchronisation; the device LM state turns the slots after the
+// last trial into no-ops. Each chunk ends with a one-block lba_decide, an async readback of the
+// state and an event; the host polls the event. pbStopFlag is read by the device itself, at every
+// point where g2o reads it (the optimize() start, lm_next): while a chunk runs, the host loop copies
+// *stop into the mapped word the kernels load with system scope, so a flag raised mid-call ends the
+// optimisation after the trial in flight, as SparseOptimizer::terminate() does.
 // stop_at: the test hook's trial count for this optimize() (INT_MAX: none).
-static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterations, int np, int nq,
-                        const volatile uint8_t *stop, int stop_at, double *final_chi, int *trials, int *cur,
-                        int *seen) {
-    hipStream_t s = e->stream;
-    auto mirror = [&]() {
+#ifndef LBA_SPEC_PHASE2
+#define LBA_SPEC_PHASE2 1   // phase 2 enqueued behind phase 1's first chunk (lba_solve)
+#endif
+struct LmPhase {
+    lba_engine *e;
+    Graph &g;
+    const ActiveSet &A;
+    int iterations;
+    const volatile uint8_t *stop;
+    int stop_at;
+    LMState *h_state;     // pinned readback of this phase's state
+    hipEvent_t ev;        // end of the last chunk's readback
+    hipStream_t s;
+    int nact = 0, n6 = 0, nbl = 0, nbt = 0, slots = 0, rc = 0;
+    LmPhase(lba_engine *e_, Graph &g_, const ActiveSet &A_, int iterations_, const volatile uint8_t *stop_, int stop_at_,
+            LMState *h_state_, hipEvent_t ev_)
+        : e(e_), g(g_), A(A_), iterations(iterations_), stop(stop_), stop_at(stop_at_), h_state(h_state_), ev(ev_),
+          s(e_->stream) {
+        if (A.P + A.Lm == 0) { rc = -1; return; }
+        if (A.P > kMaxPoses) { rc = -2; return; }
+        if ((A.Lm + kRPL - 1) / kRPL > kRedBlocks) { rc = -2; return; }   // partial regions
+        nact = (int)A.act.size();
+        n6 = 6 * A.P;
+        // lba_lin_points workgroups: landmarks (kLPB each), then free poses (256 each); its chi2 and
+        // computeScale block sums are the partials every reduction of the LM state reads (nbt of each)
+        nbl = std::max(1, (A.Lm + kLPB - 1) / kLPB);
+        nbt = nbl + nblk(A.P);
+        if (nbt > kRedBlocks) rc = -2;
+    }
+    void mirror() {
         if (stop) __atomic_store_n(e->h_stop, (unsigned)(*stop != 0), __ATOMIC_RELAXED);
-    };
-    if (A.P + A.Lm == 0) return -1;
-    if (A.P > kMaxPoses) return -2;
-    if ((A.Lm + kRPL - 1) / kRPL > kRedBlocks) return -2;   // partial regions
-    const int nact = (int)A.act.size();
-    const int n6 = 6 * A.P;
-    // lba_lin_points workgroups: landmarks (kLPB each), then free poses (256 each); its chi2 and
-    // computeScale block sums are the partials every reduction of the LM state reads (nbt of each)
-    const int nbl = std::max(1, (A.Lm + kLPB - 1) / kLPB), nbt = nbl + nblk(A.P);
-    if (nbt > kRedBlocks) return -2;
+    }
     // the LM state ping-pongs between g.lm_buf[0 / 1] at every decision: a deciding launch reads one
     // buffer and writes the other, and every later launch reads the new one
-    auto advance = [&](Graph &gd) {
+    void advance(Graph &gd) {
         gd = g;
         gd.lm_src = g.lm;
         gd.lm = g.lm == g.lm_buf[0] ? g.lm_buf[1] : g.lm_buf[0];
         g.lm = gd.lm;
-    };
-    // `decide`: the previous trial of this chunk is undecided; this slot's lba_reduce_points decides it
-    auto slot = [&](bool first, bool decide) {
+    }
+    void slot(bool first, bool decide) {
+        // `decide`: the previous trial of this chunk is undecided; this slot's lba_reduce_points decides it
         int ph;
         if (first) {   // later iterations start from the linearisation of the accepted trial
             ph = lprof_begin(e);
@@ -1819,47 +1910,63 @@ static int lba_optimize(lba_engine *e, Graph &g, const ActiveSet &A, int iterati
         ph = lprof_begin(e);
         lba_lin_points<true><<<nbt, 256, 0, s>>>(g, g.scalars + 8, g.scalars + 8 + nbt, nbl);
         lprof_end(e, ph, "lba_update_errors");
-    };
-    mirror();
-    lba_lm_init<<<1, 1, 0, s>>>(g, iterations, stop_at);
-    // first chunk: one trial per iteration (the common case: every first trial accepted); then
-    // two slots per chunk while retries remain
-    int chunk = iterations, slots = 0;
-    LMState st{};
-    while (true) {
-        for (int k = 0; k < chunk; k++) slot(slots + k == 0, k > 0);
-        slots += chunk;
-        {   // the chunk's last trial: its decision as a launch of its own (the state read back)
+    }
+    // optimize() start (levenberg.cpp:66-72 reset, the first terminate() check)
+    void init() {
+        mirror();
+        lba_lm_init<<<1, 1, 0, s>>>(g, iterations, stop_at);
+    }
+    // k trial slots of the open chunk (`chunk0`: the first slot of the chunk's enqueue)
+    int chunk0 = 0;
+    void enqueue_slots(int k) {
+        for (int i = 0; i < k; i++) slot(slots + i == 0, slots + i > chunk0);
+        slots += k;
+    }
+    // k trial slots, the chunk's last decision, the state readback and the chunk's event
+    int enqueue_chunk(int k) {
+        chunk0 = slots;
+        enqueue_slots(k);
+        return close_chunk();
+    }
+    int close_chunk() {
+        {
             const int ph = lprof_begin(e);
             Graph gd;
             advance(gd);
             lba_decide<<<1, 64, 0, s>>>(gd, nbt);
             lprof_end(e, ph, "lba_decide");
         }
-        if (hipMemcpyAsync(e->h_lm, g.lm, sizeof(LMState), hipMemcpyDeviceToHost, s) != hipSuccess) return -3;
+        if (hipMemcpyAsync(h_state, g.lm, sizeof(LMState), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipEventRecord(ev, s) != hipSuccess)
+            return -3;
+        return 0;
+    }
+    // wait for the last chunk's readback, keeping the device's copy of the flag current
+    int wait(LMState &st) {
         if (!stop) {
-            if (hipStreamSynchronize(s) != hipSuccess) return -3;
-        } else {   // poll the chunk, keeping the device's copy of the flag current
-            if (hipEventRecord(e->ev_chunk, s) != hipSuccess) return -3;
+            if (hipEventSynchronize(ev) != hipSuccess) return -3;
+        } else {
             while (true) {
                 mirror();
-                const hipError_t q = hipEventQuery(e->ev_chunk);
+                const hipError_t q = hipEventQuery(ev);
                 if (q == hipSuccess) break;
                 if (q != hipErrorNotReady) return -3;
                 for (int k = 0; k < 64; k++) __builtin_ia32_pause();   // stay on the core: a chunk is ~0.5 ms
             }
         }
-        st = *e->h_lm;
-        if (st.done) break;
-        if (slots > 10 * iterations + 1) return -3;   // cannot happen: <= 10 trials per iteration
-        chunk = 2;
+        st = *h_state;
+        return 0;
     }
-    *final_chi = st.final_chi;
-    *trials = st.trials;
-    *cur = st.cur;
-    *seen = st.seen;
-    return st.it;
-}
+    // two slots per chunk while retries remain (the first chunk holds one trial per iteration: the
+    // common case, every first trial accepted)
+    int finish(LMState &st) {
+        while (!st.done) {
+            if (slots > 10 * iterations + 1) return -3;   // cannot happen: <= 10 trials per iteration
+            if (enqueue_chunk(2) || wait(st)) return -3;
+        }
+        return 0;
+    }
+};
 
 extern "C" {
 
@@ -1870,10 +1977,11 @@ int lba_create(lba_engine **out) {
     lba_engine *e = new lba_engine();
     if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void **)&e->h_scalars, (8 + 2 * kRedBlocks) * sizeof(double)) != hipSuccess ||
-        hipHostMalloc((void **)&e->h_lm, sizeof(LMState)) != hipSuccess ||
+        hipHostMalloc((void **)&e->h_lm, 2 * sizeof(LMState)) != hipSuccess ||
         hipHostMalloc((void **)&e->h_stop, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void **)&e->d_stop, e->h_stop, 0) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_chunk, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_chunk[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_chunk[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_stage[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_stage[1], hipEventDisableTiming) != hipSuccess) {
         delete e;
@@ -1890,7 +1998,7 @@ void lba_destroy(lba_engine *e) {
     if (e->h_scalars) (void)hipHostFree(e->h_scalars);
     if (e->h_lm) (void)hipHostFree(e->h_lm);
     if (e->h_stop) (void)hipHostFree(e->h_stop);
-    if (e->ev_chunk) (void)hipEventDestroy(e->ev_chunk);
+    for (hipEvent_t ev : e->ev_chunk) if (ev) (void)hipEventDestroy(ev);
     for (int k = 0; k < 2; k++) {
         if (e->h_stage[k]) (void)hipHostFree(e->h_stage[k]);
         if (e->ev_stage[k]) (void)hipEventDestroy(e->ev_stage[k]);
@@ -1963,12 +2071,11 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
                  ocam = ua.add(p->pose_cam, sizeof(float) * 5 * np);
     if (upload_set(e, 0, e->arenaA, ua, s) || e->E.ensure(sizeof(EdgeDev) * std::max(ne, 1)) ||
         e->err.ensure(sizeof(double) * 3 * std::max(ne, 1)) ||
-        e->flags.ensure(std::max(ne, 1)) || e->scalars.ensure((8 + 2 * kRedBlocks) * sizeof(double)) ||
-        e->partial.ensure(sizeof(double) * 4 * kRedBlocks) || e->lm.ensure(2 * sizeof(LMState)) || e->arrive.ensure(64))
+        e->flags.ensure(sizeof(Pose) * np + sizeof(double) * 3 * nq + ne + 16) || e->scalars.ensure((8 + 2 * kRedBlocks) * sizeof(double)) ||
+        e->partial.ensure(sizeof(double) * 4 * kRedBlocks) || e->lm.ensure(4 * sizeof(LMState)) || e->arrive.ensure(64))
         return ORBX_EDEVICE;
-    LBA_CHK(hipMemsetAsync(e->err.p, 0, sizeof(double) * 3 * std::max(ne, 1), s));
-    LBA_CHK(hipMemsetAsync(e->arrive.p, 0, 64, s));
-    LBA_CHK(hipMemsetAsync(e->lm.p, 0, 2 * sizeof(LMState), s));   // cur = 0: (T, X) hold the estimate
+    // err, arrive and the LM state (cur = 0: (T, X) hold the estimate) are zeroed by setup's
+    // lba_init_buffers, before any kernel reads them
     int cur = 0;
     *e->h_stop = 0u;
     Graph g{};
@@ -1994,6 +2101,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     auto setup = [&](ActiveSet &A, const std::vector<EdgeDev> *edges) -> int {
         const int Kpad = std::max(4, ((3 * A.Lm + 3) / 4) * 4);
         build_schur_tiles(A, Kpad);
+        hp.mark("tiles");
         UploadSet ub;
         const size_t o_pose_hidx = ub.add(A.pose_hidx), o_point_hidx = ub.add(A.point_hidx),
                      o_hpose = ub.add(A.hpose), o_hpoint = ub.add(A.hpoint), o_pt_start = ub.add(A.pt_start),
@@ -2005,9 +2113,10 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
                      o_tp_chunk = ub.add(A.tp_chunk), o_tp_nch = ub.add(A.tp_nch);
         const size_t o_E = edges ? ub.add(*edges) : 0;
         if (upload_set(e, 1, e->arenaB, ub, s)) return -1;
+        hp.mark("stage");
         const int nact = (int)A.act.size();
         g.nact = nact;
-        if (e->on.ensure(std::max(nact, 1)) || hipMemsetAsync(e->on.p, 1, std::max(nact, 1), s) != hipSuccess) return -1;
+        if (e->on.ensure(std::max(nact, 1))) return -1;
         g.on = e->on.as<uint8_t>();
         if (e->E_lm.ensure(sizeof(EdgeDev) * std::max(nact, 1)) || e->on_lm.ensure(std::max(nact, 1))) return -1;
         g.E_lm = e->E_lm.as<EdgeDev>();
@@ -2055,15 +2164,28 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.w = g.Y + g.wrow;
         g.Hs = e->Hs.as<double>(); g.bs = e->bs.as<double>(); g.ywp = e->ywp.as<double>();
         g.x = e->x.as<double>();
-        if (hipMemsetAsync(g.Y, 0, sizeof(double) * NPW * (size_t)(g.Kpad + 4), s) != hipSuccess ||
-            hipMemsetAsync(g.Hs, 0, sizeof(double) * NP * NP, s) != hipSuccess ||
-            hipMemsetAsync(g.x, 0, sizeof(double) * (6 * A.P + 3 * A.Lm + 8), s) != hipSuccess)
-            return -1;
+        {   // zeroed / filled / copied in one launch: err, arrive, the LM state, the level flags (1),
+            // Y, Hs, x, and the trial buffers set equal to the current estimate (inactive vertices
+            // never change)
+            InitRanges R{};
+            const InitRange rr[kInitRanges] = {
+                {e->err.p, nullptr, sizeof(double) * 3 * (unsigned long long)std::max(ne, 1), 0, 0},
+                {e->arrive.p, nullptr, 64, 0, 0},
+                {e->lm.p, nullptr, 4 * sizeof(LMState), 0, 0},
+                {e->on.p, nullptr, (unsigned long long)std::max(nact, 1), 1, 0},
+                {g.Y, nullptr, sizeof(double) * NPW * (unsigned long long)(g.Kpad + 4), 0, 0},
+                {g.Hs, nullptr, sizeof(double) * NP * NP, 0, 0},
+                {g.x, nullptr, sizeof(double) * (unsigned long long)(6 * A.P + 3 * A.Lm + 8), 0, 0},
+                {cur ? g.T : g.T2, cur ? g.T2 : g.T, sizeof(Pose) * (unsigned long long)std::max(np, 1), 0, 0},
+                {cur ? g.X : g.X2, cur ? g.X2 : g.X, sizeof(double) * 3 * (unsigned long long)std::max(nq, 1), 0, 0},
+                {nullptr, nullptr, 0, 0, 0}};
+            unsigned long long most = 0;
+            for (int i = 0; i < kInitRanges; i++) { R.r[i] = rr[i]; most = std::max(most, rr[i].bytes); }
+            const unsigned gx = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>(1024, (most / 16 + 255) / 256));
+            lba_init_buffers<<<dim3(gx, kInitRanges), 256, 0, s>>>(R);
+            if (hipGetLastError() != hipSuccess) return -1;
+        }
         if (nact > 0) lba_gather_edges<<<nblk(nact), 256, 0, s>>>(g.E_lm, g.on_lm, g.E, g.pt_items, nact);
-        // trial buffers start equal to the current estimate (inactive vertices never change)
-        if (hipMemcpyAsync(cur ? g.T : g.T2, cur ? g.T2 : g.T, sizeof(Pose) * std::max(np, 1), hipMemcpyDeviceToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(cur ? g.X : g.X2, cur ? g.X2 : g.X, sizeof(double) * 3 * std::max(nq, 1), hipMemcpyDeviceToDevice, s) != hipSuccess)
-            return -1;
         return 0;
     };
     hp.mark("upload");
@@ -2072,36 +2194,84 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     hp.mark("active1");
     if (setup(A, nullptr)) return ORBX_EDEVICE;
     hp.mark("setup1");
-    // lba_optimize: >= 0 iterations, -1 = the pre-LM error evaluation failed (g2o's optimize()
-    // returning -1, a valid outcome), -3 = HIP runtime error
-    int seen = 0;
+    // the two optimize() calls (Optimizer.cc:900-917 and 964-966). -1 iterations = the pre-LM error
+    // evaluation failed (g2o's optimize() returning -1, a valid outcome). Phase 1's LM state
+    // ping-pongs in lm[0..1], phase 2's in lm[2..3]: phase 2's start and first chunk are enqueued
+    // right behind phase 1's first chunk (LBA_SPEC_PHASE2), gated on the device by
+    // lba_phase2_begin, so the common call (phase 1 done in its first chunk) has no host round trip
+    // between the optimizations; when phase 1 needs retry slots, that enqueued chunk is a no-op and
+    // phase 2 is enqueued again after them.
     const int hook1 = e->hook_phase == 1 ? e->hook_trial : INT_MAX, hook2 = e->hook_phase == 2 ? e->hook_trial : INT_MAX;
-    r->iterations[0] = lba_optimize(e, g, A, 5, np, nq, stop, hook1, &r->chi2[0], &r->trials[0], &cur, &seen);
-    if (r->iterations[0] == -3) return ORBX_EDEVICE;
-    if (r->iterations[0] < -1) return ORBX_EINVAL;
-    hp.mark("opt1");
-    // if(pbStopFlag) if(*pbStopFlag) bDoMore = false (Optimizer.cc:913-917); the hook's flag stays
-    // raised once its trial has run
-    const bool bDoMore = !(stop && *stop) && !(e->hook_phase == 1 && r->trials[0] >= e->hook_trial);
-    if (bDoMore) {
-        // phase 1 ran with every edge at level 0 (its slots are all edges): the level-1 moves and
-        // the robust-kernel drop stay on the device, no host round trip between the optimizations
-        lba_phase2_mark<<<nblk(std::max(ne, (int)A.act.size())), 256, 0, s>>>(g, const_cast<EdgeDev *>(g.E),
-                                                                              e->on.as<uint8_t>(), ne);
-        LBA_CHK(hipGetLastError());
-        r->iterations[1] = lba_optimize(e, g, A, 10, np, nq, stop, hook2, &r->chi2[1], &r->trials[1], &cur, &seen);
-        if (r->iterations[1] == -3) return ORBX_EDEVICE;
-        if (r->iterations[1] < -1) return ORBX_EINVAL;
-        if (seen) r->stopped = 1;   // phase 2 cut short by the flag
-        hp.mark("opt2");
+    Graph g2 = g;
+    g2.lm_buf[0] = g.lm_buf[0] + 2;
+    g2.lm_buf[1] = g.lm_buf[0] + 3;
+    g2.lm = g2.lm_buf[0];
+    g2.lm_src = nullptr;
+    LmPhase p1(e, g, A, 5, stop, hook1, e->h_lm, e->ev_chunk[0]);
+    LmPhase p2(e, g2, A, 10, stop, hook2, e->h_lm + 1, e->ev_chunk[1]);
+    if (p1.rc == -2 || p2.rc == -2) return ORBX_EINVAL;
+    if (p1.rc == -1) {   // no vertex to optimise: both optimize() calls return -1
+        r->iterations[0] = -1;
+        if (!(stop && *stop)) r->iterations[1] = -1;
+        else r->stopped = 1;
     } else {
-        r->stopped = 1;
+        // phase 2's start and its first `k` trial slots (the rest of its first chunk follows)
+        auto phase2_start = [&](bool spec, int k) -> int {
+            lba_phase2_begin<<<1, 1, 0, s>>>(g2, g.lm, 10, hook2, spec ? 1 : 0);
+            // phase 1 ran with every edge at level 0 (its slots are all edges): the level-1 moves and
+            // the robust-kernel drop stay on the device
+            lba_phase2_mark<<<nblk(std::max(ne, (int)A.act.size())), 256, 0, s>>>(g2, const_cast<EdgeDev *>(g.E),
+                                                                                   e->on.as<uint8_t>(), ne);
+            if (hipGetLastError() != hipSuccess) return -3;
+            p2.slots = p2.chunk0 = 0;
+            p2.enqueue_slots(k);
+            return 0;
+        };
+        LMState st1{}, st2{};
+        p1.init();
+        if (p1.enqueue_chunk(5)) return ORBX_EDEVICE;
+        // one phase-2 slot behind phase 1's first chunk: it keeps the GPU busy while the host reads
+        // phase 1's state back; a deferred one costs its few empty launches
+        const bool spec = LBA_SPEC_PHASE2 != 0;
+        if (spec && phase2_start(true, 1)) return ORBX_EDEVICE;
+        if (p1.wait(st1)) return ORBX_EDEVICE;
+        const bool first_chunk = st1.done;   // the speculative phase-2 start finds phase 1 done
+        if (p1.finish(st1)) return ORBX_EDEVICE;
+        hp.mark("opt1");
+        r->iterations[0] = st1.it;
+        r->chi2[0] = st1.final_chi;
+        r->trials[0] = st1.trials;
+        cur = st1.cur;
+        if (!spec || !first_chunk) {
+            if (phase2_start(false, 10) || p2.close_chunk()) return ORBX_EDEVICE;
+        } else {
+            p2.enqueue_slots(9);
+            if (p2.close_chunk()) return ORBX_EDEVICE;
+        }
+        if (p2.wait(st2) || p2.finish(st2)) return ORBX_EDEVICE;
+        if (st2.gate == 2) {   // if(pbStopFlag) if(*pbStopFlag) bDoMore = false: no second optimize()
+            r->stopped = 1;
+        } else {
+            r->iterations[1] = st2.it;
+            r->chi2[1] = st2.final_chi;
+            r->trials[1] = st2.trials;
+            cur = st2.cur;
+            if (st2.seen) r->stopped = 1;   // phase 2 cut short by the flag
+        }
+        hp.mark("opt2");
     }
-    lba_outliers<<<nblk(ne), 256, 0, s>>>(g.E, g.err, cur ? g.T2 : g.T, cur ? g.X2 : g.X, ne, e->flags.as<uint8_t>());
-    LBA_CHK(hipGetLastError());
-    // the three results through one page-locked staging buffer (DMA straight into it, one wait;
-    // D2H copies into the caller's pageable arrays were staged and serialised by the runtime)
+    // the three results packed by lba_outliers into one device buffer, one DMA into one page-locked
+    // staging buffer, one wait (three copies before: D2H copies into the caller's pageable arrays
+    // were staged and serialised by the runtime)
     const size_t oTd = 0, oXd = sizeof(Pose) * np, oFd = oXd + sizeof(double) * 3 * nq, down = oFd + ne + 16;
+    {   // e->flags holds `down` bytes (allocated with the call's other buffers)
+        char *dd = (char *)e->flags.p;
+        const int nT = (int)(sizeof(Pose) / sizeof(double)) * np, nX = 3 * nq;
+        lba_outliers<<<nblk(std::max(ne, std::max(nT, nX))), 256, 0, s>>>(
+            g.E, g.err, cur ? g.T2 : g.T, cur ? g.X2 : g.X, ne, nT, nX, (double *)(dd + oTd), (double *)(dd + oXd),
+            (uint8_t *)(dd + oFd));
+    }
+    LBA_CHK(hipGetLastError());
     if (down > e->h_down_bytes) {
         if (e->h_down) (void)hipHostFree(e->h_down);
         e->h_down = nullptr;
@@ -2110,9 +2280,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         e->h_down_bytes = down;
     }
     char *hd = (char *)e->h_down;
-    if (np) LBA_CHK(hipMemcpyAsync(hd + oTd, cur ? g.T2 : g.T, sizeof(Pose) * np, hipMemcpyDeviceToHost, s));
-    if (nq) LBA_CHK(hipMemcpyAsync(hd + oXd, cur ? g.X2 : g.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, s));
-    if (ne) LBA_CHK(hipMemcpyAsync(hd + oFd, e->flags.p, ne, hipMemcpyDeviceToHost, s));
+    LBA_CHK(hipMemcpyAsync(hd, e->flags.p, oFd + ne, hipMemcpyDeviceToHost, s));
     LBA_CHK(hipStreamSynchronize(s));
     std::memcpy(T.data(), hd + oTd, sizeof(Pose) * np);
     std::memcpy(X.data(), hd + oXd, sizeof(double) * 3 * nq);
