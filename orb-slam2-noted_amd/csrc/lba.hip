@@ -1536,13 +1536,13 @@ struct lba_engine {
     hipStream_t stream = nullptr;
     DBuf T, T2, X, X2, E, E_lm, on_lm, err, act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items,
         ps_start, ps_items, slot_pt, slot_ph, con, hpl, Hll, bl, Hpp, bp, Dinv, Lc, Y, ywp, on, tp_part, Hs, bs, x, partial,
-        scalars, flags, lm, arrive, arenaA, arenaB;
+        scalars, flags, lm, arrive, arenaA, arenaB, arenaC;
     double *h_scalars = nullptr;  // pinned
     LMState *h_lm = nullptr;      // pinned, one per optimize() of a call
-    void *h_stage[2] = {nullptr, nullptr};   // pinned upload staging per arena (grow-only)
-    size_t h_stage_bytes[2] = {0, 0};
-    hipEvent_t ev_stage[2] = {nullptr, nullptr};   // the last DMA out of each staging buffer
-    bool stage_rec[2] = {false, false};
+    void *h_stage[3] = {nullptr, nullptr, nullptr};   // pinned upload staging per arena (grow-only)
+    size_t h_stage_bytes[3] = {0, 0, 0};
+    hipEvent_t ev_stage[3] = {nullptr, nullptr, nullptr};   // the last DMA out of each staging buffer
+    bool stage_rec[3] = {false, false, false};
     void *h_down = nullptr;       // pinned download staging of the results (grow-only)
     size_t h_down_bytes = 0;
     // pbStopFlag as the device sees it: a page-locked, device-mapped, coherent word the host loop
@@ -1585,7 +1585,7 @@ struct HostGraph {
 
     const int32_t *pose_id, *point_id;
     const uint8_t *fixed;
-    std::vector<int> edge_point, edge_pose;
+    const int32_t *edge_point, *edge_pose;   // the caller's arrays (lba_problem), validated
 };
 
 struct ActiveSet {
@@ -1855,7 +1855,13 @@ struct LmPhase {
         g.lm = gd.lm;
     }
     void slot(bool first, bool decide) {
-        // `decide`: the previous trial of this chunk is undecided; this slot's lba_reduce_points decides it
+        slot_head(first, decide);
+        slot_tail();
+    }
+    // a trial slot up to the Schur step: the linearisation (an iteration's first slot) and the
+    // landmark reductions; `decide`: the previous trial of this chunk is undecided, this slot's
+    // lba_reduce_points decides it
+    void slot_head(bool first, bool decide) {
         int ph;
         if (first) {   // later iterations start from the linearisation of the accepted trial
             ph = lprof_begin(e);
@@ -1877,6 +1883,10 @@ struct LmPhase {
             lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nbt, std::max(1, (A.Lm + kRPL - 1) / kRPL), 6 * A.P);
             lprof_end(e, ph, "lba_pose_sums_prep");
         }
+    }
+    // the rest of a trial slot: Schur complement, solve, update + the trial's residuals
+    void slot_tail() {
+        int ph;
         if (A.P > 0) {
             ph = lprof_begin(e);
             // chunk workgroups, then b_p / b_schur rows (one wave each), then Hpp (one wave per
@@ -1926,6 +1936,18 @@ struct LmPhase {
     int enqueue_chunk(int k) {
         chunk0 = slots;
         enqueue_slots(k);
+        return close_chunk();
+    }
+    // the first chunk of an optimize() in two parts: the first slot's head (first_head), then its
+    // tail and the chunk's k - 1 other slots
+    void first_head() {
+        slots = chunk0 = 0;
+        slot_head(true, false);
+    }
+    int complete_first_chunk(int k) {
+        slot_tail();
+        slots = 1;
+        enqueue_slots(k - 1);
         return close_chunk();
     }
     int close_chunk() {
@@ -1983,7 +2005,8 @@ int lba_create(lba_engine **out) {
         hipEventCreateWithFlags(&e->ev_chunk[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_chunk[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_stage[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_stage[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&e->ev_stage[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_stage[2], hipEventDisableTiming) != hipSuccess) {
         delete e;
         return ORBX_EDEVICE;
     }
@@ -1999,7 +2022,7 @@ void lba_destroy(lba_engine *e) {
     if (e->h_lm) (void)hipHostFree(e->h_lm);
     if (e->h_stop) (void)hipHostFree(e->h_stop);
     for (hipEvent_t ev : e->ev_chunk) if (ev) (void)hipEventDestroy(ev);
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < 3; k++) {
         if (e->h_stage[k]) (void)hipHostFree(e->h_stage[k]);
         if (e->ev_stage[k]) (void)hipEventDestroy(e->ev_stage[k]);
     }
@@ -2057,8 +2080,8 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     HostGraph h;
     h.np = np; h.nq = nq; h.ne = ne;
     h.pose_id = p->pose_id; h.point_id = p->point_id; h.fixed = p->pose_fixed;
-    h.edge_point.assign(p->edge_point, p->edge_point + ne);
-    h.edge_pose.assign(p->edge_pose, p->edge_pose + ne);
+    h.edge_point = p->edge_point;
+    h.edge_pose = p->edge_pose;
     for (int k = 0; k < ne; k++)
         if (h.edge_point[k] < 0 || h.edge_point[k] >= nq || h.edge_pose[k] < 0 || h.edge_pose[k] >= np) return ORBX_EINVAL;
     hp.mark("build");
@@ -2096,12 +2119,10 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     g.lm_buf[1] = g.lm_buf[0] + 1;
     g.lm = g.lm_buf[0];
     g.lm_src = nullptr;
-    // per optimize(): the active-set index arrays (and, for the second phase, the edges with their
-    // robust kernels removed) in one upload
-    auto setup = [&](ActiveSet &A, const std::vector<EdgeDev> *edges) -> int {
+    // the active-set index arrays in one upload, the call's buffers, their initialisation and the
+    // landmark-major edge records (the Schur tile lists follow in setup_tiles)
+    auto setup = [&](ActiveSet &A) -> int {
         const int Kpad = std::max(4, ((3 * A.Lm + 3) / 4) * 4);
-        build_schur_tiles(A, Kpad);
-        hp.mark("tiles");
         UploadSet ub;
         const size_t o_pose_hidx = ub.add(A.pose_hidx), o_point_hidx = ub.add(A.point_hidx),
                      o_hpose = ub.add(A.hpose), o_hpoint = ub.add(A.hpoint), o_pt_start = ub.add(A.pt_start),
@@ -2109,9 +2130,6 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
                      o_slot_pt = ub.add(A.slot_pt), o_slot_ph = ub.add(A.slot_ph);
         const size_t o_slot_ppos = ub.add(A.slot_ppos), o_slot_lpos = ub.add(A.slot_lpos), o_lpos_ph = ub.add(A.lpos_ph),
                      o_lpos_ppos = ub.add(A.lpos_ppos);
-        const size_t o_tp_ij = ub.add(A.tp_ij), o_tp_start = ub.add(A.tp_start), o_tp_rows = ub.add(A.tp_rows),
-                     o_tp_chunk = ub.add(A.tp_chunk), o_tp_nch = ub.add(A.tp_nch);
-        const size_t o_E = edges ? ub.add(*edges) : 0;
         if (upload_set(e, 1, e->arenaB, ub, s)) return -1;
         hp.mark("stage");
         const int nact = (int)A.act.size();
@@ -2127,20 +2145,10 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.pt_start = at<int>(e->arenaB, o_pt_start); g.pt_items = at<int>(e->arenaB, o_pt_items);
         g.ps_start = at<int>(e->arenaB, o_ps_start); g.ps_items = at<int>(e->arenaB, o_ps_items);
         g.slot_pt = at<int>(e->arenaB, o_slot_pt); g.slot_ph = at<int>(e->arenaB, o_slot_ph);
-        if (edges) g.E = at<EdgeDev>(e->arenaB, o_E);
         g.slot_ppos = at<int>(e->arenaB, o_slot_ppos);
         g.slot_lpos = at<int>(e->arenaB, o_slot_lpos);
         g.lpos_ph = at<int>(e->arenaB, o_lpos_ph);
         g.lpos_ppos = at<int>(e->arenaB, o_lpos_ppos);
-        g.tp_ij = at<int2>(e->arenaB, o_tp_ij);
-        g.tp_start = at<int>(e->arenaB, o_tp_start);
-        g.tp_rows = at<int>(e->arenaB, o_tp_rows);
-        g.npairs = (int)A.tp_ij.size();
-        g.tp_chunk = at<int4>(e->arenaB, o_tp_chunk);
-        g.tp_nch = at<int2>(e->arenaB, o_tp_nch);
-        g.nchunks = (int)A.tp_chunk.size();
-        if (e->tp_part.ensure(sizeof(double) * 256 * std::max(g.nchunks, 1))) return -1;
-        g.tp_part = e->tp_part.as<double>();
         g.Kpad = Kpad;
         g.NP = std::max(kCB, ((6 * A.P + kCB - 1) / kCB) * kCB);
         const size_t NP = (size_t)g.NP, NPW = NP + 16;
@@ -2188,11 +2196,31 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         if (nact > 0) lba_gather_edges<<<nblk(nact), 256, 0, s>>>(g.E_lm, g.on_lm, g.E, g.pt_items, nact);
         return 0;
     };
+    // the block structure of the Schur product (build_schur_tiles) in an upload of its own: built on
+    // the host while the first trial slot's linearisation and landmark reductions run on the device
+    // (nothing before lba_schur_tiles reads it)
+    auto setup_tiles = [&](ActiveSet &A) -> int {
+        build_schur_tiles(A, g.Kpad);
+        UploadSet uc;
+        const size_t o_tp_ij = uc.add(A.tp_ij), o_tp_start = uc.add(A.tp_start), o_tp_rows = uc.add(A.tp_rows),
+                     o_tp_chunk = uc.add(A.tp_chunk), o_tp_nch = uc.add(A.tp_nch);
+        if (upload_set(e, 2, e->arenaC, uc, s)) return -1;
+        g.tp_ij = at<int2>(e->arenaC, o_tp_ij);
+        g.tp_start = at<int>(e->arenaC, o_tp_start);
+        g.tp_rows = at<int>(e->arenaC, o_tp_rows);
+        g.npairs = (int)A.tp_ij.size();
+        g.tp_chunk = at<int4>(e->arenaC, o_tp_chunk);
+        g.tp_nch = at<int2>(e->arenaC, o_tp_nch);
+        g.nchunks = (int)A.tp_chunk.size();
+        if (e->tp_part.ensure(sizeof(double) * 256 * std::max(g.nchunks, 1))) return -1;
+        g.tp_part = e->tp_part.as<double>();
+        return 0;
+    };
     hp.mark("upload");
     static thread_local ActiveSet A;
     build_active(h, A);
     hp.mark("active1");
-    if (setup(A, nullptr)) return ORBX_EDEVICE;
+    if (setup(A)) return ORBX_EDEVICE;
     hp.mark("setup1");
     // the two optimize() calls (Optimizer.cc:900-917 and 964-966). -1 iterations = the pre-LM error
     // evaluation failed (g2o's optimize() returning -1, a valid outcome). Phase 1's LM state
@@ -2202,19 +2230,25 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     // between the optimizations; when phase 1 needs retry slots, that enqueued chunk is a no-op and
     // phase 2 is enqueued again after them.
     const int hook1 = e->hook_phase == 1 ? e->hook_trial : INT_MAX, hook2 = e->hook_phase == 2 ? e->hook_trial : INT_MAX;
-    Graph g2 = g;
-    g2.lm_buf[0] = g.lm_buf[0] + 2;
-    g2.lm_buf[1] = g.lm_buf[0] + 3;
-    g2.lm = g2.lm_buf[0];
-    g2.lm_src = nullptr;
     LmPhase p1(e, g, A, 5, stop, hook1, e->h_lm, e->ev_chunk[0]);
-    LmPhase p2(e, g2, A, 10, stop, hook2, e->h_lm + 1, e->ev_chunk[1]);
-    if (p1.rc == -2 || p2.rc == -2) return ORBX_EINVAL;
+    if (p1.rc == -2) return ORBX_EINVAL;
     if (p1.rc == -1) {   // no vertex to optimise: both optimize() calls return -1
         r->iterations[0] = -1;
         if (!(stop && *stop)) r->iterations[1] = -1;
         else r->stopped = 1;
     } else {
+        // phase 1's first slot up to the Schur step, then the tile lists (host work that overlaps
+        // it), then the rest of the slot and of the chunk
+        p1.init();
+        p1.first_head();
+        if (setup_tiles(A)) return ORBX_EDEVICE;
+        hp.mark("tiles");
+        Graph g2 = g;
+        g2.lm_buf[0] = g.lm_buf[0] + 2;
+        g2.lm_buf[1] = g.lm_buf[0] + 3;
+        g2.lm = g2.lm_buf[0];
+        g2.lm_src = nullptr;
+        LmPhase p2(e, g2, A, 10, stop, hook2, e->h_lm + 1, e->ev_chunk[1]);
         // phase 2's start and its first `k` trial slots (the rest of its first chunk follows)
         auto phase2_start = [&](bool spec, int k) -> int {
             lba_phase2_begin<<<1, 1, 0, s>>>(g2, g.lm, 10, hook2, spec ? 1 : 0);
@@ -2228,8 +2262,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
             return 0;
         };
         LMState st1{}, st2{};
-        p1.init();
-        if (p1.enqueue_chunk(5)) return ORBX_EDEVICE;
+        if (p1.complete_first_chunk(5)) return ORBX_EDEVICE;
         // one phase-2 slot behind phase 1's first chunk: it keeps the GPU busy while the host reads
         // phase 1's state back; a deferred one costs its few empty launches
         const bool spec = LBA_SPEC_PHASE2 != 0;
