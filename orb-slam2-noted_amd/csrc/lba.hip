@@ -51,6 +51,7 @@
 #include "orb_engine.h"
 #include "orbslam2_amd.h"
 #include "se3_device.h"
+#include "lba_host.h"
 
 #define LBA_CHK(x)                                                                  \
     do {                                                                            \
@@ -1580,188 +1581,7 @@ static void lprof_end(lba_engine *e, int h, const char *name) {
 
 namespace {
 
-struct HostGraph {
-    int np, nq, ne;
-
-    const int32_t *pose_id, *point_id;
-    const uint8_t *fixed;
-    const int32_t *edge_point, *edge_pose;   // the caller's arrays (lba_problem), validated
-};
-
-struct ActiveSet {
-    int P = 0, Lm = 0;
-    std::vector<int> act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items, ps_start, ps_items, slot_pt, slot_ph,
-        slot_ppos, slot_lpos, lpos_ph, lpos_ppos;
-    std::vector<int2> tp_ij, tp_nch;     // Schur tile pairs (build_schur_tiles)
-    std::vector<int> tp_start, tp_rows;
-    std::vector<int4> tp_chunk;
-    std::vector<char> scratch_p, scratch_q;
-    std::vector<int> scratch_l, scratch_f, scratch_cnt, scratch_tiles, scratch_fill;
-    std::vector<unsigned long long> scratch_mask;
-};
-
-// Block structure of the Schur product Y Y^T over 16-column tiles: for every upper tile pair
-// (I <= J) the Y^T rows (3 per landmark, hessian order) of the landmarks with a free pose in both
-// tiles' columns, each list padded to a multiple of 4 rows with the zero row `zero_row`
-// (block_solver.hpp:354-439 visits the same pose pairs per landmark). Two passes over the
-// landmarks (count, fill); a landmark's tiles come from its free poses' 6-column blocks.
-void build_schur_tiles(ActiveSet &A, int zero_row) {
-    const int ntile = std::max(1, (6 * A.P + 15) / 16);
-    const int npairs = ntile * (ntile + 1) / 2;
-    auto pid = [&](int I, int J) { return I * ntile - I * (I - 1) / 2 + (J - I); };
-    A.tp_ij.resize(npairs);
-    for (int I = 0; I < ntile; I++)
-        for (int J = I; J < ntile; J++) A.tp_ij[pid(I, J)] = make_int2(I, J);
-    std::vector<int> &cnt = A.scratch_cnt, &tiles = A.scratch_tiles;
-    cnt.assign(npairs + 1, 0);
-    if (ntile <= 64) {
-        // common case (6P <= 1024): a landmark's tiles as one 64-bit mask, formed once and read by
-        // both passes; pairs in (I, J) order, I <= J, like the sorted-list path below
-        std::vector<unsigned long long> &mask = A.scratch_mask;
-        mask.assign(A.Lm, 0ull);
-        for (int l = 0; l < A.Lm; l++) {
-            unsigned long long m = 0;
-            for (int i = A.pt_start[l]; i < A.pt_start[l + 1]; i++) {
-                const int ph = A.slot_ph[A.pt_items[i]];
-                if (ph >= 0) m |= 1ull << (6 * ph / 16) | 1ull << ((6 * ph + 5) / 16);
-            }
-            mask[l] = m;
-            for (unsigned long long ma = m; ma; ma &= ma - 1) {
-                const int I = __builtin_ctzll(ma);
-                for (unsigned long long mb = ma; mb; mb &= mb - 1) cnt[pid(I, __builtin_ctzll(mb))] += 3;
-            }
-        }
-        A.tp_start.assign(npairs + 1, 0);
-        for (int p = 0; p < npairs; p++) A.tp_start[p + 1] = A.tp_start[p] + ((cnt[p] + 3) & ~3);
-        A.tp_rows.assign(std::max(1, A.tp_start[npairs]), zero_row);
-        std::vector<int> &fill = A.scratch_fill;
-        fill.assign(A.tp_start.begin(), A.tp_start.end() - 1);
-        for (int l = 0; l < A.Lm; l++)
-            for (unsigned long long ma = mask[l]; ma; ma &= ma - 1) {
-                const int I = __builtin_ctzll(ma);
-                for (unsigned long long mb = ma; mb; mb &= mb - 1) {
-                    int &f = fill[pid(I, __builtin_ctzll(mb))];
-                    A.tp_rows[f++] = 3 * l;
-                    A.tp_rows[f++] = 3 * l + 1;
-                    A.tp_rows[f++] = 3 * l + 2;
-                }
-            }
-    } else {
-    auto point_tiles = [&](int l) {
-        tiles.clear();
-        for (int i = A.pt_start[l]; i < A.pt_start[l + 1]; i++) {
-            const int ph = A.slot_ph[A.pt_items[i]];
-            if (ph < 0) continue;
-            tiles.push_back(6 * ph / 16);
-            tiles.push_back((6 * ph + 5) / 16);
-        }
-        std::sort(tiles.begin(), tiles.end());
-        tiles.erase(std::unique(tiles.begin(), tiles.end()), tiles.end());
-    };
-    for (int l = 0; l < A.Lm; l++) {
-        point_tiles(l);
-        for (size_t a = 0; a < tiles.size(); a++)
-            for (size_t b = a; b < tiles.size(); b++) cnt[pid(tiles[a], tiles[b])] += 3;
-    }
-    A.tp_start.assign(npairs + 1, 0);
-    for (int p = 0; p < npairs; p++) A.tp_start[p + 1] = A.tp_start[p] + ((cnt[p] + 3) & ~3);
-    A.tp_rows.assign(std::max(1, A.tp_start[npairs]), zero_row);
-    std::vector<int> &fill = A.scratch_fill;
-    fill.assign(A.tp_start.begin(), A.tp_start.end() - 1);
-    for (int l = 0; l < A.Lm; l++) {
-        point_tiles(l);
-        for (size_t a = 0; a < tiles.size(); a++)
-            for (size_t b = a; b < tiles.size(); b++) {
-                int &f = fill[pid(tiles[a], tiles[b])];
-                A.tp_rows[f++] = 3 * l;
-                A.tp_rows[f++] = 3 * l + 1;
-                A.tp_rows[f++] = 3 * l + 2;
-            }
-    }
-    }
-    // chunk workgroups: kSCH steps each, at least one per pair (empty pairs still write their tile)
-    A.tp_chunk.clear();
-    A.tp_nch.assign(npairs, make_int2(0, 0));
-    for (int p = 0; p < npairs; p++) {
-        const int steps = (A.tp_start[p + 1] - A.tp_start[p]) / 4;
-        const int nc = std::max(1, (steps + kSCH - 1) / kSCH);
-        A.tp_nch[p] = make_int2((int)A.tp_chunk.size(), nc);
-        for (int c = 0; c < nc; c++) A.tp_chunk.push_back(make_int4(p, c * kSCH, std::min(kSCH, steps - c * kSCH), c));
-    }
-}
-
-// SparseOptimizer::initializeOptimization(level) + buildIndexMapping + block structure
-// Every edge starts at level 0, so the active slots of the first optimize() are all edges in edge
-// order (the second reuses them: lba_phase2_mark). The vectors of A keep their capacity from call
-// to call (lba_solve's thread_local set).
-void build_active(const HostGraph &h, ActiveSet &A) {
-    A.act.resize(h.ne);   // slot s = edge s: only the size is used
-    std::vector<char> &pa = A.scratch_p, &qa = A.scratch_q;
-    pa.assign(h.np, 0);
-    qa.assign(h.nq, 0);
-    for (int k = 0; k < h.ne; k++) { pa[h.edge_pose[k]] = 1; qa[h.edge_point[k]] = 1; }
-    A.hpose.clear();
-    A.hpoint.clear();
-    for (int i = 0; i < h.np; i++) if (pa[i] && !h.fixed[i]) A.hpose.push_back(i);
-    for (int i = 0; i < h.nq; i++) if (qa[i]) A.hpoint.push_back(i);
-    // vertex ids order the hessian (g2o's buildIndexMapping); callers usually pass them sorted
-    auto by_id = [](std::vector<int> &v, const int32_t *id) {
-        for (size_t i = 1; i < v.size(); i++)
-            if (id[v[i]] < id[v[i - 1]]) {
-                std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return id[a] < id[b]; });
-                return;
-            }
-    };
-    by_id(A.hpose, h.pose_id);
-    by_id(A.hpoint, h.point_id);
-    A.P = (int)A.hpose.size();
-    A.Lm = (int)A.hpoint.size();
-    A.pose_hidx.assign(h.np, -1);
-    A.point_hidx.assign(h.nq, -1);
-    for (int i = 0; i < A.P; i++) A.pose_hidx[A.hpose[i]] = i;
-    for (int i = 0; i < A.Lm; i++) A.point_hidx[A.hpoint[i]] = i;
-    A.pt_start.assign(A.Lm + 1, 0);
-    A.ps_start.assign(A.P + 1, 0);
-    for (int s = 0; s < (int)A.act.size(); s++) {
-        const int k = s;
-        A.pt_start[A.point_hidx[h.edge_point[k]] + 1]++;
-        const int ph = A.pose_hidx[h.edge_pose[k]];
-        if (ph >= 0) A.ps_start[ph + 1]++;
-    }
-    for (int l = 0; l < A.Lm; l++) A.pt_start[l + 1] += A.pt_start[l];
-    for (int i = 0; i < A.P; i++) A.ps_start[i + 1] += A.ps_start[i];
-    A.pt_items.assign(std::max(1, A.pt_start[A.Lm]), 0);
-    A.ps_items.assign(std::max(1, A.ps_start[A.P]), 0);
-    std::vector<int> &fl = A.scratch_l, &fp = A.scratch_f;
-    fl.assign(A.Lm, 0);
-    fp.assign(A.P, 0);
-    // every entry of these is written by the fill loop below (size only, no initialisation pass)
-    A.slot_pt.resize(std::max<size_t>(1, A.act.size()));
-    A.slot_ph.resize(std::max<size_t>(1, A.act.size()));
-    A.slot_ppos.resize(std::max<size_t>(1, A.act.size()));
-    A.slot_lpos.resize(std::max<size_t>(1, A.act.size()));
-    A.lpos_ph.resize(std::max<size_t>(1, A.act.size()));
-    A.lpos_ppos.resize(std::max<size_t>(1, A.act.size()));
-    if (A.act.empty()) { A.slot_pt[0] = 0; A.slot_ph[0] = -1; A.slot_ppos[0] = -1; A.slot_lpos[0] = 0; A.lpos_ph[0] = -1; A.lpos_ppos[0] = -1; }
-    for (int s = 0; s < (int)A.act.size(); s++) {
-        const int k = s;
-        const int l = A.point_hidx[h.edge_point[k]];
-        const int lpos = A.pt_start[l] + fl[l]++;
-        A.pt_items[lpos] = s;
-        A.slot_lpos[s] = lpos;
-        const int ph = A.pose_hidx[h.edge_pose[k]];
-        A.lpos_ph[lpos] = ph;
-        A.slot_pt[s] = l;
-        A.slot_ph[s] = ph;
-        A.slot_ppos[s] = -1;
-        A.lpos_ppos[lpos] = -1;
-        if (ph >= 0) {
-            A.slot_ppos[s] = A.ps_start[ph] + fp[ph];
-            A.lpos_ppos[lpos] = A.slot_ppos[s];
-            A.ps_items[A.ps_start[ph] + fp[ph]++] = s;
-        }
-    }
-}
+using namespace lbaamd_host;
 
 // The host arrays of one upload step packed into the engine's page-locked staging buffer and
 // sent to one device arena in ONE DMA (one pageable copy per array before: ~40 staged copies per
@@ -1771,6 +1591,8 @@ struct UploadSet {
     std::vector<Item> items;
     size_t total = 0;
     template <class T> size_t add(const std::vector<T> &v) { return add(v.data(), sizeof(T) * v.size()); }
+    // arena space only (filled on the device)
+    template <class T> size_t reserve(const std::vector<T> &v) { return add(nullptr, sizeof(T) * v.size()); }
     size_t add(const void *src, size_t bytes) {
         const size_t off = total;
         items.push_back({src, bytes, off});
@@ -1790,7 +1612,7 @@ int upload_set(lba_engine *e, int k, DBuf &arena, const UploadSet &u, hipStream_
         e->h_stage_bytes[k] = u.total;
     }
     for (const auto &it : u.items)
-        if (it.bytes) std::memcpy((char *)e->h_stage[k] + it.off, it.src, it.bytes);
+        if (it.bytes && it.src) std::memcpy((char *)e->h_stage[k] + it.off, it.src, it.bytes);
     if (u.total > arena.n && hipStreamSynchronize(s) != hipSuccess) return -1;   // the old arena may be in use
     if (arena.ensure(u.total)) return -1;
     if (hipMemcpyAsync(arena.p, e->h_stage[k], u.total, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -2088,7 +1910,8 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     // the caller's edge arrays go up as they are (24 B per edge); lba_build_edges forms the device
     // edge records (112 B) there
     UploadSet ua;
-    const size_t oT = ua.add(T), oT2 = ua.add(T), oX = ua.add(X), oX2 = ua.add(X);
+    // the trial buffers T2 / X2 are set equal to T / X by setup's lba_init_buffers
+    const size_t oT = ua.add(T), oT2 = ua.reserve(T), oX = ua.add(X), oX2 = ua.reserve(X);
     const size_t oep = ua.add(p->edge_pose, sizeof(int32_t) * ne), oeq = ua.add(p->edge_point, sizeof(int32_t) * ne),
                  oobs = ua.add(p->edge_obs, sizeof(float) * 3 * ne), oisg = ua.add(p->edge_inv_sigma2, sizeof(float) * ne),
                  ocam = ua.add(p->pose_cam, sizeof(float) * 5 * np);
@@ -2128,8 +1951,9 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
                      o_hpose = ub.add(A.hpose), o_hpoint = ub.add(A.hpoint), o_pt_start = ub.add(A.pt_start),
                      o_pt_items = ub.add(A.pt_items), o_ps_start = ub.add(A.ps_start), o_ps_items = ub.add(A.ps_items),
                      o_slot_pt = ub.add(A.slot_pt), o_slot_ph = ub.add(A.slot_ph);
-        const size_t o_slot_ppos = ub.add(A.slot_ppos), o_slot_lpos = ub.add(A.slot_lpos), o_lpos_ph = ub.add(A.lpos_ph),
-                     o_lpos_ppos = ub.add(A.lpos_ppos);
+        // landmark-major slot order (the common case): the lpos arrays are the slot arrays
+        const size_t o_slot_ppos = ub.add(A.slot_ppos), o_slot_lpos = ub.add(A.slot_lpos),
+                     o_lpos_ph = A.mono ? o_slot_ph : ub.add(A.lpos_ph), o_lpos_ppos = A.mono ? o_slot_ppos : ub.add(A.lpos_ppos);
         if (upload_set(e, 1, e->arenaB, ub, s)) return -1;
         hp.mark("stage");
         const int nact = (int)A.act.size();
@@ -2200,7 +2024,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     // the host while the first trial slot's linearisation and landmark reductions run on the device
     // (nothing before lba_schur_tiles reads it)
     auto setup_tiles = [&](ActiveSet &A) -> int {
-        build_schur_tiles(A, g.Kpad);
+        build_schur_tiles(A, g.Kpad, kSCH);
         UploadSet uc;
         const size_t o_tp_ij = uc.add(A.tp_ij), o_tp_start = uc.add(A.tp_start), o_tp_rows = uc.add(A.tp_rows),
                      o_tp_chunk = uc.add(A.tp_chunk), o_tp_nch = uc.add(A.tp_nch);
