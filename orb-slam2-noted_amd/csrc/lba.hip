@@ -1421,10 +1421,16 @@ __global__ __launch_bounds__(256) void lba_build_edges(EdgeDev *E, int ne, const
 // outlier test of Optimizer.cc:925-962 / 977-1008: chi2 (stale _error) + depth sign
 // the call's results packed for one download: the estimate's poses (nT doubles), points (nX
 // doubles) and the erase flags of every edge, each thread one double of T, one of X and one flag
-__global__ __launch_bounds__(256) void lba_outliers(const EdgeDev *E, const double *err, const Pose *T,
-                                                    const double *X, int ne, int nT, int nX, double *outT,
+// The estimate buffers of the call's final state: (T, X) or (T2, X2) by st->cur (the last optimize()'s
+// state, read on the device: the launch can be enqueued before the host knows it).
+__global__ __launch_bounds__(256) void lba_outliers(const EdgeDev *E, const double *err, const Pose *T0,
+                                                    const Pose *T1, const double *X0, const double *X1,
+                                                    const LMState *st, int ne, int nT, int nX, double *outT,
                                                     double *outX, uint8_t *flag) {
     const int k = blockIdx.x * 256 + threadIdx.x;
+    const bool c = st->cur;
+    const Pose *T = c ? T1 : T0;
+    const double *X = c ? X1 : X0;
     if (k < nT) outT[k] = ((const double *)T)[k];
     if (k < nX) outX[k] = X[k];
     if (k >= ne) return;
@@ -2053,6 +2059,30 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     // lba_phase2_begin, so the common call (phase 1 done in its first chunk) has no host round trip
     // between the optimizations; when phase 1 needs retry slots, that enqueued chunk is a no-op and
     // phase 2 is enqueued again after them.
+    // the three results packed by lba_outliers into one device buffer, one DMA into one page-locked
+    // staging buffer (three copies before: D2H copies into the caller's pageable arrays were staged
+    // and serialised by the runtime). Enqueued right behind the last optimize()'s chunk, before its
+    // state is read back: the kernel takes the estimate buffer from that state on the device. When
+    // the chunk turns out not to be the last one, it is enqueued again after the retries.
+    const size_t oTd = 0, oXd = sizeof(Pose) * np, oFd = oXd + sizeof(double) * 3 * nq, down = oFd + ne + 16;
+    if (down > e->h_down_bytes) {
+        if (e->h_down) (void)hipHostFree(e->h_down);
+        e->h_down = nullptr;
+        e->h_down_bytes = 0;
+        LBA_CHK(hipHostMalloc(&e->h_down, down, hipHostMallocDefault));
+        e->h_down_bytes = down;
+    }
+    auto enqueue_final = [&](const LMState *stp) -> int {
+        char *dd = (char *)e->flags.p;   // `down` bytes, allocated with the call's other buffers
+        const int nT = (int)(sizeof(Pose) / sizeof(double)) * np, nX = 3 * nq;
+        lba_outliers<<<nblk(std::max(ne, std::max(nT, nX))), 256, 0, s>>>(
+            g.E, g.err, g.T, g.T2, g.X, g.X2, stp, ne, nT, nX, (double *)(dd + oTd), (double *)(dd + oXd),
+            (uint8_t *)(dd + oFd));
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(e->h_down, e->flags.p, oFd + ne, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return -3;
+        return 0;
+    };
     const int hook1 = e->hook_phase == 1 ? e->hook_trial : INT_MAX, hook2 = e->hook_phase == 2 ? e->hook_trial : INT_MAX;
     LmPhase p1(e, g, A, 5, stop, hook1, e->h_lm, e->ev_chunk[0]);
     if (p1.rc == -2) return ORBX_EINVAL;
@@ -2060,6 +2090,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         r->iterations[0] = -1;
         if (!(stop && *stop)) r->iterations[1] = -1;
         else r->stopped = 1;
+        if (enqueue_final(g.lm)) return ORBX_EDEVICE;   // lm zeroed: cur = 0
     } else {
         // phase 1's first slot up to the Schur step, then the tile lists (host work that overlaps
         // it), then the rest of the slot and of the chunk
@@ -2105,7 +2136,10 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
             p2.enqueue_slots(9);
             if (p2.close_chunk()) return ORBX_EDEVICE;
         }
+        if (enqueue_final(g2.lm)) return ORBX_EDEVICE;
+        const int slots2 = p2.slots;
         if (p2.wait(st2) || p2.finish(st2)) return ORBX_EDEVICE;
+        if (p2.slots != slots2 && enqueue_final(g2.lm)) return ORBX_EDEVICE;   // retries ran after it
         if (st2.gate == 2) {   // if(pbStopFlag) if(*pbStopFlag) bDoMore = false: no second optimize()
             r->stopped = 1;
         } else {
@@ -2117,28 +2151,8 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         }
         hp.mark("opt2");
     }
-    // the three results packed by lba_outliers into one device buffer, one DMA into one page-locked
-    // staging buffer, one wait (three copies before: D2H copies into the caller's pageable arrays
-    // were staged and serialised by the runtime)
-    const size_t oTd = 0, oXd = sizeof(Pose) * np, oFd = oXd + sizeof(double) * 3 * nq, down = oFd + ne + 16;
-    {   // e->flags holds `down` bytes (allocated with the call's other buffers)
-        char *dd = (char *)e->flags.p;
-        const int nT = (int)(sizeof(Pose) / sizeof(double)) * np, nX = 3 * nq;
-        lba_outliers<<<nblk(std::max(ne, std::max(nT, nX))), 256, 0, s>>>(
-            g.E, g.err, cur ? g.T2 : g.T, cur ? g.X2 : g.X, ne, nT, nX, (double *)(dd + oTd), (double *)(dd + oXd),
-            (uint8_t *)(dd + oFd));
-    }
-    LBA_CHK(hipGetLastError());
-    if (down > e->h_down_bytes) {
-        if (e->h_down) (void)hipHostFree(e->h_down);
-        e->h_down = nullptr;
-        e->h_down_bytes = 0;
-        LBA_CHK(hipHostMalloc(&e->h_down, down, hipHostMallocDefault));
-        e->h_down_bytes = down;
-    }
+    LBA_CHK(hipStreamSynchronize(s));   // the enqueued final copy (enqueue_final) has landed
     char *hd = (char *)e->h_down;
-    LBA_CHK(hipMemcpyAsync(hd, e->flags.p, oFd + ne, hipMemcpyDeviceToHost, s));
-    LBA_CHK(hipStreamSynchronize(s));
     std::memcpy(T.data(), hd + oTd, sizeof(Pose) * np);
     std::memcpy(X.data(), hd + oXd, sizeof(double) * 3 * nq);
     std::memcpy(r->edge_erase, hd + oFd, ne);
