@@ -1,7 +1,12 @@
-"""CPU checks of the LocalBA oracle (test infrastructure): convergence on the C4 graph."""
+"""CPU checks of the LocalBA oracle (test infrastructure): convergence on the C4 graph; and of the
+product's host-side structure build (lba_host.h)."""
+from pathlib import Path
+
 import numpy as np
 
 from orbslam2_amd import synth
+
+ROOT = Path(__file__).resolve().parents[1]
 
 
 def test_lba_oracle_converges(oracle_mod):
@@ -60,3 +65,20 @@ def test_lba_oracle_stop_hook_semantics(oracle_mod):
     for T in range(0, full["trials"][1]):
         r = oracle_mod.lba_solve(prob, hook=(2, T))
         assert r["trials"] == (full["trials"][0], T) and r["stopped"] == 1
+
+
+def test_host_structure_invariants(tmp_path):
+    """LocalBA's host structure build (csrc/lba_host.h: the active set and the Schur tile-pair row
+    lists, built per call before the device trials) on landmark-major and shuffled edge orders,
+    unsorted vertex ids and extra fixed poses: hessian order by id, CSR lists in slot order, inverse
+    maps, the landmark-major fast path's aliasing, and every tile pair's landmark rows
+    (tests/cpp/lba_host_check.cpp). CPU only."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    exe = tmp_path / "lba_host_check"
+    subprocess.run([hipcc, "-O2", "-I", str(ROOT / "orb-slam2-noted_amd" / "csrc"),
+                    str(ROOT / "tests" / "cpp" / "lba_host_check.cpp"), "-o", str(exe)], check=True,
+                   capture_output=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("ok 8"), r.stdout + r.stderr
