@@ -173,6 +173,12 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
             span = max(span, o[k] + d[k]);
         }
         const bool win8 = span <= 7;
+        // bytes of the source level from the descriptor base to the end of its last row: a 12-byte
+        // window of the last row's last column group can reach past it, and for level 0 of a
+        // batch's last image that is past the end of the caller's buffer (a fault when the buffer
+        // ends on a page: 512 VGA frames are exactly 75 x 2 MiB). Those windows load dword by dword,
+        // none starting past the end (an aligned dword never crosses a page).
+        const uint32_t lim = s0 + (uint32_t)((g.lh[l - 1] - 1) * sp + g.lw[l - 1]);
         // all loads of a thread's source rows are issued before any use (6 rows x 3 dwords
         // in flight; the level-1 pass streams the input image from HBM)
         for (int jb = threadIdx.x >> 5; jb < nsr; jb += 8 * RZ_HJ) {
@@ -182,10 +188,16 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
             for (int u = 0; u < RZ_HJ; u++) {
                 const int j = jb + 8 * u;
                 if (j < nsr) {
-                    const uint32_t a = (uint32_t)(sr0 + j) * (uint32_t)sp + (uint32_t)sxa + s0;
+                    const uint32_t a = (uint32_t)(sr0 + j) * (uint32_t)sp + (uint32_t)sxa + s0, al = a & ~3u;
                     mis[u] = (int)(a & 3u);
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rsrc, (int)(a & ~3u), 0, 0);
-                    D[u][0] = v[0]; D[u][1] = v[1]; D[u][2] = v[2];
+                    if (al + 12u <= lim) {
+                        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rsrc, (int)al, 0, 0);
+                        D[u][0] = v[0]; D[u][1] = v[1]; D[u][2] = v[2];
+                    } else {
+                        D[u][0] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)al, 0, 0);
+                        D[u][1] = al + 4u < lim ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)al + 4, 0, 0) : 0u;
+                        D[u][2] = al + 8u < lim ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)al + 8, 0, 0) : 0u;
+                    }
                 }
             }
 #pragma unroll

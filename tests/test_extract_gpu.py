@@ -204,6 +204,28 @@ def test_large_batch_matches_oracle(amd, oracle_mod):
         _assert_same_kps(ex.fetch(i), want[i % k], f"batch[{i}]")
 
 
+def test_batch_ends_at_allocation_end(amd, oracle_mod):
+    """512 VGA frames are exactly 75 x 2 MiB, so the batch's last image ends where its allocation
+    (and possibly the mapped memory) ends. The level-1 resize reads source rows as 12-byte windows;
+    the last row's last window of that image must not reach past the buffer (it did: a memory fault
+    at `bench.py --rgbd-batch 512`), and the guarded dword loads that replace it there must keep
+    every image equal to the oracle."""
+    import torch
+    h, w, n = 480, 640, 512
+    assert n * h * w == 75 * 2 * 1024 * 1024
+    src = [synth.rgbd_frame(h, w, t)[0] for t in range(4)]
+    dev = torch.empty(n * h * w, dtype=torch.uint8, device="cuda")
+    dev.view(n, h, w).copy_(torch.from_numpy(np.stack([src[i % 4] for i in range(n)])))
+    ex = amd.BatchExtractor(1000, 1.2, 8, 20, 7)
+    ex.reserve(w, h, n)
+    torch.cuda.synchronize()
+    ex.extract_device(dev.data_ptr(), n, w, h, w, h * w)
+    amd.device_sync()
+    ref = oracle_mod.Extractor(1000, 1.2, 8, 20, 7)
+    for i in (0, n - 3, n - 1):
+        _assert_same_kps(ex.fetch(i), ref.extract(src[i % 4]), f"batch[{i}]")
+
+
 def test_golden_c1_c2_on_device(amd):
     """HIP path == committed golden fixtures (independent of the oracle at run time)."""
     from test_golden_cpu import load_c1, load_c2
