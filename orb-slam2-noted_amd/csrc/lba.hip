@@ -540,7 +540,7 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused
 
 // One component `comp` of a free pose's quadratic form (Hpp upper 0..20, b_p 21..26): the pose's
 // contiguous run of pose-major records (conp), lane-strided with 8 loads in flight, then an xor
-// butterfly -- a fixed order, so lba_pose_sums (first slot) and lba_schur_tiles (every slot) form
+// butterfly -- a fixed order, so lba_reduce_points' pose workgroups (first slot) and lba_schur_tiles (every slot) form
 // the same bits. Returns the sum to every lane.
 __device__ __forceinline__ double pose_comp_sum(const Graph &g, int set, int ph, int comp, int lane) {
     const int t0 = g.ps_start[ph], t1 = g.ps_start[ph + 1];
@@ -580,11 +580,6 @@ __device__ __forceinline__ void pose_comp_store(Graph &g, int set, int w, int la
     g.Hpp[36 * ph + 6 * b + a] = v;
     if (maxdiag && a == b) g.partial[2 * kRedBlocks + 6 * ph + a] = fabs(v);
 }
-__global__ __launch_bounds__(256) void lba_pose_sums(Graph g) {
-    const LMState lm = *g.lm;
-    if (lm.done || !lm.newiter) return;
-    pose_comp_store(g, lm.cur, 4 * blockIdx.x + (threadIdx.x >> 6), threadIdx.x & 63, true);
-}
 
 // the landmark reductions on 256-thread workgroups (one landmark per thread: a merged launch with
 // the pose reductions on 1024-thread workgroups spread the landmarks over 4x fewer CUs and took
@@ -594,10 +589,19 @@ __global__ __launch_bounds__(256) void lba_pose_sums(Graph g) {
 // snapshot, a pure function), workgroup 0 stores it into lm -- the other buffer, so no workgroup
 // can read a state another one already advanced. One launch per trial fewer than a separate
 // lba_decide.
-__global__ __launch_bounds__(256) void lba_reduce_points(Graph g, int n0, int nbt) {
+// npw > 0 (an optimize()'s first slot, never a deciding one): the last npw workgroups are
+// the pose reductions (Hpp, b_p and the pose maxDiagonal partials the lambda initialisation needs),
+// in the same launch as the landmark reductions instead of one of their own
+__global__ __launch_bounds__(256) void lba_reduce_points(Graph g, int n0, int nbt, int npw) {
     __shared__ double shp[256];
     __shared__ LMState lm_s;
     LMState lm;
+    if ((int)blockIdx.x >= (int)gridDim.x - npw) {   // uniform: pose workgroups
+        lm = *g.lm;
+        if (lm.done || !lm.newiter) return;
+        pose_comp_store(g, lm.cur, 4 * ((int)blockIdx.x - ((int)gridDim.x - npw)) + (threadIdx.x >> 6), threadIdx.x & 63, true);
+        return;
+    }
     if (g.lm_src) {   // uniform
         const LMState s0 = *g.lm_src;
         if (!s0.done) {
@@ -716,7 +720,7 @@ __global__ __launch_bounds__(256) void lba_schur_tiles(Graph g) {
         const int row = 4 * ((int)blockIdx.x - g.nchunks) + wv;
         if (row >= n6) return;
         const int ph = row / 6, a = row % 6, i0 = g.ps_start[ph], i1 = g.ps_start[ph + 1];
-        const double bpv = pose_comp_sum(g, g.lm->cur, ph, 21 + a, lane);   // b_p, the order lba_pose_sums uses
+        const double bpv = pose_comp_sum(g, g.lm->cur, ph, 21 + a, lane);   // b_p, the first slot's order
         if (lane == 0) g.bp[row] = bpv;
         double v = 0;
         for (int i = i0 + lane; i < i1; i += 256) {
@@ -1697,19 +1701,22 @@ struct LmPhase {
             lprof_end(e, ph, "lba_linearize");
         }
         ph = lprof_begin(e);
+        const int nrp = std::max(1, (A.Lm + kRPL - 1) / kRPL);
+        // lambda init (levenberg.cpp:179-191) in an optimize()'s first slot: the maxDiagonal needs
+        // Hpp before the Schur step (the pose workgroups of lba_reduce_points)
+        const int npw = first && A.P > 0 ? (27 * A.P + 3) / 4 : 0;
         if (decide) {
             Graph gd;
             advance(gd);
-            lba_reduce_points<<<std::max(1, (A.Lm + kRPL - 1) / kRPL), 256, 0, s>>>(gd, nbt, nbt);
+            lba_reduce_points<<<nrp + npw, 256, 0, s>>>(gd, nbt, nbt, npw);
         } else {
-            lba_reduce_points<<<std::max(1, (A.Lm + kRPL - 1) / kRPL), 256, 0, s>>>(g, nbt, nbt);
+            lba_reduce_points<<<nrp + npw, 256, 0, s>>>(g, nbt, nbt, npw);
         }
         lprof_end(e, ph, "lba_reduce_points");
-        if (first) {   // lambda init (levenberg.cpp:179-191): the maxDiagonal needs Hpp before the Schur
+        if (first) {
             ph = lprof_begin(e);
-            if (A.P > 0) lba_pose_sums<<<(27 * A.P + 3) / 4, 256, 0, s>>>(g);
-            lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nbt, std::max(1, (A.Lm + kRPL - 1) / kRPL), 6 * A.P);
-            lprof_end(e, ph, "lba_pose_sums_prep");
+            lba_prep_slots<<<nblk(nact + A.Lm), 256, 0, s>>>(g, nbt, nrp, 6 * A.P);
+            lprof_end(e, ph, "lba_prep_slots");
         }
     }
     // the rest of a trial slot: Schur complement, solve, update + the trial's residuals
@@ -1966,9 +1973,16 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.nact = nact;
         if (e->on.ensure(std::max(nact, 1))) return -1;
         g.on = e->on.as<uint8_t>();
-        if (e->E_lm.ensure(sizeof(EdgeDev) * std::max(nact, 1)) || e->on_lm.ensure(std::max(nact, 1))) return -1;
-        g.E_lm = e->E_lm.as<EdgeDev>();
-        g.on_lm = e->on_lm.as<uint8_t>();
+        // landmark-major slot order (A.mono): the landmark-major records and level flags are the
+        // slot ones themselves, no gathered copy
+        if (A.mono) {
+            g.E_lm = const_cast<EdgeDev *>(g.E);
+            g.on_lm = e->on.as<uint8_t>();
+        } else {
+            if (e->E_lm.ensure(sizeof(EdgeDev) * std::max(nact, 1)) || e->on_lm.ensure(std::max(nact, 1))) return -1;
+            g.E_lm = e->E_lm.as<EdgeDev>();
+            g.on_lm = e->on_lm.as<uint8_t>();
+        }
         g.pose_hidx = at<int>(e->arenaB, o_pose_hidx); g.point_hidx = at<int>(e->arenaB, o_point_hidx);
         g.hpose = at<int>(e->arenaB, o_hpose); g.hpoint = at<int>(e->arenaB, o_hpoint);
         g.P = A.P; g.Lm = A.Lm;
@@ -2023,7 +2037,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
             lba_init_buffers<<<dim3(gx, kInitRanges), 256, 0, s>>>(R);
             if (hipGetLastError() != hipSuccess) return -1;
         }
-        if (nact > 0) lba_gather_edges<<<nblk(nact), 256, 0, s>>>(g.E_lm, g.on_lm, g.E, g.pt_items, nact);
+        if (nact > 0 && !A.mono) lba_gather_edges<<<nblk(nact), 256, 0, s>>>(g.E_lm, g.on_lm, g.E, g.pt_items, nact);
         return 0;
     };
     // the block structure of the Schur product (build_schur_tiles) in an upload of its own: built on

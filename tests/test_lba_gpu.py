@@ -41,6 +41,29 @@ def test_lba_matches_oracle(amd, oracle_mod, seed, n_kf, n_pts):
     assert np.array_equal(got["edge_erase"], ref["edge_erase"])
 
 
+@pytest.mark.parametrize("order", ["shuffled", "reversed_ids"])
+def test_lba_edge_orders(amd, oracle_mod, order):
+    """Edges not landmark by landmark (the general path: landmark-major records gathered, their own
+    position arrays), and vertex ids against index order (the hessian sorted by id): same results
+    as the oracle on the same problem. ORB-SLAM2 itself adds the edges map point by map point
+    (Optimizer.cc:766-848), the fast path every other test takes."""
+    prob = dict(synth.localba_problem(seed=13, n_kf=12, n_points=1200))
+    rng = np.random.default_rng(1)
+    if order == "shuffled":
+        perm = rng.permutation(len(prob["edge_point"]))
+        for k in ("edge_point", "edge_pose", "edge_obs", "edge_inv_sigma2"):
+            prob[k] = np.ascontiguousarray(np.asarray(prob[k])[perm])
+    else:
+        prob["point_id"] = np.ascontiguousarray(np.asarray(prob["point_id"])[::-1])
+        prob["pose_id"] = np.ascontiguousarray(np.asarray(prob["pose_id"])[::-1])
+    ref = oracle_mod.lba_solve(prob)
+    got = amd.LocalBundleAdjustment().solve(prob)
+    assert got["iterations"] == ref["iterations"]
+    assert _rel(got["pose_Tcw"], ref["pose_Tcw"]) < RTOL
+    assert _rel(got["point_Xw"], ref["point_Xw"]) < RTOL
+    assert np.array_equal(got["edge_erase"], ref["edge_erase"])
+
+
 def test_lba_stop_flag(amd, oracle_mod):
     prob = synth.localba_problem(seed=7, n_kf=8, n_points=300)
     got = amd.LocalBundleAdjustment().solve(prob, stop=True)
