@@ -319,8 +319,8 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
 //          the current linearisation set.
 //   UPDATE (every trial, was lba_update + lba_errors): the landmark back substitution x_l =
 //          Dinv (b_l - Hpl^T x_p) (a fixed-order butterfly over the group), X_t = X + x_l, and each
-//          slot's pose T_t = exp(x_p) T formed in the lane (pose_oplus, the same bits the pose
-//          workgroups store), then the trial's residuals and linearisation into the trial set;
+//          slot's trial pose T_t = exp(x_p) T (trial_pose, stored by the solve), then the trial's
+//          residuals and linearisation into the trial set;
 //          computeScale pieces x (lambda x + b) -> scale_part[b]. One launch instead of two, and
 //          no grid-wide wait between the update and the residuals.
 constexpr int kLPL = 8, kLPB = 256 / kLPL;
@@ -343,13 +343,10 @@ __global__ __launch_bounds__(256) void lba_lin_points(Graph g, double *scale_par
     if (UPDATE && blockIdx.x == 0 && threadIdx.x == 0)
         g.scalars[6] = __hip_atomic_load(g.stopf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ? 1.0 : 0.0;
     double sc = 0, chi = 0;
-    if ((int)blockIdx.x >= nbl) {   // free poses (UPDATE): T_t = exp(x_p) T, computeScale pieces
+    if ((int)blockIdx.x >= nbl) {   // free poses (UPDATE): computeScale pieces
         const int t = ((int)blockIdx.x - nbl) * 256 + threadIdx.x;
-        if (UPDATE && t < g.P) {
-            Pose *Tt = cur ? g.T : g.T2;
-            const int v = g.hpose[t];
+        if (UPDATE && t < g.P) {   // (T_t itself: trial_pose, at the end of the solve)
             const double *xp = g.x + 6 * t;
-            Tt[v] = pose_oplus(Tc[v], xp);
             for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + g.bp[6 * t + k]);
         }
     } else if (isl) {
@@ -391,7 +388,7 @@ __global__ __launch_bounds__(256) void lba_lin_points(Graph g, double *scale_par
         for (int i = i0 + r; i < i1; i += kLPL) {
             const int s = g.pt_items[i], ph = g.lpos_ph[i];
             const EdgeDev e = g.E_lm[i];
-            const Pose T = (UPDATE && ph >= 0) ? pose_oplus(Tc[e.pose], g.x + 6 * ph) : Tc[e.pose];
+            const Pose T = ((UPDATE && ph >= 0) ? (cur ? g.T : g.T2) : Tc)[e.pose];   // a free pose's trial T_t
             chi += linearize_slot_at(g, e, g.on_lm[i] != 0, s, i, ph >= 0 ? g.lpos_ppos[i] : -1, T, Xn, set, 2);
         }
     }
@@ -925,6 +922,15 @@ template <int J, bool FULL> __device__ __forceinline__ void chol16_factor(double
     }
 }
 
+// The trial poses T_t = exp(x_p) T of the free poses (VertexSE3Expmap::oplusImpl), formed once
+// per pose at the end of the solve from the solution in LDS, into the trial estimate buffer:
+// lba_lin_points<true> reads them instead of forming exp(x_p) T in every record's lane (the
+// exp chain was the head of each lane's linearisation). Tc: the current pose of free pose t.
+__device__ __forceinline__ void trial_pose(const Graph &g, bool cur, int t, const Pose &Tc, const double *xp) {
+    Pose *Tt = cur ? g.T : g.T2;
+    Tt[g.hpose[t]] = pose_oplus(Tc, xp + 6 * t);
+}
+
 __host__ __device__ constexpr int chol_tiled_dim(int n) { return 16 * ((n + 16) / 16); }
 __host__ __device__ constexpr size_t chol_tiled_lds(int n) {
     return sizeof(double) * ((size_t)chol_tiled_dim(n) * (chol_tiled_dim(n) + 1) + (size_t)(chol_tiled_dim(n) / 16) * 16 * 17 +
@@ -938,7 +944,9 @@ constexpr int kCT = LBA_CHOL_THREADS, kCW = kCT / 64;   // threads, waves of lba
 __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
     extern __shared__ double A[];   // N2 x LDA, then Linv[NT][16][17], y[N2], x[N2]
     __shared__ int fail;
+    __shared__ Pose tpc[kSmallNP / 6];   // the free poses' current estimates (trial_pose at the end)
     if (g.lm->done) return;
+    const bool cur = g.lm->cur;
     const int n = 6 * g.P, N2 = chol_tiled_dim(n), NT = N2 / 16, LDA = N2 + 1;
     double *Linv = A + N2 * LDA, *yv = Linv + NT * 16 * 17, *xv = yv + N2;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -998,6 +1006,12 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
         diag(0);
     } else {   // waves 1..: the lower triangle of rows 16.. (N2 <= kSmallNP = 128), all loads in flight
         constexpr int RU = (128 - 16 + kCW - 2) / (kCW - 1);
+        // the last wave also fetches the free poses' current estimates for the trial poses
+        const bool tp = wv == kCW - 1 && lane < g.P;
+        const double *tsrc = (const double *)((cur ? g.T2 : g.T) + (tp ? g.hpose[lane] : 0));
+        double tc[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) tc[k] = tp ? tsrc[k] : 0.0;
         double v[RU][2];
 #pragma unroll
         for (int u = 0; u < RU; u++)
@@ -1013,6 +1027,9 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
                 const int r = 16 + wv - 1 + (kCW - 1) * u, c = lane + 64 * h;
                 if (r < N2 && c <= r) A[r * LDA + c] = v[u][h];
             }
+        if (tp)
+#pragma unroll
+            for (int k = 0; k < 8; k++) ((double *)&tpc[lane])[k] = tc[k];
     }
     __syncthreads();
 #ifdef LBA_PROFILE
@@ -1106,6 +1123,7 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
         __syncthreads();
     }
     for (int j = tid; j < n; j += kCT) g.x[j] = xv[j];
+    if (tid < g.P) trial_pose(g, cur, tid, tpc[tid], xv);
     if (tid == 0) g.scalars[4] = 1;
 #ifdef LBA_PROFILE
     if (tid == 0)
@@ -1245,6 +1263,8 @@ __global__ __launch_bounds__(1024) void lba_chol_solve_blocked(Graph g) {
         __syncthreads();
     }
     for (int i = tid; i < n; i += 1024) g.x[i] = y[i];
+    const bool cur = g.lm->cur;
+    for (int t = tid; t < g.P; t += 1024) trial_pose(g, cur, t, (cur ? g.T2 : g.T)[g.hpose[t]], y);
 }
 
 __global__ void lba_set_ok(Graph g) {
