@@ -323,10 +323,18 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
 //          residuals and linearisation into the trial set;
 //          computeScale pieces x (lambda x + b) -> scale_part[b]. One launch instead of two, and
 //          no grid-wide wait between the update and the residuals.
-constexpr int kLPL = 8, kLPB = 256 / kLPL;
+#ifndef LBA_LIN_ROLES
+#define LBA_LIN_ROLES 1   // 1: the two linearize_slot_at roles on two waves per 8 landmarks (role 0: residual,
+                          // Hll / bl, Hpl; role 1: Hpp / bp), each redoing the landmark update. Same box:
+                          // update_errors 0.256 -> 0.232 ms per call (profiles/r04_ab_lba_roles.log)
+#endif
+constexpr int kLPL = 8, kLPB = 256 / kLPL / (LBA_LIN_ROLES ? 2 : 1);
 template <bool UPDATE>
 __global__ __launch_bounds__(256) void lba_lin_points(Graph g, double *scale_part, double *chi_part, int nbl) {
-    const int grp = threadIdx.x / kLPL, r = threadIdx.x % kLPL;
+    const int wv = threadIdx.x >> 6;
+    const int role = LBA_LIN_ROLES ? (wv & 1) : 2;   // wave-uniform
+    const int grp = LBA_LIN_ROLES ? (wv >> 1) * (64 / kLPL) + (threadIdx.x & 63) / kLPL : threadIdx.x / kLPL;
+    const int r = threadIdx.x % kLPL;
     const int l = blockIdx.x * kLPB + grp;
     const bool isl = (int)blockIdx.x < nbl && l < g.Lm;
     // the landmark's record range goes out with the LM-state load
@@ -378,7 +386,7 @@ __global__ __launch_bounds__(256) void lba_lin_points(Graph g, double *scale_par
             for (int a = 0; a < 3; a++) {
                 const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
                 Xn[a] += xa;
-                if (r == 0) {
+                if (r == 0 && role != 1) {
                     xl[a] = xa;
                     Xt[3 * v + a] = Xn[a];
                     sc += xa * (lambda * xa + bl[a]);
@@ -389,7 +397,7 @@ __global__ __launch_bounds__(256) void lba_lin_points(Graph g, double *scale_par
             const int s = g.pt_items[i], ph = g.lpos_ph[i];
             const EdgeDev e = g.E_lm[i];
             const Pose T = ((UPDATE && ph >= 0) ? (cur ? g.T : g.T2) : Tc)[e.pose];   // a free pose's trial T_t
-            chi += linearize_slot_at(g, e, g.on_lm[i] != 0, s, i, ph >= 0 ? g.lpos_ppos[i] : -1, T, Xn, set, 2);
+            chi += linearize_slot_at(g, e, g.on_lm[i] != 0, s, i, ph >= 0 ? g.lpos_ppos[i] : -1, T, Xn, set, role);
         }
     }
     if (UPDATE) {
