@@ -186,7 +186,7 @@ __device__ inline void huber(const EdgeDev &e, double chi, double &rho0, double 
 // block sum of one double per thread into *dst (also returned, to every thread)
 __device__ inline double block_sum_to(double v, double *dst) {
     __shared__ double sh[256];
-    sh[threadIdx.x] = v;
+    if (threadIdx.x < 256) sh[threadIdx.x] = v;   // (lba_lin_points' trial-pose wave holds 0)
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
         if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
@@ -319,7 +319,7 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
 //          the current linearisation set.
 //   UPDATE (every trial, was lba_update + lba_errors): the landmark back substitution x_l =
 //          Dinv (b_l - Hpl^T x_p) (a fixed-order butterfly over the group), X_t = X + x_l, and each
-//          slot's trial pose T_t = exp(x_p) T (trial_pose, stored by the solve), then the trial's
+//          slot's trial pose T_t = exp(x_p) T (the fifth wave's, below), then the trial's
 //          residuals and linearisation into the trial set;
 //          computeScale pieces x (lambda x + b) -> scale_part[b]. One launch instead of two, and
 //          no grid-wide wait between the update and the residuals.
@@ -329,14 +329,22 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
                           // update_errors 0.256 -> 0.232 ms per call (profiles/r04_ab_lba_roles.log)
 #endif
 constexpr int kLPL = 8, kLPB = 256 / kLPL / (LBA_LIN_ROLES ? 2 : 1);
+// lba_lin_points<true> workgroups carry a fifth wave that forms the trial poses T_t = exp(x_p) T
+// of a small window (6P <= kSmallNP: lba_chol_tiled's) into LDS while the other four run the
+// landmark update: the exp chain overlaps the update's loads instead of ending the solve
+// (trial_pose, which the blocked path keeps)
+constexpr int kLinThreads = 320;
 template <bool UPDATE>
-__global__ __launch_bounds__(256) void lba_lin_points(Graph g, double *scale_part, double *chi_part, int nbl) {
-    const int wv = threadIdx.x >> 6;
+__global__ __launch_bounds__(UPDATE ? kLinThreads : 256) void lba_lin_points(Graph g, double *scale_part, double *chi_part,
+                                                                           int nbl) {
+    __shared__ Pose tps[kSmallNP / 6];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int role = LBA_LIN_ROLES ? (wv & 1) : 2;   // wave-uniform
-    const int grp = LBA_LIN_ROLES ? (wv >> 1) * (64 / kLPL) + (threadIdx.x & 63) / kLPL : threadIdx.x / kLPL;
+    const int grp = LBA_LIN_ROLES ? (wv >> 1) * (64 / kLPL) + lane / kLPL : threadIdx.x / kLPL;
     const int r = threadIdx.x % kLPL;
     const int l = blockIdx.x * kLPB + grp;
-    const bool isl = (int)blockIdx.x < nbl && l < g.Lm;
+    const bool isl = (int)blockIdx.x < nbl && wv < 4 && l < g.Lm;
+    const bool small = UPDATE && 6 * g.P <= kSmallNP;   // trial poses: tps (else the solve's trial_pose)
     // the landmark's record range goes out with the LM-state load
     const int i0 = isl ? g.pt_start[l] : 0, i1 = isl ? g.pt_start[l + 1] : 0;
     const LMState lm = *g.lm;
@@ -351,15 +359,22 @@ __global__ __launch_bounds__(256) void lba_lin_points(Graph g, double *scale_par
     if (UPDATE && blockIdx.x == 0 && threadIdx.x == 0)
         g.scalars[6] = __hip_atomic_load(g.stopf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ? 1.0 : 0.0;
     double sc = 0, chi = 0;
-    if ((int)blockIdx.x >= nbl) {   // free poses (UPDATE): computeScale pieces
+    if ((int)blockIdx.x >= nbl) {   // free poses (UPDATE): T_t (small windows), computeScale pieces
         const int t = ((int)blockIdx.x - nbl) * 256 + threadIdx.x;
-        if (UPDATE && t < g.P) {   // (T_t itself: trial_pose, at the end of the solve)
+        if (UPDATE && t < g.P && threadIdx.x < 256) {
             const double *xp = g.x + 6 * t;
+            if (small) {
+                const int v = g.hpose[t];
+                (cur ? g.T : g.T2)[v] = pose_oplus(Tc[v], xp);
+            }
             for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + g.bp[6 * t + k]);
         }
-    } else if (isl) {
+    } else {
+      if (small && wv == 4 && lane < g.P) tps[lane] = pose_oplus(Tc[g.hpose[lane]], g.x + 6 * lane);
+      double Xn[3] = {0, 0, 0};
+      if (isl) {
         const int v = g.hpoint[l];
-        double Xn[3] = {Xc[3 * v], Xc[3 * v + 1], Xc[3 * v + 2]};
+        Xn[0] = Xc[3 * v]; Xn[1] = Xc[3 * v + 1]; Xn[2] = Xc[3 * v + 2];
         if (UPDATE) {
             double c[3] = {0, 0, 0};
             const double *hpL = g.hpl[cur];
@@ -393,10 +408,14 @@ __global__ __launch_bounds__(256) void lba_lin_points(Graph g, double *scale_par
                 }
             }
         }
+      }
+      if (small) __syncthreads();   // workgroup-uniform: tps complete
+      if (isl)
         for (int i = i0 + r; i < i1; i += kLPL) {
             const int s = g.pt_items[i], ph = g.lpos_ph[i];
             const EdgeDev e = g.E_lm[i];
-            const Pose T = ((UPDATE && ph >= 0) ? (cur ? g.T : g.T2) : Tc)[e.pose];   // a free pose's trial T_t
+            // a free pose's trial T_t
+            const Pose T = (UPDATE && ph >= 0) ? (small ? tps[ph] : (cur ? g.T : g.T2)[e.pose]) : Tc[e.pose];
             chi += linearize_slot_at(g, e, g.on_lm[i] != 0, s, i, ph >= 0 ? g.lpos_ppos[i] : -1, T, Xn, set, role);
         }
     }
@@ -930,10 +949,9 @@ template <int J, bool FULL> __device__ __forceinline__ void chol16_factor(double
     }
 }
 
-// The trial poses T_t = exp(x_p) T of the free poses (VertexSE3Expmap::oplusImpl), formed once
-// per pose at the end of the solve from the solution in LDS, into the trial estimate buffer:
-// lba_lin_points<true> reads them instead of forming exp(x_p) T in every record's lane (the
-// exp chain was the head of each lane's linearisation). Tc: the current pose of free pose t.
+// The trial poses T_t = exp(x_p) T of the free poses (VertexSE3Expmap::oplusImpl) of a window
+// beyond lba_chol_tiled's, formed at the end of the blocked solve into the trial estimate buffer
+// (lba_lin_points<true> forms a small window's itself). Tc: the current pose of free pose t.
 __device__ __forceinline__ void trial_pose(const Graph &g, bool cur, int t, const Pose &Tc, const double *xp) {
     Pose *Tt = cur ? g.T : g.T2;
     Tt[g.hpose[t]] = pose_oplus(Tc, xp + 6 * t);
@@ -952,9 +970,7 @@ constexpr int kCT = LBA_CHOL_THREADS, kCW = kCT / 64;   // threads, waves of lba
 __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
     extern __shared__ double A[];   // N2 x LDA, then Linv[NT][16][17], y[N2], x[N2]
     __shared__ int fail;
-    __shared__ Pose tpc[kSmallNP / 6];   // the free poses' current estimates (trial_pose at the end)
     if (g.lm->done) return;
-    const bool cur = g.lm->cur;
     const int n = 6 * g.P, N2 = chol_tiled_dim(n), NT = N2 / 16, LDA = N2 + 1;
     double *Linv = A + N2 * LDA, *yv = Linv + NT * 16 * 17, *xv = yv + N2;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1014,12 +1030,6 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
         diag(0);
     } else {   // waves 1..: the lower triangle of rows 16.. (N2 <= kSmallNP = 128), all loads in flight
         constexpr int RU = (128 - 16 + kCW - 2) / (kCW - 1);
-        // the last wave also fetches the free poses' current estimates for the trial poses
-        const bool tp = wv == kCW - 1 && lane < g.P;
-        const double *tsrc = (const double *)((cur ? g.T2 : g.T) + (tp ? g.hpose[lane] : 0));
-        double tc[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) tc[k] = tp ? tsrc[k] : 0.0;
         double v[RU][2];
 #pragma unroll
         for (int u = 0; u < RU; u++)
@@ -1035,9 +1045,6 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
                 const int r = 16 + wv - 1 + (kCW - 1) * u, c = lane + 64 * h;
                 if (r < N2 && c <= r) A[r * LDA + c] = v[u][h];
             }
-        if (tp)
-#pragma unroll
-            for (int k = 0; k < 8; k++) ((double *)&tpc[lane])[k] = tc[k];
     }
     __syncthreads();
 #ifdef LBA_PROFILE
@@ -1131,7 +1138,6 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
         __syncthreads();
     }
     for (int j = tid; j < n; j += kCT) g.x[j] = xv[j];
-    if (tid < g.P) trial_pose(g, cur, tid, tpc[tid], xv);
     if (tid == 0) g.scalars[4] = 1;
 #ifdef LBA_PROFILE
     if (tid == 0)
@@ -1781,7 +1787,7 @@ struct LmPhase {
         }
         // scalars[8..): the trial's computeScale block sums, then its chi2 block sums (nbt each)
         ph = lprof_begin(e);
-        lba_lin_points<true><<<nbt, 256, 0, s>>>(g, g.scalars + 8, g.scalars + 8 + nbt, nbl);
+        lba_lin_points<true><<<nbt, kLinThreads, 0, s>>>(g, g.scalars + 8, g.scalars + 8 + nbt, nbl);
         lprof_end(e, ph, "lba_update_errors");
     }
     // optimize() start (levenberg.cpp:66-72 reset, the first terminate() check)
