@@ -42,8 +42,12 @@ typedef struct {
  * Input range (checked by orbx_reserve / orbx_extract, ORBX_EINVAL otherwise): image width and
  * height <= 4000 (keys carry 12-bit coordinates), every pyramid level >= 40 x 40 pixels (the
  * 19-pixel FAST border plus the blur halo; ORBextractor.cc:1084-1100 detects nothing in a
- * smaller level), and scaleFactor <= 2 (the resize kernel's 4 outputs span <= 8 source bytes). */
+ * smaller level), and scaleFactor <= 2 (the resize kernel's 4 outputs span <= 8 source bytes).
+ * struct_size must be sizeof(orbx_params) of the header the caller was built against: orbx_create
+ * refuses any other value with ORBX_EINVAL, so a caller built against an older layout (fewer
+ * fields) fails at creation instead of having fields read past its struct. */
 typedef struct {
+    uint32_t struct_size;   /* = sizeof(orbx_params) */
     int32_t nfeatures;
     float scale_factor;
     int32_t nlevels;
@@ -95,11 +99,12 @@ int orbx_blurred_level(orbx_engine *e, int image, int level, uint8_t *dst, int *
 int orbx_reserve(orbx_engine *e, int w, int h, int max_images);
 /* Extract n_images frames already resident in device memory (u8, image i at
  * d_imgs + i * image_stride, rows `pitch` bytes apart; image_stride >= pitch*(h-1)+w when
- * n_images > 1). Input tail: the 16 bytes after the last pixel of the last image must be
- * readable device memory (the level-0 staging and level-1 resize read aligned dwords; the
- * extra bytes never reach a result). Asynchronous on `stream` (hipStream_t; NULL = the
- * engine's stream), ordered after the engine's previous work; results stay on the device and
- * orbx_batch_fetch waits for this engine's work only. */
+ * n_images > 1). No byte outside the images' pixels is read: the last image may end exactly at
+ * the end of the caller's allocation, as a cv::Mat's data does (ORBextractor.cc:1543-1560).
+ * Every buffer descriptor over the input carries the level's exact extent, so the hardware
+ * range check would return 0 for a byte past it instead of faulting. Asynchronous on `stream`
+ * (hipStream_t; NULL = the engine's stream), ordered after the engine's previous work; results
+ * stay on the device and orbx_batch_fetch waits for this engine's work only. */
 int orbx_extract_batch_device(orbx_engine *e, const uint8_t *d_imgs, int n_images, int w,
                               int h, int pitch, size_t image_stride, void *stream);
 /* The same in two halves on one stream, so that two engines can interleave their batches:
@@ -649,7 +654,8 @@ typedef struct lba_engine lba_engine;
  * -- by the device itself: while the call runs, the host copies *stop into a page-locked,
  * device-mapped word that the LM decision kernel reads with a system-scope load, so a flag raised
  * by another thread mid-call ends the optimisation after the trial in flight. With a non-NULL
- * `stop` the call polls its stream instead of blocking in hipStreamSynchronize. */
+ * `stop` the call polls its stream instead of blocking in hipStreamSynchronize: a short spin, then
+ * sched_yield() between queries (sleeps past 2 ms), so the core goes to any thread that wants it. */
 int lba_create(lba_engine **out);
 void lba_destroy(lba_engine *e);
 int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile uint8_t *stop);
@@ -657,7 +663,9 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
  * raised the moment trial `trial` (1-based; 0 = before the first iteration) of optimize() call
  * `phase` (1 = optimize(5), 2 = optimize(10)) has completed, and stayed raised. phase 0 removes
  * the hook. The CPU oracle has the same hook (lba_oracle_solve_hook), so a stop at any (phase,
- * trial) is parity-tested deterministically. */
+ * trial) is parity-tested deterministically. phase 3: a live raise at a deterministic point -- the
+ * call itself writes 1 into the caller's `stop` flag once it has read back its trial-th chunk of LM
+ * trials (trial >= 1; no effect when `stop` is NULL), as another thread setting mbAbortBA would. */
 int lba_set_stop_hook(lba_engine *e, int phase, int trial);
 /* Per-kernel hipEvent timing of lba_solve's trial chain on the engine stream (bench.py localba
  * roofline); same semantics as orbx_profile / orbx_profile_read. */

@@ -201,6 +201,27 @@ def stereo_matches(exL: Extractor, exR: Extractor, kL, dL, kR, dR, mbf, mb):
     return uR[:nL], dep[:nL]
 
 
+def stereo_frames(pool, idx, nfeatures=2000, mbf=386.1448, mb=None, threads=None, **ex_kw):
+    """{j: (kL, dL, kR, dR, uR, depth)} for the stereo pairs pool[j], j in idx: ORBextractor on
+    L and R + Frame::ComputeStereoMatches, one pair per task on a thread pool (the C calls release
+    the GIL). mb defaults to KITTI's mbf / fx in float (Frame.cc:136)."""
+    from concurrent.futures import ThreadPoolExecutor
+    if mb is None:
+        mb = float(np.float32(mbf) / np.float32(718.856))
+
+    def one(j):
+        L, R = pool[j]
+        exL, exR = Extractor(nfeatures, **ex_kw), Extractor(nfeatures, **ex_kw)
+        kL, dL = exL.extract(L)
+        kR, dR = exR.extract(R)
+        u, d = stereo_matches(exL, exR, kL, dL, kR, dR, mbf, mb)
+        return j, (kL, dL, kR, dR, u, d)
+    if threads is None:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    with ThreadPoolExecutor(threads) as ex:
+        return dict(ex.map(one, sorted(set(idx))))
+
+
 def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
     a = np.ascontiguousarray(a, np.uint8)
     b = np.ascontiguousarray(b, np.uint8)

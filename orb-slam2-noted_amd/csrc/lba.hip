@@ -44,6 +44,7 @@
 #include <climits>
 #include <cstring>
 #include <numeric>
+#include <sched.h>
 #include <string>
 #include <thread>
 #include <vector>
@@ -909,7 +910,9 @@ template <int J, int C> __device__ __forceinline__ void chol16_update(double (&r
 }
 
 // Lane i (of each 16-lane row) holds row i of the tile; column J is pivoted, scaled by the
-// reciprocal square root (v_rsq_f64 + 2 Newton steps) and subtracted from columns > J.
+// reciprocal square root (v_rsq_f64 + LBA_RSQ_NEWTON Newton steps, 1 in the product: the
+// near-singular windows of tests/test_lba_gpu.py::test_lba_near_singular, pivot ratios down to
+// 2e-5, keep the oracle's LM path) and subtracted from columns > J.
 // li carries column i of L^-1 by forward substitution, fed by the same broadcasts.
 // FULL (every tile but the last, all 16 rows < n): li starts as the unit column e_i and lane
 // J's own row[J] is the pivot d, so the pivot step is two products; otherwise pivots at
@@ -1596,6 +1599,7 @@ struct lba_engine {
     unsigned *d_stop = nullptr;
     hipEvent_t ev_chunk[2] = {nullptr, nullptr};   // per optimize(): its last chunk's state readback
     int hook_phase = 0, hook_trial = 0;   // lba_set_stop_hook
+    int chunks_seen = 0;                  // chunk readbacks of the current call (hook phase 3)
     // per-kernel hipEvent timing on the engine stream (lba_profile; bench.py localba roofline)
     bool prof = false;
     struct ProfRec { const char *name; hipEvent_t a, b; };
@@ -1832,20 +1836,37 @@ struct LmPhase {
             return -3;
         return 0;
     }
-    // wait for the last chunk's readback, keeping the device's copy of the flag current
+    // wait for the last chunk's readback, keeping the device's copy of the flag current. The poll
+    // gives its core away: a short pause-spin (a chunk often ends within it), then sched_yield()
+    // between queries -- free when the core is idle, and the Tracking threads' extractor calls
+    // (Frame.cc:144-153) run first when they want the core -- and, past 2 ms (only an unusually
+    // long chunk), 20 us sleeps. The flag is still mirrored at every query.
     int wait(LMState &st) {
         if (!stop) {
             if (hipEventSynchronize(ev) != hipSuccess) return -3;
         } else {
-            while (true) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int it = 0;; it++) {
                 mirror();
                 const hipError_t q = hipEventQuery(ev);
                 if (q == hipSuccess) break;
                 if (q != hipErrorNotReady) return -3;
-                for (int k = 0; k < 64; k++) __builtin_ia32_pause();   // stay on the core: a chunk is ~0.5 ms
+                if (it < 16) {
+                    for (int k = 0; k < 64; k++) __builtin_ia32_pause();
+                } else if (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2)) {
+                    sched_yield();
+                } else {
+                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+                }
             }
         }
         st = *h_state;
+        // test hook (lba_set_stop_hook phase 3): the host raises the caller's flag itself once it has
+        // read back the call's hook_trial-th chunk -- a mid-call raise at a deterministic point
+        if (stop && e->hook_phase == 3 && ++e->chunks_seen == e->hook_trial) {
+            *const_cast<volatile uint8_t *>(stop) = 1;
+            mirror();
+        }
         return 0;
     }
     // two slots per chunk while retries remain (the first chunk holds one trial per iteration: the
@@ -1971,6 +1992,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     // lba_init_buffers, before any kernel reads them
     int cur = 0;
     *e->h_stop = 0u;
+    e->chunks_seen = 0;
     Graph g{};
     g.stopf = e->d_stop;
     g.T = at<Pose>(e->arenaA, oT); g.T2 = at<Pose>(e->arenaA, oT2);
@@ -2221,7 +2243,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
 }
 
 int lba_set_stop_hook(lba_engine *e, int phase, int trial) {
-    if (!e || phase < 0 || phase > 2 || trial < 0) return ORBX_EINVAL;
+    if (!e || phase < 0 || phase > 3 || trial < 0 || (phase == 3 && trial < 1)) return ORBX_EINVAL;
     e->hook_phase = phase;
     e->hook_trial = trial;
     return ORBX_OK;

@@ -143,10 +143,20 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
     // workgroup-uniform buffer descriptors over the source level and the output level: row
     // offsets as 32-bit VGPR offsets (no per-row 64-bit address arithmetic, no flat loads)
     // (the source descriptor starts at the dword holding the level's first byte: the input image of a
-    // batch may start at any byte)
+    // batch may start at any byte). Each descriptor's record count is its level's exact extent --
+    // the source from that dword to the dword holding the last pixel of the last row, the output to
+    // its last row's end -- so the hardware range check returns 0 for (and drops stores to) any byte
+    // past the level; none is addressed (the guarded loads below), so this is defence in depth for
+    // level 1, whose source is the caller's image (include/orbslam2_amd.h: no readable tail).
     const uint32_t s0 = (uint32_t)((uintptr_t)src & 3);
+    // bytes of the source level from the descriptor base to the end of its last row: a 12-byte
+    // window of the last row's last column group can reach past it, and for level 0 of a
+    // batch's last image that is past the end of the caller's buffer (a fault when the buffer
+    // ends on a page: 512 VGA frames are exactly 75 x 2 MiB). Those windows load dword by dword,
+    // none starting past the end (an aligned dword never crosses a page).
+    const uint32_t lim = s0 + (uint32_t)((g.lh[l - 1] - 1) * sp + g.lw[l - 1]);
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(src - s0), 0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(src - s0), 0, (int)((lim + 3u) & ~3u), 0x00020000);
     // 1. horizontal pass
     {
         int2 c[4];
@@ -173,12 +183,6 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
             span = max(span, o[k] + d[k]);
         }
         const bool win8 = span <= 7;
-        // bytes of the source level from the descriptor base to the end of its last row: a 12-byte
-        // window of the last row's last column group can reach past it, and for level 0 of a
-        // batch's last image that is past the end of the caller's buffer (a fault when the buffer
-        // ends on a page: 512 VGA frames are exactly 75 x 2 MiB). Those windows load dword by dword,
-        // none starting past the end (an aligned dword never crosses a page).
-        const uint32_t lim = s0 + (uint32_t)((g.lh[l - 1] - 1) * sp + g.lw[l - 1]);
         // all loads of a thread's source rows are issued before any use (6 rows x 3 dwords
         // in flight; the level-1 pass streams the input image from HBM)
         for (int jb = threadIdx.x >> 5; jb < nsr; jb += 8 * RZ_HJ) {
@@ -229,7 +233,8 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
     __syncthreads();
     // 2. vertical pass
     uint8_t *dst = pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
-    const __amdgpu_buffer_rsrc_t rdst = __builtin_amdgcn_make_buffer_rsrc((void *)dst, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rdst =
+        __builtin_amdgcn_make_buffer_rsrc((void *)dst, 0, (dh - 1) * g.bp[l] + dw, 0x00020000);
     const int n = min(4, dw - dx0);
     if (n <= 0) return;
     const uint32_t bpl = (uint32_t)g.bp[l];
@@ -242,9 +247,11 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
         const uint32_t S0[4] = {A.x, A.y, A.z, A.w}, S1[4] = {B.x, B.y, B.z, B.w};
         uint32_t out = 0;
         if (!SIMD) {
-            // FixedPtCast (b0 S0 + b1 S1 + 2^21) >> 22 as byte 3 of 4 (b0 S0 + b1 S1) + 2^23: S <= 255 * 2^11
-            // and b0 + b1 = 2^11 keep the sum below 2^30, so two full-rate v_mad_u32_u24 per pixel and
-            // one byte gather per 4 pixels (the result is <= 255: no clamp)
+            // FixedPtCast (b0 S0 + b1 S1 + 2^21) >> 22 as byte 3 of 4 (b0 S0 + b1 S1) + 2^23: with
+            // S <= 255 * 2^11 (a0 + a1 = 2^11) and b0 + b1 = 2^11, 4 (b0 S0 + b1 S1) + 2^23 <=
+            // 255 * 2^24 + 2^23 < 2^32 -- less than one bit of headroom, so engine_reserve refuses any
+            // coefficient table whose pairs do not sum to exactly 2^11. Two full-rate
+            // v_mad_u32_u24 per pixel and one byte gather per 4 pixels (the result is <= 255: no clamp)
             const uint32_t b0 = (uint32_t)ry.z << 2, b1 = (uint32_t)ry.w << 2;
             uint32_t t[4];
 #pragma unroll
@@ -1840,10 +1847,20 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     const uint8_t *img = l == 0 ? in + (long long)b * g.in_stride : pyr + (long long)b * g.pyr_stride + g.pyr_off[l];
     const int pitch = l == 0 ? g.in_pitch : g.bp[l];
     const unsigned long long icb = (unsigned long long)(img + (long long)(ky - 15) * pitch + kx - 16);
+    // Every descriptor below carries the exact byte count from its base to the end of its level's
+    // last row, so the hardware range check zeroes anything past the level -- for level 0 that is the
+    // caller's image, which has no readable tail (include/orbslam2_amd.h). No load reaches there: a
+    // keypoint lies in the detection region [19, w - 19) x [19, h - 19) (fast_blur_kernel), the
+    // IC_Angle rows read columns kx - 16 .. kx + 15 <= w - 5 of rows ky - 15 .. ky + 15 <= h - 5 and
+    // the blurred patch columns <= kx + 21 <= w + 1 of rows <= ky + 18 <= h - 2 (a row that is not the
+    // level's last, so a byte past its width is the next row's). Loads that add a row step in
+    // soffset are covered by that argument, not by the range check.
+    const int icn = (int)((long long)(l == 0 ? g.in_pitch : g.bp[l]) * (g.lh[l] - (ky - 15) - 1) + g.lw[l] - (kx - 16));
     const int bw = g.bp[l];
     const long long c0 = (long long)b * g.blur_stride + g.blur_off[l] + (long long)(ky - 18) * bw + (kx - 18);
     const int psh = (int)(c0 & 3);
     const long long a0 = c0 - psh;
+    const int bln = (int)(((long long)bw * (g.lh[l] - (ky - 18) - 1) + g.lw[l] - (kx - 18) + psh + 3) & ~3LL);
     const long long amax = (long long)g.nimg * g.blur_stride - 4;
     const unsigned long long smask = __ballot(valid && a0 >= 0 && a0 + 36LL * bw + 4 * PW <= amax + 4);
     auto rl64 = [](unsigned long long v, int r) {
@@ -1860,7 +1877,8 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
 #pragma unroll
         for (int k = 0; k < 4; k++) P[r][k] = 0u;
         if (!((vmask >> r) & 1)) continue;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)rl64(icb, r), 0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)rl64(icb, r), 0, __builtin_amdgcn_readlane(icn, r), 0x00020000);
         const int pr = __builtin_amdgcn_readlane(pitch, r);
         if constexpr (WIDE) {
             if (wrow <= 30) {
@@ -1888,7 +1906,8 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
             if (!((smask >> r) & 1)) continue;
             const int bwr = __builtin_amdgcn_readlane(bw, r);
             const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc((void *)(blur + (long long)rl64((unsigned long long)a0, r)), 0, 0x7fffffff, 0x00020000);
+                __builtin_amdgcn_make_buffer_rsrc((void *)(blur + (long long)rl64((unsigned long long)a0, r)), 0,
+                                                  __builtin_amdgcn_readlane(bln, r), 0x00020000);
             if constexpr (WIDE) {
                 // lane t = lane + 64 k (k = 0, 1) -> row t / 3, bytes 16 (t % 3) .. + 15 of the 48
 #pragma unroll
@@ -2261,6 +2280,10 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
                 if (sx < 0) { fx = 0; sx = 0; }
                 if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
                 const int a0 = satS((1.f - fx) * 2048), a1 = satS(fx * 2048);
+                // the kernel's vertical pass has no clamp (resize_level_kernel): it needs
+                // a0 + a1 == b0 + b1 == 2^11 -- every level of every width <= 4000 at scale factors
+                // 1.1-2.0 has it (float32 emulation); enforced here, not assumed
+                if (a0 < 0 || a1 < 0 || a0 + a1 != 2048) return ORBX_EINVAL;
                 const int sx1 = std::min(sx + 1, sw - 1);
                 rzc.push_back(make_int2(sx | (a0 << 16), a1 | ((sx1 - sx) << 16)));
             }
@@ -2270,7 +2293,9 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
                 int sy = (int)std::floor(fy);
                 fy -= sy;
                 auto clip = [sh](int y) { return y >= 0 ? (y < sh ? y : sh - 1) : 0; };
-                rzr.push_back(make_int4(clip(sy), clip(sy + 1), satS((1.f - fy) * 2048), satS(fy * 2048)));
+                const int b0 = satS((1.f - fy) * 2048), b1 = satS(fy * 2048);
+                if (b0 < 0 || b1 < 0 || b0 + b1 != 2048) return ORBX_EINVAL;   // as a0 + a1 above
+                rzr.push_back(make_int4(clip(sy), clip(sy + 1), b0, b1));
             }
             g.rz_simd_end[l] = e->p.resize_mode ? simd_end_for(dw) : 0;
             // source rows one output tile spans (LDS of the horizontal pass)
@@ -2432,6 +2457,7 @@ int orbslam2_amd_device_count(void) {
 int orbx_create(const orbx_params *p, orbx_engine **out) {
     if (!p || !out) return ORBX_EINVAL;
     *out = nullptr;
+    if (p->struct_size != sizeof(orbx_params)) return ORBX_EINVAL;   // a caller built against another layout
     if (p->nlevels < 1 || p->nlevels > ORBX_MAXL || p->nfeatures < 0 || !(p->scale_factor > 1.0f))
         return ORBX_EINVAL;
     if ((unsigned)p->resize_mode > 1u || (unsigned)p->blur_mode > 1u) return ORBX_EINVAL;
@@ -2630,10 +2656,9 @@ int orbx_extract(orbx_engine *e, const uint8_t *img, int w, int h, int stride, o
     HIPCHK(hipSetDevice(e->device));
     int rc = orbamd::engine_reserve(e, w, h, std::max(1, e->max_images));
     if (rc) return rc;
-    // +16: the aligned dword loads of the level-0 staging / level-1 resize may read up to
-    // 11 bytes past the last pixel of the last row (include/orbslam2_amd.h, input tail)
+    // exactly the image: no kernel reads past its last pixel (include/orbslam2_amd.h, input range)
     const size_t img_bytes = (size_t)w * h;
-    if (e->d_in.ensure(img_bytes + 16)) return ORBX_EDEVICE;
+    if (e->d_in.ensure(img_bytes)) return ORBX_EDEVICE;
     // the host image is packed into the pinned staging buffer (the previous call's transfers on
     // this stream have completed: every call ends with a stream synchronisation) and goes up in
     // one DMA

@@ -135,6 +135,7 @@ const char *orbx_build_id(void) { return ORBX_SRC_HASH ORBX_BUILD_SUFFIX; }
 int orbx_pipeline_create(const orbx_params *p, int n_engines, orbx_pipeline **out) {
     if (!p || !out) return ORBX_EINVAL;
     *out = nullptr;
+    if (p->struct_size != sizeof(orbx_params)) return ORBX_EINVAL;
     if (n_engines <= 0) n_engines = 3;
     if (n_engines > 16) return ORBX_EINVAL;
     orbx_pipeline *pl = new orbx_pipeline();
@@ -233,8 +234,8 @@ int orbx_pipeline_stereo_batch_host(orbx_pipeline *pl, const uint8_t *h_imgs, in
         for (int j = 0; j < k; j++)
             if (hipEventCreateWithFlags(&pl->ev_d2h[j], hipEventDisableTiming) != hipSuccess) return ORBX_EDEVICE;
     }
-    // device slot: the batch in the caller's layout, + 16 readable tail bytes (orbslam2_amd.h)
-    const size_t need = 2 * (size_t)n_pairs * image_stride + 16;
+    // device slot: the batch in the caller's layout (no readable tail needed, orbslam2_amd.h)
+    const size_t need = 2 * (size_t)n_pairs * image_stride;
     if (need > pl->slot_bytes) {
         for (int sl = 0; sl < 2; sl++) {   // slots may still be read by earlier batches
             for (int j = 0; j < k; j++)

@@ -42,7 +42,7 @@ class ORBextractor {
 public:
     ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
         : nfeatures_(nfeatures), nlevels_(nlevels), scaleFactor_(scaleFactor) {
-        orbx_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, /*resize_mode*/ 0, /*blur_mode*/ 0};
+        orbx_params p{sizeof(orbx_params), nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, /*resize_mode*/ 0, /*blur_mode*/ 0};
         check(orbx_create(&p, &h_), "orbx_create");
     }
     ~ORBextractor() { orbx_destroy(h_); }

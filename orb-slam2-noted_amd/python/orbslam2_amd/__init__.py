@@ -33,7 +33,7 @@ ORBX_OK, ORBX_EINVAL, ORBX_EDEVICE, ORBX_ECAP, ORBX_ESTATE = 0, -1, -2, -3, -4
 
 
 class OrbxParams(C.Structure):
-    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+    _fields_ = [("struct_size", C.c_uint32), ("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32), ("resize_mode", C.c_int32),
                 ("blur_mode", C.c_int32)]
 
@@ -232,7 +232,7 @@ class ORBextractor:
     def __init__(self, nfeatures: int, scaleFactor: float = 1.2, nlevels: int = 8,
                  iniThFAST: int = 20, minThFAST: int = 7, resize_mode: int = 0, blur_mode: int = 0):
         self._h = C.c_void_p()
-        p = OrbxParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_mode, blur_mode)
+        p = OrbxParams(C.sizeof(OrbxParams), nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_mode, blur_mode)
         _check(lib().orbx_create(C.byref(p), C.byref(self._h)), "orbx_create")
         self.nfeatures = nfeatures
         self.nlevels = nlevels
@@ -464,7 +464,7 @@ class StereoPipeline:
                  iniThFAST: int = 20, minThFAST: int = 7, n_engines: int = 3, resize_mode: int = 0,
                  blur_mode: int = 0):
         self._h = C.c_void_p()
-        p = OrbxParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_mode, blur_mode)
+        p = OrbxParams(C.sizeof(OrbxParams), nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_mode, blur_mode)
         _check(lib().orbx_pipeline_create(C.byref(p), n_engines, C.byref(self._h)), "orbx_pipeline_create")
         self.nfeatures, self.nlevels = nfeatures, nlevels
         self.engines = []

@@ -102,6 +102,45 @@ def stereo_pair(h: int, w: int, t: int, base_seed: int = 2) -> tuple[np.ndarray,
     return left, np.clip(right, 0, 255).astype(np.uint8)
 
 
+def _stream_part(args):
+    h, w, ts, base_seed = args
+    return [stereo_pair(h, w, t, base_seed) for t in ts]
+
+
+def stream_workers() -> int:
+    """Generator processes for stereo_stream: the usable host threads, at most 16 (the GPU box's
+    CPU share; OMP_NUM_THREADS is 16 there)."""
+    import os
+    n = len(os.sched_getaffinity(0))
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return max(1, min(16, n))
+
+
+def stereo_stream(h: int, w: int, n: int, base_seed: int = 2, t_step: int = 1,
+                  workers: int | None = None) -> list[tuple[np.ndarray, np.ndarray]]:
+    """SURVEY §8d's C2 input stream: frame t (t = 0 .. n-1) = stereo_pair(h, w, t_step * t,
+    base_seed), i.e. left seed base_seed + t_step * t, disparity seed 1000 + that, noise seed
+    2000 + that. C2: base_seed 2, t_step 1, n = 512; C5 rank r: base_seed 10 + r, t_step 8 (no two
+    ranks share a frame). Generated by `workers` spawned processes (numpy only; the parent may
+    already hold the GPU, so no fork), identical to the serial loop."""
+    ts = [t_step * t for t in range(n)]
+    workers = stream_workers() if workers is None else max(1, workers)
+    if workers == 1 or n < 8:
+        return _stream_part((h, w, ts, base_seed))
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    k = max(1, -(-n // (4 * workers)))   # ~4 parts per worker
+    parts = [(h, w, ts[i:i + k], base_seed) for i in range(0, n, k)]
+    with ProcessPoolExecutor(workers, mp_context=mp.get_context("spawn")) as ex:
+        out = []
+        for p in ex.map(_stream_part, parts):
+            out.extend(p)
+    return out
+
+
 def rgbd_frame(h: int, w: int, t: int, base_seed: int = 3) -> tuple[np.ndarray, np.ndarray]:
     """C3 generator: gray frame shifted 0-3 px per frame + float depth (m), 5 % holes."""
     base = textured_image(h + 64, w + 64, base_seed)

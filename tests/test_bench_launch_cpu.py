@@ -23,6 +23,9 @@ STUB = textwrap.dedent("""
     print(f"rank {rank} chatter", flush=True)
     if mode == "fail" and rank == 1:
         sys.exit(3)
+    if mode == "fail_last" and rank == world - 1:
+        time.sleep(1)
+        sys.exit(5)
     if mode == "hang" and rank == 1:
         time.sleep(600)
     if rank == 0 and mode != "silent":
@@ -47,6 +50,22 @@ def test_self_launch_relays_rank0(stub, capsys):
     assert len(out) == 1, out                      # exactly one line on stdout: rank 0's JSON
     doc = json.loads(out[0])
     assert doc["n_gpus"] == 3 and doc["argv"] == ["ok", "--x"] and doc["launch"] == "self"
+
+
+def test_self_launch_8_ranks(stub, capsys):
+    """The driver's N = 8 form: eight ranks start with RANK 0..7, rank 0's line is relayed."""
+    rc = bench.self_launch(8, ["ok"], 180, script=stub)
+    out = capsys.readouterr()
+    assert rc == 0
+    assert json.loads(out.out.strip())["n_gpus"] == 8
+    assert all(f"rank {r} chatter" in out.err for r in range(8))
+
+
+def test_self_launch_8_ranks_last_fails(stub, capsys):
+    """One failing rank among eight (the last, after rank 0 has printed its line): the launcher exits
+    non-zero and relays no line."""
+    assert bench.self_launch(8, ["fail_last"], 180, script=stub) != 0
+    assert capsys.readouterr().out.strip() == ""
 
 
 def test_self_launch_rank_failure_is_nonzero(stub, capsys):

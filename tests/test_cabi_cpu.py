@@ -43,7 +43,7 @@ def test_pipeline_argument_errors_without_gpu():
     lib = amd.lib()
     einval = lib.orbx_pipeline_create(None, 3, None)
     assert einval != 0
-    p = amd.OrbxParams(2000, 1.2, 8, 20, 7, 0)
+    p = amd.OrbxParams(ctypes.sizeof(amd.OrbxParams), 2000, 1.2, 8, 20, 7, 0)
     out = ctypes.c_void_p()
     assert lib.orbx_pipeline_create(ctypes.byref(p), 17, ctypes.byref(out)) == einval and not out.value
     assert lib.orbx_pipeline_stereo_batch(None, None, 1, 1241, 376, 1241, 1241 * 376, 386.1448, 0.537, None) == einval
@@ -52,6 +52,19 @@ def test_pipeline_argument_errors_without_gpu():
     assert lib.orbx_pipeline_chunk(None, 0, None, None, None) == einval
     assert lib.orbx_pipeline_engines(None) == 0
     assert lib.orbx_extract_batch_device_phase(None, None, 2, 1241, 376, 1241, 1241 * 376, None, 1) == einval
+
+
+def test_params_struct_size_checked_without_gpu():
+    """orbx_create / orbx_pipeline_create refuse an orbx_params whose struct_size is not this header's
+    sizeof (a caller built against another layout) before touching the device."""
+    import orbslam2_amd as amd
+    lib = amd.lib()
+    out = ctypes.c_void_p()
+    for size in (0, ctypes.sizeof(amd.OrbxParams) - 4, ctypes.sizeof(amd.OrbxParams) + 4):
+        p = amd.OrbxParams(size, 2000, 1.2, 8, 20, 7, 0, 0)
+        assert lib.orbx_create(ctypes.byref(p), ctypes.byref(out)) == amd.ORBX_EINVAL and not out.value
+        assert lib.orbx_pipeline_create(ctypes.byref(p), 3, ctypes.byref(out)) == amd.ORBX_EINVAL and not out.value
+    assert ctypes.sizeof(amd.OrbxParams) == 32
 
 
 def test_build_id_matches_sources():

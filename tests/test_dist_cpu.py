@@ -1,6 +1,6 @@
-"""World-size-2 gloo run of the multi-GPU plumbing used by bench.py (CPU, no GPU):
-shared-state broadcast from rank 0, map-snapshot broadcast (C5), sequence sharding,
-max / sum over ranks."""
+"""gloo runs of the multi-GPU plumbing used by bench.py (CPU, no GPU) at world size 2 and at the
+8 ranks of the driver's C5 run (one per GPU of a node): shared-state broadcast from rank 0,
+map-snapshot broadcast (C5), sequence sharding, max / sum over ranks."""
 import os
 import socket
 
@@ -25,7 +25,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     state = [2000, 1.2, 8, 20, 7, 386.1448, 718.856] if rank == 0 else [0] * 7
     got = odist.broadcast_shared(state, "cpu", dist)
-    mine = list(odist.shard(8, world, rank))
+    mine = list(odist.shard(8, world, rank))   # C5: 8 sequences over the ranks
     mx = odist.max_over_ranks(float(rank + 1), "cpu", dist)
     tot = odist.sum_over_ranks(float(len(mine)), "cpu", dist)
     from orbslam2_amd import synth
@@ -36,7 +36,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 8])
 def test_gloo_world2(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

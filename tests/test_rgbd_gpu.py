@@ -108,16 +108,23 @@ def test_search_init_variants(amd, oracle_mod, window, nnratio, check_ori, gap):
         assert gxy[:n1].tobytes() == prev_out.tobytes()
 
 
-def test_c3_production_shape(amd, oracle_mod):
-    """C3 at bench.py's production shape: batches of 256 TUM RGB-D frames,
-    consecutive batches alternating over 3 engines on their own streams with no synchronisation
-    between them (bench_rgbd), each batch = extract(1000) + UndistortKeyPoints + ComputeStereoFromRGBD
-    + SearchForInitialization over its 255 consecutive pairs. Four batches (engine 0 reused while
-    engines 1 and 2 are in flight), batch b from the 8-frame pool shifted by 3b: every frame's
-    keysUn / mvuRight / mvDepth and every pair's vnMatches12 / vbPrevMatched / count bit-exact.
+@pytest.mark.parametrize("flush", [False, True], ids=["resident", "flush_at_allocation_end"])
+def test_c3_production_shape(amd, oracle_mod, flush):
+    """C3 at bench.py's production shape (shapes.C3_BATCH frames per batch, shapes.C3_ENGINES
+    engines -- the constants bench.py's defaults read): consecutive batches
+    alternating over the engines on their own streams with no synchronisation between them
+    (bench_rgbd), each batch = extract(1000) + UndistortKeyPoints + ComputeStereoFromRGBD +
+    SearchForInitialization over its 255 consecutive pairs. E + 1 batches (engine 0 reused while the
+    others are in flight), batch b from the 8-frame pool shifted by 3b: every frame's keysUn /
+    mvuRight / mvDepth and every pair's vnMatches12 / vbPrevMatched / count bit-exact. `flush`: each
+    batch's gray images and depth maps end on the last byte of their own fresh 2 MiB-multiple
+    allocation (256 VGA images are 75 MiB: the gray batch starts 1 MiB into a 76 MiB allocation).
     Reference: Frame.cc:725-776, 1131-1169; ORBmatcher.cc:580-748."""
     import torch
-    T, E, NB = 256, 3, 4
+    from orbslam2_amd import shapes
+    T, E = shapes.C3_BATCH, shapes.C3_ENGINES
+    NB = E + 1
+    assert (T, E) == (256, 4)
     pool = [synth.rgbd_frame(480, 640, t) for t in range(8)]
     ref = [_oracle_frame(oracle_mod, g, d, K_TUM, D_TUM) for g, d in pool]
     bounds = oracle_mod.image_bounds(640, 480, K_TUM, D_TUM)
@@ -129,25 +136,37 @@ def test_c3_production_shape(amd, oracle_mod):
         prev = np.stack([ku1["x"], ku1["y"]], 1)
         pair_ref[a] = oracle_mod.search_for_initialization(oracle_mod.Grid(ku1, d1, bounds),
                                                            oracle_mod.Grid(ku2, d2, bounds), prev, 100, 0.9, True)
+    def flush_copy(a):   # a device copy of `a` ending on the last byte of a 2 MiB-multiple allocation
+        raw = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        alloc = -(-raw.size // (2 << 20)) * (2 << 20)
+        buf = torch.empty(alloc, dtype=torch.uint8, device="cuda")
+        buf[alloc - raw.size:].copy_(torch.from_numpy(raw))
+        return buf, buf.data_ptr() + alloc - raw.size
+
+    torch.cuda.empty_cache()
     ins = []
     for bi in range(NB):
         idx = [(t + 3 * bi) % 8 for t in range(T)]
-        g = torch.from_numpy(np.stack([pool[i][0] for i in idx])).cuda()
-        d = torch.from_numpy(np.stack([pool[i][1] for i in idx])).cuda()
-        ins.append((idx, g, d))
+        gs, ds = np.stack([pool[i][0] for i in idx]), np.stack([pool[i][1] for i in idx])
+        if flush:
+            (gb, gp), (db, dp) = flush_copy(gs), flush_copy(ds)
+        else:
+            gb, db = torch.from_numpy(gs).cuda(), torch.from_numpy(ds).cuda()
+            gp, dp = gb.data_ptr(), db.data_ptr()
+        ins.append((idx, gb, db, gp, dp))
     exs = [amd.BatchExtractor(1000) for _ in range(E)]
     for ex in exs:
         ex.reserve(640, 480, T)
     torch.cuda.synchronize()
     for bi in range(NB):   # bench_rgbd's step, back to back
-        _, g, d = ins[bi]
+        _, _, _, gp, dp = ins[bi]
         ex = exs[bi % E]
-        ex.extract_device(g.data_ptr(), T, 640, 480, 640, 640 * 480)
-        ex.rgbd_device(d.data_ptr(), 640 * 480, 640, K_TUM, D_TUM, BF_TUM)
+        ex.extract_device(gp, T, 640, 480, 640, 640 * 480)
+        ex.rgbd_device(dp, 640 * 480, 640, K_TUM, D_TUM, BF_TUM)
         ex.search_init_device(T - 1, 0, 1, 1, 1, K_TUM, D_TUM, 100, 0.9, True)
     amd.device_sync()
-    for bi in range(1, NB):   # batch 0's engine was reused by batch 3
-        idx, _, _ = ins[bi]
+    for bi in range(1, NB):   # batch 0's engine was reused by batch E
+        idx = ins[bi][0]
         ex = exs[bi % E]
         for t in range(T):
             k, _, ku, u, dep = ref[idx[t]]
