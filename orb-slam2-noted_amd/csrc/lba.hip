@@ -966,6 +966,11 @@ __host__ __device__ constexpr size_t chol_tiled_lds(int n) {
                              2 * (size_t)chol_tiled_dim(n));
 }
 
+#ifndef LBA_SOLVE_ONEWAVE
+#define LBA_SOLVE_ONEWAVE 0   // 1: the back substitution on one wavefront, no barriers -- measured slower
+                              // (24k against 9.2k cycles, chol 35.5 against 30.0 us per trial:
+                              // profiles/r05_ab_lba_solve.log; the 16 readlane pairs per block serialise)
+#endif
 #ifndef LBA_CHOL_THREADS
 #define LBA_CHOL_THREADS 1024   // 512: 87k cycles per 120 x 120 solve, 1024: 84k (faster load phase)
 #endif
@@ -1110,6 +1115,60 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
 #endif
     // back substitution L^T x = y, y = row n of the factor, zero past n: the padded rows of
     // the last block then contribute exactly 0 and every block runs fixed 16-term sums
+#if LBA_SOLVE_ONEWAVE
+    // one wavefront, no workgroup barrier: block K's x_K = L_KK^-T y_K as 4-term partial dots
+    // reduced across lanes, x_K broadcast through SGPRs (readlane), then lane j updates
+    // y_j, y_{j+64} (j < k0) from the 16 L[k0 + k][j] of its rows -- y lives in the lanes'
+    // registers and in LDS (the x_K step reads y_K from there), ordered by wavefront LDS fences
+    if (wv != 0) return;
+    {
+        double y0 = lane < n ? A[n * LDA + lane] : 0.0, y1 = lane + 64 < n ? A[n * LDA + lane + 64] : 0.0;
+        yv[lane] = y0;
+        if (lane + 64 < N2) yv[lane + 64] = y1;
+        auto lds_sync = [] {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        lds_sync();
+        for (int K = (n - 1) / 16; K >= 0; K--) {
+            const int k0 = 16 * K;
+            const double *LK = Linv + K * 16 * 17;
+            const int c = lane & 15, p4 = 4 * (lane >> 4);
+            double sx = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; r++) sx += LK[(p4 + r) * 17 + c] * yv[k0 + p4 + r];   // LK[r][c] = 0 for r < c
+            sx += __shfl_xor(sx, 16);
+            sx += __shfl_xor(sx, 32);
+            if (lane < 16) xv[k0 + c] = sx;
+            if (k0 == 0) break;
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const long long xb = __double_as_longlong(sx);
+                const double xk = __longlong_as_double(
+                    (long long)((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(xb >> 32), k) << 32 |
+                                (unsigned)__builtin_amdgcn_readlane((int)xb, k)));
+                if (lane < k0) s0 = __builtin_fma(A[(k0 + k) * LDA + lane], xk, s0);
+                if (lane + 64 < k0) s1 = __builtin_fma(A[(k0 + k) * LDA + lane + 64], xk, s1);
+            }
+            y0 -= s0;
+            y1 -= s1;
+            if (lane < k0) yv[lane] = y0;
+            if (lane + 64 < k0) yv[lane + 64] = y1;
+            lds_sync();
+        }
+        lds_sync();
+        for (int j = lane; j < n; j += 64) g.x[j] = xv[j];
+        if (lane == 0) g.scalars[4] = 1;
+    }
+#ifdef LBA_PROFILE
+    if (lane == 0)
+        printf("LBAPROF n=%d load=%lld diag=%lld trsm=%lld trail=%lld solve=%lld\n", n, t_load, t_diag, t_trsm, t_trail,
+               clock64() - ts);
+#endif
+    return;
+#endif
     for (int j = tid; j < N2; j += kCT) yv[j] = j < n ? A[n * LDA + j] : 0.0;
     __syncthreads();
     // Each block step as 4-term partial dot products reduced across lanes (a 16-term dependent

@@ -25,6 +25,11 @@ static __constant__ int c_umax[16];
 // IC_Angle byte weights per (|v|, dword w) of the row segment u = 4w-16 .. 4w-13:
 // x = (u + 16) where |u| <= umax[|v|] else 0, y = 1 / 0 mask (built from umax on the host)
 static __constant__ uint2 c_icw[16 * 8];
+// describe2_kernel's steered-BRIEF patch loads (lanes 0..59: row lane / 10 + 6 k, dword lane % 10 of
+// the 40-byte aligned row window): bit 7 p + k of lane l = the dword can hold a pixel some rotation of
+// the pattern samples when the window starts p = 0..3 bytes before the patch (built on the host from
+// bit_pattern_31_'s radius, orbx_create); the others are not loaded (DESC_CLIP)
+static __constant__ uint32_t c_pmask[64];
 
 #define HIPCHK(x)                                                                   \
     do {                                                                            \
@@ -1788,6 +1793,9 @@ __device__ __forceinline__ int write_lane(int v, int r, int old) {
 // the patch as two 16-byte loads per lane (three lanes per 48-byte row, LDS rows of 12 dwords):
 // 3 vector-memory instructions per slot instead of 11 (the texture pipeline, TA / TD, is ~88 %
 // busy under describe2 with dword loads: tools/pmc_mem.sh)
+#ifndef ORBX_DESC_CLIP
+#define ORBX_DESC_CLIP 1   // describe2: load only the patch / IC_Angle dwords a keypoint can read
+#endif
 template <int NS, int G, int NB, int PRE, bool WIDE>
 __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
                                                         const uint8_t *blur, const uint32_t *sel, const int *sel_cnt,
@@ -1888,13 +1896,15 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
         } else {
             const int vo = vr * pr + 4 * w8;
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (k < 3 || vr <= 6) P[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 8 * k * pr, 0);
+            for (int k = 0; k < 4; k++)   // a dword with no pixel inside the umax circle has weight 0
+                if ((k < 3 || vr <= 6) && (!ORBX_DESC_CLIP || wt[k].y != 0u))
+                    P[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 8 * k * pr, 0);
         }
     }
     // steered-BRIEF patch of slot r (rows y-18 .. y+18, bytes x-18 .. x+21 as 10 aligned dwords
     // per row; lanes 0..59 -> (row lane / 10, dword lane % 10), six rows per pass) into registers
     const int rr0 = (lane * 205) >> 11, q10 = lane - 10 * rr0;
+    const uint32_t pmask = ORBX_DESC_CLIP && !WIDE ? c_pmask[lane] : ~0u;
     constexpr int TK = WIDE ? 8 : 7;   // patch registers per slot and lane
     uint32_t T[NB][G][TK];   // NB groups' patches in flight (prefetch distance NB)
     auto issue_patch = [&](int gi, uint32_t (&dst)[G][TK]) {
@@ -1920,10 +1930,12 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
                 }
             } else {
                 const int vo = rr0 * bwr + 4 * q10;
+                const uint32_t pm = pmask >> (7 * __builtin_amdgcn_readlane(psh, r));
                 if (lane < 60) {
 #pragma unroll
                     for (int k = 0; k < 7; k++)
-                        if (k < 6 || rr0 == 0) dst[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 6 * k * bwr, 0);
+                        if ((k < 6 || rr0 == 0) && ((pm >> k) & 1u))
+                            dst[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 6 * k * bwr, 0);
                 }
             }
         }
@@ -2481,7 +2493,29 @@ int orbx_create(const orbx_params *p, orbx_engine **out) {
             icw[av * 8 + w] = make_uint2(wu, wm);
         }
     }
+    // describe2's patch-load mask (c_pmask): row dy = r - 18 of the 37-row patch holds sampled pixels
+    // only at |dx| <= floor(sqrt(R^2 - (|dy| - 1/2)^2) + 1/2), R = the pattern's largest radius
+    // (cvRound moves a rotated point by <= 1/2 per axis; 1e-3 covers the float rotation's error)
+    uint32_t pmask[64] = {};
+    {
+        double R2 = 0;
+        for (int k = 0; k < 512; k++)
+            R2 = std::max(R2, (double)e->pattern[2 * k] * e->pattern[2 * k] + (double)e->pattern[2 * k + 1] * e->pattern[2 * k + 1]);
+        R2 = (std::sqrt(R2) + 1e-3) * (std::sqrt(R2) + 1e-3);
+        for (int l = 0; l < 60; l++) {
+            const int rr0 = l / 10, q = l % 10;
+            for (int k = 0; k < 7; k++) {
+                const int r = rr0 + 6 * k;
+                if (r > 36) continue;
+                const double ay = std::max(0.0, std::abs(r - 18) - 0.5);
+                const int w = ay * ay >= R2 ? -1 : std::min(18, (int)std::floor(std::sqrt(R2 - ay * ay) + 0.5));
+                for (int p = 0; p < 4; p++)   // bytes 18 - w + p .. 18 + w + p of the window
+                    if (w >= 0 && q >= (18 - w + p) / 4 && q <= (18 + w + p) / 4) pmask[l] |= 1u << (7 * p + k);
+            }
+        }
+    }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), e->pattern, 1024) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_pmask), pmask, sizeof(pmask)) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(c_umax), e->umax, sizeof(e->umax)) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(c_icw), icw, sizeof(icw)) != hipSuccess) {
         (void)hipEventDestroy(e->done);

@@ -2,7 +2,7 @@
 the box, launched by bench.py itself: `bench.py --gpus 2` without WORLD_SIZE starts
 torch.distributed.run with two ranks as a child process and relays rank 0's line,
 over gloo (ORBSLAM_DIST_BACKEND=gloo: ranks share the card, RCCL needs one GPU per rank). Each rank runs
-its own C2 stream (SURVEY §8d C5 seeds: rank r = seed 10 + r), receives the LocalBA map from rank 0
+its own 512-frame C2 stream (SURVEY §8d C5 seeds: rank r's frame t = seed 10 + r + 8 t), receives the LocalBA map from rank 0
 by broadcast, and checks with --check-parity its whole last 384-pair batch bit-exact and its
 LocalBA on the broadcast map within 1e-4 (same LM iterations, same erase set) against the oracle.
 The multi-rank timing is a rehearsal, not a measurement (two ranks share one GPU)."""
@@ -39,9 +39,9 @@ def test_c5_two_ranks_parity():
     assert [d["rank"] for d in cfg["rank_devices"]] == [0, 1], cfg
     c2 = line["parity_check"]["c2"]
     assert [p["rank"] for p in c2] == [0, 1]
-    assert [p["left_seed_first_pair"] for p in c2] == [10, 11]
-    for p in c2:
-        assert p["pairs_checked"] == 384 and p["pairs_bit_exact"] == 384, p
+    for r, p in enumerate(c2):   # rank r's stream: frame t from seed 10 + r + 8 t
+        assert p["left_seed_first_pair"] == 10 + r + 8 * p["first_frame"], p
+        assert p["pairs_checked"] == 384 and p["pairs_bit_exact"] == 384 and p["distinct_pairs"] == 384, p
     lba = line["localba"]["parity_check"]
     assert len(lba) == 2 and lba[0]["map_bytes"] == lba[1]["map_bytes"] > 0
     for p in lba:

@@ -1,7 +1,8 @@
 """Same-box A/B of the C2 leg (tools/build_ab.sh): for each library given, alternating, (1) every
 extraction / stereo kernel's duration with one engine and nothing else on the GPU (128 pairs, the
-engine profiler's hipEvents) and (2) the pipelined C2 leg's stereo frames/s (3 engines x 128 pairs,
-bench.py's own timing). Each measurement runs in a fresh process with ORBSLAM_AMD_LIB set.
+engine profiler's hipEvents) and (2) the pipelined C2 leg's stereo frames/s (3 engines x 128 pairs
+over bench.py's 512-frame stream, bench.py's own timing). Each measurement runs in a fresh process
+with ORBSLAM_AMD_LIB set; the stream is generated once (cached in $TMPDIR).
   python tools/ab_c2.py <lib_a.so> <lib_b.so> [rounds]"""
 import json
 import os
@@ -19,10 +20,10 @@ import bench   # sets GPU_MAX_HW_QUEUES before the runtime starts, as bench.py d
 import torch
 torch.cuda.init()
 import orbslam2_amd as amd
-from orbslam2_amd import synth
-pool = [synth.stereo_pair(376, 1241, t) for t in range(8)]
+st = np.load("STREAM", mmap_mode="r")   # [512][2][376][1241]
+pool = [(st[t, 0], st[t, 1]) for t in range(len(st))]
 B = 128
-imgs = np.stack([im for i in range(B) for im in pool[i % 8]])
+imgs = np.ascontiguousarray(st[:B]).reshape(2 * B, 376, 1241)
 d = torch.from_numpy(imgs).cuda()
 torch.cuda.synchronize()
 mb = float(np.float32(386.1448) / np.float32(718.856))
@@ -39,17 +40,29 @@ iso = {k: round(v[0] / 5, 4) for k, v in pl.profile_read().items()}
 pl.close()
 class A: pass
 args = A(); args.batch = 384; args.engines = 3; args.warmup = 3; args.steps = 30; args.blur_mode = 0
-bufs = bench.c2_buffers(384, 4, pool)
+buf = bench.c2_stream_buffer(pool)
 params = (2000, 1.2, 8, 20, 7, 386.1448, mb)
-el, _, ex = bench.time_c2(amd, args, None, params, bufs, 0, args.steps)
+el, _, ex = bench.time_c2(amd, args, None, params, buf, 0, args.steps)
 ex.close()
 print(json.dumps({"iso_ms": iso, "iso_total_ms": round(sum(iso.values()), 4), "c2": round(384 * 30 / el, 1)}))
 '''.replace("ROOT", str(ROOT))
 
 
+STREAM = Path(os.environ.get("TMPDIR", "/tmp")) / "ab_c2_stream.npy"
+
+
+def stream_file():
+    if not STREAM.exists():
+        sys.path.insert(0, str(ROOT / "orb-slam2-noted_amd" / "python"))
+        import numpy as np
+        from orbslam2_amd import synth
+        np.save(STREAM, np.stack([np.stack(p) for p in synth.stereo_stream(376, 1241, 512)]))
+    return STREAM
+
+
 def run(lib):
     env = dict(os.environ, ORBSLAM_AMD_LIB=str(Path(lib).resolve()))
-    r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+    r = subprocess.run([sys.executable, "-c", CHILD.replace("STREAM", str(stream_file()))], env=env, capture_output=True, text=True, timeout=300)
     if r.returncode:
         raise SystemExit(r.stderr[-2000:])
     return json.loads(r.stdout.strip().splitlines()[-1])
