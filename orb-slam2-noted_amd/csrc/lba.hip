@@ -975,10 +975,31 @@ __host__ __device__ constexpr size_t chol_tiled_lds(int n) {
 #define LBA_CHOL_THREADS 1024   // 512: 87k cycles per 120 x 120 solve, 1024: 84k (faster load phase)
 #endif
 constexpr int kCT = LBA_CHOL_THREADS, kCW = kCT / 64;   // threads, waves of lba_chol_tiled
-__global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
+#ifndef LBA_FUSE_FINISH
+#define LBA_FUSE_FINISH 1   // lba_schur_finish and lba_chol_tiled in one launch (lba_finish_chol)
+#endif
+#ifndef LBA_SPIN_LIMIT
+#define LBA_SPIN_LIMIT (1u << 24)   // bounded hand-off wait: ~1 s of polls, then the trial fails
+#endif
+// HANDOFF: the Schur matrix Hs comes from the finish blocks of the same launch (lba_finish_chol):
+// they store it write-through (sc1) and add to g.arrive[0] after their stores have drained; thread
+// 0 polls that counter with sc1 loads, the workgroup barrier orders every wave's loads after the
+// match, and every load of Hs is an sc1 load (MI355X_MICROARCH.md, hand-off table row 1)
+template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g, int nfb) {
     extern __shared__ double A[];   // N2 x LDA, then Linv[NT][16][17], y[N2], x[N2]
     __shared__ int fail;
     if (g.lm->done) return;
+    if constexpr (HANDOFF) {
+        if (threadIdx.x == 0) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(g.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nfb) {
+                if (++spins >= LBA_SPIN_LIMIT) { g.arrive[1] = 1u; break; }   // timeout word; the trial fails
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __hip_atomic_store(g.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
+        }
+        __syncthreads();
+    }
     const int n = 6 * g.P, N2 = chol_tiled_dim(n), NT = N2 / 16, LDA = N2 + 1;
     double *Linv = A + N2 * LDA, *yv = Linv + NT * 16 * 17, *xv = yv + N2;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -991,7 +1012,15 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
     const long long NP = g.NP;
     // element (r, c <= r) of the system [Hs bs; bs^T 0] padded with identity rows
     auto sys = [&](int r, int c) -> double {
-        if (r < n) return g.Hs[r * NP + c];
+        if (r < n) {
+            if constexpr (HANDOFF) {
+                const unsigned long long b = __hip_atomic_load((const unsigned long long *)(g.Hs + r * NP + c), __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);   // sc1
+                return __longlong_as_double((long long)b);
+            } else {
+                return g.Hs[r * NP + c];
+            }
+        }
         if (r == n) return c < n ? g.bs[c] : 0.0;
         return r == c ? 1.0 : 0.0;
     };
@@ -1200,12 +1229,61 @@ __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) {
         __syncthreads();
     }
     for (int j = tid; j < n; j += kCT) g.x[j] = xv[j];
-    if (tid == 0) g.scalars[4] = 1;
+    if (tid == 0) g.scalars[4] = HANDOFF && g.arrive[1] != 0u ? 0 : 1;
 #ifdef LBA_PROFILE
     if (tid == 0)
         printf("LBAPROF n=%d load=%lld diag=%lld trsm=%lld trail=%lld solve=%lld\n", n, t_load, t_diag, t_trsm, t_trail,
                clock64() - ts);
 #endif
+}
+
+__global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) { chol_tiled_body<false>(g, 0); }
+
+// lba_schur_finish + lba_chol_tiled in one launch (one kernel boundary fewer per LM trial): blocks
+// 0 .. nfb - 1 are finish blocks, four tile pairs each (one 4-wave quad per pair, lba_schur_finish's
+// work), storing Hs write-through (sc1); after every wave's stores have drained and a workgroup
+// barrier, one lane adds 1 to g.arrive[0]. Block nfb is the Cholesky (chol_tiled_body<true>), which
+// waits for nfb arrivals. Every block is resident at once (nfb + 1 <= 10 blocks on 256 CUs), so the
+// wait cannot block a producer.
+__global__ __launch_bounds__(kCT) void lba_finish_chol(Graph g, int nfb) {
+    if ((int)blockIdx.x == nfb) {
+        chol_tiled_body<true>(g, nfb);
+        return;
+    }
+    if (g.lm->done) return;   // the Cholesky block reads the same flag and does not wait
+    const int lane = threadIdx.x & 63, q = (threadIdx.x >> 6) & 3, p = 4 * (int)blockIdx.x + (int)(threadIdx.x >> 8);
+    if (p < g.npairs) {
+        const int2 ij = g.tp_ij[p], nc = g.tp_nch[p];   // (I, J); first chunk, chunk count
+        const int I = ij.x, J = ij.y, n6 = 6 * g.P;
+        const long long NP = g.NP;
+        const double lambda = g.lm->lambda;
+        double v = 0;
+        const double *tp = g.tp_part + 256LL * nc.x + 64 * q + lane;
+        for (int c0 = 0; c0 < nc.y; c0 += 32) {
+            double t[32];
+#pragma unroll
+            for (int u = 0; u < 32; u++) t[u] = c0 + u < nc.y ? tp[256LL * (c0 + u)] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 32; u++)
+                if (c0 + u < nc.y) v += t[u];
+        }
+        // C/D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * q
+        const int row = 16 * I + (lane >> 4) + 4 * q, col = 16 * J + (lane & 15);
+        if (row < n6 && col < n6) {
+            double h = 0;
+            if (row / 6 == col / 6) h = g.Hpp[36 * (row / 6) + 6 * (row % 6) + (col % 6)];
+            if (row == col) h += lambda;
+            h -= v;
+            const unsigned long long hb = (unsigned long long)__double_as_longlong(h);
+            __hip_atomic_store((unsigned long long *)(g.Hs + row * NP + col), hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (I != J)
+                __hip_atomic_store((unsigned long long *)(g.Hs + (long long)col * NP + row), hb, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(g.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // n6 > kSmallNP: blocked right-looking Cholesky in place on Hs (lower triangle), panel
@@ -1825,6 +1903,12 @@ struct LmPhase {
             // (pose, upper component))
             lba_schur_tiles<<<g.nchunks + (n6 + 3) / 4 + (21 * A.P + 3) / 4, 256, 0, s>>>(g);
             lprof_end(e, ph, "lba_schur_tiles");
+            if (LBA_FUSE_FINISH && n6 <= kSmallNP) {
+                ph = lprof_begin(e);
+                const int nfb = (g.npairs + 3) / 4;
+                lba_finish_chol<<<nfb + 1, kCT, chol_tiled_lds(n6), s>>>(g, nfb);
+                lprof_end(e, ph, "lba_finish_chol");
+            } else {
             ph = lprof_begin(e);
             lba_schur_finish<<<g.npairs, 256, 0, s>>>(g);
             lprof_end(e, ph, "lba_schur_finish");
@@ -1844,6 +1928,7 @@ struct LmPhase {
                 }
                 lba_chol_solve_blocked<<<1, 1024, sizeof(double) * n6, s>>>(g);
                 lprof_end(e, ph, "lba_chol_blocked");
+            }
             }
         } else {
             lba_set_ok<<<1, 1, 0, s>>>(g);

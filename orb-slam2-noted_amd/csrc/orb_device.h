@@ -35,6 +35,18 @@ __device__ __forceinline__ unsigned xcd_linear() {
     const unsigned q = nwg / 8, r = nwg % 8, xcd = orig % 8;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
+// Chunked form: the linear ids are cut into runs of 8 M workgroups; inside a run XCD k (which the
+// hardware gives ids k, k + 8, ...) takes M consecutive logical ids. Neighbouring workgroups share an
+// L2 while the chip as a whole still sweeps the grid in order (addresses stay close together).
+template <int M> __device__ __forceinline__ void xcd_remap2_chunk(int &bx, int &by) {
+    const unsigned nwg = gridDim.x * gridDim.y;
+    const unsigned orig = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned c = orig / (8u * M), r = orig - c * (8u * M);
+    unsigned w = c * (8u * M) + (r % 8u) * M + r / 8u;
+    if (c * (8u * M) + 8u * M > nwg) w = orig;   // the last partial run keeps the hardware order
+    bx = (int)(w % gridDim.x);
+    by = (int)(w / gridDim.x);
+}
 __device__ __forceinline__ void xcd_remap2(int &bx, int &by) {
     const unsigned w = xcd_linear();
     bx = (int)(w % gridDim.x);

@@ -61,7 +61,8 @@ struct ExtractGeom {
     int lw[ORBX_MAXL], lh[ORBX_MAXL];
     long long pyr_off[ORBX_MAXL];   // level >= 1 offset inside an image's pyramid block
     long long blur_off[ORBX_MAXL];  // offset inside an image's blurred block (all levels)
-    int bp[ORBX_MAXL];              // blurred / strength-map row pitch (lw rounded up to 16)
+    int bp[ORBX_MAXL];              // pyramid row pitch of levels >= 1 (lw rounded up to 16)
+    int bbp[ORBX_MAXL];             // blurred-level row pitch (lw rounded up to ORBX_BLUR_ALIGN)
     long long pyr_stride, blur_stride;
     int in_pitch;
     long long in_stride;

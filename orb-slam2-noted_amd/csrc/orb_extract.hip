@@ -117,6 +117,16 @@ __device__ __forceinline__ uint32_t resize_px_simd(int S0, int S1, int4 ry) {  /
 #ifndef RZ_TH
 #define RZ_TH 32    // output rows per tile
 #endif
+#ifndef ORBX_RZ_XCD
+#define ORBX_RZ_XCD 64  // > 0: XCD-aware block runs of this length in resize_level_kernel: its reads
+                        // 98 -> 53 MB per launch (~1 GB less per C2 step), C2 +0.25 % same box
+                        // (profiles/r05_traffic_xcd.log)
+#endif
+#ifndef ORBX_FB_XCD
+#define ORBX_FB_XCD 0   // > 0: the same for fast_blur_kernel -- its reads fall 1104 -> 405 MB per launch
+                        // (runs of 64) but the kernel runs 0.79 -> 0.94 ms alone and C2 loses 11 %
+                        // (runs of 16: 503 MB, 0.87 ms, -5 %): off
+#endif
 #ifndef RZ_HJ
 #define RZ_HJ 6     // source rows per thread per load batch
 #endif
@@ -130,8 +140,16 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
     return;
 #endif
     const int dw = g.lw[l], dh = g.lh[l];
-    const int b = blockIdx.y;   // streaming: the XCD remap measured no gain here
+#if ORBX_RZ_XCD
+    // XCD-aware order: each XCD takes runs of ORBX_RZ_XCD consecutive (image, tile) blocks, so tiles
+    // that share source rows and columns read them through one L2
+    int bxr, b;
+    xcd_remap2_chunk<ORBX_RZ_XCD>(bxr, b);
+    const int ty = bxr / tiles_x, tx = bxr - ty * tiles_x;
+#else
+    const int b = blockIdx.y;
     const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+#endif
     const int x0 = tx * RZ_TW, y0 = ty * RZ_TH, y1 = min(y0 + RZ_TH, dh);
     const int sr0 = ryt[y0].x, nsr = ryt[y1 - 1].y - sr0 + 1;
     int sp;
@@ -325,6 +343,9 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 // ------------------------------------------------------------------------------------
 #ifndef ORBX_BOUNDS_CHECK
 #define ORBX_BOUNDS_CHECK 0
+#endif
+#ifndef ORBX_BLUR_ALIGN
+#define ORBX_BLUR_ALIGN 128   // blurred-level row alignment in bytes (16: the pyramid's)
 #endif
 #define FB_TW 128
 #define FB_TH 16
@@ -549,8 +570,16 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     __shared__ uint16_t hlist[FB_TW * FB_TH];   // hot tile pixels (score-tile byte offsets; each at most once)
     __shared__ int ncand_sh, hcnt_sh;   // ncand_sh: brighter count | darker count << 16
     lat_prio<16>();
-    const int b = blockIdx.y;   // tiles read their own halo once: the XCD remap measured slower here
+#if ORBX_FB_XCD
+    // XCD-aware order: an XCD works runs of ORBX_FB_XCD consecutive tiles, so the halo rows and the
+    // 4-byte side columns a tile shares with its neighbours come from its own L2
+    int t, b;
+    xcd_remap2_chunk<ORBX_FB_XCD>(t, b);
+    int l = 0;
+#else
+    const int b = blockIdx.y;
     int t = blockIdx.x, l = 0;
+#endif
     while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
     t -= g.blur_tile_base[l];
     // t / blur_tiles_x by the rounded-up reciprocal (exact while t * blur_tiles_x < 2^31): scalar
@@ -738,7 +767,7 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
         // column blocks per wavefront balance the pre-filter's extra work: wavefront 2 scores
         // the ring rows (one more 8-pixel group per lane), wavefront 3 the ring columns
         const int xb0 = wv == 0 ? 0 : wv == 1 ? 3 : 6, xb1 = wv == 0 ? 3 : wv == 1 ? 6 : wv == 2 ? 6 : 8;
-        fast_blur_mfma<BM32>(tin, blur + (long long)b * g.blur_stride + g.blur_off[l], g.bp[l], x0, y0, w, h, xb0, xb1, lane);
+        fast_blur_mfma<BM32>(tin, blur + (long long)b * g.blur_stride + g.blur_off[l], g.bbp[l], x0, y0, w, h, xb0, xb1, lane);
     }
 #endif
     __syncthreads();
@@ -1570,7 +1599,7 @@ __device__ __forceinline__ void desc_slots(const ExtractGeom &g, const uint8_t *
     const int obk = g.out_base[kk + 1];
     const uint8_t *imgk = kk == 0 ? in + (long long)b * g.in_stride : pyr + (long long)b * g.pyr_stride + g.pyr_off[kk];
     const long long blurk = (long long)b * g.blur_stride + g.blur_off[kk];
-    const int pitchk = kk == 0 ? g.in_pitch : g.bp[kk], bwk = g.bp[kk], spk = g.scaled_patch[kk];
+    const int pitchk = kk == 0 ? g.in_pitch : g.bp[kk], bwk = g.bbp[kk], spk = g.scaled_patch[kk];
     const float sck = g.scale[kk];
     int inc = scl;
     inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xF, 0xF, false);   // row_shr:1
@@ -1864,7 +1893,7 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     // level's last, so a byte past its width is the next row's). Loads that add a row step in
     // soffset are covered by that argument, not by the range check.
     const int icn = (int)((long long)(l == 0 ? g.in_pitch : g.bp[l]) * (g.lh[l] - (ky - 15) - 1) + g.lw[l] - (kx - 16));
-    const int bw = g.bp[l];
+    const int bw = g.bbp[l];
     const long long c0 = (long long)b * g.blur_stride + g.blur_off[l] + (long long)(ky - 18) * bw + (kx - 18);
     const int psh = (int)(c0 & 3);
     const long long a0 = c0 - psh;
@@ -2195,8 +2224,11 @@ int engine_reserve(orbx_engine *e, int W, int H, int max_images) {
             g.pyr_off[l] = l == 0 ? 0 : pyr;
             g.bp[l] = (g.lw[l] + 15) & ~15;
             if (l > 0) pyr += ((long long)g.bp[l] * g.lh[l] + 63) & ~63LL;
+            // blurred levels: rows on ORBX_BLUR_ALIGN (128) bytes, so fast_blur_kernel's 128-column tile
+            // rows are whole 128-B lines, each written by one workgroup (no partial-line write-backs)
+            g.bbp[l] = (g.lw[l] + ORBX_BLUR_ALIGN - 1) & ~(ORBX_BLUR_ALIGN - 1);
             g.blur_off[l] = blur;
-            blur += ((long long)g.bp[l] * g.lh[l] + 63) & ~63LL;
+            blur += ((long long)g.bbp[l] * g.lh[l] + 127) & ~127LL;
             g.scale[l] = e->scale[l];
             g.inv_scale[l] = e->inv_scale[l];
             g.scaled_patch[l] = (int)(31 * e->scale[l]);
@@ -2740,7 +2772,7 @@ int orbx_blurred_level(orbx_engine *e, int image, int level, uint8_t *dst, int *
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamWaitEvent(e->stream, e->done, 0));
     HIPCHK(hipMemcpy2DAsync(dst, lw, e->d_blur.as<uint8_t>() + image * e->g.blur_stride + e->g.blur_off[level],
-                            e->g.bp[level], lw, lh, hipMemcpyDeviceToHost, e->stream));
+                            e->g.bbp[level], lw, lh, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return ORBX_OK;
 }
