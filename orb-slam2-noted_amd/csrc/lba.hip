@@ -873,7 +873,14 @@ template <int C> __device__ __forceinline__ double row_bcast(double v) {
 #ifndef LBA_DPP_VOLATILE
 #define LBA_DPP_VOLATILE 0
 #endif
+#ifndef LBA_GATE_VOLATILE
+#define LBA_GATE_VOLATILE 1
+#endif
+#if LBA_GATE_VOLATILE
 __device__ __forceinline__ void dpp_gate(double &v) { asm volatile("s_nop 1" : "+v"(v)); }
+#else
+__device__ __forceinline__ void dpp_gate(double &v) { asm("s_nop 1" : "+v"(v)); }
+#endif
 template <int C, bool NOP> __device__ __forceinline__ void fmac_bcast(double &acc, double src, double m) {
 #if LBA_DPP_VOLATILE
     if constexpr (NOP)
@@ -952,6 +959,14 @@ template <int J, bool FULL> __device__ __forceinline__ void chol16_factor(double
     }
 }
 
+#ifndef LBA_DIAG_PIPE
+#define LBA_DIAG_PIPE 1   // the diagonal tile by chol16_pipe (lba_chol16.inc, tools/gen_chol16.py): pivot J's
+                          // non-critical updates issued between the dependent steps of pivot J + 1's chain
+#endif
+#if LBA_DIAG_PIPE
+#include "lba_chol16.inc"
+#endif
+
 // The trial poses T_t = exp(x_p) T of the free poses (VertexSE3Expmap::oplusImpl) of a window
 // beyond lba_chol_tiled's, formed at the end of the blocked solve into the trial estimate buffer
 // (lba_lin_points<true> forms a small window's itself). Tc: the current pose of free pose t.
@@ -966,6 +981,37 @@ __host__ __device__ constexpr size_t chol_tiled_lds(int n) {
                              2 * (size_t)chol_tiled_dim(n));
 }
 
+// the sum of x over the 4 lanes of a quad, (l0 + l1) + (l2 + l3) in every lane, by DPP quad_perm
+template <int CTL> __device__ __forceinline__ double dpp_perm64(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)b, CTL, 0xF, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(b >> 32), CTL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double quad_sum(double x) {
+    x += dpp_perm64<0xB1>(x);          // quad_perm [1, 0, 3, 2]: lane ^ 1
+    return x + dpp_perm64<0x4E>(x);    // quad_perm [2, 3, 0, 1]: lane ^ 2
+}
+// the sum of x over the four 16-lane rows, in every lane: two swap steps on the VALU
+// (v_permlane16_swap: odd rows of the first operand <-> even rows of the second; v_permlane32_swap:
+// the upper half <-> the lower half), each lane adding its pair in the same order, so every row
+// holds the same bits (r0 + r1) + (r2 + r3)
+__device__ __forceinline__ double rows4_sum(double x) {
+    auto step = [](double v, bool half) -> double {
+        const unsigned lo = (unsigned)__double_as_longlong(v), hi = (unsigned)(__double_as_longlong(v) >> 32);
+        const auto a = half ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false) : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto b = half ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false) : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        const double u = __longlong_as_double((long long)(((unsigned long long)b[0] << 32) | a[0]));
+        const double w = __longlong_as_double((long long)(((unsigned long long)b[1] << 32) | a[1]));
+        return u + w;
+    };
+    return step(step(x, false), true);
+}
+#ifndef LBA_SOLVE_LA
+#define LBA_SOLVE_LA 1   // the back substitution with one barrier per block (wave 0 updates the next block itself):
+                         // 8.2k against 8.5k cycles (profiles/r05_lbaprof_diag_pipe_solve_la.txt); a left-looking
+                         // form on wave 0 alone (each x_K from all later x in LDS) measured 12.1-13.4k
+#endif
 #ifndef LBA_SOLVE_ONEWAVE
 #define LBA_SOLVE_ONEWAVE 0   // 1: the back substitution on one wavefront, no barriers -- measured slower
                               // (24k against 9.2k cycles, chol 35.5 against 30.0 us per trial:
@@ -1010,37 +1056,81 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
 #define LBA_T(acc) do {} while (0)
 #endif
     const long long NP = g.NP;
-    // element (r, c <= r) of the system [Hs bs; bs^T 0] padded with identity rows
-    auto sys = [&](int r, int c) -> double {
-        if (r < n) {
-            if constexpr (HANDOFF) {
-                const unsigned long long b = __hip_atomic_load((const unsigned long long *)(g.Hs + r * NP + c), __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);   // sc1
-                return __longlong_as_double((long long)b);
-            } else {
-                return g.Hs[r * NP + c];
-            }
-        }
-        if (r == n) return c < n ? g.bs[c] : 0.0;
-        return r == c ? 1.0 : 0.0;
+    // element (r, c <= r) of the system [Hs bs; bs^T 0] padded with identity rows, branch-free: Hs and
+    // bs through buffer descriptors over exactly their n rows / n entries, every other offset past
+    // the descriptor's end (the hardware returns 0), so all of a lane's loads stay in flight together
+    // (with a branch per case the compiler waited vmcnt(0) before each load: a round trip per element).
+    // HANDOFF: the Hs loads carry sc1 (aux 16), the hand-off's load form (MI355X_MICROARCH.md, row 1)
+    const auto hs_rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)g.Hs, 0, (int)(n * NP * 8), 0x00020000);
+    const auto bs_rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)g.bs, 0, n * 8, 0x00020000);
+    constexpr int kOOR = 0x40000000;   // an offset past both descriptors
+    // sys_ld issues the two loads of element (r, c) -- zero unless `ok` -- and sys_val sums them once
+    // they are needed (at most one term is nonzero), so a caller issues all of its loads first
+    auto sys_ld = [&](int r, int c, bool ok, double &h, double &b) {
+        h = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(hs_rsrc, ok && r < n ? (r * (int)NP + c) * 8 : kOOR, 0,
+                                                                            HANDOFF ? 16 : 0));
+        b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(bs_rsrc, ok && r == n ? c * 8 : kOOR, 0, 0));
     };
+    auto sys_val = [&](int r, int c, bool ok, double h, double b) -> double { return h + b + (ok && r > n && r == c ? 1.0 : 0.0); };
     if (tid == 0) fail = 0;
-    // wave 0: factor + invert diagonal tile K (lane i of each 16-lane row = row i); tile 0 comes
-    // straight from global memory while waves 1.. load the rest of the matrix into LDS
+#ifdef LBA_PROFILE
+    __shared__ long long prof_d[2];
+#endif
+    // wave 0: factor + invert diagonal tile K (lane i of each 16-lane row = row i); wave 0 loads tile
+    // 0 itself while waves 1.. load the rest of the matrix into LDS
     auto diag = [&](int K) {
         if (LBA_DIAG_PRIO) __builtin_amdgcn_s_setprio(LBA_DIAG_PRIO);
         const int k0 = 16 * K, i = lane & 15;
         double *LK = Linv + K * 16 * 17;
         double row[16], li[16];   // li: column i of L_kk^-1
         if (K == 0) {
+            // tile 0 through LDS: each load covers 4 rows x 16 columns (a row per 16-lane row), 4 loads
+            // per lane (row i per lane straight from global memory was 16 loads of 16 lines each, and
+            // the hand-off's sc1 loads all miss L2: 7.6k cycles against 4.5k for the rest of the matrix)
+            double hb[4][2];
+            const int cc = lane & 15;
 #pragma unroll
-            for (int c = 0; c < 16; c++) row[c] = c <= i ? sys(i, c) : 0.0;
-        } else {
+            for (int q = 0; q < 4; q++) {
+                const int r = (lane >> 4) + 4 * q;
+                sys_ld(r, cc, cc <= r, hb[q][0], hb[q][1]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = (lane >> 4) + 4 * q;
+                if (cc <= r) A[r * LDA + cc] = sys_val(r, cc, true, hb[q][0], hb[q][1]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // this wave's LDS stores before its reads
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        {
 #pragma unroll
             for (int c = 0; c < 16; c++) row[c] = A[(k0 + i) * LDA + k0 + c];   // the upper part (never written:
             // any bits) only ever meets lane i's own columns > i, which no broadcast reads
         }
-#ifdef LBA_DIAG_FULL   // tried: a second instantiation for the full tiles made the kernel 5 us slower
+#ifdef LBA_PROFILE
+        long long pa = 0, pb = 0;
+        if (K == 0) {
+#pragma unroll
+            for (int c = 0; c < 16; c++) asm volatile("" : "+v"(row[c]));
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            pa = clock64();
+        }
+#endif
+#if LBA_DIAG_PIPE
+#pragma unroll
+        for (int r = 0; r < 16; r++) li[r] = r == i ? 1.0 : 0.0;
+        bool bad = false;
+        chol16_pipe(row, li, n - k0, bad);
+#ifdef LBA_PROFILE
+        if (K == 0) {
+#pragma unroll
+            for (int c = 0; c < 16; c++) asm volatile("" : "+v"(row[c]), "+v"(li[c]));
+            pb = clock64();
+            if (lane == 0) { prof_d[0] = pa - t0; prof_d[1] = pb - pa; }
+        }
+#endif
+#elif defined(LBA_DIAG_FULL)   // tried: a second instantiation for the full tiles made the kernel 5 us slower
         const bool full = n - k0 >= 16;   // wave-uniform
 #pragma unroll
         for (int r = 0; r < 16; r++) li[r] = full && r == i ? 1.0 : 0.0;
@@ -1063,29 +1153,39 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
         if (lane == 0 && bad) fail = 1;
         if (LBA_DIAG_PRIO) __builtin_amdgcn_s_setprio(0);
     };
+#ifdef LBA_PROFILE
+    __shared__ long long prof_w[2];
+#endif
     if (wv == 0) {
         diag(0);
+#ifdef LBA_PROFILE
+        if (lane == 0) prof_w[0] = clock64() - t0;
+#endif
     } else {   // waves 1..: the lower triangle of rows 16.. (N2 <= kSmallNP = 128), all loads in flight
         constexpr int RU = (128 - 16 + kCW - 2) / (kCW - 1);
-        double v[RU][2];
+        double v[RU][2][2];
 #pragma unroll
         for (int u = 0; u < RU; u++)
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int r = 16 + wv - 1 + (kCW - 1) * u, c = lane + 64 * h;
-                v[u][h] = r < N2 && c <= r ? sys(r, c) : 0.0;
+                sys_ld(r, c, r < N2 && c <= r, v[u][h][0], v[u][h][1]);
             }
 #pragma unroll
         for (int u = 0; u < RU; u++)
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int r = 16 + wv - 1 + (kCW - 1) * u, c = lane + 64 * h;
-                if (r < N2 && c <= r) A[r * LDA + c] = v[u][h];
+                if (r < N2 && c <= r) A[r * LDA + c] = sys_val(r, c, true, v[u][h][0], v[u][h][1]);
             }
+#ifdef LBA_PROFILE
+        if (tid == 64) prof_w[1] = clock64() - t0;
+#endif
     }
     __syncthreads();
 #ifdef LBA_PROFILE
-    const long long t_load = 0;   // the load overlaps diag(0): both in "diag"
+    const long long t_load = prof_w[0] * 1000000LL + prof_w[1];   // wave 0's diag(0) | wave 1's load, cycles
+    if (tid == 0) printf("LBAPROF0 loads %lld factor %lld w0 %lld w1 %lld\n", prof_d[0], prof_d[1], prof_w[0], prof_w[1]);
     ta = t0;
 #endif
     LBA_T(t_diag);
@@ -1204,30 +1304,59 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
     // FMA chain per step before): x_K by wave 0, lane (column c, quarter p) over rows 4p..4p+3;
     // the rows above by 4 lanes each
     static_assert(kCT / 4 >= kSmallNP, "one pass of row quads");
+    // x_K = L_KK^-T y_K on wave 0 (y_K final in yv); the quarter sums added (r0 + r1) + (r2 + r3)
+    auto x_block = [&](int K) {
+        const int k0 = 16 * K;
+        const double *LK = Linv + K * 16 * 17;
+        const int c = lane & 15, p4 = 4 * (lane >> 4);
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) s += LK[(p4 + r) * 17 + c] * yv[k0 + p4 + r];   // LK[r][c] = 0 for r < c
+        s = rows4_sum(s);
+        if (lane < 16) xv[k0 + c] = s;
+    };
+    // y_j -= L_K^T x_K for row j, by the 4 lanes of a quad (k = 4p .. 4p + 3 each, summed (p0 + p1) + (p2 + p3))
+    auto y_update = [&](int k0, int j, int q4) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) s += A[(k0 + q4 + k) * LDA + j] * xv[k0 + q4 + k];
+        s = quad_sum(s);
+        if ((lane & 3) == 0) yv[j] -= s;
+    };
+#if LBA_SOLVE_LA
+    // One barrier per block: with x_K published, wave 0 updates block K - 1's rows itself and forms
+    // x_{K-1} at once (its own LDS accesses are ordered), while waves 1.. update the rows above
+    // block K - 1; the barrier then publishes x_{K-1} and those rows. The same sums in the same
+    // order as the two-barrier form (LBA_SOLVE_LA=0), so the solution is bit-identical.
+    {
+        int K = (n - 1) / 16;
+        if (wv == 0) x_block(K);
+        __syncthreads();
+        for (; K > 0; K--) {
+            const int k0 = 16 * K, kp = k0 - 16;
+            if (wv == 0) {
+                y_update(k0, kp + (lane >> 2), 4 * (lane & 3));
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // block K - 1's y before x_block reads it
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                x_block(K - 1);
+            } else {
+                const int j = (tid - 64) >> 2;
+                if (j < kp) y_update(k0, j, 4 * (tid & 3));   // a row's 4 lanes are a quad: all in or all out
+            }
+            __syncthreads();
+        }
+    }
+#else
     for (int K = (n - 1) / 16; K >= 0; K--) {
         const int k0 = 16 * K;
-        if (wv == 0) {   // x_K = L_KK^-T y_K
-            const double *LK = Linv + K * 16 * 17;
-            const int c = lane & 15, p4 = 4 * (lane >> 4);
-            double s = 0.0;
-#pragma unroll
-            for (int r = 0; r < 4; r++) s += LK[(p4 + r) * 17 + c] * yv[k0 + p4 + r];   // LK[r][c] = 0 for r < c
-            s += __shfl_xor(s, 16);
-            s += __shfl_xor(s, 32);
-            if (lane < 16) xv[k0 + c] = s;
-        }
+        if (wv == 0) x_block(K);
         __syncthreads();
-        const int j = tid >> 2, q4 = 4 * (tid & 3);
-        if (j < k0) {   // a row's 4 lanes are a quad: all in or all out
-            double s = 0.0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) s += A[(k0 + q4 + k) * LDA + j] * xv[k0 + q4 + k];
-            s += __shfl_xor(s, 1);
-            s += __shfl_xor(s, 2);
-            if ((tid & 3) == 0) yv[j] -= s;
-        }
+        const int j = tid >> 2;
+        if (j < k0) y_update(k0, j, 4 * (tid & 3));   // a row's 4 lanes are a quad: all in or all out
         __syncthreads();
     }
+#endif
     for (int j = tid; j < n; j += kCT) g.x[j] = xv[j];
     if (tid == 0) g.scalars[4] = HANDOFF && g.arrive[1] != 0u ? 0 : 1;
 #ifdef LBA_PROFILE
