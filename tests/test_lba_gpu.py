@@ -20,9 +20,11 @@ def _rel(a, b):
 
 # 6P <= 128 runs the single-workgroup LDS Cholesky; 22 / 40 / 64 free KFs (6P = 132, 240,
 # 384) run the blocked Cholesky with the MFMA trailing update (ORB-SLAM2's covisibility
-# window is not bounded by 21 keyframes).
+# window is not bounded by 21 keyframes). 8 and 16 free KFs (6P = 48, 96) put the appended
+# right-hand-side row first in its 16-row tile (the diagonal tile's pivot limit is 0).
 @pytest.mark.parametrize("seed,n_kf,n_pts", [(4, 20, 3000), (5, 10, 800), (6, 20, 1500), (9, 21, 1500),
-                                             (10, 22, 2000), (11, 40, 4000), (12, 64, 6000)])
+                                             (10, 22, 2000), (11, 40, 4000), (12, 64, 6000),
+                                             (13, 16, 1500), (14, 8, 600)])
 def test_lba_matches_oracle(amd, oracle_mod, seed, n_kf, n_pts):
     prob = synth.localba_problem(seed=seed, n_kf=n_kf, n_points=n_pts)
     ref = oracle_mod.lba_solve(prob)
