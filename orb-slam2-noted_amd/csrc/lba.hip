@@ -184,17 +184,35 @@ __device__ inline void huber(const EdgeDev &e, double chi, double &rho0, double 
     else { const double s = sqrt(chi); rho0 = 2 * s * e.delta - e.dsqr; rho1 = e.delta / s; }
 }
 
-// block sum of one double per thread into *dst (also returned, to every thread)
+#ifndef LBA_BLOCK_SUM_1B
+#define LBA_BLOCK_SUM_1B 1   // block sums / maxima in one barrier (wave 0 folds), not eight
+#endif
+// block sum of one double per thread (threads < 256) into *dst; the sum is returned to thread 0.
+// The tree is the 8-step LDS fold's (t += t + s for s = 128 .. 1, the same additions in the same
+// order, so the same bits) in one barrier: wave 0 adds (v_t + v_t+128) + (v_t+64 + v_t+192) and
+// folds the rest across its lanes
 __device__ inline double block_sum_to(double v, double *dst) {
     __shared__ double sh[256];
     if (threadIdx.x < 256) sh[threadIdx.x] = v;   // (lba_lin_points' trial-pose wave holds 0)
     __syncthreads();
+#if LBA_BLOCK_SUM_1B
+    double a = 0;
+    if (threadIdx.x < 64) {
+        const int t = threadIdx.x;
+        a = (sh[t] + sh[t + 128]) + (sh[t + 64] + sh[t + 192]);
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) a += __shfl_down(a, s);   // lane 0: the tree's additions
+        if (t == 0) *dst = a;
+    }
+    return a;
+#else
     for (int s = 128; s > 0; s >>= 1) {
         if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
         __syncthreads();
     }
     if (threadIdx.x == 0) *dst = sh[0];
     return sh[0];
+#endif
 }
 
 // ---- linearize: errors + robust chi2 + per-edge quadratic-form pieces
@@ -537,11 +555,21 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused
     hv_s[threadIdx.x] = v;
     sh[threadIdx.x] = dmax;
     __syncthreads();
+#if LBA_BLOCK_SUM_1B
+    if (threadIdx.x < 64) {   // a maximum: any order gives the same bits
+        const int t = threadIdx.x;
+        double m = fmax(fmax(sh[t], sh[t + 64]), fmax(sh[t + 128], sh[t + 192]));
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) m = fmax(m, __shfl_xor(m, s));
+        if (t == 0) g.partial[kRedBlocks + blockIdx.x] = m;
+    }
+#else
     for (int s = 128; s > 0; s >>= 1) {
         if ((int)threadIdx.x < s) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
         __syncthreads();
     }
     if (threadIdx.x == 0) g.partial[kRedBlocks + blockIdx.x] = sh[0];
+#endif
     if (!fused) return;   // uniform
     }
     if (l >= g.Lm) return;
