@@ -184,6 +184,9 @@ __device__ inline void huber(const EdgeDev &e, double chi, double &rho0, double 
     else { const double s = sqrt(chi); rho0 = 2 * s * e.delta - e.dsqr; rho1 = e.delta / s; }
 }
 
+#ifndef LBA_JAC_RCP
+#define LBA_JAC_RCP 1   // the linearisation's Jacobians by products with 1 / z (one FP64 division per record)
+#endif
 #ifndef LBA_BLOCK_SUM_1B
 #define LBA_BLOCK_SUM_1B 1   // block sums / maxima in one barrier (wave 0 folds), not eight
 #endif
@@ -253,6 +256,20 @@ __device__ __forceinline__ double linearize_slot_at(const Graph &g, const EdgeDe
     quat_to_R(T.q, R);
     const double x = p[0], y = p[1], z = p[2], z2 = z * z, fx = e.fx, fy = e.fy, bf = e.bf;
     double Jt[18];
+#if LBA_JAC_RCP
+    // g2o's Jacobians (types_six_dof_expmap.cpp:103-139, 188-234) with one division, 1 / z, and
+    // products by it: within an ulp or two of the quotients, and ~20 FP64 division sequences fewer
+    // per record on the linearisation's dependent chain
+    const double iz = 1.0 / z, iz2 = iz * iz;
+    Jt[0] = x * y * iz2 * fx; Jt[1] = -(1 + (x * x * iz2)) * fx; Jt[2] = y * iz * fx;
+    Jt[3] = -iz * fx; Jt[4] = 0; Jt[5] = x * iz2 * fx;
+    Jt[6] = (1 + y * y * iz2) * fy; Jt[7] = -x * y * iz2 * fy; Jt[8] = -x * iz * fy;
+    Jt[9] = 0; Jt[10] = -iz * fy; Jt[11] = y * iz2 * fy;
+    if (e.stereo) {
+        Jt[12] = Jt[0] - bf * y * iz2; Jt[13] = Jt[1] + bf * x * iz2; Jt[14] = Jt[2];
+        Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf * iz2;
+    }
+#else
     Jt[0] = x * y / z2 * fx; Jt[1] = -(1 + (x * x / z2)) * fx; Jt[2] = y / z * fx;
     Jt[3] = -1. / z * fx; Jt[4] = 0; Jt[5] = x / z2 * fx;
     Jt[6] = (1 + y * y / z2) * fy; Jt[7] = -x * y / z2 * fy; Jt[8] = -x / z * fy;
@@ -261,6 +278,7 @@ __device__ __forceinline__ double linearize_slot_at(const Graph &g, const EdgeDe
         Jt[12] = Jt[0] - bf * y / z2; Jt[13] = Jt[1] + bf * x / z2; Jt[14] = Jt[2];
         Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf / z2;
     }
+#endif
     const int D = e.stereo ? 3 : 2;
     const double wW = r1 * e.info;
     double omr[3];
@@ -284,6 +302,20 @@ __device__ __forceinline__ double linearize_slot_at(const Graph &g, const EdgeDe
     }
     if (role == 1) return 0.0;
     double Jp[9];
+#if LBA_JAC_RCP
+    if (!e.stereo) {
+        const double tmp[6] = {fx, 0, -x * iz * fx, 0, fy, -y * iz * fy};
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++)
+                Jp[3 * i + j] = (-iz * tmp[3 * i]) * R[j] + (-iz * tmp[3 * i + 1]) * R[3 + j] + (-iz * tmp[3 * i + 2]) * R[6 + j];
+    } else {
+        for (int j = 0; j < 3; j++) {
+            Jp[j] = -fx * R[j] * iz + fx * x * R[6 + j] * iz2;
+            Jp[3 + j] = -fy * R[3 + j] * iz + fy * y * R[6 + j] * iz2;
+            Jp[6 + j] = Jp[j] - bf * R[6 + j] * iz2;
+        }
+    }
+#else
     if (!e.stereo) {
         const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
         for (int i = 0; i < 2; i++)
@@ -297,6 +329,7 @@ __device__ __forceinline__ double linearize_slot_at(const Graph &g, const EdgeDe
             Jp[6 + j] = Jp[j] - bf * R[6 + j] / z2;
         }
     }
+#endif
     int u = 0;
 #pragma unroll
     for (int a = 0; a < 3; a++)
