@@ -82,3 +82,17 @@ def test_host_structure_invariants(tmp_path):
                    capture_output=True, timeout=300)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("ok 8"), r.stdout + r.stderr
+
+
+def test_chol16_include_is_generated():
+    """csrc/lba_chol16.inc (the software-pipelined diagonal-tile Cholesky, lba.hip LBA_DIAG_PIPE) is the
+    output of tools/gen_chol16.py: a hand edit of either would drift from the other."""
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "gen_chol16.py")], capture_output=True, text=True,
+                         check=True).stdout
+    inc = (ROOT / "orb-slam2-noted_amd" / "csrc" / "lba_chol16.inc").read_text()
+    assert out.rstrip("\n") == inc.rstrip("\n")
+    # every instruction of the pipelined tile is an ordered (volatile) statement; the column
+    # updates: 120 of L and 120 of its inverse
+    assert inc.count("v_fmac_f64_dpp") == 240 and inc.count("v_rsq_f64") == 16
