@@ -663,10 +663,21 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
  * raised the moment trial `trial` (1-based; 0 = before the first iteration) of optimize() call
  * `phase` (1 = optimize(5), 2 = optimize(10)) has completed, and stayed raised. phase 0 removes
  * the hook. The CPU oracle has the same hook (lba_oracle_solve_hook), so a stop at any (phase,
- * trial) is parity-tested deterministically. phase 3: a live raise at a deterministic point -- the
- * call itself writes 1 into the caller's `stop` flag once it has read back its trial-th chunk of LM
- * trials (trial >= 1; no effect when `stop` is NULL), as another thread setting mbAbortBA would. */
+ * trial) is parity-tested deterministically. phase 3: a live raise at a deterministic point -- once
+ * the call has read back its trial-th chunk of LM trials (trial >= 1; no effect when `stop` is NULL),
+ * the flag the device sees reads as raised for the rest of the call, through the same mirrored word
+ * as another thread setting mbAbortBA would (the caller's flag itself is never written). */
 int lba_set_stop_hook(lba_engine *e, int phase, int trial);
+/* Test options (no reference counterpart; the defaults are the product's):
+ *   LBA_OPT_FUSE_FINISH  1 (default): the Schur finish and the Cholesky of a window of <= 21 free
+ *                        poses in one launch with an in-launch hand-off; 0: two launches. Both give
+ *                        bit-identical results (tests/test_lba_gpu.py).
+ *   LBA_OPT_SPIN_LIMIT   the in-launch hand-off wait's poll bound; < 0: the default (~1 s); 0: every
+ *                        wait times out (fault injection). A timed-out wait ends the optimisation and
+ *                        lba_solve returns ORBX_EDEVICE. */
+#define LBA_OPT_FUSE_FINISH 1
+#define LBA_OPT_SPIN_LIMIT 2
+int lba_set_test_option(lba_engine *e, int option, long long value);
 /* Per-kernel hipEvent timing of lba_solve's trial chain on the engine stream (bench.py localba
  * roofline); same semantics as orbx_profile / orbx_profile_read. */
 int lba_profile(lba_engine *e, int enable);

@@ -81,6 +81,8 @@ struct LMState {
     int seen;       // a terminate() check of this optimize() found pbStopFlag raised
     int gate;       // the second optimize()'s start (lba_phase2_begin): 0 run, 1 deferred (enqueued before the
                     // first optimize() had ended), 2 skipped (bDoMore false, Optimizer.cc:913-917)
+    int fault;      // a trial's in-launch hand-off timed out (Graph::arrive[1]): the optimisation ended
+                    // there and lba_solve returns ORBX_EDEVICE
 };
 
 struct EdgeDev {
@@ -135,7 +137,8 @@ struct Graph {
     const LMState *lm_src; // a deciding lba_reduce_points: the state before the decision (ping-pong)
     LMState *lm_buf[2];    // the two state buffers (host bookkeeping: lm is one of them)
     const unsigned *stopf; // pbStopFlag mirrored by lba_solve's host loop into page-locked, device-mapped memory
-    unsigned *arrive;      // lba_errors block-arrival counter (the last block runs the LM decision)
+    unsigned *arrive;      // [0]: lba_finish_chol's finish-block arrivals; [1]: its hand-off timeout (fault) word
+    unsigned spin_limit;   // the hand-off wait's poll bound (kSpinLimit; lba_set_test_option)
     int Kpad;              // Y^T rows 3 Lm rounded up to 4; row Kpad (and up to Kpad + 3) is zero
     int NP;                // Schur dimension 6P padded to a multiple of kCB
     const int2 *tp_ij;     // upper tile pairs (I, J) of the Schur matrix
@@ -184,12 +187,6 @@ __device__ inline void huber(const EdgeDev &e, double chi, double &rho0, double 
     else { const double s = sqrt(chi); rho0 = 2 * s * e.delta - e.dsqr; rho1 = e.delta / s; }
 }
 
-#ifndef LBA_JAC_RCP
-#define LBA_JAC_RCP 1   // the linearisation's Jacobians by products with 1 / z (one FP64 division per record)
-#endif
-#ifndef LBA_BLOCK_SUM_1B
-#define LBA_BLOCK_SUM_1B 1   // block sums / maxima in one barrier (wave 0 folds), not eight
-#endif
 // block sum of one double per thread (threads < 256) into *dst; the sum is returned to thread 0.
 // The tree is the 8-step LDS fold's (t += t + s for s = 128 .. 1, the same additions in the same
 // order, so the same bits) in one barrier: wave 0 adds (v_t + v_t+128) + (v_t+64 + v_t+192) and
@@ -198,7 +195,6 @@ __device__ inline double block_sum_to(double v, double *dst) {
     __shared__ double sh[256];
     if (threadIdx.x < 256) sh[threadIdx.x] = v;   // (lba_lin_points' trial-pose wave holds 0)
     __syncthreads();
-#if LBA_BLOCK_SUM_1B
     double a = 0;
     if (threadIdx.x < 64) {
         const int t = threadIdx.x;
@@ -208,14 +204,6 @@ __device__ inline double block_sum_to(double v, double *dst) {
         if (t == 0) *dst = a;
     }
     return a;
-#else
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *dst = sh[0];
-    return sh[0];
-#endif
 }
 
 // ---- linearize: errors + robust chi2 + per-edge quadratic-form pieces
@@ -254,9 +242,8 @@ __device__ __forceinline__ double linearize_slot_at(const Graph &g, const EdgeDe
     double p[3], R[9];
     pose_map(T, Xp, p);
     quat_to_R(T.q, R);
-    const double x = p[0], y = p[1], z = p[2], z2 = z * z, fx = e.fx, fy = e.fy, bf = e.bf;
+    const double x = p[0], y = p[1], z = p[2], fx = e.fx, fy = e.fy, bf = e.bf;
     double Jt[18];
-#if LBA_JAC_RCP
     // g2o's Jacobians (types_six_dof_expmap.cpp:103-139, 188-234) with one division, 1 / z, and
     // products by it: within an ulp or two of the quotients, and ~20 FP64 division sequences fewer
     // per record on the linearisation's dependent chain
@@ -269,16 +256,6 @@ __device__ __forceinline__ double linearize_slot_at(const Graph &g, const EdgeDe
         Jt[12] = Jt[0] - bf * y * iz2; Jt[13] = Jt[1] + bf * x * iz2; Jt[14] = Jt[2];
         Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf * iz2;
     }
-#else
-    Jt[0] = x * y / z2 * fx; Jt[1] = -(1 + (x * x / z2)) * fx; Jt[2] = y / z * fx;
-    Jt[3] = -1. / z * fx; Jt[4] = 0; Jt[5] = x / z2 * fx;
-    Jt[6] = (1 + y * y / z2) * fy; Jt[7] = -x * y / z2 * fy; Jt[8] = -x / z * fy;
-    Jt[9] = 0; Jt[10] = -1. / z * fy; Jt[11] = y / z2 * fy;
-    if (e.stereo) {
-        Jt[12] = Jt[0] - bf * y / z2; Jt[13] = Jt[1] + bf * x / z2; Jt[14] = Jt[2];
-        Jt[15] = Jt[3]; Jt[16] = 0; Jt[17] = Jt[5] - bf / z2;
-    }
-#endif
     const int D = e.stereo ? 3 : 2;
     const double wW = r1 * e.info;
     double omr[3];
@@ -302,7 +279,6 @@ __device__ __forceinline__ double linearize_slot_at(const Graph &g, const EdgeDe
     }
     if (role == 1) return 0.0;
     double Jp[9];
-#if LBA_JAC_RCP
     if (!e.stereo) {
         const double tmp[6] = {fx, 0, -x * iz * fx, 0, fy, -y * iz * fy};
         for (int i = 0; i < 2; i++)
@@ -315,21 +291,6 @@ __device__ __forceinline__ double linearize_slot_at(const Graph &g, const EdgeDe
             Jp[6 + j] = Jp[j] - bf * R[6 + j] * iz2;
         }
     }
-#else
-    if (!e.stereo) {
-        const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
-        for (int i = 0; i < 2; i++)
-            for (int j = 0; j < 3; j++)
-                Jp[3 * i + j] = (-1. / z * tmp[3 * i]) * R[j] + (-1. / z * tmp[3 * i + 1]) * R[3 + j] +
-                                (-1. / z * tmp[3 * i + 2]) * R[6 + j];
-    } else {
-        for (int j = 0; j < 3; j++) {
-            Jp[j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
-            Jp[3 + j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
-            Jp[6 + j] = Jp[j] - bf * R[6 + j] / z2;
-        }
-    }
-#endif
     int u = 0;
 #pragma unroll
     for (int a = 0; a < 3; a++)
@@ -375,12 +336,10 @@ __device__ __forceinline__ double linearize_slot(const Graph &g, const EdgeDev &
 //          residuals and linearisation into the trial set;
 //          computeScale pieces x (lambda x + b) -> scale_part[b]. One launch instead of two, and
 //          no grid-wide wait between the update and the residuals.
-#ifndef LBA_LIN_ROLES
-#define LBA_LIN_ROLES 1   // 1: the two linearize_slot_at roles on two waves per 8 landmarks (role 0: residual,
-                          // Hll / bl, Hpl; role 1: Hpp / bp), each redoing the landmark update. Same box:
-                          // update_errors 0.256 -> 0.232 ms per call (profiles/r04_ab_lba_roles.log)
-#endif
-constexpr int kLPL = 8, kLPB = 256 / kLPL / (LBA_LIN_ROLES ? 2 : 1);
+// The two linearize_slot_at roles run on two waves per 8 landmarks (role 0: residual, Hll / bl,
+// Hpl; role 1: Hpp / bp), each redoing the landmark update. Same box: update_errors 0.256 -> 0.232 ms
+// per call against one wave doing both (profiles/r04_ab_lba_roles.log)
+constexpr int kLPL = 8, kLPB = 256 / kLPL / 2;
 // lba_lin_points<true> workgroups carry a fifth wave that forms the trial poses T_t = exp(x_p) T
 // of a small window (6P <= kSmallNP: lba_chol_tiled's) into LDS while the other four run the
 // landmark update: the exp chain overlaps the update's loads instead of ending the solve
@@ -391,8 +350,8 @@ __global__ __launch_bounds__(UPDATE ? kLinThreads : 256) void lba_lin_points(Gra
                                                                            int nbl) {
     __shared__ Pose tps[kSmallNP / 6];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int role = LBA_LIN_ROLES ? (wv & 1) : 2;   // wave-uniform
-    const int grp = LBA_LIN_ROLES ? (wv >> 1) * (64 / kLPL) + lane / kLPL : threadIdx.x / kLPL;
+    const int role = wv & 1;   // wave-uniform
+    const int grp = (wv >> 1) * (64 / kLPL) + lane / kLPL;
     const int r = threadIdx.x % kLPL;
     const int l = blockIdx.x * kLPB + grp;
     const bool isl = (int)blockIdx.x < nbl && wv < 4 && l < g.Lm;
@@ -533,11 +492,8 @@ __device__ __forceinline__ void slot_y(const Graph &g, int l, int ph, int ppos, 
 // bl 3) of the landmark's contiguous run of landmark-major records (conl) in CSR order, 8 records
 // in flight; the |diagonal| maximum of the block's 16 landmarks -> partial[kRedBlocks + blockIdx]
 constexpr int kRPL = 16;   // landmarks per lba_reduce_points workgroup
-#ifndef LBA_FUSED_PREP
-#define LBA_FUSED_PREP 1   // 1: with lambda known (a new iteration after the first), the landmark half
-                           // of the Schur step runs here and lba_prep_slots returns at once
-#endif
-static_assert(LBA_FUSED_PREP == 1, "lba_prep_slots runs only in the first slot of an optimize()");
+// With lambda known (a new iteration after the first) the landmark half of the Schur step runs in
+// lba_reduce_points, and lba_prep_slots returns at once: it runs only in an optimize()'s first slot.
 // fused (lambda = the LM state's): after the sums, the group's lanes gather the landmark's 9
 // values through LDS, each factors (Hll + lambda I)^-1 = L L^T (point_factor_of: the bits
 // lba_prep_slots forms) and lane r writes the Y blocks of records r, r + 16, ...; lane 0 writes
@@ -588,7 +544,6 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused
     hv_s[threadIdx.x] = v;
     sh[threadIdx.x] = dmax;
     __syncthreads();
-#if LBA_BLOCK_SUM_1B
     if (threadIdx.x < 64) {   // a maximum: any order gives the same bits
         const int t = threadIdx.x;
         double m = fmax(fmax(sh[t], sh[t + 64]), fmax(sh[t + 128], sh[t + 192]));
@@ -596,13 +551,6 @@ __device__ __forceinline__ void reduce_points_body(Graph &g, int set, bool fused
         for (int s = 32; s > 0; s >>= 1) m = fmax(m, __shfl_xor(m, s));
         if (t == 0) g.partial[kRedBlocks + blockIdx.x] = m;
     }
-#else
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) g.partial[kRedBlocks + blockIdx.x] = sh[0];
-#endif
     if (!fused) return;   // uniform
     }
     if (l >= g.Lm) return;
@@ -705,7 +653,7 @@ __global__ __launch_bounds__(256) void lba_reduce_points(Graph g, int n0, int nb
         lm = *g.lm;
     }
     if (lm.done) return;
-    reduce_points_body(g, lm.cur, LBA_FUSED_PREP && lm.it > 0, !lm.newiter, lm.lambda, n0, shp);
+    reduce_points_body(g, lm.cur, lm.it > 0, !lm.newiter, lm.lambda, n0, shp);
 }
 
 // First kernel of an LM trial (setLambda + the landmark half of the Schur complement).
@@ -724,7 +672,7 @@ __global__ __launch_bounds__(256) void lba_prep_slots(Graph g, int n0, int n1, i
     const int ph = ist ? g.slot_ph[t] : -1, l_t = ist ? g.slot_pt[t] : 0, lpos = ist ? g.slot_lpos[t] : 0,
               ppos = ist ? g.slot_ppos[t] : 0;
     const LMState lm = *g.lm;
-    if (lm.done || (LBA_FUSED_PREP && lm.newiter && lm.it > 0)) return;   // lba_reduce_points did it
+    if (lm.done || (lm.newiter && lm.it > 0)) return;   // lba_reduce_points did it
     const int mode = lm.newiter ? (lm.it == 0 ? 2 : 1) : 0;
     double lambda = lm.lambda;
     if (mode == 2 || (mode == 1 && blockIdx.x == 0)) {   // uniform per block
@@ -788,10 +736,7 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 // diagonal 6 x 6 blocks and lambda on the diagonal (setLambda). Workgroups past the chunks form
 // b_schur, one wave per row: b_p - the sum of the pose's slot pieces Y_block w_l (ywp, written
 // pose-major by lba_prep_slots).
-#ifndef LBA_KSCH
-#define LBA_KSCH 64
-#endif
-constexpr int kSCH = LBA_KSCH;   // MFMA steps (4 Y^T rows each) per chunk workgroup
+constexpr int kSCH = 64;   // MFMA steps (4 Y^T rows each) per chunk workgroup
 __global__ __launch_bounds__(256) void lba_schur_tiles(Graph g) {
     if (g.lm->done) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -908,125 +853,15 @@ __global__ __launch_bounds__(256) void lba_schur_finish(Graph g) {
 // substitution L^T x = y runs block by block: x_K = L_KK^-T y_K (wave 0), then every earlier
 // row subtracts L_K^T x_K in parallel. Rows >= n are treated as unit pivots. 3 barriers per
 // panel + 2 per back-substitution block.
-// value of lane C of each 16-lane row, v_mov_b32_dpp row_newbcast (no LDS, no SGPR trip)
-template <int C> __device__ __forceinline__ double row_bcast(double v) {
-    const long long b = __double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)b, 0x150 + C, 0xF, 0xF, false);
-    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(b >> 32), 0x150 + C, 0xF, 0xF, false);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-#ifndef LBA_RSQ_NEWTON
-#define LBA_RSQ_NEWTON 1   // Newton steps after v_rsq_f64 on the pivot (the diagonal chain's latency; 2: 0.5 us per trial slower, same LM path, profiles/r04_ab_lba_rsq1.log)
-#endif
-#ifndef LBA_DIAG_PRIO
-#define LBA_DIAG_PRIO 0    // s_setprio of wave 0 while it factors a diagonal tile (critical path)
-#endif
-
-#ifndef LBA_DPP_FMAC
-#define LBA_DPP_FMAC 1   // 1: the column updates as v_fmac_f64 with a DPP64 row_newbcast source
-#endif
-// acc += (value of lane C of each 16-lane row of src) * m: the broadcast folded into the FMA
-// (v_fmac_f64_dpp, DPP64 row_newbcast). The compiler does not track hazards across inline asm:
-// every VALU write of a VGPR that a DPP then reads passes a dpp_gate (two wait states, and the
-// readers depend on it), so the asm itself can stay non-volatile and the scheduler may overlap a
-// pivot's column updates with the next pivot's chain (LBA_DPP_VOLATILE=1: the old fixed order)
-#ifndef LBA_DPP_VOLATILE
-#define LBA_DPP_VOLATILE 0
-#endif
-#ifndef LBA_GATE_VOLATILE
-#define LBA_GATE_VOLATILE 1
-#endif
-#if LBA_GATE_VOLATILE
-__device__ __forceinline__ void dpp_gate(double &v) { asm volatile("s_nop 1" : "+v"(v)); }
-#else
-__device__ __forceinline__ void dpp_gate(double &v) { asm("s_nop 1" : "+v"(v)); }
-#endif
-template <int C, bool NOP> __device__ __forceinline__ void fmac_bcast(double &acc, double src, double m) {
-#if LBA_DPP_VOLATILE
-    if constexpr (NOP)
-        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                     : "+v"(acc) : "v"(src), "v"(m), "i"(C));
-    else
-        asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(src), "v"(m), "i"(C));
-#else
-    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(src), "v"(m), "i"(C));
-#endif
-}
-template <int C> __device__ __forceinline__ double bcast64(double src) {
-    double d;
-#if LBA_DPP_VOLATILE
-    asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(d) : "v"(src), "i"(C));
-#else
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(d) : "v"(src), "i"(C));
-#endif
-    return d;
-}
-
-template <int J, int C> __device__ __forceinline__ void chol16_update(double (&row)[16], double (&li)[16], double nr, double nl) {
-    if constexpr (C < 16) {
-#if LBA_DPP_FMAC
-        fmac_bcast<C, C == J + 1>(row[C], row[J], nr);   // row[C] -= L[C][J] row[J]
-        fmac_bcast<C, false>(li[C], row[J], nl);         // li[C] -= L[C][J] li[J]
-#else
-        const double l = row_bcast<C>(row[J]);   // L[C][J]
-        row[C] = __builtin_fma(-row[J], l, row[C]);
-        li[C] = __builtin_fma(-l, li[J], li[C]);
-#endif
-        chol16_update<J, C + 1>(row, li, nr, nl);
-    }
-}
-
-// Lane i (of each 16-lane row) holds row i of the tile; column J is pivoted, scaled by the
-// reciprocal square root (v_rsq_f64 + LBA_RSQ_NEWTON Newton steps, 1 in the product: the
-// near-singular windows of tests/test_lba_gpu.py::test_lba_near_singular, pivot ratios down to
-// 2e-5, keep the oracle's LM path) and subtracted from columns > J.
-// li carries column i of L^-1 by forward substitution, fed by the same broadcasts.
-// FULL (every tile but the last, all 16 rows < n): li starts as the unit column e_i and lane
-// J's own row[J] is the pivot d, so the pivot step is two products; otherwise pivots at
-// J >= lim (rows >= n: padding and the appended right-hand side) are forced to 1, li starts at 0
-// and lane J takes the unit diagonal term at its pivot.
-template <int J, bool FULL> __device__ __forceinline__ void chol16_factor(double (&row)[16], double (&li)[16], int i, int lim,
-                                                                          bool &bad) {
-    if constexpr (J < 16) {
-#if LBA_DPP_FMAC
-#if !LBA_DPP_VOLATILE
-        dpp_gate(row[J]);   // row[J] was last written by a VALU (the pivot J - 1 update, or the load)
-#endif
-        double d = bcast64<J>(row[J]);
-#else
-        double d = row_bcast<J>(row[J]);
-#endif
-        if (!FULL && J >= lim) d = 1.0;
-        bad |= !(d > 0);
-        const double h = 0.5 * d;
-        double y = __builtin_amdgcn_rsq(d);
-        y = __builtin_fma(y, __builtin_fma(-(h * y), y, 0.5), y);
-#if LBA_RSQ_NEWTON > 1
-        y = __builtin_fma(y, __builtin_fma(-(h * y), y, 0.5), y);
-#endif
-        if constexpr (FULL) {
-            row[J] = row[J] * y;   // lane J: d * y
-            li[J] = li[J] * y;     // lane J: 1 * y
-        } else {
-            row[J] = i == J ? d * y : row[J] * y;
-            li[J] = (i == J ? 1.0 + li[J] : li[J]) * y;   // li[J] held -sum L[J][k] li[k]
-        }
-#if LBA_DPP_FMAC && !LBA_DPP_VOLATILE
-        dpp_gate(row[J]);   // the scaled row[J] is the DPP source of every column update
-#endif
-        chol16_update<J, J + 1>(row, li, -row[J], -li[J]);
-        chol16_factor<J + 1, FULL>(row, li, i, lim, bad);
-    }
-}
-
-#ifndef LBA_DIAG_PIPE
-#define LBA_DIAG_PIPE 1   // the diagonal tile by chol16_pipe (lba_chol16.inc, tools/gen_chol16.py): pivot J's
-                          // non-critical updates issued between the dependent steps of pivot J + 1's chain
-#endif
-#if LBA_DIAG_PIPE
+// The 16 x 16 diagonal tile: lane i of each 16-lane row holds row i of the tile and column i of
+// L_kk^-1; pivot J's column is broadcast by DPP64 row_newbcast, scaled by v_rsq_f64 + one Newton
+// step (the near-singular windows of tests/test_lba_gpu.py::test_lba_near_singular, pivot ratios
+// down to 2e-5, keep the oracle's LM path) and subtracted from the later columns with
+// v_fmac_f64_dpp. chol16_pipe is straight-line code generated by tools/gen_chol16.py (pivot J's
+// non-critical updates placed between the dependent steps of pivot J + 1's chain, wait states
+// written out): 3108 -> 2416 cycles a tile against the compiler-scheduled form
+// (profiles/r05_chol16_bench.txt).
 #include "lba_chol16.inc"
-#endif
 
 // The trial poses T_t = exp(x_p) T of the free poses (VertexSE3Expmap::oplusImpl) of a window
 // beyond lba_chol_tiled's, formed at the end of the blocked solve into the trial estimate buffer
@@ -1068,44 +903,42 @@ __device__ __forceinline__ double rows4_sum(double x) {
     };
     return step(step(x, false), true);
 }
-#ifndef LBA_SOLVE_LA
-#define LBA_SOLVE_LA 1   // the back substitution with one barrier per block (wave 0 updates the next block itself):
-                         // 8.2k against 8.5k cycles (profiles/r05_lbaprof_diag_pipe_solve_la.txt); a left-looking
-                         // form on wave 0 alone (each x_K from all later x in LDS) measured 12.1-13.4k
-#endif
-#ifndef LBA_SOLVE_ONEWAVE
-#define LBA_SOLVE_ONEWAVE 0   // 1: the back substitution on one wavefront, no barriers -- measured slower
-                              // (24k against 9.2k cycles, chol 35.5 against 30.0 us per trial:
-                              // profiles/r05_ab_lba_solve.log; the 16 readlane pairs per block serialise)
-#endif
-#ifndef LBA_CHOL_THREADS
-#define LBA_CHOL_THREADS 1024   // 512: 87k cycles per 120 x 120 solve, 1024: 84k (faster load phase)
-#endif
-constexpr int kCT = LBA_CHOL_THREADS, kCW = kCT / 64;   // threads, waves of lba_chol_tiled
-#ifndef LBA_FUSE_FINISH
-#define LBA_FUSE_FINISH 1   // lba_schur_finish and lba_chol_tiled in one launch (lba_finish_chol)
-#endif
-#ifndef LBA_SPIN_LIMIT
-#define LBA_SPIN_LIMIT (1u << 24)   // bounded hand-off wait: ~1 s of polls, then the trial fails
-#endif
+// 1024 threads: 84k cycles per 120 x 120 solve against 87k for 512 (faster load phase)
+constexpr int kCT = 1024, kCW = kCT / 64;   // threads, waves of lba_chol_tiled
+constexpr unsigned kSpinLimit = 1u << 24;   // bounded hand-off wait (~1 s of polls): Graph::spin_limit's default
 // HANDOFF: the Schur matrix Hs comes from the finish blocks of the same launch (lba_finish_chol):
 // they store it write-through (sc1) and add to g.arrive[0] after their stores have drained; thread
-// 0 polls that counter with sc1 loads, the workgroup barrier orders every wave's loads after the
-// match, and every load of Hs is an sc1 load (MI355X_MICROARCH.md, hand-off table row 1)
+// 0 polls that counter, the workgroup barrier orders every wave's loads after the match, and every
+// load of Hs is an sc1 load -- MI355X_MICROARCH.md's valid hand-off form that replaces the release /
+// acquire pair (an agent-scope release here writes back L2: 20.5 us per trial measured);
+// the memory clobber of the producer's `s_waitcnt vmcnt(0)` keeps the compiler from moving its
+// stores past the counter add. tests/test_lba_gpu.py::test_lba_fused_finish_bit_identical runs the
+// fused and the two-launch path (lba_set_test_option) and requires identical outputs.
+// A wait that exceeds g.spin_limit polls records a fault in g.arrive[1] and abandons the trial; the
+// next LM decision turns it into LMState::fault (done), and lba_solve returns ORBX_EDEVICE.
 template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g, int nfb) {
     extern __shared__ double A[];   // N2 x LDA, then Linv[NT][16][17], y[N2], x[N2]
-    __shared__ int fail;
+    __shared__ int fail, tmo;
     if (g.lm->done) return;
     if constexpr (HANDOFF) {
         if (threadIdx.x == 0) {
             unsigned spins = 0;
-            while (__hip_atomic_load(g.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nfb) {
-                if (++spins >= LBA_SPIN_LIMIT) { g.arrive[1] = 1u; break; }   // timeout word; the trial fails
+            int to = g.spin_limit == 0;   // 0: fault injection (lba_set_test_option), every wait times out
+            while (!to && __hip_atomic_load(g.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nfb) {
+                if (++spins >= g.spin_limit) { to = 1; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
-            __hip_atomic_store(g.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
+            if (to) {   // late finish blocks still add to arrive[0]: it is left alone (every later launch of
+                        // the call is a no-op once the fault is decided; lba_solve's setup zeroes it)
+                __hip_atomic_store(g.arrive + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                g.scalars[4] = 0;
+            } else {
+                __hip_atomic_store(g.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
+            }
+            tmo = to;
         }
         __syncthreads();
+        if (tmo) return;   // uniform
     }
     const int n = 6 * g.P, N2 = chol_tiled_dim(n), NT = N2 / 16, LDA = N2 + 1;
     double *Linv = A + N2 * LDA, *yv = Linv + NT * 16 * 17, *xv = yv + N2;
@@ -1140,7 +973,6 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
     // wave 0: factor + invert diagonal tile K (lane i of each 16-lane row = row i); wave 0 loads tile
     // 0 itself while waves 1.. load the rest of the matrix into LDS
     auto diag = [&](int K) {
-        if (LBA_DIAG_PRIO) __builtin_amdgcn_s_setprio(LBA_DIAG_PRIO);
         const int k0 = 16 * K, i = lane & 15;
         double *LK = Linv + K * 16 * 17;
         double row[16], li[16];   // li: column i of L_kk^-1
@@ -1178,7 +1010,6 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
             pa = clock64();
         }
 #endif
-#if LBA_DIAG_PIPE
 #pragma unroll
         for (int r = 0; r < 16; r++) li[r] = r == i ? 1.0 : 0.0;
         bool bad = false;
@@ -1191,19 +1022,6 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
             if (lane == 0) { prof_d[0] = pa - t0; prof_d[1] = pb - pa; }
         }
 #endif
-#elif defined(LBA_DIAG_FULL)   // tried: a second instantiation for the full tiles made the kernel 5 us slower
-        const bool full = n - k0 >= 16;   // wave-uniform
-#pragma unroll
-        for (int r = 0; r < 16; r++) li[r] = full && r == i ? 1.0 : 0.0;
-        bool bad = false;
-        if (full) chol16_factor<0, true>(row, li, i, 16, bad);
-        else chol16_factor<0, false>(row, li, i, n - k0, bad);
-#else
-#pragma unroll
-        for (int r = 0; r < 16; r++) li[r] = 0.0;
-        bool bad = false;
-        chol16_factor<0, false>(row, li, i, n - k0, bad);
-#endif
         // every 16-lane row computed the same tile: all lanes store (same values), so the
         // compiler cannot sink the li chain into a lane < 16 branch and keep every broadcast
         // live until there
@@ -1212,7 +1030,6 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
 #pragma unroll
         for (int r = 0; r < 16; r++) LK[r * 17 + i] = li[r];
         if (lane == 0 && bad) fail = 1;
-        if (LBA_DIAG_PRIO) __builtin_amdgcn_s_setprio(0);
     };
 #ifdef LBA_PROFILE
     __shared__ long long prof_w[2];
@@ -1305,60 +1122,6 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
 #endif
     // back substitution L^T x = y, y = row n of the factor, zero past n: the padded rows of
     // the last block then contribute exactly 0 and every block runs fixed 16-term sums
-#if LBA_SOLVE_ONEWAVE
-    // one wavefront, no workgroup barrier: block K's x_K = L_KK^-T y_K as 4-term partial dots
-    // reduced across lanes, x_K broadcast through SGPRs (readlane), then lane j updates
-    // y_j, y_{j+64} (j < k0) from the 16 L[k0 + k][j] of its rows -- y lives in the lanes'
-    // registers and in LDS (the x_K step reads y_K from there), ordered by wavefront LDS fences
-    if (wv != 0) return;
-    {
-        double y0 = lane < n ? A[n * LDA + lane] : 0.0, y1 = lane + 64 < n ? A[n * LDA + lane + 64] : 0.0;
-        yv[lane] = y0;
-        if (lane + 64 < N2) yv[lane + 64] = y1;
-        auto lds_sync = [] {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        };
-        lds_sync();
-        for (int K = (n - 1) / 16; K >= 0; K--) {
-            const int k0 = 16 * K;
-            const double *LK = Linv + K * 16 * 17;
-            const int c = lane & 15, p4 = 4 * (lane >> 4);
-            double sx = 0.0;
-#pragma unroll
-            for (int r = 0; r < 4; r++) sx += LK[(p4 + r) * 17 + c] * yv[k0 + p4 + r];   // LK[r][c] = 0 for r < c
-            sx += __shfl_xor(sx, 16);
-            sx += __shfl_xor(sx, 32);
-            if (lane < 16) xv[k0 + c] = sx;
-            if (k0 == 0) break;
-            double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const long long xb = __double_as_longlong(sx);
-                const double xk = __longlong_as_double(
-                    (long long)((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(xb >> 32), k) << 32 |
-                                (unsigned)__builtin_amdgcn_readlane((int)xb, k)));
-                if (lane < k0) s0 = __builtin_fma(A[(k0 + k) * LDA + lane], xk, s0);
-                if (lane + 64 < k0) s1 = __builtin_fma(A[(k0 + k) * LDA + lane + 64], xk, s1);
-            }
-            y0 -= s0;
-            y1 -= s1;
-            if (lane < k0) yv[lane] = y0;
-            if (lane + 64 < k0) yv[lane + 64] = y1;
-            lds_sync();
-        }
-        lds_sync();
-        for (int j = lane; j < n; j += 64) g.x[j] = xv[j];
-        if (lane == 0) g.scalars[4] = 1;
-    }
-#ifdef LBA_PROFILE
-    if (lane == 0)
-        printf("LBAPROF n=%d load=%lld diag=%lld trsm=%lld trail=%lld solve=%lld\n", n, t_load, t_diag, t_trsm, t_trail,
-               clock64() - ts);
-#endif
-    return;
-#endif
     for (int j = tid; j < N2; j += kCT) yv[j] = j < n ? A[n * LDA + j] : 0.0;
     __syncthreads();
     // Each block step as 4-term partial dot products reduced across lanes (a 16-term dependent
@@ -1384,11 +1147,10 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
         s = quad_sum(s);
         if ((lane & 3) == 0) yv[j] -= s;
     };
-#if LBA_SOLVE_LA
     // One barrier per block: with x_K published, wave 0 updates block K - 1's rows itself and forms
     // x_{K-1} at once (its own LDS accesses are ordered), while waves 1.. update the rows above
     // block K - 1; the barrier then publishes x_{K-1} and those rows. The same sums in the same
-    // order as the two-barrier form (LBA_SOLVE_LA=0), so the solution is bit-identical.
+    // order as a two-barrier form (x_K, barrier, rows, barrier), so the solution is bit-identical to it.
     {
         int K = (n - 1) / 16;
         if (wv == 0) x_block(K);
@@ -1408,18 +1170,8 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
             __syncthreads();
         }
     }
-#else
-    for (int K = (n - 1) / 16; K >= 0; K--) {
-        const int k0 = 16 * K;
-        if (wv == 0) x_block(K);
-        __syncthreads();
-        const int j = tid >> 2;
-        if (j < k0) y_update(k0, j, 4 * (tid & 3));   // a row's 4 lanes are a quad: all in or all out
-        __syncthreads();
-    }
-#endif
     for (int j = tid; j < n; j += kCT) g.x[j] = xv[j];
-    if (tid == 0) g.scalars[4] = HANDOFF && g.arrive[1] != 0u ? 0 : 1;
+    if (tid == 0) g.scalars[4] = 1;
 #ifdef LBA_PROFILE
     if (tid == 0)
         printf("LBAPROF n=%d load=%lld diag=%lld trsm=%lld trail=%lld solve=%lld\n", n, t_load, t_diag, t_trsm, t_trail,
@@ -1649,7 +1401,10 @@ __global__ void lba_phase2_begin(Graph g, const LMState *p1, int iterations, int
     s.iterations = iterations;
     s.newiter = 1;
     s.stop_at = stop_at;
-    if (spec && !s1.done) {
+    if (s1.fault) {
+        s.done = 1;
+        s.fault = 1;
+    } else if (spec && !s1.done) {
         s.done = 1;
         s.gate = 1;
     } else if (__hip_atomic_load(g.stopf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u || s1.trials >= s1.stop_at) {
@@ -1693,6 +1448,11 @@ __device__ inline void decide_sums(const Graph &g, int nbt, double *sums_s) {
 // accepted trial's chi2 itself -- the value g2o's activeRobustChi2() recomputes there.
 __device__ LMState lm_next(const Graph &g, LMState s, double sc_sum, double chi_sum) {
     const double *sc = g.scalars;
+    if (g.arrive[1] != 0u) {   // written by an earlier launch of this call: every workgroup reads the same
+        s.fault = 1;
+        s.done = 1;
+        return s;
+    }
     if (s.qmax == 0) {
         if (s.it == 0) s.currentChi = sc[0];
         s.iniChi = s.currentChi;
@@ -1927,6 +1687,11 @@ struct lba_engine {
     hipEvent_t ev_chunk[2] = {nullptr, nullptr};   // per optimize(): its last chunk's state readback
     int hook_phase = 0, hook_trial = 0;   // lba_set_stop_hook
     int chunks_seen = 0;                  // chunk readbacks of the current call (hook phase 3)
+    bool hook_raised = false;             // hook phase 3 fired in this call: ORed into the mirrored flag
+    // lba_set_test_option: the two-launch finish + Cholesky path instead of lba_finish_chol, and the
+    // hand-off wait's poll bound
+    bool fuse_finish = true;
+    unsigned spin_limit = kSpinLimit;
     // per-kernel hipEvent timing on the engine stream (lba_profile; bench.py localba roofline)
     bool prof = false;
     struct ProfRec { const char *name; hipEvent_t a, b; };
@@ -2011,9 +1776,6 @@ int nblk(int n) { return std::max(1, (n + 255) / 256); }
 // *stop into the mapped word the kernels load with system scope, so a flag raised mid-call ends the
 // optimisation after the trial in flight, as SparseOptimizer::terminate() does.
 // stop_at: the test hook's trial count for this optimize() (INT_MAX: none).
-#ifndef LBA_SPEC_PHASE2
-#define LBA_SPEC_PHASE2 1   // phase 2 enqueued behind phase 1's first chunk (lba_solve)
-#endif
 struct LmPhase {
     lba_engine *e;
     Graph &g;
@@ -2041,7 +1803,7 @@ struct LmPhase {
         if (nbt > kRedBlocks) rc = -2;
     }
     void mirror() {
-        if (stop) __atomic_store_n(e->h_stop, (unsigned)(*stop != 0), __ATOMIC_RELAXED);
+        if (stop) __atomic_store_n(e->h_stop, (unsigned)(*stop != 0 || e->hook_raised), __ATOMIC_RELAXED);
     }
     // the LM state ping-pongs between g.lm_buf[0 / 1] at every decision: a deciding launch reads one
     // buffer and writes the other, and every later launch reads the new one
@@ -2093,7 +1855,7 @@ struct LmPhase {
             // (pose, upper component))
             lba_schur_tiles<<<g.nchunks + (n6 + 3) / 4 + (21 * A.P + 3) / 4, 256, 0, s>>>(g);
             lprof_end(e, ph, "lba_schur_tiles");
-            if (LBA_FUSE_FINISH && n6 <= kSmallNP) {
+            if (e->fuse_finish && n6 <= kSmallNP) {
                 ph = lprof_begin(e);
                 const int nfb = (g.npairs + 3) / 4;
                 lba_finish_chol<<<nfb + 1, kCT, chol_tiled_lds(n6), s>>>(g, nfb);
@@ -2195,10 +1957,16 @@ struct LmPhase {
             }
         }
         st = *h_state;
-        // test hook (lba_set_stop_hook phase 3): the host raises the caller's flag itself once it has
-        // read back the call's hook_trial-th chunk -- a mid-call raise at a deterministic point
+        if (st.fault) {   // a hand-off wait timed out (lba_finish_chol): the results are not the oracle's
+            (void)hipStreamSynchronize(s);
+            fprintf(stderr, "orbslam2_amd lba: Schur hand-off wait timed out\n");
+            return -4;
+        }
+        // test hook (lba_set_stop_hook phase 3): once the call's hook_trial-th chunk is read back, the
+        // mirrored flag reads as raised from then on (an engine-owned flag ORed into it: the caller's
+        // const flag is never written) -- a mid-call raise at a deterministic point
         if (stop && e->hook_phase == 3 && ++e->chunks_seen == e->hook_trial) {
-            *const_cast<volatile uint8_t *>(stop) = 1;
+            e->hook_raised = true;
             mirror();
         }
         return 0;
@@ -2327,8 +2095,10 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     int cur = 0;
     *e->h_stop = 0u;
     e->chunks_seen = 0;
+    e->hook_raised = false;
     Graph g{};
     g.stopf = e->d_stop;
+    g.spin_limit = e->spin_limit;
     g.T = at<Pose>(e->arenaA, oT); g.T2 = at<Pose>(e->arenaA, oT2);
     g.X = at<double>(e->arenaA, oX); g.X2 = at<double>(e->arenaA, oX2);
     if (ne > 0)
@@ -2459,7 +2229,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     // the two optimize() calls (Optimizer.cc:900-917 and 964-966). -1 iterations = the pre-LM error
     // evaluation failed (g2o's optimize() returning -1, a valid outcome). Phase 1's LM state
     // ping-pongs in lm[0..1], phase 2's in lm[2..3]: phase 2's start and first chunk are enqueued
-    // right behind phase 1's first chunk (LBA_SPEC_PHASE2), gated on the device by
+    // right behind phase 1's first chunk, gated on the device by
     // lba_phase2_begin, so the common call (phase 1 done in its first chunk) has no host round trip
     // between the optimizations; when phase 1 needs retry slots, that enqueued chunk is a no-op and
     // phase 2 is enqueued again after them.
@@ -2524,7 +2294,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         if (p1.complete_first_chunk(5)) return ORBX_EDEVICE;
         // one phase-2 slot behind phase 1's first chunk: it keeps the GPU busy while the host reads
         // phase 1's state back; a deferred one costs its few empty launches
-        const bool spec = LBA_SPEC_PHASE2 != 0;
+        const bool spec = true;
         if (spec && phase2_start(true, 1)) return ORBX_EDEVICE;
         if (p1.wait(st1)) return ORBX_EDEVICE;
         const bool first_chunk = st1.done;   // the speculative phase-2 start finds phase 1 done
@@ -2574,6 +2344,18 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
     for (int i = 0; i < 3 * nq; i++) r->point_Xw[i] = (float)X[i];
     hp.mark("convert");
     return ORBX_OK;
+}
+
+int lba_set_test_option(lba_engine *e, int option, long long value) {
+    if (!e) return ORBX_EINVAL;
+    switch (option) {
+        case LBA_OPT_FUSE_FINISH: e->fuse_finish = value != 0; return ORBX_OK;
+        case LBA_OPT_SPIN_LIMIT:   // < 0: the default; 0: every hand-off wait times out (fault injection)
+            if (value > 0xFFFFFFFFLL) return ORBX_EINVAL;
+            e->spin_limit = value < 0 ? kSpinLimit : (unsigned)value;
+            return ORBX_OK;
+        default: return ORBX_EINVAL;
+    }
 }
 
 int lba_set_stop_hook(lba_engine *e, int phase, int trial) {

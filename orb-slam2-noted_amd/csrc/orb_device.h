@@ -146,19 +146,6 @@ __device__ __forceinline__ int wave_lane() { return (int)__lane_id(); }
 // everything derived from it (slot / cell / keypoint ids, their loads and branches) scalar
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
-// Issue priority of the latency-bound extraction kernels' waves against the VALU-bound
-// fast_blur_kernel they share the CUs with under the stereo pipeline (s_setprio: among ready
-// waves of a SIMD the higher priority issues first). ORBX_PRIO_MASK selects the kernels
-// (1 resize, 2 quadtree, 4 describe, 8 stereo_match_left, 16 fast_blur), ORBX_PRIO the level.
-#ifndef ORBX_PRIO
-#define ORBX_PRIO 0
-#endif
-#ifndef ORBX_PRIO_MASK
-#define ORBX_PRIO_MASK 0
-#endif
-template <int BIT> __device__ __forceinline__ void lat_prio() {
-    if constexpr (ORBX_PRIO > 0 && (ORBX_PRIO_MASK & BIT) != 0) __builtin_amdgcn_s_setprio(ORBX_PRIO);
-}
 
 // order LDS traffic between lanes of one wavefront (LDS executes a wave's ops in order)
 __device__ __forceinline__ void wave_lds_sync() {

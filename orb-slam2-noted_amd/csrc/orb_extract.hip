@@ -28,7 +28,7 @@ static __constant__ uint2 c_icw[16 * 8];
 // describe2_kernel's steered-BRIEF patch loads (lanes 0..59: row lane / 10 + 6 k, dword lane % 10 of
 // the 40-byte aligned row window): bit 7 p + k of lane l = the dword can hold a pixel some rotation of
 // the pattern samples when the window starts p = 0..3 bytes before the patch (built on the host from
-// bit_pattern_31_'s radius, orbx_create); the others are not loaded (DESC_CLIP)
+// bit_pattern_31_'s radius, orbx_create); the others are not loaded
 static __constant__ uint32_t c_pmask[64];
 
 #define HIPCHK(x)                                                                   \
@@ -114,42 +114,24 @@ __device__ __forceinline__ uint32_t resize_px_simd(int S0, int S1, int4 ry) {  /
 }
 
 #define RZ_TW 128   // output columns per tile (32 column groups of 4)
-#ifndef RZ_TH
-#define RZ_TH 32    // output rows per tile
-#endif
-#ifndef ORBX_RZ_XCD
-#define ORBX_RZ_XCD 64  // > 0: XCD-aware block runs of this length in resize_level_kernel: its reads
-                        // 98 -> 53 MB per launch (~1 GB less per C2 step), C2 +0.25 % same box
-                        // (profiles/r05_traffic_xcd.log)
-#endif
-#ifndef ORBX_FB_XCD
-#define ORBX_FB_XCD 0   // > 0: the same for fast_blur_kernel -- its reads fall 1104 -> 405 MB per launch
-                        // (runs of 64) but the kernel runs 0.79 -> 0.94 ms alone and C2 loses 11 %
-                        // (runs of 16: 503 MB, 0.87 ms, -5 %): off
-#endif
-#ifndef RZ_HJ
+#define RZ_TH 32    // output rows per tile (16 / 64: 3.4 / 3.0 % slower)
+// XCD-aware block runs of 64 workgroups in resize_level_kernel: its reads 98 -> 53 MB per launch
+// (~1 GB less per C2 step), C2 +0.25 % same box (profiles/r05_traffic_xcd.log). The same runs for
+// fast_blur_kernel cut its reads 1104 -> 405 MB per launch but made it 0.79 -> 0.94 ms alone and C2
+// 11 % slower: not used there.
+#define ORBX_RZ_XCD 64
 #define RZ_HJ 6     // source rows per thread per load batch
-#endif
 
 template <bool SIMD>
 __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l, int tiles_x, const int2 *cxt,
                                                            const int4 *ryt, const uint8_t *in, uint8_t *pyr) {
     extern __shared__ uint4 rz_h[];   // [source row][32 column groups] horizontal sums
-    lat_prio<1>();
-#ifdef EXP_SKIP_RESIZE   // marginal-cost experiments only (tools/skip_exp.py): levels left unwritten
-    return;
-#endif
     const int dw = g.lw[l], dh = g.lh[l];
-#if ORBX_RZ_XCD
     // XCD-aware order: each XCD takes runs of ORBX_RZ_XCD consecutive (image, tile) blocks, so tiles
     // that share source rows and columns read them through one L2
     int bxr, b;
     xcd_remap2_chunk<ORBX_RZ_XCD>(bxr, b);
     const int ty = bxr / tiles_x, tx = bxr - ty * tiles_x;
-#else
-    const int b = blockIdx.y;
-    const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
-#endif
     const int x0 = tx * RZ_TW, y0 = ty * RZ_TH, y1 = min(y0 + RZ_TH, dh);
     const int sr0 = ryt[y0].x, nsr = ryt[y1 - 1].y - sr0 + 1;
     int sp;
@@ -344,9 +326,7 @@ __global__ __launch_bounds__(256) void resize_level_kernel(ExtractGeom g, int l,
 #ifndef ORBX_BOUNDS_CHECK
 #define ORBX_BOUNDS_CHECK 0
 #endif
-#ifndef ORBX_BLUR_ALIGN
-#define ORBX_BLUR_ALIGN 128   // blurred-level row alignment in bytes (16: the pyramid's)
-#endif
+#define ORBX_BLUR_ALIGN 128   // blurred-level row alignment in bytes (16, the pyramid's: 481 -> 468 MB written, C2 -0.7 %)
 #define FB_TW 128
 #define FB_TH 16
 #define FB_SB (FB_TW + 8)   // staged bytes per tile row (cols x0-4 .. x0+131)
@@ -569,17 +549,8 @@ __global__ __launch_bounds__(256) void fast_blur_kernel(ExtractGeom g, const uin
     __shared__ uint16_t clist[FB_CCAP];   // pooled candidates (score-tile byte offsets | FB_INTILE)
     __shared__ uint16_t hlist[FB_TW * FB_TH];   // hot tile pixels (score-tile byte offsets; each at most once)
     __shared__ int ncand_sh, hcnt_sh;   // ncand_sh: brighter count | darker count << 16
-    lat_prio<16>();
-#if ORBX_FB_XCD
-    // XCD-aware order: an XCD works runs of ORBX_FB_XCD consecutive tiles, so the halo rows and the
-    // 4-byte side columns a tile shares with its neighbours come from its own L2
-    int t, b;
-    xcd_remap2_chunk<ORBX_FB_XCD>(t, b);
-    int l = 0;
-#else
     const int b = blockIdx.y;
     int t = blockIdx.x, l = 0;
-#endif
     while (l + 1 < g.nlevels && t >= g.blur_tile_base[l + 1]) l++;
     t -= g.blur_tile_base[l];
     // t / blur_tiles_x by the rounded-up reciprocal (exact while t * blur_tiles_x < 2^31): scalar
@@ -1208,7 +1179,6 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     unsigned char *qt_nodes, uint32_t *sel, int *sel_cnt) {
     extern __shared__ __align__(16) unsigned char qt_lds[];
     __shared__ QShared S;
-    lat_prio<2>();
     int l, b;
     xcd_remap2(l, b);
     const int tid = threadIdx.x;
@@ -1572,235 +1542,9 @@ __device__ __forceinline__ int wave_sum_dpp(int v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-// wave-uniform location of one output slot: level, output row, packed key
-struct DescSlot {
-    int valid, l, off;
-    uint32_t key;
-    const uint8_t *img;   // level l of image b (IC_Angle reads), row pitch `pitch`
-    long long blur0;      // offset of level l of image b in the blurred pyramid, row pitch `bw`
-    int pitch, bw;
-    float scale;
-    int spatch;
-};
-
-// The wavefront's DESC_R output slots in one round trip: lanes k < L load the per-level
-// selected counts of image b, lanes r < DESC_R the slots' keys, a DPP scan over the first row
-// gives the level prefix (the output row of slot = keypoints of the lower levels + index).
-template <int DESC_R>
-__device__ __forceinline__ void desc_slots(const ExtractGeom &g, const uint8_t *in, const uint8_t *pyr,
-                                           const uint32_t *sel, const int *sel_cnt, int *cnt, int s0, int b, int lane,
-                                           DescSlot *d) {
-    const int L = g.nlevels, cap = g.out_base[L];   // L <= ORBX_MAXL = 16: one DPP row
-    const int scl = lane < L ? sel_cnt[(long long)b * L + lane] : 0;
-    const uint32_t keyl = (lane < DESC_R && s0 + lane < cap) ? sel[(long long)b * cap + s0 + lane] : 0u;
-    // per-level geometry on lane k (vector loads issued with the two above: no dependent
-    // scalar load once the slot's level is known)
-    const int kk = min(lane, L - 1);
-    const int obk = g.out_base[kk + 1];
-    const uint8_t *imgk = kk == 0 ? in + (long long)b * g.in_stride : pyr + (long long)b * g.pyr_stride + g.pyr_off[kk];
-    const long long blurk = (long long)b * g.blur_stride + g.blur_off[kk];
-    const int pitchk = kk == 0 ? g.in_pitch : g.bp[kk], bwk = g.bbp[kk], spk = g.scaled_patch[kk];
-    const float sck = g.scale[kk];
-    int inc = scl;
-    inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xF, 0xF, false);   // row_shr:1
-    inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xF, 0xF, false);   // row_shr:2
-    inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xF, 0xF, false);   // row_shr:4
-    inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xF, 0xF, false);   // row_shr:8
-    if (s0 == 0) {
-        const int tot = __builtin_amdgcn_readlane(inc, L - 1);
-        if (lane == 0) cnt[b] = tot;
-    }
-#pragma unroll
-    for (int r = 0; r < DESC_R; r++) {
-        d[r] = DescSlot{};
-        const int slot = s0 + r;
-        if (slot >= cap) continue;
-        // level = number of levels k + 1 < L whose first slot out_base[k + 1] <= slot
-        const int l = __popcll(__ballot(lane + 1 < L && slot >= obk));
-        const int idx = slot - (l ? __builtin_amdgcn_readlane(obk, l - 1) : 0);
-        const int nl = __builtin_amdgcn_readlane(scl, l);
-        if (idx >= nl) continue;
-        d[r].valid = 1;
-        d[r].l = l;
-        d[r].off = __builtin_amdgcn_readlane(inc, l) - nl + idx;
-        d[r].key = (uint32_t)__builtin_amdgcn_readlane((int)keyl, r);
-        const unsigned long long ip = (unsigned long long)imgk;
-        d[r].img = (const uint8_t *)((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ip, l) |
-                                     (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(ip >> 32), l) << 32);
-        d[r].blur0 = (long long)((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)blurk, l) |
-                                 (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)((unsigned long long)blurk >> 32), l) << 32);
-        d[r].pitch = __builtin_amdgcn_readlane(pitchk, l);
-        d[r].bw = __builtin_amdgcn_readlane(bwk, l);
-        d[r].spatch = __builtin_amdgcn_readlane(spk, l);
-        d[r].scale = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sck), l));
-    }
-}
-
-// K5: IC_Angle (:94-141) + computeOrbDescriptor (:153-204) + keypoint assembly
-// (:1603-1657) for DESC_R consecutive output slots per wavefront (3 by default: 17.9 KB of
-// LDS per workgroup keeps eight workgroups on a CU), in three phases:
-//  1. per slot: IC_Angle moments (v_dot4 over the lane's 4 row dwords, DPP wave sums) and the
-//     37 x 40 steered-BRIEF patch of the blurred level staged into the slot's LDS buffer --
-//     all global reads of the wavefront are issued before any result is needed;
-//  2. lanes 0..DESC_R-1 evaluate fastAtan2 and glibc sincosf for their slot in one pass;
-//  3. per slot: the 256 tests from LDS (pattern coordinates pre-converted to float once per
-//     wavefront), ballot bit-packing, output rows.
-template <int DESC_R>
-__global__ __launch_bounds__(256) void describe_kernel(ExtractGeom g, const uint8_t *in,
-                                                       const uint8_t *pyr, const uint8_t *blur,
-                                                       const uint32_t *sel, const int *sel_cnt,
-                                                       orbx_kp *kps, uint8_t *desc, int *cnt) {
-    lat_prio<4>();
-    const int lane = threadIdx.x & 63, wv = wave_id();
-    int bxr, b;
-    xcd_remap2(bxr, b);
-    __shared__ uint32_t patch[4][DESC_R][372];
-    const int s0 = (bxr * 4 + wv) * DESC_R;
-    DescSlot d[DESC_R];
-    desc_slots<DESC_R>(g, in, pyr, sel, sel_cnt, cnt, s0, b, lane, d);
-    bool any = false;
-#pragma unroll
-    for (int r = 0; r < DESC_R; r++) any |= d[r].valid != 0;
-    if (!any) return;
-    // phase 1
-    int M10[DESC_R], M01[DESC_R], PSH[DESC_R];
-    const long long amax = (long long)g.nimg * g.blur_stride - 4;
-#pragma unroll
-    for (int r = 0; r < DESC_R; r++) {
-        M10[r] = M01[r] = PSH[r] = 0;
-        if (!d[r].valid) continue;
-        const int x = key_x(d[r].key) + 16, y = key_y(d[r].key) + 16;  // + minBorderX/Y (:1177-1186)
-        const uint8_t *img = d[r].img;
-        const int pitch = d[r].pitch;
-        // IC_Angle over the circular patch (|u| <= umax[|v|]): rows v = -15..15 as 8 dwords
-        // (u = -16..15), sum_u u*p = sum (u+16)*p - 16 * sum p with v_dot4_u32_u8 (exact)
-        // lane -> dword w = lane % 8 of rows v0, v0 + 8, v0 + 16, v0 + 24 (v0 = lane / 8 - 15);
-        // unaligned dword loads (the rows start anywhere)
-        const int w = lane & 7, v0 = (lane >> 3) - 15;
-        const uint8_t *rowc = img + (long long)(y + v0) * pitch + x - 16 + 4 * w;
-        int m01 = 0, m10 = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int v = v0 + 8 * k;
-            if (k < 3 || v <= 15) {
-                const uint2 wt = c_icw[(v < 0 ? -v : v) * 8 + w];
-                uint32_t P;
-                __builtin_memcpy(&P, rowc + (long long)(8 * k) * pitch, 4);
-                const int su = (int)__builtin_amdgcn_udot4(P, wt.x, 0u, false);
-                const int sm = (int)__builtin_amdgcn_udot4(P, wt.y, 0u, false);
-                m10 += su - 16 * sm;
-                m01 += v * sm;
-            }
-        }
-        M10[r] = wave_sum_dpp(m10);
-        M01[r] = wave_sum_dpp(m01);
-        // the rotated pattern stays within +-18 pixels (|rot(p)| <= 13 sqrt 2): rows y-18 ..
-        // y+18, bytes x-18 .. x+21 as 10 aligned dwords per row (the pitch is 16-aligned, so
-        // every row has the same misalignment)
-        const int bw = d[r].bw;
-        const long long c0 = d[r].blur0 + (long long)(y - 18) * bw + (x - 18);
-        const int sh = (int)(c0 & 3);
-        PSH[r] = sh;
-        const long long a0 = c0 - sh;
-        uint32_t *pt = patch[wv][r];
-        if (a0 >= 0 && a0 + 36LL * bw + 40 <= amax + 4) {   // wave-uniform: no clamping needed
-            // lanes 0..59 -> (row lane / 10, dword lane % 10), six rows per pass
-            const int bw4 = bw >> 2, rr0 = (lane * 205) >> 11, q = lane - 10 * rr0;
-            const uint32_t *src = (const uint32_t *)(blur + a0) + (long long)rr0 * bw4 + q;
-            if (lane < 60) {
-#pragma unroll
-                for (int k = 0; k < 7; k++)
-                    if (k < 6 || rr0 == 0) pt[10 * (rr0 + 6 * k) + q] = src[(long long)(6 * k) * bw4];
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 6; k++) {
-                const int idx = lane + 64 * k;
-                if (idx < 370) {
-                    const int rr = idx / 10, q = idx - rr * 10;
-                    long long ad = a0 + (long long)rr * bw + 4 * q;
-                    ad = ad < 0 ? 0 : (ad > amax ? amax & ~3LL : ad);
-                    pt[idx] = *(const uint32_t *)(blur + ad);
-                }
-            }
-        }
-    }
-    // phase 2: lane r computes slot r's angle = fastAtan2(m01, m10) and (float) cos / sin
-    float ang = 0.f, sa = 0.f, ca = 1.f;
-    if (lane < DESC_R) {
-        int m10 = M10[0], m01 = M01[0];
-#pragma unroll
-        for (int r = 1; r < DESC_R; r++) if (lane == r) { m10 = M10[r]; m01 = M01[r]; }
-        ang = fast_atan2_deg((float)m01, (float)m10);
-        const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
-        glibc_sincosf(ang * factorPI, &sa, &ca);
-    }
-    // pattern coordinates of the lane's 4 test pairs as floats (int8 -> f32, exact), the two
-    // points of a pair packed for v_pk_mul_f32 / v_pk_add_f32
-    f32x2 PX[4], PY[4];
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const uint32_t pw = ((const uint32_t *)c_pattern)[w * 64 + lane];   // x0 y0 x1 y1 as int8
-        PX[w] = f32x2{(float)(int8_t)(pw & 0xFF), (float)(int8_t)((pw >> 16) & 0xFF)};
-        PY[w] = f32x2{(float)(int8_t)((pw >> 8) & 0xFF), (float)(int8_t)(pw >> 24)};
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // phase 3
-    const int cap = g.out_base[g.nlevels];
-#pragma unroll
-    for (int r = 0; r < DESC_R; r++) {
-        if (!d[r].valid) continue;
-        const float angle = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), r));
-        const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), r));
-        const float bs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), r));
-        // GET_VALUE(idx) = center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)] (:158-160), the
-        // products and sums rounded one by one as on x86 (no contraction). cvRound (round half
-        // to even) as v + 1.5*2^23: for |v| < 2^22 the float sum holds round(v) in its low
-        // mantissa bits, bits = 0x4B400000 + round(v); the rotated offsets are within +-18, so
-        // the byte index (dy + 18) * 40 + dx + 18 + PSH = bits_y * 40 + bits_x - C (24-bit
-        // multiply of bits_y's low 24 bits 0x400000 + dy, unsigned wrap-around).
-        const uint8_t *pc = (const uint8_t *)patch[wv][r];
-        const uint32_t ib = (uint32_t)(18 * 40 + 18 + PSH[r]) - (0x400000u * 40u + 0x4B400000u);
-        const f32x2 av = {a, a}, bv = {bs, bs}, MAG = {12582912.0f, 12582912.0f};
-        unsigned long long words[4];
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const f32x2 qy = (PX[w] * bv + PY[w] * av) + MAG;
-            const f32x2 qx = (PX[w] * av - PY[w] * bv) + MAG;
-            const uint32_t i0 = __umul24(__float_as_uint(qy.x), 40u) + __float_as_uint(qx.x) + ib;
-            const uint32_t i1 = __umul24(__float_as_uint(qy.y), 40u) + __float_as_uint(qx.y) + ib;
-#ifdef EXP_SKIP_BRIEF   // marginal-cost experiments only (tools/skip_exp.py)
-            words[w] = i0 == i1;
-#else
-            words[w] = __ballot(pc[i0] < pc[i1]);
-#endif
-        }
-        if (lane == 0) {
-            const int l = d[r].l;
-            const long long o = (long long)b * cap + d[r].off;
-            unsigned long long *dd = (unsigned long long *)(desc + o * 32);
-            dd[0] = words[0]; dd[1] = words[1]; dd[2] = words[2]; dd[3] = words[3];
-            orbx_kp kp;
-            const float s = d[r].scale;
-            kp.x = (float)(key_x(d[r].key) + 16);
-            kp.y = (float)(key_y(d[r].key) + 16);
-            if (l != 0) { kp.x *= s; kp.y *= s; }  // :1642-1651
-            kp.size = (float)d[r].spatch;
-            kp.angle = angle;
-            kp.response = (float)key_score(d[r].key);
-            kp.octave = l;
-            kp.class_id = -1;
-            kps[o] = kp;
-        }
-    }
-}
-
-// K5, software-pipelined form: NS output slots per wavefront (same arithmetic, same outputs as
-// describe_kernel). describe_kernel spends a dependent global round trip on every 3 slots and
-// runs its per-wavefront fixed work (slot resolution, fastAtan2 + glibc sincosf on 3 lanes) for
-// 3 keypoints; here
+// K5: IC_Angle (:94-141) + computeOrbDescriptor (:153-204) + keypoint assembly (:1603-1657), NS = 8
+// output slots per wavefront (3 per wavefront with a dependent global round trip per slot before:
+// 444 -> 340 us per 128 pairs alone):
 //  1. the NS slots are resolved lane-parallel (lane r = slot s0 + r: level, output row, key,
 //     IC_Angle row base, blurred-patch base) in one round trip;
 //  2. the IC_Angle rows of all NS slots and the steered-BRIEF patches of the first G slots are
@@ -1818,42 +1562,33 @@ __device__ __forceinline__ int write_lane(int v, int r, int old) {
     return old;
 }
 
-// WIDE: the IC_Angle rows as one 16-byte load per lane (two lanes per 32-byte row segment) and
-// the patch as two 16-byte loads per lane (three lanes per 48-byte row, LDS rows of 12 dwords):
-// 3 vector-memory instructions per slot instead of 11 (the texture pipeline, TA / TD, is ~88 %
-// busy under describe2 with dword loads: tools/pmc_mem.sh)
-#ifndef ORBX_DESC_CLIP
-#define ORBX_DESC_CLIP 1   // describe2: load only the patch / IC_Angle dwords a keypoint can read
-#endif
-template <int NS, int G, int NB, int PRE, bool WIDE>
+// Loads: only the patch / IC_Angle dwords a keypoint can read (c_pmask, c_icw: 370 -> 308-310 patch
+// and 248 -> 208 IC_Angle dwords per slot, C2 +0.65 %). Measured and not kept: 4, 6 or
+// 12 slots per wavefront, groups of 4, prefetch distance 2-4 (1-4 % slower, more VGPRs); 16-byte
+// loads (the texture pipeline stays as busy, no faster).
+constexpr int kDescNS = 8;   // slots per wavefront (the moment butterfly holds 8)
 __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uint8_t *in, const uint8_t *pyr,
                                                         const uint8_t *blur, const uint32_t *sel, const int *sel_cnt,
                                                         orbx_kp *kps, uint8_t *desc, int *cnt) {
+    constexpr int NS = kDescNS, G = 2, NB = 2, PRE = 1;   // slots, group size, patch buffers, groups issued early
     static_assert(NS % G == 0 && NS <= 8, "slot groups; the moment butterfly holds 8 slots");
     constexpr int NG = NS / G;
-    lat_prio<4>();
     const int lane = threadIdx.x & 63, wv = wave_id();
     int bxr, b;
     xcd_remap2(bxr, b);
-    constexpr int PW = WIDE ? 12 : 10;   // patch row stride in dwords (LDS)
-    constexpr int PSZ = WIDE ? 444 : 372;
+    constexpr int PW = 10;   // patch row stride in dwords (LDS)
+    constexpr int PSZ = 372;
     __shared__ __align__(16) uint32_t patch[4][G][PSZ];
     const int L = g.nlevels, cap = g.out_base[L];   // L <= ORBX_MAXL = 16: one DPP row
     const int s0 = (bxr * 4 + wv) * NS;
     // IC_Angle byte weights of the lane's four rows (the same for every slot): issued first, with
     // the slot loads, instead of after each slot's rows
     const int w8 = lane & 7, vr = lane >> 3;
-    // WIDE: lane -> row lane / 2 (v = row - 15; row 31 unused), bytes 16 (lane & 1) .. + 15
-    const int wrow = lane >> 1, wh = lane & 1, wv15 = wrow - 15;
     uint2 wt[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        if constexpr (WIDE) {
-            wt[k] = wrow <= 30 ? c_icw[(wv15 < 0 ? -wv15 : wv15) * 8 + 4 * wh + k] : make_uint2(0u, 0u);
-        } else {
-            const int v = vr - 15 + 8 * k;
-            wt[k] = (k < 3 || vr <= 6) ? c_icw[(v < 0 ? -v : v) * 8 + w8] : make_uint2(0u, 0u);
-        }
+        const int v = vr - 15 + 8 * k;
+        wt[k] = (k < 3 || vr <= 6) ? c_icw[(v < 0 ? -v : v) * 8 + w8] : make_uint2(0u, 0u);
     }
     // 1. lane k < L: selected keypoints of level k; lane r < NS: slot s0 + r
     const int scl = lane < L ? sel_cnt[(long long)b * L + lane] : 0;
@@ -1917,24 +1652,16 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void *)rl64(icb, r), 0, __builtin_amdgcn_readlane(icn, r), 0x00020000);
         const int pr = __builtin_amdgcn_readlane(pitch, r);
-        if constexpr (WIDE) {
-            if (wrow <= 30) {
-                const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, wrow * pr + 16 * wh, 0, 0));
-                P[r][0] = q.x; P[r][1] = q.y; P[r][2] = q.z; P[r][3] = q.w;
-            }
-        } else {
-            const int vo = vr * pr + 4 * w8;
+        const int vo = vr * pr + 4 * w8;
 #pragma unroll
-            for (int k = 0; k < 4; k++)   // a dword with no pixel inside the umax circle has weight 0
-                if ((k < 3 || vr <= 6) && (!ORBX_DESC_CLIP || wt[k].y != 0u))
-                    P[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 8 * k * pr, 0);
-        }
+        for (int k = 0; k < 4; k++)   // a dword with no pixel inside the umax circle has weight 0
+            if ((k < 3 || vr <= 6) && wt[k].y != 0u) P[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 8 * k * pr, 0);
     }
     // steered-BRIEF patch of slot r (rows y-18 .. y+18, bytes x-18 .. x+21 as 10 aligned dwords
     // per row; lanes 0..59 -> (row lane / 10, dword lane % 10), six rows per pass) into registers
     const int rr0 = (lane * 205) >> 11, q10 = lane - 10 * rr0;
-    const uint32_t pmask = ORBX_DESC_CLIP && !WIDE ? c_pmask[lane] : ~0u;
-    constexpr int TK = WIDE ? 8 : 7;   // patch registers per slot and lane
+    const uint32_t pmask = c_pmask[lane];
+    constexpr int TK = 7;   // patch registers per slot and lane
     uint32_t T[NB][G][TK];   // NB groups' patches in flight (prefetch distance NB)
     auto issue_patch = [&](int gi, uint32_t (&dst)[G][TK]) {
 #pragma unroll
@@ -1947,25 +1674,12 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc((void *)(blur + (long long)rl64((unsigned long long)a0, r)), 0,
                                                   __builtin_amdgcn_readlane(bln, r), 0x00020000);
-            if constexpr (WIDE) {
-                // lane t = lane + 64 k (k = 0, 1) -> row t / 3, bytes 16 (t % 3) .. + 15 of the 48
+            const int vo = rr0 * bwr + 4 * q10;
+            const uint32_t pm = pmask >> (7 * __builtin_amdgcn_readlane(psh, r));
+            if (lane < 60) {
 #pragma unroll
-                for (int k = 0; k < 2; k++) {
-                    const int t = lane + 64 * k, pr3 = (t * 171) >> 9, pj = t - 3 * pr3;   // t / 3 for t < 128
-                    if (pr3 < 37) {
-                        const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, pr3 * bwr + 16 * pj, 0, 0));
-                        dst[j][4 * k] = q.x; dst[j][4 * k + 1] = q.y; dst[j][4 * k + 2] = q.z; dst[j][4 * k + 3] = q.w;
-                    }
-                }
-            } else {
-                const int vo = rr0 * bwr + 4 * q10;
-                const uint32_t pm = pmask >> (7 * __builtin_amdgcn_readlane(psh, r));
-                if (lane < 60) {
-#pragma unroll
-                    for (int k = 0; k < 7; k++)
-                        if ((k < 6 || rr0 == 0) && ((pm >> k) & 1u))
-                            dst[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 6 * k * bwr, 0);
-                }
+                for (int k = 0; k < 7; k++)
+                    if ((k < 6 || rr0 == 0) && ((pm >> k) & 1u)) dst[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 6 * k * bwr, 0);
             }
         }
     };
@@ -1984,26 +1698,14 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     for (int r = 0; r < 8; r++) {
         int m01 = 0, m10 = 0;
         if (r < NS && ((vmask >> r) & 1)) {
-            if constexpr (WIDE) {
-                int sms = 0;
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < 4; k++) {
+                const int v = vr - 15 + 8 * k;
+                if (k < 3 || vr <= 6) {
                     const int su = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].x, 0u, false);
                     const int sm = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].y, 0u, false);
                     m10 += su - 16 * sm;
-                    sms += sm;
-                }
-                m01 = wv15 * sms;
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const int v = vr - 15 + 8 * k;
-                    if (k < 3 || vr <= 6) {
-                        const int su = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].x, 0u, false);
-                        const int sm = (int)__builtin_amdgcn_udot4(P[r < NS ? r : 0][k], wt[k].y, 0u, false);
-                        m10 += su - 16 * sm;
-                        m01 += v * sm;
-                    }
+                    m01 += v * sm;
                 }
             }
         }
@@ -2054,15 +1756,7 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
             if (!((vmask >> r) & 1)) continue;
             uint32_t *pt = patch[wv][j];
             if ((smask >> r) & 1) {
-                if constexpr (WIDE) {
-#pragma unroll
-                    for (int k = 0; k < 2; k++) {
-                        const int t = lane + 64 * k, pr3 = (t * 171) >> 9, pj = t - 3 * pr3;
-                        if (pr3 < 37)
-                            *(uint4 *)&pt[PW * pr3 + 4 * pj] = make_uint4(T[gi % NB][j][4 * k], T[gi % NB][j][4 * k + 1],
-                                                                          T[gi % NB][j][4 * k + 2], T[gi % NB][j][4 * k + 3]);
-                    }
-                } else if (lane < 60) {
+                if (lane < 60) {
 #pragma unroll
                     for (int k = 0; k < 7; k++)
                         if (k < 6 || rr0 == 0) pt[10 * (rr0 + 6 * k) + q10] = T[gi % NB][j][k];
@@ -2090,8 +1784,12 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
             if (!((vmask >> r) & 1)) continue;
             const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), r));
             const float bs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), r));
-            // GET_VALUE(idx) = center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)] (:158-160), as
-            // in describe_kernel: cvRound by + 1.5*2^23, byte index from the float bits
+            // GET_VALUE(idx) = center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)] (:158-160), the
+            // products and sums rounded one by one as on x86 (no contraction). cvRound (round half to
+            // even) as v + 1.5*2^23: for |v| < 2^22 the float sum holds round(v) in its low mantissa
+            // bits, bits = 0x4B400000 + round(v); the rotated offsets are within +-18, so the byte
+            // index (dy + 18) * 4 PW + dx + 18 + psh = bits_y * 4 PW + bits_x - C (24-bit multiply of
+            // bits_y's low 24 bits 0x400000 + dy, unsigned wrap-around)
             const uint8_t *pc = (const uint8_t *)patch[wv][j];
             const uint32_t ib = (uint32_t)(18 * 4 * PW + 18 + __builtin_amdgcn_readlane(psh, r)) - (0x400000u * 4u * PW + 0x4B400000u);
             const f32x2 av = {a, a}, bv = {bs, bs}, MAG = {12582912.0f, 12582912.0f};
@@ -2101,11 +1799,7 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
                 const f32x2 qx = (PX[w] * av - PY[w] * bv) + MAG;
                 const uint32_t i0 = __umul24(__float_as_uint(qy.x), 4u * PW) + __float_as_uint(qx.x) + ib;
                 const uint32_t i1 = __umul24(__float_as_uint(qy.y), 4u * PW) + __float_as_uint(qx.y) + ib;
-#ifdef EXP_SKIP_BRIEF   // marginal-cost experiments only (tools/skip_exp.py)
-                const unsigned long long word = i0 == i1;
-#else
                 const unsigned long long word = __ballot(pc[i0] < pc[i1]);
-#endif
                 dlo = (uint32_t)write_lane((int)(uint32_t)word, 4 * r + w, (int)dlo);
                 dhi = (uint32_t)write_lane((int)(uint32_t)(word >> 32), 4 * r + w, (int)dhi);
             }
@@ -2441,37 +2135,12 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
         e->d_qt_nodes.as<unsigned char>(), e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>());
     prof_end(e, s, ph, "quadtree_kernel");
     ph = prof_begin(e, s);
-    static const int desc_r = orbx_knob("ORBX_DESC_R", 3);  // tuning knob: 2 0.92 ms, 3 0.88, 4 0.97, 6 1.18 per 256 pairs
-    const dim3 dg4((cap + 15) / 16, n), dg3((cap + 11) / 12, n), dg2((cap + 7) / 8, n), dg6((cap + 23) / 24, n);
-    uint8_t *d_blur = e->d_blur.as<uint8_t>();
-    const uint32_t *d_sel = e->d_sel.as<uint32_t>();
-    const int *d_sel_cnt = e->d_sel_cnt.as<int>();
-    orbx_kp *d_kps = e->d_kps.as<orbx_kp>();
-    uint8_t *d_desc = e->d_desc.as<uint8_t>();
-    int *d_cnt = e->d_cnt.as<int>();
-    // describe2_kernel<NS, G> (default 8 slots per wavefront in groups of 2); ORBX_DESC_V=0 runs
-    // describe_kernel<ORBX_DESC_R> instead
-    static const int desc_v = orbx_knob("ORBX_DESC_V", 82);
+    const uint8_t *d_blur = e->d_blur.as<uint8_t>();
     for (int rep = 0; rep < ((exp_twice() & 4) ? 2 : 1); rep++)
-    if (desc_v != 0) {
-        switch (desc_v) {
-        case 62: describe2_kernel<6, 2, 2, 1, false><<<dim3((cap + 23) / 24, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 8222: describe2_kernel<8, 2, 2, 2, false><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 8242: describe2_kernel<8, 2, 4, 2, false><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 42: describe2_kernel<4, 2, 2, 1, false><<<dim3((cap + 15) / 16, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 8241: describe2_kernel<8, 2, 4, 1, false><<<(dim3((cap + 31) / 32, n)), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 83: describe2_kernel<8, 2, 2, 1, true><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        case 832: describe2_kernel<8, 4, 2, 1, true><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        default: describe2_kernel<8, 2, 2, 1, false><<<dim3((cap + 31) / 32, n), 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-        }
-    } else
-    switch (desc_r) {
-    case 2: describe_kernel<2><<<dg2, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-    default: describe_kernel<3><<<dg3, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-    case 6: describe_kernel<6><<<dg6, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-    case 4: describe_kernel<4><<<dg4, 256, 0, s>>>(g, d_imgs, pyr, d_blur, d_sel, d_sel_cnt, d_kps, d_desc, d_cnt); break;
-    }
-    prof_end(e, s, ph, desc_v != 0 ? "describe2_kernel" : "describe_kernel");
+        describe2_kernel<<<dim3((cap + 4 * kDescNS - 1) / (4 * kDescNS), n), 256, 0, s>>>(
+            g, d_imgs, pyr, d_blur, e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>(), e->d_kps.as<orbx_kp>(),
+            e->d_desc.as<uint8_t>(), e->d_cnt.as<int>());
+    prof_end(e, s, ph, "describe2_kernel");
     }
     HIPCHK(hipGetLastError());
     HIPCHK(mark_done(e, s));

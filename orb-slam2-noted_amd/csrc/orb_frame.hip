@@ -279,11 +279,9 @@ __device__ __forceinline__ void min2_row(uint32_t &k1, uint32_t &k2) {
     min2_dpp_step<0x140>(k1, k2);   // row_mirror
 }
 
-#ifndef SI_SPEC
-#define SI_SPEC 0   // 1: speculative 64-keypoint windows in search_init_resolve_kernel -- bit-exact, but the
-                    // kernel alone 166 against 150 us per 256-frame batch and the C3 leg +1.2 % (below the
-                    // 3 % bar of VERDICT r4 item 7): profiles/r05_ab_c3_spec.log, r05_c3_prof_spec_*.csv
-#endif
+// (Measured and not kept: speculative 64-keypoint windows in this walk -- bit-exact, but the kernel
+// alone 166 against 150 us per 256-frame batch and the C3 leg +1.2 %: profiles/r05_ab_c3_spec.log,
+// tools/archive/pruned_r06.patch.)
 __global__ __launch_bounds__(256) void search_init_resolve_kernel(SearchArgs a, float *prev_xy, int *m12, int *nmatch) {
     extern __shared__ uint32_t rs_lds[];
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = wave_id();
@@ -329,94 +327,6 @@ __global__ __launch_bounds__(256) void search_init_resolve_kernel(SearchArgs a, 
             for (int j = lane; j < n; j += 64) stage[o + j] = L[(long long)i1 * a.cap0 + j];
         }
         __syncthreads();
-#if SI_SPEC
-        if (wv == 0) {
-            // Speculative windows (the claim-set technique of track_local_resolve_kernel): lane j decides
-            // F1 keypoint w0 + j against the state at the window start -- its two smallest visible
-            // (dist << 12 | position) keys over its own list. A claim (i2, d) by an earlier lane k only
-            // ever lowers vMatchedDistance[i2], i.e. hides i2 from later keypoints with dist(i2) >= d;
-            // hiding a candidate that is neither a lane's best nor its second leaves its decision as it
-            // is, so lane j is valid unless an earlier lane's claim hides its best, or its second when
-            // that can turn its ratio-test rejection into an acceptance. The
-            // valid prefix (lane 0 always) commits in lane order: the first claimer of an i2 evicts its
-            // owner from before the window, every later one the claimer before it (ORBmatcher.cc:
-            // 659-690), the last one owns it; then the window restarts at the first invalid lane.
-            __builtin_amdgcn_s_setprio(3);
-            for (int w0 = s0; w0 < e0;) {
-                const int i1 = w0 + lane;
-                const bool act = i1 < e0;
-                const int n = act ? pre[i1 + 1] - pre[i1] : 0, o = act ? pre[i1] - pre[s0] : 0;
-                int nmax = n;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
-                uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
-                for (int t = 0; t < nmax; t += 4) {   // four entries and their state words in flight
-                    uint32_t e[4], st[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) e[u] = t + u < n ? stage[o + t + u] : 0xFFFFFFFFu;
-#pragma unroll
-                    for (int u = 0; u < 4; u++) st[u] = t + u < n ? vst[e[u] & 0xFFFFu] : 0u;
-#pragma unroll
-                    for (int u = 0; u < 4; u++)
-                        if (t + u < n) {
-                            const int dist = (int)((e[u] >> 16) & 0x1FFu);
-                            if (!((int)(st[u] & 0xFFFFu) <= dist)) min2_merge(k1, k2, (uint32_t)dist << 12 | (uint32_t)(t + u), 0xFFFFFFFFu);
-                        }
-                }
-                uint32_t went = 0, wsec = 0xFFFFFFFFu;
-                int bd = 0, bd2 = INT_MAX;
-                bool accept = false;
-                if (k1 != 0xFFFFFFFFu) {
-                    bd = (int)(k1 >> 12);
-                    bd2 = k2 == 0xFFFFFFFFu ? INT_MAX : (int)(k2 >> 12);
-                    went = stage[o + (int)(k1 & 0xFFFu)];
-                    if (k2 != 0xFFFFFFFFu) wsec = stage[o + (int)(k2 & 0xFFFu)];
-                    accept = bd <= 50 && bd < (float)bd2 * a.nnratio;   // TH_LOW, mfNNratio
-                }
-                const int ci2 = accept ? (int)(went & 0xFFFFu) : -1;
-                const int b_i2 = k1 != 0xFFFFFFFFu ? (int)(went & 0xFFFFu) : -1;
-                // hiding the second only matters to a keypoint the ratio test rejected: an accepted one
-                // stays accepted with a larger second (bd < nnratio d2 <= nnratio d3), one over TH_LOW
-                // stays rejected
-                const int s_i2 = k2 != 0xFFFFFFFFu && !accept && bd <= 50 ? (int)(wsec & 0xFFFFu) : -1;
-                bool bad = false;
-                for (unsigned long long m = __ballot(ci2 >= 0); m; m &= m - 1) {   // wave-uniform
-                    const int k = __builtin_ctzll(m);
-                    const int ck = __builtin_amdgcn_readlane(ci2, k), dk = __builtin_amdgcn_readlane(bd, k);
-                    if (k < lane && ((ck == b_i2 && dk <= bd) || (ck == s_i2 && dk <= bd2))) bad = true;
-                }
-                const unsigned long long badm = __ballot(bad && act);
-                const int ncommit = badm ? __builtin_ctzll(badm) : min(64, e0 - w0);
-                const bool claim = lane < ncommit && ci2 >= 0;
-                bool later = false, earlier = false;
-                for (unsigned long long m = __ballot(claim); m; m &= m - 1) {
-                    const int k = __builtin_ctzll(m);
-                    const int ck = __builtin_amdgcn_readlane(ci2, k);
-                    if (claim && ck == ci2) {
-                        later |= k > lane;
-                        earlier |= k < lane;
-                    }
-                }
-                const uint32_t sst = claim ? vst[ci2] : 0u;   // the owner before the window (read before the writes)
-                const int prev = (int)(int16_t)(sst >> 16);
-                int delta = claim ? 1 - (earlier ? 1 : (prev >= 0 ? 1 : 0)) : 0;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) delta += __shfl_xor(delta, off, 64);
-                nmatches += delta;
-                if (claim) {
-                    if (!earlier && prev >= 0) M12[prev] = -1;
-                    M12[i1] = later ? (int16_t)-1 : (int16_t)ci2;
-                    if (!later) vst[ci2] = (uint32_t)(uint16_t)bd | (uint32_t)(uint16_t)(int16_t)i1 << 16;
-                    if (a.check_ori) bin_of[i1] = (int8_t)(went >> 25);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                w0 += ncommit;
-            }
-            __builtin_amdgcn_s_setprio(0);
-        }
-#else
         if (wv == 0) {
             // The walk is one wave's dependent chain and shares its CU with other engines'
             // VALU-bound extraction waves (C3 runs batches on three streams): issue priority keeps
@@ -502,7 +412,6 @@ __global__ __launch_bounds__(256) void search_init_resolve_kernel(SearchArgs a, 
             }
             __builtin_amdgcn_s_setprio(0);
         }
-#endif
         __syncthreads();
         s0 = e0;
     }

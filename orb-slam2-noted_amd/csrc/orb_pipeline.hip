@@ -78,12 +78,10 @@ static int pipeline_run(orbx_pipeline *pl, const uint8_t *d_imgs, int n_pairs, i
         // fast_blur then starts the moment that one ends (measured against ordering the whole
         // phase 1: 71.2-71.8k vs 68.1-69.6k stereo frames/s, and no pipeline phase that leaves
         // describe without a fast_blur to overlap)
-        static const bool whole_p1 = orbamd::orbx_knob("ORBX_PIPE_ORDER_P1", 0) != 0;
         const bool gate = pl->last_p1 >= 0 && pl->last_p1 != j;
-        if (gate && whole_p1 && hipStreamWaitEvent(s, pl->ev_p1[pl->last_p1], 0) != hipSuccess) return ORBX_EDEVICE;
         const uint8_t *src = d_imgs + (size_t)2 * pl->first[j] * image_stride;
         const int n_img = 2 * pl->count[j];
-        orbx_engine_fb_gate(e, gate && !whole_p1 ? pl->ev_p1[pl->last_p1] : nullptr);
+        orbx_engine_fb_gate(e, gate ? pl->ev_p1[pl->last_p1] : nullptr);
         int rc = orbx_extract_batch_device_phase(e, src, n_img, w, h, pitch, image_stride, s, 1);
         orbx_engine_fb_gate(e, nullptr);
         if (rc) return rc;

@@ -10,8 +10,7 @@
 //                         LDS once, then per keypoint on one wavefront: 64-wide popcount Hamming
 //                         + (dist, index) min-reduce (= first minimum in right-index order,
 //                         :912-978), the 11x11 SAD over incR in [-5, 5] (:981-1063), parabola
-//                         fit and depth (stereo_match_left: the same with one keypoint per
-//                         wavefront reading global memory, ORBX_ST_V=0)
+//                         fit and depth
 //   S3 stereo_median_cut  one workgroup per pair: median of the SAD distances and the
 //                         1.5*1.4*median rejection (:1112-1127)
 #include <hip/hip_runtime.h>
@@ -79,10 +78,7 @@ __device__ __forceinline__ const uint8_t *side_level(const ExtractGeom &g, const
 // keypoint's final slot = bucket start + its rank among the bucket's few members by (y, index).
 // Replaces a 4096-key bitonic sort in LDS (86 -> ~10 us for one pair: the single-frame latency).
 #define ST_THREADS 512
-#ifndef ORBX_ST_WIN
-#define ORBX_ST_WIN 1   // SAD window: one 20-byte right load per lane, centre pixels by ds_bpermute
-#endif
-// Workgroups n_pairs .. 2 n_pairs - 1 (ORBX_ST_V = 1) bucket the LEFT keypoints of pair
+// Workgroups n_pairs .. 2 n_pairs - 1 bucket the LEFT keypoints of pair
 // blockIdx.x - n_pairs by image row into lidx (any order inside a row: S2 writes each result to
 // the keypoint's own slot, so the order only groups keypoints of nearby rows into workgroups).
 __global__ __launch_bounds__(ST_THREADS) void stereo_sort_right(ExtractGeom g, StereoArgs a, uint4 *sorted,
@@ -192,7 +188,6 @@ __device__ __forceinline__ void stereo_refine(const orbx_kp &kpL, bool matched, 
         const int rr = lane & 15, sgrp = lane >> 4, rrc = min(rr, 10);
         uint32_t LD[3];
         __builtin_memcpy(LD, imL + (long long)(r0 + rrc) * pitchL + cL0, 12);   // 11 pixels + 1 (in the level)
-#if ORBX_ST_WIN
         // the lane's right-window bytes of all three passes in one 20-byte load: pass p reads cols
         // cR + 4 p + s - 10 .. + 11, i.e. dwords p .. p + 2 of the block at cR + s - 10 (its last
         // bytes reach at most one column past the reference's window, still inside the level's
@@ -203,31 +198,17 @@ __device__ __forceinline__ void stereo_refine(const orbx_kp &kpL, bool matched, 
         __builtin_memcpy(WR, imR + (long long)(r0 + rrc) * pitchR + cR - 10 + sgrp, 20);
         const int c5 = ((lane & ~15) | 5) << 2;
         const int cl = (int)((__builtin_amdgcn_ds_bpermute(c5, (int)LD[1]) >> 8) & 0xFF);   // col cL0 + 5
-#else
-        const int cl = imL[(long long)(r0 + 5) * pitchL + cL0 + 5];
-        uint32_t RD[3];
-#endif
         const uint32_t Lp[6] = {__builtin_amdgcn_perm(0u, LD[0], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[0], 0x0c030c02u),
                                 __builtin_amdgcn_perm(0u, LD[1], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[1], 0x0c030c02u),
                                 __builtin_amdgcn_perm(0u, LD[2], 0x0c010c00u), __builtin_amdgcn_perm(0u, LD[2], 0x0c0c0c02u)};
         const uint32_t ONES = 0x01010101u;
-#if !ORBX_ST_WIN
-        const uint8_t *rowR = imR + (long long)(r0 + rrc) * pitchR + cR - 5;
-        const uint8_t *rowC = imR + (long long)(r0 + 5) * pitchR + cR;
-#endif
         int sums[12];
 #pragma unroll
         for (int pss = 0; pss < 3; pss++) {
             const int inc = 4 * pss + sgrp - 5;
-#if ORBX_ST_WIN
             const uint32_t RD[3] = {WR[pss], WR[pss + 1], WR[pss + 2]};
             const int kc = (int)((__builtin_amdgcn_ds_bpermute(c5, (int)WR[pss + 1]) >> 8) & 0xFF);   // col cR + inc
             const uint32_t KA = (uint32_t)(kc - cl + 256), KA2 = KA * 0x10001u;
-#else
-            const int incc = min(inc, 5);
-            const uint32_t KA = (uint32_t)(rowC[incc] - cl + 256), KA2 = KA * 0x10001u;
-            __builtin_memcpy(RD, rowR + incc, 12);   // cols cR + inc - 5 .. + 6 (endu < width)
-#endif
             uint32_t acc = __builtin_amdgcn_sad_u16(Lp[0] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04010400u), 0u);
             acc = __builtin_amdgcn_sad_u16(Lp[1] + KA2, __builtin_amdgcn_perm(ONES, RD[0], 0x04030402u), acc);
             acc = __builtin_amdgcn_sad_u16(Lp[2] + KA2, __builtin_amdgcn_perm(ONES, RD[1], 0x04010400u), acc);
@@ -272,96 +253,16 @@ __device__ __forceinline__ void stereo_refine(const orbx_kp &kpL, bool matched, 
     }
 }
 
-// ---- S2: per left keypoint
-__global__ __launch_bounds__(256) void stereo_match_left(ExtractGeom g, StereoArgs a,
-                                                         const uint4 *sorted,
-                                                         float *u_right, float *depth, int *sad) {
-    lat_prio<8>();
-    const int lane = threadIdx.x & 63, wv = wave_id();
-    int bxr, p;
-    xcd_remap2(bxr, p);
-    const int iL = bxr * 4 + wv;
-    if (iL >= a.cap) return;
-    const int imgL = a.L.img_base + a.L.img_step * p, imgR = a.R.img_base + a.R.img_step * p;
-    const int nL = min(a.L.cnt[imgL], a.cap), nR = min(a.R.cnt[imgR], a.cap);
-    const long long o = (long long)p * a.cap + iL;
-    if (iL >= nL) return;
-    const orbx_kp kpL = a.L.kps[(long long)imgL * a.cap + iL];
-    const orbx_kp *kR = a.R.kps + (long long)imgR * a.cap;
-    const int levelL = kpL.octave;
-    const float vL = kpL.y, uL = kpL.x;
-    const float minD = 0, maxD = a.maxD;
-    const float minU = uL - maxD, maxU = uL - minD;
-    const int row = (int)vL;
-    int bestDist = 100;  // ORBmatcher::TH_HIGH
-    int bestIdxR = 0;
-    if (maxU >= 0) {
-        // candidates: right keypoints whose band [floor(y-r), ceil(y+r)] contains `row`
-        const uint4 *srt = sorted + (long long)p * a.sort_cap;
-        const float ylo = (float)row - a.rmax - 2.0f;
-        // first entry with y >= floor(ylo): entries below ylo fail the band test anyway
-        // (y + r < row - 2), so starting there is exact
-        const int lo = a.rowtab[(long long)p * a.nrows + min(max((int)floorf(ylo), 0), a.nrows - 1)];
-        const float yhi = (float)row + a.rmax + 2.0f;
-        const uint8_t *dL = a.L.desc + ((long long)imgL * a.cap + iL) * 32;
-        const uint8_t *dR = a.R.desc + (long long)imgR * a.cap * 32;
-        unsigned best = 0xFFFFFFFFu;
-        // two candidates per lane per pass (their record and descriptor loads in flight
-        // together: one dependent round trip per 128 candidates of the band)
-        for (int base = lo; base < nR; base += 128) {
-            const int c0 = base + lane, c1 = c0 + 64;
-            const uint4 e0 = c0 < nR ? srt[c0] : make_uint4(0x7f800000u, 0u, 0u, 0u);   // +inf y: past the band
-            const uint4 e1 = c1 < nR ? srt[c1] : make_uint4(0x7f800000u, 0u, 0u, 0u);
-            auto take = [&](const uint4 &e) {
-                const float ky = __uint_as_float(e.x);
-                const int oct = (int)(e.w >> 16);
-                const float kx = __uint_as_float(e.y);
-                const int minr = (int)(int16_t)(e.z & 0xFFFFu), maxr = (int)(int16_t)(e.z >> 16);
-                return ky <= yhi && row >= minr && row <= maxr && oct >= levelL - 1 && oct <= levelL + 1 && kx >= minU &&
-                       kx <= maxU;
-            };
-            const bool t0 = take(e0), t1 = take(e1);
-            const int i0 = (int)(e0.w & 0xFFFFu), i1 = (int)(e1.w & 0xFFFFu);
-            const int d0 = t0 ? hamming32(dL, dR + (long long)i0 * 32) : 0;
-            const int d1 = t1 ? hamming32(dL, dR + (long long)i1 * 32) : 0;
-            if (t0) best = min(best, ((unsigned)d0 << 16) | (unsigned)i0);
-            if (t1) best = min(best, ((unsigned)d1 << 16) | (unsigned)i1);
-            // sorted by y: a record past yhi ends the band (ky > yhi, or c >= nR read as +inf)
-            if (__any(__uint_as_float(e1.x) > yhi)) break;
-        }
-        // (dist, index) minimum over the wavefront once, after the scan (DPP row mins, then rows)
-        best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x111, 0xF, 0xF, false));
-        best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x112, 0xF, 0xF, false));
-        best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x114, 0xF, 0xF, false));
-        best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x118, 0xF, 0xF, false));
-        best = min(min((unsigned)__builtin_amdgcn_readlane((int)best, 15), (unsigned)__builtin_amdgcn_readlane((int)best, 31)),
-                   min((unsigned)__builtin_amdgcn_readlane((int)best, 47), (unsigned)__builtin_amdgcn_readlane((int)best, 63)));
-        if (best != 0xFFFFFFFFu && (int)(best >> 16) < bestDist) {
-            bestDist = (int)(best >> 16);
-            bestIdxR = (int)(best & 0xFFFF);
-        }
-    }
-    const bool matched = maxU >= 0 && bestDist < (100 + 50) / 2;   // thOrbDist (Frame.cc:842)
-    int pitchL, pitchR;
-    const uint8_t *imL = side_level(g, a.L, imgL, levelL, &pitchL), *imR = side_level(g, a.R, imgR, levelL, &pitchR);
-    stereo_refine(kpL, matched, matched ? kR[bestIdxR].x : 0.0f, imL, pitchL, imR, pitchR, g.lw[levelL], g.scale[levelL],
-                  g.inv_scale[levelL], a.mbf, a.maxD, lane, o, u_right, depth, sad);
-}
-
-// ---- S2, staged form (ORBX_ST_V = 1): one workgroup per ST_NK left keypoints of nearby rows
+// ---- S2: one workgroup per ST_NK left keypoints of nearby rows
 // (S1's row buckets), whose candidate bands overlap: the union of their bands -- the sorted right
 // records and the right descriptors they index -- is staged in LDS once (one global round trip
 // per workgroup instead of a record and a descriptor load per keypoint), then each wavefront scans
-// ORBX_ST_KPW keypoints from LDS. The candidate set and the (dist, index) minimum are those of the
-// per-keypoint form: band [first record with y >= floor(row - rmax - 2), first with
-// y >= floor(row + rmax + 2) + 1) and the same per-record test; a union wider than ST_SCAP records
-// scans global memory instead.
-#ifndef ORBX_ST_V
-#define ORBX_ST_V 1
-#endif
-#ifndef ORBX_ST_KPW
+// ORBX_ST_KPW keypoints from LDS (201 -> 177 us per 128 pairs alone against one keypoint per wavefront
+// reading global memory; 1, 2, 4 or 16 keypoints per wavefront measured slower). The
+// candidate set is band [first record with y >= floor(row - rmax - 2), first with
+// y >= floor(row + rmax + 2) + 1) with the reference's per-record test (:912-978); a union wider than
+// ST_SCAP records scans global memory instead.
 #define ORBX_ST_KPW 8
-#endif
 #define ST_NW 4
 #define ST_NK (ST_NW * ORBX_ST_KPW)
 #define ST_SCAP 256
@@ -377,7 +278,6 @@ __global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g,
     __shared__ uint4 s_rec[ST_SCAP], s_d0[ST_SCAP], s_d1[ST_SCAP];
     __shared__ int s_kp[ST_NK][3];   // left keypoint index (-1: none), band [lo, hi)
     __shared__ int s_lo, s_hi;
-    lat_prio<8>();
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
     int bxr, p;
     xcd_remap2(bxr, p);
@@ -572,22 +472,15 @@ static int run_stereo(const ExtractGeom &g, StereoArgs &a, int n_pairs, orbx_eng
     const size_t sort_lds = 4 * (2 * (size_t)a.nrows + 2 * (size_t)a.cap);
     if (sort_lds > 64 * 1024) return ORBX_EINVAL;
     int ph = prof_begin(store, s);
-    const bool staged = ORBX_ST_V == 1;
-    if (staged && store->d_st_res.ensure(4 * (size_t)n_pairs * sc)) return ORBX_EDEVICE;
+    if (store->d_st_res.ensure(4 * (size_t)n_pairs * sc)) return ORBX_EDEVICE;
     int *lidx = store->d_st_res.as<int>();
-    stereo_sort_right<<<staged ? 2 * n_pairs : n_pairs, ST_THREADS, sort_lds, s>>>(g, a, store->d_st_sorted.as<uint4>(),
-                                                                                  n_pairs, lidx);
+    stereo_sort_right<<<2 * n_pairs, ST_THREADS, sort_lds, s>>>(g, a, store->d_st_sorted.as<uint4>(), n_pairs, lidx);
     prof_end(store, s, ph, "stereo_sort_right");
     ph = prof_begin(store, s);
-    for (int rep = 0; rep < ((exp_twice() & 8) ? 2 : 1); rep++) {
-        if (staged)
-            stereo_match_staged<<<dim3((a.cap + ST_NK - 1) / ST_NK, n_pairs), ST_NW * 64, 0, s>>>(
-                g, a, store->d_st_sorted.as<uint4>(), lidx, u, d, sad);
-        else
-            stereo_match_left<<<dim3((a.cap + 3) / 4, n_pairs), 256, 0, s>>>(g, a, store->d_st_sorted.as<uint4>(), u, d,
-                                                                           sad);
-    }
-    prof_end(store, s, ph, staged ? "stereo_match_staged" : "stereo_match_left");
+    for (int rep = 0; rep < ((exp_twice() & 8) ? 2 : 1); rep++)
+        stereo_match_staged<<<dim3((a.cap + ST_NK - 1) / ST_NK, n_pairs), ST_NW * 64, 0, s>>>(
+            g, a, store->d_st_sorted.as<uint4>(), lidx, u, d, sad);
+    prof_end(store, s, ph, "stereo_match_staged");
     ph = prof_begin(store, s);
     stereo_median_cut<<<n_pairs, ST_THREADS, 0, s>>>(a, u, d, sad);
     prof_end(store, s, ph, "stereo_median_cut");

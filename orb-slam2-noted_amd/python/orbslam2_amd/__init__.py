@@ -101,6 +101,7 @@ SIGNATURES = [
     ("lba_destroy", None, [_P]),
     ("lba_solve", _I, [_P, _P, _P, _P]),
     ("lba_set_stop_hook", _I, [_P, _I, _I]),
+    ("lba_set_test_option", _I, [_P, _I, C.c_longlong]),
     ("orbx_profile_read", _I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     ("orbt_create", _I, [C.POINTER(C.c_void_p)]),
     ("orbt_destroy", None, [_P]),
@@ -711,6 +712,14 @@ class LocalBundleAdjustment:
         """lba_set_stop_hook: act as if pbStopFlag were raised after trial `trial` of optimize() call
         `phase` (1 or 2; 0 removes the hook)."""
         _check(lib().lba_set_stop_hook(self._h, int(phase), int(trial)), "lba_set_stop_hook")
+
+    LBA_OPT_FUSE_FINISH = 1
+    LBA_OPT_SPIN_LIMIT = 2
+
+    def set_test_option(self, option: int, value: int):
+        """lba_set_test_option: LBA_OPT_FUSE_FINISH (1 fused, 0 two launches) or LBA_OPT_SPIN_LIMIT
+        (< 0 default, 0 fault injection: every in-launch hand-off wait times out)."""
+        _check(lib().lba_set_test_option(self._h, int(option), int(value)), "lba_set_test_option")
 
     def solve(self, prob: dict, stop=False) -> dict:
         """`stop`: a bool (the flag's value for the whole call) or a ctypes.c_uint8 shared with

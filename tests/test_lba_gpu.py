@@ -197,10 +197,11 @@ def test_lba_stop_flag_live(amd, oracle_mod):
 
 
 def test_lba_stop_flag_live_deterministic(amd, oracle_mod):
-    """The live flag at a deterministic point (lba_set_stop_hook phase 3): the call itself raises the
-    caller's flag -- through the same mirror a second thread's write goes through -- once it has read
-    back its first chunk of trials (phase 1's five), while phase 2 is still queued. The call must return
-    stopped = 1 with the flag raised, and equal the oracle stopped at the trial the device observed."""
+    """The live flag at a deterministic point (lba_set_stop_hook phase 3): once the call has read back
+    its first chunk of trials (phase 1's five), while phase 2 is still queued, the word the device reads
+    turns raised -- the same mirrored word a second thread's write reaches (an engine-owned flag ORed
+    in: the caller's const flag is not written). The call must return stopped = 1 and equal
+    the oracle stopped at the trial the device observed."""
     import ctypes
     prob = synth.localba_problem(seed=12, n_kf=64, n_points=6000)
     lba = amd.LocalBundleAdjustment()
@@ -210,8 +211,41 @@ def test_lba_stop_flag_live_deterministic(amd, oracle_mod):
     flag = ctypes.c_uint8(0)
     got = lba.solve(prob, stop=flag)
     lba.set_stop_hook(0, 0)
-    assert flag.value == 1, "the hook did not raise the flag"
+    assert flag.value == 0, "the hook wrote the caller's flag"
     assert got["stopped"] == 1, (got["iterations"], got["trials"], full["trials"])
     hook = (1, got["trials"][0]) if got["iterations"][1] == 0 and got["trials"][1] == 0 else (2, got["trials"][1])
     assert sum(got["trials"]) < sum(full["trials"])
     _same(got, oracle_mod.lba_solve(prob, hook=hook), ("live-hook", chunk, hook))
+
+
+@pytest.mark.parametrize("seed,n_kf,n_pts", [(4, 20, 3000), (9, 21, 1500), (14, 8, 600)])
+def test_lba_fused_finish_bit_identical(amd, seed, n_kf, n_pts):
+    """lba_finish_chol (the Schur finish blocks hand Hs to the Cholesky block inside one launch:
+    write-through stores, an agent-scope counter, sc1 loads) against the two-launch path
+    (lba_schur_finish, then lba_chol_tiled, ordered by the kernel boundary): identical bits in every
+    output (the hand-off's memory ordering is checked, not assumed)."""
+    prob = synth.localba_problem(seed=seed, n_kf=n_kf, n_points=n_pts)
+    lba = amd.LocalBundleAdjustment()
+    fused = lba.solve(prob)
+    lba.set_test_option(lba.LBA_OPT_FUSE_FINISH, 0)
+    split = lba.solve(prob)
+    lba.set_test_option(lba.LBA_OPT_FUSE_FINISH, 1)
+    again = lba.solve(prob)
+    for k in ("pose_Tcw", "point_Xw", "edge_erase"):
+        assert np.asarray(fused[k]).tobytes() == np.asarray(split[k]).tobytes(), k
+        assert np.asarray(fused[k]).tobytes() == np.asarray(again[k]).tobytes(), k
+    assert fused["iterations"] == split["iterations"] and fused["trials"] == split["trials"]
+    assert fused["chi2"] == split["chi2"]
+
+
+def test_lba_handoff_timeout_is_an_error(amd, oracle_mod):
+    """A hand-off wait that times out (LBA_OPT_SPIN_LIMIT 0: every wait does) must not pass for a
+    rejected LM trial: lba_solve returns ORBX_EDEVICE. The engine is usable afterwards:
+    with the default bound the next call equals the oracle."""
+    prob = synth.localba_problem(seed=9, n_kf=21, n_points=1500)
+    lba = amd.LocalBundleAdjustment()
+    lba.set_test_option(lba.LBA_OPT_SPIN_LIMIT, 0)
+    with pytest.raises(amd.OrbslamError, match="status -2"):
+        lba.solve(prob)
+    lba.set_test_option(lba.LBA_OPT_SPIN_LIMIT, -1)
+    _same(lba.solve(prob), oracle_mod.lba_solve(prob), "after the fault")

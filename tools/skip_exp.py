@@ -1,7 +1,7 @@
 """Marginal cost of each part of the C2 step (experiment, not a parity path): the bench's C2
 pipeline (3 engines x 128 pairs, 384 pairs per step) timed with instrumented builds of the same
-sources in which one part is compiled out (make variant VDEFS=-D...: EXP_SKIP_RESIZE,
-FB_SKIP_PRE / FB_SKIP_EXACT / FB_SKIP_BLUR, EXP_SKIP_BRIEF; outputs of a skipped part are
+sources in which one part is compiled out (make variant VDEFS=-D...: FB_SKIP_PRE / FB_SKIP_EXACT /
+FB_SKIP_BLUR; EXP_SKIP_RESIZE and EXP_SKIP_BRIEF were removed in round 6; outputs of a skipped part are
 garbage and downstream work may change with them, so only skips whose outputs feed nothing
 but pixel values are clean), or with an idempotent kernel launched twice (lib:mask ->
 ORBX_EXP_TWICE=mask, orb_engine.h: the clean way to read a kernel's marginal cost). One
