@@ -1864,22 +1864,29 @@ struct LmPhase {
             ph = lprof_begin(e);
             lba_schur_finish<<<g.npairs, 256, 0, s>>>(g);
             lprof_end(e, ph, "lba_schur_finish");
-            ph = lprof_begin(e);
             if (n6 <= kSmallNP) {
+                ph = lprof_begin(e);
                 lba_chol_tiled<<<1, kCT, chol_tiled_lds(n6), s>>>(g);
                 lprof_end(e, ph, "lba_chol_tiled");
-            } else {
+            } else {   // every launch its own profile record: lba_profile_read's counts are launches
+                ph = lprof_begin(e);
                 lba_set_ok<<<1, 1, 0, s>>>(g);
+                lprof_end(e, ph, "lba_set_ok");
                 for (int kb = 0; kb < n6; kb += kCB) {
                     const int rows = n6 - kb - kCB;
+                    ph = lprof_begin(e);
                     lba_chol_panel<<<std::max(1, (rows + 255) / 256), 256, 0, s>>>(g, kb);
+                    lprof_end(e, ph, "lba_chol_panel");
                     if (rows > 0) {
                         const int nt = (rows + 15) / 16;
+                        ph = lprof_begin(e);
                         lba_chol_update<<<nt * (nt + 1) / 2, 64, 0, s>>>(g, kb, nt);
+                        lprof_end(e, ph, "lba_chol_update");
                     }
                 }
+                ph = lprof_begin(e);
                 lba_chol_solve_blocked<<<1, 1024, sizeof(double) * n6, s>>>(g);
-                lprof_end(e, ph, "lba_chol_blocked");
+                lprof_end(e, ph, "lba_chol_solve_blocked");
             }
             }
         } else {
