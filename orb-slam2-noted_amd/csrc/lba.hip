@@ -139,6 +139,8 @@ struct Graph {
     const unsigned *stopf; // pbStopFlag mirrored by lba_solve's host loop into page-locked, device-mapped memory
     unsigned *arrive;      // [0]: lba_finish_chol's finish-block arrivals; [1]: its hand-off timeout (fault) word
     unsigned spin_limit;   // the hand-off wait's poll bound (kSpinLimit; lba_set_test_option)
+    double *W;             // 6P > kSmallNP: the Cholesky's work matrix [N2][LDW] (chol_global_body)
+    int LDW;
     int Kpad;              // Y^T rows 3 Lm rounded up to 4; row Kpad (and up to Kpad + 3) is zero
     int NP;                // Schur dimension 6P padded to a multiple of kCB
     const int2 *tp_ij;     // upper tile pairs (I, J) of the Schur matrix
@@ -1181,15 +1183,267 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_tiled_body(Graph &g
 
 __global__ __launch_bounds__(kCT) void lba_chol_tiled(Graph g) { chol_tiled_body<false>(g, 0); }
 
+// order a wavefront's LDS writes before its reads (LDS executes a wave's ops in order)
+__device__ __forceinline__ void lds_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// 6P > kSmallNP: the Schur system [Hs bs; bs^T 0] factored by one 1024-thread workgroup with the
+// matrix in a global work buffer g.W (N2 x N2, lower triangle, L2-resident) instead of LDS (a window
+// of 22-93 free keyframes: 132 <= 6P <= 558). The algorithm is chol_tiled_body's, tile for tile, so a
+// large window gets the same one-launch trial tail as a small one (the blocked path before: two
+// launches per 32-column panel, 21 launches per trial at 40 free keyframes, 0.68 ms per trial):
+//   * copy: [Hs bs; bs^T 0] plus identity rows into W's lower tiles (waves 1..15; wave 0 builds tile
+//     (0, 0) in LDS and factors it meanwhile);
+//   * per 16-column panel K: the panel below L_IK = A_IK L_KK^-T on FP64 MFMA, stored into W and into
+//     an LDS copy of the panel (Pc); the trailing lower tiles A_IJ -= L_IK L_JK^T on FP64 MFMA with both
+//     operands from Pc, read-modify-write in W, four tiles' loads in flight per wave; wave 0 updates
+//     tile (K + 1, K + 1) first (into LDS, Dt) and factors it while the other waves update the rest;
+//   * the back substitution block by block with the LDS inverses (chol_tiled_body's, its row updates
+//     reading W), then the trial poses T_t = exp(x_p) T (lba_lin_points reads them for a large window).
+// LDS: Linv [NT][16][17] | Pc [N2][17] | Dt [16][17] | y [N2] | x [N2].
+__host__ __device__ constexpr size_t chol_global_lds(int n) {
+    return sizeof(double) * ((size_t)(chol_tiled_dim(n) / 16) * 16 * 17 + (size_t)chol_tiled_dim(n) * 17 + 16 * 17 +
+                             2 * (size_t)chol_tiled_dim(n));
+}
+constexpr int kBigNP = 558;   // 6 * 93 free poses: chol_global_lds(558) + the static LDS <= 160 KB
+static_assert(chol_global_lds(kBigNP) + 64 <= 160 * 1024, "chol_global_body's LDS");
+
+template <bool HANDOFF> __device__ __forceinline__ void chol_global_body(Graph &g, int nfb) {
+    extern __shared__ double A[];
+    __shared__ int fail, tmo;
+    if (g.lm->done) return;
+    if constexpr (HANDOFF) {   // as chol_tiled_body
+        if (threadIdx.x == 0) {
+            unsigned spins = 0;
+            int to = g.spin_limit == 0;
+            while (!to && __hip_atomic_load(g.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nfb) {
+                if (++spins >= g.spin_limit) { to = 1; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (to) {
+                __hip_atomic_store(g.arrive + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                g.scalars[4] = 0;
+            } else {
+                __hip_atomic_store(g.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            tmo = to;
+        }
+        __syncthreads();
+        if (tmo) return;
+    }
+    const int n = 6 * g.P, N2 = chol_tiled_dim(n), NT = N2 / 16;
+    const long long LDW = g.LDW;
+    double *W = g.W;
+    double *Linv = A, *Pc = Linv + NT * 16 * 17, *Dt = Pc + N2 * 17, *yv = Dt + 16 * 17, *xv = yv + N2;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const long long NP = g.NP;
+    const auto hs_rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)g.Hs, 0, (int)(n * NP * 8), 0x00020000);
+    const auto bs_rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)g.bs, 0, n * 8, 0x00020000);
+    constexpr int kOOR = 0x40000000;
+    auto sys_ld = [&](int r, int c, bool ok, double &h, double &b) {
+        h = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(hs_rsrc, ok && r < n ? (r * (int)NP + c) * 8 : kOOR, 0,
+                                                                            HANDOFF ? 16 : 0));
+        b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(bs_rsrc, ok && r == n ? c * 8 : kOOR, 0, 0));
+    };
+    auto sys_val = [&](int r, int c, bool ok, double h, double b) -> double { return h + b + (ok && r > n && r == c ? 1.0 : 0.0); };
+    if (tid == 0) fail = 0;
+    // lower tile t of the NT x NT tile triangle (row-major over I >= J) -> (I, J)
+    auto tile_of = [](int t, int &I, int &J) {
+        int i = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+        if ((i + 1) * (i + 2) / 2 <= t) i++;
+        if (i * (i + 1) / 2 > t) i--;
+        I = i;
+        J = t - i * (i + 1) / 2;
+    };
+    // wave 0: factor + invert the diagonal tile held in Dt (lane i of each 16-lane row = row i)
+    auto diag = [&](int K) {
+        const int k0 = 16 * K, i = lane & 15;
+        double row[16], li[16];
+#pragma unroll
+        for (int c = 0; c < 16; c++) row[c] = Dt[i * 17 + c];
+#pragma unroll
+        for (int r = 0; r < 16; r++) li[r] = r == i ? 1.0 : 0.0;
+        bool bad = false;
+        chol16_pipe(row, li, n - k0, bad);
+        double *LK = Linv + K * 16 * 17;
+#pragma unroll
+        for (int r = 0; r < 16; r++) LK[r * 17 + i] = li[r];
+        // the factored tile into W: its row n (when n is not a multiple of 16) is part of y
+        if (lane < 16)
+#pragma unroll
+            for (int c = 0; c < 16; c++) W[(k0 + i) * LDW + k0 + c] = row[c];
+        if (lane == 0 && bad) fail = 1;
+    };
+    // 1. copy: wave 0 builds tile (0, 0) in Dt and factors it; waves 1.. copy the other lower tiles
+    const int ntri = NT * (NT + 1) / 2;
+    if (wv == 0) {
+        double hb[4][2];
+        const int cc = lane & 15;
+#pragma unroll
+        for (int q = 0; q < 4; q++) sys_ld((lane >> 4) + 4 * q, cc, cc <= (lane >> 4) + 4 * q, hb[q][0], hb[q][1]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = (lane >> 4) + 4 * q;
+            Dt[r * 17 + cc] = cc <= r ? sys_val(r, cc, true, hb[q][0], hb[q][1]) : 0.0;
+        }
+        lds_wave_sync();
+        diag(0);
+    } else {
+        for (int t0 = wv; t0 < ntri; t0 += 4 * (kCW - 1)) {   // 4 tiles' loads in flight per wave
+            double hb[4][4][2];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * (kCW - 1);
+                int I = 0, J = 0;
+                if (t < ntri) tile_of(t, I, J);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int r = 16 * I + (lane >> 4) + 4 * q, c = 16 * J + (lane & 15);
+                    sys_ld(r, c, t > 0 && t < ntri && c <= r, hb[u][q][0], hb[u][q][1]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * (kCW - 1);
+                if (t <= 0 || t >= ntri) continue;
+                int I, J;
+                tile_of(t, I, J);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int r = 16 * I + (lane >> 4) + 4 * q, c = 16 * J + (lane & 15);
+                    W[r * LDW + c] = sys_val(r, c, c <= r, hb[u][q][0], hb[u][q][1]);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int K = 0; K < NT; K++) {
+        if (fail) {   // uniform after the barrier
+            if (tid == 0) g.scalars[4] = 0;
+            return;
+        }
+        const int k0 = 16 * K, r0 = k0 + 16, m = NT - K - 1;
+        const double *LK = Linv + K * 16 * 17;
+        // 2. panel: L_IK = A_IK L_KK^-T into W and Pc (rows r0 ..)
+        for (int I = wv; I < m; I += kCW) {
+            const int ri = r0 + 16 * I;
+            double a[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) a[kk] = W[(ri + (lane & 15)) * LDW + k0 + 4 * kk + (lane >> 4)];
+            double4_t acc = {0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kk], LK[(lane & 15) * 17 + 4 * kk + (lane >> 4)], acc, 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = ri + (lane >> 4) + 4 * q;
+                W[r * LDW + k0 + (lane & 15)] = acc[q];
+                Pc[r * 17 + (lane & 15)] = acc[q];
+            }
+        }
+        __syncthreads();
+        if (m == 0) break;
+        // 3. trailing lower tiles of the m x m tile triangle below / right of panel K: tile 0 = (K + 1,
+        // K + 1) -> wave 0 (into Dt, then its factor), the others -> waves 1.., four tiles per batch
+        const int ntile = m * (m + 1) / 2;
+        auto upd = [&](int I, int J, double4_t acc) {
+            const int ri = r0 + 16 * I, cj = r0 + 16 * J;
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Pc[(ri + (lane & 15)) * 17 + 4 * kk + (lane >> 4)],
+                                                           Pc[(cj + (lane & 15)) * 17 + 4 * kk + (lane >> 4)], acc, 0, 0, 0);
+            return acc;
+        };
+        if (wv == 0) {
+            double4_t acc;
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc[q] = W[(r0 + (lane >> 4) + 4 * q) * LDW + r0 + (lane & 15)];
+            acc = upd(0, 0, acc);
+#pragma unroll
+            for (int q = 0; q < 4; q++) Dt[((lane >> 4) + 4 * q) * 17 + (lane & 15)] = acc[q];
+            lds_wave_sync();
+            diag(K + 1);
+        } else {
+            for (int t0 = wv; t0 < ntile; t0 += 4 * (kCW - 1)) {
+                double4_t acc[4];
+                int It[4], Jt[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int t = t0 + u * (kCW - 1);
+                    It[u] = Jt[u] = 0;
+                    if (t < ntile) tile_of(t, It[u], Jt[u]);
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        acc[u][q] = t < ntile ? W[(r0 + 16 * It[u] + (lane >> 4) + 4 * q) * LDW + r0 + 16 * Jt[u] + (lane & 15)] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int t = t0 + u * (kCW - 1);
+                    if (t >= ntile) continue;
+                    const double4_t o = upd(It[u], Jt[u], acc[u]);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) W[(r0 + 16 * It[u] + (lane >> 4) + 4 * q) * LDW + r0 + 16 * Jt[u] + (lane & 15)] = o[q];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // 4. back substitution L^T x = y (chol_tiled_body's, the row updates reading W)
+    for (int j = tid; j < N2; j += kCT) yv[j] = j < n ? W[n * LDW + j] : 0.0;
+    __syncthreads();
+    auto x_block = [&](int K) {
+        const int k0 = 16 * K;
+        const double *LK = Linv + K * 16 * 17;
+        const int c = lane & 15, p4 = 4 * (lane >> 4);
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) s += LK[(p4 + r) * 17 + c] * yv[k0 + p4 + r];
+        s = rows4_sum(s);
+        if (lane < 16) xv[k0 + c] = s;
+    };
+    auto y_update = [&](int k0, int j, int q4) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) s += W[(k0 + q4 + k) * LDW + j] * xv[k0 + q4 + k];
+        s = quad_sum(s);
+        if ((lane & 3) == 0) yv[j] -= s;
+    };
+    {
+        int K = (n - 1) / 16;
+        if (wv == 0) x_block(K);
+        __syncthreads();
+        for (; K > 0; K--) {
+            const int k0 = 16 * K, kp = k0 - 16;
+            if (wv == 0) {
+                y_update(k0, kp + (lane >> 2), 4 * (lane & 3));
+                lds_wave_sync();
+                x_block(K - 1);
+            } else {
+                for (int j = (tid - 64) >> 2; j < kp; j += (kCT - 64) / 4) y_update(k0, j, 4 * (tid & 3));
+            }
+            __syncthreads();
+        }
+    }
+    for (int j = tid; j < n; j += kCT) g.x[j] = xv[j];
+    const bool cur = g.lm->cur;
+    for (int t = tid; t < g.P; t += kCT) trial_pose(g, cur, t, (cur ? g.T2 : g.T)[g.hpose[t]], xv);
+    if (tid == 0) g.scalars[4] = 1;
+}
+
+__global__ __launch_bounds__(kCT) void lba_chol_global(Graph g) { chol_global_body<false>(g, 0); }
+
 // lba_schur_finish + lba_chol_tiled in one launch (one kernel boundary fewer per LM trial): blocks
 // 0 .. nfb - 1 are finish blocks, four tile pairs each (one 4-wave quad per pair, lba_schur_finish's
 // work), storing Hs write-through (sc1); after every wave's stores have drained and a workgroup
 // barrier, one lane adds 1 to g.arrive[0]. Block nfb is the Cholesky (chol_tiled_body<true>), which
 // waits for nfb arrivals. Every block is resident at once (nfb + 1 <= 10 blocks on 256 CUs), so the
 // wait cannot block a producer.
-__global__ __launch_bounds__(kCT) void lba_finish_chol(Graph g, int nfb) {
+template <bool BIG> __global__ __launch_bounds__(kCT) void lba_finish_chol(Graph g, int nfb) {
     if ((int)blockIdx.x == nfb) {
-        chol_tiled_body<true>(g, nfb);
+        if constexpr (BIG) chol_global_body<true>(g, nfb);
+        else chol_tiled_body<true>(g, nfb);
         return;
     }
     if (g.lm->done) return;   // the Cholesky block reads the same flag and does not wait
@@ -1671,7 +1925,7 @@ struct lba_engine {
     hipStream_t stream = nullptr;
     DBuf T, T2, X, X2, E, E_lm, on_lm, err, act, pose_hidx, point_hidx, hpose, hpoint, pt_start, pt_items,
         ps_start, ps_items, slot_pt, slot_ph, con, hpl, Hll, bl, Hpp, bp, Dinv, Lc, Y, ywp, on, tp_part, Hs, bs, x, partial,
-        scalars, flags, lm, arrive, arenaA, arenaB, arenaC;
+        scalars, flags, lm, arrive, arenaA, arenaB, arenaC, Wm;
     double *h_scalars = nullptr;  // pinned
     LMState *h_lm = nullptr;      // pinned, one per optimize() of a call
     void *h_stage[3] = {nullptr, nullptr, nullptr};   // pinned upload staging per arena (grow-only)
@@ -1855,10 +2109,14 @@ struct LmPhase {
             // (pose, upper component))
             lba_schur_tiles<<<g.nchunks + (n6 + 3) / 4 + (21 * A.P + 3) / 4, 256, 0, s>>>(g);
             lprof_end(e, ph, "lba_schur_tiles");
-            if (e->fuse_finish && n6 <= kSmallNP) {
+            const bool big = n6 > kSmallNP && n6 <= kBigNP;
+            if (e->fuse_finish && (n6 <= kSmallNP || big)) {
                 ph = lprof_begin(e);
                 const int nfb = (g.npairs + 3) / 4;
-                lba_finish_chol<<<nfb + 1, kCT, chol_tiled_lds(n6), s>>>(g, nfb);
+                if (big)
+                    lba_finish_chol<true><<<nfb + 1, kCT, chol_global_lds(n6), s>>>(g, nfb);
+                else
+                    lba_finish_chol<false><<<nfb + 1, kCT, chol_tiled_lds(n6), s>>>(g, nfb);
                 lprof_end(e, ph, "lba_finish_chol");
             } else {
             ph = lprof_begin(e);
@@ -1868,6 +2126,10 @@ struct LmPhase {
                 ph = lprof_begin(e);
                 lba_chol_tiled<<<1, kCT, chol_tiled_lds(n6), s>>>(g);
                 lprof_end(e, ph, "lba_chol_tiled");
+            } else if (big) {
+                ph = lprof_begin(e);
+                lba_chol_global<<<1, kCT, chol_global_lds(n6), s>>>(g);
+                lprof_end(e, ph, "lba_chol_global");
             } else {   // every launch its own profile record: lba_profile_read's counts are launches
                 ph = lprof_begin(e);
                 lba_set_ok<<<1, 1, 0, s>>>(g);
@@ -2183,6 +2445,14 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.w = g.Y + g.wrow;
         g.Hs = e->Hs.as<double>(); g.bs = e->bs.as<double>(); g.ywp = e->ywp.as<double>();
         g.x = e->x.as<double>();
+        g.W = nullptr;
+        g.LDW = 0;
+        if (6 * A.P > kSmallNP && 6 * A.P <= kBigNP) {   // chol_global_body's work matrix (fully rewritten per trial)
+            const int N2 = chol_tiled_dim(6 * A.P);
+            if (e->Wm.ensure(sizeof(double) * (size_t)N2 * N2)) return -1;
+            g.W = e->Wm.as<double>();
+            g.LDW = N2;
+        }
         {   // zeroed / filled / copied in one launch: err, arrive, the LM state, the level flags (1),
             // Y, Hs, x, and the trial buffers set equal to the current estimate (inactive vertices
             // never change)

@@ -18,13 +18,13 @@ def _rel(a, b):
     return np.abs(a - b).max() / max(np.abs(b).max(), 1e-12)
 
 
-# 6P <= 128 runs the single-workgroup LDS Cholesky; 22 / 40 / 64 free KFs (6P = 132, 240,
-# 384) run the blocked Cholesky with the MFMA trailing update (ORB-SLAM2's covisibility
-# window is not bounded by 21 keyframes). 8 and 16 free KFs (6P = 48, 96) put the appended
+# 6P <= 128 runs the single-workgroup LDS Cholesky; 22 / 40 / 64 / 93 free KFs (6P = 132, 240,
+# 384, 558) the single-workgroup Cholesky over a global work matrix (chol_global_body); 100 free
+# KFs (6P = 600) the multi-launch blocked Cholesky (ORB-SLAM2's covisibility window is not bounded). 8 and 16 free KFs (6P = 48, 96) put the appended
 # right-hand-side row first in its 16-row tile (the diagonal tile's pivot limit is 0).
 @pytest.mark.parametrize("seed,n_kf,n_pts", [(4, 20, 3000), (5, 10, 800), (6, 20, 1500), (9, 21, 1500),
                                              (10, 22, 2000), (11, 40, 4000), (12, 64, 6000),
-                                             (13, 16, 1500), (14, 8, 600)])
+                                             (13, 16, 1500), (14, 8, 600), (16, 93, 7000), (17, 100, 7000)])
 def test_lba_matches_oracle(amd, oracle_mod, seed, n_kf, n_pts):
     prob = synth.localba_problem(seed=seed, n_kf=n_kf, n_points=n_pts)
     ref = oracle_mod.lba_solve(prob)
@@ -218,9 +218,10 @@ def test_lba_stop_flag_live_deterministic(amd, oracle_mod):
     _same(got, oracle_mod.lba_solve(prob, hook=hook), ("live-hook", chunk, hook))
 
 
-@pytest.mark.parametrize("seed,n_kf,n_pts", [(4, 20, 3000), (9, 21, 1500), (14, 8, 600)])
+@pytest.mark.parametrize("seed,n_kf,n_pts", [(4, 20, 3000), (9, 21, 1500), (14, 8, 600), (10, 22, 2000), (11, 40, 4000)])
 def test_lba_fused_finish_bit_identical(amd, seed, n_kf, n_pts):
-    """lba_finish_chol (the Schur finish blocks hand Hs to the Cholesky block inside one launch:
+    """lba_finish_chol (the Schur finish blocks hand Hs to the Cholesky block inside one launch, for the
+    LDS Cholesky (<= 21 free keyframes) and the global-work-matrix one (22..93):
     write-through stores, an agent-scope counter, sc1 loads) against the two-launch path
     (lba_schur_finish, then lba_chol_tiled, ordered by the kernel boundary): identical bits in every
     output (the hand-off's memory ordering is checked, not assumed)."""
