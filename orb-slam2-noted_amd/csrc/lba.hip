@@ -1190,25 +1190,33 @@ __device__ __forceinline__ void lds_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 // 6P > kSmallNP: the Schur system [Hs bs; bs^T 0] factored by one 1024-thread workgroup with the
-// matrix in a global work buffer g.W (N2 x N2, lower triangle, L2-resident) instead of LDS (a window
-// of 22-93 free keyframes: 132 <= 6P <= 558). The algorithm is chol_tiled_body's, tile for tile, so a
-// large window gets the same one-launch trial tail as a small one (the blocked path before: two
-// launches per 32-column panel, 21 launches per trial at 40 free keyframes, 0.68 ms per trial):
-//   * copy: [Hs bs; bs^T 0] plus identity rows into W's lower tiles (waves 1..15; wave 0 builds tile
-//     (0, 0) in LDS and factors it meanwhile);
-//   * per 16-column panel K: the panel below L_IK = A_IK L_KK^-T on FP64 MFMA, stored into W and into
-//     an LDS copy of the panel (Pc); the trailing lower tiles A_IJ -= L_IK L_JK^T on FP64 MFMA with both
-//     operands from Pc, read-modify-write in W, four tiles' loads in flight per wave; wave 0 updates
-//     tile (K + 1, K + 1) first (into LDS, Dt) and factors it while the other waves update the rest;
-//   * the back substitution block by block with the LDS inverses (chol_tiled_body's, its row updates
-//     reading W), then the trial poses T_t = exp(x_p) T (lba_lin_points reads them for a large window).
-// LDS: Linv [NT][16][17] | Pc [N2][17] | Dt [16][17] | y [N2] | x [N2].
+// matrix in a global work buffer g.W (N2 x N2, lower tiles, L2-resident) instead of LDS: a window of
+// 22-88 free keyframes (132 <= 6P <= 528) gets the same one-launch trial tail as a small one (the
+// blocked path before: two launches per 32-column panel, 21 launches per trial at 40 free keyframes,
+// 0.68 ms per trial). chol_tiled_body's tiles and arithmetic, with the trailing update over two
+// 16-column panels per pass (one read-modify-write of a tile per 32 columns: the pass is bound by the
+// CU's memory and LDS bandwidth, profiles/r06_lbaprof_global*.txt):
+//   * columns K, K + 1 (K even): (B) the panel below L_IK = A_IK L_KK^-T on FP64 MFMA, into W and the
+//     LDS panel copy Pc[0]; (C) column K + 1 updated by panel K -- wave 0 takes the diagonal tile
+//     (K + 1, K + 1) into LDS (Dt) and factors it (chol16_pipe), the other waves store the rest; (D)
+//     its panel L_{I,K+1} into W and Pc[1]; (E) the trailing lower tiles A_IJ -= L_IK L_JK^T +
+//     L_{I,K+1} L_{J,K+1}^T (8 MFMAs, operands from Pc) read-modify-write in W, four tiles' loads in
+//     flight per wave, wave 0 taking (K + 2, K + 2) into Dt and factoring it;
+//   * the first pass (K = 0) reads the handed-over Hs / bs (+ identity rows) directly, so no copy of
+//     the system into W; the diagonal tile's factor goes to W (its row n is part of y), its inverse to
+//     g.W's inverse area;
+//   * the back substitution block by block (chol_tiled_body's, with the inverses copied back into LDS
+//     and every row update's W loads issued one block ahead), then the trial poses T_t = exp(x_p) T
+//     (lba_lin_points reads them for a large window).
+// LDS: Pc [2][N2][17] (after the factor: the inverses [NT][16][17]) | LKs [16][17] | Dt [16][17] | y | x.
 __host__ __device__ constexpr size_t chol_global_lds(int n) {
-    return sizeof(double) * ((size_t)(chol_tiled_dim(n) / 16) * 16 * 17 + (size_t)chol_tiled_dim(n) * 17 + 16 * 17 +
-                             2 * (size_t)chol_tiled_dim(n));
+    return sizeof(double) * (2 * (size_t)chol_tiled_dim(n) * 17 + 2 * 16 * 17 + 2 * (size_t)chol_tiled_dim(n));
 }
-constexpr int kBigNP = 558;   // 6 * 93 free poses: chol_global_lds(558) + the static LDS <= 160 KB
+constexpr int kBigNP = 528;   // 6 * 88 free poses: chol_global_lds(528) + the static LDS <= 160 KB
 static_assert(chol_global_lds(kBigNP) + 64 <= 160 * 1024, "chol_global_body's LDS");
+__host__ __device__ constexpr size_t chol_global_w(int n) {   // doubles of g.W: the matrix, then the inverses
+    return (size_t)chol_tiled_dim(n) * chol_tiled_dim(n) + (size_t)(chol_tiled_dim(n) / 16) * 256;
+}
 
 template <bool HANDOFF> __device__ __forceinline__ void chol_global_body(Graph &g, int nfb) {
     extern __shared__ double A[];
@@ -1235,201 +1243,315 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_global_body(Graph &
     }
     const int n = 6 * g.P, N2 = chol_tiled_dim(n), NT = N2 / 16;
     const long long LDW = g.LDW;
-    double *W = g.W;
-    double *Linv = A, *Pc = Linv + NT * 16 * 17, *Dt = Pc + N2 * 17, *yv = Dt + 16 * 17, *xv = yv + N2;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // W and, past it, Lg ([NT][16][16] inverses of the diagonal tiles) through one buffer descriptor with
+    // 32-bit element offsets: 64-bit addresses hoisted out of the panel loop spilled VGPRs
+    const auto w_rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)g.W, 0, (int)(8 * chol_global_w(n)), 0x00020000);
+    const int LG = N2 * (int)LDW;
+    auto wld = [&](int e) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(w_rsrc, 8 * e, 0, 0)); };
+    typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+    auto wst = [&](int e, double v) { __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), w_rsrc, 8 * e, 0, 0); };
+    double *Pc0 = A, *Pc1 = A + N2 * 17, *LKs = Pc1 + N2 * 17, *Dt = LKs + 16 * 17, *yv = Dt + 16 * 17, *xv = yv + N2;
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform
+    int lr = lane & 15, lq = lane >> 4;   // MFMA operand row / k quarter; C layout: row lq + 4q, column lr
+#ifdef LBA_PROFILE
+    const long long tg0 = clock64();
+    long long tgf = 0, tgb = 0, tgc = 0, tgd = 0, tge = 0, tgx;
+#define LBA_TG(acc) do { acc += clock64() - tgx; tgx = clock64(); } while (0)
+#else
+#define LBA_TG(acc) do {} while (0)
+#endif
     const long long NP = g.NP;
     const auto hs_rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)g.Hs, 0, (int)(n * NP * 8), 0x00020000);
-    const auto bs_rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)g.bs, 0, n * 8, 0x00020000);
     constexpr int kOOR = 0x40000000;
-    auto sys_ld = [&](int r, int c, bool ok, double &h, double &b) {
-        h = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(hs_rsrc, ok && r < n ? (r * (int)NP + c) * 8 : kOOR, 0,
-                                                                            HANDOFF ? 16 : 0));
-        b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(bs_rsrc, ok && r == n ? c * 8 : kOOR, 0, 0));
+    // bs, the system's row n, staged in LDS (the y area, unused until the back substitution)
+    for (int j = tid; j < n; j += kCT) yv[j] = g.bs[j];
+    // element (r, c <= r) of the system: the handed-over Hs (sc1 loads; 0 past row n - 1), bs as row n
+    // (from LDS), identity past it
+    auto hs_ld = [&](int r, int c, bool ok) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(hs_rsrc, ok && r < n ? (r * (int)NP + c) * 8 : kOOR,
+                                                                               0, HANDOFF ? 16 : 0));
     };
-    auto sys_val = [&](int r, int c, bool ok, double h, double b) -> double { return h + b + (ok && r > n && r == c ? 1.0 : 0.0); };
-    if (tid == 0) fail = 0;
-    // lower tile t of the NT x NT tile triangle (row-major over I >= J) -> (I, J)
-    auto tile_of = [](int t, int &I, int &J) {
-        int i = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
-        if ((i + 1) * (i + 2) / 2 <= t) i++;
-        if (i * (i + 1) / 2 > t) i--;
-        I = i;
-        J = t - i * (i + 1) / 2;
+    auto hs_val = [&](int r, int c, bool ok, double h) -> double {
+        return h + (ok && r == n ? yv[c] : 0.0) + (ok && r > n && r == c ? 1.0 : 0.0);
     };
-    // wave 0: factor + invert the diagonal tile held in Dt (lane i of each 16-lane row = row i)
+    // the 16 x 16 tile at (r0, c0) in C layout: from Hs (first pass) or from W
+    auto tile_ld = [&](bool hs, int r0, int c0, double (&v)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = r0 + lq + 4 * q, c = c0 + lr;
+            v[q] = hs ? hs_ld(r, c, c <= r) : wld(r * (int)LDW + c);
+        }
+    };
+    auto tile_val = [&](bool hs, int r0, int c0, const double (&v)[4]) {
+        double4_t acc;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = r0 + lq + 4 * q, c = c0 + lr;
+            acc[q] = hs ? hs_val(r, c, c <= r, v[q]) : v[q];
+        }
+        return acc;
+    };
+    auto tile_st = [&](int r0, int c0, const double4_t &acc) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) wst((r0 + lq + 4 * q) * (int)LDW + c0 + lr, acc[q]);
+    };
+    auto dt_st = [&](const double4_t &acc) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) Dt[(lq + 4 * q) * 17 + lr] = acc[q];
+    };
+    // acc -= P_I P_J^T for panel cache P (rows ri, cj of the tile pair)
+    auto mm = [&](const double *P, int ri, int cj, double4_t acc) {
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-P[(ri + lr) * 17 + 4 * kk + lq], P[(cj + lr) * 17 + 4 * kk + lq], acc, 0, 0, 0);
+        return acc;
+    };
+    // wave 0: factor + invert the diagonal tile K held in Dt (lane i of each 16-lane row = row i): the
+    // inverse into LKs and Lg, the factor's rows into W
     auto diag = [&](int K) {
-        const int k0 = 16 * K, i = lane & 15;
+        const int k0 = 16 * K, i = lr;
+        lds_wave_sync();
         double row[16], li[16];
 #pragma unroll
         for (int c = 0; c < 16; c++) row[c] = Dt[i * 17 + c];
+        // the unit column formed here, from a value the compiler cannot hoist (hoisted out of the panel
+        // loop, e_i stayed live across it and spilled 145 VGPRs)
+        double one = 1.0;
+        asm volatile("" : "+v"(one));
 #pragma unroll
-        for (int r = 0; r < 16; r++) li[r] = r == i ? 1.0 : 0.0;
+        for (int r = 0; r < 16; r++) li[r] = r == i ? one : 0.0;
         bool bad = false;
         chol16_pipe(row, li, n - k0, bad);
-        double *LK = Linv + K * 16 * 17;
 #pragma unroll
-        for (int r = 0; r < 16; r++) LK[r * 17 + i] = li[r];
-        // the factored tile into W: its row n (when n is not a multiple of 16) is part of y
-        if (lane < 16)
+        for (int r = 0; r < 16; r++) LKs[r * 17 + i] = li[r];
+        if (lane < 16) {
 #pragma unroll
-            for (int c = 0; c < 16; c++) W[(k0 + i) * LDW + k0 + c] = row[c];
+            for (int r = 0; r < 16; r++) wst(LG + K * 256 + r * 16 + i, li[r]);
+#pragma unroll
+            for (int c = 0; c < 16; c++) wst((k0 + i) * (int)LDW + k0 + c, row[c]);
+        }
         if (lane == 0 && bad) fail = 1;
     };
-    // 1. copy: wave 0 builds tile (0, 0) in Dt and factors it; waves 1.. copy the other lower tiles
-    const int ntri = NT * (NT + 1) / 2;
+    // panel of column K: L_IK = A_IK L_KK^-T for tiles I > K (A from Hs in the first pass), into W and P
+    auto panel = [&](int K, bool hs, double *P) {
+        const int k0 = 16 * K;
+        for (int I = K + 1 + wv; I < NT; I += kCW) {
+            const int ri = 16 * I;
+            double a[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const int r = ri + lr, c = k0 + 4 * kk + lq;
+                a[kk] = hs ? hs_ld(r, c, true) : wld(r * (int)LDW + c);
+            }
+            double4_t acc = {0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const double av = hs ? hs_val(ri + lr, k0 + 4 * kk + lq, true, a[kk]) : a[kk];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, LKs[lr * 17 + 4 * kk + lq], acc, 0, 0, 0);
+            }
+            tile_st(ri, k0, acc);
+#pragma unroll
+            for (int q = 0; q < 4; q++) P[(ri + lq + 4 * q) * 17 + lr] = acc[q];
+        }
+    };
+    if (tid == 0) fail = 0;
+    __syncthreads();   // bs in LDS
+    // tile (0, 0) from Hs into Dt, factored by wave 0
     if (wv == 0) {
-        double hb[4][2];
-        const int cc = lane & 15;
-#pragma unroll
-        for (int q = 0; q < 4; q++) sys_ld((lane >> 4) + 4 * q, cc, cc <= (lane >> 4) + 4 * q, hb[q][0], hb[q][1]);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int r = (lane >> 4) + 4 * q;
-            Dt[r * 17 + cc] = cc <= r ? sys_val(r, cc, true, hb[q][0], hb[q][1]) : 0.0;
-        }
-        lds_wave_sync();
+        double v[4];
+        tile_ld(true, 0, 0, v);
+        dt_st(tile_val(true, 0, 0, v));
         diag(0);
-    } else {
-        for (int t0 = wv; t0 < ntri; t0 += 4 * (kCW - 1)) {   // 4 tiles' loads in flight per wave
-            double hb[4][4][2];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int t = t0 + u * (kCW - 1);
-                int I = 0, J = 0;
-                if (t < ntri) tile_of(t, I, J);
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int r = 16 * I + (lane >> 4) + 4 * q, c = 16 * J + (lane & 15);
-                    sys_ld(r, c, t > 0 && t < ntri && c <= r, hb[u][q][0], hb[u][q][1]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int t = t0 + u * (kCW - 1);
-                if (t <= 0 || t >= ntri) continue;
-                int I, J;
-                tile_of(t, I, J);
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int r = 16 * I + (lane >> 4) + 4 * q, c = 16 * J + (lane & 15);
-                    W[r * LDW + c] = sys_val(r, c, c <= r, hb[u][q][0], hb[u][q][1]);
-                }
-            }
-        }
     }
     __syncthreads();
-    for (int K = 0; K < NT; K++) {
+#ifdef LBA_PROFILE
+    tgf = clock64() - tg0;
+    tgx = clock64();
+#endif
+    // one pass over columns K, K + 1; hs: the first pass, A from the handed-over system. Returns 1 when the factorization is complete, -1 on a non-positive pivot.
+    auto pass = [&](int K, bool hs) -> int {
+        {   // the lane indices re-derived from an opaque copy: the offsets built from them are formed per pass
+            // instead of hoisted out of the loop and kept live (spilled) across it
+            int l = lane;
+            asm volatile("" : "+v"(l));
+            lr = l & 15;
+            lq = l >> 4;
+        }
+        panel(K, hs, Pc0);   // (B)
+        __syncthreads();
+        LBA_TG(tgb);
+        if (K + 1 >= NT) return 1;
+        {   // (C) column K + 1 by panel K: wave 0 the diagonal tile (into Dt, factored), the others the rest
+            const int k1 = 16 * (K + 1);
+            for (int I = K + 1 + wv; I < NT; I += kCW) {
+                const int ri = 16 * I;
+                double v[4];
+                tile_ld(hs, ri, k1, v);
+                const double4_t acc = mm(Pc0, ri, k1, tile_val(hs, ri, k1, v));
+                if (I == K + 1) dt_st(acc);
+                else tile_st(ri, k1, acc);
+            }
+            if (wv == 0) diag(K + 1);
+        }
+        __syncthreads();
+        LBA_TG(tgc);
+        if (fail) return -1;
+        panel(K + 1, false, Pc1);   // (D)
+        __syncthreads();
+        LBA_TG(tgd);
+        const int m = NT - K - 2;
+        if (m <= 0) return 1;
+        // (E) the trailing tiles (I, J), K + 2 <= J <= I: tile 0 = (K + 2, K + 2) -> wave 0 (Dt, factored),
+        // the others -> waves 1.., four tiles' loads in flight per batch
+        const int r0 = 16 * (K + 2);
+        if (wv == 0) {
+            double v[4];
+            tile_ld(hs, r0, r0, v);
+            dt_st(mm(Pc1, r0, r0, mm(Pc0, r0, r0, tile_val(hs, r0, r0, v))));
+            diag(K + 2);
+        } else {
+            const int ntile = m * (m + 1) / 2;
+            auto tile_of = [](int t, int &I, int &J) {   // lower tile t of the triangle (row-major, I >= J)
+                int i = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+                if ((i + 1) * (i + 2) / 2 <= t) i++;
+                if (i * (i + 1) / 2 > t) i--;
+                I = i;
+                J = t - i * (i + 1) / 2;
+            };
+            // four tiles' loads in flight per wave: six or eight measured slower (E 354k -> 368k / 380k cycles
+            // at 6P = 384, profiles/r06_lbaprof_global_*.txt); so did rows of four tiles per wave sharing their
+            // A fragments (485k: fewer tiles in flight)
+            constexpr int TB = 4;
+            for (int t0 = wv; t0 < ntile; t0 += TB * (kCW - 1)) {
+                double v[TB][4];
+                int It[TB], Jt[TB];
+#pragma unroll
+                for (int u = 0; u < TB; u++) {
+                    const int t = t0 + u * (kCW - 1);
+                    It[u] = Jt[u] = 0;
+                    if (t < ntile) tile_of(t, It[u], Jt[u]);
+                    tile_ld(hs && t < ntile, r0 + 16 * It[u], r0 + 16 * Jt[u], v[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < TB; u++) {
+                    const int t = t0 + u * (kCW - 1);
+                    if (t >= ntile) continue;
+                    const int ri = r0 + 16 * It[u], cj = r0 + 16 * Jt[u];
+                    tile_st(ri, cj, mm(Pc1, ri, cj, mm(Pc0, ri, cj, tile_val(hs, ri, cj, v[u]))));
+                }
+            }
+        }
+        __syncthreads();
+        LBA_TG(tge);
+        return 0;
+    };
+    for (int K = 0;; K += 2) {
         if (fail) {   // uniform after the barrier
             if (tid == 0) g.scalars[4] = 0;
             return;
         }
-        const int k0 = 16 * K, r0 = k0 + 16, m = NT - K - 1;
-        const double *LK = Linv + K * 16 * 17;
-        // 2. panel: L_IK = A_IK L_KK^-T into W and Pc (rows r0 ..)
-        for (int I = wv; I < m; I += kCW) {
-            const int ri = r0 + 16 * I;
-            double a[4];
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++) a[kk] = W[(ri + (lane & 15)) * LDW + k0 + 4 * kk + (lane >> 4)];
-            double4_t acc = {0, 0, 0, 0};
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kk], LK[(lane & 15) * 17 + 4 * kk + (lane >> 4)], acc, 0, 0, 0);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int r = ri + (lane >> 4) + 4 * q;
-                W[r * LDW + k0 + (lane & 15)] = acc[q];
-                Pc[r * 17 + (lane & 15)] = acc[q];
-            }
+        const int st = pass(K, K == 0);
+        if (st < 0) {
+            if (tid == 0) g.scalars[4] = 0;
+            return;
         }
-        __syncthreads();
-        if (m == 0) break;
-        // 3. trailing lower tiles of the m x m tile triangle below / right of panel K: tile 0 = (K + 1,
-        // K + 1) -> wave 0 (into Dt, then its factor), the others -> waves 1.., four tiles per batch
-        const int ntile = m * (m + 1) / 2;
-        auto upd = [&](int I, int J, double4_t acc) {
-            const int ri = r0 + 16 * I, cj = r0 + 16 * J;
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Pc[(ri + (lane & 15)) * 17 + 4 * kk + (lane >> 4)],
-                                                           Pc[(cj + (lane & 15)) * 17 + 4 * kk + (lane >> 4)], acc, 0, 0, 0);
-            return acc;
-        };
-        if (wv == 0) {
-            double4_t acc;
-#pragma unroll
-            for (int q = 0; q < 4; q++) acc[q] = W[(r0 + (lane >> 4) + 4 * q) * LDW + r0 + (lane & 15)];
-            acc = upd(0, 0, acc);
-#pragma unroll
-            for (int q = 0; q < 4; q++) Dt[((lane >> 4) + 4 * q) * 17 + (lane & 15)] = acc[q];
-            lds_wave_sync();
-            diag(K + 1);
-        } else {
-            for (int t0 = wv; t0 < ntile; t0 += 4 * (kCW - 1)) {
-                double4_t acc[4];
-                int It[4], Jt[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int t = t0 + u * (kCW - 1);
-                    It[u] = Jt[u] = 0;
-                    if (t < ntile) tile_of(t, It[u], Jt[u]);
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        acc[u][q] = t < ntile ? W[(r0 + 16 * It[u] + (lane >> 4) + 4 * q) * LDW + r0 + 16 * Jt[u] + (lane & 15)] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int t = t0 + u * (kCW - 1);
-                    if (t >= ntile) continue;
-                    const double4_t o = upd(It[u], Jt[u], acc[u]);
-#pragma unroll
-                    for (int q = 0; q < 4; q++) W[(r0 + 16 * It[u] + (lane >> 4) + 4 * q) * LDW + r0 + 16 * Jt[u] + (lane & 15)] = o[q];
-                }
-            }
-        }
-        __syncthreads();
+        if (st > 0) break;
     }
-    // 4. back substitution L^T x = y (chol_tiled_body's, the row updates reading W)
-    for (int j = tid; j < N2; j += kCT) yv[j] = j < n ? W[n * LDW + j] : 0.0;
+#ifdef LBA_PROFILE
+    const long long tg2 = clock64();
+    long long tgs1 = 0;
+#endif
+    // back substitution L^T x = y (chol_tiled_body's): the inverses back into LDS (over the panel copies)
+    double *Linv = A;
+    for (int e = tid; e < NT * 256; e += kCT) {
+        const int K = e >> 8, r = (e >> 4) & 15, c = e & 15;
+        Linv[K * 272 + r * 17 + c] = wld(LG + e);
+    }
+    for (int j = tid; j < N2; j += kCT) yv[j] = j < n ? wld(n * (int)LDW + j) : 0.0;
     __syncthreads();
     auto x_block = [&](int K) {
         const int k0 = 16 * K;
-        const double *LK = Linv + K * 16 * 17;
-        const int c = lane & 15, p4 = 4 * (lane >> 4);
+        const double *LK = Linv + K * 272;
+        const int c = lr, p4 = 4 * lq;
         double s = 0.0;
 #pragma unroll
         for (int r = 0; r < 4; r++) s += LK[(p4 + r) * 17 + c] * yv[k0 + p4 + r];
         s = rows4_sum(s);
         if (lane < 16) xv[k0 + c] = s;
     };
-    auto y_update = [&](int k0, int j, int q4) {
+    // y_j -= L_K^T x_K by the 4 lanes of a quad; the W values of the row (loaded a block ahead)
+    auto y_apply = [&](int k0, int j, int q4, const double (&wr)[4]) {
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) s += W[(k0 + q4 + k) * LDW + j] * xv[k0 + q4 + k];
+        for (int k = 0; k < 4; k++) s += wr[k] * xv[k0 + q4 + k];
         s = quad_sum(s);
         if ((lane & 3) == 0) yv[j] -= s;
     };
+    auto w_ld = [&](int k0, int j, int q4, bool ok, double (&wr)[4]) {
+#pragma unroll
+        for (int k = 0; k < 4; k++)   // !ok: an offset past the descriptor's end (the load returns 0), no branch
+            wr[k] = wld(((k0 + q4 + k) * (int)LDW + j) | (ok ? 0 : 0x08000000));
+    };
     {
-        int K = (n - 1) / 16;
-        if (wv == 0) x_block(K);
-        __syncthreads();
-        for (; K > 0; K--) {
+        constexpr int NJ = 3;   // rows per thread of waves 1..15: (kBigNP + 15) / 240 + 1
+        static_assert((kCT - 64) / 4 * NJ >= kBigNP + 16, "rows of the back substitution");
+        const int q4w = 4 * (lane & 3), q4o = 4 * (tid & 3), j0 = (tid - 64) >> 2;
+        const int K0 = (n - 1) / 16;
+        struct WRows { double v[NJ][4]; };   // the W rows one block's update reads (a value: stays in registers)
+        auto issue = [&](int K) __attribute__((always_inline)) {
+            WRows wr;
+            if (K <= 0) return wr;
+            const int k0 = 16 * K, kp = k0 - 16;
+            if (wv == 0) w_ld(k0, kp + (lane >> 2), q4w, true, wr.v[0]);
+            else
+#pragma unroll
+                for (int u = 0; u < NJ; u++) w_ld(k0, j0 + 240 * u, q4o, j0 + 240 * u < kp, wr.v[u]);
+            return wr;
+        };
+        // block K (x_K published): rows of block K - 1 and x_{K-1} by wave 0, the rows above by the others
+        auto step = [&](int K, WRows wr) __attribute__((always_inline)) {
             const int k0 = 16 * K, kp = k0 - 16;
             if (wv == 0) {
-                y_update(k0, kp + (lane >> 2), 4 * (lane & 3));
+                y_apply(k0, kp + (lane >> 2), q4w, wr.v[0]);
                 lds_wave_sync();
                 x_block(K - 1);
             } else {
-                for (int j = (tid - 64) >> 2; j < kp; j += (kCT - 64) / 4) y_update(k0, j, 4 * (tid & 3));
+#pragma unroll
+                for (int u = 0; u < NJ; u++)
+                    if (j0 + 240 * u < kp) y_apply(k0, j0 + 240 * u, q4o, wr.v[u]);
             }
-            __syncthreads();
+            // LDS-only barrier: __syncthreads() would also wait for the next block's W loads in flight
+            // (vmcnt counts loads and stores alike); the solve reads W only, so LDS order is all it needs
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        };
+        WRows wa = issue(K0);
+        if (wv == 0) x_block(K0);
+        __syncthreads();
+#ifdef LBA_PROFILE
+        tgs1 = clock64();
+#endif
+        // two blocks per iteration, the next block's rows loading while this one's are applied
+        for (int K = K0; K > 0; K -= 2) {
+            const WRows wb = issue(K - 1);
+            step(K, wa);
+            if (K - 1 <= 0) break;
+            wa = issue(K - 2);
+            step(K - 1, wb);
         }
     }
+#ifdef LBA_PROFILE
+    const long long tgs2 = clock64();
+#endif
     for (int j = tid; j < n; j += kCT) g.x[j] = xv[j];
     const bool cur = g.lm->cur;
     for (int t = tid; t < g.P; t += kCT) trial_pose(g, cur, t, (cur ? g.T2 : g.T)[g.hpose[t]], xv);
     if (tid == 0) g.scalars[4] = 1;
+#ifdef LBA_PROFILE
+    if (tid == 0)
+        printf("LBAPROFG n=%d diag0=%lld B=%lld C=%lld D=%lld E=%lld solve=%lld (setup %lld loop %lld poses %lld) total=%lld\n", n,
+               tgf, tgb, tgc, tgd, tge, clock64() - tg2, tgs1 - tg2, tgs2 - tgs1, clock64() - tgs2, clock64() - tg0);
+#endif
+#undef LBA_TG
 }
 
 __global__ __launch_bounds__(kCT) void lba_chol_global(Graph g) { chol_global_body<false>(g, 0); }
@@ -2449,7 +2571,7 @@ int lba_solve(lba_engine *e, const lba_problem *p, lba_result *r, const volatile
         g.LDW = 0;
         if (6 * A.P > kSmallNP && 6 * A.P <= kBigNP) {   // chol_global_body's work matrix (fully rewritten per trial)
             const int N2 = chol_tiled_dim(6 * A.P);
-            if (e->Wm.ensure(sizeof(double) * (size_t)N2 * N2)) return -1;
+            if (e->Wm.ensure(sizeof(double) * chol_global_w(6 * A.P))) return -1;
             g.W = e->Wm.as<double>();
             g.LDW = N2;
         }

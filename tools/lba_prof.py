@@ -1,4 +1,4 @@
-"""LocalBA C4 profiling driver: N calls of LocalBundleAdjustment on the synthetic 20 KF x 3000 MP
+"""LocalBA C4 profiling driver (or a larger window: [calls seed n_kf n_points]): N calls of LocalBundleAdjustment on the synthetic 20 KF x 3000 MP
 graph (bench.py's localba leg without the rest), wall time per call. Run under rocprofv3
 --kernel-trace --stats (per-kernel device time) or --pmc (MFMA counters).
     python tools/lba_prof.py [calls]"""
@@ -13,7 +13,8 @@ import orbslam2_amd as amd  # noqa: E402
 from orbslam2_amd import synth  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-prob = synth.localba_problem(seed=4)
+# optional: seed n_kf n_points (a larger window, e.g. 12 64 6000)
+prob = synth.localba_problem(*(int(a) for a in sys.argv[2:5])) if len(sys.argv) > 4 else synth.localba_problem(seed=4)
 lba = amd.LocalBundleAdjustment()
 for _ in range(2):
     r = lba.solve(prob)
