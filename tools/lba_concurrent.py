@@ -17,17 +17,17 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "orb-slam2-noted_amd" / "python"))
 sys.path.insert(0, str(ROOT))
-import bench  # noqa: E402  (GPU_MAX_HW_QUEUES as bench.py sets it)
-import torch  # noqa: E402
-
-torch.cuda.init()
-import orbslam2_amd as amd  # noqa: E402
 from orbslam2_amd import synth  # noqa: E402
 
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    # the stream first: its worker processes must not inherit or open the GPU
     pool = synth.stereo_stream(376, 1241, 512)
+    import bench  # GPU_MAX_HW_QUEUES as bench.py sets it, before the runtime starts
+    import torch
+    torch.cuda.init()
+    import orbslam2_amd as amd
     buf = bench.c2_stream_buffer(pool)
     mb = float(np.float32(386.1448) / np.float32(718.856))
     B = 384
