@@ -674,9 +674,13 @@ int lba_set_stop_hook(lba_engine *e, int phase, int trial);
  *                        bit-identical results (tests/test_lba_gpu.py).
  *   LBA_OPT_SPIN_LIMIT   the in-launch hand-off wait's poll bound; < 0: the default (~1 s); 0: every
  *                        wait times out (fault injection). A timed-out wait ends the optimisation and
- *                        lba_solve returns ORBX_EDEVICE. */
+ *                        lba_solve returns ORBX_EDEVICE.
+ *   LBA_OPT_STREAM_PRIORITY  the engine's stream recreated at the device's lowest (0) or highest (1,
+ *                        the default) stream priority (LocalBA beside a saturating extraction stream,
+ *                        DESIGN §5). */
 #define LBA_OPT_FUSE_FINISH 1
 #define LBA_OPT_SPIN_LIMIT 2
+#define LBA_OPT_STREAM_PRIORITY 3
 int lba_set_test_option(lba_engine *e, int option, long long value);
 /* Per-kernel hipEvent timing of lba_solve's trial chain on the engine stream (bench.py localba
  * roofline); same semantics as orbx_profile / orbx_profile_read. */

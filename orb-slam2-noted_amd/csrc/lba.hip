@@ -2380,7 +2380,12 @@ int lba_create(lba_engine **out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORBX_EDEVICE;
     lba_engine *e = new lba_engine();
-    if (hipGetDevice(&e->device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+    // the engine stream at the device's highest priority: LocalMapping's LocalBA beside Tracking's
+    // extraction (Frame.cc:144-153 on other threads) -- beside a saturating C2 stream 34 -> 8.7 ms per
+    // call (profiles/r06_lba_concurrent.log); alone no difference
+    int prio_least = 0, prio_greatest = 0;
+    if (hipGetDevice(&e->device) != hipSuccess || hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
         hipHostMalloc((void **)&e->h_scalars, (8 + 2 * kRedBlocks) * sizeof(double)) != hipSuccess ||
         hipHostMalloc((void **)&e->h_lm, 2 * sizeof(LMState)) != hipSuccess ||
         hipHostMalloc((void **)&e->h_stop, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -2749,6 +2754,17 @@ int lba_set_test_option(lba_engine *e, int option, long long value) {
     if (!e) return ORBX_EINVAL;
     switch (option) {
         case LBA_OPT_FUSE_FINISH: e->fuse_finish = value != 0; return ORBX_OK;
+        case LBA_OPT_STREAM_PRIORITY: {   // the engine stream recreated at the device's lowest (0) / highest (1) priority
+            int least = 0, greatest = 0;
+            if (hipSetDevice(e->device) != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess ||
+                hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+                return ORBX_EDEVICE;
+            hipStream_t ns = nullptr;
+            if (hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, value ? greatest : least) != hipSuccess) return ORBX_EDEVICE;
+            (void)hipStreamDestroy(e->stream);
+            e->stream = ns;
+            return ORBX_OK;
+        }
         case LBA_OPT_SPIN_LIMIT:   // < 0: the default; 0: every hand-off wait times out (fault injection)
             if (value > 0xFFFFFFFFLL) return ORBX_EINVAL;
             e->spin_limit = value < 0 ? kSpinLimit : (unsigned)value;

@@ -715,6 +715,7 @@ class LocalBundleAdjustment:
 
     LBA_OPT_FUSE_FINISH = 1
     LBA_OPT_SPIN_LIMIT = 2
+    LBA_OPT_STREAM_PRIORITY = 3
 
     def set_test_option(self, option: int, value: int):
         """lba_set_test_option: LBA_OPT_FUSE_FINISH (1 fused, 0 two launches) or LBA_OPT_SPIN_LIMIT

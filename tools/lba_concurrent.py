@@ -59,9 +59,11 @@ def main():
 
 
     res = []
+    settings = [(1, 0), (0, 0), (1, 1)]   # (fused finish, high stream priority)
     for r in range(rounds):
-        for fused in (1, 0):
+        for fused, prio in settings:
             lba.set_test_option(lba.LBA_OPT_FUSE_FINISH, fused)
+            lba.set_test_option(lba.LBA_OPT_STREAM_PRIORITY, prio)
             alone = []
             lba_calls(alone)
             both, cnt, flag = [], [], threading.Event()
@@ -73,15 +75,15 @@ def main():
             flag.set()
             th.join()
             el = time.perf_counter() - t0
-            row = {"round": r, "fused": fused, "lba_ms_alone": round(alone[0] * 1e3, 4),
+            row = {"round": r, "fused": fused, "high_priority": prio, "lba_ms_alone": round(alone[0] * 1e3, 4),
                    "lba_ms_beside_c2": round(both[0] * 1e3, 4), "c2_frames_per_s_beside_lba": round(cnt[0] * B / el, 1)}
             res.append(row)
             print(json.dumps(row), flush=True)
     lba.set_test_option(lba.LBA_OPT_FUSE_FINISH, 1)
-    for fused in (1, 0):
-        sel = [x for x in res if x["fused"] == fused]
-        print("SUMMARY fused=%d lba alone %.4f ms, beside C2 %.4f ms, C2 %.0f frames/s" % (
-            fused, np.mean([x["lba_ms_alone"] for x in sel]), np.mean([x["lba_ms_beside_c2"] for x in sel]),
+    for fused, prio in settings:
+        sel = [x for x in res if x["fused"] == fused and x["high_priority"] == prio]
+        print("SUMMARY fused=%d high_priority=%d lba alone %.4f ms, beside C2 %.4f ms, C2 %.0f frames/s" % (
+            fused, prio, np.mean([x["lba_ms_alone"] for x in sel]), np.mean([x["lba_ms_beside_c2"] for x in sel]),
             np.mean([x["c2_frames_per_s_beside_lba"] for x in sel])))
 
 
