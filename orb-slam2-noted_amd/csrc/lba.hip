@@ -1520,9 +1520,11 @@ template <bool HANDOFF> __device__ __forceinline__ void chol_global_body(Graph &
                 for (int u = 0; u < NJ; u++)
                     if (j0 + 240 * u < kp) y_apply(k0, j0 + 240 * u, q4o, wr.v[u]);
             }
-            // LDS-only barrier: __syncthreads() would also wait for the next block's W loads in flight
-            // (vmcnt counts loads and stores alike); the solve reads W only, so LDS order is all it needs
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            // LDS-only barrier (fences scoped to LDS): __syncthreads() would also wait for the next
+            // block's W loads in flight (vmcnt counts loads and stores alike); the solve reads W only
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         };
         WRows wa = issue(K0);
         if (wv == 0) x_block(K0);
