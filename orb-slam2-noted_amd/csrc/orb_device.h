@@ -81,32 +81,29 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {
     return a;
 }
 
-struct SinCosTab {
-    double sign[4];
-    double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
+// glibc's sincosf table (__sincosf_table, sincosf.h) as immediates: entry 1 is entry 0 with the cosine
+// coefficients c0..c4 negated, and since negation is exact and round-to-nearest is sign-symmetric,
+// the cosine polynomial on entry 1 is exactly the negated one on entry 0. No table in memory: a vector
+// load of the table (its index is per lane) made every caller wait vmcnt(0) for all its loads in flight.
+struct SinCosK {
+    static constexpr double hpi_inv = 0x1.45F306DC9C883p+23, hpi = 0x1.921FB54442D18p0;
+    static constexpr double c0 = 0x1p0, c1 = -0x1ffffffd0c621cp-54, c2 = 0x1.55553e1068f19p-5, c3 = -0x1.6c087e89a359dp-10,
+                            c4 = 0x1.99343027bf8c3p-16;
+    static constexpr double s1 = -0x1.555545995a603p-3, s2 = 0x1.1107605230bc4p-7, s3 = -0x1.994eb3774cf24p-13;
 };
-
-static __constant__ SinCosTab kSinCosTab[2] = {
-    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0,
-     -0x1ffffffd0c621cp-54, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10,
-     0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7,
-     -0x1.994eb3774cf24p-13},
-    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0,
-     0x1ffffffd0c621cp-54, -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10,
-     -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7,
-     -0x1.994eb3774cf24p-13}};
-
-__device__ __forceinline__ const SinCosTab &sincos_tab(int i) { return kSinCosTab[i]; }
 
 __device__ __forceinline__ uint32_t abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
 
-__device__ __forceinline__ float sc_poly(double x, double x2, const SinCosTab &p, int n) {
+// glibc's sinf_poly: n even -> the sine polynomial, odd -> the cosine polynomial (of table entry 0;
+// entry 1's is its negation, applied by the caller)
+__device__ __forceinline__ float sc_poly(double x, double x2, int n) {
+    using K = SinCosK;
     if ((n & 1) == 0) {
-        double x3 = x * x2, s1 = p.s2 + x2 * p.s3, x7 = x3 * x2, s = x + x3 * p.s1;
+        double x3 = x * x2, s1 = K::s2 + x2 * K::s3, x7 = x3 * x2, s = x + x3 * K::s1;
         return (float)(s + x7 * s1);
     }
-    double x4 = x2 * x2, c2 = p.c3 + x2 * p.c4, c1 = p.c0 + x2 * p.c1, x6 = x4 * x2;
-    double c = c1 + x4 * p.c2;
+    double x4 = x2 * x2, c2 = K::c3 + x2 * K::c4, c1 = K::c0 + x2 * K::c1, x6 = x4 * x2;
+    double c = c1 + x4 * K::c2;
     return (float)(c + x6 * c2);
 }
 
@@ -116,19 +113,18 @@ __device__ __forceinline__ void glibc_sincosf(float y, float *s_out, float *c_ou
     const float pio4 = 0x1.921FB6p-1f;
     if (abstop12(y) < abstop12(pio4)) {
         if (abstop12(y) < abstop12(0x1p-12f)) { *c_out = 1.0f; *s_out = y; return; }
-        const SinCosTab &p = sincos_tab(0);
-        *c_out = sc_poly(x, x * x, p, 1);
-        *s_out = sc_poly(x, x * x, p, 0);
+        *c_out = sc_poly(x, x * x, 1);
+        *s_out = sc_poly(x, x * x, 0);
         return;
     }
-    const SinCosTab &p0 = sincos_tab(0);
-    double r = x * p0.hpi_inv;
+    double r = x * SinCosK::hpi_inv;
     int n = ((int32_t)r + 0x800000) >> 24;
-    x = x - n * p0.hpi;
-    double s = p0.sign[n & 3];
-    const SinCosTab &p = sincos_tab((n & 2) ? 1 : 0);
-    *c_out = sc_poly(x * s, x * x, p, n ^ 1);
-    *s_out = sc_poly(x * s, x * x, p, n);
+    x = x - n * SinCosK::hpi;
+    const double s = ((n ^ (n >> 1)) & 1) ? -1.0 : 1.0;   // glibc's sign[n & 3] = {1, -1, -1, 1}
+    const bool neg = (n & 2) != 0;                        // table entry 1: its cosine polynomial negated
+    const float cv = sc_poly(x * s, x * x, n ^ 1), sv = sc_poly(x * s, x * x, n);
+    *c_out = (neg && ((n ^ 1) & 1)) ? -cv : cv;
+    *s_out = (neg && (n & 1)) ? -sv : sv;
 }
 
 // Packed candidate key: score (8b) | x (12b) << 8 | y (12b) << 20, x/y relative to

@@ -22,14 +22,20 @@ namespace orbamd {
 
 static __constant__ __attribute__((aligned(16))) int8_t c_pattern[1024];  // bit_pattern_31_ (ORBextractor.cc:209-467) as data
 static __constant__ int c_umax[16];
-// IC_Angle byte weights per (|v|, dword w) of the row segment u = 4w-16 .. 4w-13:
-// x = (u + 16) where |u| <= umax[|v|] else 0, y = 1 / 0 mask (built from umax on the host)
-static __constant__ uint2 c_icw[16 * 8];
-// describe2_kernel's steered-BRIEF patch loads (lanes 0..59: row lane / 10 + 6 k, dword lane % 10 of
-// the 40-byte aligned row window): bit 7 p + k of lane l = the dword can hold a pixel some rotation of
-// the pattern samples when the window starts p = 0..3 bytes before the patch (built on the host from
-// bit_pattern_31_'s radius, orbx_create); the others are not loaded
-static __constant__ uint32_t c_pmask[64];
+// describe2_kernel's per-lane constants (built on the host, orbx_create), one 48-byte load per lane:
+//  * wt[k]: IC_Angle byte weights of the lane's row v = lane / 8 - 15 + 8 k, dword w = lane % 8 (the
+//    row segment u = 4w-16 .. 4w-13): x = (u + 16) where |u| <= umax[|v|] else 0, y = 1 / 0 mask;
+//  * pmask: the steered-BRIEF patch loads (lanes 0..59: row lane / 10 + 6 k, dword lane % 10 of the
+//    40-byte aligned row window): bit 7 p + k = the dword can hold a pixel some rotation of the
+//    pattern samples when the window starts p = 0..3 bytes before the patch (from bit_pattern_31_'s
+//    radius); the others are not loaded.
+// One table, so pmask arrives with the weights the first IC_Angle loads already wait for (a separate
+// constant load was sunk to its first use and waited vmcnt(0) behind every load in flight there)
+struct DescLane {
+    uint2 wt[4];
+    uint32_t pmask, pad[3];
+};
+static __constant__ __attribute__((aligned(16))) DescLane c_dlane[64];
 
 #define HIPCHK(x)                                                                   \
     do {                                                                            \
@@ -1584,12 +1590,11 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     // IC_Angle byte weights of the lane's four rows (the same for every slot): issued first, with
     // the slot loads, instead of after each slot's rows
     const int w8 = lane & 7, vr = lane >> 3;
+    const DescLane dl = c_dlane[lane];
     uint2 wt[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int v = vr - 15 + 8 * k;
-        wt[k] = (k < 3 || vr <= 6) ? c_icw[(v < 0 ? -v : v) * 8 + w8] : make_uint2(0u, 0u);
-    }
+    for (int k = 0; k < 4; k++) wt[k] = dl.wt[k];
+    const uint32_t pmask = dl.pmask;
     // 1. lane k < L: selected keypoints of level k; lane r < NS: slot s0 + r
     const int scl = lane < L ? sel_cnt[(long long)b * L + lane] : 0;
     const int slot = s0 + lane;
@@ -1652,7 +1657,10 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void *)rl64(icb, r), 0, __builtin_amdgcn_readlane(icn, r), 0x00020000);
         const int pr = __builtin_amdgcn_readlane(pitch, r);
-        const int vo = vr * pr + 4 * w8;
+        // 24-bit multiply-add: a plain int multiply-add became v_mad_u64_u32 with an undefined high
+        // addend register that aliased a load destination of the previous slot, so every slot waited
+        // vmcnt(0) for the previous one's rows
+        const int vo = (int)__umul24((unsigned)vr, (unsigned)pr) + 4 * w8;
 #pragma unroll
         for (int k = 0; k < 4; k++)   // a dword with no pixel inside the umax circle has weight 0
             if ((k < 3 || vr <= 6) && wt[k].y != 0u) P[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 8 * k * pr, 0);
@@ -1660,7 +1668,6 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
     // steered-BRIEF patch of slot r (rows y-18 .. y+18, bytes x-18 .. x+21 as 10 aligned dwords
     // per row; lanes 0..59 -> (row lane / 10, dword lane % 10), six rows per pass) into registers
     const int rr0 = (lane * 205) >> 11, q10 = lane - 10 * rr0;
-    const uint32_t pmask = c_pmask[lane];
     constexpr int TK = 7;   // patch registers per slot and lane
     uint32_t T[NB][G][TK];   // NB groups' patches in flight (prefetch distance NB)
     auto issue_patch = [&](int gi, uint32_t (&dst)[G][TK]) {
@@ -1674,7 +1681,7 @@ __global__ __launch_bounds__(256) void describe2_kernel(ExtractGeom g, const uin
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc((void *)(blur + (long long)rl64((unsigned long long)a0, r)), 0,
                                                   __builtin_amdgcn_readlane(bln, r), 0x00020000);
-            const int vo = rr0 * bwr + 4 * q10;
+            const int vo = (int)__umul24((unsigned)rr0, (unsigned)bwr) + 4 * q10;
             const uint32_t pm = pmask >> (7 * __builtin_amdgcn_readlane(psh, r));
             if (lane < 60) {
 #pragma unroll
@@ -2215,10 +2222,18 @@ int orbx_create(const orbx_params *p, orbx_engine **out) {
             }
         }
     }
+    DescLane dlane[64] = {};
+    for (int l = 0; l < 64; l++) {
+        const int w8 = l & 7, vr = l >> 3;
+        for (int k = 0; k < 4; k++) {
+            const int v = vr - 15 + 8 * k;
+            if (k < 3 || vr <= 6) dlane[l].wt[k] = icw[std::abs(v) * 8 + w8];
+        }
+        dlane[l].pmask = pmask[l];
+    }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), e->pattern, 1024) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_pmask), pmask, sizeof(pmask)) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(c_umax), e->umax, sizeof(e->umax)) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_icw), icw, sizeof(icw)) != hipSuccess) {
+        hipMemcpyToSymbol(HIP_SYMBOL(c_dlane), dlane, sizeof(dlane)) != hipSuccess) {
         (void)hipEventDestroy(e->done);
         (void)hipStreamDestroy(e->stream);
         delete e;
