@@ -215,7 +215,7 @@ struct orbm_matcher {
     hipEvent_t done = nullptr;
     hipStream_t done_stream = nullptr;
     orbamd::DevBuf q, db, off, idx, out;                                    // Hamming scans
-    orbamd::DevBuf kun, desc, cnt, keys, nkeys, prev, m12, nmatch, list, lcnt;   // SearchForInitialization
+    orbamd::DevBuf kun, desc, cnt, keys, nkeys, cstart, prev, m12, nmatch, list, lcnt;   // SearchForInitialization
 };
 
 namespace orbamd {

@@ -33,6 +33,7 @@ using namespace orbamd;
 namespace orbframe {
 
 constexpr int GRID_COLS = 64, GRID_ROWS = 48;   // Frame.h:55-60
+constexpr int GRID_CELLS = GRID_COLS * GRID_ROWS;
 // LDS of one search_init_resolve_kernel workgroup: list stage + per-F1 prefix + vMatchedDistance /
 // v21 / M12 (u16) + rotation bins (i8). 64 KB holds a 4096-keypoint frame (fixed part 45,076 B,
 // stage 5,115 entries >= cap0); two workgroups still fit a CU's 160 KB.
@@ -91,9 +92,12 @@ struct GridParams {
 };
 
 // Per frame: keys (cell << 16 | index) of keypoints that fall in the grid, sorted -> the
-// candidate order of GetFeaturesInArea (ix, then iy, then insertion order).
+// candidate order of GetFeaturesInArea (ix, then iy, then insertion order) -- and the first key
+// position of every cell (cstart[c], c = ix * GRID_ROWS + iy; cstart[GRID_CELLS] = the valid key
+// count), so a column's cell range [iy0, iy1] is keys [cstart[ix R + iy0], cstart[ix R + iy1 + 1])
+// in two loads (a binary search over the keys was ~10 dependent global loads per bound).
 __global__ __launch_bounds__(256) void grid_sort_kernel(GridParams gp, const orbx_kp *kun, const int *cnt,
-                                                        int cap, int sort_cap, uint32_t *keys, int *nkeys) {
+                                                        int cap, int sort_cap, uint32_t *keys, int *nkeys, int *cstart) {
     extern __shared__ uint32_t sk[];
     const int b = blockIdx.x;
     const int n = min(cnt[b], cap);
@@ -125,22 +129,20 @@ __global__ __launch_bounds__(256) void grid_sort_kernel(GridParams gp, const orb
     if (threadIdx.x == 0) valid = 0;
     __syncthreads();
     int mine = 0;
-    for (int i = threadIdx.x; i < sort_cap; i += 256) {
-        keys[(long long)b * sort_cap + i] = sk[i];
-        mine += sk[i] != 0xFFFFFFFFu;
+    int *cs = cstart + (long long)b * (GRID_CELLS + 1);
+    for (int i = threadIdx.x; i <= sort_cap; i += 256) {
+        // cells (cell of key i - 1, cell of key i] start at i (invalid keys: cell GRID_CELLS)
+        const int c1 = i < sort_cap ? min((int)(sk[i] >> 16), GRID_CELLS) : GRID_CELLS;
+        const int c0 = i > 0 ? min((int)(sk[i - 1] >> 16), GRID_CELLS) : -1;
+        for (int c = c0 + 1; c <= c1; c++) cs[c] = i;
+        if (i < sort_cap) {
+            keys[(long long)b * sort_cap + i] = sk[i];
+            mine += sk[i] != 0xFFFFFFFFu;
+        }
     }
     atomicAdd(&valid, mine);
     __syncthreads();
     if (threadIdx.x == 0) nkeys[b] = valid;
-}
-
-__device__ inline int lower_bound_u32(const uint32_t *a, int n, uint32_t v) {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int m = (lo + hi) >> 1;
-        if (a[m] < v) lo = m + 1; else hi = m;
-    }
-    return lo;
 }
 
 
@@ -165,6 +167,7 @@ struct SearchArgs {
     int cap, sort_cap, cap0;   // cap0: level-0 keypoint capacity (list length bound)
     const uint32_t *keys;      // grid-sorted keys per image
     const int *nkeys;
+    const int *cstart;         // per image: first key of every grid cell (GRID_CELLS + 1)
     GridParams gp;
     float r, nnratio;
     int check_ori;
@@ -204,18 +207,15 @@ __global__ __launch_bounds__(256) void search_init_cand_kernel(SearchArgs a, con
         if (lane == 0) *cnt_out = 0;
         return;
     }
-    const int nk = a.nkeys[i2img];
     const uint32_t *sk = a.keys + (long long)i2img * a.sort_cap;
+    const int *cs = a.cstart + (long long)i2img * (GRID_CELLS + 1);
     int *run_pre = run_pre_s[wv], *run_lo = run_lo_s[wv];
     const int nx = nMaxCellX - nMinCellX + 1;
     int len = 0, lo = 0;
-    if (lane < nx) {
+    if (lane < nx) {   // column ix, cells nMinCellY .. nMaxCellY: one key range
         const int ix = nMinCellX + lane;
-        const uint32_t k0 = (uint32_t)(ix * GRID_ROWS + nMinCellY) << 16;
-        const uint32_t k1 = ((uint32_t)(ix * GRID_ROWS + nMaxCellY) << 16) | 0xFFFFu;
-        lo = lower_bound_u32(sk, nk, k0);
-        len = lower_bound_u32(sk, nk, k1 + 1u) - lo;
-        if (k1 == 0xFFFFFFFFu) len = nk - lo;
+        lo = cs[ix * GRID_ROWS + nMinCellY];
+        len = cs[ix * GRID_ROWS + nMaxCellY + 1] - lo;
     }
     int incl = len;   // exclusive prefix of run lengths over lanes
     for (int off = 1; off < 64; off <<= 1) {
@@ -506,7 +506,7 @@ using namespace orbframe;
 // valid for the extraction generation `kun_gen` (n images x `kun_cap` keypoints); m12 / prev
 // for `si_pairs` pairs of the SearchForInitialization run that followed.
 struct orbf_state {
-    DevBuf kun, uR, dep, keys, nkeys, prev, m12, nmatch, depth_in, list, lcnt;
+    DevBuf kun, uR, dep, keys, nkeys, cstart, prev, m12, nmatch, depth_in, list, lcnt;
     long long kun_gen = -1;
     int kun_n = 0, kun_cap = 0, si_pairs = 0;
 };
@@ -520,7 +520,7 @@ namespace orbamd {
 void frame_state_free(orbx_engine *e) {
     if (!e->fs) return;
     orbf_state *S = e->fs;
-    DevBuf *bufs[] = {&S->kun, &S->uR, &S->dep, &S->keys, &S->nkeys, &S->prev, &S->m12, &S->nmatch,
+    DevBuf *bufs[] = {&S->kun, &S->uR, &S->dep, &S->keys, &S->nkeys, &S->cstart, &S->prev, &S->m12, &S->nmatch,
                       &S->depth_in, &S->list, &S->lcnt};
     for (DevBuf *b : bufs) b->release();
     delete S;
@@ -602,12 +602,13 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
     FR_CHK(order_after_done(e, s));
     const GridParams gp = make_grid(cam, e->W, e->H);
     if (S.keys.ensure(4 * (size_t)n * sort_cap) || S.nkeys.ensure(4 * (size_t)n) ||
+        S.cstart.ensure(4 * (size_t)n * (GRID_CELLS + 1)) ||
         S.prev.ensure(8 * (size_t)n_pairs * cap) || S.m12.ensure(4 * (size_t)n_pairs * cap) ||
         S.nmatch.ensure(4 * (size_t)n_pairs))
         return ORBX_EDEVICE;
     int ph = prof_begin(e, s);
     grid_sort_kernel<<<n, 256, 4 * sort_cap, s>>>(gp, S.kun.as<orbx_kp>(), e->d_cnt.as<int>(), cap, sort_cap,
-                                                  S.keys.as<uint32_t>(), S.nkeys.as<int>());
+                                                  S.keys.as<uint32_t>(), S.nkeys.as<int>(), S.cstart.as<int>());
     prof_end(e, s, ph, "grid_sort_kernel");
     init_prev_xy<<<dim3((cap + 255) / 256, n_pairs), 256, 0, s>>>(S.kun.as<orbx_kp>(), e->d_cnt.as<int>(), cap, f1_base,
                                                                   f1_step, S.prev.as<float>());
@@ -623,6 +624,7 @@ int orbm_search_init_batch_device(orbx_engine *e, int n_pairs, int f1_base, int 
     a.cap0 = cap0;
     a.keys = S.keys.as<uint32_t>();
     a.nkeys = S.nkeys.as<int>();
+    a.cstart = S.cstart.as<int>();
     a.gp = gp;
     a.r = (float)window;
     a.nnratio = nnratio;
@@ -705,7 +707,8 @@ int orbm_search_for_initialization(orbm_matcher *m, const orbm_frame *F1, const 
     FR_CHK(order_after_done(m, s));
     FR_CHK(hipStreamWaitEvent(s, m->done, 0));
     if (m->kun.ensure(sizeof(orbx_kp) * 2 * (size_t)cap) || m->desc.ensure(64 * (size_t)cap) || m->cnt.ensure(8) ||
-        m->keys.ensure(8 * (size_t)sort_cap) || m->nkeys.ensure(8) || m->prev.ensure(8 * (size_t)cap) ||
+        m->keys.ensure(8 * (size_t)sort_cap) || m->nkeys.ensure(8) || m->cstart.ensure(8 * (size_t)(GRID_CELLS + 1)) ||
+        m->prev.ensure(8 * (size_t)cap) ||
         m->m12.ensure(4 * (size_t)cap) || m->nmatch.ensure(4) || m->list.ensure(4 * (size_t)cap0 * cap0) ||
         m->lcnt.ensure(4 * (size_t)cap0))
         return ORBX_EDEVICE;
@@ -731,13 +734,15 @@ int orbm_search_for_initialization(orbm_matcher *m, const orbm_frame *F1, const 
     a.cap0 = cap0;
     a.keys = m->keys.as<uint32_t>();
     a.nkeys = m->nkeys.as<int>();
+    a.cstart = m->cstart.as<int>();
     a.gp = gp;
     a.r = (float)window;
     a.nnratio = m->nnratio;
     a.check_ori = m->check_ori;
     a.list = m->list.as<uint32_t>();
     a.lcnt = m->lcnt.as<int>();
-    grid_sort_kernel<<<2, 256, 4 * sort_cap, s>>>(gp, a.kun, a.cnt, cap, sort_cap, m->keys.as<uint32_t>(), m->nkeys.as<int>());
+    grid_sort_kernel<<<2, 256, 4 * sort_cap, s>>>(gp, a.kun, a.cnt, cap, sort_cap, m->keys.as<uint32_t>(), m->nkeys.as<int>(),
+                                                  m->cstart.as<int>());
     search_init_cand_kernel<<<dim3((cap0 + 3) / 4, 1), 256, 0, s>>>(a, m->prev.as<float>());
     search_init_resolve_kernel<<<1, 256, 4 * (size_t)a.stage_cap + fixed, s>>>(a, m->prev.as<float>(), m->m12.as<int>(),
                                                                               m->nmatch.as<int>());

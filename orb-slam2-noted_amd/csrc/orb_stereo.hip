@@ -651,7 +651,7 @@ void orbm_destroy(orbm_matcher *m) {
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     if (m->done) { (void)hipEventSynchronize(m->done); (void)hipEventDestroy(m->done); }
     DevBuf *bufs[] = {&m->q, &m->db, &m->off, &m->idx, &m->out, &m->kun, &m->desc, &m->cnt, &m->keys,
-                      &m->nkeys, &m->prev, &m->m12, &m->nmatch, &m->list, &m->lcnt};
+                      &m->nkeys, &m->cstart, &m->prev, &m->m12, &m->nmatch, &m->list, &m->lcnt};
     for (DevBuf *b : bufs) b->release();
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
