@@ -11,7 +11,7 @@ import csv, glob, sys, collections
 acc = collections.defaultdict(lambda: collections.defaultdict(float)); disp = collections.defaultdict(set); dur = collections.defaultdict(float)
 for f in glob.glob(sys.argv[1] + '/**/*counter_collection.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r['Kernel_Name'].split('(')[0].split('::')[-1]
+        k = r['Kernel_Name'].split('(')[0].split('::')[-1].split('<')[0]
         acc[k][r['Counter_Name']] += float(r['Counter_Value']); disp[k].add(r['Dispatch_Id'])
 k = 'fast_blur_kernel'; c = acc[k]; n = len(disp[k]); w = c['SQ_WAVES']
 print(f"{sys.argv[2]:8s} fast_blur valu/launch {c['SQ_INSTS_VALU']/n/1e6:7.2f}M valu/wave {c['SQ_INSTS_VALU']/w:6.1f} lds/wave {c['SQ_INSTS_LDS']/w:5.1f} salu/wave {c['SQ_INSTS_SALU']/w:5.1f}")
