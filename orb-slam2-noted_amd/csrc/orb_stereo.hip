@@ -277,13 +277,21 @@ __global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g,
                                                                   int *sad) {
     __shared__ uint4 s_rec[ST_SCAP], s_d0[ST_SCAP], s_d1[ST_SCAP];
     __shared__ int s_kp[ST_NK][3];   // left keypoint index (-1: none), band [lo, hi)
+    // each slot's left keypoint (x, y, octave) and descriptor, loaded once by the prologue with its
+    // row: the wavefront's keypoint loop then starts each keypoint without a global round trip
+    __shared__ float s_kx[ST_NK], s_ky[ST_NK];
+    __shared__ int s_ko[ST_NK];
+    __shared__ uint4 s_q[ST_NK][2];
     __shared__ int s_lo, s_hi;
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
     int bxr, p;
     xcd_remap2(bxr, p);
     const int imgL = a.L.img_base + a.L.img_step * p, imgR = a.R.img_base + a.R.img_step * p;
-    const int nL = min(a.L.cnt[imgL], a.cap), nR = min(a.R.cnt[imgR], a.cap);
     const int s0 = bxr * ST_NK;
+    // the slot's lidx entry goes out with the keypoint counts (inside the pair's sort_cap row; used
+    // only below nL)
+    const int iLs = tid < ST_NK && s0 + tid < a.sort_cap ? lidx[(long long)p * a.sort_cap + s0 + tid] : -1;
+    const int nL = min(a.L.cnt[imgL], a.cap), nR = min(a.R.cnt[imgR], a.cap);
     if (s0 >= nL) return;   // workgroup-uniform, before any barrier
     const orbx_kp *kL = a.L.kps + (long long)imgL * a.cap;
     const orbx_kp *kR = a.R.kps + (long long)imgR * a.cap;
@@ -294,8 +302,15 @@ __global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g,
     if (tid < ST_NK) {
         int iL = -1, lo = 0, hi = 0;
         if (s0 + tid < nL) {
-            iL = lidx[(long long)p * a.sort_cap + s0 + tid];
-            const int row = (int)kL[iL].y;
+            iL = iLs;
+            const orbx_kp k = kL[iL];
+            const uint4 *dq = (const uint4 *)(a.L.desc + ((long long)imgL * a.cap + iL) * 32);
+            s_q[tid][0] = dq[0];
+            s_q[tid][1] = dq[1];
+            s_kx[tid] = k.x;
+            s_ky[tid] = k.y;
+            s_ko[tid] = k.octave;
+            const int row = (int)k.y;
             const float ylo = (float)row - a.rmax - 2.0f, yhi = (float)row + a.rmax + 2.0f;
             lo = rowtab[min(max((int)floorf(ylo), 0), a.nrows - 1)];
             const int hr = (int)floorf(yhi) + 1;
@@ -328,7 +343,10 @@ __global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g,
         const int iL = __builtin_amdgcn_readfirstlane(s_kp[slot][0]);
         if (iL < 0) break;   // the workgroup's last slots past nL
         const int lo = __builtin_amdgcn_readfirstlane(s_kp[slot][1]), hi = __builtin_amdgcn_readfirstlane(s_kp[slot][2]);
-        const orbx_kp kpL = kL[iL];
+        orbx_kp kpL;   // x, y, octave: what the match and stereo_refine read
+        kpL.x = s_kx[slot];
+        kpL.y = s_ky[slot];
+        kpL.octave = __builtin_amdgcn_readfirstlane(s_ko[slot]);
         const int levelL = kpL.octave;
         const float vL = kpL.y, uL = kpL.x;
         const float minD = 0, maxD = a.maxD;
@@ -337,9 +355,11 @@ __global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g,
         const float yhi = (float)row + a.rmax + 2.0f;
         int bestDist = 100;  // ORBmatcher::TH_HIGH
         int bestIdxR = 0;
+        float bestX = 0.0f;   // the best right keypoint's x (staged: from its LDS record)
+        bool haveX = false;
         if (maxU >= 0) {
-            const uint4 *dL4 = (const uint4 *)(a.L.desc + ((long long)imgL * a.cap + iL) * 32);
-            const uint4 q0 = dL4[0], q1 = dL4[1];
+            const uint4 *dL4 = (const uint4 *)(a.L.desc + ((long long)imgL * a.cap + iL) * 32);   // (the global path)
+            const uint4 q0 = s_q[slot][0], q1 = s_q[slot][1];
             unsigned best = 0xFFFFFFFFu;
             // the per-record test as one branch-free predicate (bitwise: no short-circuit branches)
             auto take = [&](const uint4 &e) {
@@ -351,6 +371,7 @@ __global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g,
                        (kx <= maxU);
             };
             const uint4 NONE = make_uint4(0x7f800000u, 0u, 0u, 0u);
+            int jb = 0;   // staged: the LDS slot of the lane's best record
             if (staged) {
                 // LDS slots past the band are read anyway (clamped into the array) and masked
                 const int end = hi - ulo;
@@ -359,8 +380,14 @@ __global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g,
                     const int j0 = min(c0, ST_SCAP - 1), j1 = min(c1, ST_SCAP - 1);
                     const uint4 e0 = s_rec[j0], e1 = s_rec[j1];
                     const bool t0 = (c0 < end) & take(e0), t1 = (c1 < end) & take(e1);
-                    if (t0) best = min(best, ((unsigned)hamming_v(q0, q1, s_d0[j0], s_d1[j0]) << 16) | (e0.w & 0xFFFFu));
-                    if (t1) best = min(best, ((unsigned)hamming_v(q0, q1, s_d0[j1], s_d1[j1]) << 16) | (e1.w & 0xFFFFu));
+                    if (t0) {
+                        const unsigned k0 = ((unsigned)hamming_v(q0, q1, s_d0[j0], s_d1[j0]) << 16) | (e0.w & 0xFFFFu);
+                        if (k0 < best) { best = k0; jb = j0; }
+                    }
+                    if (t1) {
+                        const unsigned k1 = ((unsigned)hamming_v(q0, q1, s_d0[j1], s_d1[j1]) << 16) | (e1.w & 0xFFFFu);
+                        if (k1 < best) { best = k1; jb = j1; }
+                    }
                 }
             } else {
                 for (int base = lo; base < hi; base += 128) {
@@ -372,6 +399,7 @@ __global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g,
                     if (t1) best = min(best, ((unsigned)hamming32((const uint8_t *)dL4, dRg + (long long)i1 * 32) << 16) | (unsigned)i1);
                 }
             }
+            const unsigned mine = best;   // the lane's own minimum (keys are unique: one record each)
             best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x111, 0xF, 0xF, false));
             best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x112, 0xF, 0xF, false));
             best = min(best, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)best, 0x114, 0xF, 0xF, false));
@@ -381,12 +409,18 @@ __global__ __launch_bounds__(ST_NW * 64) void stereo_match_staged(ExtractGeom g,
             if (best != 0xFFFFFFFFu && (int)(best >> 16) < bestDist) {
                 bestDist = (int)(best >> 16);
                 bestIdxR = (int)(best & 0xFFFF);
+                if (staged) {   // the record holding it: its x instead of a global load of kR[bestIdxR]
+                    const unsigned long long own = __ballot(mine == best);
+                    const int jw = __builtin_amdgcn_readlane(jb, (int)__builtin_ctzll(own));
+                    bestX = __uint_as_float(s_rec[jw].y);
+                    haveX = true;
+                }
             }
         }
         const bool matched = maxU >= 0 && bestDist < (100 + 50) / 2;   // thOrbDist (Frame.cc:842)
         int pitchL, pitchR;
         const uint8_t *imL = side_level(g, a.L, imgL, levelL, &pitchL), *imR = side_level(g, a.R, imgR, levelL, &pitchR);
-        stereo_refine(kpL, matched, matched ? kR[bestIdxR].x : 0.0f, imL, pitchL, imR, pitchR, g.lw[levelL],
+        stereo_refine(kpL, matched, matched ? (haveX ? bestX : kR[bestIdxR].x) : 0.0f, imL, pitchL, imR, pitchR, g.lw[levelL],
                       g.scale[levelL], g.inv_scale[levelL], a.mbf, a.maxD, lane, (long long)p * a.cap + iL, u_right, depth,
                       sad);
     }
