@@ -1180,6 +1180,10 @@ __device__ void qt_move(QShared &S, QT &Q, QCnt base) {
     __syncthreads();
 }
 
+// NL: the node arrays in LDS (ORBX_QT_NODES_LDS) or in global scratch, a template argument so every
+// node access compiles to one address space (a pointer chosen at run time between LDS and global
+// compiles to flat loads and stores, which wait on both counters)
+template <bool NL>
 __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     ExtractGeom g, const int *cell_cnt, const uint32_t *cell_keys, uint32_t *qt_keys,
     unsigned char *qt_nodes, uint32_t *sel, int *sel_cnt) {
@@ -1200,19 +1204,10 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     const int N = g.N[l], nIni = g.nIni[l];
     const int NC = g.node_cap, NP = g.node_pow2;
     int par = 0;
-    QT Q;
-    Q.NC = NC; Q.NP = NP;
     // ---- LDS / global carving
     unsigned char *lds = qt_lds;
-    {
-        unsigned char *p = g.qt_nodes_in_lds ? lds : qt_nodes + ((long long)b * g.nlevels + l) * g.qt_node_stride * 4;
-        Q.outrec = (unsigned long long *)p; p += 8 * NP;
-        Q.sortbuf = (unsigned long long *)p; p += 8 * NP;
-        Q.tmp = (QTmp *)p; p += sizeof(QTmp) * NC;
-        Q.cur = (QNode *)p; p += sizeof(QNode) * NC;
-        Q.nxt = (QNode *)p; p += sizeof(QNode) * NC;
-        if (g.qt_nodes_in_lds) lds = p;
-    }
+    unsigned char *const nodes = NL ? lds : qt_nodes + ((long long)b * g.nlevels + l) * g.qt_node_stride * 4;
+    if (NL) lds += 16 * NP + (sizeof(QTmp) + 2 * sizeof(QNode)) * NC;
     // ---- 1. gather the cells' keypoints in cell order -> M. A cell's slots hold its FAST
     //         survivors at min(iniThFAST, minThFAST) with score M - 1; FAST at iniThFAST keeps
     //         those with score >= iniThFAST, and the cell retries at minThFAST when none does
@@ -1264,11 +1259,24 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
             M += (int)tot;
         }
     }
-    Q.M = M;
 #ifdef ORBX_QT_PROFILE
     const long long t_gm = wall_clock64();
 #endif
-    if (M <= g.qt_kl) {
+    // the rest in two copies, keys in LDS (KL) or in global scratch: each key access one address space
+    // (the working set is a local of each copy)
+    auto body = [&](auto kl_tag) {
+    constexpr bool KL = decltype(kl_tag)::value;
+    QT Q;
+    Q.NC = NC; Q.NP = NP; Q.M = M;
+    {
+        unsigned char *p = nodes;
+        Q.outrec = (unsigned long long *)p; p += 8 * NP;
+        Q.sortbuf = (unsigned long long *)p; p += 8 * NP;
+        Q.tmp = (QTmp *)p; p += sizeof(QTmp) * NC;
+        Q.cur = (QNode *)p; p += sizeof(QNode) * NC;
+        Q.nxt = (QNode *)p;
+    }
+    if (KL) {
         Q.K[0] = (uint32_t *)lds;
         Q.K[1] = Q.K[0] + g.qt_kl;
         Q.NO[0] = (int16_t *)(Q.K[1] + g.qt_kl);
@@ -1424,23 +1432,27 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
             // buffer, free until qt_move, or the whole key area when the keys live in global
             // scratch -- into sortbuf; the bitonic network over sortbuf when neither fits
             const int na16 = (na + 15) & ~15;
-            const bool keys_lds = M <= g.qt_kl;
+            const bool keys_lds = KL;
             const bool rank = na16 <= (keys_lds ? g.qt_kl / 2 : 12 * g.qt_kl / 8);
-            unsigned long long *stage = rank ? (keys_lds ? (unsigned long long *)Q.keys(Q.src ^ 1) : (unsigned long long *)lds) : Q.sortbuf;
+            // (each branch with its own pointer: one address space per access)
+            unsigned long long *const rstage = keys_lds ? (unsigned long long *)Q.keys(Q.src ^ 1) : (unsigned long long *)lds;
             int np2 = 1;
             while (np2 < na) np2 <<= 1;
-            const int nfill = rank ? na16 : np2;
-            for (int i = tid; i < nfill; i += ORBX_QT_THREADS) {
-                unsigned long long v = 0;
-                if (i < na) {
-                    const QNode &q = Q.cur[i];
-                    v = ((unsigned long long)(uint32_t)q.n << 40) | ((unsigned long long)(uint32_t)(q.id & 0xFFFFFF) << 16) | (unsigned)i;
+            auto fill = [&](unsigned long long *stage, int nfill) {
+                for (int i = tid; i < nfill; i += ORBX_QT_THREADS) {
+                    unsigned long long v = 0;
+                    if (i < na) {
+                        const QNode &q = Q.cur[i];
+                        v = ((unsigned long long)(uint32_t)q.n << 40) | ((unsigned long long)(uint32_t)(q.id & 0xFFFFFF) << 16) | (unsigned)i;
+                    }
+                    stage[i] = v;
                 }
-                stage[i] = v;
-            }
+            };
+            if (rank) fill(rstage, na16);
+            else fill(Q.sortbuf, np2);
             if (tid == 0) S.cross = na;
             __syncthreads();
-            if (rank) block_rank_sort_desc(stage, Q.sortbuf, na);
+            if (rank) block_rank_sort_desc(rstage, Q.sortbuf, na);
             else block_sort_desc(Q.sortbuf, np2);
             // first sorted position whose split brings the size to >= N
             {
@@ -1533,6 +1545,9 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
                NP, nout, qt_rounds, qt_t[0], wall_clock64(), qt_t[1] - qt_t[0], qt_t[2] - qt_t[1], qt_t[3] - qt_t[2], qt_t[4] - qt_t[3],
                qt_t[5] - qt_t[4], qt_t[6] - qt_t[5], qt_sub[0], qt_sub[1], qt_sub[2], t_gm - qt_t[0]);
 #endif
+    };
+    if (M <= g.qt_kl) body(std::true_type{});
+    else body(std::false_type{});
 }
 
 // ------------------------------------------------------------------------------------
@@ -2137,7 +2152,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     size_t lds = 12 * (size_t)g.qt_kl;
     if (g.qt_nodes_in_lds) lds += (2 * sizeof(QNode) + sizeof(QTmp)) * g.node_cap + 16 * (size_t)g.node_pow2;
     for (int rep = 0; rep < ((exp_twice() & 2) ? 2 : 1); rep++)
-    quadtree_kernel<<<dim3(L, n), ORBX_QT_THREADS, lds, s>>>(
+    (g.qt_nodes_in_lds ? quadtree_kernel<true> : quadtree_kernel<false>)<<<dim3(L, n), ORBX_QT_THREADS, lds, s>>>(
         g, e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>(), e->d_qt.as<uint32_t>(),
         e->d_qt_nodes.as<unsigned char>(), e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>());
     prof_end(e, s, ph, "quadtree_kernel");
