@@ -1489,9 +1489,11 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     //         order inside the cell; rank = (cell, row, column in the cell), from the key
     {
         const int na = S.n_act;
+        // each node's best key as a u64 maximum: in LDS (the idle key buffer) when it fits, else in
+        // the node scratch; two copies so each access has one address space
+        auto step5 = [&](unsigned long long *best) {
         const int R = (M + ORBX_QT_THREADS - 1) / ORBX_QT_THREADS;
         const int i0 = tid * R, i1 = min(i0 + R, M);
-        unsigned long long *best = Q.sortbuf;
         const int hC = g.hcell[l], wC = g.wcell[l];
         for (int i = tid; i < na; i += ORBX_QT_THREADS) best[i] = 0ull;
         __syncthreads();
@@ -1516,6 +1518,9 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
                 Q.outrec[o] = ((unsigned long long)(uint32_t)(Q.cur[t].id + 0x40000000) << 32) | key;
             }
         }
+        };
+        if (KL && 2 * na <= g.qt_kl) step5((unsigned long long *)Q.keys(Q.src ^ 1));
+        else step5(Q.sortbuf);
         __syncthreads();
         if (tid == 0) S.n_out += na;
         __syncthreads();
