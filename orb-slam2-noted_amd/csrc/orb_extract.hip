@@ -1189,8 +1189,10 @@ __global__ __launch_bounds__(ORBX_QT_THREADS) void quadtree_kernel(
     unsigned char *qt_nodes, uint32_t *sel, int *sel_cnt) {
     extern __shared__ __align__(16) unsigned char qt_lds[];
     __shared__ QShared S;
-    int l, b;
-    xcd_remap2(l, b);
+    // grid (images, levels) in hardware order: every image's level 0 -- the longest workgroups --
+    // is dispatched first, then level 1, ... (longest first shortens the kernel's tail); the
+    // workgroups share no data, so no XCD-aware remap
+    const int b = blockIdx.x, l = blockIdx.y;
     const int tid = threadIdx.x;
 #ifdef ORBX_QT_PROFILE
     long long qt_t[8], qt_sub[3] = {0, 0, 0};
@@ -2157,7 +2159,7 @@ int engine_extract_device(orbx_engine *e, const uint8_t *d_imgs, int n, int pitc
     size_t lds = 12 * (size_t)g.qt_kl;
     if (g.qt_nodes_in_lds) lds += (2 * sizeof(QNode) + sizeof(QTmp)) * g.node_cap + 16 * (size_t)g.node_pow2;
     for (int rep = 0; rep < ((exp_twice() & 2) ? 2 : 1); rep++)
-    (g.qt_nodes_in_lds ? quadtree_kernel<true> : quadtree_kernel<false>)<<<dim3(L, n), ORBX_QT_THREADS, lds, s>>>(
+    (g.qt_nodes_in_lds ? quadtree_kernel<true> : quadtree_kernel<false>)<<<dim3(n, L), ORBX_QT_THREADS, lds, s>>>(
         g, e->d_cell_cnt.as<int>(), e->d_cell_keys.as<uint32_t>(), e->d_qt.as<uint32_t>(),
         e->d_qt_nodes.as<unsigned char>(), e->d_sel.as<uint32_t>(), e->d_sel_cnt.as<int>());
     prof_end(e, s, ph, "quadtree_kernel");
